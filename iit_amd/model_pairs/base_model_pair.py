@@ -1,0 +1,406 @@
+"""Model-pair engine core (parity: ``/root/reference/iit/model_pairs/base_model_pair.py:23-326``).
+
+A model pair holds an HL causal model, an LL network and a correspondence
+``corr: {HLNode: {LLNode}}``.  ``do_intervention`` runs the source ("ablation")
+input through both models, then re-runs the base input with source activations
+spliced in at the HL node / its mapped LL nodes.
+
+MI355X-native execution: when the LL model is a native
+``iit_amd`` model (it accepts a ``RunPlan``), the intervention is compiled to a
+plan instead of Python hook closures:
+
+1. source LL run: ``no_grad``, captures only ``corr[hl_node]`` hooks, stops after
+   the deepest one (the reference caches every hook of a full forward);
+2. base LL run: the splice happens inside the fused kernels / skips dead producers;
+   only the logits the loss reads are computed (``logits="last"`` for IOI).
+
+Any other ``HookedRootModule`` LL model takes the reference path
+(``run_with_cache`` + ``run_with_hooks`` with clone/index-put hooks).
+
+Training (``train``): same loop, metric names, early stop and scheduler logic as
+the reference, plus: a flat fp32 parameter arena with a fused clip+Adam
+(:mod:`iit_amd.ops.optim`), data parallelism over RCCL with bucketed all-reduce
+overlapped with backward (:mod:`iit_amd.parallel.ddp`), device-resident loaders,
+deferred metric reads (no per-step ``.item()``), a NaN/Inf step guard, optional
+wandb / JSONL sinks, and checkpoint / resume (:mod:`iit_amd.utils.checkpoint`).
+"""
+from __future__ import annotations
+
+from abc import ABC, abstractmethod
+from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple, final
+
+import numpy as np
+import torch
+from torch import Tensor
+
+from ..config import WANDB_ENTITY
+from ..core.correspondence import Correspondence
+from ..core.index import EVERYTHING, Ix, TorchIndex
+from ..core.metric import MetricStoreCollection, MetricType
+from ..core.nodes import HLNode, HookName, LLNode
+from ..data.iit_dataset import IITDataset
+from ..engine.plan import RunPlan
+from ..hooks.hook_points import ActivationCache, HookPoint
+from ..parallel import dist as pdist
+from ..utils.progress import progress
+from ..utils.sinks import make_sink
+
+
+def _is_native(model) -> bool:
+    return getattr(model, "supports_run_plan", False) or hasattr(model, "run_capture")
+
+
+def _underlying_module(model) -> torch.nn.Module:
+    return model if isinstance(model, torch.nn.Module) else getattr(model, "model")
+
+
+def _ll_nodes_of(corr, hl_node) -> List[LLNode]:
+    v = corr[hl_node]
+    if isinstance(v, LLNode):
+        return [v]
+    return sorted(v, key=lambda n: (n.name, repr(n.index)))
+
+
+class BaseModelPair(ABC):
+    hl_model: Any
+    ll_model: Any
+    hl_cache: Any
+    ll_cache: Any
+    corr: Correspondence
+    training_args: Dict[str, Any]
+    wandb_method: str
+    rng: np.random.Generator
+    dataset_class = IITDataset
+
+    # ------------------------------------------------------------------ abstract API
+    @property
+    @abstractmethod
+    def loss_fn(self) -> Callable[[Tensor, Tensor], Tensor]:
+        ...
+
+    @staticmethod
+    @abstractmethod
+    def make_train_metrics() -> MetricStoreCollection:
+        ...
+
+    @staticmethod
+    @abstractmethod
+    def make_test_metrics() -> MetricStoreCollection:
+        ...
+
+    @abstractmethod
+    def run_train_step(self, base_input, ablation_input, loss_fn, optimizer) -> Dict[str, Any]:
+        ...
+
+    @abstractmethod
+    def run_eval_step(self, base_input, ablation_input, loss_fn) -> Dict[str, Any]:
+        ...
+
+    # ------------------------------------------------------------------ intervention
+    def hl_run_kwargs(self) -> Dict[str, Any]:
+        """Extra kwargs for HL forwards (IOI uses ``last_only`` to skip [B,S,V] logits)."""
+        return {}
+
+    def ll_logits_mode(self) -> str:
+        """Which LL logits the losses read: ``full`` ([B,S,V]) or ``last`` ([B,V])."""
+        return "full"
+
+    def native(self) -> bool:
+        """Use the plan-driven engine (False = reference closure/hook semantics, "reference-equivalent eager")."""
+        return self.training_args.get("engine", "native") != "reference" and _is_native(self.ll_model)
+
+    def ll_source_cache(self, x: Tensor, ll_nodes: Iterable[LLNode]):
+        names = sorted({n.name for n in ll_nodes})
+        model = self.ll_model
+        if self.native():
+            return ActivationCache(model.run_capture(x, names), model)
+        _, cache = model.run_with_cache(x)
+        return cache
+
+    def ll_intervened_forward(self, x: Tensor, ll_nodes: Iterable[LLNode], logits: Optional[str] = None):
+        logits = logits or self.ll_logits_mode()
+        model = self.ll_model
+        if self.native():
+            plan = RunPlan.with_splices(
+                [(n.name, n.index, self.ll_cache[n.name]) for n in ll_nodes], logits=logits)
+            return model(x, plan=plan)
+        out = model.run_with_hooks(x, fwd_hooks=[(n.name, self.make_ll_ablation_hook(n)) for n in ll_nodes])
+        return out[:, -1] if logits == "last" and out.dim() == 3 else out
+
+    def ll_forward(self, x: Tensor, logits: Optional[str] = None):
+        logits = logits or self.ll_logits_mode()
+        model = self.ll_model
+        if logits in ("last", "argmax") and self.native():
+            return model(x, plan=RunPlan(logits=logits))
+        out = model(x)
+        if logits == "argmax":
+            return out.argmax(dim=-1)
+        return out[:, -1] if logits == "last" and out.dim() == 3 else out
+
+    def do_intervention(self, base_input, ablation_input, hl_node: HLNode, verbose: bool = False
+                        ) -> Tuple[Tensor, Tensor]:
+        ablation_x = ablation_input[0]
+        base_x = base_input[0]
+        hl_kw = self.hl_run_kwargs()
+        hl_ablation_output, self.hl_cache = self.hl_model.run_with_cache(ablation_input, **hl_kw)
+        ll_nodes = _ll_nodes_of(self.corr, hl_node)
+        self.ll_cache = self.ll_source_cache(ablation_x, ll_nodes)
+        hl_output = self.hl_model.run_with_hooks(
+            base_input, fwd_hooks=[(hl_node.name, self.make_hl_ablation_hook(hl_node))], **hl_kw)
+        ll_output = self.ll_intervened_forward(base_x, ll_nodes)
+        if verbose:
+            print(f"{hl_node=}, {ll_nodes=}\n{hl_output=}")
+        return hl_output, ll_output
+
+    @staticmethod
+    def get_label_idxs():
+        return Ix[[None]]
+
+    def make_hl_model(self, hl_graph):
+        raise NotImplementedError
+
+    def set_corr(self, corr):
+        self.corr = corr
+
+    def sample_hl_name(self) -> HLNode:
+        return self.rng.choice(list(self.corr.keys()))
+
+    def make_hl_ablation_hook(self, hl_node: HLNode):
+        if not isinstance(hl_node, HLNode):
+            raise AssertionError(f"hl_node is not an instance of HLNode, but {type(hl_node)}")
+        if hl_node.index is None:
+            return self.hl_ablation_hook
+        index = hl_node.index
+
+        def hl_ablation_hook(act: Tensor, hook: HookPoint) -> Tensor:
+            src = self.hl_cache[hook.name]
+            if isinstance(act, (int, float)):
+                return src
+            if index == EVERYTHING:
+                return src.clone()
+            out = act.clone()
+            out[index.as_index] = src[index.as_index]
+            return out
+
+        return hl_ablation_hook
+
+    def hl_ablation_hook(self, act: Tensor, hook: HookPoint) -> Tensor:
+        return self.hl_cache[hook.name]
+
+    def make_ll_ablation_hook(self, ll_node: LLNode) -> Callable[[Tensor, HookPoint], Tensor]:
+        if ll_node.subspace is not None:
+            raise NotImplementedError("subspace interventions are not supported")
+        index = ll_node.index if ll_node.index is not None else EVERYTHING
+
+        def ll_ablation_hook(act: Tensor, hook: HookPoint) -> Tensor:
+            out = act.clone()
+            out[index.as_index] = self.ll_cache[hook.name][index.as_index].to(out.dtype)
+            return out
+
+        return ll_ablation_hook
+
+    def get_IIT_loss_over_batch(self, base_input, ablation_input, hl_node: HookName, loss_fn):
+        hl_output, ll_output = self.do_intervention(base_input, ablation_input, hl_node)
+        return loss_fn(ll_output, hl_output)
+
+    # ------------------------------------------------------------------ optimisation
+    def _ll_module(self) -> torch.nn.Module:
+        return _underlying_module(self.ll_model)
+
+    def make_optimizer(self, lr: float):
+        module = self._ll_module()
+        fused = self.training_args.get("fused_optimizer", None)
+        if fused is None:
+            fused = next(module.parameters()).is_cuda
+        if fused:
+            from ..engine.flat import FlatParams
+            from ..ops.optim import FusedAdam
+            flat = getattr(module, "_flat_params", None)
+            if flat is None:
+                flat = FlatParams(module, with_bf16_shadow=getattr(module, "wants_bf16_shadow", False))
+                module._flat_params = flat
+            opt = FusedAdam(flat, lr=lr)
+        else:
+            opt = torch.optim.Adam(module.parameters(), lr=lr)
+        self._setup_reducer(opt)
+        return opt
+
+    def _setup_reducer(self, optimizer):
+        self._reducer = None
+        if pdist.world_size() > 1:
+            from ..engine.flat import FlatParams
+            from ..parallel.ddp import GradReducer
+            flat = getattr(optimizer, "flat", None)
+            if flat is None:
+                module = self._ll_module()
+                flat = getattr(module, "_flat_params", None) or FlatParams(module)
+                module._flat_params = flat
+            self._reducer = GradReducer(flat, bucket_mb=self.training_args.get("bucket_mb", 64.0),
+                                        overlap=self.training_args.get("overlap_allreduce", True))
+
+    def backward(self, loss: Tensor) -> None:
+        """``loss.backward()`` + data-parallel gradient averaging + reference grad semantics."""
+        reducer = getattr(self, "_reducer", None)
+        if reducer is not None:
+            reducer.start()
+        loss.backward()
+        if reducer is not None:
+            reducer.finish()
+        # the reference's hook-based splices leave every LL parameter on the autograd
+        # graph (zero gradients for dead paths); the native engine skips dead compute,
+        # so give untouched parameters an explicit zero gradient (Adam still steps them).
+        for p in self._ll_module().parameters():
+            if p.requires_grad and p.grad is None:
+                p.grad = torch.zeros_like(p)
+
+    def clip_grad_fn(self, optimizer=None):
+        max_norm = self.training_args.get("clip_grad_norm")
+        if not max_norm:
+            return
+        if optimizer is not None and hasattr(optimizer, "flat"):
+            optimizer.pending_clip = max_norm
+            return
+        from ..ops.optim import clip_grad_norm_
+        clip_grad_norm_(list(self._ll_module().parameters()), max_norm)
+
+    def optimizer_step(self, optimizer):
+        clip = getattr(optimizer, "pending_clip", None)
+        if clip is not None and hasattr(optimizer, "flat"):
+            optimizer.pending_clip = None
+            optimizer.step(clip_norm=clip)
+        else:
+            optimizer.step()
+
+    def step_scheduler(self, lr_scheduler, test_metrics):
+        if isinstance(lr_scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
+            val_metric = self.training_args.get("scheduler_val_metric", "val/accuracy")
+            values = test_metrics.to_dict()
+            if val_metric not in values:
+                raise ValueError(f"val_metric {val_metric} not found in test_metrics {test_metrics}")
+            lr_scheduler.step(values[val_metric])
+            return
+        try:
+            lr_scheduler.step()
+        except Exception as e:  # pragma: no cover - parity with reference warning path
+            print(f"WARNING: Could not step lr_scheduler {lr_scheduler} with exception {e}")
+
+    # ------------------------------------------------------------------ training loop
+    def train(self, train_set, test_set, epochs: int = 1000, use_wandb: bool = False,
+              checkpoint_dir: Optional[str] = None, resume: bool = False, max_steps: Optional[int] = None):
+        training_args = self.training_args
+        if pdist.is_main():
+            print(f"{training_args=}")
+        if not isinstance(train_set, IITDataset):
+            raise AssertionError(f"train_set is not an instance of IITDataset, but {type(train_set)}")
+        if not isinstance(test_set, IITDataset):
+            raise AssertionError(f"test_set is not an instance of IITDataset, but {type(test_set)}")
+        pdist.broadcast_module(self._ll_module())
+        train_loader, test_loader = self.make_loaders(train_set, test_set, training_args["batch_size"],
+                                                      training_args["num_workers"])
+        early_stop = training_args["early_stop"]
+        optimizer = self.make_optimizer(training_args["lr"])
+        loss_fn = self.loss_fn
+        scheduler_cls = training_args.get("lr_scheduler", None)
+        lr_scheduler = None
+        if scheduler_cls == torch.optim.lr_scheduler.ReduceLROnPlateau:
+            lr_scheduler = scheduler_cls(optimizer, mode=training_args.get("scheduler_mode", "max"),
+                                         factor=0.1, patience=10)
+        elif scheduler_cls:
+            lr_scheduler = scheduler_cls(optimizer)
+        sink = make_sink(use_wandb and pdist.is_main(), project="iit", entity=WANDB_ENTITY,
+                         config={**{k: str(v) for k, v in training_args.items()}, "method": self.wandb_method})
+        start_epoch = 0
+        if checkpoint_dir and resume:
+            from ..utils.checkpoint import load_resume_state
+            start_epoch = load_resume_state(checkpoint_dir, self, optimizer, lr_scheduler)
+        self.optimizer = optimizer
+        epoch = start_epoch
+        for epoch in progress(range(start_epoch, epochs), disable=not pdist.is_main()):
+            train_metrics = self._run_train_epoch(train_loader, loss_fn, optimizer, max_steps=max_steps)
+            test_metrics = self._run_eval_epoch(test_loader, loss_fn)
+            self._reduce_metrics(train_metrics)
+            self._reduce_metrics(test_metrics)
+            if lr_scheduler is not None:
+                self.step_scheduler(lr_scheduler, test_metrics)
+            self.test_metrics = test_metrics
+            self.train_metrics = train_metrics
+            if pdist.is_main():
+                self._print_and_log_metrics(epoch, train_metrics.metrics + test_metrics.metrics, sink)
+            if checkpoint_dir and pdist.is_main():
+                from ..utils.checkpoint import save_resume_state
+                save_resume_state(checkpoint_dir, self, optimizer, lr_scheduler, epoch + 1)
+            if early_stop and self._check_early_stop_condition(test_metrics.metrics):
+                break
+        if sink is not None:
+            sink.log({"final epoch": epoch})
+            sink.close()
+
+    @final
+    @staticmethod
+    def make_loaders(dataset: IITDataset, test_dataset: IITDataset, batch_size: int, num_workers: int):
+        return dataset.make_loader(batch_size, num_workers), test_dataset.make_loader(batch_size, num_workers)
+
+    def _run_train_epoch(self, loader, loss_fn, optimizer, max_steps: Optional[int] = None) -> MetricStoreCollection:
+        self._ll_module().train()
+        metrics = self.make_train_metrics()
+        for i, (base_input, ablation_input) in enumerate(progress(loader, total=len(loader),
+                                                                  disable=not pdist.is_main(), leave=False)):
+            metrics.update(self.run_train_step(base_input, ablation_input, loss_fn, optimizer))
+            if max_steps is not None and i + 1 >= max_steps:
+                break
+        return metrics
+
+    def _run_eval_epoch(self, loader, loss_fn) -> MetricStoreCollection:
+        self._ll_module().eval()
+        metrics = self.make_test_metrics()
+        with torch.no_grad():
+            for base_input, ablation_input in loader:
+                metrics.update(self.run_eval_step(base_input, ablation_input, loss_fn))
+        return metrics
+
+    @staticmethod
+    def _reduce_metrics(collection: MetricStoreCollection) -> None:
+        """Average each metric's epoch value over data-parallel ranks (one small all-reduce)."""
+        if pdist.world_size() <= 1:
+            return
+        vals = []
+        for m in collection.metrics:
+            if len(m) == 0:
+                continue
+            vals.append(np.atleast_1d(np.mean(np.stack([np.asarray(v, dtype=np.float64) for v in m._values()]), axis=0)))
+        if not vals:
+            return
+        flat = torch.tensor(np.concatenate(vals), dtype=torch.float64)
+        if torch.distributed.get_backend() == "nccl":
+            flat = flat.cuda()
+        pdist.all_reduce_mean_(flat)
+        flat = flat.cpu().numpy()
+        off = 0
+        for m, v in zip([m for m in collection.metrics if len(m)], vals):
+            n = v.size
+            red = flat[off:off + n]
+            off += n
+            m._store = [red if (m.type == MetricType.LOG) else float(red[0])]
+
+    @staticmethod
+    def _check_early_stop_condition(test_metrics) -> bool:
+        """True iff every ACCURACY metric reached 100 % (reference Q1 semantics)."""
+        got = False
+        for metric in test_metrics:
+            if metric.type == MetricType.ACCURACY:
+                got = True
+                if metric.get_value() < 100:
+                    return False
+        if not got:
+            raise ValueError("No accuracy metric found in test_metrics!")
+        return True
+
+    @staticmethod
+    def _print_and_log_metrics(epoch, metrics, sink=None):
+        line = ", ".join(str(m) for m in metrics)
+        print(f"\nEpoch {epoch}: {line}")
+        if sink is not None:
+            sink.log({"epoch": epoch})
+            for m in metrics:
+                v = m.get_value()
+                sink.log({m.get_name(): v.tolist() if isinstance(v, np.ndarray) else v})

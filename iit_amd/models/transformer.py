@@ -1,0 +1,417 @@
+"""TransformerLens-compatible hooked transformer, built natively for MI355X.
+
+Replaces the reference's external ``transformer_lens.HookedTransformer``
+(SURVEY.md §2.1 X1, §2.6): identical hook names and shapes, parameter names and
+layouts (``W_Q [H,d,dh]``, ``W_O [H,dh,d]``, ``W_in [d,d_mlp]``...), named-parameter
+order, ``mask``/``IGNORE`` buffers, GPT-2 init and ``cfg.to_dict()`` keys, so
+checkpoints written by ``torch.save(model.state_dict())`` load in both.
+
+Execution is plan-driven instead of closure-driven:
+
+* every hook site calls ``_Run.site`` which applies the active ``RunPlan``
+  (capture / splice / StopGrad scale) and then the user ``HookPoint``;
+* hook sites nobody listens to are never materialised when the fused HIP op
+  backend is active (``iit_amd.ops.hip_ops``): LN, QKV, attention, MLP and the
+  residual adds run as fused kernels, and splices of ``attn.hook_z`` (whole or
+  per head) / ``mlp.hook_post`` happen *inside* those kernels (or skip the dead
+  producer entirely for whole-tensor splices);
+* a capture-only plan stops the forward right after its last captured hook;
+* ``logits_at=-1`` (or a plan with ``logits="last"``) computes the unembed only
+  for the last position (all IOI losses only read ``[:, -1]``).
+
+Parameters are always fp32 masters; ``cfg.dtype`` selects the compute dtype
+(fp32 = reference parity mode, bf16 = MI355X fast mode).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Union
+
+import torch
+from torch import nn
+
+from ..engine.plan import RunPlan
+from ..hooks.hook_points import HookedRootModule, HookPoint
+from ..ops import select_ops
+from ..ops.torch_ops import TorchOps
+from .config import HookedTransformerConfig, make_config
+
+
+class _StopForward(Exception):
+    pass
+
+
+class _Run:
+    """Per-forward execution state: the plan plus the active op backend."""
+
+    __slots__ = ("plan", "ops", "remaining")
+
+    def __init__(self, plan: Optional[RunPlan], ops):
+        self.plan = plan
+        self.ops = ops
+        self.remaining = None
+        if plan is not None and plan.logits == "none" and plan.truncate and plan.capture:
+            self.remaining = set(plan.capture)
+
+    def live(self, hp: HookPoint) -> bool:
+        return hp.is_live or (self.plan is not None and self.plan.touches(hp.name))
+
+    def whole_splice(self, name: str):
+        if self.plan is None:
+            return None
+        spl = self.plan.splice.get(name)
+        if spl and len(spl) == 1 and spl[0].whole:
+            return spl[0]
+        return None
+
+    def site(self, hp: HookPoint, x: torch.Tensor, spliced: bool = False) -> torch.Tensor:
+        plan = self.plan
+        name = hp.name
+        if plan is not None:
+            if not spliced and name in plan.splice:
+                for s in plan.splice[name]:
+                    x = s.apply(x)
+            if name in plan.scale:
+                x = x / plan.scale[name]
+            if name in plan.zero_grad and isinstance(x, torch.Tensor) and x.requires_grad:
+                idxs = plan.zero_grad[name]
+
+                def _mask(g, _idxs=idxs):
+                    g = g.clone()
+                    for ix in _idxs:
+                        g[ix.as_index] = 0
+                    return g
+
+                x = x.view_as(x)
+                x.register_hook(_mask)
+        x = hp(x)
+        if plan is not None and name in plan.capture:
+            plan.cache[name] = x.detach()
+            if self.remaining is not None:
+                self.remaining.discard(name)
+                if not self.remaining:
+                    raise _StopForward()
+        return x
+
+
+# ---------------------------------------------------------------------------- modules
+class Embed(nn.Module):
+    def __init__(self, cfg: HookedTransformerConfig):
+        super().__init__()
+        self.W_E = nn.Parameter(torch.empty(cfg.d_vocab, cfg.d_model))
+
+
+class PosEmbed(nn.Module):
+    def __init__(self, cfg: HookedTransformerConfig):
+        super().__init__()
+        self.W_pos = nn.Parameter(torch.empty(cfg.n_ctx, cfg.d_model))
+
+
+class Unembed(nn.Module):
+    def __init__(self, cfg: HookedTransformerConfig):
+        super().__init__()
+        self.W_U = nn.Parameter(torch.empty(cfg.d_model, cfg.d_vocab_out))
+        self.b_U = nn.Parameter(torch.zeros(cfg.d_vocab_out))
+
+
+class LayerNormSite(nn.Module):
+    """``LN`` (affine) or ``LNPre`` (no params) with TL hook names."""
+
+    def __init__(self, cfg: HookedTransformerConfig, affine: bool):
+        super().__init__()
+        self.eps = cfg.eps
+        if affine:
+            self.w = nn.Parameter(torch.ones(cfg.d_model))
+            self.b = nn.Parameter(torch.zeros(cfg.d_model))
+        else:
+            self.w = None
+            self.b = None
+        self.hook_scale = HookPoint()
+        self.hook_normalized = HookPoint()
+
+    def run(self, x, run: _Run):
+        if run.live(self.hook_scale) or run.live(self.hook_normalized) or not run.ops.fused:
+            return TorchOps.layer_norm(
+                run.ops, x, self.w, self.b, self.eps,
+                hook_scale=lambda t: run.site(self.hook_scale, t),
+                hook_normalized=lambda t: run.site(self.hook_normalized, t),
+            )
+        return run.ops.layer_norm(x, self.w, self.b, self.eps)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: HookedTransformerConfig, layer: int):
+        super().__init__()
+        H, d, dh = cfg.n_heads, cfg.d_model, cfg.d_head
+        self.cfg = cfg
+        self.layer = layer
+        self.W_Q = nn.Parameter(torch.empty(H, d, dh))
+        self.W_K = nn.Parameter(torch.empty(H, d, dh))
+        self.W_V = nn.Parameter(torch.empty(H, d, dh))
+        self.W_O = nn.Parameter(torch.empty(H, dh, d))
+        self.b_Q = nn.Parameter(torch.zeros(H, dh))
+        self.b_K = nn.Parameter(torch.zeros(H, dh))
+        self.b_V = nn.Parameter(torch.zeros(H, dh))
+        self.b_O = nn.Parameter(torch.zeros(d))
+        causal = torch.tril(torch.ones(cfg.n_ctx, cfg.n_ctx, dtype=torch.bool))
+        self.register_buffer("mask", causal)
+        self.register_buffer("IGNORE", torch.tensor(float("-inf")))
+        self.attn_scale = math.sqrt(dh) if cfg.use_attn_scale else 1.0
+        if cfg.scale_attn_by_inverse_layer_idx:
+            self.attn_scale *= layer + 1
+        self.hook_k = HookPoint()
+        self.hook_q = HookPoint()
+        self.hook_v = HookPoint()
+        self.hook_z = HookPoint()
+        self.hook_attn_scores = HookPoint()
+        self.hook_pattern = HookPoint()
+        self.hook_result = HookPoint()
+
+    def inner_live(self, run: _Run) -> bool:
+        return any(run.live(h) for h in (self.hook_q, self.hook_k, self.hook_v, self.hook_attn_scores,
+                                         self.hook_pattern))
+
+    def compute_z(self, x, run: _Run):
+        ops = run.ops
+        q, k, v = ops.qkv(x, self.W_Q, self.W_K, self.W_V, self.b_Q, self.b_K, self.b_V)
+        q = run.site(self.hook_q, q)
+        k = run.site(self.hook_k, k)
+        v = run.site(self.hook_v, v)
+        causal = self.cfg.attention_dir == "causal"
+        z_spl = run.plan.splice.get(self.hook_z.name) if run.plan is not None else None
+        if ops.fused and not (run.live(self.hook_attn_scores) or run.live(self.hook_pattern)):
+            heads = z_spl[0].head_mask(self.cfg.n_heads) if (z_spl and len(z_spl) == 1) else None
+            if heads is not None:
+                z = ops.attention(q, k, v, causal, self.attn_scale, patch_heads=heads, patch_src=z_spl[0].src)
+                return z, True
+            return ops.attention(q, k, v, causal, self.attn_scale), False
+        z = TorchOps.attention(
+            ops, q, k, v, causal, self.attn_scale,
+            hook_scores=lambda t: run.site(self.hook_attn_scores, t),
+            hook_pattern=lambda t: run.site(self.hook_pattern, t),
+            ignore=float(self.IGNORE),
+        )
+        return z, False
+
+
+class MLP(nn.Module):
+    def __init__(self, cfg: HookedTransformerConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.W_in = nn.Parameter(torch.empty(cfg.d_model, cfg.d_mlp))
+        self.b_in = nn.Parameter(torch.zeros(cfg.d_mlp))
+        self.W_out = nn.Parameter(torch.empty(cfg.d_mlp, cfg.d_model))
+        self.b_out = nn.Parameter(torch.zeros(cfg.d_model))
+        self.hook_pre = HookPoint()
+        self.hook_post = HookPoint()
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, cfg: HookedTransformerConfig, layer: int):
+        super().__init__()
+        self.cfg = cfg
+        self.layer = layer
+        affine = cfg.normalization_type == "LN"
+        if cfg.normalization_type not in ("LN", "LNPre", None):
+            raise NotImplementedError(f"normalization_type {cfg.normalization_type}")
+        self.ln1 = LayerNormSite(cfg, affine) if cfg.normalization_type else None
+        if not cfg.attn_only:
+            self.ln2 = LayerNormSite(cfg, affine) if cfg.normalization_type else None
+        self.attn = Attention(cfg, layer)
+        if not cfg.attn_only:
+            self.mlp = MLP(cfg)
+        self.hook_attn_in = HookPoint()
+        self.hook_q_input = HookPoint()
+        self.hook_k_input = HookPoint()
+        self.hook_v_input = HookPoint()
+        self.hook_mlp_in = HookPoint()
+        self.hook_attn_out = HookPoint()
+        self.hook_mlp_out = HookPoint()
+        self.hook_resid_pre = HookPoint()
+        if not cfg.attn_only:
+            self.hook_resid_mid = HookPoint()
+        self.hook_resid_post = HookPoint()
+
+    def _norm(self, ln, x, run):
+        if ln is None:
+            return x.to(run.ops.dtype)
+        return ln.run(x, run)
+
+    def forward(self, resid: torch.Tensor, run: _Run) -> torch.Tensor:
+        ops = run.ops
+        attn = self.attn
+        resid = run.site(self.hook_resid_pre, resid)
+
+        # ---- attention -----------------------------------------------------------
+        spl = run.whole_splice(attn.hook_z.name)
+        ln1_live = self.ln1 is not None and (run.live(self.ln1.hook_scale) or run.live(self.ln1.hook_normalized))
+        if spl is not None and not attn.inner_live(run) and not ln1_live:
+            z = run.site(attn.hook_z, spl.src.to(ops.dtype), spliced=True)
+        else:
+            x = self._norm(self.ln1, resid, run)
+            z, spliced = attn.compute_z(x, run)
+            z = run.site(attn.hook_z, z, spliced=spliced)
+        attn_out_live = run.live(self.hook_attn_out) or self.cfg.use_attn_result
+        if self.cfg.use_attn_result:
+            result = run.site(attn.hook_result, ops.o_result(z, attn.W_O))
+            attn_out = result.sum(-2) + ops.w(attn.b_O)
+            attn_out = run.site(self.hook_attn_out, attn_out)
+            resid_mid_pre = ops.residual(resid, attn_out)
+        elif attn_out_live or not ops.fused:
+            attn_out = run.site(self.hook_attn_out, ops.o_proj(z, attn.W_O, attn.b_O))
+            resid_mid_pre = ops.residual(resid, attn_out)
+        else:
+            resid_mid_pre = ops.o_proj_residual(z, attn.W_O, attn.b_O, resid)
+
+        if self.cfg.attn_only:
+            return run.site(self.hook_resid_post, resid_mid_pre)
+        resid_mid = run.site(self.hook_resid_mid, resid_mid_pre)
+
+        # ---- MLP -----------------------------------------------------------------
+        mlp = self.mlp
+        spl = run.whole_splice(mlp.hook_post.name)
+        ln2_live = self.ln2 is not None and (run.live(self.ln2.hook_scale) or run.live(self.ln2.hook_normalized))
+        if spl is not None and not run.live(mlp.hook_pre) and not ln2_live:
+            post = run.site(mlp.hook_post, spl.src.to(ops.dtype), spliced=True)
+        else:
+            x = self._norm(self.ln2, resid_mid, run)
+            pre_hook = (lambda t: run.site(mlp.hook_pre, t)) if run.live(mlp.hook_pre) else None
+            _, post = ops.mlp_in(x, mlp.W_in, mlp.b_in, self.cfg.act_fn, hook_pre=pre_hook)
+            post = run.site(mlp.hook_post, post)
+        if run.live(self.hook_mlp_out) or not ops.fused:
+            mlp_out = run.site(self.hook_mlp_out, ops.mlp_out(post, mlp.W_out, mlp.b_out))
+            resid_post = ops.residual(resid_mid, mlp_out)
+        else:
+            resid_post = ops.mlp_out_residual(post, mlp.W_out, mlp.b_out, resid_mid)
+        return run.site(self.hook_resid_post, resid_post)
+
+
+class HookedTransformer(HookedRootModule):
+    def __init__(self, cfg: Union[HookedTransformerConfig, dict], tokenizer=None, move_to_device: bool = True,
+                 default_padding_side: str = "right"):
+        super().__init__()
+        self.cfg = make_config(cfg)
+        cfg = self.cfg
+        self.tokenizer = tokenizer
+        self.embed = Embed(cfg)
+        self.hook_embed = HookPoint()
+        self.pos_embed = PosEmbed(cfg)
+        self.hook_pos_embed = HookPoint()
+        self.blocks = nn.ModuleList([TransformerBlock(cfg, l) for l in range(cfg.n_layers)])
+        if cfg.normalization_type in ("LN", "LNPre"):
+            self.ln_final = LayerNormSite(cfg, cfg.normalization_type == "LN")
+        else:
+            self.ln_final = None
+        self.unembed = Unembed(cfg)
+        self.op_backend: Optional[str] = None  # None = auto (see iit_amd.ops.select_ops)
+        if cfg.init_weights:
+            self.init_weights()
+        if move_to_device and cfg.device is not None:
+            self.to(cfg.device)
+        self.setup()
+
+    # ------------------------------------------------------------------ init
+    def init_weights(self) -> None:
+        """GPT-2 init (TL ``_init_weights_gpt2``): N(0, initializer_range) for every ``W_*``."""
+        for name, p in self.named_parameters():
+            if "W_" in name:
+                nn.init.normal_(p, std=self.cfg.initializer_range)
+
+    # ------------------------------------------------------------------ backend
+    def set_op_backend(self, backend: Optional[str]) -> "HookedTransformer":
+        self.op_backend = backend
+        return self
+
+    def ops(self):
+        return select_ops(self, self.op_backend)
+
+    # ------------------------------------------------------------------ forward
+    def _embed(self, tokens: torch.Tensor, run: _Run) -> torch.Tensor:
+        ops = run.ops
+        B, S = tokens.shape
+        if ops.fused and not (run.live(self.hook_embed) or run.live(self.hook_pos_embed)):
+            return ops.embed_pos(tokens, self.embed.W_E, self.pos_embed.W_pos)
+        e = run.site(self.hook_embed, ops.embed(tokens, self.embed.W_E))
+        p = run.site(self.hook_pos_embed, ops.pos_embed(B, S, self.pos_embed.W_pos))
+        return ops.residual(e, p)
+
+    def forward(self, input, return_type: Optional[str] = "logits", loss_per_token: bool = False,
+                prepend_bos: Optional[bool] = None, stop_at_layer: Optional[int] = None,
+                past_kv_cache=None, *, plan: Optional[RunPlan] = None, logits_at: Optional[int] = None):
+        tokens = self.to_tokens(input, prepend_bos=prepend_bos) if isinstance(input, (str, list)) else input
+        if tokens.dim() == 1:
+            tokens = tokens.unsqueeze(0)
+        if tokens.device != self.embed.W_E.device:
+            tokens = tokens.to(self.embed.W_E.device)
+        run = _Run(plan, self.ops())
+        try:
+            resid = self._embed(tokens, run)
+            n_blocks = len(self.blocks) if stop_at_layer is None else stop_at_layer
+            for block in self.blocks[:n_blocks]:
+                resid = block(resid, run)
+            if stop_at_layer is not None:
+                return resid
+            want = plan.logits if plan is not None else ("last" if logits_at == -1 else "full")
+            if plan is not None and plan.logits == "none":
+                return None
+            if return_type is None:
+                return None
+            if want == "last":
+                resid = resid[:, -1:]
+            x = resid if self.ln_final is None else self.ln_final.run(resid, run)
+            if want == "argmax":
+                return run.ops.unembed_argmax(x, self.unembed.W_U, self.unembed.b_U)
+            logits = run.ops.unembed(x, self.unembed.W_U, self.unembed.b_U)
+            if want == "last":
+                logits = logits[:, 0]
+            if return_type == "logits":
+                return logits
+            loss = lm_cross_entropy_loss(logits.float(), tokens, per_token=loss_per_token)
+            if return_type == "loss":
+                return loss
+            if return_type == "both":
+                return logits, loss
+            raise ValueError(f"invalid return_type {return_type}")
+        except _StopForward:
+            return None
+
+    # ------------------------------------------------------------------ helpers
+    supports_run_plan = True
+
+    def run_capture(self, tokens: torch.Tensor, names, truncate: bool = True, base_plan: Optional[RunPlan] = None):
+        """Source run of an interchange intervention: no grad, capture ``names`` only, stop early."""
+        plan = RunPlan.capture_only(list(names), truncate=truncate)
+        if base_plan is not None:
+            plan = base_plan.merged(plan)
+        with torch.no_grad():
+            self.forward(tokens, plan=plan)
+        return plan.cache
+
+    def to_tokens(self, input, prepend_bos: Optional[bool] = None):
+        if self.tokenizer is None:
+            raise ValueError("to_tokens requires a tokenizer")
+        bos = self.cfg.default_prepend_bos if prepend_bos is None else prepend_bos
+        texts = [input] if isinstance(input, str) else list(input)
+        rows = [([self.tokenizer.bos_token_id] if bos else []) + self.tokenizer.encode(t) for t in texts]
+        width = max(len(r) for r in rows)
+        pad = self.tokenizer.pad_token_id if self.tokenizer.pad_token_id is not None else 0
+        rows = [r + [pad] * (width - len(r)) for r in rows]
+        return torch.tensor(rows, dtype=torch.long, device=self.embed.W_E.device)
+
+    @property
+    def W_E(self):
+        return self.embed.W_E
+
+    @property
+    def W_U(self):
+        return self.unembed.W_U
+
+    @property
+    def W_pos(self):
+        return self.pos_embed.W_pos
+
+
+def lm_cross_entropy_loss(logits: torch.Tensor, tokens: torch.Tensor, per_token: bool = False):
+    logp = torch.log_softmax(logits, dim=-1)
+    picked = logp[:, :-1].gather(-1, tokens[:, 1:, None])[..., 0]
+    return -picked if per_token else -picked.mean()

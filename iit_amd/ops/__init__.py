@@ -1,0 +1,44 @@
+"""Op backends for the native LL models.
+
+* ``torch`` – :class:`TorchOps`, reference semantics, any device / dtype (oracle).
+* ``hip``   – :class:`iit_amd.ops.hip_ops.HipOps`, hand-written gfx950 kernels
+  (bf16 activations, fp32 accumulation / residual stream / master weights).
+
+``select_ops(model, backend)`` picks per call: ``backend=None`` means "hip when
+the model lives on a GPU and computes in bf16, else torch".  Asking for ``hip``
+explicitly on a GPU when the extension is not built raises (no silent fallback).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .torch_ops import TorchOps, gelu_new
+
+_TORCH_OPS_CACHE = {}
+
+
+def _torch_ops(dtype):
+    ops = _TORCH_OPS_CACHE.get(dtype)
+    if ops is None:
+        ops = _TORCH_OPS_CACHE[dtype] = TorchOps(dtype)
+    return ops
+
+
+def select_ops(model, backend: Optional[str] = None):
+    cfg = model.cfg
+    dtype = cfg.dtype
+    on_gpu = next(model.parameters()).is_cuda
+    if backend is None:
+        from .. import config as _config
+        env = _config.backend()
+        backend = "hip" if (on_gpu and dtype == torch.bfloat16 and env == "hip") else "torch"
+    if backend == "torch":
+        return _torch_ops(dtype)
+    if backend == "hip":
+        if not on_gpu:
+            raise RuntimeError("hip op backend requires the model on a GPU")
+        from .hip_ops import get_hip_ops
+        return get_hip_ops(model)
+    raise ValueError(f"unknown op backend {backend}")

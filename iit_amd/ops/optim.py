@@ -1,0 +1,97 @@
+"""Fused clip + Adam over a flat parameter arena.
+
+Math is ``torch.optim.Adam`` (amsgrad=False) preceded by
+``clip_grad_norm_(params, max_norm)`` exactly as the reference does in
+``step_on_loss`` (``/root/reference/iit/model_pairs/iit_behavior_model_pair.py:60-64``,
+``base_model_pair.py:176-180,229``): total L2 norm over every parameter,
+``coef = min(1, max_norm / (norm + 1e-6))``.
+
+On a GPU with the HIP extension loaded the whole update is two launches
+(a two-stage global-norm reduction and one fused clip+Adam+bf16-shadow pass);
+the norm never leaves the device, so a training step has no host sync.
+Elsewhere a vectorised torch implementation of the same math is used.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from ..engine.flat import FlatParams
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, use_hip: Optional[bool] = None):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(flat.params, defaults)
+        self.flat = flat
+        self.exp_avg = torch.zeros_like(flat.data)
+        self.exp_avg_sq = torch.zeros_like(flat.data)
+        self.step_count = 0
+        self._norm_buf = torch.zeros(2, dtype=torch.float32, device=flat.data.device)
+        if use_hip is None:
+            use_hip = flat.data.is_cuda
+        self._hip = None
+        if use_hip:
+            from . import hip_kernels
+            self._hip = hip_kernels.lib()
+
+    def zero_grad(self, set_to_none: bool = False):  # noqa: D401 - arena memset
+        self.flat.zero_grad()
+
+    @torch.no_grad()
+    def step(self, closure=None, clip_norm: Optional[float] = None):
+        if closure is not None:
+            with torch.enable_grad():
+                closure()
+        self.flat.rebind_grads()
+        group = self.param_groups[0]
+        lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+        self.step_count += 1
+        t = self.step_count
+        bc1 = 1.0 - b1 ** t
+        bc2 = 1.0 - b2 ** t
+        g = self.flat.grad
+        if self._hip is not None:
+            from . import hip_kernels
+            hip_kernels.adam_step(self.flat, self.exp_avg, self.exp_avg_sq, self._norm_buf, lr=lr, b1=b1, b2=b2,
+                                  eps=eps, wd=wd, bc1=bc1, bc2=bc2, clip_norm=clip_norm)
+        else:
+            if clip_norm:
+                norm = torch.linalg.vector_norm(g)
+                g.mul_(torch.clamp(clip_norm / (norm + 1e-6), max=1.0))
+            if wd:
+                g = g.add(self.flat.data, alpha=wd)
+            self.exp_avg.mul_(b1).add_(g, alpha=1 - b1)
+            self.exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
+            denom = (self.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(eps)
+            self.flat.data.addcdiv_(self.exp_avg, denom, value=-lr / bc1)
+            self.flat.refresh_shadow()
+        for p in self.flat.params:
+            self.state[p]["step"] = t
+
+    # ---------------------------------------------------------------- checkpointing
+    def state_dict(self):
+        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+                "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd["step"])
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        for g, saved in zip(self.param_groups, sd["param_groups"]):
+            g.update(saved)
+
+
+def clip_grad_norm_(params, max_norm: float) -> torch.Tensor:
+    """Sync-free global-norm clip (same math as ``torch.nn.utils.clip_grad_norm_``)."""
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return torch.zeros(())
+    norm = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(g) for g in grads]))
+    coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+    for g in grads:
+        g.mul_(coef)
+    return norm

@@ -1,0 +1,78 @@
+"""Process-group plumbing: one process per MI355X, RCCL over xGMI.
+
+``torch.distributed`` backend ``"nccl"`` *is* RCCL on ROCm.  ``init_distributed``
+reads the torchrun env (``RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*``), binds the
+process to ``cuda:LOCAL_RANK`` and falls back to ``gloo`` on CPU (the CPU test
+path).  Rendezvous defaults to 127.0.0.1.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+def is_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def rank() -> int:
+    return dist.get_rank() if is_initialized() else 0
+
+
+def world_size() -> int:
+    return dist.get_world_size() if is_initialized() else 1
+
+
+def is_main() -> bool:
+    return rank() == 0
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> bool:
+    """Initialise the default process group from torchrun env vars. Returns True if distributed."""
+    if is_initialized():
+        return True
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1:
+        return False
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+    return True
+
+
+def barrier():
+    if is_initialized():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
+    """Make every rank start from rank ``src``'s parameters and buffers."""
+    if not is_initialized() or world_size() == 1:
+        return
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t.data, src)
+
+
+def all_reduce_mean_(t: torch.Tensor) -> torch.Tensor:
+    if is_initialized() and world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t.div_(world_size())
+    return t
+
+
+def destroy():
+    if is_initialized():
+        dist.destroy_process_group()

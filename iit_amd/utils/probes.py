@@ -1,0 +1,116 @@
+"""Linear probes from LL node activations to HL intermediate variables.
+
+Parity: ``/root/reference/iit/utils/probes.py:8-132``.  A probe is a bias-free
+``nn.Linear`` from the flattened node activation (``cache[name][index]``) to the
+HL node's ``num_classes``; ground truth comes from
+``hl_model.get_idx_to_intermediate(name)(int_vars)``.  Probe GEMMs are plain
+library GEMMs (hipBLASLt via torch), SURVEY.md §2.3 K22.
+
+On native LL models the activations are gathered with a capture-only plan (only
+the probed hooks, forward truncated after the deepest), instead of caching every
+hook of a full forward.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Optional
+
+import torch
+import torch.nn as nn
+
+from ..config import DEVICE
+from ..core.nodes import HLNode, LLNode
+
+
+def _nodes(v) -> List[LLNode]:
+    return [v] if isinstance(v, LLNode) else list(v)
+
+
+def capture_hooks(ll_model, x: torch.Tensor, names: Iterable[str]) -> Dict[str, torch.Tensor]:
+    names = sorted(set(names))
+    if getattr(ll_model, "supports_run_plan", False) or hasattr(ll_model, "run_capture"):
+        return ll_model.run_capture(x, names)
+    _, cache = ll_model.run_with_cache(x, names_filter=lambda n: n in names)
+    return cache
+
+
+def construct_probe(high_level_node: HLNode, ll_nodes, dummy_cache, bias: bool = False) -> nn.Linear:
+    nodes = _nodes(ll_nodes)
+    if len(nodes) > 1:
+        raise NotImplementedError("probing a union of LL nodes is not supported")
+    size = sum(dummy_cache[n.name][n.index.as_index].flatten().shape[0] for n in nodes)
+    return nn.Linear(size, high_level_node.num_classes, bias=bias).to(DEVICE)
+
+
+def construct_probes(model_pair, input_shape, bias: bool = False, input_dtype: Optional[torch.dtype] = None):
+    dtype = input_dtype
+    if dtype is None:
+        dtype = torch.long if getattr(model_pair.ll_model, "supports_run_plan", False) else torch.float32
+    names = [n.name for v in model_pair.corr.values() for n in _nodes(v)]
+    with torch.no_grad():
+        dummy = capture_hooks(model_pair.ll_model, torch.zeros(input_shape, dtype=dtype, device=DEVICE), names)
+    return {hl.name: construct_probe(hl, lls, dummy, bias=bias) for hl, lls in model_pair.corr.items()}
+
+
+def probe_logits(probe: nn.Linear, cache, ll_node: LLNode) -> torch.Tensor:
+    act = cache[ll_node.name][ll_node.index.as_index]
+    return probe(act.reshape(-1, probe.weight.shape[1]).to(probe.weight.dtype))
+
+
+def train_probes_on_model_pair(model_pair, input_shape, train_set, training_args: dict):
+    probes = construct_probes(model_pair, input_shape=input_shape)
+    params = [p for probe in probes.values() for p in probe.parameters()]
+    for probe in probes.values():
+        probe.train()
+    opt = torch.optim.Adam(params, lr=training_args["lr"])
+    criterion = nn.CrossEntropyLoss()
+    losses = {k: [] for k in probes}
+    accs = {k: [] for k in probes}
+    loader = torch.utils.data.DataLoader(train_set, batch_size=training_args["batch_size"], shuffle=True,
+                                         num_workers=training_args.get("num_workers", 0))
+    names = [n.name for v in model_pair.corr.values() for n in _nodes(v)]
+    for _ in range(training_args["epochs"]):
+        loss_run = {k: torch.zeros((), device=DEVICE) for k in probes}
+        acc_run = {k: torch.zeros((), device=DEVICE) for k in probes}
+        for x, y, int_vars in loader:
+            opt.zero_grad()
+            x = x.to(DEVICE)
+            with torch.no_grad():
+                cache = capture_hooks(model_pair.ll_model, x, names)
+            total = 0
+            for hl_name, probe in probes.items():
+                gt = model_pair.hl_model.get_idx_to_intermediate(hl_name)(int_vars.to(DEVICE)).to(DEVICE)
+                for node in _nodes(model_pair.corr[hl_name]):
+                    out = probe_logits(probe, cache, node)
+                    l = criterion(out, gt)
+                    total = total + l
+                    loss_run[hl_name] += l.detach()
+                    acc_run[hl_name] += (out.argmax(1) == gt).float().mean()
+            total.backward()
+            opt.step()
+        n = max(1, len(loader))
+        for k in probes:
+            losses[k].append(float(loss_run[k]) / n)
+            accs[k].append(float(acc_run[k]) / n)
+    return {"probes": probes, "loss": losses, "accuracy": accs}
+
+
+def evaluate_probe(probes, model_pair, test_set, criterion):
+    stats = {"test loss": {}, "test accuracy": {}}
+    names = [n.name for v in model_pair.corr.values() for n in _nodes(v)]
+    loader = torch.utils.data.DataLoader(test_set, batch_size=256, shuffle=True, num_workers=0)
+    for hl_name, probe in probes.items():
+        probe.eval()
+        loss = torch.zeros((), device=DEVICE)
+        acc = torch.zeros((), device=DEVICE)
+        with torch.no_grad():
+            for x, y, int_vars in loader:
+                cache = capture_hooks(model_pair.ll_model, x.to(DEVICE), names)
+                gt = model_pair.hl_model.get_idx_to_intermediate(hl_name)(int_vars.to(DEVICE)).to(DEVICE)
+                for node in _nodes(model_pair.corr[hl_name]):
+                    out = probe_logits(probe, cache, node)
+                    loss += criterion(out, gt)
+                    acc += (out.argmax(1) == gt).float().mean()
+        n = max(1, len(loader))
+        stats["test loss"][hl_name] = float(loss) / n
+        stats["test accuracy"][hl_name] = float(acc) / n
+    return stats
