@@ -1,0 +1,156 @@
+"""Headline benchmark: IIT (base, source) intervened pairs/sec on IOI with a GPT-2-small LL model.
+
+Config (BASELINE.json): IOI task, LL = GPT-2-small architecture (12L / 768d / 12H,
+d_mlp 3072, V 50257, LNPre, gelu_new) with random init, bf16 compute (fp32
+master weights / Adam), IOI_ModelPair strict IIT + behaviour multi-task step
+exactly as ``train_ioi.py`` (batch 256 per GPU, Adam lr 1e-4, weights
+iit/behaviour/strict = 1/1/0.4, clip 1.0): per step one IIT, one strict and one
+behaviour optimizer update (3 backward passes, 5 LL forwards, 2 HL forwards).
+Data: synthetic offline IOI prompts (BOS + 16 tokens), see iit_amd.tasks.ioi.
+
+Weak scaling: every rank processes ``--batch`` pairs per step; the value is the
+whole-job rate (global pairs / max-over-ranks step time).
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="pairs per GPU per step")
+    ap.add_argument("--model", default="gpt2-small", choices=["gpt2-small", "ioi-6l"])
+    ap.add_argument("--engine", default="native", choices=["native", "reference"],
+                    help="reference = reference-semantics eager path (hook closures, full caches, full logits)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--graphs", type=int, default=int(os.environ.get("IIT_GRAPHS", "0")))
+    ap.add_argument("--profile-dir", default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    from iit_amd.parallel import dist as pdist
+    distributed = pdist.init_distributed()
+    rank, world = pdist.rank(), pdist.world_size()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+    from iit_amd.data.iit_dataset import IITDataset, train_test_split
+    from iit_amd.model_pairs import IOI_ModelPair
+    from iit_amd.models.config import gpt2_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.tasks.ioi import ioi_cfg, make_ioi_corr, make_ioi_dataset_and_hl
+
+    torch.manual_seed(0)
+    np.random.seed(0)
+    cfg = gpt2_config_dict()
+    if args.model == "ioi-6l":
+        cfg.update(ioi_cfg)
+    cfg.update(device=str(dev), init_weights=True,
+               dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32)
+    ll = HookedTransformer(cfg)
+    if args.engine == "reference" or args.dtype == "fp32":
+        ll.set_op_backend("torch")
+    ds, hl = make_ioi_dataset_and_hl(12000, ll, device=dev,
+                                     label_format="onehot" if args.engine == "reference" else "index")
+    train_ds, test_ds = train_test_split(ds, test_size=0.2, random_state=42)
+    train_set = IITDataset(train_ds, train_ds, seed=0, device=dev)
+    test_set = IITDataset(test_ds, test_ds, seed=0, device=dev)
+    training_args = {"batch_size": args.batch, "lr": 1e-4, "iit_weight": 1.0, "behavior_weight": 1.0,
+                     "strict_weight": 0.4, "next_token": False, "lr_scheduler": None, "clip_grad_norm": 1.0,
+                     "early_stop": True, "use_single_loss": False, "engine": args.engine}
+    pair = IOI_ModelPair(ll_model=ll, hl_model=hl, corr=make_ioi_corr(cfg["n_layers"]), training_args=training_args)
+    pdist.broadcast_module(ll)
+    opt = pair.make_optimizer(training_args["lr"])
+    loss_fn = pair.loss_fn
+    loader = train_set.make_loader(args.batch, 0)
+
+    def batches():
+        while True:
+            for b in loader:
+                yield b
+
+    it = batches()
+    step_fn = pair.run_train_step
+    if args.graphs:
+        from iit_amd.engine.graphs import GraphedTrainStep
+        step_fn = GraphedTrainStep(pair, opt, loss_fn)
+
+    for _ in range(args.warmup):
+        base, abl = next(it)
+        step_fn(base, abl, loss_fn, opt)
+    batches_timed = [next(it) for _ in range(args.steps)]
+    pdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for base, abl in batches_timed:
+        out = step_fn(base, abl, loss_fn, opt)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    pdist.barrier()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev if distributed and dev.type == "cuda" else "cpu")
+    if distributed:
+        torch.distributed.all_reduce(dt_t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    ms = dt / args.steps * 1000.0
+    global_batch = args.batch * world
+    value = global_batch * args.steps / dt
+
+    # IIA / accuracy on held-out pairs (outside the timed region)
+    metrics = pair.make_test_metrics()
+    with torch.no_grad():
+        for i, (base, abl) in enumerate(test_set.make_loader(args.batch, 0)):
+            metrics.update(pair.run_eval_step(base, abl, loss_fn))
+            if i >= 3:
+                break
+    vals = metrics.to_dict()
+    train_loss = {k: float(v) for k, v in out.items()} if isinstance(out, dict) else {}
+
+    if rank == 0:
+        rec = {
+            "metric": "IIT (base,source) intervened pairs/sec, IOI GPT-2-small, IOI_ModelPair IIT+strict+behavior step",
+            "value": round(value, 2),
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (offline IOI prompts, random-init weights)",
+            "config": {"model": "gpt2-small 12L/768d/12H (TL GPT-2 cfg, LNPre, gelu_new, V=50257)"
+                       if args.model == "gpt2-small" else "ioi-6l 6L/64d/4H",
+                       "global_batch": global_batch, "seq_len": int(train_set.base_data.dataset.prompts.shape[1] - 1),
+                       "parallelism": f"dp{world}", "engine": args.engine, "graphs": bool(args.graphs)},
+            "val_IIA": round(float(vals["val/IIA"]), 3),
+            "val_accuracy": round(float(vals["val/accuracy"]), 3),
+            "last_train_losses": {k: round(v, 4) for k, v in train_loss.items()},
+        }
+        print(json.dumps(rec))
+    pdist.destroy()
+
+
+if __name__ == "__main__":
+    main()

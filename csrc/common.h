@@ -1,0 +1,45 @@
+// Shared helpers for the iit_amd gfx950 (MI355X / CDNA4) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+#define IIT_EXPORT extern "C" __attribute__((visibility("default")))
+
+__device__ __forceinline__ float bf2f(__bf16 v) { return (float)v; }
+__device__ __forceinline__ __bf16 f2bf(float v) { return (__bf16)v; }
+__device__ __forceinline__ float u16_to_f(u16 v) { return __uint_as_float(((unsigned)v) << 16); }
+
+// wave64 reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// gelu_new (tanh approximation, as TransformerLens / GPT-2)
+__device__ __forceinline__ float gelu_new_f(float x) {
+  const float c = 0.7978845608028654f;  // sqrt(2/pi)
+  float u = c * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float gelu_new_grad_f(float x) {
+  const float c = 0.7978845608028654f;
+  float x2 = x * x;
+  float u = c * (x + 0.044715f * x2 * x);
+  float t = tanhf(u);
+  float du = c * (1.f + 3.f * 0.044715f * x2);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
+}
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,565 @@
+// Non-GEMM kernels of the iit_amd engine for gfx950 (MI355X).  All wave64-native.
+//
+//  embed_pos_fwd / embed_bwd / pos_bwd     token+position embedding (fp32 residual stream)
+//  ln_fwd / ln_bwd                          LN / LNPre, one wave per row, fp32 stats
+//  attn_small_fwd / attn_small_bwd          causal attention for S <= 64, dh <= 128, one
+//                                           workgroup per (batch, head); per-head splice of
+//                                           hook_z inside the kernel (patched heads copy the
+//                                           source z and get zero q/k/v gradient)
+//  ce_fwd / ce_bwd                          row-wise cross entropy over the vocab (+argmax)
+//  sumsq_partial / adam_flat                global-norm clip + Adam over the flat arena
+//  shadow_refresh                           fp32 master -> bf16 compute copies (+transposes)
+//  colsum_accum, dgelu, add_f32, cast       small elementwise / reduction helpers
+#include "common.h"
+
+// ============================================================================ embedding
+__global__ void embed_pos_fwd_kernel(const long* __restrict__ tok, const float* __restrict__ WE,
+                                     const float* __restrict__ Wpos, float* __restrict__ out, int T, int S, int d) {
+  const int t = blockIdx.x;
+  if (t >= T) return;
+  const long v = tok[t];
+  const int s = t % S;
+  const float4* e = (const float4*)(WE + v * (long)d);
+  const float4* p = (const float4*)(Wpos + (long)s * d);
+  float4* o = (float4*)(out + (long)t * d);
+  for (int i = threadIdx.x; i < d / 4; i += blockDim.x) {
+    float4 a = e[i], b = p[i];
+    o[i] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+}
+
+IIT_EXPORT int iit_embed_pos_fwd(const long* tok, const float* WE, const float* Wpos, float* out, int T, int S,
+                                 int d, void* stream) {
+  hipLaunchKernelGGL(embed_pos_fwd_kernel, dim3(T), dim3(d >= 256 ? 64 : 64), 0, (hipStream_t)stream, tok, WE, Wpos,
+                     out, T, S, d);
+  return hipGetLastError();
+}
+
+// dW_E[tok[t]] += g[t]   (fp32 atomics, one 256-B segment per wave-instruction)
+__global__ void embed_bwd_kernel(const long* __restrict__ tok, const float* __restrict__ g, float* __restrict__ dWE,
+                                 int T, int d) {
+  const int t = blockIdx.x;
+  const long v = tok[t];
+  for (int i = threadIdx.x; i < d; i += blockDim.x) atomicAdd(dWE + v * (long)d + i, g[(long)t * d + i]);
+}
+
+// dW_pos[s] += sum_b g[b, s]
+__global__ void pos_bwd_kernel(const float* __restrict__ g, float* __restrict__ dWpos, int B, int S, int d) {
+  const int s = blockIdx.x;
+  for (int i = threadIdx.x; i < d; i += blockDim.x) {
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) acc += g[((long)b * S + s) * d + i];
+    dWpos[(long)s * d + i] += acc;
+  }
+}
+
+IIT_EXPORT int iit_embed_pos_bwd(const long* tok, const float* g, float* dWE, float* dWpos, int B, int S, int d,
+                                 void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dWE) hipLaunchKernelGGL(embed_bwd_kernel, dim3(B * S), dim3(256), 0, st, tok, g, dWE, B * S, d);
+  if (dWpos) hipLaunchKernelGGL(pos_bwd_kernel, dim3(S), dim3(256), 0, st, g, dWpos, B, S, d);
+  return hipGetLastError();
+}
+
+// ============================================================================ layer norm
+// y = (x - mean) * rstd  (* w + b);   one wave per row, up to 32 floats per lane (d <= 2048)
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ b, __bf16* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int T, int d, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const float* xr = x + (long)row * d;
+  float v[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    v[i] = c < d ? xr[c] : 0.f;
+    s += v[i];
+  }
+  const float mu = wave_sum(s) / d;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    const float z = c < d ? v[i] - mu : 0.f;
+    v[i] = z;
+    s2 += z * z;
+  }
+  const float rstd = rsqrtf(wave_sum(s2) / d + eps);
+  __bf16* yr = y + (long)row * d;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < d) {
+      float o = v[i] * rstd;
+      if (w) o = o * w[c] + b[c];
+      yr[c] = f2bf(o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mu;
+    rstd_out[row] = rstd;
+  }
+}
+
+IIT_EXPORT int iit_ln_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd, int T,
+                          int d, float eps, void* stream) {
+  dim3 grid((T + 3) / 4), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  if (d <= 256) hipLaunchKernelGGL((ln_fwd_kernel<4>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps);
+  else if (d <= 1024) hipLaunchKernelGGL((ln_fwd_kernel<16>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps);
+  else if (d <= 2048) hipLaunchKernelGGL((ln_fwd_kernel<32>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps);
+  else if (d <= 4096) hipLaunchKernelGGL((ln_fwd_kernel<64>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps);
+  else return (int)hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w;  dw += dy * xhat, db += dy
+template <int VPL, bool DY_F32>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const float* __restrict__ w, float* __restrict__ dx,
+                                                     float* __restrict__ dw, float* __restrict__ db, int T, int d,
+                                                     int accumulate) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const float mu = mean[row], rs = rstd[row];
+  float g[VPL], xh[VPL];
+  float sg = 0.f, sgx = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    float dy = 0.f, xv = 0.f;
+    if (c < d) {
+      dy = DY_F32 ? ((const float*)dy_)[(long)row * d + c] : bf2f(((const __bf16*)dy_)[(long)row * d + c]);
+      xv = (x[(long)row * d + c] - mu) * rs;
+      if (dw) {
+        atomicAdd(dw + c, dy * xv);
+        atomicAdd(db + c, dy);
+      }
+      if (w) dy *= w[c];
+    }
+    g[i] = dy;
+    xh[i] = xv;
+    sg += dy;
+    sgx += dy * xv;
+  }
+  sg = wave_sum(sg) / d;
+  sgx = wave_sum(sgx) / d;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < d) {
+      const float o = rs * (g[i] - sg - xh[i] * sgx);
+      float* p = dx + (long)row * d + c;
+      *p = accumulate ? *p + o : o;
+    }
+  }
+}
+
+IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
+                          const float* w, float* dx, float* dw, float* db, int T, int d, int accumulate, void* stream) {
+  dim3 grid((T + 3) / 4), block(256);
+  hipStream_t s = (hipStream_t)stream;
+#define LNB(V)                                                                                                   \
+  if (dy_f32) hipLaunchKernelGGL((ln_bwd_kernel<V, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate); \
+  else hipLaunchKernelGGL((ln_bwd_kernel<V, false>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate);
+  if (d <= 256) { LNB(4) }
+  else if (d <= 1024) { LNB(16) }
+  else if (d <= 2048) { LNB(32) }
+  else if (d <= 4096) { LNB(64) }
+  else return (int)hipErrorInvalidValue;
+#undef LNB
+  return hipGetLastError();
+}
+
+// ============================================================================ attention (S <= 64)
+// qkv: [B*S, ld_qkv] bf16 with q at column h*dh, k at HD + h*dh, v at 2*HD + h*dh (HD = H*dh).
+// z:   [B*S, ld_z] bf16 at column h*dh.  lse: [B*H*S] fp32.
+// head_mask bit h set => z[:, h] := zsrc[:, h] (interchange splice of hook_z).
+__global__ __launch_bounds__(64) void attn_small_fwd_kernel(const __bf16* __restrict__ qkv, __bf16* __restrict__ z,
+                                                            float* __restrict__ lse, const __bf16* __restrict__ zsrc,
+                                                            unsigned long long head_mask, int B, int S, int H, int dh,
+                                                            long ld_qkv, long ld_z, long ld_src, float scale, int causal) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int lane = threadIdx.x;
+  const int HD = H * dh;
+  const long row0 = (long)b * S;
+  if ((head_mask >> h) & 1ull) {
+    for (int i = lane; i < S * dh; i += 64) {
+      const int s = i / dh, e = i % dh;
+      z[(row0 + s) * ld_z + h * dh + e] = zsrc[(row0 + s) * ld_src + h * dh + e];
+    }
+    if (lse)
+      for (int s = lane; s < S; s += 64) lse[(long)bh * S + s] = 0.f;
+    return;
+  }
+  const int P = dh + 1;
+  float* q = sm;
+  float* k = q + S * P;
+  float* v = k + S * P;
+  float* pr = v + S * P;  // [S][S+1]
+  for (int i = lane; i < S * dh; i += 64) {
+    const int s = i / dh, e = i % dh;
+    const __bf16* r = qkv + (row0 + s) * ld_qkv + h * dh + e;
+    q[s * P + e] = bf2f(r[0]);
+    k[s * P + e] = bf2f(r[HD]);
+    v[s * P + e] = bf2f(r[2 * HD]);
+  }
+  __syncthreads();
+  const int SP = S + 1;
+  for (int i = lane; i < S * S; i += 64) {
+    const int qi = i / S, kj = i % S;
+    float acc = -INFINITY;
+    if (!causal || kj <= qi) {
+      acc = 0.f;
+      for (int e = 0; e < dh; ++e) acc += q[qi * P + e] * k[kj * P + e];
+      acc *= scale;
+    }
+    pr[qi * SP + kj] = acc;
+  }
+  __syncthreads();
+  for (int qi = lane; qi < S; qi += 64) {
+    float m = -INFINITY;
+    for (int kj = 0; kj < S; ++kj) m = fmaxf(m, pr[qi * SP + kj]);
+    float sum = 0.f;
+    for (int kj = 0; kj < S; ++kj) {
+      const float e = pr[qi * SP + kj] == -INFINITY ? 0.f : __expf(pr[qi * SP + kj] - m);
+      pr[qi * SP + kj] = e;
+      sum += e;
+    }
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+    for (int kj = 0; kj < S; ++kj) pr[qi * SP + kj] *= inv;
+    if (lse) lse[(long)bh * S + qi] = m + __logf(sum);
+  }
+  __syncthreads();
+  for (int i = lane; i < S * dh; i += 64) {
+    const int qi = i / dh, e = i % dh;
+    float acc = 0.f;
+    const int kmax = causal ? qi + 1 : S;
+    for (int kj = 0; kj < kmax; ++kj) acc += pr[qi * SP + kj] * v[kj * P + e];
+    z[(row0 + qi) * ld_z + h * dh + e] = f2bf(acc);
+  }
+}
+
+IIT_EXPORT int iit_attn_small_fwd(const void* qkv, void* z, float* lse, const void* zsrc, unsigned long long head_mask,
+                                  int B, int S, int H, int dh, long ld_qkv, long ld_z, long ld_src, float scale,
+                                  int causal, void* stream) {
+  if (S > 64 || dh > 128) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)(3 * S * (dh + 1) + S * (S + 1)) * sizeof(float);
+  hipLaunchKernelGGL(attn_small_fwd_kernel, dim3(B * H), dim3(64), lds, (hipStream_t)stream, (const __bf16*)qkv,
+                     (__bf16*)z, lse, (const __bf16*)zsrc, head_mask, B, S, H, dh, ld_qkv, ld_z, ld_src, scale, causal);
+  return hipGetLastError();
+}
+
+// dqkv written in the qkv layout; patched heads get zero gradient.
+__global__ __launch_bounds__(64) void attn_small_bwd_kernel(const __bf16* __restrict__ qkv, const __bf16* __restrict__ dz,
+                                                            const float* __restrict__ lse, __bf16* __restrict__ dqkv,
+                                                            unsigned long long head_mask, int B, int S, int H, int dh,
+                                                            long ld_qkv, long ld_dz, float scale, int causal) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int lane = threadIdx.x;
+  const int HD = H * dh;
+  const long row0 = (long)b * S;
+  if ((head_mask >> h) & 1ull) {
+    for (int i = lane; i < S * dh; i += 64) {
+      const int s = i / dh, e = i % dh;
+      __bf16* r = dqkv + (row0 + s) * ld_qkv + h * dh + e;
+      r[0] = f2bf(0.f);
+      r[HD] = f2bf(0.f);
+      r[2 * HD] = f2bf(0.f);
+    }
+    return;
+  }
+  const int P = dh + 1, SP = S + 1;
+  float* q = sm;
+  float* k = q + S * P;
+  float* v = k + S * P;
+  float* g = v + S * P;   // dz
+  float* pm = g + S * P;  // P  [S][S+1]
+  float* ds = pm + S * SP; // dS
+  for (int i = lane; i < S * dh; i += 64) {
+    const int s = i / dh, e = i % dh;
+    const __bf16* r = qkv + (row0 + s) * ld_qkv + h * dh + e;
+    q[s * P + e] = bf2f(r[0]);
+    k[s * P + e] = bf2f(r[HD]);
+    v[s * P + e] = bf2f(r[2 * HD]);
+    g[s * P + e] = bf2f(dz[(row0 + s) * ld_dz + h * dh + e]);
+  }
+  __syncthreads();
+  // recompute P and dP
+  for (int i = lane; i < S * S; i += 64) {
+    const int qi = i / S, kj = i % S;
+    float p = 0.f, dp = 0.f;
+    if (!causal || kj <= qi) {
+      float sc = 0.f;
+      for (int e = 0; e < dh; ++e) sc += q[qi * P + e] * k[kj * P + e];
+      p = __expf(sc * scale - lse[(long)bh * S + qi]);
+      for (int e = 0; e < dh; ++e) dp += g[qi * P + e] * v[kj * P + e];
+    }
+    pm[qi * SP + kj] = p;
+    ds[qi * SP + kj] = dp;
+  }
+  __syncthreads();
+  for (int qi = lane; qi < S; qi += 64) {
+    float dsum = 0.f;
+    for (int kj = 0; kj < S; ++kj) dsum += pm[qi * SP + kj] * ds[qi * SP + kj];
+    for (int kj = 0; kj < S; ++kj) ds[qi * SP + kj] = pm[qi * SP + kj] * (ds[qi * SP + kj] - dsum) * scale;
+  }
+  __syncthreads();
+  for (int i = lane; i < S * dh; i += 64) {
+    const int s = i / dh, e = i % dh;
+    float dq = 0.f, dk = 0.f, dv = 0.f;
+    for (int j = 0; j < S; ++j) {
+      dq += ds[s * SP + j] * k[j * P + e];   // dQ[s] = sum_kj dS[s][kj] K[kj]
+      dk += ds[j * SP + s] * q[j * P + e];   // dK[s] = sum_qi dS[qi][s] Q[qi]
+      dv += pm[j * SP + s] * g[j * P + e];   // dV[s] = sum_qi P[qi][s] dZ[qi]
+    }
+    __bf16* r = dqkv + (row0 + s) * ld_qkv + h * dh + e;
+    r[0] = f2bf(dq);
+    r[HD] = f2bf(dk);
+    r[2 * HD] = f2bf(dv);
+  }
+}
+
+IIT_EXPORT int iit_attn_small_bwd(const void* qkv, const void* dz, const float* lse, void* dqkv,
+                                  unsigned long long head_mask, int B, int S, int H, int dh, long ld_qkv, long ld_dz,
+                                  float scale, int causal, void* stream) {
+  if (S > 64 || dh > 128) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)(4 * S * (dh + 1) + 2 * S * (S + 1)) * sizeof(float);
+  hipLaunchKernelGGL(attn_small_bwd_kernel, dim3(B * H), dim3(64), lds, (hipStream_t)stream, (const __bf16*)qkv,
+                     (const __bf16*)dz, lse, (__bf16*)dqkv, head_mask, B, S, H, dh, ld_qkv, ld_dz, scale, causal);
+  return hipGetLastError();
+}
+
+// ============================================================================ cross entropy
+// one 256-thread block per row of fp32 logits: lse, loss = lse - x[label], argmax (first index on ties)
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ logits, long ld, const long* __restrict__ labels,
+                                                     float* __restrict__ loss, float* __restrict__ lse_out,
+                                                     long* __restrict__ amax, int V) {
+  __shared__ float sm[8];
+  __shared__ int si[8];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* x = logits + (long)row * ld;
+  float m = -INFINITY;
+  int mi = 0x7fffffff;
+  for (int i = tid; i < V; i += 256) {
+    const float v = x[i];
+    if (v > m) { m = v; mi = i; }
+  }
+  // (value, index) argmax with first-index tie-break
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64);
+    const int oi = __shfl_xor(mi, o, 64);
+    if (om > m || (om == m && oi < mi)) { m = om; mi = oi; }
+  }
+  if (lane == 0) { sm[w] = m; si[w] = mi; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int j = 1; j < 4; ++j)
+      if (sm[j] > sm[0] || (sm[j] == sm[0] && si[j] < si[0])) { sm[0] = sm[j]; si[0] = si[j]; }
+  }
+  __syncthreads();
+  m = sm[0];
+  mi = si[0];
+  float s = 0.f;
+  for (int i = tid; i < V; i += 256) s += __expf(x[i] - m);
+  s = wave_sum(s);
+  __syncthreads();
+  if (lane == 0) sm[4 + w] = s;
+  __syncthreads();
+  if (tid == 0) {
+    const float tot = sm[4] + sm[5] + sm[6] + sm[7];
+    const float l = m + __logf(tot);
+    if (lse_out) lse_out[row] = l;
+    if (loss && labels) loss[row] = l - x[labels[row]];
+    if (amax) amax[row] = mi;
+  }
+}
+
+IIT_EXPORT int iit_ce_fwd(const float* logits, long ld, const long* labels, float* loss, float* lse, long* amax, int R,
+                          int V, void* stream) {
+  hipLaunchKernelGGL(ce_fwd_kernel, dim3(R), dim3(256), 0, (hipStream_t)stream, logits, ld, labels, loss, lse, amax, V);
+  return hipGetLastError();
+}
+
+// dlogits = (softmax - onehot) * gscale[0] * inv_rows   (fp32 out, ld_out may be padded; pad columns zeroed)
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ logits, long ld, const long* __restrict__ labels,
+                                                     const float* __restrict__ lse, const float* __restrict__ gscale,
+                                                     float inv_rows, float* __restrict__ out, long ld_out, int V) {
+  const int row = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= ld_out) return;
+  float v = 0.f;
+  if (i < V) {
+    const float p = __expf(logits[(long)row * ld + i] - lse[row]);
+    v = (p - (i == labels[row] ? 1.f : 0.f)) * gscale[0] * inv_rows;
+  }
+  out[(long)row * ld_out + i] = v;
+}
+
+IIT_EXPORT int iit_ce_bwd(const float* logits, long ld, const long* labels, const float* lse, const float* gscale,
+                          float inv_rows, void* out, long ld_out, int R, int V, void* stream) {
+  dim3 grid((unsigned)((ld_out + 255) / 256), R);
+  hipLaunchKernelGGL(ce_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, logits, ld, labels, lse, gscale, inv_rows,
+                     (float*)out, ld_out, V);
+  return hipGetLastError();
+}
+
+// ============================================================================ optimizer
+// partial sums of g^2 per block (grid-stride over float4)
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ g, long n4, float* __restrict__ part) {
+  __shared__ float sm[4];
+  float s = 0.f;
+  const float4* g4 = (const float4*)g;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const float4 v = g4[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = sm[0] + sm[1] + sm[2] + sm[3];
+}
+
+// Adam (torch semantics, amsgrad=False) with the clip coefficient computed on device from the partial sums.
+__global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                                        float* __restrict__ v, long n4, const float* __restrict__ part,
+                                                        int nparts, float clip, float lr, float b1, float b2, float eps,
+                                                        float wd, float bc1, float bc2_sqrt) {
+  __shared__ float coef_s;
+  if (threadIdx.x < 64) {
+    float s = 0.f;
+    if (clip > 0.f)
+      for (int i = threadIdx.x; i < nparts; i += 64) s += part[i];
+    s = wave_sum(s);
+    if (threadIdx.x == 0) coef_s = clip > 0.f ? fminf(1.f, clip / (sqrtf(s) + 1e-6f)) : 1.f;
+  }
+  __syncthreads();
+  const float coef = coef_s;
+  const float step = lr / bc1;
+  float4* p4 = (float4*)p;
+  float4* g4 = (float4*)g;
+  float4* m4 = (float4*)m;
+  float4* v4 = (float4*)v;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 gg = g4[i], pp = p4[i], mm = m4[i], vv = v4[i];
+    float* gs = (float*)&gg;
+    float* ps = (float*)&pp;
+    float* ms = (float*)&mm;
+    float* vs = (float*)&vv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float gr = gs[e] * coef;
+      gs[e] = gr;
+      if (wd != 0.f) gr += wd * ps[e];
+      ms[e] = b1 * ms[e] + (1.f - b1) * gr;
+      vs[e] = b2 * vs[e] + (1.f - b2) * gr * gr;
+      ps[e] -= step * ms[e] / (sqrtf(vs[e]) / bc2_sqrt + eps);
+    }
+    g4[i] = gg;
+    p4[i] = pp;
+    m4[i] = mm;
+    v4[i] = vv;
+  }
+}
+
+IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, long n, float* part, int nparts, float clip,
+                             float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const long n4 = n / 4;
+  if (clip > 0.f) hipLaunchKernelGGL(sumsq_partial_kernel, dim3(nparts), dim3(256), 0, s, g, n4, part);
+  const int blocks = (int)min((n4 + 255) / 256, 4096L);
+  hipLaunchKernelGGL(adam_flat_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, n4, part, nparts, clip, lr, b1, b2,
+                     eps, wd, bc1, sqrtf(bc2));
+  return hipGetLastError();
+}
+
+// ============================================================================ shadow weights
+// dst (bf16) = src (fp32) viewed as [rows][cols]; transpose -> dst[c][r] with leading dim ld.
+struct ShadowDesc {
+  const float* src;
+  __bf16* dst;
+  int rows, cols;
+  long ld;
+  int transpose;
+  int pad_;
+};
+
+__global__ __launch_bounds__(256) void shadow_refresh_kernel(const ShadowDesc* __restrict__ descs) {
+  __shared__ float tile[32][33];
+  const ShadowDesc d = descs[blockIdx.y];
+  const int tiles_c = (d.cols + 31) / 32;
+  const int ntiles = tiles_c * ((d.rows + 31) / 32);
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int r0 = (t / tiles_c) * 32, c0 = (t % tiles_c) * 32;
+    if (!d.transpose) {
+      for (int i = ty; i < 32; i += 8) {
+        const int r = r0 + i, c = c0 + tx;
+        if (r < d.rows && c < d.cols) d.dst[(long)r * d.ld + c] = f2bf(d.src[(long)r * d.cols + c]);
+      }
+    } else {
+      for (int i = ty; i < 32; i += 8) {
+        const int r = r0 + i, c = c0 + tx;
+        tile[i][tx] = (r < d.rows && c < d.cols) ? d.src[(long)r * d.cols + c] : 0.f;
+      }
+      __syncthreads();
+      for (int i = ty; i < 32; i += 8) {
+        const int c = c0 + i, r = r0 + tx;
+        if (r < d.rows && c < d.cols) d.dst[(long)c * d.ld + r] = f2bf(tile[tx][i]);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+IIT_EXPORT int iit_shadow_refresh(const void* descs, int n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(shadow_refresh_kernel, dim3(512, n), dim3(256), 0, (hipStream_t)stream, (const ShadowDesc*)descs);
+  return hipGetLastError();
+}
+
+IIT_EXPORT int iit_shadow_desc_size() { return (int)sizeof(ShadowDesc); }
+
+// ============================================================================ small helpers
+// db[n] (+)= sum_t x[t][n]     x bf16 or fp32, row chunks of 64, fp32 atomics
+template <bool F32>
+__global__ void colsum_kernel(const void* __restrict__ x, long ld, float* __restrict__ out, int T, int N) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const int t0 = blockIdx.y * 64, t1 = min(T, t0 + 64);
+  float s = 0.f;
+  for (int t = t0; t < t1; ++t) s += F32 ? ((const float*)x)[(long)t * ld + n] : bf2f(((const __bf16*)x)[(long)t * ld + n]);
+  atomicAdd(out + n, s);
+}
+
+IIT_EXPORT int iit_colsum_accum(const void* x, int f32, long ld, float* out, int T, int N, void* stream) {
+  dim3 grid((N + 255) / 256, (T + 63) / 64);
+  if (f32) hipLaunchKernelGGL(colsum_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
+  else hipLaunchKernelGGL(colsum_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
+  return hipGetLastError();
+}
+
+// dpre = dpost * gelu_new'(pre)   (bf16, contiguous)
+__global__ void dgelu_kernel(const __bf16* __restrict__ dpost, const __bf16* __restrict__ pre, __bf16* __restrict__ out, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    out[i] = f2bf(bf2f(dpost[i]) * gelu_new_grad_f(bf2f(pre[i])));
+}
+
+IIT_EXPORT int iit_dgelu(const void* dpost, const void* pre, void* out, long n, void* stream) {
+  const int blocks = (int)min((n + 255) / 256, 8192L);
+  hipLaunchKernelGGL(dgelu_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const __bf16*)dpost,
+                     (const __bf16*)pre, (__bf16*)out, n);
+  return hipGetLastError();
+}
+
+IIT_EXPORT int iit_device_sync() { return hipDeviceSynchronize(); }

@@ -15,8 +15,9 @@ import numpy as np
 def _same(x, y) -> bool:
     try:
         import torch
-        if isinstance(x, torch.Tensor):
-            return isinstance(y, torch.Tensor) and x.shape == y.shape and bool((x == y).all())
+        if isinstance(x, torch.Tensor) or isinstance(y, torch.Tensor):
+            return (isinstance(x, torch.Tensor) and isinstance(y, torch.Tensor) and x.shape == y.shape
+                    and bool((x == y).all()))
     except ImportError:  # pragma: no cover
         pass
     if isinstance(x, np.ndarray):

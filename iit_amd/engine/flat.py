@@ -51,6 +51,9 @@ class FlatParams:
                 p.data = view
                 p.grad = self.grad[o:o + n].view(p.shape)
         self.index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
+        self.version = 0
+        self._listeners = []
+        module._flat_params = self
         if with_bf16_shadow:
             self.shadow = torch.empty(off, dtype=torch.bfloat16, device=dev)
             self.refresh_shadow()
@@ -73,6 +76,18 @@ class FlatParams:
     def grad_view(self, p: torch.Tensor) -> torch.Tensor:
         o, n = self.offsets[self.index[id(p)]]
         return self.grad[o:o + n].view(p.shape)
+
+    # ---------------------------------------------------------------- updates
+    def add_listener(self, fn) -> None:
+        """``fn()`` runs (on the current stream) after every optimizer update of the arena."""
+        self._listeners.append(fn)
+
+    def after_step(self) -> None:
+        self.version += 1
+        self.module._iit_weights_version = getattr(self.module, "_iit_weights_version", 0) + 1
+        self.refresh_shadow()
+        for fn in self._listeners:
+            fn()
 
     # ---------------------------------------------------------------- shadow
     def refresh_shadow(self) -> None:

@@ -62,6 +62,11 @@ class IOI_ModelPair(StrictIITModelPair):
             # last-position logits [B, V]; target may be [B], [B, V] probs, [B, S] ids or [B, S, V] probs
             if target.dim() == 3 or (target.dim() == 2 and not target.dtype.is_floating_point):
                 target = target[:, -1]
+            if target.dtype.is_floating_point and target.dim() == 2:
+                target = target.argmax(-1) if bool((target.sum(-1) == 1).all()) else target
+            if not target.dtype.is_floating_point:
+                from ..ops import cross_entropy
+                return cross_entropy(output, target)
             return F.cross_entropy(output, target)
         if self.next_token:
             B, S, V = output.shape

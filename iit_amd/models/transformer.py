@@ -317,6 +317,15 @@ class HookedTransformer(HookedRootModule):
             if "W_" in name:
                 nn.init.normal_(p, std=self.cfg.initializer_range)
 
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        res = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self.mark_weights_changed()
+        return res
+
+    def mark_weights_changed(self) -> None:
+        """Invalidate derived bf16 compute copies after an out-of-band weight update."""
+        self._iit_weights_version = getattr(self, "_iit_weights_version", 0) + 1
+
     # ------------------------------------------------------------------ backend
     def set_op_backend(self, backend: Optional[str]) -> "HookedTransformer":
         self.op_backend = backend
@@ -344,6 +353,9 @@ class HookedTransformer(HookedRootModule):
         if tokens.device != self.embed.W_E.device:
             tokens = tokens.to(self.embed.W_E.device)
         run = _Run(plan, self.ops())
+        begin = getattr(run.ops, "begin_forward", None)
+        if begin is not None:
+            begin()
         try:
             resid = self._embed(tokens, run)
             n_blocks = len(self.blocks) if stop_at_layer is None else stop_at_layer
@@ -357,13 +369,11 @@ class HookedTransformer(HookedRootModule):
             if return_type is None:
                 return None
             if want == "last":
-                resid = resid[:, -1:]
+                resid = resid[:, -1]  # [B, d]: only the position every IOI loss reads
             x = resid if self.ln_final is None else self.ln_final.run(resid, run)
             if want == "argmax":
                 return run.ops.unembed_argmax(x, self.unembed.W_U, self.unembed.b_U)
             logits = run.ops.unembed(x, self.unembed.W_U, self.unembed.b_U)
-            if want == "last":
-                logits = logits[:, 0]
             if return_type == "logits":
                 return logits
             loss = lm_cross_entropy_loss(logits.float(), tokens, per_token=loss_per_token)

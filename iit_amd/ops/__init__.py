@@ -42,3 +42,11 @@ def select_ops(model, backend: Optional[str] = None):
         from .hip_ops import get_hip_ops
         return get_hip_ops(model)
     raise ValueError(f"unknown op backend {backend}")
+
+
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """Mean CE with index targets; fused HIP kernel on GPU (fp32 logits, any row stride)."""
+    if logits.is_cuda and logits.dim() == 2 and not target.dtype.is_floating_point:
+        from .hip_ops import cross_entropy as _hip_ce
+        return _hip_ce(logits, target)
+    return torch.nn.functional.cross_entropy(logits.float(), target)

@@ -1,0 +1,82 @@
+"""Build the gfx950 kernel library in-tree: ``iit_amd/_native/libiit_hip.so``.
+
+Compiled directly with ``hipcc --offload-arch=gfx950`` (no hipify, no torch
+extension machinery): the library exposes a plain C ABI that
+:mod:`iit_amd.ops.hip_kernels` binds with ``ctypes`` and launches on the current
+torch stream, so every launch is capturable in HIP graphs.  A source hash stamp
+avoids rebuilding an up-to-date library (the built ``.so`` travels to the GPU box
+with the repository snapshot).
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+CSRC = os.path.join(ROOT, "csrc")
+OUT_DIR = os.path.join(ROOT, "iit_amd", "_native")
+LIB = os.path.join(OUT_DIR, "libiit_hip.so")
+SOURCES = ["gemm.hip", "kernels.hip", "flash_attn.hip"]
+ARCH = os.environ.get("IIT_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    return "hipcc"
+
+
+def sources():
+    return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+
+
+def source_hash() -> str:
+    h = hashlib.sha256()
+    for p in sources() + [os.path.join(CSRC, "common.h")]:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(ARCH.encode())
+    return h.hexdigest()[:16]
+
+
+def is_up_to_date() -> bool:
+    stamp = LIB + ".stamp"
+    return os.path.exists(LIB) and os.path.exists(stamp) and open(stamp).read().strip() == source_hash()
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and is_up_to_date():
+        return LIB
+    os.makedirs(OUT_DIR, exist_ok=True)
+    objs = []
+    procs = []
+    for src in sources():
+        obj = os.path.join(OUT_DIR, os.path.basename(src) + ".o")
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
+               "-I", CSRC, "-c", src, "-o", obj]
+        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        objs.append(obj)
+    for cmd, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError(f"hipcc failed: {' '.join(cmd)}\n{out.decode(errors='replace')}")
+        if verbose and out:
+            print(out.decode(errors="replace"))
+    tmp = LIB + ".tmp"
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    res = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if res.returncode != 0:
+        raise RuntimeError(f"link failed: {res.stdout.decode(errors='replace')}")
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    with open(LIB + ".stamp", "w") as f:
+        f.write(source_hash())
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,192 @@
+"""ctypes bindings to ``libiit_hip.so`` (the hand-written gfx950 kernels in ``csrc/``).
+
+Every launcher takes raw device pointers and the *current torch stream*, so the
+kernels interleave with torch ops and are captured by ``torch.cuda.graph``.
+Loading is strict: on a GPU, a missing / unbuildable library raises instead of
+silently falling back to PyTorch ops.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import build as _build
+
+c_void_p, c_long, c_int, c_float, c_ull = ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_float, ctypes.c_ulonglong
+
+EPI_BF16, EPI_BF16_BIAS3, EPI_F32_RESID, EPI_GELU, EPI_DGELU, EPI_F32_ACC, EPI_F32_ACC_QKV, EPI_F32_STORE = range(8)
+MODE_NN, MODE_AKM, MODE_BKM, MODE_AF32, MODE_BF32 = 0, 1, 2, 4, 8
+
+_LIB = None
+
+_SIGS = {
+    "iit_gemm": [c_void_p] * 10 + [c_long] * 5 + [c_int] * 12 + [c_void_p],
+    "iit_embed_pos_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "iit_embed_pos_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "iit_ln_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
+    "iit_ln_bwd": [c_void_p, c_int] + [c_void_p] * 7 + [c_int, c_int, c_int, c_void_p],
+    "iit_attn_small_fwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float, c_int,
+                                            c_void_p],
+    "iit_attn_small_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
+    "iit_ce_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "iit_ce_bwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_long, c_int, c_int, c_void_p],
+    "iit_adam_flat": [c_void_p] * 4 + [c_long, c_void_p, c_int] + [c_float] * 8 + [c_void_p],
+    "iit_shadow_refresh": [c_void_p, c_int, c_void_p],
+    "iit_shadow_desc_size": [],
+    "iit_colsum_accum": [c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_void_p],
+    "iit_dgelu": [c_void_p, c_void_p, c_void_p, c_long, c_void_p],
+    "iit_device_sync": [],
+}
+
+
+def lib():
+    """Load (building first if stale) the kernel library."""
+    global _LIB
+    if _LIB is None:
+        if not _build.is_up_to_date():
+            _build.build()
+        L = ctypes.CDLL(_build.LIB)
+        for name, argtypes in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argtypes
+            fn.restype = c_int
+        _LIB = L
+    return _LIB
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:
+        return False
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with hip error {rc}")
+
+
+# ------------------------------------------------------------------------------ GEMM
+N_CU = 256
+
+
+def _tiling(M: int, N: int, K: int, allow_split: bool):
+    t128 = math.ceil(M / 128) * math.ceil(N / 128)
+    if t128 >= 240:
+        return 1, 1
+    t64 = math.ceil(M / 64) * math.ceil(N / 64)
+    splits = 1
+    if allow_split and t64 < 240 and K >= 1024:
+        splits = max(1, min(math.ceil(480 / t64), K // 512))
+    return 0, splits
+
+
+def gemm(A, B, C, *, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, mode: int = MODE_NN, epi: int = EPI_BF16,
+         C2=None, C3=None, bias0=None, bias1=None, bias2=None, resid=None, ldr: int = 0, aux=None, ldc2: int = 0,
+         bias_cols: int = 0, qkv=(0, 0, 0), atomic: bool = False, splits: Optional[int] = None):
+    """C = A @ B (+ epilogue). Operand layouts: see ``csrc/gemm.hip``; strides in elements."""
+    can_split = epi in (EPI_F32_ACC, EPI_F32_ACC_QKV)
+    big, auto_splits = _tiling(M, N, K, can_split)
+    if splits is None:
+        splits = auto_splits
+    if K % 8 != 0 and not (mode & MODE_AKM):
+        if any(ld % 8 for ld in (lda,)):
+            pass
+    rc = lib().iit_gemm(_p(A), _p(B), _p(C), _p(C2), _p(C3), _p(bias0), _p(bias1), _p(bias2), _p(resid), _p(aux),
+                        lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi, splits, big, bias_cols, qkv[0], qkv[1], qkv[2],
+                        int(atomic), _stream())
+    _check(rc, "iit_gemm")
+
+
+# ------------------------------------------------------------------------------ others
+def embed_pos_fwd(tokens, W_E, W_pos, out, B, S, d):
+    _check(lib().iit_embed_pos_fwd(_p(tokens), _p(W_E), _p(W_pos), _p(out), B * S, S, d, _stream()), "embed_pos_fwd")
+
+
+def embed_pos_bwd(tokens, g, dWE, dWpos, B, S, d):
+    _check(lib().iit_embed_pos_bwd(_p(tokens), _p(g), _p(dWE), _p(dWpos), B, S, d, _stream()), "embed_pos_bwd")
+
+
+def ln_fwd(x, w, b, y, mean, rstd, T, d, eps):
+    _check(lib().iit_ln_fwd(_p(x), _p(w), _p(b), _p(y), _p(mean), _p(rstd), T, d, eps, _stream()), "ln_fwd")
+
+
+def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False):
+    _check(lib().iit_ln_bwd(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx), _p(dw),
+                            _p(db), T, d, int(accumulate), _stream()), "ln_bwd")
+
+
+def heads_to_mask(heads: Optional[Sequence[int]]) -> int:
+    m = 0
+    for h in heads or ():
+        m |= 1 << int(h)
+    return m
+
+
+def attn_small_fwd(qkv, z, lse, zsrc, head_mask, B, S, H, dh, ld_qkv, ld_z, ld_src, scale, causal):
+    _check(lib().iit_attn_small_fwd(_p(qkv), _p(z), _p(lse), _p(zsrc), head_mask, B, S, H, dh, ld_qkv, ld_z, ld_src,
+                                    scale, int(causal), _stream()), "attn_small_fwd")
+
+
+def attn_small_bwd(qkv, dz, lse, dqkv, head_mask, B, S, H, dh, ld_qkv, ld_dz, scale, causal):
+    _check(lib().iit_attn_small_bwd(_p(qkv), _p(dz), _p(lse), _p(dqkv), head_mask, B, S, H, dh, ld_qkv, ld_dz, scale,
+                                    int(causal), _stream()), "attn_small_bwd")
+
+
+def ce_fwd(logits, ld, labels, loss, lse, amax, R, V):
+    _check(lib().iit_ce_fwd(_p(logits), ld, _p(labels), _p(loss), _p(lse), _p(amax), R, V, _stream()), "ce_fwd")
+
+
+def ce_bwd(logits, ld, labels, lse, gscale, inv_rows, out, ld_out, R, V):
+    _check(lib().iit_ce_bwd(_p(logits), ld, _p(labels), _p(lse), _p(gscale), inv_rows, _p(out), ld_out, R, V,
+                            _stream()), "ce_bwd")
+
+
+def colsum_accum(x, ld, out, T, N):
+    _check(lib().iit_colsum_accum(_p(x), int(x.dtype == torch.float32), ld, _p(out), T, N, _stream()), "colsum")
+
+
+def dgelu(dpost, pre, out):
+    _check(lib().iit_dgelu(_p(dpost), _p(pre), _p(out), dpost.numel(), _stream()), "dgelu")
+
+
+def shadow_refresh(descs: torch.Tensor, n: int):
+    _check(lib().iit_shadow_refresh(_p(descs), n, _stream()), "shadow_refresh")
+
+
+_SHADOW_DTYPE = np.dtype([("src", np.uint64), ("dst", np.uint64), ("rows", np.int32), ("cols", np.int32),
+                          ("ld", np.int64), ("transpose", np.int32), ("pad", np.int32)])
+
+
+def make_shadow_descs(entries, device) -> torch.Tensor:
+    """entries: (src fp32 tensor [rows, cols] contiguous, dst bf16 tensor (base ptr), rows, cols, ld, transpose)."""
+    assert _SHADOW_DTYPE.itemsize == lib().iit_shadow_desc_size()
+    arr = np.zeros(len(entries), dtype=_SHADOW_DTYPE)
+    for i, (src_ptr, dst_ptr, rows, cols, ld, tr) in enumerate(entries):
+        arr[i] = (src_ptr, dst_ptr, rows, cols, ld, int(tr), 0)
+    return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
+
+
+def adam_step(flat, exp_avg, exp_avg_sq, norm_buf, *, lr, b1, b2, eps, wd, bc1, bc2, clip_norm):
+    n = flat.numel
+    nparts = 1024
+    part = getattr(flat, "_norm_parts", None)
+    if part is None or part.numel() < nparts:
+        part = flat._norm_parts = torch.zeros(nparts, dtype=torch.float32, device=flat.data.device)
+    _check(lib().iit_adam_flat(_p(flat.data), _p(flat.grad), _p(exp_avg), _p(exp_avg_sq), n, _p(part), nparts,
+                               float(clip_norm or 0.0), lr, b1, b2, eps, wd, bc1, bc2, _stream()), "adam_flat")
+    flat.after_step()

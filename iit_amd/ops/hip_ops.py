@@ -1,0 +1,565 @@
+"""HIP op backend: autograd Functions over the hand-written gfx950 kernels.
+
+Numerics: bf16 activations / GEMM operands, fp32 accumulation, fp32 residual
+stream, fp32 master weights and gradients.
+
+Weights: :class:`ModelShadow` keeps bf16 compute copies of every matrix in the
+two layouts the GEMMs want (``[N][K]`` for the forward, ``[K][N]`` for the
+input-gradient GEMM), packed QKV, and a padded-ld unembedding; one batched
+``shadow_refresh`` launch re-derives them after each optimizer update.
+
+Gradients: weight/bias gradients are accumulated *inside* the backward GEMM
+epilogues straight into ``param.grad`` (the flat fp32 arena when present) and the
+Function returns ``None`` for them; :mod:`iit_amd.engine.grad_hooks` tells the
+data-parallel reducer the gradient is final.
+
+Interventions: ``attention(..., patch_heads, patch_src)`` splices source ``z``
+for the listed heads inside the attention kernel; patched heads produce zero
+q/k/v gradient (the spliced value is a constant), exactly like the reference's
+clone + index-put hook.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import torch
+from torch.autograd import Function
+
+from ..engine import grad_hooks
+from . import hip_kernels as K
+from .torch_ops import TorchOps, act_fn
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _pad8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+def _grad_slot(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    if p is None or not p.requires_grad:
+        return None
+    g = p.grad
+    if g is None:
+        g = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        p.grad = g
+    return g
+
+
+def _done(*params):
+    for p in params:
+        if p is not None and p.requires_grad:
+            grad_hooks.notify(p)
+
+
+# ============================================================================ shadow weights
+class ModelShadow:
+    """bf16 compute copies of a HookedTransformer's matrices (refreshed in one launch)."""
+
+    def __init__(self, model):
+        self.model = model
+        cfg = model.cfg
+        self.dev = next(model.parameters()).device
+        H, d, dh = cfg.n_heads, cfg.d_model, cfg.d_head
+        self.HD = H * dh
+        self.V = cfg.d_vocab_out
+        self.Vp = _pad8(self.V)
+        self.layers = []
+        e = lambda *s: torch.empty(*s, dtype=BF16, device=self.dev)  # noqa: E731
+        for blk in model.blocks:
+            L = {"qkv_T": e(3 * self.HD, d), "qkv": e(d, 3 * self.HD), "o_T": e(d, self.HD), "o": e(self.HD, d)}
+            if not cfg.attn_only:
+                dm = cfg.d_mlp
+                L.update({"in_T": e(dm, d), "in": e(d, dm), "out_T": e(d, dm), "out": e(dm, d)})
+            self.layers.append(L)
+        self.U_T = e(self.V, d)
+        self.U = e(d, self.Vp)
+        self._layout_sig = None
+        self._value_sig = None
+        self._descs = None
+        self._n = 0
+
+    def _entries(self):
+        m, cfg = self.model, self.model.cfg
+        H, d, dh, HD = cfg.n_heads, cfg.d_model, cfg.d_head, self.HD
+        out = []
+        for blk, L in zip(m.blocks, self.layers):
+            a = blk.attn
+            for which, W in enumerate((a.W_Q, a.W_K, a.W_V)):
+                for h in range(H):
+                    src = W.data_ptr() + h * d * dh * 4
+                    out.append((src, L["qkv_T"].data_ptr() + (which * HD + h * dh) * d * 2, d, dh, d, 1))
+                    out.append((src, L["qkv"].data_ptr() + (which * HD + h * dh) * 2, d, dh, 3 * HD, 0))
+            out.append((a.W_O.data_ptr(), L["o_T"].data_ptr(), HD, d, HD, 1))
+            out.append((a.W_O.data_ptr(), L["o"].data_ptr(), HD, d, d, 0))
+            if not cfg.attn_only:
+                mlp, dm = blk.mlp, cfg.d_mlp
+                out.append((mlp.W_in.data_ptr(), L["in_T"].data_ptr(), d, dm, d, 1))
+                out.append((mlp.W_in.data_ptr(), L["in"].data_ptr(), d, dm, dm, 0))
+                out.append((mlp.W_out.data_ptr(), L["out_T"].data_ptr(), dm, d, dm, 1))
+                out.append((mlp.W_out.data_ptr(), L["out"].data_ptr(), dm, d, d, 0))
+        W_U = m.unembed.W_U
+        out.append((W_U.data_ptr(), self.U_T.data_ptr(), d, self.V, d, 1))
+        out.append((W_U.data_ptr(), self.U.data_ptr(), d, self.V, self.Vp, 0))
+        return out
+
+    def _matrices(self):
+        m = self.model
+        ps = []
+        for blk in m.blocks:
+            a = blk.attn
+            ps += [a.W_Q, a.W_K, a.W_V, a.W_O]
+            if not m.cfg.attn_only:
+                ps += [blk.mlp.W_in, blk.mlp.W_out]
+        ps.append(m.unembed.W_U)
+        return ps
+
+    def ensure(self):
+        m = self.model
+        flat = getattr(m, "_flat_params", None)
+        mats = self._matrices()
+        if flat is not None:
+            layout = ("flat", id(flat), flat.data.data_ptr())
+            value = (getattr(m, "_iit_weights_version", 0), flat.version)
+        else:
+            layout = tuple(p.data_ptr() for p in mats)
+            value = (getattr(m, "_iit_weights_version", 0), tuple(p._version for p in mats))
+        if layout != self._layout_sig:
+            for p in mats:
+                if not p.is_contiguous() or p.dtype != F32:
+                    raise RuntimeError("HIP backend needs contiguous fp32 master weights")
+            entries = self._entries()
+            self._descs = K.make_shadow_descs(entries, self.dev)
+            self._n = len(entries)
+            self._layout_sig = layout
+            self._value_sig = None
+        if value != self._value_sig:
+            K.shadow_refresh(self._descs, self._n)
+            self._value_sig = value
+
+    def mark_stale(self):
+        self._value_sig = None
+
+
+# ============================================================================ autograd functions
+def _flat2(t: torch.Tensor) -> torch.Tensor:
+    return t.reshape(-1, t.shape[-1])
+
+
+class EmbedPosFn(Function):
+    @staticmethod
+    def forward(ctx, tokens, W_E, W_pos):
+        B, S = tokens.shape
+        d = W_E.shape[1]
+        tok = tokens.contiguous()
+        out = torch.empty(B, S, d, dtype=F32, device=tokens.device)
+        K.embed_pos_fwd(tok, W_E, W_pos, out, B, S, d)
+        ctx.save_for_backward(tok)
+        ctx.params = (W_E, W_pos)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (tok,) = ctx.saved_tensors
+        W_E, W_pos = ctx.params
+        B, S = tok.shape
+        K.embed_pos_bwd(tok, g.contiguous(), _grad_slot(W_E), _grad_slot(W_pos), B, S, W_E.shape[1])
+        _done(W_E, W_pos)
+        return None, None, None
+
+
+class LayerNormFn(Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        shape = x.shape
+        d = shape[-1]
+        x2 = _flat2(x.float().contiguous())
+        T = x2.shape[0]
+        y = torch.empty(T, d, dtype=BF16, device=x.device)
+        mean = torch.empty(T, dtype=F32, device=x.device)
+        rstd = torch.empty(T, dtype=F32, device=x.device)
+        K.ln_fwd(x2, w, b, y, mean, rstd, T, d, eps)
+        ctx.save_for_backward(x2, mean, rstd)
+        ctx.params = (w, b)
+        ctx.in_dtype = x.dtype
+        return y.view(*shape[:-1], d)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, mean, rstd = ctx.saved_tensors
+        w, b = ctx.params
+        T, d = x2.shape
+        dx = torch.empty(T, d, dtype=F32, device=x2.device)
+        dw = _grad_slot(w) if w is not None else None
+        db = _grad_slot(b) if b is not None else None
+        K.ln_bwd(_flat2(dy.contiguous()), x2, mean, rstd, w, dx, dw, db, T, d)
+        _done(w, b)
+        dx = dx.view(*dy.shape[:-1], d)
+        return (dx if ctx.in_dtype == F32 else dx.to(ctx.in_dtype)), None, None, None
+
+
+class QKVFn(Function):
+    """x [B,S,d] bf16 -> packed qkv [B,S,3,H,dh] bf16 (bias fused)."""
+
+    @staticmethod
+    def forward(ctx, x, layer, W_Q, W_K, W_V, b_Q, b_K, b_V):
+        B, S, d = x.shape
+        H, dh = W_Q.shape[0], W_Q.shape[2]
+        HD = H * dh
+        x2 = _flat2(x.to(BF16).contiguous())
+        T = x2.shape[0]
+        out = torch.empty(B, S, 3, H, dh, dtype=BF16, device=x.device)
+        K.gemm(x2, layer["qkv_T"], out, M=T, N=3 * HD, K=d, lda=d, ldb=d, ldc=3 * HD, epi=K.EPI_BF16_BIAS3,
+               bias0=b_Q, bias1=b_K, bias2=b_V, bias_cols=HD)
+        ctx.save_for_backward(x2)
+        ctx.layer = layer
+        ctx.params = (W_Q, W_K, W_V, b_Q, b_K, b_V)
+        ctx.dims = (B, S, d, H, dh)
+        return out
+
+    @staticmethod
+    def backward(ctx, dqkv):
+        (x2,) = ctx.saved_tensors
+        W_Q, W_K, W_V, b_Q, b_K, b_V = ctx.params
+        B, S, d, H, dh = ctx.dims
+        HD = H * dh
+        T = B * S
+        g = dqkv.to(BF16).contiguous().view(T, 3 * HD)
+        dx = torch.empty(T, d, dtype=BF16, device=g.device)
+        K.gemm(g, ctx.layer["qkv"], dx, M=T, N=d, K=3 * HD, lda=3 * HD, ldb=3 * HD, ldc=d, epi=K.EPI_BF16)
+        gq, gk, gv = _grad_slot(W_Q), _grad_slot(W_K), _grad_slot(W_V)
+        if gq is not None:
+            K.gemm(x2, g, gq, C2=gk, C3=gv, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=0,
+                   mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_ACC_QKV, qkv=(dh, H, d))
+        for i, bp in enumerate((b_Q, b_K, b_V)):
+            gb = _grad_slot(bp)
+            if gb is not None:
+                K.colsum_accum(g[:, i * HD:], 3 * HD, gb, T, HD)
+        _done(W_Q, W_K, W_V, b_Q, b_K, b_V)
+        return dx.view(B, S, d), None, None, None, None, None, None, None
+
+
+class AttnFn(Function):
+    """packed qkv [B,S,3,H,dh] -> z [B,S,H,dh]; heads in ``mask`` take ``zsrc`` (interchange splice)."""
+
+    @staticmethod
+    def forward(ctx, qkv, zsrc, mask, causal, scale):
+        B, S, _, H, dh = qkv.shape
+        qkv = qkv.contiguous()
+        z = torch.empty(B, S, H, dh, dtype=BF16, device=qkv.device)
+        lse = torch.empty(B * H * S, dtype=F32, device=qkv.device)
+        src = None
+        if mask:
+            src = zsrc.to(BF16).contiguous()
+        K.attn_small_fwd(qkv, z, lse, src, mask, B, S, H, dh, 3 * H * dh, H * dh, H * dh, scale, causal)
+        ctx.save_for_backward(qkv, lse)
+        ctx.cfg = (mask, causal, scale)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        qkv, lse = ctx.saved_tensors
+        mask, causal, scale = ctx.cfg
+        B, S, _, H, dh = qkv.shape
+        dz = dz.to(BF16).contiguous()
+        dqkv = torch.empty_like(qkv)
+        K.attn_small_bwd(qkv, dz, lse, dqkv, mask, B, S, H, dh, 3 * H * dh, H * dh, scale, causal)
+        return dqkv, None, None, None, None
+
+
+class LinearFn(Function):
+    """y = x @ W + b with TL-layout master W [K, N]; out kinds: bf16, f32 (store) or f32 residual."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, w_fwd, w_bwd, ld_bwd, resid, out_kind):
+        lead = x.shape[:-1]
+        Kd = x.shape[-1]
+        N = W.shape[-1] if W.dim() == 2 else W.shape[-1]
+        x2 = _flat2(x.to(BF16).contiguous())
+        T = x2.shape[0]
+        dev = x.device
+        if out_kind == "bf16":
+            out = torch.empty(T, N, dtype=BF16, device=dev)
+            K.gemm(x2, w_fwd, out, M=T, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=N, epi=K.EPI_BF16, bias0=b)
+            res = out.view(*lead, N)
+        elif out_kind == "f32":
+            Np = _pad8(N)
+            out = torch.empty(T, Np, dtype=F32, device=dev)
+            K.gemm(x2, w_fwd, out, M=T, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=Np, epi=K.EPI_F32_STORE, bias0=b)
+            res = out[:, :N].view(*lead, N) if Np == N else out[:, :N].unflatten(0, lead)
+        else:  # residual
+            r2 = _flat2(resid.float().contiguous())
+            out = torch.empty(T, N, dtype=F32, device=dev)
+            K.gemm(x2, w_fwd, out, M=T, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=N, epi=K.EPI_F32_RESID, bias0=b, resid=r2,
+                   ldr=N)
+            res = out.view(*lead, N)
+        ctx.save_for_backward(x2)
+        ctx.params = (W, b)
+        ctx.w_bwd = w_bwd
+        ctx.ld_bwd = ld_bwd
+        ctx.meta = (lead, Kd, N, out_kind, x.dtype)
+        return res
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x2,) = ctx.saved_tensors
+        W, b = ctx.params
+        lead, Kd, N, out_kind, x_dtype = ctx.meta
+        T = x2.shape[0]
+        g2 = gy.reshape(T, N) if gy.is_contiguous() else None
+        if g2 is None:
+            # strided (padded) gradients of the f32 logits view
+            if gy.dim() >= 2 and gy.stride(-1) == 1 and gy.reshape(-1, N).stride(0) % 8 == 0:
+                g2 = gy.reshape(-1, N)
+            else:
+                g2 = gy.contiguous().reshape(T, N)
+        gf32 = g2.dtype == F32
+        if not gf32 and g2.dtype != BF16:
+            g2 = g2.to(BF16)
+        if g2.stride(0) % 8 != 0:  # 16-byte aligned rows for the vector loads
+            padded = torch.zeros(T, _pad8(N), dtype=g2.dtype, device=g2.device)
+            padded[:, :N] = g2
+            g2 = padded[:, :N]
+        ldg = g2.stride(0)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            amode = K.MODE_AF32 if gf32 else K.MODE_NN
+            _, splits = K._tiling(T, Kd, N, True)
+            if splits == 1 and x_dtype == BF16:
+                dxb = torch.empty(T, Kd, dtype=BF16, device=g2.device)
+                K.gemm(g2, ctx.w_bwd, dxb, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ld_bwd, ldc=Kd, mode=amode,
+                       epi=K.EPI_BF16)
+                dx = dxb.view(*lead, Kd)
+            else:
+                dxf = torch.zeros(T, Kd, dtype=F32, device=g2.device)
+                K.gemm(g2, ctx.w_bwd, dxf, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ld_bwd, ldc=Kd, mode=amode,
+                       epi=K.EPI_F32_ACC, splits=splits)
+                dx = dxf.to(x_dtype).view(*lead, Kd)
+        gW = _grad_slot(W)
+        if gW is not None:
+            mode = K.MODE_AKM | K.MODE_BKM | (K.MODE_BF32 if gf32 else 0)
+            K.gemm(x2, g2, gW, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=N, mode=mode, epi=K.EPI_F32_ACC)
+        gb = _grad_slot(b)
+        if gb is not None:
+            K.colsum_accum(g2, ldg, gb, T, N)
+        _done(W, b)
+        gres = None
+        if out_kind == "resid":
+            gres = gy
+        return dx, None, None, None, None, None, gres, None
+
+
+class MLPInFn(Function):
+    """(pre, post) = (x @ W_in + b_in, gelu_new(pre)) in one GEMM epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, W_in, b_in, w_fwd, w_bwd):
+        lead = x.shape[:-1]
+        d = x.shape[-1]
+        dm = W_in.shape[1]
+        x2 = _flat2(x.to(BF16).contiguous())
+        T = x2.shape[0]
+        post = torch.empty(T, dm, dtype=BF16, device=x.device)
+        pre = torch.empty(T, dm, dtype=BF16, device=x.device)
+        K.gemm(x2, w_fwd, post, C2=pre, M=T, N=dm, K=d, lda=d, ldb=d, ldc=dm, ldc2=dm, epi=K.EPI_GELU, bias0=b_in)
+        ctx.save_for_backward(x2, pre)
+        ctx.params = (W_in, b_in)
+        ctx.w_bwd = w_bwd
+        ctx.meta = (lead, d, dm)
+        return pre.view(*lead, dm), post.view(*lead, dm)
+
+    @staticmethod
+    def backward(ctx, gpre, gpost):
+        x2, pre = ctx.saved_tensors
+        W_in, b_in = ctx.params
+        lead, d, dm = ctx.meta
+        T = x2.shape[0]
+        dpre = torch.empty(T, dm, dtype=BF16, device=x2.device)
+        if gpost is not None:
+            K.dgelu(gpost.to(BF16).contiguous().view(T, dm), pre, dpre)
+            if gpre is not None:
+                dpre = (dpre.float() + gpre.float().reshape(T, dm)).to(BF16)
+        else:
+            dpre = gpre.to(BF16).contiguous().view(T, dm)
+        dx = torch.empty(T, d, dtype=BF16, device=x2.device)
+        K.gemm(dpre, ctx.w_bwd, dx, M=T, N=d, K=dm, lda=dm, ldb=dm, ldc=d, epi=K.EPI_BF16)
+        gW = _grad_slot(W_in)
+        if gW is not None:
+            K.gemm(x2, dpre, gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm, mode=K.MODE_AKM | K.MODE_BKM,
+                   epi=K.EPI_F32_ACC)
+        gb = _grad_slot(b_in)
+        if gb is not None:
+            K.colsum_accum(dpre, dm, gb, T, dm)
+        _done(W_in, b_in)
+        return dx.view(*lead, d), None, None, None, None
+
+
+class CrossEntropyFn(Function):
+    """mean_r CE(logits[r], labels[r]) over fp32 logits with any row stride; fused fwd stats + bwd."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        R, V = logits.shape
+        if logits.stride(1) != 1:
+            logits = logits.contiguous()
+        ld = logits.stride(0)
+        loss = torch.empty(R, dtype=F32, device=logits.device)
+        lse = torch.empty(R, dtype=F32, device=logits.device)
+        lab = labels.contiguous()
+        K.ce_fwd(logits, ld, lab, loss, lse, None, R, V)
+        ctx.save_for_backward(logits, lab, lse)
+        return loss.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, lab, lse = ctx.saved_tensors
+        R, V = logits.shape
+        ld = logits.stride(0)
+        ldo = _pad8(V)
+        buf = torch.empty(R, ldo, dtype=F32, device=logits.device)
+        gs = g.reshape(1).float().contiguous()
+        K.ce_bwd(logits, ld, lab, lse, gs, 1.0 / R, buf, ldo, R, V)
+        return buf[:, :V], None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    return CrossEntropyFn.apply(logits.float(), labels)
+
+
+# ============================================================================ op backend
+class HipOps(TorchOps):
+    name = "hip"
+    fused = True
+
+    def __init__(self, model):
+        super().__init__(BF16)
+        self.model = model
+        self.shadow = ModelShadow(model)
+        self._layer_of = {}
+        for i, blk in enumerate(model.blocks):
+            self._layer_of[id(blk.attn.W_Q)] = i
+            self._layer_of[id(blk.attn.W_O)] = i
+            if not model.cfg.attn_only:
+                self._layer_of[id(blk.mlp.W_in)] = i
+                self._layer_of[id(blk.mlp.W_out)] = i
+
+    def begin_forward(self):
+        self.shadow.ensure()
+
+    def _L(self, p):
+        return self.shadow.layers[self._layer_of[id(p)]]
+
+    # -- residual stream ------------------------------------------------------------
+    def embed(self, tokens, W_E):
+        return W_E[tokens]
+
+    def pos_embed(self, batch, seq, W_pos, offset: int = 0):
+        return W_pos[offset:offset + seq].unsqueeze(0).expand(batch, seq, W_pos.shape[-1])
+
+    def embed_pos(self, tokens, W_E, W_pos):
+        return EmbedPosFn.apply(tokens, W_E, W_pos)
+
+    def residual(self, a, b):
+        return a.float() + b.float()
+
+    def layer_norm(self, x, w, b, eps):
+        return LayerNormFn.apply(x, w, b, eps)
+
+    # -- attention -------------------------------------------------------------------
+    def qkv(self, x, W_Q, W_K, W_V, b_Q, b_K, b_V):
+        self.shadow.ensure()
+        packed = QKVFn.apply(x, self._L(W_Q), W_Q, W_K, W_V, b_Q, b_K, b_V)
+        q, k, v = packed[:, :, 0], packed[:, :, 1], packed[:, :, 2]
+        q._iit_packed = k._iit_packed = v._iit_packed = packed
+        return q, k, v
+
+    def attention(self, q, k, v, causal, attn_scale, patch_heads: Optional[Sequence[int]] = None, patch_src=None,
+                  hook_scores=None, hook_pattern=None, ignore=float("-inf")):
+        S, dh = q.shape[1], q.shape[-1]
+        if S > 64 or dh > 128:
+            # long sequences: reference math (flash kernel: iit_amd.ops.flash_attention when built)
+            z = TorchOps.attention(self, q, k, v, causal, attn_scale)
+            if patch_heads:
+                z = z.clone()
+                z[:, :, list(patch_heads)] = patch_src[:, :, list(patch_heads)].to(z.dtype)
+            return z
+        packed = getattr(q, "_iit_packed", None)
+        if packed is None or getattr(k, "_iit_packed", None) is not packed or getattr(v, "_iit_packed", None) is not packed:
+            packed = torch.stack([q, k, v], dim=2).to(BF16)
+        mask = K.heads_to_mask(patch_heads)
+        return AttnFn.apply(packed, patch_src, mask, causal, 1.0 / attn_scale)
+
+    def o_proj(self, z, W_O, b_O):
+        L = self._L(W_O)
+        B, S, H, dh = z.shape
+        return LinearFn.apply(z.reshape(B, S, H * dh), W_O, b_O, L["o_T"], L["o"], W_O.shape[-1], None, "bf16")
+
+    def o_proj_residual(self, z, W_O, b_O, resid):
+        L = self._L(W_O)
+        B, S, H, dh = z.shape
+        return LinearFn.apply(z.reshape(B, S, H * dh), W_O, b_O, L["o_T"], L["o"], W_O.shape[-1], resid, "resid")
+
+    def o_result(self, z, W_O):
+        return torch.einsum("bshe,hed->bshd", z.to(BF16), W_O.to(BF16))
+
+    # -- MLP ---------------------------------------------------------------------------
+    def mlp_in(self, x, W_in, b_in, act: str, hook_pre=None):
+        L = self._L(W_in)
+        if hook_pre is None and act in ("gelu_new", "gelu_fast", "gelu_pytorch_tanh"):
+            return MLPInFn.apply(x, W_in, b_in, L["in_T"], L["in"])
+        pre = LinearFn.apply(x, W_in, b_in, L["in_T"], L["in"], W_in.shape[1], None, "bf16")
+        if hook_pre is not None:
+            pre = hook_pre(pre)
+        return pre, act_fn(act)(pre)
+
+    def mlp_out(self, post, W_out, b_out):
+        L = self._L(W_out)
+        return LinearFn.apply(post, W_out, b_out, L["out_T"], L["out"], W_out.shape[1], None, "bf16")
+
+    def mlp_out_residual(self, post, W_out, b_out, resid):
+        L = self._L(W_out)
+        return LinearFn.apply(post, W_out, b_out, L["out_T"], L["out"], W_out.shape[1], resid, "resid")
+
+    # -- unembed -------------------------------------------------------------------------
+    def unembed(self, x, W_U, b_U):
+        sh = self.shadow
+        sh.ensure()
+        return LinearFn.apply(x, W_U, b_U, sh.U_T, sh.U, sh.Vp, None, "f32")
+
+    def unembed_argmax(self, x, W_U, b_U, chunk: int = 8192):
+        sh = self.shadow
+        sh.ensure()
+        lead = x.shape[:-1]
+        d = x.shape[-1]
+        x2 = _flat2(x.to(BF16).contiguous())
+        T = x2.shape[0]
+        V = W_U.shape[1]
+        buf = torch.empty(T, chunk, dtype=F32, device=x.device)
+        best_v = best_i = None
+        for s in range(0, V, chunk):
+            n = min(chunk, V - s)
+            K.gemm(x2, sh.U_T[s:s + n], buf, M=T, N=n, K=d, lda=d, ldb=d, ldc=chunk, epi=K.EPI_F32_STORE,
+                   bias0=b_U[s:s + n])
+            v, i = buf[:, :n].max(dim=-1)
+            i = i + s
+            if best_v is None:
+                best_v, best_i = v, i
+            else:
+                upd = v > best_v
+                best_v = torch.where(upd, v, best_v)
+                best_i = torch.where(upd, i, best_i)
+        return best_i.view(*lead)
+
+
+_OPS = {}
+
+
+def get_hip_ops(model) -> HipOps:
+    K.lib()  # strict: fail loudly if the kernel library is unavailable
+    ops = getattr(model, "_iit_hip_ops", None)
+    if ops is None:
+        ops = HipOps(model)
+        model._iit_hip_ops = ops
+    return ops

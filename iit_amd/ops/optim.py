@@ -30,6 +30,7 @@ class FusedAdam(torch.optim.Optimizer):
         self.exp_avg = torch.zeros_like(flat.data)
         self.exp_avg_sq = torch.zeros_like(flat.data)
         self.step_count = 0
+        self.pending_clip = None
         self._norm_buf = torch.zeros(2, dtype=torch.float32, device=flat.data.device)
         if use_hip is None:
             use_hip = flat.data.is_cuda
@@ -68,7 +69,7 @@ class FusedAdam(torch.optim.Optimizer):
             self.exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
             denom = (self.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(eps)
             self.flat.data.addcdiv_(self.exp_avg, denom, value=-lr / bc1)
-            self.flat.refresh_shadow()
+            self.flat.after_step()
         for p in self.flat.params:
             self.state[p]["step"] = t
 

@@ -1,0 +1,184 @@
+"""T1: HIP kernel <-> fp32 PyTorch reference parity.
+
+Every hand-written gfx950 kernel is compared against a plain fp32 PyTorch
+implementation of the same op.  bf16 operands -> tolerances scale with K.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+@pytest.fixture(scope="module")
+def K():
+    from iit_amd.ops import hip_kernels
+    hip_kernels.lib()
+    return hip_kernels
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def rel_err(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 384, 256), (4096, 768, 768), (200, 130, 72), (64, 50257 // 7, 64)])
+def test_gemm_nn_bias(K, M, N, Kd):
+    torch.manual_seed(0)
+    A = torch.randn(M, Kd, device=dev)
+    W = torch.randn(N, Kd, device=dev) / math.sqrt(Kd)  # [N][K]
+    b = torch.randn(N, device=dev)
+    C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    K.gemm(bf(A), bf(W), C, M=M, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=N, epi=K.EPI_BF16, bias0=b)
+    ref = bf(A).float() @ bf(W).float().T + b
+    assert rel_err(C, ref) < 1e-2
+
+
+def test_gemm_asymmetric_identity(K):
+    """A = I with an asymmetric B catches row/col swaps in the C layout."""
+    n = 128
+    A = torch.eye(n, device=dev)
+    B = torch.arange(n * n, device=dev, dtype=torch.float32).view(n, n) % 97
+    C = torch.empty(n, n, dtype=torch.float32, device=dev)
+    K.gemm(bf(A), bf(B), C, M=n, N=n, K=n, lda=n, ldb=n, ldc=n, epi=K.EPI_F32_STORE)
+    # C = A @ B^T with B stored [N][K]
+    assert torch.equal(C, bf(B).float().T)
+
+
+@pytest.mark.parametrize("M,N,T", [(768, 768, 4096), (64, 200, 96), (128, 256, 300)])
+def test_gemm_kmajor_accumulate(K, M, N, T):
+    torch.manual_seed(1)
+    X = torch.randn(T, M, device=dev)
+    G = torch.randn(T, N, device=dev)
+    out = torch.randn(M, N, device=dev)
+    ref = out + bf(X).float().T @ bf(G).float()
+    K.gemm(bf(X), bf(G), out, M=M, N=N, K=T, lda=M, ldb=N, ldc=N, mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_ACC)
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_gemm_kmajor_fp32_b_splitk(K):
+    torch.manual_seed(2)
+    M, N, T = 256, 128, 8192
+    X = torch.randn(T, M, device=dev)
+    G = torch.randn(T, N, device=dev)
+    out = torch.zeros(M, N, device=dev)
+    K.gemm(bf(X), G, out, M=M, N=N, K=T, lda=M, ldb=N, ldc=N, mode=K.MODE_AKM | K.MODE_BKM | K.MODE_BF32,
+           epi=K.EPI_F32_ACC, splits=4)
+    ref = bf(X).float().T @ bf(G).float()
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_gemm_fp32_a_residual_gelu(K):
+    torch.manual_seed(3)
+    M, N, Kd = 512, 256, 192
+    A = torch.randn(M, Kd, device=dev)
+    W = torch.randn(N, Kd, device=dev) / math.sqrt(Kd)
+    b = torch.randn(N, device=dev)
+    R = torch.randn(M, N, device=dev)
+    C = torch.empty(M, N, device=dev)
+    K.gemm(A, bf(W), C, M=M, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=N, mode=K.MODE_AF32, epi=K.EPI_F32_STORE)
+    assert rel_err(C, bf(A).float() @ bf(W).float().T) < 1e-2
+    K.gemm(bf(A), bf(W), C, M=M, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=N, epi=K.EPI_F32_RESID, bias0=b, resid=R, ldr=N)
+    assert rel_err(C, R + bf(A).float() @ bf(W).float().T + b) < 1e-2
+    post = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    K.gemm(bf(A), bf(W), post, C2=pre, M=M, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=N, ldc2=N, epi=K.EPI_GELU, bias0=b)
+    from iit_amd.ops.torch_ops import gelu_new
+    ref_pre = bf(A).float() @ bf(W).float().T + b
+    assert rel_err(pre, ref_pre) < 1e-2
+    assert rel_err(post, gelu_new(ref_pre)) < 1e-2
+
+
+def test_layernorm(K):
+    torch.manual_seed(4)
+    T, d = 1000, 768
+    x = torch.randn(T, d, device=dev) * 3 + 1
+    y = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
+    mean = torch.empty(T, device=dev)
+    rstd = torch.empty(T, device=dev)
+    K.ln_fwd(x, None, None, y, mean, rstd, T, d, 1e-5)
+    xc = x - x.mean(-1, keepdim=True)
+    ref = xc / (xc.pow(2).mean(-1, keepdim=True) + 1e-5).sqrt()
+    assert rel_err(y, ref) < 1e-2
+    xr = x.clone().requires_grad_(True)
+    xc = xr - xr.mean(-1, keepdim=True)
+    out = xc / (xc.pow(2).mean(-1, keepdim=True) + 1e-5).sqrt()
+    g = torch.randn(T, d, device=dev)
+    out.backward(g)
+    dx = torch.empty(T, d, device=dev)
+    K.ln_bwd(g, x, mean, rstd, None, dx, None, None, T, d)
+    assert rel_err(dx, xr.grad) < 1e-3
+
+
+@pytest.mark.parametrize("S,H,dh", [(16, 12, 64), (16, 4, 16), (33, 3, 32)])
+def test_attention_fwd_bwd_with_head_splice(K, S, H, dh):
+    torch.manual_seed(5)
+    B = 7
+    qkv = torch.randn(B, S, 3, H, dh, device=dev)
+    zsrc = torch.randn(B, S, H, dh, device=dev)
+    patched = [1] if H > 1 else []
+    mask = K.heads_to_mask(patched)
+    z = torch.empty(B, S, H, dh, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * H * S, device=dev)
+    q16 = bf(qkv).contiguous()
+    K.attn_small_fwd(q16, z, lse, bf(zsrc), mask, B, S, H, dh, 3 * H * dh, H * dh, H * dh, 1 / math.sqrt(dh), True)
+    qf = q16.float().requires_grad_(True)
+    q, k, v = qf[:, :, 0], qf[:, :, 1], qf[:, :, 2]
+    sc = torch.einsum("bqhe,bkhe->bhqk", q, k) / math.sqrt(dh)
+    sc = sc.masked_fill(~torch.ones(S, S, dtype=torch.bool, device=dev).tril(), float("-inf"))
+    ref = torch.einsum("bkhe,bhqk->bqhe", v, sc.softmax(-1))
+    for h in patched:
+        ref = ref.clone()
+        ref[:, :, h] = bf(zsrc)[:, :, h].float()
+    assert rel_err(z, ref) < 1e-2
+    g = torch.randn(B, S, H, dh, device=dev)
+    ref.backward(g)
+    dq = torch.empty_like(q16)
+    K.attn_small_bwd(q16, bf(g), lse, dq, mask, B, S, H, dh, 3 * H * dh, H * dh, 1 / math.sqrt(dh), True)
+    assert rel_err(dq, qf.grad) < 2e-2
+    for h in patched:
+        assert dq[:, :, :, h].abs().max().item() == 0
+
+
+def test_cross_entropy(K):
+    torch.manual_seed(6)
+    R, V = 64, 50257
+    from iit_amd.ops.hip_ops import cross_entropy
+    logits = (torch.randn(R, V, device=dev) * 4).requires_grad_(True)
+    labels = torch.randint(0, V, (R,), device=dev)
+    loss = cross_entropy(logits, labels) * 0.7
+    loss.backward()
+    lr = logits.detach().clone().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lr, labels) * 0.7
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-4
+    assert rel_err(logits.grad, lr.grad) < 1e-4
+
+
+def test_flat_adam_matches_torch(K):
+    torch.manual_seed(7)
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.ops.optim import FusedAdam
+    m1 = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.Linear(128, 33)).to(dev)
+    m2 = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.Linear(128, 33)).to(dev)
+    m2.load_state_dict(m1.state_dict())
+    flat = FlatParams(m1)
+    opt1 = FusedAdam(flat, lr=1e-2)
+    opt2 = torch.optim.Adam(m2.parameters(), lr=1e-2)
+    for _ in range(5):
+        x = torch.randn(16, 64, device=dev)
+        opt1.zero_grad()
+        m1(x).pow(2).sum().backward()
+        opt1.step(clip_norm=1.0)
+        opt2.zero_grad()
+        m2(x).pow(2).sum().backward()
+        torch.nn.utils.clip_grad_norm_(m2.parameters(), 1.0)
+        opt2.step()
+    for p1, p2 in zip(m1.parameters(), m2.parameters()):
+        assert torch.allclose(p1, p2, atol=1e-5, rtol=1e-4)
