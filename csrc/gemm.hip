@@ -132,15 +132,12 @@ struct TileLoader {
       const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
       const __bf16* a0 = lds + (kbase + 8 * g + q) * LDS_ROW + row0 + 4 * p;
       typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
-      i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(a0));
-      i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(a0 + 4 * LDS_ROW));
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        o[e] = __builtin_bit_cast(__bf16, v0[e]);
-        o[e + 4] = __builtin_bit_cast(__bf16, v1[e]);
-      }
-      return o;
+      const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(a0));
+      const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(a0 + 4 * LDS_ROW));
+      // whole-vector reinterpretation: element-wise bit_casts of the tr16 results are
+      // miscompiled by hipcc (ROCm 7.2) into duplicated halves
+      const i16x8 w = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+      return __builtin_bit_cast(bf16x8, w);
     }
   }
 };
@@ -315,12 +312,20 @@ IIT_EXPORT int iit_gemm(const void* A, const void* B, void* C, void* C2, void* C
   IIT_GEMM_CASE(0, false, false, false, false, EPI_DGELU)
   IIT_GEMM_CASE(0, false, false, false, false, EPI_F32_STORE)
   IIT_GEMM_CASE(0, false, false, false, false, EPI_F32_ACC)
+  // forward GEMMs straight from TL-layout ([K][N]) bf16 weights: B k-major (tr16 reads)
+  IIT_GEMM_CASE(2, false, true, false, false, EPI_BF16)
+  IIT_GEMM_CASE(2, false, true, false, false, EPI_BF16_BIAS3)
+  IIT_GEMM_CASE(2, false, true, false, false, EPI_F32_RESID)
+  IIT_GEMM_CASE(2, false, true, false, false, EPI_GELU)
+  IIT_GEMM_CASE(2, false, true, false, false, EPI_F32_STORE)
   // dX from the fp32 residual-stream gradient
   IIT_GEMM_CASE(4, false, false, true, false, EPI_BF16)
   IIT_GEMM_CASE(4, false, false, true, false, EPI_DGELU)
   IIT_GEMM_CASE(4, false, false, true, false, EPI_F32_ACC)
   IIT_GEMM_CASE(4, false, false, true, false, EPI_F32_STORE)
   // weight gradients: both operands k-major (reduction over tokens)
+  IIT_GEMM_CASE(1, true, false, false, false, EPI_F32_ACC)
+  IIT_GEMM_CASE(2, false, true, false, false, EPI_F32_ACC)
   IIT_GEMM_CASE(3, true, true, false, false, EPI_F32_ACC)
   IIT_GEMM_CASE(3, true, true, false, false, EPI_F32_ACC_QKV)
   IIT_GEMM_CASE(11, true, true, false, true, EPI_F32_ACC)

@@ -563,3 +563,39 @@ IIT_EXPORT int iit_dgelu(const void* dpost, const void* pre, void* out, long n, 
 }
 
 IIT_EXPORT int iit_device_sync() { return hipDeviceSynchronize(); }
+
+// ---------------------------------------------------------------------------- diagnostics
+// probe of ds_read_b64_tr_b16 lane semantics: LDS holds [4 rows][16 cols] of value row*16+col,
+// lane 4q+p (within each 16-lane group) addresses row q, columns 4p..4p+3.
+__global__ void probe_tr16_kernel(short* out) {
+  __shared__ __attribute__((aligned(16))) short lds[64];
+  const int l = threadIdx.x;
+  lds[l] = (short)l;
+  __syncthreads();
+  const int li = l & 15, q = li >> 2, p = li & 3;
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(lds + q * 16 + 4 * p));
+  for (int e = 0; e < 4; ++e) out[l * 4 + e] = v[e];
+}
+
+IIT_EXPORT int iit_probe_tr16(void* out, void* stream) {
+  hipLaunchKernelGGL(probe_tr16_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (short*)out);
+  return hipGetLastError();
+}
+
+// probe 2: LDS [16 rows][16 cols], lane l addresses row 4*(l>>4) + ((l&15)>>2), columns 4*(l&3)
+__global__ void probe_tr16b_kernel(short* out) {
+  __shared__ __attribute__((aligned(16))) short lds[256];
+  const int l = threadIdx.x;
+  for (int i = l; i < 256; i += 64) lds[i] = (short)i;
+  __syncthreads();
+  const int row = 4 * (l >> 4) + ((l & 15) >> 2), col = 4 * (l & 3);
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(lds + row * 16 + col));
+  for (int e = 0; e < 4; ++e) out[l * 4 + e] = v[e];
+}
+
+IIT_EXPORT int iit_probe_tr16b(void* out, void* stream) {
+  hipLaunchKernelGGL(probe_tr16b_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (short*)out);
+  return hipGetLastError();
+}

@@ -39,8 +39,12 @@ def test_forward_backward_parity(norm):
     assert rel(lf, lr) < 2e-2
     lr.float().pow(2).mean().backward()
     lf.float().pow(2).mean().backward()
+    scale = max(p.grad.norm().item() for p in ref.parameters())
     for (n, pr), (_, pf) in zip(ref.named_parameters(), fast.named_parameters()):
         assert pf.grad is not None, n
+        if pr.grad.norm().item() < 1e-4 * scale:  # e.g. b_K: exactly zero in exact arithmetic
+            assert pf.grad.norm().item() < 1e-3 * scale, n
+            continue
         assert rel(pf.grad, pr.grad) < 6e-2, n
 
 
@@ -77,11 +81,14 @@ def test_capture_and_splice_semantics():
         fast.zero_grad(set_to_none=True)
         out_r.float().pow(2).mean().backward()
         out_f.float().pow(2).mean().backward()
+        scale = max(p.grad.norm().item() for p in ref.parameters() if p.grad is not None)
         for (n, pr), (_, pf) in zip(ref.named_parameters(), fast.named_parameters()):
             gr = pr.grad if pr.grad is not None else torch.zeros_like(pr)
             gf = pf.grad if pf.grad is not None else torch.zeros_like(pf)
             if gr.abs().max() == 0:
-                assert gf.abs().max() == 0, n
+                assert gf.abs().max() == 0, n  # spliced-away producers get exactly no gradient
+            elif gr.norm().item() < 1e-4 * scale:  # b_K: zero in exact arithmetic
+                assert gf.norm().item() < 1e-3 * scale, n
             else:
                 assert rel(gf, gr) < 8e-2, n
 
