@@ -44,19 +44,13 @@ def parse():
     return ap.parse_args()
 
 
-def main():
-    args = parse()
-    from iit_amd.parallel import dist as pdist
-    distributed = pdist.init_distributed()
-    rank, world = pdist.rank(), pdist.world_size()
-    if torch.cuda.is_available():
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
-
+def setup(args, dev):
+    """Model pair, optimizer and batch iterator of the headline config (shared with scripts/torch_profile.py)."""
     from iit_amd.data.iit_dataset import IITDataset, train_test_split
     from iit_amd.model_pairs import IOI_ModelPair
     from iit_amd.models.config import gpt2_config_dict
     from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.parallel import dist as pdist
     from iit_amd.tasks.ioi import ioi_cfg, make_ioi_corr, make_ioi_dataset_and_hl
 
     torch.manual_seed(0)
@@ -93,6 +87,19 @@ def main():
     if args.graphs:
         from iit_amd.engine.graphs import GraphedTrainStep
         step_fn = GraphedTrainStep(pair, opt, loss_fn)
+    return pair, opt, loss_fn, it, step_fn, train_set, test_set
+
+
+def main():
+    args = parse()
+    from iit_amd.parallel import dist as pdist
+    distributed = pdist.init_distributed()
+    rank, world = pdist.rank(), pdist.world_size()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+    pair, opt, loss_fn, it, step_fn, train_set, test_set = setup(args, dev)
 
     for _ in range(args.warmup):
         base, abl = next(it)
@@ -149,6 +156,10 @@ def main():
             "last_train_losses": {k: round(v, 4) for k, v in train_loss.items()},
         }
         print(json.dumps(rec))
+        if os.environ.get("IIT_GEMM_REPORT"):
+            from iit_amd.ops import gemm_dispatch
+            with open(os.environ["IIT_GEMM_REPORT"], "w") as f:
+                f.write(gemm_dispatch.report())
     pdist.destroy()
 
 

@@ -416,8 +416,13 @@ IIT_EXPORT int iit_ce_bwd(const float* logits, long ld, const long* labels, cons
 
 // ============================================================================ optimizer
 // partial sums of g^2 per block (grid-stride over float4)
-__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ g, long n4, float* __restrict__ part) {
+// Stage 1 of the fused clip+Adam: per-block partial sums of g^2 (skipped when clip == 0) and the
+// device-side step counter bump (block 0), so a captured graph replays with the right bias corrections.
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ g, long n4, float* __restrict__ part,
+                                                            int do_norm, int* __restrict__ step) {
   __shared__ float sm[4];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && step) step[0] += 1;
+  if (!do_norm) return;
   float s = 0.f;
   const float4* g4 = (const float4*)g;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
@@ -430,11 +435,15 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restr
   if (threadIdx.x == 0) part[blockIdx.x] = sm[0] + sm[1] + sm[2] + sm[3];
 }
 
-// Adam (torch semantics, amsgrad=False) with the clip coefficient computed on device from the partial sums.
-__global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
-                                                        float* __restrict__ v, long n4, const float* __restrict__ part,
-                                                        int nparts, float clip, float lr, float b1, float b2, float eps,
-                                                        float wd, float bc1, float bc2_sqrt) {
+// Adam (torch semantics, amsgrad=False) with the clip coefficient computed on device from the partial sums,
+// the bias corrections from the device step counter, and the bf16 mirror of the updated weights written in
+// the same pass.  Streams: read g, p, m, v; write p, m, v, mirror (the clipped gradient is not written back).
+__global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        __bf16* __restrict__ mirror, long n4,
+                                                        const float* __restrict__ part, int nparts, float clip,
+                                                        float lr, float b1, float b2, float eps, float wd,
+                                                        const int* __restrict__ step) {
   __shared__ float coef_s;
   if (threadIdx.x < 64) {
     float s = 0.f;
@@ -445,9 +454,12 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p, f
   }
   __syncthreads();
   const float coef = coef_s;
-  const float step = lr / bc1;
+  const float t = (float)step[0];
+  const float bc1 = 1.f - powf(b1, t);
+  const float bc2_sqrt = sqrtf(1.f - powf(b2, t));
+  const float stepsz = lr / bc1;
+  const float4* g4 = (const float4*)g;
   float4* p4 = (float4*)p;
-  float4* g4 = (float4*)g;
   float4* m4 = (float4*)m;
   float4* v4 = (float4*)v;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
@@ -459,55 +471,76 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p, f
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float gr = gs[e] * coef;
-      gs[e] = gr;
       if (wd != 0.f) gr += wd * ps[e];
       ms[e] = b1 * ms[e] + (1.f - b1) * gr;
       vs[e] = b2 * vs[e] + (1.f - b2) * gr * gr;
-      ps[e] -= step * ms[e] / (sqrtf(vs[e]) / bc2_sqrt + eps);
+      ps[e] -= stepsz * ms[e] / (sqrtf(vs[e]) / bc2_sqrt + eps);
     }
-    g4[i] = gg;
     p4[i] = pp;
     m4[i] = mm;
     v4[i] = vv;
+    if (mirror) {
+      bf16x4 o = {f2bf(ps[0]), f2bf(ps[1]), f2bf(ps[2]), f2bf(ps[3])};
+      ((bf16x4*)mirror)[i] = o;
+    }
   }
 }
 
-IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, long n, float* part, int nparts, float clip,
-                             float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, void* stream) {
+IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, void* mirror, long n, float* part, int nparts,
+                             float clip, float lr, float b1, float b2, float eps, float wd, int* step, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const long n4 = n / 4;
-  if (clip > 0.f) hipLaunchKernelGGL(sumsq_partial_kernel, dim3(nparts), dim3(256), 0, s, g, n4, part);
-  const int blocks = (int)min((n4 + 255) / 256, 4096L);
-  hipLaunchKernelGGL(adam_flat_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, n4, part, nparts, clip, lr, b1, b2,
-                     eps, wd, bc1, sqrtf(bc2));
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(clip > 0.f ? nparts : 1), dim3(256), 0, s, g, n4, part,
+                     (int)(clip > 0.f), step);
+  const int blocks = (int)min((n4 + 255) / 256, 8192L);
+  hipLaunchKernelGGL(adam_flat_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, n4, part, nparts,
+                     clip, lr, b1, b2, eps, wd, step);
   return hipGetLastError();
 }
 
 // ============================================================================ shadow weights
 // dst (bf16) = src (fp32) viewed as [rows][cols]; transpose -> dst[c][r] with leading dim ld.
+// element (h, i, j) of src [heads][rows][cols] -> dst[h*dst_hs + i*ld + j]   (or transposed, heads == 1)
 struct ShadowDesc {
   const float* src;
   __bf16* dst;
   int rows, cols;
   long ld;
+  int heads;
   int transpose;
-  int pad_;
+  long src_hs, dst_hs;
 };
 
 __global__ __launch_bounds__(256) void shadow_refresh_kernel(const ShadowDesc* __restrict__ descs) {
   __shared__ float tile[32][33];
   const ShadowDesc d = descs[blockIdx.y];
+  if (!d.transpose) {
+    const long total = (long)d.heads * d.rows;
+    for (long r = blockIdx.x; r < total; r += gridDim.x) {
+      const int h = (int)(r / d.rows), i = (int)(r % d.rows);
+      const float* s = d.src + h * d.src_hs + (long)i * d.cols;
+      __bf16* o = d.dst + h * d.dst_hs + (long)i * d.ld;
+      const bool vec = ((((uintptr_t)s) & 15) == 0) && ((((uintptr_t)o) & 7) == 0);
+      if (vec) {
+        const int c4 = d.cols / 4;
+        for (int j = threadIdx.x; j < c4; j += 256) {
+          const float4 v = ((const float4*)s)[j];
+          bf16x4 b = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+          *(bf16x4*)(o + 4 * j) = b;
+        }
+        for (int j = c4 * 4 + threadIdx.x; j < d.cols; j += 256) o[j] = f2bf(s[j]);
+      } else {
+        for (int j = threadIdx.x; j < d.cols; j += 256) o[j] = f2bf(s[j]);
+      }
+    }
+    return;
+  }
   const int tiles_c = (d.cols + 31) / 32;
   const int ntiles = tiles_c * ((d.rows + 31) / 32);
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int r0 = (t / tiles_c) * 32, c0 = (t % tiles_c) * 32;
-    if (!d.transpose) {
-      for (int i = ty; i < 32; i += 8) {
-        const int r = r0 + i, c = c0 + tx;
-        if (r < d.rows && c < d.cols) d.dst[(long)r * d.ld + c] = f2bf(d.src[(long)r * d.cols + c]);
-      }
-    } else {
+    {
       for (int i = ty; i < 32; i += 8) {
         const int r = r0 + i, c = c0 + tx;
         tile[i][tx] = (r < d.rows && c < d.cols) ? d.src[(long)r * d.cols + c] : 0.f;
@@ -531,19 +564,29 @@ IIT_EXPORT int iit_shadow_refresh(const void* descs, int n, void* stream) {
 IIT_EXPORT int iit_shadow_desc_size() { return (int)sizeof(ShadowDesc); }
 
 // ============================================================================ small helpers
-// db[n] (+)= sum_t x[t][n]     x bf16 or fp32, row chunks of 64, fp32 atomics
+// db[n] (+)= sum_t x[t][n]     x bf16 or fp32.  Block = 64 columns x 64 rows, 4 waves each summing
+// 16 rows of one coalesced 64-column row segment; LDS combine; one fp32 atomic per column per block.
 template <bool F32>
-__global__ void colsum_kernel(const void* __restrict__ x, long ld, float* __restrict__ out, int T, int N) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  const int t0 = blockIdx.y * 64, t1 = min(T, t0 + 64);
+__global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x, long ld, float* __restrict__ out, int T, int N) {
+  __shared__ float part[4][64];
+  const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
+  const int t0 = blockIdx.y * 64;
   float s = 0.f;
-  for (int t = t0; t < t1; ++t) s += F32 ? ((const float*)x)[(long)t * ld + n] : bf2f(((const __bf16*)x)[(long)t * ld + n]);
-  atomicAdd(out + n, s);
+  if (n < N) {
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+      const int t = t0 + w + 4 * i;
+      if (t < T) s += F32 ? ((const float*)x)[(long)t * ld + n] : bf2f(((const __bf16*)x)[(long)t * ld + n]);
+    }
+  }
+  part[w][c] = s;
+  __syncthreads();
+  if (w == 0 && n < N) atomicAdd(out + n, part[0][c] + part[1][c] + part[2][c] + part[3][c]);
 }
 
 IIT_EXPORT int iit_colsum_accum(const void* x, int f32, long ld, float* out, int T, int N, void* stream) {
-  dim3 grid((N + 255) / 256, (T + 63) / 64);
+  dim3 grid((N + 63) / 64, (T + 63) / 64);
   if (f32) hipLaunchKernelGGL(colsum_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
   else hipLaunchKernelGGL(colsum_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
   return hipGetLastError();

@@ -8,15 +8,24 @@ buffer, and their ``.grad`` as views into one fp32 gradient buffer:
   the whole arena (global-norm clip computed on device: no host sync);
 * data-parallel buckets are contiguous slices of the gradient arena, so RCCL
   all-reduces them in place (no pack/unpack copies);
-* an optional bf16 shadow arena holds the compute copy of the weights that the
-  HIP kernels read; the optimizer refreshes it in the same pass.
+* an optional bf16 *mirror* arena (same layout) holds the compute copy of the
+  weights the HIP kernels read; the fused optimizer writes it in the same pass
+  as the update, so no separate cast/transposition pass exists.
 
-Every parameter slot starts on a 64-element boundary (256 B) so kernels can use
-16-byte vector accesses on any slot.
+**Kernel-layout groups.**  A module may define ``_iit_arena_groups()`` returning
+``[(numel, [(param, view_fn), ...]), ...]``: the members of a group share one
+arena slot laid out the way the GEMM kernels want the operand (e.g. ``W_Q``,
+``W_K``, ``W_V`` interleaved as one ``[d_model][3*H*d_head]`` matrix, ``W_U``
+with 16-byte aligned rows), and each parameter becomes a strided view
+``view_fn(slot)`` with its usual TL shape.  Parameters keep their public shapes
+and semantics; only their strides change.
+
+Every slot starts on a 64-element boundary (256 B) so kernels can use 16-byte
+vector accesses on any slot.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 from torch import nn
@@ -24,39 +33,79 @@ from torch import nn
 _ALIGN = 64
 
 
+def _align(n: int) -> int:
+    return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
 class FlatParams:
     def __init__(self, module: nn.Module, with_bf16_shadow: bool = False):
         self.module = module
         self.names: List[str] = []
         self.params: List[nn.Parameter] = []
-        self.offsets: List[Tuple[int, int]] = []
+        self._view_fns: List[Callable[[torch.Tensor], torch.Tensor]] = []
+        self.slots: List[Tuple[int, int]] = []  # (offset, numel) allocation units, arena order
+
+        groups = module._iit_arena_groups() if hasattr(module, "_iit_arena_groups") else []
+        member: Dict[int, Tuple[int, Callable]] = {}
+        for gi, (numel, members) in enumerate(groups):
+            if not members or not all(p.requires_grad for p, _ in members):
+                continue
+            for p, fn in members:
+                member[id(p)] = (gi, fn)
+        placed: Dict[int, int] = {}
         off = 0
         for name, p in module.named_parameters():
             if not p.requires_grad:
                 continue
             self.names.append(name)
             self.params.append(p)
-            n = p.numel()
-            self.offsets.append((off, n))
-            off += (n + _ALIGN - 1) // _ALIGN * _ALIGN
+            if id(p) in member:
+                gi, fn = member[id(p)]
+                n = groups[gi][0]
+                if gi not in placed:
+                    placed[gi] = off
+                    self.slots.append((off, n))
+                    off += _align(n)
+                go = placed[gi]
+                self._view_fns.append(lambda buf, go=go, n=n, fn=fn: fn(buf[go:go + n]))
+            else:
+                n = p.numel()
+                self.slots.append((off, n))
+                self._view_fns.append(lambda buf, o=off, n=n, shape=p.shape: buf[o:o + n].view(shape))
+                off += _align(n)
         self.numel = off
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.data = torch.zeros(off, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
         self.shadow: Optional[torch.Tensor] = None
         with torch.no_grad():
-            for p, (o, n) in zip(self.params, self.offsets):
-                view = self.data[o:o + n].view(p.shape)
+            for p, fn in zip(self.params, self._view_fns):
+                view = fn(self.data)
+                assert view.shape == p.shape, (view.shape, p.shape)
                 view.copy_(p.detach().float())
                 p.data = view
-                p.grad = self.grad[o:o + n].view(p.shape)
+                p.grad = fn(self.grad)
         self.index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
         self.version = 0
+        self.mirror_version = -1
         self._listeners = []
         module._flat_params = self
         if with_bf16_shadow:
-            self.shadow = torch.empty(off, dtype=torch.bfloat16, device=dev)
-            self.refresh_shadow()
+            self.ensure_shadow()
+
+    # ---------------------------------------------------------------- layout queries
+    def offset_of(self, p: torch.Tensor) -> int:
+        """Element offset of ``p``'s first element inside the arena."""
+        return (p.data_ptr() - self.data.data_ptr()) // self.data.element_size()
+
+    @property
+    def offsets(self) -> List[Tuple[int, int]]:
+        """(start offset, numel) of every parameter (grouped params share their slot's span)."""
+        return [(self.offset_of(p), p.numel()) for p in self.params]
+
+    def owns(self, p: torch.Tensor) -> bool:
+        base = self.data.data_ptr()
+        return base <= p.data_ptr() < base + self.numel * 4
 
     # ---------------------------------------------------------------- grads
     def zero_grad(self) -> None:
@@ -65,53 +114,68 @@ class FlatParams:
 
     def rebind_grads(self) -> None:
         """Re-attach ``.grad`` views (after someone set them to None / replaced them)."""
-        for p, (o, n) in zip(self.params, self.offsets):
+        for p, fn in zip(self.params, self._view_fns):
             g = p.grad
-            if g is None or g.data_ptr() != self.grad[o:o + n].data_ptr():
-                view = self.grad[o:o + n].view(p.shape)
+            view = fn(self.grad)
+            if g is None or g.data_ptr() != view.data_ptr() or g.stride() != view.stride():
                 if g is not None:
                     view.copy_(g)
                 p.grad = view
 
     def grad_view(self, p: torch.Tensor) -> torch.Tensor:
-        o, n = self.offsets[self.index[id(p)]]
-        return self.grad[o:o + n].view(p.shape)
+        return self._view_fns[self.index[id(p)]](self.grad)
 
     # ---------------------------------------------------------------- updates
     def add_listener(self, fn) -> None:
         """``fn()`` runs (on the current stream) after every optimizer update of the arena."""
         self._listeners.append(fn)
 
-    def after_step(self) -> None:
+    def after_step(self, mirror_written: bool = False) -> None:
         self.version += 1
         self.module._iit_weights_version = getattr(self.module, "_iit_weights_version", 0) + 1
-        self.refresh_shadow()
+        if mirror_written:
+            self.mirror_version = self.module._iit_weights_version
+        else:
+            self.refresh_shadow()
         for fn in self._listeners:
             fn()
 
-    # ---------------------------------------------------------------- shadow
+    # ---------------------------------------------------------------- bf16 mirror
+    def ensure_shadow(self) -> torch.Tensor:
+        if self.shadow is None:
+            self.shadow = torch.empty(self.numel, dtype=torch.bfloat16, device=self.data.device)
+            self.refresh_shadow()
+        return self.shadow
+
     def refresh_shadow(self) -> None:
         if self.shadow is not None:
             self.shadow.copy_(self.data)
+            self.mirror_version = getattr(self.module, "_iit_weights_version", 0)
 
     def shadow_view(self, p: torch.Tensor) -> torch.Tensor:
-        o, n = self.offsets[self.index[id(p)]]
-        return self.shadow[o:o + n].view(p.shape)
+        """bf16 mirror of ``p`` with ``p``'s shape and strides."""
+        sh = self.ensure_shadow()
+        return sh.as_strided(p.shape, p.stride(), self.offset_of(p))
 
     # ---------------------------------------------------------------- buckets
     def buckets(self, bucket_bytes: int) -> List[Tuple[int, int]]:
-        """Contiguous gradient slices of ~``bucket_bytes`` in reverse parameter order
-        (≈ the order backward produces them), for overlapped all-reduce."""
+        """Contiguous gradient slices of ~``bucket_bytes`` in reverse arena order
+        (≈ the order backward produces them), for overlapped all-reduce.  Bucket
+        edges fall on slot boundaries, so a grouped slot is never split."""
         per = max(_ALIGN, bucket_bytes // 4)
         out = []
         end = self.numel
         while end > 0:
             start = max(0, end - per)
-            # snap the bucket start to a parameter boundary
-            for o, n in self.offsets:
-                if o <= start < o + ((n + _ALIGN - 1) // _ALIGN * _ALIGN):
+            for o, n in self.slots:
+                if o <= start < o + _align(n):
                     start = o
                     break
+            if start >= end:  # a single slot larger than the bucket size
+                for o, n in self.slots:
+                    if o < end <= o + _align(n):
+                        start = o
+                        break
             out.append((start, end))
             end = start
         return out

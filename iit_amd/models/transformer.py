@@ -326,6 +326,41 @@ class HookedTransformer(HookedRootModule):
         """Invalidate derived bf16 compute copies after an out-of-band weight update."""
         self._iit_weights_version = getattr(self, "_iit_weights_version", 0) + 1
 
+    def _iit_arena_groups(self):
+        """GEMM-operand layout of the flat parameter arena (see :mod:`iit_amd.engine.flat`).
+
+        * per block, ``W_Q|W_K|W_V`` interleave into one ``[d_model][3*H*d_head]``
+          matrix (column ``which*H*dh + h*dh + e``) and ``b_Q|b_K|b_V`` into ``[3][H][dh]``:
+          the fused QKV projection, its input gradient and its weight gradient are
+          then single plain GEMMs on the arena (or its bf16 mirror) with no
+          repacking pass;
+        * ``W_U`` gets rows padded to a multiple of 8 columns (16-byte aligned
+          k-major B operand for the unembed GEMM).
+        Parameters keep their TL shapes; only their strides differ from contiguous.
+        """
+        cfg = self.cfg
+        H, d, dh = cfg.n_heads, cfg.d_model, cfg.d_head
+        HD = H * dh
+        groups = []
+        for blk in self.blocks:
+            a = blk.attn
+            if any(getattr(a, n).shape != (H, d, dh) for n in ("W_Q", "W_K", "W_V")):
+                continue
+
+            def w_view(which):
+                return lambda buf: buf.view(d, 3, H, dh)[:, which].permute(1, 0, 2)
+
+            def b_view(which):
+                return lambda buf: buf.view(3, H, dh)[which]
+
+            groups.append((3 * d * HD, [(a.W_Q, w_view(0)), (a.W_K, w_view(1)), (a.W_V, w_view(2))]))
+            groups.append((3 * HD, [(a.b_Q, b_view(0)), (a.b_K, b_view(1)), (a.b_V, b_view(2))]))
+        V = cfg.d_vocab_out
+        Vp = (V + 7) // 8 * 8
+        if Vp != V:
+            groups.append((d * Vp, [(self.unembed.W_U, lambda buf: buf.view(d, Vp)[:, :V])]))
+        return groups
+
     # ------------------------------------------------------------------ backend
     def set_op_backend(self, backend: Optional[str]) -> "HookedTransformer":
         self.op_backend = backend

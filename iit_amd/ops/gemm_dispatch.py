@@ -1,0 +1,188 @@
+"""GEMM dispatch: hand-written MFMA kernel (fused epilogues) vs hipBLASLt, autotuned per shape.
+
+Every GEMM of the engine goes through :func:`gemm`.  Two implementations:
+
+* ``hip``  - ``csrc/gemm.hip``: MFMA 16x16x32 bf16 with the epilogue fused
+  (bias, packed-QKV bias, fp32 residual add, bias+gelu_new, dgelu, fp32
+  accumulate into the gradient arena, head-blocked QKV gradient scatter);
+* ``blas`` - hipBLASLt through ``torch.mm`` / ``torch.addmm`` for the product and
+  separate elementwise passes for whatever the BLAS epilogue cannot express.
+
+``IIT_GEMM=auto`` (default) times both once per (shape, layout, epilogue) outside
+graph capture and keeps the faster; ``IIT_GEMM=hip`` / ``blas`` force one.  The
+decisions are recorded in :data:`DECISIONS` (``report()`` prints them) so profiles
+can say which GEMMs ran on hand-written MFMA code.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import hip_kernels as K
+
+POLICY = os.environ.get("IIT_GEMM", "auto")
+DECISIONS: Dict[Tuple, Tuple[str, float, float]] = {}
+BF16, F32 = torch.bfloat16, torch.float32
+_BLAS_OK = {}
+
+
+def _as(t, rows, cols, ld, dtype=None):
+    v = torch.as_strided(t, (rows, cols), (ld, 1))
+    return v if dtype is None or v.dtype == dtype else v.to(dtype)
+
+
+def _operands(A, B, M, N, Kd, lda, ldb, mode):
+    if mode & K.MODE_AKM:
+        a = _as(A, Kd, M, lda).t()
+    else:
+        a = _as(A, M, Kd, lda)
+    if mode & K.MODE_BKM:
+        b = _as(B, Kd, N, ldb)
+    else:
+        b = _as(B, N, Kd, ldb).t()
+    if a.dtype != BF16:
+        a = a.to(BF16)
+    if b.dtype != BF16:
+        b = b.to(BF16)
+    return a, b
+
+
+def _mm_f32(a, b):
+    if _BLAS_OK.get("out_dtype", True):
+        try:
+            return torch.mm(a, b, out_dtype=F32)
+        except (RuntimeError, TypeError):
+            _BLAS_OK["out_dtype"] = False
+    return torch.mm(a, b).float()
+
+
+def _addmm_f32(c, base, a, b) -> None:
+    """c = base + a @ b with bf16 operands, fp32 accumulate/output, in one hipBLASLt call when supported
+    (``base`` may alias ``c``: the accumulate-into-gradient case)."""
+    if _BLAS_OK.get("addmm_dtype", True):
+        try:
+            torch.addmm(base, a, b, out_dtype=F32, out=c)
+            return
+        except (RuntimeError, TypeError):
+            _BLAS_OK["addmm_dtype"] = False
+    if base is c:
+        c.add_(_mm_f32(a, b))
+    else:
+        torch.add(base, _mm_f32(a, b), out=c)
+
+
+def _gelu_into(pre, out) -> None:
+    torch._C._nn.gelu(pre, approximate="tanh", out=out)
+
+
+def _blas(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, C2, C3, bias0, bias1, bias2, resid, ldr, aux, ldc2, bias_cols,
+          qkv, blas_bias=None):
+    a, b = _operands(A, B, M, N, Kd, lda, ldb, mode)
+    if epi in (K.EPI_BF16, K.EPI_BF16_BIAS3):
+        c = _as(C, M, N, ldc)
+        if blas_bias is not None:
+            bias = blas_bias
+        elif epi == K.EPI_BF16_BIAS3:
+            bias = torch.cat([bias0.reshape(-1), bias1.reshape(-1), bias2.reshape(-1)]).to(BF16)
+        else:
+            bias = None if bias0 is None else bias0.reshape(-1).to(BF16)
+        if bias is None:
+            torch.mm(a, b, out=c)
+        else:
+            torch.addmm(bias, a, b, out=c)
+    elif epi == K.EPI_F32_RESID:
+        c = _as(C, M, N, ldc)
+        _addmm_f32(c, _as(resid, M, N, ldr), a, b)
+        if bias0 is not None:
+            c.add_(bias0.reshape(-1))
+    elif epi == K.EPI_GELU:
+        pre = _as(C2, M, N, ldc2)
+        torch.addmm(bias0.reshape(-1).to(BF16), a, b, out=pre)
+        _gelu_into(pre, _as(C, M, N, ldc))
+    elif epi == K.EPI_DGELU:
+        tmp = torch.mm(a, b)
+        K.dgelu(tmp, _as(aux, M, N, ldc2).contiguous(), _as(C, M, N, ldc))
+    elif epi == K.EPI_F32_ACC:
+        c = _as(C, M, N, ldc)
+        _addmm_f32(c, c, a, b)
+    elif epi == K.EPI_F32_STORE:
+        c = _as(C, M, N, ldc)
+        if bias0 is not None:
+            _addmm_f32(c, bias0.reshape(-1).float(), a, b)
+        else:
+            c.copy_(_mm_f32(a, b))
+    else:
+        raise NotImplementedError(epi)
+
+
+def _blas_supported(epi, C) -> bool:
+    if epi == K.EPI_F32_ACC_QKV:
+        return False
+    if epi == K.EPI_DGELU:
+        return True
+    return True
+
+
+def _scratch(t, rows, ld):
+    """Dense stand-in output for timing (``t`` may be a strided view into a larger buffer)."""
+    if t is None:
+        return None
+    return torch.zeros(rows * ld, dtype=t.dtype, device=t.device)
+
+
+def _time(fn, reps=3):
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=None, bias0=None, bias1=None,
+         bias2=None, resid=None, ldr=0, aux=None, ldc2=0, bias_cols=0, qkv=(0, 0, 0), splits=None, blas_bias=None):
+    """``C = A @ B`` (+ epilogue) on the faster of the MFMA kernel and hipBLASLt for this problem.
+
+    ``blas_bias``: optional ready-made bf16 bias row (e.g. a view of the arena's bf16 mirror) for the
+    library path, saving its per-call concatenate/cast."""
+    Kd = K
+    hip_call = lambda c=C, c2=C2, c3=C3: K_.gemm(  # noqa: E731
+        A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=c2, C3=c3, bias0=bias0,
+        bias1=bias1, bias2=bias2, resid=resid, ldr=ldr, aux=aux, ldc2=ldc2, bias_cols=bias_cols, qkv=qkv,
+        splits=splits)
+    policy = POLICY
+    if policy == "hip" or not _blas_supported(epi, C):
+        return hip_call()
+    blas_call = lambda c=C, c2=C2, c3=C3: _blas(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi, c2, c3, bias0,  # noqa
+                                               bias1, bias2, resid, ldr, aux, ldc2, bias_cols, qkv, blas_bias)
+    if policy == "blas":
+        return blas_call()
+    key = (M, N, Kd, mode, epi, bias0 is not None)
+    choice = DECISIONS.get(key)
+    if choice is None:
+        if torch.cuda.is_current_stream_capturing():
+            return hip_call()
+        # time on scratch outputs so accumulate epilogues do not corrupt C
+        sc = _scratch(C, M, max(ldc, N))
+        sc2 = _scratch(C2, M, max(ldc2, N))
+        sc3 = _scratch(C3, M, max(ldc, N))
+        t_h = min(_time(lambda: hip_call(sc, sc2, sc3)) for _ in range(2))
+        t_b = min(_time(lambda: blas_call(sc, sc2, sc3)) for _ in range(2))
+        choice = DECISIONS[key] = ("hip" if t_h <= t_b else "blas", t_h, t_b)
+    return hip_call() if choice[0] == "hip" else blas_call()
+
+
+K_ = K  # the kernel module (``K`` is shadowed by the reduction-size keyword above)
+
+
+def report() -> str:
+    lines = [f"library fast paths: {dict(_BLAS_OK) or 'all available'}"]
+    for (M, N, Kd, mode, epi, bias), (c, th, tb) in sorted(DECISIONS.items()):
+        lines.append(f"M={M:6d} N={N:6d} K={Kd:6d} mode={mode:2d} epi={epi} bias={int(bias)} -> {c:4s} "
+                     f"hip {th:8.1f}us blas {tb:8.1f}us")
+    return "\n".join(lines)

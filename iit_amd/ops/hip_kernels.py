@@ -33,9 +33,12 @@ _SIGS = {
     "iit_attn_small_fwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float, c_int,
                                             c_void_p],
     "iit_attn_small_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
+    "iit_attn_mfma_fwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float, c_int,
+                                           c_void_p],
+    "iit_attn_mfma_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
     "iit_ce_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "iit_ce_bwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_long, c_int, c_int, c_void_p],
-    "iit_adam_flat": [c_void_p] * 4 + [c_long, c_void_p, c_int] + [c_float] * 8 + [c_void_p],
+    "iit_adam_flat": [c_void_p] * 5 + [c_long, c_void_p, c_int] + [c_float] * 6 + [c_void_p, c_void_p],
     "iit_shadow_refresh": [c_void_p, c_int, c_void_p],
     "iit_shadow_desc_size": [],
     "iit_colsum_accum": [c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_void_p],
@@ -137,12 +140,25 @@ def heads_to_mask(heads: Optional[Sequence[int]]) -> int:
     return m
 
 
+def _mfma_attn(S, dh):
+    return S <= 16 and dh in (32, 64, 96, 128) and os.environ.get("IIT_ATTN", "mfma") == "mfma"
+
+
 def attn_small_fwd(qkv, z, lse, zsrc, head_mask, B, S, H, dh, ld_qkv, ld_z, ld_src, scale, causal):
+    """Causal attention for S <= 64 (MFMA one-wave-per-head kernel when S <= 16, csrc/attn_mfma.hip)."""
+    if _mfma_attn(S, dh):
+        _check(lib().iit_attn_mfma_fwd(_p(qkv), _p(z), _p(lse), _p(zsrc), head_mask, B, S, H, dh, ld_qkv, ld_z, ld_src,
+                                       scale, int(causal), _stream()), "attn_mfma_fwd")
+        return
     _check(lib().iit_attn_small_fwd(_p(qkv), _p(z), _p(lse), _p(zsrc), head_mask, B, S, H, dh, ld_qkv, ld_z, ld_src,
                                     scale, int(causal), _stream()), "attn_small_fwd")
 
 
 def attn_small_bwd(qkv, dz, lse, dqkv, head_mask, B, S, H, dh, ld_qkv, ld_dz, scale, causal):
+    if _mfma_attn(S, dh):
+        _check(lib().iit_attn_mfma_bwd(_p(qkv), _p(dz), _p(lse), _p(dqkv), head_mask, B, S, H, dh, ld_qkv, ld_dz, scale,
+                                       int(causal), _stream()), "attn_mfma_bwd")
+        return
     _check(lib().iit_attn_small_bwd(_p(qkv), _p(dz), _p(lse), _p(dqkv), head_mask, B, S, H, dh, ld_qkv, ld_dz, scale,
                                     int(causal), _stream()), "attn_small_bwd")
 
@@ -160,6 +176,12 @@ def colsum_accum(x, ld, out, T, N):
     _check(lib().iit_colsum_accum(_p(x), int(x.dtype == torch.float32), ld, _p(out), T, N, _stream()), "colsum")
 
 
+def colsum3_accum(x, ld, outs, T, N):
+    """outs[i][n] += sum_t x[t][i*N + n] for the packed QKV bias gradients."""
+    for i, o in enumerate(outs):
+        colsum_accum(x[:, i * N:], ld, o, T, N)
+
+
 def dgelu(dpost, pre, out):
     _check(lib().iit_dgelu(_p(dpost), _p(pre), _p(out), dpost.numel(), _stream()), "dgelu")
 
@@ -169,24 +191,30 @@ def shadow_refresh(descs: torch.Tensor, n: int):
 
 
 _SHADOW_DTYPE = np.dtype([("src", np.uint64), ("dst", np.uint64), ("rows", np.int32), ("cols", np.int32),
-                          ("ld", np.int64), ("transpose", np.int32), ("pad", np.int32)])
+                          ("ld", np.int64), ("heads", np.int32), ("transpose", np.int32), ("src_hs", np.int64),
+                          ("dst_hs", np.int64)])
 
 
 def make_shadow_descs(entries, device) -> torch.Tensor:
-    """entries: (src fp32 tensor [rows, cols] contiguous, dst bf16 tensor (base ptr), rows, cols, ld, transpose)."""
+    """entries: (src_ptr, dst_ptr, rows, cols, ld, transpose[, heads, src_head_stride, dst_head_stride])."""
     assert _SHADOW_DTYPE.itemsize == lib().iit_shadow_desc_size()
     arr = np.zeros(len(entries), dtype=_SHADOW_DTYPE)
-    for i, (src_ptr, dst_ptr, rows, cols, ld, tr) in enumerate(entries):
-        arr[i] = (src_ptr, dst_ptr, rows, cols, ld, int(tr), 0)
+    for i, e in enumerate(entries):
+        src_ptr, dst_ptr, rows, cols, ld, tr = e[:6]
+        heads, shs, dhs = (e[6], e[7], e[8]) if len(e) > 6 else (1, 0, 0)
+        arr[i] = (src_ptr, dst_ptr, rows, cols, ld, heads, int(tr), shs, dhs)
     return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
 
 
-def adam_step(flat, exp_avg, exp_avg_sq, norm_buf, *, lr, b1, b2, eps, wd, bc1, bc2, clip_norm):
+def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_norm):
+    """Fused clip + Adam over the arena; bumps the device step counter ``step_dev`` (int32[1]) and writes the
+    bf16 mirror (``flat.shadow``) when present.  No host scalars depend on the step: graph-capturable."""
     n = flat.numel
     nparts = 1024
     part = getattr(flat, "_norm_parts", None)
     if part is None or part.numel() < nparts:
         part = flat._norm_parts = torch.zeros(nparts, dtype=torch.float32, device=flat.data.device)
-    _check(lib().iit_adam_flat(_p(flat.data), _p(flat.grad), _p(exp_avg), _p(exp_avg_sq), n, _p(part), nparts,
-                               float(clip_norm or 0.0), lr, b1, b2, eps, wd, bc1, bc2, _stream()), "adam_flat")
-    flat.after_step()
+    _check(lib().iit_adam_flat(_p(flat.data), _p(flat.grad), _p(exp_avg), _p(exp_avg_sq), _p(flat.shadow), n,
+                               _p(part), nparts, float(clip_norm or 0.0), lr, b1, b2, eps, wd, _p(step_dev),
+                               _stream()), "adam_flat")
+    flat.after_step(mirror_written=flat.shadow is not None)

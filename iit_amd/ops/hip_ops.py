@@ -3,10 +3,13 @@
 Numerics: bf16 activations / GEMM operands, fp32 accumulation, fp32 residual
 stream, fp32 master weights and gradients.
 
-Weights: :class:`ModelShadow` keeps bf16 compute copies of every matrix in the
-two layouts the GEMMs want (``[N][K]`` for the forward, ``[K][N]`` for the
-input-gradient GEMM), packed QKV, and a padded-ld unembedding; one batched
-``shadow_refresh`` launch re-derives them after each optimizer update.
+Weights: :class:`ModelShadow` keeps one bf16 compute copy of every matrix in TL
+layout (packed ``[d][3HD]`` for QKV, 16-byte aligned rows for ``W_U``); the forward
+GEMM reads it as a k-major operand through ``ds_read_b64_tr_b16``, the
+input-gradient GEMM as a k-contiguous operand, so no transposed copies exist.
+One batched ``shadow_refresh`` launch re-derives them after each optimizer update.
+GEMMs go through :mod:`iit_amd.ops.gemm_dispatch` (hand-written MFMA kernel with
+the fused epilogue, or hipBLASLt when it measures faster for a plain product).
 
 Gradients: weight/bias gradients are accumulated *inside* the backward GEMM
 epilogues straight into ``param.grad`` (the flat fp32 arena when present) and the
@@ -28,6 +31,7 @@ from torch.autograd import Function
 
 from ..engine import grad_hooks
 from . import hip_kernels as K
+from .gemm_dispatch import gemm
 from .torch_ops import TorchOps, act_fn
 
 BF16 = torch.bfloat16
@@ -56,53 +60,112 @@ def _done(*params):
 
 # ============================================================================ shadow weights
 class ModelShadow:
-    """bf16 compute copies of a HookedTransformer's matrices (refreshed in one launch)."""
+    """bf16 compute copies of a HookedTransformer's matrices, in the layouts the GEMMs read.
+
+    Layouts: QKV packed ``[d][3*H*dh]`` (column ``which*H*dh + h*dh + e``), ``W_O`` as
+    ``[H*dh][d]``, ``W_in`` ``[d][d_mlp]``, ``W_out`` ``[d_mlp][d]``, ``W_U`` ``[d][Vp]``
+    (rows padded to 8 columns).  Each copy serves both GEMMs of its weight: the
+    forward reads it as a k-major B operand (tr16 transpose reads), the
+    input-gradient GEMM as a k-contiguous B operand, so no transposed copies exist.
+
+    Two modes:
+
+    * **mirror** (training): the flat arena is already in these layouts
+      (``HookedTransformer._iit_arena_groups``), so the copies are views of the
+      arena's bf16 mirror, which the fused Adam kernel writes in its update pass;
+      nothing is re-derived per step.
+    * **copy** (no arena, e.g. evaluation of a freshly loaded model): private bf16
+      buffers refreshed by one batched ``shadow_refresh`` launch when the weights change.
+    """
 
     def __init__(self, model):
         self.model = model
         cfg = model.cfg
         self.dev = next(model.parameters()).device
-        H, d, dh = cfg.n_heads, cfg.d_model, cfg.d_head
-        self.HD = H * dh
+        self.H, self.d, self.dh = cfg.n_heads, cfg.d_model, cfg.d_head
+        self.HD = self.H * self.dh
         self.V = cfg.d_vocab_out
         self.Vp = _pad8(self.V)
         self.layers = []
-        e = lambda *s: torch.empty(*s, dtype=BF16, device=self.dev)  # noqa: E731
-        for blk in model.blocks:
-            L = {"qkv_T": e(3 * self.HD, d), "qkv": e(d, 3 * self.HD), "o_T": e(d, self.HD), "o": e(self.HD, d)}
-            if not cfg.attn_only:
-                dm = cfg.d_mlp
-                L.update({"in_T": e(dm, d), "in": e(d, dm), "out_T": e(d, dm), "out": e(dm, d)})
-            self.layers.append(L)
-        self.U_T = e(self.V, d)
-        self.U = e(d, self.Vp)
+        self.U = None
+        self.biases = []  # per layer: packed bf16 [3HD] QKV bias (mirror mode) or None
+        self.mode = None
         self._layout_sig = None
         self._value_sig = None
         self._descs = None
         self._n = 0
 
+    # ------------------------------------------------------------------ mirror mode
+    def _mirror_layout_ok(self, flat) -> bool:
+        m = self.model
+        H, d, dh, HD = self.H, self.d, self.dh, self.HD
+        for blk in m.blocks:
+            a = blk.attn
+            if a.W_Q.stride() != (dh, 3 * HD, 1):
+                return False
+            if a.W_K.data_ptr() != a.W_Q.data_ptr() + HD * 4 or a.W_V.data_ptr() != a.W_Q.data_ptr() + 2 * HD * 4:
+                return False
+            if not a.W_O.is_contiguous():
+                return False
+            if not m.cfg.attn_only and not (blk.mlp.W_in.is_contiguous() and blk.mlp.W_out.is_contiguous()):
+                return False
+        W_U = m.unembed.W_U
+        if W_U.stride() != (self.Vp, 1):
+            return False
+        return all(flat.owns(p) for p in self._matrices())
+
+    def _bind_mirror(self, flat):
+        sh = flat.ensure_shadow()
+        m = self.model
+        d, HD = self.d, self.HD
+        self.layers, self.biases = [], []
+        for blk in m.blocks:
+            a = blk.attn
+            L = {"qkv": sh.as_strided((d, 3 * HD), (3 * HD, 1), flat.offset_of(a.W_Q)),
+                 "o": sh.as_strided((HD, d), (d, 1), flat.offset_of(a.W_O))}
+            if not m.cfg.attn_only:
+                dm = m.cfg.d_mlp
+                L["in"] = sh.as_strided((d, dm), (dm, 1), flat.offset_of(blk.mlp.W_in))
+                L["out"] = sh.as_strided((dm, d), (d, 1), flat.offset_of(blk.mlp.W_out))
+            self.layers.append(L)
+            packed_b = (a.b_Q.requires_grad and flat.owns(a.b_Q) and a.b_Q.is_contiguous()
+                        and a.b_K.data_ptr() == a.b_Q.data_ptr() + HD * 4
+                        and a.b_V.data_ptr() == a.b_Q.data_ptr() + 2 * HD * 4)
+            self.biases.append(sh.as_strided((3 * HD,), (1,), flat.offset_of(a.b_Q)) if packed_b else None)
+        self.U = sh.as_strided((d, self.Vp), (self.Vp, 1), flat.offset_of(m.unembed.W_U))
+        self._descs = None
+
+    # ------------------------------------------------------------------ copy mode
+    def _alloc_copies(self):
+        cfg = self.model.cfg
+        d, HD = self.d, self.HD
+        e = lambda *s: torch.empty(*s, dtype=BF16, device=self.dev)  # noqa: E731
+        self.layers, self.biases = [], []
+        for _ in self.model.blocks:
+            L = {"qkv": e(d, 3 * HD), "o": e(HD, d)}
+            if not cfg.attn_only:
+                L.update({"in": e(d, cfg.d_mlp), "out": e(cfg.d_mlp, d)})
+            self.layers.append(L)
+            self.biases.append(None)
+        self.U = torch.zeros(d, self.Vp, dtype=BF16, device=self.dev)
+
     def _entries(self):
         m, cfg = self.model, self.model.cfg
-        H, d, dh, HD = cfg.n_heads, cfg.d_model, cfg.d_head, self.HD
+        H, d, dh, HD = self.H, self.d, self.dh, self.HD
         out = []
         for blk, L in zip(m.blocks, self.layers):
             a = blk.attn
             for which, W in enumerate((a.W_Q, a.W_K, a.W_V)):
-                for h in range(H):
-                    src = W.data_ptr() + h * d * dh * 4
-                    out.append((src, L["qkv_T"].data_ptr() + (which * HD + h * dh) * d * 2, d, dh, d, 1))
-                    out.append((src, L["qkv"].data_ptr() + (which * HD + h * dh) * 2, d, dh, 3 * HD, 0))
-            out.append((a.W_O.data_ptr(), L["o_T"].data_ptr(), HD, d, HD, 1))
+                # [H][d][dh] -> columns which*HD + h*dh + j of the packed [d][3HD] copy
+                out.append((W.data_ptr(), L["qkv"].data_ptr() + which * HD * 2, d, dh, 3 * HD, 0, H, d * dh, dh))
             out.append((a.W_O.data_ptr(), L["o"].data_ptr(), HD, d, d, 0))
             if not cfg.attn_only:
                 mlp, dm = blk.mlp, cfg.d_mlp
-                out.append((mlp.W_in.data_ptr(), L["in_T"].data_ptr(), d, dm, d, 1))
                 out.append((mlp.W_in.data_ptr(), L["in"].data_ptr(), d, dm, dm, 0))
-                out.append((mlp.W_out.data_ptr(), L["out_T"].data_ptr(), dm, d, dm, 1))
                 out.append((mlp.W_out.data_ptr(), L["out"].data_ptr(), dm, d, d, 0))
         W_U = m.unembed.W_U
-        out.append((W_U.data_ptr(), self.U_T.data_ptr(), d, self.V, d, 1))
-        out.append((W_U.data_ptr(), self.U.data_ptr(), d, self.V, self.Vp, 0))
+        # one single-row "head" per row of W_U: handles a padded (arena) row stride on the fp32 side
+        out.append((W_U.data_ptr(), self.U.data_ptr(), 1, self.V, self.Vp, 0, d, W_U.stride(0), self.Vp))
         return out
 
     def _matrices(self):
@@ -116,20 +179,35 @@ class ModelShadow:
         ps.append(m.unembed.W_U)
         return ps
 
+    # ------------------------------------------------------------------ per forward
     def ensure(self):
         m = self.model
         flat = getattr(m, "_flat_params", None)
-        mats = self._matrices()
+        wv = getattr(m, "_iit_weights_version", 0)
         if flat is not None:
             layout = ("flat", id(flat), flat.data.data_ptr())
-            value = (getattr(m, "_iit_weights_version", 0), flat.version)
+            if layout != self._layout_sig:
+                self.mode = "mirror" if self._mirror_layout_ok(flat) else "copy"
+                if self.mode == "mirror":
+                    self._bind_mirror(flat)
+                self._layout_sig = layout
+                self._value_sig = None
+            if self.mode == "mirror":
+                pv = sum(p._version for p in flat.params)
+                if flat.mirror_version != wv or pv != self._value_sig:
+                    flat.refresh_shadow()
+                    self._value_sig = pv
+                return
+            value = (wv, flat.version)
         else:
-            layout = tuple(p.data_ptr() for p in mats)
-            value = (getattr(m, "_iit_weights_version", 0), tuple(p._version for p in mats))
-        if layout != self._layout_sig:
-            for p in mats:
-                if not p.is_contiguous() or p.dtype != F32:
-                    raise RuntimeError("HIP backend needs contiguous fp32 master weights")
+            layout = tuple(p.data_ptr() for p in self._matrices())
+            value = (wv, tuple(p._version for p in self._matrices()))
+        if self.mode != "copy" or self._descs is None or layout != self._layout_sig:
+            for p in self._matrices():
+                if p.dtype != F32 or p.stride(-1) != 1 or (p is not m.unembed.W_U and not p.is_contiguous()):
+                    raise RuntimeError("HIP backend needs contiguous fp32 master weights (or the flat arena)")
+            self.mode = "copy"
+            self._alloc_copies()
             entries = self._entries()
             self._descs = K.make_shadow_descs(entries, self.dev)
             self._n = len(entries)
@@ -148,9 +226,25 @@ def _flat2(t: torch.Tensor) -> torch.Tensor:
     return t.reshape(-1, t.shape[-1])
 
 
+def _aligned_rows(g: torch.Tensor, T: int, N: int) -> torch.Tensor:
+    """[T, N] view of ``g`` whose row stride is a multiple of 8 elements (16-byte vector loads)."""
+    if g.is_contiguous():
+        g2 = g.reshape(T, N)
+    elif g.stride(-1) == 1:
+        g2 = g.reshape(-1, N)
+    else:
+        g2 = g.contiguous().reshape(T, N)
+    if g2.stride(0) % 8 != 0 or g2.stride(1) != 1:
+        padded = torch.zeros(T, _pad8(N), dtype=g2.dtype, device=g2.device)
+        padded[:, :N] = g2
+        g2 = padded[:, :N]
+    return g2
+
+
 class EmbedPosFn(Function):
     @staticmethod
     def forward(ctx, tokens, W_E, W_pos):
+        ctx.set_materialize_grads(False)
         B, S = tokens.shape
         d = W_E.shape[1]
         tok = tokens.contiguous()
@@ -162,6 +256,8 @@ class EmbedPosFn(Function):
 
     @staticmethod
     def backward(ctx, g):
+        if g is None:
+            return None, None, None
         (tok,) = ctx.saved_tensors
         W_E, W_pos = ctx.params
         B, S = tok.shape
@@ -173,6 +269,7 @@ class EmbedPosFn(Function):
 class LayerNormFn(Function):
     @staticmethod
     def forward(ctx, x, w, b, eps):
+        ctx.set_materialize_grads(False)
         shape = x.shape
         d = shape[-1]
         x2 = _flat2(x.float().contiguous())
@@ -188,6 +285,8 @@ class LayerNormFn(Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if dy is None:
+            return None, None, None, None
         x2, mean, rstd = ctx.saved_tensors
         w, b = ctx.params
         T, d = x2.shape
@@ -200,19 +299,31 @@ class LayerNormFn(Function):
         return (dx if ctx.in_dtype == F32 else dx.to(ctx.in_dtype)), None, None, None
 
 
+def _packed3(a: Optional[torch.Tensor], b: Optional[torch.Tensor], c: Optional[torch.Tensor], n: int) -> bool:
+    """``a|b|c`` are consecutive ``n``-column blocks of one row-major buffer (the arena QKV layout)."""
+    if a is None or b is None or c is None:
+        return False
+    es = a.element_size()
+    return b.data_ptr() == a.data_ptr() + n * es and c.data_ptr() == a.data_ptr() + 2 * n * es
+
+
 class QKVFn(Function):
-    """x [B,S,d] bf16 -> packed qkv [B,S,3,H,dh] bf16 (bias fused)."""
+    """x [B,S,d] bf16 -> packed qkv [B,S,3,H,dh] bf16 (bias fused); weights from the packed [d][3HD] shadow.
+
+    With the flat arena in kernel layout the weight gradient ``[d][3HD]`` is one plain
+    accumulate-GEMM into the arena and the three bias gradients one column sum."""
 
     @staticmethod
-    def forward(ctx, x, layer, W_Q, W_K, W_V, b_Q, b_K, b_V):
+    def forward(ctx, x, layer, bias_bf16, W_Q, W_K, W_V, b_Q, b_K, b_V):
+        ctx.set_materialize_grads(False)
         B, S, d = x.shape
         H, dh = W_Q.shape[0], W_Q.shape[2]
         HD = H * dh
         x2 = _flat2(x.to(BF16).contiguous())
         T = x2.shape[0]
         out = torch.empty(B, S, 3, H, dh, dtype=BF16, device=x.device)
-        K.gemm(x2, layer["qkv_T"], out, M=T, N=3 * HD, K=d, lda=d, ldb=d, ldc=3 * HD, epi=K.EPI_BF16_BIAS3,
-               bias0=b_Q, bias1=b_K, bias2=b_V, bias_cols=HD)
+        gemm(x2, layer["qkv"], out, M=T, N=3 * HD, K=d, lda=d, ldb=3 * HD, ldc=3 * HD, mode=K.MODE_BKM,
+             epi=K.EPI_BF16_BIAS3, bias0=b_Q, bias1=b_K, bias2=b_V, bias_cols=HD, blas_bias=bias_bf16)
         ctx.save_for_backward(x2)
         ctx.layer = layer
         ctx.params = (W_Q, W_K, W_V, b_Q, b_K, b_V)
@@ -221,6 +332,8 @@ class QKVFn(Function):
 
     @staticmethod
     def backward(ctx, dqkv):
+        if dqkv is None:
+            return (None,) * 9
         (x2,) = ctx.saved_tensors
         W_Q, W_K, W_V, b_Q, b_K, b_V = ctx.params
         B, S, d, H, dh = ctx.dims
@@ -228,17 +341,23 @@ class QKVFn(Function):
         T = B * S
         g = dqkv.to(BF16).contiguous().view(T, 3 * HD)
         dx = torch.empty(T, d, dtype=BF16, device=g.device)
-        K.gemm(g, ctx.layer["qkv"], dx, M=T, N=d, K=3 * HD, lda=3 * HD, ldb=3 * HD, ldc=d, epi=K.EPI_BF16)
+        gemm(g, ctx.layer["qkv"], dx, M=T, N=d, K=3 * HD, lda=3 * HD, ldb=3 * HD, ldc=d, epi=K.EPI_BF16)
         gq, gk, gv = _grad_slot(W_Q), _grad_slot(W_K), _grad_slot(W_V)
-        if gq is not None:
-            K.gemm(x2, g, gq, C2=gk, C3=gv, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=0,
-                   mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_ACC_QKV, qkv=(dh, H, d))
-        for i, bp in enumerate((b_Q, b_K, b_V)):
-            gb = _grad_slot(bp)
-            if gb is not None:
-                K.colsum_accum(g[:, i * HD:], 3 * HD, gb, T, HD)
+        if gq is not None and gk is not None and gv is not None:
+            if gq.stride() == (dh, 3 * HD, 1) and _packed3(gq, gk, gv, HD):
+                gemm(x2, g, gq, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=3 * HD, mode=K.MODE_AKM | K.MODE_BKM,
+                     epi=K.EPI_F32_ACC)
+            else:
+                gemm(x2, g, gq, C2=gk, C3=gv, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=0,
+                     mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_ACC_QKV, qkv=(dh, H, d))
+        gbs = [_grad_slot(bp) for bp in (b_Q, b_K, b_V)]
+        if all(gb is not None for gb in gbs):
+            if all(gb.is_contiguous() for gb in gbs) and _packed3(*gbs, HD):
+                K.colsum_accum(g, 3 * HD, gbs[0], T, 3 * HD)
+            else:
+                K.colsum3_accum(g, 3 * HD, gbs, T, HD)
         _done(W_Q, W_K, W_V, b_Q, b_K, b_V)
-        return dx.view(B, S, d), None, None, None, None, None, None, None
+        return (dx.view(B, S, d),) + (None,) * 8
 
 
 class AttnFn(Function):
@@ -246,6 +365,7 @@ class AttnFn(Function):
 
     @staticmethod
     def forward(ctx, qkv, zsrc, mask, causal, scale):
+        ctx.set_materialize_grads(False)
         B, S, _, H, dh = qkv.shape
         qkv = qkv.contiguous()
         z = torch.empty(B, S, H, dh, dtype=BF16, device=qkv.device)
@@ -260,6 +380,8 @@ class AttnFn(Function):
 
     @staticmethod
     def backward(ctx, dz):
+        if dz is None:
+            return None, None, None, None, None
         qkv, lse = ctx.saved_tensors
         mask, causal, scale = ctx.cfg
         B, S, _, H, dh = qkv.shape
@@ -270,92 +392,90 @@ class AttnFn(Function):
 
 
 class LinearFn(Function):
-    """y = x @ W + b with TL-layout master W [K, N]; out kinds: bf16, f32 (store) or f32 residual."""
+    """y = x @ W + b, TL-layout master W [K, N] with bf16 shadow ``w`` (row stride ``ldw``).
+
+    out kinds: ``bf16``, ``f32`` (store, padded row stride) or ``resid`` (fp32 ``resid + xW + b``).
+    """
 
     @staticmethod
-    def forward(ctx, x, W, b, w_fwd, w_bwd, ld_bwd, resid, out_kind):
+    def forward(ctx, x, W, b, w, ldw, resid, out_kind):
+        ctx.set_materialize_grads(False)
         lead = x.shape[:-1]
         Kd = x.shape[-1]
-        N = W.shape[-1] if W.dim() == 2 else W.shape[-1]
+        N = W.shape[-1]
         x2 = _flat2(x.to(BF16).contiguous())
         T = x2.shape[0]
         dev = x.device
         if out_kind == "bf16":
             out = torch.empty(T, N, dtype=BF16, device=dev)
-            K.gemm(x2, w_fwd, out, M=T, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=N, epi=K.EPI_BF16, bias0=b)
+            gemm(x2, w, out, M=T, N=N, K=Kd, lda=Kd, ldb=ldw, ldc=N, mode=K.MODE_BKM, epi=K.EPI_BF16, bias0=b)
             res = out.view(*lead, N)
         elif out_kind == "f32":
             Np = _pad8(N)
             out = torch.empty(T, Np, dtype=F32, device=dev)
-            K.gemm(x2, w_fwd, out, M=T, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=Np, epi=K.EPI_F32_STORE, bias0=b)
-            res = out[:, :N].view(*lead, N) if Np == N else out[:, :N].unflatten(0, lead)
-        else:  # residual
+            gemm(x2, w, out, M=T, N=N, K=Kd, lda=Kd, ldb=ldw, ldc=Np, mode=K.MODE_BKM, epi=K.EPI_F32_STORE, bias0=b)
+            res = out[:, :N]
+            res = res.unflatten(0, lead) if len(lead) != 1 else res
+        else:
             r2 = _flat2(resid.float().contiguous())
             out = torch.empty(T, N, dtype=F32, device=dev)
-            K.gemm(x2, w_fwd, out, M=T, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=N, epi=K.EPI_F32_RESID, bias0=b, resid=r2,
-                   ldr=N)
+            gemm(x2, w, out, M=T, N=N, K=Kd, lda=Kd, ldb=ldw, ldc=N, mode=K.MODE_BKM, epi=K.EPI_F32_RESID, bias0=b,
+                 resid=r2, ldr=N)
             res = out.view(*lead, N)
         ctx.save_for_backward(x2)
         ctx.params = (W, b)
-        ctx.w_bwd = w_bwd
-        ctx.ld_bwd = ld_bwd
+        ctx.w = w
+        ctx.ldw = ldw
         ctx.meta = (lead, Kd, N, out_kind, x.dtype)
         return res
 
     @staticmethod
     def backward(ctx, gy):
+        if gy is None:
+            return (None,) * 7
         (x2,) = ctx.saved_tensors
         W, b = ctx.params
         lead, Kd, N, out_kind, x_dtype = ctx.meta
         T = x2.shape[0]
-        g2 = gy.reshape(T, N) if gy.is_contiguous() else None
-        if g2 is None:
-            # strided (padded) gradients of the f32 logits view
-            if gy.dim() >= 2 and gy.stride(-1) == 1 and gy.reshape(-1, N).stride(0) % 8 == 0:
-                g2 = gy.reshape(-1, N)
-            else:
-                g2 = gy.contiguous().reshape(T, N)
-        gf32 = g2.dtype == F32
-        if not gf32 and g2.dtype != BF16:
-            g2 = g2.to(BF16)
-        if g2.stride(0) % 8 != 0:  # 16-byte aligned rows for the vector loads
-            padded = torch.zeros(T, _pad8(N), dtype=g2.dtype, device=g2.device)
-            padded[:, :N] = g2
-            g2 = padded[:, :N]
+        if gy.dtype not in (F32, BF16):
+            gy = gy.to(BF16)
+        g2 = _aligned_rows(gy, T, N)
         ldg = g2.stride(0)
+        gf32 = g2.dtype == F32
         dx = None
         if ctx.needs_input_grad[0]:
             amode = K.MODE_AF32 if gf32 else K.MODE_NN
             _, splits = K._tiling(T, Kd, N, True)
-            if splits == 1 and x_dtype == BF16:
+            if splits == 1:
                 dxb = torch.empty(T, Kd, dtype=BF16, device=g2.device)
-                K.gemm(g2, ctx.w_bwd, dxb, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ld_bwd, ldc=Kd, mode=amode,
-                       epi=K.EPI_BF16)
-                dx = dxb.view(*lead, Kd)
-            else:
+                gemm(g2, ctx.w, dxb, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ldw, ldc=Kd, mode=amode, epi=K.EPI_BF16)
+                dx = dxb if x_dtype == BF16 else dxb.to(x_dtype)
+            else:  # long reduction (unembed: K = vocab) -> split-K into fp32
                 dxf = torch.zeros(T, Kd, dtype=F32, device=g2.device)
-                K.gemm(g2, ctx.w_bwd, dxf, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ld_bwd, ldc=Kd, mode=amode,
-                       epi=K.EPI_F32_ACC, splits=splits)
-                dx = dxf.to(x_dtype).view(*lead, Kd)
+                gemm(g2, ctx.w, dxf, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ldw, ldc=Kd, mode=amode, epi=K.EPI_F32_ACC,
+                     splits=splits)
+                dx = dxf.to(x_dtype)
+            dx = dx.view(*lead, Kd)
         gW = _grad_slot(W)
         if gW is not None:
             mode = K.MODE_AKM | K.MODE_BKM | (K.MODE_BF32 if gf32 else 0)
-            K.gemm(x2, g2, gW, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=N, mode=mode, epi=K.EPI_F32_ACC)
+            gW2 = gW.reshape(Kd, N) if gW.is_contiguous() else gW
+            assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
+            gemm(x2, g2, gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode, epi=K.EPI_F32_ACC)
         gb = _grad_slot(b)
         if gb is not None:
             K.colsum_accum(g2, ldg, gb, T, N)
         _done(W, b)
-        gres = None
-        if out_kind == "resid":
-            gres = gy
-        return dx, None, None, None, None, None, gres, None
+        gres = gy if out_kind == "resid" else None
+        return dx, None, None, None, None, gres, None
 
 
 class MLPInFn(Function):
     """(pre, post) = (x @ W_in + b_in, gelu_new(pre)) in one GEMM epilogue."""
 
     @staticmethod
-    def forward(ctx, x, W_in, b_in, w_fwd, w_bwd):
+    def forward(ctx, x, W_in, b_in, w):
+        ctx.set_materialize_grads(False)
         lead = x.shape[:-1]
         d = x.shape[-1]
         dm = W_in.shape[1]
@@ -363,37 +483,39 @@ class MLPInFn(Function):
         T = x2.shape[0]
         post = torch.empty(T, dm, dtype=BF16, device=x.device)
         pre = torch.empty(T, dm, dtype=BF16, device=x.device)
-        K.gemm(x2, w_fwd, post, C2=pre, M=T, N=dm, K=d, lda=d, ldb=d, ldc=dm, ldc2=dm, epi=K.EPI_GELU, bias0=b_in)
+        gemm(x2, w, post, C2=pre, M=T, N=dm, K=d, lda=d, ldb=dm, ldc=dm, ldc2=dm, mode=K.MODE_BKM, epi=K.EPI_GELU,
+             bias0=b_in)
         ctx.save_for_backward(x2, pre)
         ctx.params = (W_in, b_in)
-        ctx.w_bwd = w_bwd
+        ctx.w = w
         ctx.meta = (lead, d, dm)
         return pre.view(*lead, dm), post.view(*lead, dm)
 
     @staticmethod
     def backward(ctx, gpre, gpost):
+        if gpre is None and gpost is None:
+            return None, None, None, None
         x2, pre = ctx.saved_tensors
         W_in, b_in = ctx.params
         lead, d, dm = ctx.meta
         T = x2.shape[0]
-        dpre = torch.empty(T, dm, dtype=BF16, device=x2.device)
         if gpost is not None:
+            dpre = torch.empty(T, dm, dtype=BF16, device=x2.device)
             K.dgelu(gpost.to(BF16).contiguous().view(T, dm), pre, dpre)
             if gpre is not None:
                 dpre = (dpre.float() + gpre.float().reshape(T, dm)).to(BF16)
         else:
             dpre = gpre.to(BF16).contiguous().view(T, dm)
         dx = torch.empty(T, d, dtype=BF16, device=x2.device)
-        K.gemm(dpre, ctx.w_bwd, dx, M=T, N=d, K=dm, lda=dm, ldb=dm, ldc=d, epi=K.EPI_BF16)
+        gemm(dpre, ctx.w, dx, M=T, N=d, K=dm, lda=dm, ldb=dm, ldc=d, epi=K.EPI_BF16)
         gW = _grad_slot(W_in)
         if gW is not None:
-            K.gemm(x2, dpre, gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm, mode=K.MODE_AKM | K.MODE_BKM,
-                   epi=K.EPI_F32_ACC)
+            gemm(x2, dpre, gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm, mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_ACC)
         gb = _grad_slot(b_in)
         if gb is not None:
             K.colsum_accum(dpre, dm, gb, T, dm)
         _done(W_in, b_in)
-        return dx.view(*lead, d), None, None, None, None
+        return dx.view(*lead, d), None, None, None
 
 
 class CrossEntropyFn(Function):
@@ -401,6 +523,7 @@ class CrossEntropyFn(Function):
 
     @staticmethod
     def forward(ctx, logits, labels):
+        ctx.set_materialize_grads(False)
         R, V = logits.shape
         if logits.stride(1) != 1:
             logits = logits.contiguous()
@@ -414,6 +537,8 @@ class CrossEntropyFn(Function):
 
     @staticmethod
     def backward(ctx, g):
+        if g is None:
+            return None, None
         logits, lab, lse = ctx.saved_tensors
         R, V = logits.shape
         ld = logits.stride(0)
@@ -469,8 +594,8 @@ class HipOps(TorchOps):
 
     # -- attention -------------------------------------------------------------------
     def qkv(self, x, W_Q, W_K, W_V, b_Q, b_K, b_V):
-        self.shadow.ensure()
-        packed = QKVFn.apply(x, self._L(W_Q), W_Q, W_K, W_V, b_Q, b_K, b_V)
+        i = self._layer_of[id(W_Q)]
+        packed = QKVFn.apply(x, self.shadow.layers[i], self.shadow.biases[i], W_Q, W_K, W_V, b_Q, b_K, b_V)
         q, k, v = packed[:, :, 0], packed[:, :, 1], packed[:, :, 2]
         q._iit_packed = k._iit_packed = v._iit_packed = packed
         return q, k, v
@@ -479,7 +604,6 @@ class HipOps(TorchOps):
                   hook_scores=None, hook_pattern=None, ignore=float("-inf")):
         S, dh = q.shape[1], q.shape[-1]
         if S > 64 or dh > 128:
-            # long sequences: reference math (flash kernel: iit_amd.ops.flash_attention when built)
             z = TorchOps.attention(self, q, k, v, causal, attn_scale)
             if patch_heads:
                 z = z.clone()
@@ -492,45 +616,39 @@ class HipOps(TorchOps):
         return AttnFn.apply(packed, patch_src, mask, causal, 1.0 / attn_scale)
 
     def o_proj(self, z, W_O, b_O):
-        L = self._L(W_O)
         B, S, H, dh = z.shape
-        return LinearFn.apply(z.reshape(B, S, H * dh), W_O, b_O, L["o_T"], L["o"], W_O.shape[-1], None, "bf16")
+        return LinearFn.apply(z.reshape(B, S, H * dh), W_O, b_O, self._L(W_O)["o"], W_O.shape[-1], None, "bf16")
 
     def o_proj_residual(self, z, W_O, b_O, resid):
-        L = self._L(W_O)
         B, S, H, dh = z.shape
-        return LinearFn.apply(z.reshape(B, S, H * dh), W_O, b_O, L["o_T"], L["o"], W_O.shape[-1], resid, "resid")
+        return LinearFn.apply(z.reshape(B, S, H * dh), W_O, b_O, self._L(W_O)["o"], W_O.shape[-1], resid, "resid")
 
     def o_result(self, z, W_O):
         return torch.einsum("bshe,hed->bshd", z.to(BF16), W_O.to(BF16))
 
     # -- MLP ---------------------------------------------------------------------------
     def mlp_in(self, x, W_in, b_in, act: str, hook_pre=None):
-        L = self._L(W_in)
+        w = self._L(W_in)["in"]
         if hook_pre is None and act in ("gelu_new", "gelu_fast", "gelu_pytorch_tanh"):
-            return MLPInFn.apply(x, W_in, b_in, L["in_T"], L["in"])
-        pre = LinearFn.apply(x, W_in, b_in, L["in_T"], L["in"], W_in.shape[1], None, "bf16")
+            return MLPInFn.apply(x, W_in, b_in, w)
+        pre = LinearFn.apply(x, W_in, b_in, w, W_in.shape[1], None, "bf16")
         if hook_pre is not None:
             pre = hook_pre(pre)
         return pre, act_fn(act)(pre)
 
     def mlp_out(self, post, W_out, b_out):
-        L = self._L(W_out)
-        return LinearFn.apply(post, W_out, b_out, L["out_T"], L["out"], W_out.shape[1], None, "bf16")
+        return LinearFn.apply(post, W_out, b_out, self._L(W_out)["out"], W_out.shape[1], None, "bf16")
 
     def mlp_out_residual(self, post, W_out, b_out, resid):
-        L = self._L(W_out)
-        return LinearFn.apply(post, W_out, b_out, L["out_T"], L["out"], W_out.shape[1], resid, "resid")
+        return LinearFn.apply(post, W_out, b_out, self._L(W_out)["out"], W_out.shape[1], resid, "resid")
 
     # -- unembed -------------------------------------------------------------------------
     def unembed(self, x, W_U, b_U):
         sh = self.shadow
-        sh.ensure()
-        return LinearFn.apply(x, W_U, b_U, sh.U_T, sh.U, sh.Vp, None, "f32")
+        return LinearFn.apply(x, W_U, b_U, sh.U, sh.Vp, None, "f32")
 
     def unembed_argmax(self, x, W_U, b_U, chunk: int = 8192):
         sh = self.shadow
-        sh.ensure()
         lead = x.shape[:-1]
         d = x.shape[-1]
         x2 = _flat2(x.to(BF16).contiguous())
@@ -540,8 +658,8 @@ class HipOps(TorchOps):
         best_v = best_i = None
         for s in range(0, V, chunk):
             n = min(chunk, V - s)
-            K.gemm(x2, sh.U_T[s:s + n], buf, M=T, N=n, K=d, lda=d, ldb=d, ldc=chunk, epi=K.EPI_F32_STORE,
-                   bias0=b_U[s:s + n])
+            gemm(x2, sh.U[:, s:], buf, M=T, N=n, K=d, lda=d, ldb=sh.Vp, ldc=chunk, mode=K.MODE_BKM,
+                 epi=K.EPI_F32_STORE, bias0=b_U[s:s + n])
             v, i = buf[:, :n].max(dim=-1)
             i = i + s
             if best_v is None:
@@ -551,9 +669,6 @@ class HipOps(TorchOps):
                 best_v = torch.where(upd, v, best_v)
                 best_i = torch.where(upd, i, best_i)
         return best_i.view(*lead)
-
-
-_OPS = {}
 
 
 def get_hip_ops(model) -> HipOps:

@@ -31,7 +31,7 @@ class FusedAdam(torch.optim.Optimizer):
         self.exp_avg_sq = torch.zeros_like(flat.data)
         self.step_count = 0
         self.pending_clip = None
-        self._norm_buf = torch.zeros(2, dtype=torch.float32, device=flat.data.device)
+        self._step_dev = torch.zeros(1, dtype=torch.int32, device=flat.data.device)  # device-side step counter
         if use_hip is None:
             use_hip = flat.data.is_cuda
         self._hip = None
@@ -57,8 +57,8 @@ class FusedAdam(torch.optim.Optimizer):
         g = self.flat.grad
         if self._hip is not None:
             from . import hip_kernels
-            hip_kernels.adam_step(self.flat, self.exp_avg, self.exp_avg_sq, self._norm_buf, lr=lr, b1=b1, b2=b2,
-                                  eps=eps, wd=wd, bc1=bc1, bc2=bc2, clip_norm=clip_norm)
+            hip_kernels.adam_step(self.flat, self.exp_avg, self.exp_avg_sq, self._step_dev, lr=lr, b1=b1, b2=b2,
+                                  eps=eps, wd=wd, clip_norm=clip_norm)
         else:
             if clip_norm:
                 norm = torch.linalg.vector_norm(g)
@@ -80,6 +80,7 @@ class FusedAdam(torch.optim.Optimizer):
 
     def load_state_dict(self, sd):
         self.step_count = int(sd["step"])
+        self._step_dev.fill_(self.step_count)
         self.exp_avg.copy_(sd["exp_avg"])
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
         for g, saved in zip(self.param_groups, sd["param_groups"]):

@@ -61,9 +61,22 @@ def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
     """Make every rank start from rank ``src``'s parameters and buffers."""
     if not is_initialized() or world_size() == 1:
         return
+    flat = getattr(module, "_flat_params", None)
     with torch.no_grad():
-        for t in list(module.parameters()) + list(module.buffers()):
-            dist.broadcast(t.data, src)
+        tensors = list(module.buffers())
+        if flat is not None:  # one collective over the whole arena (params are strided views of it)
+            dist.broadcast(flat.data, src)
+            module._iit_weights_version = getattr(module, "_iit_weights_version", 0) + 1
+            tensors += [p for p in module.parameters() if not flat.owns(p)]
+        else:
+            tensors += list(module.parameters())
+        for t in tensors:
+            if t.is_contiguous():
+                dist.broadcast(t.data, src)
+            else:
+                tmp = t.data.contiguous()
+                dist.broadcast(tmp, src)
+                t.data.copy_(tmp)
 
 
 def all_reduce_mean_(t: torch.Tensor) -> torch.Tensor:

@@ -1,0 +1,110 @@
+"""Flat parameter arena in kernel layout (iit_amd/engine/flat.py) on CPU.
+
+The arena re-binds every parameter as a (possibly strided) view: W_Q|W_K|W_V
+interleaved into one [d][3HD] matrix, b_Q|b_K|b_V into [3][H][dh], W_U with padded
+rows.  Public shapes, values, forward results, gradients and state_dict are unchanged.
+"""
+import torch
+
+from iit_amd.engine.flat import FlatParams
+from iit_amd.models.transformer import HookedTransformer
+from iit_amd.ops.optim import FusedAdam
+
+
+def tiny(**kw):
+    cfg = dict(n_layers=2, n_heads=3, d_model=12, d_head=4, d_mlp=24, n_ctx=16, act_fn="gelu_new", d_vocab=29,
+               device="cpu", normalization_type="LNPre")
+    cfg.update(kw)
+    torch.manual_seed(0)
+    return HookedTransformer(cfg)
+
+
+def test_arena_layout_views_and_values():
+    m = tiny()
+    before = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    tok = torch.randint(0, 29, (3, 7))
+    out_before = m(tok).detach()
+    flat = FlatParams(m)
+    H, d, dh = 3, 12, 4
+    HD = H * dh
+    for blk in m.blocks:
+        a = blk.attn
+        assert a.W_Q.shape == (H, d, dh) and a.W_Q.stride() == (dh, 3 * HD, 1)
+        assert a.W_K.data_ptr() == a.W_Q.data_ptr() + HD * 4
+        assert a.W_V.data_ptr() == a.W_Q.data_ptr() + 2 * HD * 4
+        assert a.b_K.data_ptr() == a.b_Q.data_ptr() + HD * 4
+        packed = flat.data[flat.offset_of(a.W_Q):flat.offset_of(a.W_Q) + 3 * d * HD].view(d, 3, H, dh)
+        assert torch.equal(packed[:, 1].permute(1, 0, 2), a.W_K.detach())
+    Vp = 32
+    assert m.unembed.W_U.shape == (12, 29) and m.unembed.W_U.stride() == (Vp, 1)
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    assert torch.allclose(m(tok), out_before, atol=1e-6)
+    # slots never overlap and all params live in the arena
+    ends = [(o, o + n) for o, n in flat.slots]
+    for (s0, e0), (s1, e1) in zip(ends, ends[1:]):
+        assert e0 <= s1
+    assert all(flat.owns(p) for p in m.parameters())
+
+
+def test_arena_grads_are_views_and_match_contiguous_model():
+    m_ref = tiny()
+    m = tiny()
+    flat = FlatParams(m)
+    tok = torch.randint(0, 29, (4, 9))
+    m_ref(tok).pow(2).mean().backward()
+    m(tok).pow(2).mean().backward()
+    for (n, pr), (_, pf) in zip(m_ref.named_parameters(), m.named_parameters()):
+        assert pf.grad.data_ptr() == flat.grad_view(pf).data_ptr(), n
+        assert pf.grad.stride() == pf.stride(), n
+        assert torch.allclose(pf.grad, pr.grad, atol=1e-6, rtol=1e-5), n
+    flat.zero_grad()
+    assert all(p.grad.abs().max() == 0 for p in m.parameters())
+
+
+def test_arena_adam_matches_torch_adam_and_padding_stays_zero():
+    m_ref = tiny()
+    m = tiny()
+    flat = FlatParams(m)
+    opt = FusedAdam(flat, lr=1e-2, use_hip=False)
+    opt_ref = torch.optim.Adam(m_ref.parameters(), lr=1e-2)
+    for _ in range(3):
+        tok = torch.randint(0, 29, (4, 9))
+        opt.zero_grad()
+        m(tok).pow(2).mean().backward()
+        opt.step(clip_norm=1.0)
+        opt_ref.zero_grad()
+        m_ref(tok).pow(2).mean().backward()
+        torch.nn.utils.clip_grad_norm_(m_ref.parameters(), 1.0)
+        opt_ref.step()
+    for (n, pr), (_, pf) in zip(m_ref.named_parameters(), m.named_parameters()):
+        if n.endswith("b_K"):  # gradient is zero in exact arithmetic: Adam normalises rounding noise
+            continue
+        assert torch.allclose(pf, pr, atol=1e-5, rtol=1e-4), n
+    W_U = m.unembed.W_U
+    pad = flat.data[flat.offset_of(W_U):flat.offset_of(W_U) + 12 * 32].view(12, 32)[:, 29:]
+    assert pad.abs().max() == 0
+
+
+def test_arena_mirror_and_buckets():
+    m = tiny()
+    flat = FlatParams(m, with_bf16_shadow=True)
+    for p in m.parameters():
+        assert torch.equal(flat.shadow_view(p).float(), p.detach().to(torch.bfloat16).float())
+    bks = flat.buckets(256)
+    assert bks[0][1] == flat.numel and bks[-1][0] == 0
+    starts = {o for o, _ in flat.slots}
+    for s, e in bks:
+        assert s in starts
+    covered = sorted(bks)
+    for (s0, e0), (s1, e1) in zip(covered, covered[1:]):
+        assert e0 == s1
+
+
+def test_frozen_attention_falls_back_to_contiguous():
+    m = tiny()
+    for blk in m.blocks:
+        blk.attn.W_K.requires_grad_(False)
+    FlatParams(m)
+    a = m.blocks[0].attn
+    assert a.W_Q.is_contiguous() and a.W_V.is_contiguous()

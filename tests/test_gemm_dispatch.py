@@ -1,0 +1,77 @@
+"""The library-GEMM side of ``iit_amd.ops.gemm_dispatch`` against fp32 references.
+
+The dispatcher picks, per (shape, layout, epilogue), between the hand-written
+MFMA kernel and hipBLASLt (``torch.mm``); both must implement the same operand
+layouts and epilogues.  The library side is plain torch, so it is checked on CPU
+here; the HIP side is checked by ``test_hip_kernels.py`` on the GPU.
+"""
+import torch
+
+from iit_amd.ops import gemm_dispatch as gd
+from iit_amd.ops import hip_kernels as K
+from iit_amd.ops.torch_ops import gelu_new
+
+BF = torch.bfloat16
+
+
+def _ref_ops(A, B, M, N, Kd, mode):
+    a = A.float().view(-1)
+    b = B.float().view(-1)
+    if mode & K.MODE_AKM:
+        am = a[: Kd * M].view(Kd, M).t()
+    else:
+        am = a[: M * Kd].view(M, Kd)
+    if mode & K.MODE_BKM:
+        bm = b[: Kd * N].view(Kd, N)
+    else:
+        bm = b[: N * Kd].view(N, Kd).t()
+    return am.to(BF).float() @ bm.to(BF).float()
+
+
+def _call(A, B, C, M, N, Kd, mode, epi, **kw):
+    defaults = dict(C2=None, C3=None, bias0=None, bias1=None, bias2=None, resid=None, ldr=0, aux=None, ldc2=0,
+                    bias_cols=0, qkv=(0, 0, 0))
+    defaults.update(kw)
+    lda = M if mode & K.MODE_AKM else Kd
+    ldb = N if mode & K.MODE_BKM else Kd
+    gd._blas(A, B, C, M, N, Kd, lda, ldb, N, mode, epi, **{k: defaults[k] for k in
+             ("C2", "C3", "bias0", "bias1", "bias2", "resid", "ldr", "aux", "ldc2", "bias_cols", "qkv")})
+
+
+def test_blas_layouts_and_bias3():
+    torch.manual_seed(0)
+    M, H, dh, Kd = 24, 3, 8, 16
+    N = 3 * H * dh
+    for mode in (K.MODE_NN, K.MODE_BKM, K.MODE_AKM | K.MODE_BKM):
+        A = torch.randn(M * Kd).to(BF)
+        B = torch.randn(N * Kd).to(BF)
+        bq, bk, bv = (torch.randn(H, dh) for _ in range(3))  # TL per-head bias shapes
+        C = torch.empty(M, N, dtype=BF)
+        _call(A, B, C, M, N, Kd, mode, K.EPI_BF16_BIAS3, bias0=bq, bias1=bk, bias2=bv, bias_cols=H * dh)
+        ref = _ref_ops(A, B, M, N, Kd, mode) + torch.cat([bq.reshape(-1), bk.reshape(-1), bv.reshape(-1)])
+        assert torch.allclose(C.float(), ref, atol=0.1, rtol=0.02), mode
+
+
+def test_blas_residual_gelu_acc_store():
+    torch.manual_seed(1)
+    M, N, Kd = 20, 12, 32
+    A = torch.randn(M, Kd).to(BF)
+    B = torch.randn(N, Kd).to(BF)
+    bias = torch.randn(N)
+    base = _ref_ops(A, B, M, N, Kd, K.MODE_NN)
+    R = torch.randn(M, N)
+    C = torch.empty(M, N)
+    _call(A, B, C, M, N, Kd, K.MODE_NN, K.EPI_F32_RESID, bias0=bias, resid=R, ldr=N)
+    assert torch.allclose(C, R + base + bias, atol=0.05, rtol=0.02)
+    post = torch.empty(M, N, dtype=BF)
+    pre = torch.empty(M, N, dtype=BF)
+    _call(A, B, post, M, N, Kd, K.MODE_NN, K.EPI_GELU, bias0=bias, C2=pre, ldc2=N)
+    assert torch.allclose(pre.float(), base + bias, atol=0.1, rtol=0.02)
+    assert torch.allclose(post.float(), gelu_new(pre.float()), atol=0.05, rtol=0.02)
+    acc = torch.randn(M, N)
+    exp = acc + base
+    _call(A, B, acc, M, N, Kd, K.MODE_NN, K.EPI_F32_ACC)
+    assert torch.allclose(acc, exp, atol=0.05, rtol=0.02)
+    st = torch.empty(M, N)
+    _call(A, B, st, M, N, Kd, K.MODE_NN, K.EPI_F32_STORE, bias0=bias)
+    assert torch.allclose(st, base + bias, atol=0.05, rtol=0.02)
