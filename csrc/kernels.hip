@@ -443,16 +443,27 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p, c
                                                         __bf16* __restrict__ mirror, long n4,
                                                         const float* __restrict__ part, int nparts, float clip,
                                                         float lr, float b1, float b2, float eps, float wd,
-                                                        const int* __restrict__ step) {
+                                                        int* __restrict__ step, int* __restrict__ skipped) {
   __shared__ float coef_s;
+  __shared__ int bad_s;
   if (threadIdx.x < 64) {
     float s = 0.f;
-    if (clip > 0.f)
+    if (clip > 0.f || skipped)
       for (int i = threadIdx.x; i < nparts; i += 64) s += part[i];
     s = wave_sum(s);
-    if (threadIdx.x == 0) coef_s = clip > 0.f ? fminf(1.f, clip / (sqrtf(s) + 1e-6f)) : 1.f;
+    if (threadIdx.x == 0) {
+      coef_s = clip > 0.f ? fminf(1.f, clip / (sqrtf(s) + 1e-6f)) : 1.f;
+      bad_s = skipped != nullptr && !isfinite(s);
+    }
   }
   __syncthreads();
+  if (bad_s) {  // non-finite gradient: skip the whole update (uniform over the grid), count it, undo the step bump
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      step[0] -= 1;
+      skipped[0] += 1;
+    }
+    return;
+  }
   const float coef = coef_s;
   const float t = (float)step[0];
   const float bc1 = 1.f - powf(b1, t);
@@ -486,15 +497,18 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p, c
   }
 }
 
+// ``skipped`` (nullable) enables the non-finite-gradient guard: the global norm is then always computed and a
+// step whose gradient contains inf/nan leaves weights, moments and the step counter untouched.
 IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, void* mirror, long n, float* part, int nparts,
-                             float clip, float lr, float b1, float b2, float eps, float wd, int* step, void* stream) {
+                             float clip, float lr, float b1, float b2, float eps, float wd, int* step, int* skipped,
+                             void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const long n4 = n / 4;
-  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(clip > 0.f ? nparts : 1), dim3(256), 0, s, g, n4, part,
-                     (int)(clip > 0.f), step);
+  const bool norm = clip > 0.f || skipped != nullptr;
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(norm ? nparts : 1), dim3(256), 0, s, g, n4, part, (int)norm, step);
   const int blocks = (int)min((n4 + 255) / 256, 8192L);
   hipLaunchKernelGGL(adam_flat_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, n4, part, nparts,
-                     clip, lr, b1, b2, eps, wd, step);
+                     clip, lr, b1, b2, eps, wd, step, skipped);
   return hipGetLastError();
 }
 

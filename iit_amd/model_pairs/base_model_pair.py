@@ -286,7 +286,10 @@ class BaseModelPair(ABC):
 
     # ------------------------------------------------------------------ training loop
     def train(self, train_set, test_set, epochs: int = 1000, use_wandb: bool = False,
-              checkpoint_dir: Optional[str] = None, resume: bool = False, max_steps: Optional[int] = None):
+              checkpoint_dir: Optional[str] = None, resume: bool = False, max_steps: Optional[int] = None,
+              fault_hook: Optional[Callable[[int], None]] = None):
+        """Reference training loop (``base_model_pair.py:204-261``) plus resume and a test-only
+        ``fault_hook(epoch)`` called after each epoch's checkpoint (fault-injection seam)."""
         training_args = self.training_args
         if pdist.is_main():
             print(f"{training_args=}")
@@ -326,9 +329,12 @@ class BaseModelPair(ABC):
             self.train_metrics = train_metrics
             if pdist.is_main():
                 self._print_and_log_metrics(epoch, train_metrics.metrics + test_metrics.metrics, sink)
-            if checkpoint_dir and pdist.is_main():
+            if checkpoint_dir:
                 from ..utils.checkpoint import save_resume_state
                 save_resume_state(checkpoint_dir, self, optimizer, lr_scheduler, epoch + 1)
+                pdist.barrier()
+            if fault_hook is not None:
+                fault_hook(epoch)
             if early_stop and self._check_early_stop_condition(test_metrics.metrics):
                 break
         if sink is not None:

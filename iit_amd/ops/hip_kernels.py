@@ -38,7 +38,7 @@ _SIGS = {
     "iit_attn_mfma_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
     "iit_ce_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "iit_ce_bwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_long, c_int, c_int, c_void_p],
-    "iit_adam_flat": [c_void_p] * 5 + [c_long, c_void_p, c_int] + [c_float] * 6 + [c_void_p, c_void_p],
+    "iit_adam_flat": [c_void_p] * 5 + [c_long, c_void_p, c_int] + [c_float] * 6 + [c_void_p, c_void_p, c_void_p],
     "iit_shadow_refresh": [c_void_p, c_int, c_void_p],
     "iit_shadow_desc_size": [],
     "iit_colsum_accum": [c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_void_p],
@@ -206,7 +206,7 @@ def make_shadow_descs(entries, device) -> torch.Tensor:
     return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
 
 
-def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_norm):
+def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_norm, skipped=None):
     """Fused clip + Adam over the arena; bumps the device step counter ``step_dev`` (int32[1]) and writes the
     bf16 mirror (``flat.shadow``) when present.  No host scalars depend on the step: graph-capturable."""
     n = flat.numel
@@ -216,5 +216,5 @@ def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_
         part = flat._norm_parts = torch.zeros(nparts, dtype=torch.float32, device=flat.data.device)
     _check(lib().iit_adam_flat(_p(flat.data), _p(flat.grad), _p(exp_avg), _p(exp_avg_sq), _p(flat.shadow), n,
                                _p(part), nparts, float(clip_norm or 0.0), lr, b1, b2, eps, wd, _p(step_dev),
-                               _stream()), "adam_flat")
+                               _p(skipped), _stream()), "adam_flat")
     flat.after_step(mirror_written=flat.shadow is not None)

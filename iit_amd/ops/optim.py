@@ -22,8 +22,16 @@ from ..engine.flat import FlatParams
 
 
 class FusedAdam(torch.optim.Optimizer):
+    """Adam over a :class:`FlatParams` arena.
+
+    ``nan_guard`` (default on): a step whose (clipped) gradient holds inf/nan is
+    skipped entirely -- weights, moments and the step counter stay untouched -- and
+    counted in :attr:`skipped_steps`.  On the GPU the check runs inside the fused
+    kernel (no host sync); the device step counter is the authoritative step count.
+    """
+
     def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, use_hip: Optional[bool] = None):
+                 weight_decay: float = 0.0, use_hip: Optional[bool] = None, nan_guard: bool = True):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(flat.params, defaults)
         self.flat = flat
@@ -31,13 +39,20 @@ class FusedAdam(torch.optim.Optimizer):
         self.exp_avg_sq = torch.zeros_like(flat.data)
         self.step_count = 0
         self.pending_clip = None
-        self._step_dev = torch.zeros(1, dtype=torch.int32, device=flat.data.device)  # device-side step counter
+        self.nan_guard = nan_guard
+        dev = flat.data.device
+        self._step_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # device-side step counter
+        self._skipped_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         if use_hip is None:
             use_hip = flat.data.is_cuda
         self._hip = None
         if use_hip:
             from . import hip_kernels
             self._hip = hip_kernels.lib()
+
+    @property
+    def skipped_steps(self) -> int:
+        return int(self._skipped_dev.item())
 
     def zero_grad(self, set_to_none: bool = False):  # noqa: D401 - arena memset
         self.flat.zero_grad()
@@ -50,37 +65,44 @@ class FusedAdam(torch.optim.Optimizer):
         self.flat.rebind_grads()
         group = self.param_groups[0]
         lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
-        self.step_count += 1
-        t = self.step_count
-        bc1 = 1.0 - b1 ** t
-        bc2 = 1.0 - b2 ** t
         g = self.flat.grad
         if self._hip is not None:
             from . import hip_kernels
+            self.step_count += 1
             hip_kernels.adam_step(self.flat, self.exp_avg, self.exp_avg_sq, self._step_dev, lr=lr, b1=b1, b2=b2,
-                                  eps=eps, wd=wd, clip_norm=clip_norm)
-        else:
-            if clip_norm:
-                norm = torch.linalg.vector_norm(g)
-                g.mul_(torch.clamp(clip_norm / (norm + 1e-6), max=1.0))
-            if wd:
-                g = g.add(self.flat.data, alpha=wd)
-            self.exp_avg.mul_(b1).add_(g, alpha=1 - b1)
-            self.exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
-            denom = (self.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(eps)
-            self.flat.data.addcdiv_(self.exp_avg, denom, value=-lr / bc1)
-            self.flat.after_step()
-        for p in self.flat.params:
-            self.state[p]["step"] = t
+                                  eps=eps, wd=wd, clip_norm=clip_norm,
+                                  skipped=self._skipped_dev if self.nan_guard else None)
+            return
+        norm = torch.linalg.vector_norm(g) if (clip_norm or self.nan_guard) else None
+        if self.nan_guard and not bool(torch.isfinite(norm)):
+            self._skipped_dev += 1
+            return
+        self.step_count += 1
+        self._step_dev += 1
+        t = self.step_count
+        bc1 = 1.0 - b1 ** t
+        bc2 = 1.0 - b2 ** t
+        if clip_norm:
+            g.mul_(torch.clamp(clip_norm / (norm + 1e-6), max=1.0))
+        if wd:
+            g = g.add(self.flat.data, alpha=wd)
+        self.exp_avg.mul_(b1).add_(g, alpha=1 - b1)
+        self.exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
+        denom = (self.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(eps)
+        self.flat.data.addcdiv_(self.exp_avg, denom, value=-lr / bc1)
+        self.flat.after_step()
 
     # ---------------------------------------------------------------- checkpointing
     def state_dict(self):
-        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+        self.step_count = int(self._step_dev.item())  # device counter is authoritative (guarded skips)
+        return {"step": self.step_count, "skipped": self.skipped_steps, "exp_avg": self.exp_avg,
+                "exp_avg_sq": self.exp_avg_sq,
                 "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]}
 
     def load_state_dict(self, sd):
         self.step_count = int(sd["step"])
         self._step_dev.fill_(self.step_count)
+        self._skipped_dev.fill_(int(sd.get("skipped", 0)))
         self.exp_avg.copy_(sd["exp_avg"])
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
         for g, saved in zip(self.param_groups, sd["param_groups"]):

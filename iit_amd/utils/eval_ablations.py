@@ -1,0 +1,305 @@
+"""Post-training circuit verification sweeps (parity: ``/root/reference/iit/utils/eval_ablations.py:15-352``).
+
+For every candidate LL node (all / in-circuit / not-in-circuit, via
+:mod:`iit_amd.utils.node_picker`):
+
+* **resample ablation** — patch the node's activation from the source input
+  into the base run and score the change against the HL's *base* output:
+  KL(HL_base || LL_patched) at the label index (default) or, with
+  ``Categorical_Metric.ACCURACY``, the fraction of label-changing pairs whose
+  prediction flipped away from the HL base label; regression HL: fraction of
+  label-changing pairs whose output moved by more than ``atol``;
+* **mean / zero ablation** — replace the node by its dataset mean (or 0) and count
+  the fraction of correctly-predicted base inputs whose prediction flips.
+
+MI355X-native execution: with a plan-capable LL model the source activation is
+captured by a truncated ``run_capture`` and the patch is an in-kernel splice
+(:class:`iit_amd.engine.plan.RunPlan`); the per-node sweep never builds hook
+closures, computes only the logits the metric reads, and accumulates scores on
+device (one host read per sweep instead of one per node per batch).  Any other
+LL model takes the reference hook path.
+"""
+from __future__ import annotations
+
+import os
+from enum import Enum
+from typing import Callable, Dict, Optional
+
+import torch
+
+from ..core.index import EVERYTHING, TorchIndex
+from ..core.nodes import LLNode
+from ..engine.plan import RunPlan
+from ..hooks.hook_points import HookPoint
+from .eval_metrics import kl_div
+from .node_picker import get_all_nodes, get_nodes_in_circuit, get_nodes_not_in_circuit
+from .progress import progress
+
+
+class Categorical_Metric(Enum):
+    ACCURACY = 1
+    KL = 2
+
+
+# ----------------------------------------------------------------------------- helpers
+def _native(model_pair) -> bool:
+    return model_pair.native() if hasattr(model_pair, "native") else False
+
+
+def _reduced_logits(model_pair) -> bool:
+    """LL outputs are already at the label position ([B, V]) in the native IOI mode."""
+    return _native(model_pair) and model_pair.ll_logits_mode() == "last"
+
+
+def _at(out: torch.Tensor, label_idx: TorchIndex, reduced: bool) -> torch.Tensor:
+    return out if reduced else out[label_idx.as_index]
+
+
+def _hl_out(model_pair, base_in):
+    kw = model_pair.hl_run_kwargs() if hasattr(model_pair, "hl_run_kwargs") else {}
+    with torch.no_grad():
+        out = model_pair.hl_model(base_in, **kw)
+    return out, bool(kw.get("last_only", False))
+
+
+def _labels_at(y: torch.Tensor, label_idx: TorchIndex) -> torch.Tensor:
+    if y.dtype.is_floating_point:
+        y = torch.argmax(y, dim=-1)
+    return y[label_idx.as_index]
+
+
+def _nodes(model_pair, node_type: str, with_suffixes: bool = False):
+    assert node_type in ["a", "c", "n"], "type must be one of 'a', 'c', or 'n'"
+    if node_type == "n":
+        return get_nodes_not_in_circuit(model_pair.ll_model, model_pair.corr)
+    if node_type == "c":
+        return get_nodes_in_circuit(model_pair.corr)
+    if with_suffixes:
+        return get_all_nodes(model_pair.ll_model, model_pair.corr.get_suffixes())
+    return get_all_nodes(model_pair.ll_model)
+
+
+# ----------------------------------------------------------------------------- resample ablation
+def do_intervention(model_pair, base_input, ablation_input, node: LLNode, hooker: Optional[Callable] = None):
+    """LL output on ``base_input`` with ``node`` patched from ``ablation_input`` (``eval_ablations.py:20-32``)."""
+    if _native(model_pair):
+        with torch.no_grad():
+            model_pair.ll_cache = model_pair.ll_source_cache(ablation_input, [node])
+            return model_pair.ll_intervened_forward(base_input, [node])
+    _, cache = model_pair.ll_model.run_with_cache(ablation_input)
+    model_pair.ll_cache = cache
+    hooker = hooker or model_pair.make_ll_ablation_hook(node)
+    return model_pair.ll_model.run_with_hooks(base_input, fwd_hooks=[(node.name, hooker)])
+
+
+def resample_ablate_node(model_pair, base_in, ablation_in, node: LLNode, results: Dict, hooker: Optional[Callable] = None,
+                         atol: float = 5e-2, verbose: bool = False,
+                         categorical_metric: Categorical_Metric = Categorical_Metric.KL) -> None:
+    """Adds this batch's score for ``node`` to ``results[node]`` (a device scalar; summed over batches)."""
+    base_x, base_y = base_in[0], base_in[1]
+    ablation_y = ablation_in[1]
+    reduced = _reduced_logits(model_pair)
+    ll_out = do_intervention(model_pair, base_x, ablation_in[0], node, hooker)
+    base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
+    if model_pair.hl_model.is_categorical():
+        label_idx = model_pair.get_label_idxs()
+        label_unchanged = _labels_at(base_y, label_idx) == _labels_at(ablation_y, label_idx)
+        ll_at = _at(ll_out, label_idx, reduced)
+        hl_at = _at(base_hl_out.squeeze() if not hl_reduced else base_hl_out, label_idx, hl_reduced)
+        if categorical_metric == Categorical_Metric.KL:
+            score = kl_div(ll_at, hl_at, EVERYTHING).mean()
+            if verbose:
+                print(node, "kl base_hl vs ll_out:", float(score),
+                      "fraction of labels changed:", float((~label_unchanged).float().mean()))
+        else:
+            ll_pred = torch.argmax(ll_at, dim=-1)
+            hl_pred = torch.argmax(hl_at, dim=-1)
+            changed = (~label_unchanged).float() * (ll_pred != hl_pred).float()
+            score = changed.sum() / (~label_unchanged).float().sum()
+    else:
+        label_unchanged = base_y == ablation_y
+        ll_unchanged = torch.isclose(ll_out.float().squeeze(), base_hl_out.float().to(ll_out.device).squeeze(),
+                                     atol=atol)
+        changed = (~label_unchanged).float().reshape(ll_unchanged.shape) * (~ll_unchanged).float()
+        score = changed.sum() / (~label_unchanged).float().sum()
+    results[node] = results[node] + score.detach()
+
+
+def check_causal_effect(model_pair, dataset, batch_size: int = 256, node_type: str = "a", verbose: bool = False,
+                        categorical_metric: Categorical_Metric = Categorical_Metric.KL) -> Dict[LLNode, float]:
+    """Mean resample-ablation score per node over the dataset (``eval_ablations.py:128-161``)."""
+    nodes = _nodes(model_pair, node_type)
+    hookers = {} if _native(model_pair) else {n: model_pair.make_ll_ablation_hook(n) for n in nodes}
+    results = {n: 0 for n in nodes}
+    loader = dataset.make_loader(batch_size=batch_size, num_workers=0)
+    nb = 0
+    for base_in, ablation_in in progress(loader, desc="resample ablation"):
+        nb += 1
+        for node in nodes:
+            resample_ablate_node(model_pair, base_in, ablation_in, node, results, hookers.get(node), verbose=verbose,
+                                 categorical_metric=categorical_metric)
+    return {n: float(v) / max(nb, 1) for n, v in results.items()}
+
+
+# ----------------------------------------------------------------------------- mean / zero ablation
+def get_mean_cache(model_pair, dataset, batch_size: int = 8, names=None) -> Dict[str, torch.Tensor]:
+    """Dataset mean of every (or the named) LL hook activation, shape [1, ...] (``eval_ablations.py:164-173``)."""
+    loader = dataset.make_loader(batch_size=batch_size, num_workers=0)
+    n = len(loader)
+    mean_cache: Dict[str, torch.Tensor] = {}
+    model = model_pair.ll_model
+    with torch.no_grad():
+        for batch in progress(loader, desc="mean cache"):
+            x = batch[0]
+            if _native(model_pair):
+                wanted = names if names is not None else list(model.hook_dict.keys())
+                cache = model.run_capture(x, sorted(wanted))
+            else:
+                _, cache = model.run_with_cache(x)
+            for name, t in cache.items():
+                m = t.float().mean(dim=0, keepdim=True) / n
+                mean_cache[name] = mean_cache[name] + m if name in mean_cache else m
+    return mean_cache
+
+
+def make_ablation_hook(node: LLNode, mean_cache: Optional[Dict[str, torch.Tensor]], use_mean_cache: bool = True
+                       ) -> Callable[[torch.Tensor, HookPoint], torch.Tensor]:
+    if node.subspace is not None:
+        raise NotImplementedError("Subspace not supported yet.")
+    index = node.index if node.index is not None else EVERYTHING
+
+    def zero_hook(act: torch.Tensor, hook: HookPoint) -> torch.Tensor:
+        act[index.as_index] = 0
+        return act
+
+    def mean_hook(act: torch.Tensor, hook: HookPoint) -> torch.Tensor:
+        act[index.as_index] = mean_cache[node.name][index.as_index].to(act.dtype)
+        return act
+
+    return mean_hook if use_mean_cache else zero_hook
+
+
+def _ablation_value(node: LLNode, mean_cache, use_mean_cache: bool, like: torch.Tensor) -> torch.Tensor:
+    if use_mean_cache:
+        return mean_cache[node.name].to(like.dtype).expand_as(like)
+    return torch.zeros_like(like)
+
+
+def ablate_node(model_pair, base_in, node: LLNode, results: Dict, hook: Optional[Callable] = None, atol: float = 5e-2,
+                verbose: bool = False, mean_cache=None, use_mean_cache: bool = True, shapes=None) -> None:
+    base_x, base_y = base_in[0], base_in[1]
+    model = model_pair.ll_model
+    reduced = _reduced_logits(model_pair)
+    with torch.no_grad():
+        if _native(model_pair):
+            like = shapes[node.name] if shapes is not None else model.run_capture(base_x, [node.name])[node.name]
+            if like.shape[0] != base_x.shape[0]:
+                like = like[:1].expand(base_x.shape[0], *like.shape[1:])
+            val = _ablation_value(node, mean_cache, use_mean_cache, like)
+            plan = RunPlan.with_splices([(node.name, node.index, val)], logits=model_pair.ll_logits_mode())
+            ll_out = model(base_x, plan=plan)
+            base_ll_out = model_pair.ll_forward(base_x)
+        else:
+            ll_out = model.run_with_hooks(base_x, fwd_hooks=[(node.name, hook)])
+            base_ll_out = model(base_x)
+        base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
+    if model_pair.hl_model.is_categorical():
+        label_idx = model_pair.get_label_idxs()
+        ll_pred = torch.argmax(_at(ll_out.squeeze() if not reduced else ll_out, label_idx, reduced), dim=-1)
+        hl_pred = torch.argmax(_at(base_hl_out.squeeze() if not hl_reduced else base_hl_out, label_idx, hl_reduced),
+                               dim=-1)
+        base_pred = torch.argmax(_at(base_ll_out.squeeze() if not reduced else base_ll_out, label_idx, reduced),
+                                 dim=-1)
+        accuracy = (base_pred == hl_pred).float()
+        changed = (ll_pred != hl_pred).float() * accuracy
+    else:
+        ll_unchanged = torch.isclose(ll_out.float().squeeze(), base_hl_out.float().squeeze(), atol=atol)
+        accuracy = torch.isclose(base_ll_out.float().squeeze(), base_hl_out.float().squeeze(), atol=atol).float()
+        changed = (~ll_unchanged).float() * accuracy
+    results[node] = results[node] + changed.sum() / (accuracy.sum() + 1e-6)
+
+
+def check_causal_effect_on_ablation(model_pair, dataset, batch_size: int = 256, node_type: str = "a",
+                                    mean_cache: Optional[Dict[str, torch.Tensor]] = None, verbose: bool = False
+                                    ) -> Dict[LLNode, float]:
+    """Mean (or zero) ablation effect per node (``eval_ablations.py:262-295``)."""
+    use_mean_cache = bool(mean_cache)
+    nodes = _nodes(model_pair, node_type, with_suffixes=True)
+    native = _native(model_pair)
+    hookers = {} if native else {n: make_ablation_hook(n, mean_cache, use_mean_cache) for n in nodes}
+    results = {n: 0 for n in nodes}
+    loader = dataset.make_loader(batch_size=batch_size, num_workers=0)
+    nb = 0
+    for base_in in progress(loader, desc="ablation"):
+        nb += 1
+        shapes = None
+        if native:
+            with torch.no_grad():
+                shapes = model_pair.ll_model.run_capture(base_in[0], sorted({n.name for n in nodes}))
+        for node in nodes:
+            ablate_node(model_pair, base_in, node, results, hookers.get(node), verbose=verbose, mean_cache=mean_cache,
+                        use_mean_cache=use_mean_cache, shapes=shapes)
+    return {n: float(v) / max(nb, 1) for n, v in results.items()}
+
+
+def get_causal_effects_for_all_nodes(model_pair, uni_test_set, batch_size: int = 256, use_mean_cache: bool = True):
+    mean_cache = get_mean_cache(model_pair, uni_test_set, batch_size=batch_size) if use_mean_cache else None
+    za_not = check_causal_effect_on_ablation(model_pair, uni_test_set, batch_size=batch_size, node_type="n",
+                                             mean_cache=mean_cache)
+    za_in = check_causal_effect_on_ablation(model_pair, uni_test_set, batch_size=batch_size, node_type="c",
+                                            mean_cache=mean_cache)
+    return za_not, za_in
+
+
+# ----------------------------------------------------------------------------- reporting
+def _node_label(node: LLNode) -> str:
+    if "mlp" in node.name:
+        return node.name
+    if node.index is not None and node.index != EVERYTHING:
+        return f"{node.name}, head {str(node.index).split(',')[-2]}"
+    return f"{node.name}, head [:]"
+
+
+def make_dataframe_of_results(result_not_in_circuit, result_in_circuit):
+    import pandas as pd
+    df = pd.DataFrame({
+        "node": [_node_label(n) for n in result_not_in_circuit] + [_node_label(n) for n in result_in_circuit],
+        "status": ["not_in_circuit"] * len(result_not_in_circuit) + ["in_circuit"] * len(result_in_circuit),
+        "causal effect": list(result_not_in_circuit.values()) + list(result_in_circuit.values()),
+    })
+    return df.sort_values("status", ascending=False)
+
+
+def make_combined_dataframe_of_results(result_not_in_circuit, result_in_circuit, za_result_not_in_circuit,
+                                       za_result_in_circuit, use_mean_cache: bool = False):
+    df = make_dataframe_of_results(result_not_in_circuit, result_in_circuit)
+    df2 = make_dataframe_of_results(za_result_not_in_circuit, za_result_in_circuit)
+    df["resample_ablate_effect"] = df.pop("causal effect")
+    df["mean_ablate_effect" if use_mean_cache else "zero_ablate_effect"] = df2.pop("causal effect")
+    return df
+
+
+def save_result(df, save_dir: str, model_pair=None) -> None:
+    """``results.csv`` (+ ``results.png`` table render, + ``meta.log`` training args) under ``save_dir``."""
+    os.makedirs(save_dir, exist_ok=True)
+    try:
+        _render_table_png(df, os.path.join(save_dir, "results.png"))
+    except Exception as e:  # rendering is best-effort, as in the reference
+        print(f"Error exporting dataframe to image: {e}")
+    df.to_csv(os.path.join(save_dir, "results.csv"))
+    if model_pair is None:
+        return
+    with open(os.path.join(save_dir, "meta.log"), "w") as f:
+        f.write(str(model_pair.training_args))
+
+
+def _render_table_png(df, path: str) -> None:
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    fig, ax = plt.subplots(figsize=(min(20, 2 + 2.2 * len(df.columns)), 0.4 + 0.3 * len(df)))
+    ax.axis("off")
+    cells = [[f"{v:.4f}" if isinstance(v, float) else str(v) for v in row] for row in df.itertuples(index=False)]
+    ax.table(cellText=cells, colLabels=list(df.columns), loc="center")
+    fig.savefig(path, bbox_inches="tight", dpi=120)
+    plt.close(fig)

@@ -1,0 +1,83 @@
+"""Causal-effect sweeps (iit_amd.utils.eval_ablations / eval_metrics): native plan engine vs reference hooks."""
+import torch
+
+from iit_amd.core.index import Ix
+from iit_amd.data.iit_dataset import IITDataset, IITUniqueDataset
+from iit_amd.tasks.ioi import make_ioi_corr, make_ioi_dataset_and_hl
+from iit_amd.utils import eval_ablations as ea
+from iit_amd.utils.eval_metrics import accuracy_affected, kl_div
+
+
+def _pair(n_layers=6):
+    from iit_amd.model_pairs import IOI_ModelPair
+    from iit_amd.models.config import gpt2_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    cfg = gpt2_config_dict()
+    cfg.update(n_layers=n_layers, d_model=32, n_heads=4, d_head=8, d_mlp=64, device="cpu")
+    torch.manual_seed(0)
+    ll = HookedTransformer(cfg)
+    ds, hl = make_ioi_dataset_and_hl(96, ll, device="cpu")
+    pair = IOI_ModelPair(hl, ll, make_ioi_corr(n_layers), training_args={"batch_size": 32, "lr_scheduler": None})
+    return pair, ds
+
+
+def test_kl_div_matches_definition():
+    torch.manual_seed(0)
+    a = torch.randn(5, 7, 11)
+    b = torch.randn(5, 7, 11).softmax(-1)  # already a pmf: used as-is
+    kl = kl_div(a, b, Ix[:, -1])
+    pa = a[:, -1].softmax(-1)
+    pb = b[:, -1]
+    assert torch.allclose(kl, (pb * (pb.log() - pa.log())).sum(-1), atol=1e-6)
+    unchanged = torch.tensor([True, False, False, True, False])
+    r = accuracy_affected(a, b, unchanged, Ix[:, -1])
+    flips = (a[:, -1].argmax(-1) != b[:, -1].argmax(-1)).float() * (~unchanged).float()
+    assert torch.isclose(r, flips.sum() / 3)
+
+
+def test_resample_ablation_native_equals_reference():
+    pair, ds = _pair()
+    iit_set = IITDataset(ds, ds, seed=0, device="cpu")
+    res = {}
+    for engine in ("native", "reference"):
+        pair.training_args["engine"] = engine
+        torch.manual_seed(0)
+        res[engine] = {**ea.check_causal_effect(pair, iit_set, batch_size=32, node_type="n"),
+                       **ea.check_causal_effect(pair, iit_set, batch_size=32, node_type="c")}
+    assert res["native"].keys() == res["reference"].keys()
+    assert len(res["native"]) == 8 + 7  # [OBS] 8 nodes not in the IOI circuit; 7 corr LL nodes
+    for node in res["native"]:
+        assert abs(res["native"][node] - res["reference"][node]) < 1e-4, node
+    torch.manual_seed(0)
+    pair.training_args["engine"] = "native"
+    acc = ea.check_causal_effect(pair, iit_set, batch_size=32, node_type="c",
+                                 categorical_metric=ea.Categorical_Metric.ACCURACY)
+    assert all(0.0 <= v <= 1.0 for v in acc.values())
+
+
+def test_mean_and_zero_ablation_native_equals_reference(tmp_path):
+    pair, ds = _pair()
+    uni = IITUniqueDataset(ds, ds, seed=0, device="cpu")
+    out = {}
+    for engine in ("native", "reference"):
+        pair.training_args["engine"] = engine
+        torch.manual_seed(0)
+        mean_cache = ea.get_mean_cache(pair, uni, batch_size=32)
+        torch.manual_seed(0)
+        za_n, za_c = (ea.check_causal_effect_on_ablation(pair, uni, batch_size=32, node_type=t, mean_cache=mean_cache)
+                      for t in ("n", "c"))
+        torch.manual_seed(0)
+        zero = ea.check_causal_effect_on_ablation(pair, uni, batch_size=32, node_type="c", mean_cache=None)
+        out[engine] = (mean_cache, za_n, za_c, zero)
+    mc_n, mc_r = out["native"][0], out["reference"][0]
+    for k in ("blocks.0.attn.hook_z", "blocks.3.mlp.hook_post"):
+        assert torch.allclose(mc_n[k], mc_r[k], atol=1e-5)
+    for i in (1, 2, 3):
+        for node, v in out["native"][i].items():
+            assert abs(v - out["reference"][i][node]) < 1e-3, node
+    df = ea.make_combined_dataframe_of_results(out["native"][1], out["native"][2], out["native"][1], out["native"][2],
+                                               use_mean_cache=True)
+    assert list(df.columns) == ["node", "status", "resample_ablate_effect", "mean_ablate_effect"]
+    ea.save_result(df, str(tmp_path / "results"), pair)
+    assert (tmp_path / "results" / "results.csv").exists()
+    assert (tmp_path / "results" / "meta.log").read_text().startswith("{")

@@ -1,0 +1,22 @@
+"""The reference's entry-point scripts run end to end on CPU (tiny sizes): train_ioi.py -> eval_ioi.py."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def test_train_then_eval_ioi(tmp_path):
+    import eval_ioi
+    import train_ioi
+    root = str(tmp_path / "models" / "ioi")
+    train_ioi.main(["--num-samples", "96", "--epochs", "1", "--batch-size", "32", "--save-root", root,
+                    "--max-steps", "2", "--no-early-stop"])
+    d = os.path.join(root, "IOI_ModelPair", "100_100_40")
+    assert os.path.exists(os.path.join(d, "ll_model.pth"))
+    df = eval_ioi.main(["-w", "100_100_40", "--root", root, "--num-samples", "64", "-b", "32",
+                        "--resample-batch-size", "32", "-m", "true"])
+    assert set(df["status"]) == {"in_circuit", "not_in_circuit"}
+    assert len(df) == 8 + 7
+    assert os.path.exists(os.path.join(d, "results", "results.csv"))
+    assert os.path.exists(os.path.join(d, "results", "metric_collection.log"))
