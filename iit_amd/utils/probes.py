@@ -51,6 +51,23 @@ def construct_probes(model_pair, input_shape, bias: bool = False, input_dtype: O
     return {hl.name: construct_probe(hl, lls, dummy, bias=bias) for hl, lls in model_pair.corr.items()}
 
 
+def _batches(dataset, batch_size: int, shuffle: bool, num_workers: int = 0):
+    """``(x, y, int_vars)`` batches; device-side ``gather`` when the dataset supports it (no per-item Python)."""
+    gather = getattr(dataset, "gather", None)
+    if gather is not None:
+        n = len(dataset)
+        order = torch.randperm(n) if shuffle else torch.arange(n)
+        order = order.to(DEVICE)
+        for s in range(0, n, batch_size):
+            yield gather(order[s:s + batch_size])
+        return
+    yield from torch.utils.data.DataLoader(dataset, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers)
+
+
+def _num_batches(dataset, batch_size: int) -> int:
+    return (len(dataset) + batch_size - 1) // batch_size
+
+
 def probe_logits(probe: nn.Linear, cache, ll_node: LLNode) -> torch.Tensor:
     act = cache[ll_node.name][ll_node.index.as_index]
     return probe(act.reshape(-1, probe.weight.shape[1]).to(probe.weight.dtype))
@@ -65,13 +82,12 @@ def train_probes_on_model_pair(model_pair, input_shape, train_set, training_args
     criterion = nn.CrossEntropyLoss()
     losses = {k: [] for k in probes}
     accs = {k: [] for k in probes}
-    loader = torch.utils.data.DataLoader(train_set, batch_size=training_args["batch_size"], shuffle=True,
-                                         num_workers=training_args.get("num_workers", 0))
+    bs = training_args["batch_size"]
     names = [n.name for v in model_pair.corr.values() for n in _nodes(v)]
     for _ in range(training_args["epochs"]):
         loss_run = {k: torch.zeros((), device=DEVICE) for k in probes}
         acc_run = {k: torch.zeros((), device=DEVICE) for k in probes}
-        for x, y, int_vars in loader:
+        for x, y, int_vars in _batches(train_set, bs, True, training_args.get("num_workers", 0)):
             opt.zero_grad()
             x = x.to(DEVICE)
             with torch.no_grad():
@@ -87,7 +103,7 @@ def train_probes_on_model_pair(model_pair, input_shape, train_set, training_args
                     acc_run[hl_name] += (out.argmax(1) == gt).float().mean()
             total.backward()
             opt.step()
-        n = max(1, len(loader))
+        n = max(1, _num_batches(train_set, bs))
         for k in probes:
             losses[k].append(float(loss_run[k]) / n)
             accs[k].append(float(acc_run[k]) / n)
@@ -97,20 +113,19 @@ def train_probes_on_model_pair(model_pair, input_shape, train_set, training_args
 def evaluate_probe(probes, model_pair, test_set, criterion):
     stats = {"test loss": {}, "test accuracy": {}}
     names = [n.name for v in model_pair.corr.values() for n in _nodes(v)]
-    loader = torch.utils.data.DataLoader(test_set, batch_size=256, shuffle=True, num_workers=0)
     for hl_name, probe in probes.items():
         probe.eval()
         loss = torch.zeros((), device=DEVICE)
         acc = torch.zeros((), device=DEVICE)
         with torch.no_grad():
-            for x, y, int_vars in loader:
+            for x, y, int_vars in _batches(test_set, 256, True):
                 cache = capture_hooks(model_pair.ll_model, x.to(DEVICE), names)
                 gt = model_pair.hl_model.get_idx_to_intermediate(hl_name)(int_vars.to(DEVICE)).to(DEVICE)
                 for node in _nodes(model_pair.corr[hl_name]):
                     out = probe_logits(probe, cache, node)
                     loss += criterion(out, gt)
                     acc += (out.argmax(1) == gt).float().mean()
-        n = max(1, len(loader))
+        n = max(1, _num_batches(test_set, 256))
         stats["test loss"][hl_name] = float(loss) / n
         stats["test accuracy"][hl_name] = float(acc) / n
     return stats
