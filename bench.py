@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--engine", default="native", choices=["native", "reference"],
                     help="reference = reference-semantics eager path (hook closures, full caches, full logits)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--graphs", type=int, default=int(os.environ.get("IIT_GRAPHS", "0")))
+    ap.add_argument("--graphs", type=int, default=int(os.environ.get("IIT_GRAPHS", "1")),
+                    help="capture each train-step phase as a HIP graph (default on; 0 = eager)")
     ap.add_argument("--profile-dir", default=None)
     return ap.parse_args()
 
@@ -84,9 +85,11 @@ def setup(args, dev):
 
     it = batches()
     step_fn = pair.run_train_step
-    if args.graphs:
+    if args.graphs and dev.type == "cuda" and args.engine == "native":
         from iit_amd.engine.graphs import GraphedTrainStep
-        step_fn = GraphedTrainStep(pair, opt, loss_fn)
+        g = GraphedTrainStep(pair, opt, loss_fn)
+        if g.enabled:
+            step_fn = g
     return pair, opt, loss_fn, it, step_fn, train_set, test_set
 
 
@@ -101,8 +104,10 @@ def main():
 
     pair, opt, loss_fn, it, step_fn, train_set, test_set = setup(args, dev)
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         base, abl = next(it)
+        if i == 0 and hasattr(step_fn, "prime"):
+            step_fn.prime(base, abl, loss_fn, opt)  # capture every phase graph before timing
         step_fn(base, abl, loss_fn, opt)
     batches_timed = [next(it) for _ in range(args.steps)]
     pdist.barrier()
@@ -150,7 +155,8 @@ def main():
             "config": {"model": "gpt2-small 12L/768d/12H (TL GPT-2 cfg, LNPre, gelu_new, V=50257)"
                        if args.model == "gpt2-small" else "ioi-6l 6L/64d/4H",
                        "global_batch": global_batch, "seq_len": int(train_set.base_data.dataset.prompts.shape[1] - 1),
-                       "parallelism": f"dp{world}", "engine": args.engine, "graphs": bool(args.graphs)},
+                       "parallelism": f"dp{world}", "engine": args.engine,
+                       "graphs": bool(getattr(step_fn, "enabled", False))},
             "val_IIA": round(float(vals["val/IIA"]), 3),
             "val_accuracy": round(float(vals["val/accuracy"]), 3),
             "last_train_losses": {k: round(v, 4) for k, v in train_loss.items()},

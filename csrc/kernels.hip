@@ -118,11 +118,14 @@ IIT_EXPORT int iit_ln_fwd(const float* x, const float* w, const float* b, void* 
   return hipGetLastError();
 }
 
-// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w;  dw += dy * xhat, db += dy
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) (+ dres),  g = dy * w;  dw += dy * xhat, db += dy
+// ``dres`` (nullable) is the residual stream's skip-connection gradient: fusing it here saves autograd's
+// separate gradient-sum pass over the fp32 residual.
 template <int VPL, bool DY_F32>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ w, float* __restrict__ dx,
+                                                     const float* __restrict__ dres,
                                                      float* __restrict__ dw, float* __restrict__ db, int T, int d,
                                                      int accumulate) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -155,7 +158,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
   for (int i = 0; i < VPL; ++i) {
     const int c = lane + i * 64;
     if (c < d) {
-      const float o = rs * (g[i] - sg - xh[i] * sgx);
+      float o = rs * (g[i] - sg - xh[i] * sgx);
+      if (dres) o += dres[(long)row * d + c];
       float* p = dx + (long)row * d + c;
       *p = accumulate ? *p + o : o;
     }
@@ -163,12 +167,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
 }
 
 IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
-                          const float* w, float* dx, float* dw, float* db, int T, int d, int accumulate, void* stream) {
+                          const float* w, float* dx, const float* dres, float* dw, float* db, int T, int d,
+                          int accumulate, void* stream) {
   dim3 grid((T + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
 #define LNB(V)                                                                                                   \
-  if (dy_f32) hipLaunchKernelGGL((ln_bwd_kernel<V, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate); \
-  else hipLaunchKernelGGL((ln_bwd_kernel<V, false>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate);
+  if (dy_f32) hipLaunchKernelGGL((ln_bwd_kernel<V, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, dw, db, T, d, accumulate); \
+  else hipLaunchKernelGGL((ln_bwd_kernel<V, false>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, dw, db, T, d, accumulate);
   if (d <= 256) { LNB(4) }
   else if (d <= 1024) { LNB(16) }
   else if (d <= 2048) { LNB(32) }
@@ -340,45 +345,61 @@ IIT_EXPORT int iit_attn_small_bwd(const void* qkv, const void* dz, const float* 
 }
 
 // ============================================================================ cross entropy
-// one 256-thread block per row of fp32 logits: lse, loss = lse - x[label], argmax (first index on ties)
-__global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ logits, long ld, const long* __restrict__ labels,
-                                                     float* __restrict__ loss, float* __restrict__ lse_out,
-                                                     long* __restrict__ amax, int V) {
-  __shared__ float sm[8];
-  __shared__ int si[8];
+// Per row: loss = lse - x[label], lse = max + log(sum exp(x - max)), argmax (first index on ties).
+// One 1024-thread block per row, a single pass with an online (max, sum) rescale and 16-byte loads.
+__device__ __forceinline__ void online_add(float& m, float& s, int& mi, float v, int i) {
+  if (v > m) {
+    s = s * __expf(m - v) + 1.f;
+    m = v;
+    mi = i;
+  } else {
+    s += __expf(v - m);
+  }
+}
+
+__device__ __forceinline__ void online_merge(float& m, float& s, int& mi, float om, float os, int oi) {
+  if (om > m || (om == m && oi < mi)) {
+    s = os + (m == -INFINITY ? 0.f : s * __expf(m - om));
+    m = om;
+    mi = oi;
+  } else {
+    s += (om == -INFINITY ? 0.f : os * __expf(om - m));
+  }
+}
+
+__global__ __launch_bounds__(1024) void ce_fwd_kernel(const float* __restrict__ logits, long ld, const long* __restrict__ labels,
+                                                      float* __restrict__ loss, float* __restrict__ lse_out,
+                                                      long* __restrict__ amax, int V) {
+  __shared__ float sm_m[16], sm_s[16];
+  __shared__ int sm_i[16];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float* x = logits + (long)row * ld;
-  float m = -INFINITY;
+  float m = -INFINITY, s = 0.f;
   int mi = 0x7fffffff;
-  for (int i = tid; i < V; i += 256) {
-    const float v = x[i];
-    if (v > m) { m = v; mi = i; }
+  int head = 0;
+  if ((((uintptr_t)x) & 15) == 0) {
+    const int v4 = V / 4;
+    for (int i = tid; i < v4; i += 1024) {
+      const float4 q = ((const float4*)x)[i];
+      online_add(m, s, mi, q.x, 4 * i);
+      online_add(m, s, mi, q.y, 4 * i + 1);
+      online_add(m, s, mi, q.z, 4 * i + 2);
+      online_add(m, s, mi, q.w, 4 * i + 3);
+    }
+    head = v4 * 4;
   }
-  // (value, index) argmax with first-index tie-break
+  for (int i = head + tid; i < V; i += 1024) online_add(m, s, mi, x[i], i);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const float om = __shfl_xor(m, o, 64);
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
     const int oi = __shfl_xor(mi, o, 64);
-    if (om > m || (om == m && oi < mi)) { m = om; mi = oi; }
+    online_merge(m, s, mi, om, os, oi);
   }
-  if (lane == 0) { sm[w] = m; si[w] = mi; }
+  if (lane == 0) { sm_m[w] = m; sm_s[w] = s; sm_i[w] = mi; }
   __syncthreads();
   if (tid == 0) {
-    for (int j = 1; j < 4; ++j)
-      if (sm[j] > sm[0] || (sm[j] == sm[0] && si[j] < si[0])) { sm[0] = sm[j]; si[0] = si[j]; }
-  }
-  __syncthreads();
-  m = sm[0];
-  mi = si[0];
-  float s = 0.f;
-  for (int i = tid; i < V; i += 256) s += __expf(x[i] - m);
-  s = wave_sum(s);
-  __syncthreads();
-  if (lane == 0) sm[4 + w] = s;
-  __syncthreads();
-  if (tid == 0) {
-    const float tot = sm[4] + sm[5] + sm[6] + sm[7];
-    const float l = m + __logf(tot);
+    for (int j = 1; j < 16; ++j) online_merge(m, s, mi, sm_m[j], sm_s[j], sm_i[j]);
+    const float l = m + __logf(s);
     if (lse_out) lse_out[row] = l;
     if (loss && labels) loss[row] = l - x[labels[row]];
     if (amax) amax[row] = mi;
@@ -387,14 +408,15 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ l
 
 IIT_EXPORT int iit_ce_fwd(const float* logits, long ld, const long* labels, float* loss, float* lse, long* amax, int R,
                           int V, void* stream) {
-  hipLaunchKernelGGL(ce_fwd_kernel, dim3(R), dim3(256), 0, (hipStream_t)stream, logits, ld, labels, loss, lse, amax, V);
+  hipLaunchKernelGGL(ce_fwd_kernel, dim3(R), dim3(1024), 0, (hipStream_t)stream, logits, ld, labels, loss, lse, amax, V);
   return hipGetLastError();
 }
 
-// dlogits = (softmax - onehot) * gscale[0] * inv_rows   (fp32 out, ld_out may be padded; pad columns zeroed)
+// dlogits = (softmax - onehot) * gscale[0] * inv_rows   (fp32 or bf16 out, ld_out may be padded; pad columns zeroed)
+template <typename OUT>
 __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ logits, long ld, const long* __restrict__ labels,
                                                      const float* __restrict__ lse, const float* __restrict__ gscale,
-                                                     float inv_rows, float* __restrict__ out, long ld_out, int V) {
+                                                     float inv_rows, OUT* __restrict__ out, long ld_out, int V) {
   const int row = blockIdx.y;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= ld_out) return;
@@ -403,14 +425,18 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ l
     const float p = __expf(logits[(long)row * ld + i] - lse[row]);
     v = (p - (i == labels[row] ? 1.f : 0.f)) * gscale[0] * inv_rows;
   }
-  out[(long)row * ld_out + i] = v;
+  out[(long)row * ld_out + i] = (OUT)v;
 }
 
 IIT_EXPORT int iit_ce_bwd(const float* logits, long ld, const long* labels, const float* lse, const float* gscale,
-                          float inv_rows, void* out, long ld_out, int R, int V, void* stream) {
+                          float inv_rows, void* out, long ld_out, int R, int V, int out_bf16, void* stream) {
   dim3 grid((unsigned)((ld_out + 255) / 256), R);
-  hipLaunchKernelGGL(ce_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, logits, ld, labels, lse, gscale, inv_rows,
-                     (float*)out, ld_out, V);
+  if (out_bf16)
+    hipLaunchKernelGGL(ce_bwd_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, logits, ld, labels, lse, gscale,
+                       inv_rows, (__bf16*)out, ld_out, V);
+  else
+    hipLaunchKernelGGL(ce_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, logits, ld, labels, lse, gscale,
+                       inv_rows, (float*)out, ld_out, V);
   return hipGetLastError();
 }
 
@@ -599,23 +625,133 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x,
   if (w == 0 && n < N) atomicAdd(out + n, part[0][c] + part[1][c] + part[2][c] + part[3][c]);
 }
 
+// Vectorised variant: 256 threads = 32 column groups (16 B each: 8 bf16 / 4 fp32 columns) x 8 row groups,
+// 128 rows per block; LDS combine over row groups, one fp32 atomic per column per block.
+template <bool F32>
+__global__ __launch_bounds__(256) void colsum_vec_kernel(const void* __restrict__ x, long ld, float* __restrict__ out,
+                                                         int T, int N) {
+  constexpr int CPT = F32 ? 4 : 8;  // columns per thread
+  __shared__ float part[8][32 * CPT];
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c0 = (blockIdx.x * 32 + cg) * CPT;
+  const int t0 = blockIdx.y * 128;
+  float acc[CPT];
+#pragma unroll
+  for (int e = 0; e < CPT; ++e) acc[e] = 0.f;
+  if (c0 < N) {
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+      const int t = t0 + rg + 8 * i;
+      if (t < T) {
+        if (F32) {
+          const float4 v = *(const float4*)((const float*)x + (long)t * ld + c0);
+          acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+        } else {
+          const bf16x8 v = *(const bf16x8*)((const __bf16*)x + (long)t * ld + c0);
+#pragma unroll
+          for (int e = 0; e < CPT; ++e) acc[e] += bf2f(v[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < CPT; ++e) part[rg][cg * CPT + e] = acc[e];
+  __syncthreads();
+  const int col = threadIdx.x;  // 256 threads cover the block's 32*CPT columns (CPT=8) or twice (CPT=4)
+  if (col < 32 * CPT) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) s += part[r][col];
+    const int n = blockIdx.x * 32 * CPT + col;
+    if (n < N) atomicAdd(out + n, s);
+  }
+}
+
 IIT_EXPORT int iit_colsum_accum(const void* x, int f32, long ld, float* out, int T, int N, void* stream) {
+  const int cpt = f32 ? 4 : 8;
+  const bool vec = (N % cpt == 0) && (ld % cpt == 0) && ((((uintptr_t)x) & 15) == 0);
+  if (vec) {
+    dim3 grid((N + 32 * cpt - 1) / (32 * cpt), (T + 127) / 128);
+    if (f32) hipLaunchKernelGGL(colsum_vec_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
+    else hipLaunchKernelGGL(colsum_vec_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
+    return hipGetLastError();
+  }
   dim3 grid((N + 63) / 64, (T + 63) / 64);
   if (f32) hipLaunchKernelGGL(colsum_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
   else hipLaunchKernelGGL(colsum_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
   return hipGetLastError();
 }
 
-// dpre = dpost * gelu_new'(pre)   (bf16, contiguous)
+// dpre = dpost * gelu_new'(pre)   (bf16, contiguous; 8 elements / 16 B per thread when n % 8 == 0)
 __global__ void dgelu_kernel(const __bf16* __restrict__ dpost, const __bf16* __restrict__ pre, __bf16* __restrict__ out, long n) {
+  if ((n & 7) == 0) {
+    const long n8 = n >> 3;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+      const bf16x8 g = ((const bf16x8*)dpost)[i], x = ((const bf16x8*)pre)[i];
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(g[e]) * gelu_new_grad_f(bf2f(x[e])));
+      ((bf16x8*)out)[i] = o;
+    }
+    return;
+  }
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
     out[i] = f2bf(bf2f(dpost[i]) * gelu_new_grad_f(bf2f(pre[i])));
 }
 
 IIT_EXPORT int iit_dgelu(const void* dpost, const void* pre, void* out, long n, void* stream) {
-  const int blocks = (int)min((n + 255) / 256, 8192L);
+  const long work = (n & 7) == 0 ? n / 8 : n;
+  const int blocks = (int)min((work + 255) / 256, 8192L);
   hipLaunchKernelGGL(dgelu_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const __bf16*)dpost,
                      (const __bf16*)pre, (__bf16*)out, n);
+  return hipGetLastError();
+}
+
+// out[m][n] = base[m][n] + y[m][n] + bias[n]  (fp32 out/base, bf16 y; base may alias out, bias nullable).
+// Completes a library GEMM that wrote bf16 into the fp32 residual / gradient accumulate epilogues.
+template <bool VEC>
+__global__ __launch_bounds__(256) void add_bf16_kernel(float* __restrict__ out, long ldo, const float* base, long ldb,
+                                                       const __bf16* __restrict__ y, long ldy,
+                                                       const float* __restrict__ bias, int M, int N) {
+  if (VEC) {
+    const int n8 = N >> 3;
+    const long total = (long)M * n8;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+      const int m = (int)(i / n8), c = (int)(i % n8) * 8;
+      const bf16x8 v = *(const bf16x8*)(y + m * ldy + c);
+      const float4 b0 = *(const float4*)(base + m * ldb + c), b1 = *(const float4*)(base + m * ldb + c + 4);
+      float4 o0 = make_float4(b0.x + bf2f(v[0]), b0.y + bf2f(v[1]), b0.z + bf2f(v[2]), b0.w + bf2f(v[3]));
+      float4 o1 = make_float4(b1.x + bf2f(v[4]), b1.y + bf2f(v[5]), b1.z + bf2f(v[6]), b1.w + bf2f(v[7]));
+      if (bias) {
+        const float4 c0 = *(const float4*)(bias + c), c1 = *(const float4*)(bias + c + 4);
+        o0.x += c0.x; o0.y += c0.y; o0.z += c0.z; o0.w += c0.w;
+        o1.x += c1.x; o1.y += c1.y; o1.z += c1.z; o1.w += c1.w;
+      }
+      *(float4*)(out + m * ldo + c) = o0;
+      *(float4*)(out + m * ldo + c + 4) = o1;
+    }
+    return;
+  }
+  const long total = (long)M * N;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int m = (int)(i / N), n = (int)(i % N);
+    out[m * ldo + n] = base[m * ldb + n] + bf2f(y[m * ldy + n]) + (bias ? bias[n] : 0.f);
+  }
+}
+
+IIT_EXPORT int iit_add_bf16(float* out, long ldo, const float* base, long ldb, const void* y, long ldy,
+                            const float* bias, int M, int N, void* stream) {
+  const bool vec = (N % 8 == 0) && (ldo % 4 == 0) && (ldb % 4 == 0) && (ldy % 8 == 0) &&
+                   ((((uintptr_t)out) | ((uintptr_t)base)) & 15) == 0 && (((uintptr_t)y) & 15) == 0 &&
+                   (!bias || (((uintptr_t)bias) & 15) == 0);
+  const long work = vec ? (long)M * (N / 8) : (long)M * N;
+  const int blocks = (int)min((work + 255) / 256, 8192L);
+  if (vec)
+    hipLaunchKernelGGL(add_bf16_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, out, ldo, base, ldb,
+                       (const __bf16*)y, ldy, bias, M, N);
+  else
+    hipLaunchKernelGGL(add_bf16_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, out, ldo, base, ldb,
+                       (const __bf16*)y, ldy, bias, M, N);
   return hipGetLastError();
 }
 

@@ -1,0 +1,179 @@
+"""HIP-graph captured IIT training steps (HIP graphs instead of a tracing compiler).
+
+An IIT step is a short chain of optimizer *phases* (IIT, strict, behaviour for
+``IOI_ModelPair``); each phase is a fixed kernel sequence for a given sampled
+node: source capture forward, spliced base forward, HL forwards, loss, backward,
+fused clip+Adam.  The only host decisions are the node samples, taken from the
+pair's RNG *before* the phase runs.  So :class:`GraphedTrainStep`:
+
+* keeps static device buffers for the batch (each new batch is copied in: six
+  small ``copy_`` launches);
+* runs the first ``warmup`` occurrences of every phase key eagerly (this also
+  settles lazily-built state: GEMM autotune decisions, the bf16 weight mirror,
+  hipBLASLt heuristics), then captures the phase once with
+  ``torch.cuda.graph`` into a memory pool shared by all phase graphs (phases
+  never run concurrently) and replays it from then on;
+* returns clones of the captured loss outputs, so metric stores never alias
+  buffers a later replay overwrites.
+
+The fused Adam keeps its step counter / bias corrections / NaN-guard on device,
+so replays are exact continuations of the eager schedule; the step-level
+semantics (RNG stream, phase order, 3 optimizer steps per IOI batch) are the
+pair's own ``run_train_step`` -- this class only swaps the phase executor.
+
+Batches whose shapes differ from the captured ones (e.g. a short final batch)
+run eagerly.  Data-parallel runs capture too only with ``IIT_GRAPHS_DP=1``
+(RCCL collectives inside captured graphs).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional, Tuple
+
+import torch
+
+
+def _clone_out(out):
+    if isinstance(out, tuple):
+        loss, extras = out
+        return loss.clone(), {k: v.clone() for k, v in extras.items()}
+    return out.clone()
+
+
+def _detach_out(out):
+    if isinstance(out, tuple):
+        loss, extras = out
+        return loss.detach(), {k: v.detach() for k, v in extras.items()}
+    return out.detach()
+
+
+class GraphedTrainStep:
+    def __init__(self, pair, optimizer=None, loss_fn=None, warmup: int = 1, enabled: Optional[bool] = None):
+        self.pair = pair
+        self.optimizer = optimizer
+        self.loss_fn = loss_fn
+        self.warmup = warmup
+        if enabled is None:
+            enabled = torch.cuda.is_available()
+            ws = torch.distributed.get_world_size() if (torch.distributed.is_available()
+                                                       and torch.distributed.is_initialized()) else 1
+            if ws > 1 and os.environ.get("IIT_GRAPHS_DP", "0") != "1":
+                enabled = False
+        self.enabled = enabled
+        self.graphs: Dict[Tuple, Tuple[torch.cuda.CUDAGraph, object]] = {}
+        self.seen: Dict[Tuple, int] = {}
+        self.pool = torch.cuda.graph_pool_handle() if enabled else None
+        self._static = None
+        self._sig = None
+        self.captures = 0
+        self.replays = 0
+        self.failed: Dict[Tuple, str] = {}
+        pair._phase_runner = self._run_phase
+
+    # ------------------------------------------------------------------ static inputs
+    def _stage(self, base, abl):
+        """Returns (base, abl, eager): static buffers holding this batch, or the batch itself + eager=True."""
+        if not self.enabled:
+            return base, abl, True
+        sig = tuple((tuple(t.shape), t.dtype, t.device) for t in tuple(base) + tuple(abl))
+        if self._static is None:
+            self._static = (tuple(t.clone() for t in base), tuple(t.clone() for t in abl))
+            self._sig = sig
+            return self._static[0], self._static[1], False
+        if sig != self._sig:  # e.g. a short last batch: eager, keep the captured buffers
+            return base, abl, True
+        sb, sa = self._static
+        for d, src in zip(sb + sa, tuple(base) + tuple(abl)):
+            d.copy_(src, non_blocking=True)
+        return sb, sa, False
+
+    # ------------------------------------------------------------------ phases
+    @staticmethod
+    def _eager(compute_loss, optimizer, step_fn):
+        out = compute_loss()
+        loss = out[0] if isinstance(out, tuple) else out
+        step_fn(loss, optimizer)
+        return _detach_out(out)
+
+    def _run_phase(self, key, compute_loss, optimizer, step_fn):
+        full = (key, self._sig)
+        if not self.enabled or self._current_eager:
+            return self._eager(compute_loss, optimizer, step_fn)
+        ent = self.graphs.get(full)
+        if ent is None:
+            n = self.seen.get(full, 0)
+            if n < self.warmup:
+                self.seen[full] = n + 1
+                return self._eager(compute_loss, optimizer, step_fn)
+            if full in self.failed:
+                return self._eager(compute_loss, optimizer, step_fn)
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, pool=self.pool):
+                    out = compute_loss()
+                    loss = out[0] if isinstance(out, tuple) else out
+                    step_fn(loss, optimizer)
+                    static_out = _detach_out(out)
+            except Exception as e:  # something in the phase is not capturable: keep it eager
+                self.failed[full] = repr(e)
+                import traceback
+                tb = "".join(traceback.format_exc(limit=12)) if len(self.failed) == 1 else ""
+                print(f"[iit graphs] phase {key} not captured ({type(e).__name__}: {str(e)[:160]}); "
+                      f"running it eagerly\n{tb}")
+                torch.cuda.synchronize()
+                return self._eager(compute_loss, optimizer, step_fn)
+            ent = self.graphs[full] = (g, static_out)
+            self.captures += 1
+        g, static_out = ent
+        g.replay()
+        self.replays += 1
+        return _clone_out(static_out)
+
+    # ------------------------------------------------------------------ step
+    def __call__(self, base_input, ablation_input, loss_fn=None, optimizer=None):
+        loss_fn = loss_fn or self.loss_fn
+        optimizer = optimizer or self.optimizer
+        sb, sa, eager = self._stage(base_input, ablation_input)
+        self._current_eager = eager
+        try:
+            return self.pair.run_train_step(sb, sa, loss_fn, optimizer)
+        finally:
+            self._current_eager = False
+
+    _current_eager = False
+
+    def prime(self, base_input, ablation_input, loss_fn=None, optimizer=None) -> int:
+        """Capture every phase key up front (untimed warmup): force each HL / strict node in turn.
+
+        Each forced phase is a real optimizer step (warmup steps train too); the pair's
+        node-sampling RNG is saved and restored, so the sampled sequence of the run
+        that follows is unchanged.  Returns the number of graphs captured so far."""
+        import copy
+        pair = self.pair
+        rng_state = copy.deepcopy(pair.rng)
+        hl_nodes = list(pair.corr.keys())
+        ll_nodes = list(getattr(pair, "nodes_not_in_circuit", []) or [None])
+        orig_hl = pair.__dict__.get("sample_hl_name")
+        orig_ll = pair.__dict__.get("sample_ll_node")
+        try:
+            n = max(len(hl_nodes), len(ll_nodes))
+            for rep in range(self.warmup + 1):
+                for i in range(n):
+                    pair.sample_hl_name = lambda i=i: hl_nodes[i % len(hl_nodes)]
+                    if ll_nodes[0] is not None:
+                        pair.sample_ll_node = lambda i=i: ll_nodes[i % len(ll_nodes)]
+                    self(base_input, ablation_input, loss_fn, optimizer)
+        finally:
+            for name, orig in (("sample_hl_name", orig_hl), ("sample_ll_node", orig_ll)):
+                if orig is None:
+                    pair.__dict__.pop(name, None)
+                else:
+                    setattr(pair, name, orig)
+            pair.rng = rng_state
+        return self.captures
+
+    def detach(self) -> None:
+        """Restore eager phases on the pair (graphs are released)."""
+        if getattr(self.pair, "_phase_runner", None) == self._run_phase:
+            self.pair._phase_runner = None
+        self.graphs.clear()

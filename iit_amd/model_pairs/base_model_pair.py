@@ -199,6 +199,26 @@ class BaseModelPair(ABC):
 
         return ll_ablation_hook
 
+    def run_phase(self, key, compute_loss: Callable[[], Tensor], optimizer, step_fn) -> Tensor:
+        """One optimizer phase of a train step: ``loss = compute_loss(); step_fn(loss, optimizer)``.
+
+        ``compute_loss`` may return ``(loss, extras)``; the phase then returns
+        ``(loss, extras)`` detached (e.g. the parts of a single combined loss).
+
+        ``key`` names the phase's static structure (phase kind + sampled node), so
+        :class:`iit_amd.engine.graphs.GraphedTrainStep` can capture each distinct
+        phase once as a HIP graph and replay it; without a runner it runs eagerly."""
+        runner = getattr(self, "_phase_runner", None)
+        if runner is not None:
+            return runner(key, compute_loss, optimizer, step_fn)
+        out = compute_loss()
+        if isinstance(out, tuple):  # (loss, {name: tensor}) -> (loss, detached extras)
+            loss, extras = out
+            step_fn(loss, optimizer)
+            return loss.detach(), {k: v.detach() for k, v in extras.items()}
+        step_fn(out, optimizer)
+        return out.detach()
+
     def get_IIT_loss_over_batch(self, base_input, ablation_input, hl_node: HookName, loss_fn):
         hl_output, ll_output = self.do_intervention(base_input, ablation_input, hl_node)
         return loss_fn(ll_output, hl_output)

@@ -71,18 +71,25 @@ class IITBehaviorModelPair(IITModelPair):
         self.optimizer_step(optimizer)
 
     def run_train_step(self, base_input, ablation_input, loss_fn, optimizer):
-        single = self.training_args["use_single_loss"]
+        args = self.training_args
         hl_node = self.sample_hl_name()
-        iit_loss = self.get_IIT_loss_over_batch(base_input, ablation_input, hl_node, loss_fn) \
-            * self.training_args["iit_weight"]
-        if not single:
-            self.step_on_loss(iit_loss, optimizer)
-        behavior_loss = self.get_behaviour_loss_over_batch(base_input, loss_fn) * self.training_args["behavior_weight"]
-        if not single:
-            self.step_on_loss(behavior_loss, optimizer)
-        else:
-            self.step_on_loss(iit_loss + behavior_loss, optimizer)
-        return {"train/iit_loss": iit_loss.detach(), "train/behavior_loss": behavior_loss.detach()}
+
+        def iit():
+            return self.get_IIT_loss_over_batch(base_input, ablation_input, hl_node, loss_fn) * args["iit_weight"]
+
+        def behavior():
+            return self.get_behaviour_loss_over_batch(base_input, loss_fn) * args["behavior_weight"]
+
+        if args["use_single_loss"]:
+            def total():
+                parts = {"iit": iit(), "behavior": behavior()}
+                return parts["iit"] + parts["behavior"], parts
+
+            _, parts = self.run_phase(("single", hl_node.name), total, optimizer, self.step_on_loss)
+            return {"train/iit_loss": parts["iit"], "train/behavior_loss": parts["behavior"]}
+        iit_loss = self.run_phase(("iit", hl_node.name), iit, optimizer, self.step_on_loss)
+        behavior_loss = self.run_phase(("behavior",), behavior, optimizer, self.step_on_loss)
+        return {"train/iit_loss": iit_loss, "train/behavior_loss": behavior_loss}
 
     def run_eval_step(self, base_input, ablation_input, loss_fn):
         atol = self.training_args["atol"]

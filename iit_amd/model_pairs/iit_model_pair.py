@@ -82,10 +82,15 @@ class IITModelPair(BaseModelPair):
         accuracy = (top1 == labels_of(hl_output, ll_output)).float().mean()
         return {"val/iit_loss": loss.detach(), "val/accuracy": accuracy}
 
-    def run_train_step(self, base_input, ablation_input, loss_fn, optimizer):
+    def _plain_step(self, loss, optimizer) -> None:
+        """zero_grad -> backward -> step (no clipping: reference ``iit_model_pair.py:85-99``)."""
         optimizer.zero_grad()
-        hl_node = self.sample_hl_name()
-        loss = self.get_IIT_loss_over_batch(base_input, ablation_input, hl_node, loss_fn)
         self.backward(loss)
         self.optimizer_step(optimizer)
-        return {"train/iit_loss": loss.detach()}
+
+    def run_train_step(self, base_input, ablation_input, loss_fn, optimizer):
+        hl_node = self.sample_hl_name()
+        loss = self.run_phase(("iit", hl_node.name),
+                              lambda: self.get_IIT_loss_over_batch(base_input, ablation_input, hl_node, loss_fn),
+                              optimizer, self._plain_step)
+        return {"train/iit_loss": loss}

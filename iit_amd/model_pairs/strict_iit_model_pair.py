@@ -49,24 +49,34 @@ class StrictIITModelPair(IITBehaviorModelPair):
         return loss_fn(out.squeeze(), base_y)
 
     def run_train_step(self, base_input, ablation_input, loss_fn, optimizer):
-        single = self.training_args["use_single_loss"]
+        args = self.training_args
         hl_node = self.sample_hl_name()
-        iit_loss = self.get_IIT_loss_over_batch(base_input, ablation_input, hl_node, loss_fn) \
-            * self.training_args["iit_weight"]
-        if not single:
-            self.step_on_loss(iit_loss, optimizer)
+
+        def iit():
+            return self.get_IIT_loss_over_batch(base_input, ablation_input, hl_node, loss_fn) * args["iit_weight"]
+
+        if args["use_single_loss"]:
+            ll_node = self.sample_ll_node()
+
+            def total():
+                parts = {"iit": iit(),
+                         "strict": self.get_strict_loss_over_batch(base_input, ablation_input, ll_node, loss_fn)
+                         * args["strict_weight"],
+                         "behavior": self.get_behaviour_loss_over_batch(base_input, loss_fn) * args["behavior_weight"]}
+                return parts["iit"] + parts["behavior"] + parts["strict"], parts
+
+            _, parts = self.run_phase(("single", hl_node.name, ll_node.name, repr(ll_node.index)), total, optimizer,
+                                      self.step_on_loss)
+            return {"train/iit_loss": parts["iit"], "train/behavior_loss": parts["behavior"],
+                    "train/strict_loss": parts["strict"]}
+        iit_loss = self.run_phase(("iit", hl_node.name), iit, optimizer, self.step_on_loss)
+        # the strict node is drawn after the IIT phase, as in the reference (same RNG stream)
         ll_node = self.sample_ll_node()
-        strict_loss = self.get_strict_loss_over_batch(base_input, ablation_input, ll_node, loss_fn) \
-            * self.training_args["strict_weight"]
-        if not single:
-            self.step_on_loss(strict_loss, optimizer)
-        behavior_loss = self.get_behaviour_loss_over_batch(base_input, loss_fn) * self.training_args["behavior_weight"]
-        if not single:
-            self.step_on_loss(behavior_loss, optimizer)
-        else:
-            self.step_on_loss(iit_loss + behavior_loss + strict_loss, optimizer)
-        return {
-            "train/iit_loss": iit_loss.detach(),
-            "train/behavior_loss": behavior_loss.detach(),
-            "train/strict_loss": strict_loss.detach(),
-        }
+        strict_loss = self.run_phase(
+            ("strict", ll_node.name, repr(ll_node.index)),
+            lambda: self.get_strict_loss_over_batch(base_input, ablation_input, ll_node, loss_fn) * args["strict_weight"],
+            optimizer, self.step_on_loss)
+        behavior_loss = self.run_phase(
+            ("behavior",), lambda: self.get_behaviour_loss_over_batch(base_input, loss_fn) * args["behavior_weight"],
+            optimizer, self.step_on_loss)
+        return {"train/iit_loss": iit_loss, "train/behavior_loss": behavior_loss, "train/strict_loss": strict_loss}

@@ -237,6 +237,15 @@ class TransformerBlock(nn.Module):
             return x.to(run.ops.dtype)
         return ln.run(x, run)
 
+    def _norm_fork(self, ln, x, run):
+        """(normed x, residual to carry forward): fused backends return a passthrough of ``x`` whose
+        gradient the LN backward kernel adds in (one pass instead of LN-bwd + autograd's sum)."""
+        fork = getattr(run.ops, "layer_norm_fork", None)
+        if (ln is None or fork is None or run.live(ln.hook_scale) or run.live(ln.hook_normalized)
+                or not x.requires_grad):
+            return self._norm(ln, x, run), x
+        return fork(x, ln.w, ln.b, ln.eps)
+
     def forward(self, resid: torch.Tensor, run: _Run) -> torch.Tensor:
         ops = run.ops
         attn = self.attn
@@ -248,7 +257,7 @@ class TransformerBlock(nn.Module):
         if spl is not None and not attn.inner_live(run) and not ln1_live:
             z = run.site(attn.hook_z, spl.src.to(ops.dtype), spliced=True)
         else:
-            x = self._norm(self.ln1, resid, run)
+            x, resid = self._norm_fork(self.ln1, resid, run)
             z, spliced = attn.compute_z(x, run)
             z = run.site(attn.hook_z, z, spliced=spliced)
         attn_out_live = run.live(self.hook_attn_out) or self.cfg.use_attn_result
@@ -274,7 +283,7 @@ class TransformerBlock(nn.Module):
         if spl is not None and not run.live(mlp.hook_pre) and not ln2_live:
             post = run.site(mlp.hook_post, spl.src.to(ops.dtype), spliced=True)
         else:
-            x = self._norm(self.ln2, resid_mid, run)
+            x, resid_mid = self._norm_fork(self.ln2, resid_mid, run)
             pre_hook = (lambda t: run.site(mlp.hook_pre, t)) if run.live(mlp.hook_pre) else None
             _, post = ops.mlp_in(x, mlp.W_in, mlp.b_in, self.cfg.act_fn, hook_pre=pre_hook)
             post = run.site(mlp.hook_post, post)

@@ -133,20 +133,59 @@ def _scratch(t, rows, ld):
     return torch.zeros(rows * ld, dtype=t.dtype, device=t.device)
 
 
-def _time(fn, reps=3):
+def _time(fn, reps: int = 10) -> float:
+    """GPU time per call in microseconds.
+
+    Candidates are timed as a captured graph of ``reps`` back-to-back calls, so the
+    number reflects device time only (training steps run as graph replays, where
+    host launch overhead is gone); if capture fails the eager loop is timed."""
     fn()
+    torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / reps * 1e3
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        s.record()
+        g.replay()
+        e.record()
+        e.synchronize()
+        return s.elapsed_time(e) / reps * 1e3
+    except Exception:
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        e.synchronize()
+        return s.elapsed_time(e) / reps * 1e3
+
+
+def _blas16(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, resid, ldr):
+    """fp32-output epilogues as a bf16-output library GEMM + one fused ``add_bf16`` pass
+    (hipBLASLt's bf16-in/fp32-out kernels are markedly slower than its bf16-out ones on gfx950)."""
+    a, b = _operands(A, B, M, N, Kd, lda, ldb, mode)
+    y = torch.mm(a, b)
+    bias = None if bias0 is None else bias0.reshape(-1).float().contiguous()
+    if epi == K.EPI_F32_RESID:
+        K.add_bf16(C, ldc, resid, ldr, y, N, bias, M, N)
+    else:  # EPI_F32_ACC: C += y
+        K.add_bf16(C, ldc, C, ldc, y, N, None, M, N)
+
+
+_BLAS16_EPIS = (K.EPI_F32_RESID, K.EPI_F32_ACC)
 
 
 def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=None, bias0=None, bias1=None,
          bias2=None, resid=None, ldr=0, aux=None, ldc2=0, bias_cols=0, qkv=(0, 0, 0), splits=None, blas_bias=None):
-    """``C = A @ B`` (+ epilogue) on the faster of the MFMA kernel and hipBLASLt for this problem.
+    """``C = A @ B`` (+ epilogue) on the fastest measured implementation for this problem:
+
+    * ``hip``    -- the hand-written MFMA kernel with the epilogue fused;
+    * ``blas``   -- hipBLASLt (``torch.mm`` / ``addmm``; fp32-output variants for fp32 epilogues);
+    * ``blas16`` -- (fp32 residual / accumulate epilogues) hipBLASLt bf16 output + the fused
+      :func:`iit_amd.ops.hip_kernels.add_bf16` pass.
 
     ``blas_bias``: optional ready-made bf16 bias row (e.g. a view of the arena's bf16 mirror) for the
     library path, saving its per-call concatenate/cast."""
@@ -160,8 +199,12 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         return hip_call()
     blas_call = lambda c=C, c2=C2, c3=C3: _blas(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi, c2, c3, bias0,  # noqa
                                                bias1, bias2, resid, ldr, aux, ldc2, bias_cols, qkv, blas_bias)
-    if policy == "blas":
-        return blas_call()
+    calls = {"hip": hip_call, "blas": blas_call}
+    if epi in _BLAS16_EPIS:
+        calls["blas16"] = lambda c=C, c2=C2, c3=C3: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
+                                                           bias0, resid, ldr)
+    if policy in calls:
+        return calls[policy]()
     key = (M, N, Kd, mode, epi, bias0 is not None)
     choice = DECISIONS.get(key)
     if choice is None:
@@ -171,10 +214,10 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         sc = _scratch(C, M, max(ldc, N))
         sc2 = _scratch(C2, M, max(ldc2, N))
         sc3 = _scratch(C3, M, max(ldc, N))
-        t_h = min(_time(lambda: hip_call(sc, sc2, sc3)) for _ in range(2))
-        t_b = min(_time(lambda: blas_call(sc, sc2, sc3)) for _ in range(2))
-        choice = DECISIONS[key] = ("hip" if t_h <= t_b else "blas", t_h, t_b)
-    return hip_call() if choice[0] == "hip" else blas_call()
+        times = {name: min(_time(lambda f=f: f(sc, sc2, sc3)) for _ in range(2)) for name, f in calls.items()}
+        best = min(times, key=times.get)
+        choice = DECISIONS[key] = (best, times)
+    return calls[choice[0]]()
 
 
 K_ = K  # the kernel module (``K`` is shadowed by the reduction-size keyword above)
@@ -182,7 +225,7 @@ K_ = K  # the kernel module (``K`` is shadowed by the reduction-size keyword abo
 
 def report() -> str:
     lines = [f"library fast paths: {dict(_BLAS_OK) or 'all available'}"]
-    for (M, N, Kd, mode, epi, bias), (c, th, tb) in sorted(DECISIONS.items()):
-        lines.append(f"M={M:6d} N={N:6d} K={Kd:6d} mode={mode:2d} epi={epi} bias={int(bias)} -> {c:4s} "
-                     f"hip {th:8.1f}us blas {tb:8.1f}us")
+    for (M, N, Kd, mode, epi, bias), (c, times) in sorted(DECISIONS.items()):
+        ts = "  ".join(f"{k} {v:8.1f}us" for k, v in times.items())
+        lines.append(f"M={M:6d} N={N:6d} K={Kd:6d} mode={mode:2d} epi={epi} bias={int(bias)} -> {c:6s} {ts}")
     return "\n".join(lines)

@@ -29,7 +29,7 @@ _SIGS = {
     "iit_embed_pos_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_embed_pos_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_ln_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
-    "iit_ln_bwd": [c_void_p, c_int] + [c_void_p] * 7 + [c_int, c_int, c_int, c_void_p],
+    "iit_ln_bwd": [c_void_p, c_int] + [c_void_p] * 8 + [c_int, c_int, c_int, c_void_p],
     "iit_attn_small_fwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float, c_int,
                                             c_void_p],
     "iit_attn_small_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
@@ -37,12 +37,14 @@ _SIGS = {
                                            c_void_p],
     "iit_attn_mfma_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
     "iit_ce_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "iit_ce_bwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_long, c_int, c_int, c_void_p],
+    "iit_ce_bwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_long, c_int, c_int, c_int,
+                   c_void_p],
     "iit_adam_flat": [c_void_p] * 5 + [c_long, c_void_p, c_int] + [c_float] * 6 + [c_void_p, c_void_p, c_void_p],
     "iit_shadow_refresh": [c_void_p, c_int, c_void_p],
     "iit_shadow_desc_size": [],
     "iit_colsum_accum": [c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_void_p],
     "iit_dgelu": [c_void_p, c_void_p, c_void_p, c_long, c_void_p],
+    "iit_add_bf16": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_int, c_void_p],
     "iit_device_sync": [],
 }
 
@@ -128,9 +130,10 @@ def ln_fwd(x, w, b, y, mean, rstd, T, d, eps):
     _check(lib().iit_ln_fwd(_p(x), _p(w), _p(b), _p(y), _p(mean), _p(rstd), T, d, eps, _stream()), "ln_fwd")
 
 
-def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False):
-    _check(lib().iit_ln_bwd(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx), _p(dw),
-                            _p(db), T, d, int(accumulate), _stream()), "ln_bwd")
+def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False, dres=None):
+    """dx = LN'(dy) (+ dres, the skip-connection gradient, fp32 [T, d])."""
+    _check(lib().iit_ln_bwd(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx),
+                            _p(dres), _p(dw), _p(db), T, d, int(accumulate), _stream()), "ln_bwd")
 
 
 def heads_to_mask(heads: Optional[Sequence[int]]) -> int:
@@ -168,8 +171,9 @@ def ce_fwd(logits, ld, labels, loss, lse, amax, R, V):
 
 
 def ce_bwd(logits, ld, labels, lse, gscale, inv_rows, out, ld_out, R, V):
+    """dlogits into ``out`` (fp32 or bf16, row stride ``ld_out``; pad columns zeroed)."""
     _check(lib().iit_ce_bwd(_p(logits), ld, _p(labels), _p(lse), _p(gscale), inv_rows, _p(out), ld_out, R, V,
-                            _stream()), "ce_bwd")
+                            int(out.dtype == torch.bfloat16), _stream()), "ce_bwd")
 
 
 def colsum_accum(x, ld, out, T, N):
@@ -184,6 +188,11 @@ def colsum3_accum(x, ld, outs, T, N):
 
 def dgelu(dpost, pre, out):
     _check(lib().iit_dgelu(_p(dpost), _p(pre), _p(out), dpost.numel(), _stream()), "dgelu")
+
+
+def add_bf16(out, ldo, base, ldb, y, ldy, bias, M, N):
+    """out = base + y + bias (fp32 out/base, bf16 y, fp32 bias or None); base may alias out."""
+    _check(lib().iit_add_bf16(_p(out), ldo, _p(base), ldb, _p(y), ldy, _p(bias), M, N, _stream()), "add_bf16")
 
 
 def shadow_refresh(descs: torch.Tensor, n: int):

@@ -299,6 +299,45 @@ class LayerNormFn(Function):
         return (dx if ctx.in_dtype == F32 else dx.to(ctx.in_dtype)), None, None, None
 
 
+class LayerNormForkFn(Function):
+    """``(LN(x), x)``: the second output carries the residual stream past the norm, so the backward gets
+    both gradients and sums them inside the LN-backward kernel (no separate autograd add over [T, d])."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        ctx.set_materialize_grads(False)
+        shape = x.shape
+        d = shape[-1]
+        x2 = _flat2(x.float().contiguous())
+        T = x2.shape[0]
+        y = torch.empty(T, d, dtype=BF16, device=x.device)
+        mean = torch.empty(T, dtype=F32, device=x.device)
+        rstd = torch.empty(T, dtype=F32, device=x.device)
+        K.ln_fwd(x2, w, b, y, mean, rstd, T, d, eps)
+        ctx.save_for_backward(x2, mean, rstd)
+        ctx.params = (w, b)
+        ctx.in_dtype = x.dtype
+        return y.view(*shape[:-1], d), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dpass):
+        if dy is None:
+            return dpass, None, None, None
+        x2, mean, rstd = ctx.saved_tensors
+        w, b = ctx.params
+        T, d = x2.shape
+        dres = None
+        if dpass is not None:
+            dres = _flat2(dpass.float().contiguous())
+        dx = torch.empty(T, d, dtype=F32, device=x2.device)
+        dw = _grad_slot(w) if w is not None else None
+        db = _grad_slot(b) if b is not None else None
+        K.ln_bwd(_flat2(dy.contiguous()), x2, mean, rstd, w, dx, dw, db, T, d, dres=dres)
+        _done(w, b)
+        dx = dx.view(*dy.shape[:-1], d)
+        return (dx if ctx.in_dtype == F32 else dx.to(ctx.in_dtype)), None, None, None
+
+
 def _packed3(a: Optional[torch.Tensor], b: Optional[torch.Tensor], c: Optional[torch.Tensor], n: int) -> bool:
     """``a|b|c`` are consecutive ``n``-column blocks of one row-major buffer (the arena QKV layout)."""
     if a is None or b is None or c is None:
@@ -437,14 +476,15 @@ class LinearFn(Function):
         W, b = ctx.params
         lead, Kd, N, out_kind, x_dtype = ctx.meta
         T = x2.shape[0]
-        if gy.dtype not in (F32, BF16):
-            gy = gy.to(BF16)
-        g2 = _aligned_rows(gy, T, N)
+        # one bf16 copy of an fp32 gradient (residual-stream outputs) serves both GEMMs and the bias sum;
+        # the skip connection keeps the fp32 gradient
+        gres = gy if out_kind == "resid" else None
+        g16 = gy if gy.dtype == BF16 else gy.to(BF16)
+        g2 = _aligned_rows(g16, T, N)
         ldg = g2.stride(0)
-        gf32 = g2.dtype == F32
         dx = None
         if ctx.needs_input_grad[0]:
-            amode = K.MODE_AF32 if gf32 else K.MODE_NN
+            amode = K.MODE_NN
             _, splits = K._tiling(T, Kd, N, True)
             if splits == 1:
                 dxb = torch.empty(T, Kd, dtype=BF16, device=g2.device)
@@ -458,7 +498,7 @@ class LinearFn(Function):
             dx = dx.view(*lead, Kd)
         gW = _grad_slot(W)
         if gW is not None:
-            mode = K.MODE_AKM | K.MODE_BKM | (K.MODE_BF32 if gf32 else 0)
+            mode = K.MODE_AKM | K.MODE_BKM
             gW2 = gW.reshape(Kd, N) if gW.is_contiguous() else gW
             assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
             gemm(x2, g2, gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode, epi=K.EPI_F32_ACC)
@@ -466,7 +506,6 @@ class LinearFn(Function):
         if gb is not None:
             K.colsum_accum(g2, ldg, gb, T, N)
         _done(W, b)
-        gres = gy if out_kind == "resid" else None
         return dx, None, None, None, None, gres, None
 
 
@@ -543,6 +582,8 @@ class CrossEntropyFn(Function):
         R, V = logits.shape
         ld = logits.stride(0)
         ldo = _pad8(V)
+        # fp32: autograd casts a gradient to its input's dtype anyway (the unembed backward makes the one
+        # bf16 copy its GEMMs read)
         buf = torch.empty(R, ldo, dtype=F32, device=logits.device)
         gs = g.reshape(1).float().contiguous()
         K.ce_bwd(logits, ld, lab, lse, gs, 1.0 / R, buf, ldo, R, V)
@@ -591,6 +632,10 @@ class HipOps(TorchOps):
 
     def layer_norm(self, x, w, b, eps):
         return LayerNormFn.apply(x, w, b, eps)
+
+    def layer_norm_fork(self, x, w, b, eps):
+        """``(LN(x), x_passthrough)``; use the passthrough for the skip connection."""
+        return LayerNormForkFn.apply(x, w, b, eps)
 
     # -- attention -------------------------------------------------------------------
     def qkv(self, x, W_Q, W_K, W_V, b_Q, b_K, b_V):

@@ -56,10 +56,14 @@ class NameMoverHead(nn.Module):
         self.d_vocab_out = d_vocab
         names = torch.as_tensor(names)
         self.register_buffer("names", names.clone(), persistent=False)
+        # vocab-sized membership table: a gather instead of torch.isin (sort-based, not graph-capturable)
+        table = torch.zeros(max(d_vocab, int(names.max()) + 1 if names.numel() else 1), dtype=torch.float32)
+        table[names.long()] = 1.0
+        self.register_buffer("name_table", table, persistent=False)
 
     def deltas(self, tokens: torch.Tensor, s_inhibition: torch.Tensor):
         """Per-position logit increments: +10 at each name token, -15 at each inhibited token."""
-        is_name = torch.isin(tokens, self.names.to(tokens.device)).float()
+        is_name = self.name_table.to(tokens.device)[tokens]
         inhibited = s_inhibition.ne(-1).float()
         return 10.0 * is_name, -15.0 * inhibited
 

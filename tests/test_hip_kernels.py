@@ -191,3 +191,71 @@ def test_flat_adam_matches_torch(K):
         opt2.step()
     for p1, p2 in zip(m1.parameters(), m2.parameters()):
         assert torch.allclose(p1, p2, atol=1e-5, rtol=1e-4)
+
+
+def test_add_bf16_and_vector_dgelu(K):
+    torch.manual_seed(8)
+    M, N = 300, 768
+    out = torch.randn(M, 800, device=dev)[:, :N]
+    base = torch.randn(M, N, device=dev)
+    y = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    b = torch.randn(N, device=dev)
+    K.add_bf16(out, out.stride(0), base, N, y, N, b, M, N)
+    assert torch.allclose(out, base + y.float() + b, atol=1e-6)
+    acc = torch.randn(M, 770, device=dev)  # odd width -> scalar path
+    ref = acc + torch.ones_like(acc)
+    K.add_bf16(acc, 770, acc, 770, torch.ones(M, 770, device=dev, dtype=torch.bfloat16), 770, None, M, 770)
+    assert torch.allclose(acc, ref)
+    from iit_amd.ops.torch_ops import gelu_new
+    pre = torch.randn(4096, 8, device=dev).to(torch.bfloat16)
+    g = torch.randn(4096, 8, device=dev).to(torch.bfloat16)
+    x = pre.float().requires_grad_(True)
+    gelu_new(x).backward(g.float())
+    out2 = torch.empty_like(pre)
+    K.dgelu(g, pre, out2)
+    assert rel_err(out2, x.grad) < 1e-2
+
+
+def test_dispatch_blas16_epilogues(K):
+    from iit_amd.ops import gemm_dispatch as gd
+    torch.manual_seed(9)
+    M, N, Kd = 512, 768, 1024
+    A, W = bf(torch.randn(M, Kd, device=dev)), bf(torch.randn(N, Kd, device=dev) / 32)
+    R, b = torch.randn(M, N, device=dev), torch.randn(N, device=dev)
+    C = torch.empty(M, N, device=dev)
+    gd._blas16(A, W, C, M, N, Kd, Kd, Kd, N, K.MODE_NN, K.EPI_F32_RESID, b, R, N)
+    assert rel_err(C, R + A.float() @ W.float().T + b) < 1e-2
+    G = torch.randn(Kd, N, device=dev)
+    X, Y = bf(torch.randn(M, Kd, device=dev)), bf(torch.randn(M, N, device=dev))
+    ref = G + X.float().T @ Y.float()
+    gd._blas16(X, Y, G, Kd, N, M, Kd, N, N, K.MODE_AKM | K.MODE_BKM, K.EPI_F32_ACC, None, None, 0)
+    assert rel_err(G, ref) < 1e-2
+
+
+@pytest.mark.parametrize("T,N,f32", [(4096, 3072, False), (4096, 768, True), (300, 130, False), (77, 36, True)])
+def test_colsum(K, T, N, f32):
+    torch.manual_seed(10)
+    x = torch.randn(T, N, device=dev)
+    x = x if f32 else bf(x)
+    out = torch.randn(N, device=dev)
+    ref = out + x.float().sum(0)
+    K.colsum_accum(x, N, out, T, N)
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_cross_entropy_bf16_grad_kernel(K):
+    torch.manual_seed(11)
+    R, V = 8, 1000
+    logits = torch.randn(R, V, device=dev) * 3
+    labels = torch.randint(0, V, (R,), device=dev)
+    loss = torch.empty(R, device=dev)
+    lse = torch.empty(R, device=dev)
+    amax = torch.empty(R, dtype=torch.long, device=dev)
+    K.ce_fwd(logits, V, labels, loss, lse, amax, R, V)
+    assert torch.allclose(lse, logits.logsumexp(-1), atol=1e-4)
+    assert torch.equal(amax, logits.argmax(-1))
+    out = torch.empty(R, 1008, dtype=torch.bfloat16, device=dev)
+    g = torch.ones(1, device=dev)
+    K.ce_bwd(logits, V, labels, lse, g, 1.0 / R, out, 1008, R, V)
+    ref = (logits.softmax(-1) - torch.nn.functional.one_hot(labels, V)) / R
+    assert rel_err(out[:, :V], ref) < 1e-2 and out[:, V:].abs().max() == 0
