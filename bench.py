@@ -59,12 +59,16 @@ def setup(args, dev):
     cfg = gpt2_config_dict()
     if args.model == "ioi-6l":
         cfg.update(ioi_cfg)
+    tiny = os.environ.get("IIT_BENCH_TINY") == "1"  # CPU rehearsal of the launch path only (tests)
+    if tiny:
+        cfg.update(n_layers=2, d_model=16, n_heads=2, d_head=8, d_mlp=32)
+        args.batch = min(args.batch, 16)
     cfg.update(device=str(dev), init_weights=True,
                dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     ll = HookedTransformer(cfg)
     if args.engine == "reference" or args.dtype == "fp32":
         ll.set_op_backend("torch")
-    ds, hl = make_ioi_dataset_and_hl(12000, ll, device=dev,
+    ds, hl = make_ioi_dataset_and_hl(512 if tiny else 12000, ll, device=dev,
                                      label_format="onehot" if args.engine == "reference" else "index")
     train_ds, test_ds = train_test_split(ds, test_size=0.2, random_state=42)
     train_set = IITDataset(train_ds, train_ds, seed=0, device=dev)
@@ -75,6 +79,7 @@ def setup(args, dev):
     pair = IOI_ModelPair(ll_model=ll, hl_model=hl, corr=make_ioi_corr(cfg["n_layers"]), training_args=training_args)
     pdist.broadcast_module(ll)
     opt = pair.make_optimizer(training_args["lr"])
+    pair.restrict_embedding_reduce(train_set)  # DP: reduce only W_E rows of dataset tokens (exact)
     loss_fn = pair.loss_fn
     loader = train_set.make_loader(args.batch, 0)
 
@@ -152,8 +157,10 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (offline IOI prompts, random-init weights)",
-            "config": {"model": "gpt2-small 12L/768d/12H (TL GPT-2 cfg, LNPre, gelu_new, V=50257)"
-                       if args.model == "gpt2-small" else "ioi-6l 6L/64d/4H",
+            "config": {"model": ("tiny-test 2L/16d (launch rehearsal, not a measurement)"
+                                 if os.environ.get("IIT_BENCH_TINY") == "1" else
+                                 "gpt2-small 12L/768d/12H (TL GPT-2 cfg, LNPre, gelu_new, V=50257)"
+                                 if args.model == "gpt2-small" else "ioi-6l 6L/64d/4H"),
                        "global_batch": global_batch, "seq_len": int(train_set.base_data.dataset.prompts.shape[1] - 1),
                        "parallelism": f"dp{world}", "engine": args.engine,
                        "graphs": bool(getattr(step_fn, "enabled", False))},

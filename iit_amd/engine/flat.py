@@ -112,14 +112,20 @@ class FlatParams:
         self.grad.zero_()
         self.rebind_grads()
 
-    def rebind_grads(self) -> None:
-        """Re-attach ``.grad`` views (after someone set them to None / replaced them)."""
+    def rebind_grads(self, zero_missing: bool = False) -> None:
+        """Re-attach ``.grad`` views (after someone set them to None / replaced them).
+
+        A replaced gradient is copied into its slot; with ``zero_missing`` a ``None``
+        gradient (``optimizer.zero_grad(set_to_none=True)``) gets its slot zeroed, so
+        the arena equals the gradients autograd is about to accumulate."""
         for p, fn in zip(self.params, self._view_fns):
             g = p.grad
             view = fn(self.grad)
             if g is None or g.data_ptr() != view.data_ptr() or g.stride() != view.stride():
                 if g is not None:
                     view.copy_(g)
+                elif zero_missing:
+                    view.zero_()
                 p.grad = view
 
     def grad_view(self, p: torch.Tensor) -> torch.Tensor:

@@ -22,8 +22,13 @@ semantics (RNG stream, phase order, 3 optimizer steps per IOI batch) are the
 pair's own ``run_train_step`` -- this class only swaps the phase executor.
 
 Batches whose shapes differ from the captured ones (e.g. a short final batch)
-run eagerly.  Data-parallel runs capture too only with ``IIT_GRAPHS_DP=1``
-(RCCL collectives inside captured graphs).
+run eagerly.
+
+Data parallel: collectives are never captured.  Each phase becomes two graphs
+around an eager gradient all-reduce -- ``[forward + backward]`` -> bucketed
+RCCL all-reduce of the gradient arena -> ``[clip + Adam]`` -- so every rank issues
+the identical collective sequence whatever gets captured, and the launch-bound
+compute still runs as replays.  (``IIT_GRAPHS_DP=0`` keeps DP runs fully eager.)
 """
 from __future__ import annotations
 
@@ -53,13 +58,14 @@ class GraphedTrainStep:
         self.optimizer = optimizer
         self.loss_fn = loss_fn
         self.warmup = warmup
+        ws = torch.distributed.get_world_size() if (torch.distributed.is_available()
+                                                   and torch.distributed.is_initialized()) else 1
         if enabled is None:
             enabled = torch.cuda.is_available()
-            ws = torch.distributed.get_world_size() if (torch.distributed.is_available()
-                                                       and torch.distributed.is_initialized()) else 1
-            if ws > 1 and os.environ.get("IIT_GRAPHS_DP", "0") != "1":
+            if ws > 1 and os.environ.get("IIT_GRAPHS_DP", "1") == "0":
                 enabled = False
         self.enabled = enabled
+        self.split = ws > 1  # DP: graphs around the (eager) gradient all-reduce
         self.graphs: Dict[Tuple, Tuple[torch.cuda.CUDAGraph, object]] = {}
         self.seen: Dict[Tuple, int] = {}
         self.pool = torch.cuda.graph_pool_handle() if enabled else None
@@ -95,10 +101,75 @@ class GraphedTrainStep:
         step_fn(loss, optimizer)
         return _detach_out(out)
 
+    def _splittable(self, step_fn) -> bool:
+        from ..model_pairs.iit_behavior_model_pair import IITBehaviorModelPair
+        return getattr(step_fn, "__func__", None) is IITBehaviorModelPair.step_on_loss
+
+    def _run_split_phase(self, full, key, compute_loss, optimizer):
+        """DP phase: graph(forward + backward) -> eager all-reduce -> graph(clip + Adam)."""
+        pair = self.pair
+        reducer = getattr(pair, "_reducer", None)
+
+        def fwd_bwd():
+            out = compute_loss()
+            loss = out[0] if isinstance(out, tuple) else out
+            optimizer.zero_grad()
+            if reducer is not None:
+                reducer.paused = True  # no collective may be issued from inside a capture
+            try:
+                loss.backward()
+            finally:
+                if reducer is not None:
+                    reducer.paused = False
+            return _detach_out(out)
+
+        def update():
+            pair.clip_grad_fn(optimizer)
+            pair.optimizer_step(optimizer)
+
+        ent = self.graphs.get(full)
+        if ent is None:
+            n = self.seen.get(full, 0)
+            if n < self.warmup or full in self.failed:
+                self.seen[full] = n + 1
+                out = fwd_bwd()
+                if reducer is not None:
+                    reducer.reduce_all()
+                update()
+                return out
+            ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(ga, pool=self.pool):
+                    static_out = fwd_bwd()
+                with torch.cuda.graph(gb, pool=self.pool):
+                    update()
+            except Exception as e:
+                self.failed[full] = repr(e)
+                print(f"[iit graphs] DP phase {key} not captured ({type(e).__name__}: {str(e)[:160]}); eager")
+                torch.cuda.synchronize()
+                out = fwd_bwd()
+                if reducer is not None:
+                    reducer.reduce_all()
+                update()
+                return out
+            ent = self.graphs[full] = ((ga, gb), static_out)
+            self.captures += 1
+        (ga, gb), static_out = ent
+        ga.replay()
+        if reducer is not None:
+            reducer.reduce_all()
+        gb.replay()
+        self.replays += 1
+        return _clone_out(static_out)
+
     def _run_phase(self, key, compute_loss, optimizer, step_fn):
         full = (key, self._sig)
         if not self.enabled or self._current_eager:
             return self._eager(compute_loss, optimizer, step_fn)
+        if self.split:
+            if not self._splittable(step_fn):
+                return self._eager(compute_loss, optimizer, step_fn)
+            return self._run_split_phase(full, key, compute_loss, optimizer)
         ent = self.graphs.get(full)
         if ent is None:
             n = self.seen.get(full, 0)

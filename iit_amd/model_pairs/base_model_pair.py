@@ -54,6 +54,18 @@ def _underlying_module(model) -> torch.nn.Module:
     return model if isinstance(model, torch.nn.Module) else getattr(model, "model")
 
 
+def dataset_token_ids(dataset) -> Optional[Tensor]:
+    """Distinct input token ids of a (possibly nested / subset) IOI-style dataset, or None."""
+    seen = set()
+    while dataset is not None and id(dataset) not in seen:
+        seen.add(id(dataset))
+        fn = getattr(dataset, "token_ids", None)
+        if callable(fn):
+            return fn()
+        dataset = getattr(dataset, "base_data", None) or getattr(dataset, "dataset", None)
+    return None
+
+
 def _ll_nodes_of(corr, hl_node) -> List[LLNode]:
     v = corr[hl_node]
     if isinstance(v, LLNode):
@@ -258,6 +270,18 @@ class BaseModelPair(ABC):
             self._reducer = GradReducer(flat, bucket_mb=self.training_args.get("bucket_mb", 64.0),
                                         overlap=self.training_args.get("overlap_allreduce", True))
 
+    def restrict_embedding_reduce(self, dataset) -> None:
+        """Data parallel: all-reduce only the embedding rows of tokens the dataset contains (exact: no
+        other row can receive gradient).  No-op without a reducer or a token-id source."""
+        reducer = getattr(self, "_reducer", None)
+        module = self._ll_module()
+        embed = getattr(getattr(module, "embed", None), "W_E", None)
+        if reducer is None or embed is None or id(embed) not in reducer.flat.index:
+            return
+        ids = dataset_token_ids(dataset)
+        if ids is not None:
+            reducer.set_row_subset(embed, ids)
+
     def backward(self, loss: Tensor) -> None:
         """``loss.backward()`` + data-parallel gradient averaging + reference grad semantics."""
         reducer = getattr(self, "_reducer", None)
@@ -322,6 +346,7 @@ class BaseModelPair(ABC):
                                                       training_args["num_workers"])
         early_stop = training_args["early_stop"]
         optimizer = self.make_optimizer(training_args["lr"])
+        self.restrict_embedding_reduce(train_set)
         loss_fn = self.loss_fn
         scheduler_cls = training_args.get("lr_scheduler", None)
         lr_scheduler = None

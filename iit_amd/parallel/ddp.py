@@ -22,6 +22,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from ..engine import grad_hooks
 from ..engine.flat import FlatParams
 from . import dist as pdist
 
@@ -45,18 +46,34 @@ class GradReducer:
                     break
         self._pending = list(self._bucket_count)
         self._launched = [False] * len(self.buckets)
+        self._ready = [False] * len(flat.params)
         self._works = []
         self._hooks = []
+        self._listener = None
+        self._subsets = {}
+        self.paused = False  # True while a graph-captured backward runs (reduction happens after it)
         if self.overlap:
             for i, p in enumerate(flat.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+            # gradients the fused HIP kernels write directly (no autograd accumulation) report here
+            index = {id(p): i for i, p in enumerate(flat.params)}
+            self._listener = grad_hooks.add_listener(
+                lambda p, _index=index: self._mark_ready(_index[id(p)]) if id(p) in _index else None)
+
+    def _mark_ready(self, i: int) -> None:
+        # each parameter's gradient is final when first reported within a backward (the engine writes every
+        # weight gradient exactly once per backward); repeats are ignored
+        if self.paused or self._ready[i]:
+            return
+        self._ready[i] = True
+        b = self._param_bucket[i]
+        self._pending[b] -= 1
+        if self._pending[b] == 0:
+            self._launch(b)
 
     def _make_hook(self, i: int):
         def hook(_p, _i=i):
-            b = self._param_bucket[_i]
-            self._pending[b] -= 1
-            if self._pending[b] == 0:
-                self._launch(b)
+            self._mark_ready(_i)
         return hook
 
     def _launch(self, b: int):
@@ -64,14 +81,33 @@ class GradReducer:
             return
         self._launched[b] = True
         s, e = self.buckets[b]
-        buf = self.flat.grad[s:e]
         op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
-        self._works.append((dist.all_reduce(buf, op=op, async_op=True), buf))
+        # a parameter with a row subset is reduced compactly; the rest of the bucket in contiguous pieces
+        pieces, cur = [], s
+        for i, (o, n, width, rows) in sorted(self._subsets.items(), key=lambda kv: kv[1][0]):
+            if o >= s and o + n <= e:
+                if o > cur:
+                    pieces.append(("dense", cur, o))
+                pieces.append(("rows", o, n, width, rows))
+                cur = o + n
+        if cur < e:
+            pieces.append(("dense", cur, e))
+        for pc in pieces:
+            if pc[0] == "dense":
+                buf = self.flat.grad[pc[1]:pc[2]]
+                self._works.append((dist.all_reduce(buf, op=op, async_op=True), buf, None))
+            else:
+                _, o, n, width, rows = pc
+                full = self.flat.grad[o:o + n].view(-1, width)
+                buf = full.index_select(0, rows)
+                self._works.append((dist.all_reduce(buf, op=op, async_op=True), buf, (full, rows)))
 
     def start(self):
-        """Call before ``backward``."""
+        """Call before ``backward``: every gradient must live in the arena the buckets reduce."""
+        self.flat.rebind_grads(zero_missing=True)
         self._pending = list(self._bucket_count)
         self._launched = [False] * len(self.buckets)
+        self._ready = [False] * len(self.flat.params)
         self._works = []
 
     def finish(self):
@@ -81,14 +117,36 @@ class GradReducer:
         for b in range(len(self.buckets)):
             if not self._launched[b]:
                 self._launch(b)
-        for work, buf in self._works:
+        for work, buf, scatter in self._works:
             work.wait()
             if not self._use_avg:
                 buf.div_(self.world)
+            if scatter is not None:
+                full, rows = scatter
+                full.index_copy_(0, rows, buf)
         self._works = []
         self.flat.rebind_grads()
+
+    def reduce_all(self) -> None:
+        """Non-overlapped reduction of the whole arena (the graph-captured step's collective phase)."""
+        if not self.enabled:
+            return
+        self.start()
+        self.finish()
+
+    def set_row_subset(self, param, rows: torch.Tensor) -> None:
+        """Reduce only ``rows`` of ``param``'s gradient (e.g. the embedding rows of the tokens the dataset
+        contains; every other row is zero on every rank).  Exact, and ~25 % less traffic for GPT-2's W_E."""
+        i = self.flat.index[id(param)]
+        o = self.flat.offset_of(param)
+        n = param.numel()
+        width = param.shape[-1]
+        self._subsets[i] = (o, n, width, rows.to(self.flat.grad.device).long().unique())
 
     def remove(self):
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        if self._listener is not None:
+            grad_hooks.remove_listener(self._listener)
+            self._listener = None

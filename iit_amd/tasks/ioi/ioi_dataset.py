@@ -111,6 +111,10 @@ class IOIDatasetWrapper(IOIDataset):
         p = self.prompts[idx]
         return p[:-1], self._labels(p[1:]), self.io_ids[idx:idx + 1]
 
+    def token_ids(self) -> torch.Tensor:
+        """Distinct input token ids (the only embedding rows that can receive gradient)."""
+        return torch.unique(self.prompts[:, :-1])
+
     def gather(self, idx: torch.Tensor):
         """Batched ``__getitem__``: one device gather for a whole batch of indices."""
         p = self.prompts.index_select(0, idx.to(self.prompts.device))

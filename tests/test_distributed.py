@@ -1,0 +1,142 @@
+"""T3: data parallelism without a cluster -- gloo, world_size 2, on CPU.
+
+* DP(2) x (B/2) == 1 x B: same losses and the same weights after several Strict-IIT
+  steps (3 optimizer steps each, global-norm clip after the bucketed all-reduce);
+* every rank samples the same HL / strict node sequence (identically seeded RNG);
+* epoch metrics are averaged across ranks;
+* ``bench.py`` runs under ``torch.distributed.run`` with the driver's flags.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _make(global_batch: int):
+    from iit_amd.data.iit_dataset import IITDataset
+    from iit_amd.model_pairs import IOI_ModelPair
+    from iit_amd.models.config import gpt2_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.tasks.ioi import make_ioi_corr, make_ioi_dataset_and_hl
+    cfg = gpt2_config_dict()
+    cfg.update(n_layers=2, d_model=16, n_heads=2, d_head=8, d_mlp=32, device="cpu")
+    torch.manual_seed(0)
+    ll = HookedTransformer(cfg)
+    ds, hl = make_ioi_dataset_and_hl(256, ll, device="cpu")
+    train = IITDataset(ds, ds, seed=0, device="cpu")
+    pair = IOI_ModelPair(hl, ll, make_ioi_corr(2), training_args={
+        "batch_size": global_batch, "lr": 1e-3, "lr_scheduler": None, "strict_weight": 0.4, "bucket_mb": 0.05})
+    return pair, train
+
+
+def _train(pair, train, per_rank_batch, steps=4):
+    opt = pair.make_optimizer(1e-3)
+    torch.manual_seed(5)
+    loader = train.make_loader(per_rank_batch, 0)
+    losses, nodes = [], []
+    orig = pair.sample_hl_name
+    pair.sample_hl_name = lambda: (lambda n: (nodes.append(n.name), n)[1])(orig())
+    for i, (base, abl) in enumerate(loader):
+        if i >= steps:
+            break
+        out = pair.run_train_step(base, abl, pair.loss_fn, opt)
+        losses.append([float(out[k]) for k in sorted(out)])
+    return losses, nodes
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from iit_amd.parallel import dist as pdist
+    pdist.init_distributed("gloo")
+    torch.set_num_threads(2)
+    pair, train = _make(64)
+    pdist.broadcast_module(pair.ll_model)
+    losses, nodes = _train(pair, train, per_rank_batch=32)
+    # metric all-reduce: each rank contributes its own value; the result is the mean
+    from iit_amd.core.metric import MetricStore, MetricStoreCollection, MetricType
+    mc = MetricStoreCollection([MetricStore("val/IIA", MetricType.ACCURACY)])
+    mc.update({"val/IIA": float(rank)})
+    pair._reduce_metrics(mc)
+    torch.save({"losses": losses, "nodes": nodes, "metric": mc.metrics[0].get_value(),
+                "params": {n: p.detach().clone() for n, p in pair.ll_model.named_parameters()}},
+               os.path.join(out_dir, f"rank{rank}.pt"))
+    pdist.destroy()
+
+
+def test_dp2_equals_single_process(tmp_path):
+    pair, train = _make(64)
+    ref_losses, ref_nodes = _train(pair, train, per_rank_batch=64)
+    ref_params = {n: p.detach().clone() for n, p in pair.ll_model.named_parameters()}
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r = [torch.load(tmp_path / f"rank{i}.pt", weights_only=True) for i in range(2)]
+    assert r[0]["nodes"] == r[1]["nodes"] == ref_nodes
+    for i in range(2):
+        for n, p in ref_params.items():
+            assert torch.allclose(r[i]["params"][n], p, atol=2e-5, rtol=1e-4), (i, n)
+    # per-rank losses are shard means; their average is the global-batch loss
+    avg = torch.tensor(r[0]["losses"]) / 2 + torch.tensor(r[1]["losses"]) / 2
+    assert torch.allclose(avg, torch.tensor(ref_losses), atol=1e-4)
+    assert r[0]["metric"] == pytest.approx(50.0) and r[1]["metric"] == pytest.approx(50.0)  # mean of 0, 100 (x100)
+
+
+def test_bench_under_torchrun_gloo(tmp_path):
+    """The driver's multi-GPU launch line, rehearsed on CPU with 2 gloo ranks and a tiny config."""
+    env = dict(os.environ, IIT_BENCH_TINY="1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+           "2", "--warmup", "1"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(tmp_path))
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["value"] > 0 and rec["scaling"] == "weak"
+
+
+def _worker_subset(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from iit_amd.parallel import dist as pdist
+    pdist.init_distributed("gloo")
+    torch.set_num_threads(2)
+    pair, train = _make(64)
+    pdist.broadcast_module(pair.ll_model)
+    opt = pair.make_optimizer(1e-3)
+    pair.restrict_embedding_reduce(train)
+    assert pair._reducer._subsets, "embedding row subset not installed"
+    torch.manual_seed(5)
+    for i, (base, abl) in enumerate(train.make_loader(32, 0)):
+        if i >= 3:
+            break
+        pair.run_train_step(base, abl, pair.loss_fn, opt)
+    torch.save({n: p.detach().clone() for n, p in pair.ll_model.named_parameters()},
+               os.path.join(out_dir, f"subset{rank}.pt"))
+    pdist.destroy()
+
+
+def test_dp2_embedding_row_subset_reduce_is_exact(tmp_path):
+    pair, train = _make(64)
+    _train(pair, train, per_rank_batch=64, steps=3)
+    ref = {n: p.detach().clone() for n, p in pair.ll_model.named_parameters()}
+    mp.spawn(_worker_subset, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for i in range(2):
+        got = torch.load(tmp_path / f"subset{i}.pt", weights_only=True)
+        for n, p in ref.items():
+            assert torch.allclose(got[n], p, atol=2e-5, rtol=1e-4), (i, n)

@@ -65,3 +65,24 @@ def test_prime_captures_all_phase_keys_and_keeps_rng():
     n = g.prime(base, abl)
     assert n == len(pair.corr) + len(pair.nodes_not_in_circuit) + 1, g.failed
     assert pair.rng.random() == before
+
+
+def test_split_graphs_for_data_parallel_match_eager():
+    """The DP form (graph[fwd+bwd] -> eager all-reduce -> graph[clip+Adam]) on one GPU (no-op reduce)."""
+    from iit_amd.engine.graphs import GraphedTrainStep
+    le1, _ = _run("eager")
+    le2, _ = _run("eager")
+    pair, opt, train = _setup()
+    torch.manual_seed(1)
+    batches = [b for _, b in zip(range(10), train.make_loader(64, 0))]
+    g = GraphedTrainStep(pair, opt, pair.loss_fn)
+    g.split = True
+    losses = []
+    for base, abl in batches * 3:
+        out = g(base, abl, pair.loss_fn, opt)
+        losses.append(torch.stack([out[k] for k in sorted(out)]))
+    ls = torch.stack(losses).cpu()
+    assert g.captures > 0 and not g.failed, g.failed
+    noise = (le1 - le2).abs().max().item()
+    assert torch.allclose(le1[:4], ls[:4], rtol=1e-3, atol=1e-3)
+    assert (le1 - ls).abs().max().item() <= 3 * noise + 5e-3
