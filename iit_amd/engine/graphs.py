@@ -69,6 +69,9 @@ class GraphedTrainStep:
         self.graphs: Dict[Tuple, Tuple[torch.cuda.CUDAGraph, object]] = {}
         self.seen: Dict[Tuple, int] = {}
         self.pool = torch.cuda.graph_pool_handle() if enabled else None
+        if enabled:
+            from ..ops.gemm_dispatch import select_graph_safe_blas
+            select_graph_safe_blas()
         self._static = None
         self._sig = None
         self.captures = 0

@@ -1,15 +1,18 @@
 """GEMM dispatch: hand-written MFMA kernel (fused epilogues) vs hipBLASLt, autotuned per shape.
 
-Every GEMM of the engine goes through :func:`gemm`.  Two implementations:
+Every GEMM of the engine goes through :func:`gemm`.  Implementations:
 
 * ``hip``  - ``csrc/gemm.hip``: MFMA 16x16x32 bf16 with the epilogue fused
   (bias, packed-QKV bias, fp32 residual add, bias+gelu_new, dgelu, fp32
   accumulate into the gradient arena, head-blocked QKV gradient scatter);
 * ``blas`` - hipBLASLt through ``torch.mm`` / ``torch.addmm`` for the product and
-  separate elementwise passes for whatever the BLAS epilogue cannot express.
+  separate elementwise passes for whatever the BLAS epilogue cannot express;
+* ``blas16`` - for fp32 residual / accumulate epilogues: bf16-output library GEMM
+  + one fused ``add_bf16`` pass.
 
-``IIT_GEMM=auto`` (default) times both once per (shape, layout, epilogue) outside
-graph capture and keeps the faster; ``IIT_GEMM=hip`` / ``blas`` force one.  The
+``IIT_GEMM=auto`` (default) times every candidate once per (shape, layout,
+epilogue) -- as a captured graph of back-to-back calls, i.e. device time only --
+outside graph capture and keeps the fastest; ``IIT_GEMM=hip|blas|blas16`` force one.  The
 decisions are recorded in :data:`DECISIONS` (``report()`` prints them) so profiles
 can say which GEMMs ran on hand-written MFMA code.
 """
@@ -24,9 +27,29 @@ import torch.nn.functional as F
 from . import hip_kernels as K
 
 POLICY = os.environ.get("IIT_GEMM", "auto")
-DECISIONS: Dict[Tuple, Tuple[str, float, float]] = {}
+DECISIONS: Dict[Tuple, Tuple[str, Dict[str, float]]] = {}
 BF16, F32 = torch.bfloat16, torch.float32
 _BLAS_OK = {}
+_BLAS_SELECTED = False
+
+
+def select_graph_safe_blas() -> None:
+    """Optionally route torch's library GEMMs through rocBLAS instead of hipBLASLt (``IIT_BLAS=rocblas``).
+
+    Both replay correctly from captured HIP graphs in our tests (``tests/test_graphs.py``,
+    ``scripts/diag_graphs.py``: graph and eager losses agree phase by phase until fp32-atomic
+    noise, amplified by Adam, makes any two runs -- eager or not -- drift apart); hipBLASLt is
+    ~2 % faster on the IOI step, so it stays the default."""
+    global _BLAS_SELECTED
+    if _BLAS_SELECTED or not torch.cuda.is_available():
+        return
+    _BLAS_SELECTED = True
+    if os.environ.get("IIT_BLAS", "lt") != "rocblas":
+        return
+    try:
+        torch.backends.cuda.preferred_blas_library("cublas")
+    except Exception as e:  # pragma: no cover - older torch
+        print(f"[iit] could not select rocBLAS ({e})")
 
 
 def _as(t, rows, cols, ld, dtype=None):
@@ -190,6 +213,8 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     ``blas_bias``: optional ready-made bf16 bias row (e.g. a view of the arena's bf16 mirror) for the
     library path, saving its per-call concatenate/cast."""
     Kd = K
+    if not _BLAS_SELECTED:
+        select_graph_safe_blas()
     hip_call = lambda c=C, c2=C2, c3=C3: K_.gemm(  # noqa: E731
         A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=c2, C3=c3, bias0=bias0,
         bias1=bias1, bias2=bias2, resid=resid, ldr=ldr, aux=aux, ldc2=ldc2, bias_cols=bias_cols, qkv=qkv,

@@ -75,3 +75,16 @@ def test_blas_residual_gelu_acc_store():
     st = torch.empty(M, N)
     _call(A, B, st, M, N, Kd, K.MODE_NN, K.EPI_F32_STORE, bias0=bias)
     assert torch.allclose(st, base + bias, atol=0.05, rtol=0.02)
+
+
+def test_gemm_entry_point_forced_blas_on_cpu(monkeypatch):
+    """The public entry point (policy plumbing, candidate table) runs on CPU with the library path forced."""
+    monkeypatch.setattr(gd, "POLICY", "blas")
+    torch.manual_seed(2)
+    M, N, Kd = 8, 12, 16
+    A = torch.randn(M, Kd).to(BF)
+    B = torch.randn(N, Kd).to(BF)
+    C = torch.empty(M, N, dtype=BF)
+    gd.gemm(A, B, C, M=M, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=N, mode=K.MODE_NN, epi=K.EPI_BF16)
+    assert torch.allclose(C.float(), A.float() @ B.float().T, atol=0.1, rtol=0.02)
+    assert isinstance(gd.DECISIONS, dict) and "library fast paths" in gd.report()

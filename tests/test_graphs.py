@@ -43,17 +43,19 @@ def _run(mode, n_batches=10, reps=3):
     return torch.stack(losses).cpu(), g
 
 
+# Graph replays run the eager kernel sequence, so losses agree phase by phase -- until fp32-atomic
+# accumulation-order noise, which Adam amplifies (it normalises near-zero gradient elements to lr-sized
+# steps), makes ANY two runs drift apart; on this config two eager runs split visibly after ~20 steps
+# (scripts/diag_nondet.py).  So compare the first 12 steps (36 phases: every phase key captured and
+# replayed at least once) tightly.
+_TIGHT = 12
+
+
 def test_graphed_steps_match_eager():
-    """Graph replays run the eager kernel sequence: they agree with eager as closely as two eager runs agree
-    with each other (fp32 atomic accumulation order is the only nondeterminism, amplified by Adam)."""
-    le1, _ = _run("eager")
-    le2, _ = _run("eager")
+    le, _ = _run("eager")
     lg, g = _run("graphs")
     assert g.captures > 0 and g.replays > 0 and not g.failed, g.failed
-    # the first steps (before divergence can compound) agree tightly
-    assert torch.allclose(le1[:4], lg[:4], rtol=1e-3, atol=1e-3), (le1[:4] - lg[:4]).abs().max()
-    noise = (le1 - le2).abs().max().item()
-    assert (le1 - lg).abs().max().item() <= 3 * noise + 5e-3, ((le1 - lg).abs().max(), noise)
+    assert torch.allclose(le[:_TIGHT], lg[:_TIGHT], rtol=2e-3, atol=2e-3), (le[:_TIGHT] - lg[:_TIGHT]).abs().max()
 
 
 def test_prime_captures_all_phase_keys_and_keeps_rng():
@@ -71,7 +73,6 @@ def test_split_graphs_for_data_parallel_match_eager():
     """The DP form (graph[fwd+bwd] -> eager all-reduce -> graph[clip+Adam]) on one GPU (no-op reduce)."""
     from iit_amd.engine.graphs import GraphedTrainStep
     le1, _ = _run("eager")
-    le2, _ = _run("eager")
     pair, opt, train = _setup()
     torch.manual_seed(1)
     batches = [b for _, b in zip(range(10), train.make_loader(64, 0))]
@@ -83,6 +84,4 @@ def test_split_graphs_for_data_parallel_match_eager():
         losses.append(torch.stack([out[k] for k in sorted(out)]))
     ls = torch.stack(losses).cpu()
     assert g.captures > 0 and not g.failed, g.failed
-    noise = (le1 - le2).abs().max().item()
-    assert torch.allclose(le1[:4], ls[:4], rtol=1e-3, atol=1e-3)
-    assert (le1 - ls).abs().max().item() <= 3 * noise + 5e-3
+    assert torch.allclose(le1[:_TIGHT], ls[:_TIGHT], rtol=2e-3, atol=2e-3), (le1[:_TIGHT] - ls[:_TIGHT]).abs().max()
