@@ -115,22 +115,32 @@ class Unembed(nn.Module):
 
 
 class LayerNormSite(nn.Module):
-    """``LN`` (affine) or ``LNPre`` (no params) with TL hook names."""
+    """``LN`` (affine) / ``LNPre`` (no params) or ``RMS`` (weight only) / ``RMSPre`` with TL hook names."""
 
-    def __init__(self, cfg: HookedTransformerConfig, affine: bool):
+    def __init__(self, cfg: HookedTransformerConfig, affine: bool, rms: bool = False):
         super().__init__()
         self.eps = cfg.eps
-        if affine:
-            self.w = nn.Parameter(torch.ones(cfg.d_model))
-            self.b = nn.Parameter(torch.zeros(cfg.d_model))
-        else:
-            self.w = None
-            self.b = None
+        self.rms = rms
+        self.w = nn.Parameter(torch.ones(cfg.d_model)) if affine else None
+        self.b = nn.Parameter(torch.zeros(cfg.d_model)) if (affine and not rms) else None
         self.hook_scale = HookPoint()
         self.hook_normalized = HookPoint()
 
+    @staticmethod
+    def make(cfg: HookedTransformerConfig, kind: Optional[str]) -> Optional["LayerNormSite"]:
+        if kind is None:
+            return None
+        if kind not in ("LN", "LNPre", "RMS", "RMSPre"):
+            raise NotImplementedError(f"normalization_type {kind}")
+        return LayerNormSite(cfg, affine=kind in ("LN", "RMS"), rms=kind in ("RMS", "RMSPre"))
+
     def run(self, x, run: _Run):
-        if run.live(self.hook_scale) or run.live(self.hook_normalized) or not run.ops.fused:
+        live = run.live(self.hook_scale) or run.live(self.hook_normalized)
+        if self.rms:
+            hs = (lambda t: run.site(self.hook_scale, t)) if live else None
+            hn = (lambda t: run.site(self.hook_normalized, t)) if live else None
+            return TorchOps.rms_norm(run.ops, x, self.w, self.eps, hook_scale=hs, hook_normalized=hn)
+        if live or not run.ops.fused:
             return TorchOps.layer_norm(
                 run.ops, x, self.w, self.b, self.eps,
                 hook_scale=lambda t: run.site(self.hook_scale, t),
@@ -139,20 +149,51 @@ class LayerNormSite(nn.Module):
         return run.ops.layer_norm(x, self.w, self.b, self.eps)
 
 
+def rotary_tables(cfg: HookedTransformerConfig):
+    """TL rotary sin/cos ``[n_ctx, rotary_dim]`` (angles repeated per pair layout)."""
+    rd = cfg.rotary_dim or cfg.d_head
+    pos = torch.arange(cfg.n_ctx, dtype=torch.float64)
+    freq = cfg.rotary_base ** (-torch.arange(0, rd, 2, dtype=torch.float64) / rd)
+    ang = pos[:, None] * freq[None, :]
+    ang = ang.repeat_interleave(2, dim=-1) if cfg.rotary_adjacent_pairs else torch.cat([ang, ang], dim=-1)
+    return ang.sin().float(), ang.cos().float()
+
+
 class Attention(nn.Module):
     def __init__(self, cfg: HookedTransformerConfig, layer: int):
         super().__init__()
         H, d, dh = cfg.n_heads, cfg.d_model, cfg.d_head
         self.cfg = cfg
         self.layer = layer
+        n_kv = cfg.n_key_value_heads or H
+        self.n_kv = n_kv
+        self.gqa = n_kv != H  # grouped-query attention (TL ``_W_K`` / ``_W_V`` naming)
         self.W_Q = nn.Parameter(torch.empty(H, d, dh))
-        self.W_K = nn.Parameter(torch.empty(H, d, dh))
-        self.W_V = nn.Parameter(torch.empty(H, d, dh))
+        if self.gqa:
+            if H % n_kv:
+                raise ValueError("n_heads must be a multiple of n_key_value_heads")
+            self._W_K = nn.Parameter(torch.empty(n_kv, d, dh))
+            self._W_V = nn.Parameter(torch.empty(n_kv, d, dh))
+        else:
+            self.W_K = nn.Parameter(torch.empty(H, d, dh))
+            self.W_V = nn.Parameter(torch.empty(H, d, dh))
         self.W_O = nn.Parameter(torch.empty(H, dh, d))
         self.b_Q = nn.Parameter(torch.zeros(H, dh))
-        self.b_K = nn.Parameter(torch.zeros(H, dh))
-        self.b_V = nn.Parameter(torch.zeros(H, dh))
+        if self.gqa:
+            self._b_K = nn.Parameter(torch.zeros(n_kv, dh))
+            self._b_V = nn.Parameter(torch.zeros(n_kv, dh))
+        else:
+            self.b_K = nn.Parameter(torch.zeros(H, dh))
+            self.b_V = nn.Parameter(torch.zeros(H, dh))
         self.b_O = nn.Parameter(torch.zeros(d))
+        self.rotary = cfg.positional_embedding_type == "rotary"
+        if self.rotary:
+            self.rotary_dim = cfg.rotary_dim or dh
+            sin, cos = rotary_tables(cfg)
+            self.register_buffer("rotary_sin", sin)
+            self.register_buffer("rotary_cos", cos)
+            self.hook_rot_q = HookPoint()
+            self.hook_rot_k = HookPoint()
         causal = torch.tril(torch.ones(cfg.n_ctx, cfg.n_ctx, dtype=torch.bool))
         self.register_buffer("mask", causal)
         self.register_buffer("IGNORE", torch.tensor(float("-inf")))
@@ -167,16 +208,47 @@ class Attention(nn.Module):
         self.hook_pattern = HookPoint()
         self.hook_result = HookPoint()
 
+    # grouped-query attention: TL exposes the expanded per-query-head views
+    def _kv(self, name: str):
+        p = self._parameters.get(name)
+        if p is not None:
+            return p
+        kv = self._parameters.get("_" + name)
+        if kv is None:  # (during registration) -> AttributeError keeps hasattr() honest
+            raise AttributeError(name)
+        return kv.repeat_interleave(self.cfg.n_heads // self.n_kv, dim=0)
+
+    W_K = property(lambda self: self._kv("W_K"))
+    W_V = property(lambda self: self._kv("W_V"))
+    b_K = property(lambda self: self._kv("b_K"))
+    b_V = property(lambda self: self._kv("b_V"))
+
+    def kv_params(self):
+        """(W_K, W_V, b_K, b_V) as stored (kv heads for GQA)."""
+        if self.gqa:
+            return self._W_K, self._W_V, self._b_K, self._b_V
+        return self.W_K, self.W_V, self.b_K, self.b_V
+
     def inner_live(self, run: _Run) -> bool:
         return any(run.live(h) for h in (self.hook_q, self.hook_k, self.hook_v, self.hook_attn_scores,
                                          self.hook_pattern))
 
     def compute_z(self, x, run: _Run):
         ops = run.ops
-        q, k, v = ops.qkv(x, self.W_Q, self.W_K, self.W_V, self.b_Q, self.b_K, self.b_V)
+        Wk, Wv, bk, bv = self.kv_params()
+        q, k, v = ops.qkv(x, self.W_Q, Wk, Wv, self.b_Q, bk, bv)
         q = run.site(self.hook_q, q)
         k = run.site(self.hook_k, k)
         v = run.site(self.hook_v, v)
+        if self.rotary:
+            q = run.site(self.hook_rot_q, TorchOps.rotary(ops, q, self.rotary_cos, self.rotary_sin, self.rotary_dim,
+                                                          self.cfg.rotary_adjacent_pairs))
+            k = run.site(self.hook_rot_k, TorchOps.rotary(ops, k, self.rotary_cos, self.rotary_sin, self.rotary_dim,
+                                                          self.cfg.rotary_adjacent_pairs))
+        if self.gqa:
+            rep = self.cfg.n_heads // self.n_kv
+            k = k.repeat_interleave(rep, dim=2)
+            v = v.repeat_interleave(rep, dim=2)
         causal = self.cfg.attention_dir == "causal"
         z_spl = run.plan.splice.get(self.hook_z.name) if run.plan is not None else None
         if ops.fused and not (run.live(self.hook_attn_scores) or run.live(self.hook_pattern)):
@@ -198,11 +270,16 @@ class MLP(nn.Module):
     def __init__(self, cfg: HookedTransformerConfig):
         super().__init__()
         self.cfg = cfg
+        self.gated = cfg.gated_mlp
         self.W_in = nn.Parameter(torch.empty(cfg.d_model, cfg.d_mlp))
+        if self.gated:  # TL GatedMLP (SwiGLU with act_fn="silu")
+            self.W_gate = nn.Parameter(torch.empty(cfg.d_model, cfg.d_mlp))
         self.b_in = nn.Parameter(torch.zeros(cfg.d_mlp))
         self.W_out = nn.Parameter(torch.empty(cfg.d_mlp, cfg.d_model))
         self.b_out = nn.Parameter(torch.zeros(cfg.d_model))
         self.hook_pre = HookPoint()
+        if self.gated:
+            self.hook_pre_linear = HookPoint()
         self.hook_post = HookPoint()
 
 
@@ -211,12 +288,9 @@ class TransformerBlock(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.layer = layer
-        affine = cfg.normalization_type == "LN"
-        if cfg.normalization_type not in ("LN", "LNPre", None):
-            raise NotImplementedError(f"normalization_type {cfg.normalization_type}")
-        self.ln1 = LayerNormSite(cfg, affine) if cfg.normalization_type else None
+        self.ln1 = LayerNormSite.make(cfg, cfg.normalization_type)
         if not cfg.attn_only:
-            self.ln2 = LayerNormSite(cfg, affine) if cfg.normalization_type else None
+            self.ln2 = LayerNormSite.make(cfg, cfg.normalization_type)
         self.attn = Attention(cfg, layer)
         if not cfg.attn_only:
             self.mlp = MLP(cfg)
@@ -241,7 +315,7 @@ class TransformerBlock(nn.Module):
         """(normed x, residual to carry forward): fused backends return a passthrough of ``x`` whose
         gradient the LN backward kernel adds in (one pass instead of LN-bwd + autograd's sum)."""
         fork = getattr(run.ops, "layer_norm_fork", None)
-        if (ln is None or fork is None or run.live(ln.hook_scale) or run.live(ln.hook_normalized)
+        if (ln is None or ln.rms or fork is None or run.live(ln.hook_scale) or run.live(ln.hook_normalized)
                 or not x.requires_grad):
             return self._norm(ln, x, run), x
         return fork(x, ln.w, ln.b, ln.eps)
@@ -280,12 +354,18 @@ class TransformerBlock(nn.Module):
         mlp = self.mlp
         spl = run.whole_splice(mlp.hook_post.name)
         ln2_live = self.ln2 is not None and (run.live(self.ln2.hook_scale) or run.live(self.ln2.hook_normalized))
-        if spl is not None and not run.live(mlp.hook_pre) and not ln2_live:
+        pre_lin_live = mlp.gated and run.live(mlp.hook_pre_linear)
+        if spl is not None and not run.live(mlp.hook_pre) and not ln2_live and not pre_lin_live:
             post = run.site(mlp.hook_post, spl.src.to(ops.dtype), spliced=True)
         else:
             x, resid_mid = self._norm_fork(self.ln2, resid_mid, run)
             pre_hook = (lambda t: run.site(mlp.hook_pre, t)) if run.live(mlp.hook_pre) else None
-            _, post = ops.mlp_in(x, mlp.W_in, mlp.b_in, self.cfg.act_fn, hook_pre=pre_hook)
+            if mlp.gated:
+                lin_hook = (lambda t: run.site(mlp.hook_pre_linear, t)) if run.live(mlp.hook_pre_linear) else None
+                _, post = TorchOps.mlp_gated_in(ops, x, mlp.W_gate, mlp.W_in, mlp.b_in, self.cfg.act_fn,
+                                                hook_pre=pre_hook, hook_pre_linear=lin_hook)
+            else:
+                _, post = ops.mlp_in(x, mlp.W_in, mlp.b_in, self.cfg.act_fn, hook_pre=pre_hook)
             post = run.site(mlp.hook_post, post)
         if run.live(self.hook_mlp_out) or not ops.fused:
             mlp_out = run.site(self.hook_mlp_out, ops.mlp_out(post, mlp.W_out, mlp.b_out))
@@ -304,13 +384,17 @@ class HookedTransformer(HookedRootModule):
         self.tokenizer = tokenizer
         self.embed = Embed(cfg)
         self.hook_embed = HookPoint()
-        self.pos_embed = PosEmbed(cfg)
-        self.hook_pos_embed = HookPoint()
+        self.rotary = cfg.positional_embedding_type == "rotary"
+        if cfg.positional_embedding_type not in ("standard", "rotary"):
+            raise NotImplementedError(f"positional_embedding_type {cfg.positional_embedding_type}")
+        if not self.rotary:
+            self.pos_embed = PosEmbed(cfg)
+            self.hook_pos_embed = HookPoint()
         self.blocks = nn.ModuleList([TransformerBlock(cfg, l) for l in range(cfg.n_layers)])
-        if cfg.normalization_type in ("LN", "LNPre"):
-            self.ln_final = LayerNormSite(cfg, cfg.normalization_type == "LN")
-        else:
-            self.ln_final = None
+        final = cfg.normalization_type
+        if cfg.final_rms and final in ("LN", "LNPre"):
+            final = "RMS" if final == "LN" else "RMSPre"
+        self.ln_final = LayerNormSite.make(cfg, final)
         self.unembed = Unembed(cfg)
         self.op_backend: Optional[str] = None  # None = auto (see iit_amd.ops.select_ops)
         if cfg.init_weights:
@@ -353,7 +437,7 @@ class HookedTransformer(HookedRootModule):
         groups = []
         for blk in self.blocks:
             a = blk.attn
-            if any(getattr(a, n).shape != (H, d, dh) for n in ("W_Q", "W_K", "W_V")):
+            if a.gqa or any(getattr(a, n).shape != (H, d, dh) for n in ("W_Q", "W_K", "W_V")):
                 continue
 
             def w_view(which):
@@ -382,6 +466,9 @@ class HookedTransformer(HookedRootModule):
     def _embed(self, tokens: torch.Tensor, run: _Run) -> torch.Tensor:
         ops = run.ops
         B, S = tokens.shape
+        if self.rotary:  # positions enter through the rotary q/k rotation
+            return run.site(self.hook_embed, ops.embed(tokens, self.embed.W_E)).to(
+                torch.float32 if ops.fused else ops.dtype)
         if ops.fused and not (run.live(self.hook_embed) or run.live(self.hook_pos_embed)):
             return ops.embed_pos(tokens, self.embed.W_E, self.pos_embed.W_pos)
         e = run.site(self.hook_embed, ops.embed(tokens, self.embed.W_E))
@@ -462,6 +549,8 @@ class HookedTransformer(HookedRootModule):
 
     @property
     def W_pos(self):
+        if self.rotary:
+            raise AttributeError("rotary models have no W_pos")
         return self.pos_embed.W_pos
 
 

@@ -26,6 +26,14 @@ def _torch_ops(dtype):
     return ops
 
 
+def hip_supported(cfg) -> bool:
+    """Architectures the fused HIP backend implements (GPT-2 family); others run TorchOps on the GPU
+    (bf16 compute, library GEMMs) until their kernels exist (RMSNorm / rotary / SwiGLU / GQA)."""
+    return (cfg.positional_embedding_type == "standard" and cfg.normalization_type in ("LN", "LNPre", None)
+            and not cfg.gated_mlp and (cfg.n_key_value_heads in (None, cfg.n_heads))
+            and not cfg.parallel_attn_mlp and not cfg.final_rms)
+
+
 def select_ops(model, backend: Optional[str] = None):
     cfg = model.cfg
     dtype = cfg.dtype
@@ -33,7 +41,7 @@ def select_ops(model, backend: Optional[str] = None):
     if backend is None:
         from .. import config as _config
         env = _config.backend()
-        backend = "hip" if (on_gpu and dtype == torch.bfloat16 and env == "hip") else "torch"
+        backend = "hip" if (on_gpu and dtype == torch.bfloat16 and env == "hip" and hip_supported(cfg)) else "torch"
     if backend == "torch":
         return _torch_ops(dtype)
     if backend == "hip":

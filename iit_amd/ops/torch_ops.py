@@ -64,6 +64,35 @@ class TorchOps:
             y = hook_normalized(y)
         return y
 
+    def rms_norm(self, x, w: Optional[torch.Tensor], eps: float, hook_scale=None, hook_normalized=None):
+        """TL ``RMSNorm`` / ``RMSNormPre``: ``x / sqrt(mean(x^2) + eps) (* w)``."""
+        x = x.to(self.dtype)
+        scale = (x.pow(2).mean(-1, keepdim=True) + eps).sqrt()
+        if hook_scale is not None:
+            scale = hook_scale(scale)
+        y = x / scale
+        if w is not None:
+            y = y * self.w(w)
+        if hook_normalized is not None:
+            y = hook_normalized(y)
+        return y
+
+    def rotary(self, x, cos, sin, rotary_dim: int, adjacent_pairs: bool = False, offset: int = 0):
+        """Rotary position embedding of ``x [B, S, H, dh]`` on its first ``rotary_dim`` features
+        (TL ``apply_rotary``; GPT-NeoX half-split pairs, or adjacent (even, odd) pairs)."""
+        S = x.shape[1]
+        c = cos[offset:offset + S].to(x.dtype)[None, :, None, :]
+        s = sin[offset:offset + S].to(x.dtype)[None, :, None, :]
+        xr, xp = x[..., :rotary_dim], x[..., rotary_dim:]
+        if adjacent_pairs:
+            x1, x2 = xr[..., 0::2], xr[..., 1::2]
+            flipped = torch.stack([-x2, x1], dim=-1).flatten(-2)
+        else:
+            half = rotary_dim // 2
+            flipped = torch.cat([-xr[..., half:], xr[..., :half]], dim=-1)
+        out = xr * c + flipped * s
+        return torch.cat([out, xp], dim=-1) if xp.shape[-1] else out
+
     def qkv(self, x, W_Q, W_K, W_V, b_Q, b_K, b_V):
         q = torch.einsum("bsd,hde->bshe", x, self.w(W_Q)) + self.w(b_Q)
         k = torch.einsum("bsd,hde->bshe", x, self.w(W_K)) + self.w(b_K)
@@ -97,6 +126,16 @@ class TorchOps:
         if hook_pre is not None:
             pre = hook_pre(pre)
         return pre, act_fn(act)(pre)
+
+    def mlp_gated_in(self, x, W_gate, W_in, b_in, act: str, hook_pre=None, hook_pre_linear=None):
+        """TL ``GatedMLP``: ``pre = x W_gate`` (hook_pre), ``pre_linear = x W_in + b_in``, ``post = act(pre) * pre_linear``."""
+        pre = x @ self.w(W_gate)
+        if hook_pre is not None:
+            pre = hook_pre(pre)
+        pre_linear = x @ self.w(W_in) + self.w(b_in)
+        if hook_pre_linear is not None:
+            pre_linear = hook_pre_linear(pre_linear)
+        return pre, act_fn(act)(pre) * pre_linear
 
     def mlp_out(self, post, W_out, b_out):
         return post @ self.w(W_out) + self.w(b_out)
