@@ -1,0 +1,241 @@
+"""BERT-style hooked encoder (the MQNLI LL model of ``BASELINE.json`` config 4).
+
+TransformerLens ``HookedEncoder`` names and layouts (``embed.embed.W_E``,
+``embed.pos_embed.W_pos``, ``embed.token_type_embed.W_token_type``, ``embed.ln``,
+``blocks.L.attn.W_Q [H, d, dh]`` ..., post-LN blocks with ``ln1`` after attention and
+``ln2`` after the MLP, ``mlm_head`` + ``unembed``), plus an optional sequence-
+classification head on the first ([CLS]) position with HF BERT semantics
+(``pooler.W``/``pooler.b`` dense + tanh, ``classifier.W``/``classifier.b``) -- the
+head MQNLI's 3-way entailment label is read from.
+
+Every hook site goes through the same plan executor as the decoder
+(:class:`iit_amd.models.transformer._Run`), so the native intervention engine
+(capture-only truncated source runs, splices, StopGrad scaling) works unchanged.
+Compute runs through :class:`iit_amd.ops.torch_ops.TorchOps` in the model's
+``cfg.dtype`` (bf16 on MI355X with library GEMMs; fp32 oracle on CPU).
+
+``from_hf_bert`` converts an in-memory HF ``BertForSequenceClassification`` /
+``BertForMaskedLM`` / ``BertModel`` (random-init or local weights; nothing is
+downloaded).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Union
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ..engine.plan import RunPlan
+from ..hooks.hook_points import HookedRootModule, HookPoint
+from ..ops.torch_ops import TorchOps
+from .config import HookedTransformerConfig, make_config
+from .transformer import MLP, Attention, LayerNormSite, _Run, _StopForward
+
+_OPS = {}
+
+
+def _ops(dtype):
+    if dtype not in _OPS:
+        _OPS[dtype] = TorchOps(dtype)
+    return _OPS[dtype]
+
+
+def bert_config_dict(size: str = "bert-base", **overrides):
+    presets = {
+        "bert-base": dict(n_layers=12, d_model=768, n_heads=12, d_head=64, d_mlp=3072, d_vocab=30522, n_ctx=512),
+        "bert-tiny": dict(n_layers=2, d_model=64, n_heads=4, d_head=16, d_mlp=128, d_vocab=128, n_ctx=64),
+    }
+    cfg = dict(presets[size])
+    cfg.update(act_fn="gelu", normalization_type="LN", attention_dir="bidirectional", eps=1e-12,
+               original_architecture="BertForMaskedLM", model_name=size, initializer_range=0.02)
+    cfg.update(overrides)
+    return HookedTransformerConfig.from_dict(cfg).to_dict()
+
+
+class BertEmbed(nn.Module):
+    def __init__(self, cfg: HookedTransformerConfig, n_token_types: int = 2):
+        super().__init__()
+        self.embed = nn.Module()
+        self.embed.W_E = nn.Parameter(torch.empty(cfg.d_vocab, cfg.d_model))
+        self.pos_embed = nn.Module()
+        self.pos_embed.W_pos = nn.Parameter(torch.empty(cfg.n_ctx, cfg.d_model))
+        self.token_type_embed = nn.Module()
+        self.token_type_embed.W_token_type = nn.Parameter(torch.empty(n_token_types, cfg.d_model))
+        self.ln = LayerNormSite(cfg, affine=True)
+        self.hook_embed = HookPoint()
+        self.hook_pos_embed = HookPoint()
+        self.hook_token_type_embed = HookPoint()
+
+
+class BertBlock(nn.Module):
+    """Post-LN encoder block: ``x = ln1(x + attn(x)); x = ln2(x + mlp(x))``."""
+
+    def __init__(self, cfg: HookedTransformerConfig, layer: int):
+        super().__init__()
+        self.cfg = cfg
+        self.attn = Attention(cfg, layer)
+        self.ln1 = LayerNormSite(cfg, affine=True)
+        self.mlp = MLP(cfg)
+        self.ln2 = LayerNormSite(cfg, affine=True)
+        self.hook_attn_out = HookPoint()
+        self.hook_mlp_in = HookPoint()
+        self.hook_mlp_out = HookPoint()
+        self.hook_resid_pre = HookPoint()
+        self.hook_resid_mid = HookPoint()
+        self.hook_resid_post = HookPoint()
+        self.hook_normalized_resid_post = HookPoint()
+
+    def forward(self, resid, run: _Run, key_mask: Optional[torch.Tensor]):
+        ops, attn = run.ops, self.attn
+        resid = run.site(self.hook_resid_pre, resid)
+        q, k, v = ops.qkv(resid, attn.W_Q, attn.W_K, attn.W_V, attn.b_Q, attn.b_K, attn.b_V)
+        q, k, v = run.site(attn.hook_q, q), run.site(attn.hook_k, k), run.site(attn.hook_v, v)
+        scores = torch.einsum("bqhe,bkhe->bhqk", q, k) / attn.attn_scale
+        if key_mask is not None:
+            scores = scores.masked_fill(~key_mask[:, None, None, :], float("-inf"))
+        scores = run.site(attn.hook_attn_scores, scores)
+        pattern = run.site(attn.hook_pattern, torch.softmax(scores.float(), dim=-1).to(scores.dtype))
+        z = run.site(attn.hook_z, torch.einsum("bkhe,bhqk->bqhe", v, pattern))
+        attn_out = run.site(self.hook_attn_out, ops.o_proj(z, attn.W_O, attn.b_O))
+        resid_mid = run.site(self.hook_resid_mid, resid + attn_out)
+        x = self.ln1.run(resid_mid, run)
+        x = run.site(self.hook_mlp_in, x)
+        pre_hook = (lambda t: run.site(self.mlp.hook_pre, t)) if run.live(self.mlp.hook_pre) else None
+        _, post = ops.mlp_in(x, self.mlp.W_in, self.mlp.b_in, self.cfg.act_fn, hook_pre=pre_hook)
+        post = run.site(self.mlp.hook_post, post)
+        mlp_out = run.site(self.hook_mlp_out, ops.mlp_out(post, self.mlp.W_out, self.mlp.b_out))
+        resid_post = run.site(self.hook_resid_post, x + mlp_out)
+        return run.site(self.hook_normalized_resid_post, self.ln2.run(resid_post, run))
+
+
+class HookedEncoder(HookedRootModule):
+    """BERT encoder; ``n_classes`` adds the [CLS] pooler + classifier head (forward then returns ``[B, C]``)."""
+
+    supports_run_plan = True
+
+    def __init__(self, cfg: Union[HookedTransformerConfig, dict], n_classes: Optional[int] = None,
+                 move_to_device: bool = True):
+        super().__init__()
+        self.cfg = make_config(cfg)
+        cfg = self.cfg
+        self.embed = BertEmbed(cfg)
+        self.hook_full_embed = HookPoint()
+        self.blocks = nn.ModuleList([BertBlock(cfg, l) for l in range(cfg.n_layers)])
+        self.n_classes = n_classes
+        self.sep_token_id: Optional[int] = None  # set -> token types derived from [SEP] when not given
+        if n_classes:
+            self.pooler = nn.Module()
+            self.pooler.W = nn.Parameter(torch.empty(cfg.d_model, cfg.d_model))
+            self.pooler.b = nn.Parameter(torch.zeros(cfg.d_model))
+            self.classifier = nn.Module()
+            self.classifier.W = nn.Parameter(torch.empty(cfg.d_model, n_classes))
+            self.classifier.b = nn.Parameter(torch.zeros(n_classes))
+            self.hook_pooled = HookPoint()
+        else:
+            self.mlm_head = nn.Module()
+            self.mlm_head.W = nn.Parameter(torch.empty(cfg.d_model, cfg.d_model))
+            self.mlm_head.b = nn.Parameter(torch.zeros(cfg.d_model))
+            self.mlm_head.ln = LayerNormSite(cfg, affine=True)
+            self.unembed = nn.Module()
+            self.unembed.W_U = nn.Parameter(torch.empty(cfg.d_model, cfg.d_vocab_out))
+            self.unembed.b_U = nn.Parameter(torch.zeros(cfg.d_vocab_out))
+        for name, p in self.named_parameters():
+            if name.endswith((".W_E", ".W_pos", ".W_token_type")) or ".W_" in name or name.endswith(".W"):
+                nn.init.normal_(p, std=cfg.initializer_range)
+        if move_to_device and cfg.device is not None:
+            self.to(cfg.device)
+        self.setup()
+
+    def mark_weights_changed(self) -> None:
+        self._iit_weights_version = getattr(self, "_iit_weights_version", 0) + 1
+
+    def forward(self, input, token_type_ids: Optional[torch.Tensor] = None,
+                attention_mask: Optional[torch.Tensor] = None, *, plan: Optional[RunPlan] = None,
+                return_type: Optional[str] = "logits"):
+        tokens = input
+        if tokens.dim() == 1:
+            tokens = tokens.unsqueeze(0)
+        dev = self.embed.embed.W_E.device
+        tokens = tokens.to(dev)
+        run = _Run(plan, _ops(self.cfg.dtype))
+        ops = run.ops
+        B, S = tokens.shape
+        if token_type_ids is None:
+            sep = getattr(self, "sep_token_id", None)
+            if sep is None:
+                token_type_ids = torch.zeros_like(tokens)
+            else:  # segment B starts after the first [SEP] (BERT sentence-pair convention)
+                is_sep = (tokens == sep).long()
+                token_type_ids = ((is_sep.cumsum(-1) - is_sep) > 0).long()
+        key_mask = None if attention_mask is None else attention_mask.to(dev).bool()
+        try:
+            e = run.site(self.embed.hook_embed, ops.embed(tokens, self.embed.embed.W_E))
+            p = run.site(self.embed.hook_pos_embed, ops.pos_embed(B, S, self.embed.pos_embed.W_pos))
+            t = run.site(self.embed.hook_token_type_embed, ops.w(self.embed.token_type_embed.W_token_type)[token_type_ids])
+            x = self.embed.ln.run(e + p + t, run)
+            x = run.site(self.hook_full_embed, x)
+            for blk in self.blocks:
+                x = blk(x, run, key_mask)
+            if plan is not None and plan.logits == "none" or return_type is None:
+                return None
+            if self.n_classes:
+                pooled = torch.tanh(x[:, 0] @ ops.w(self.pooler.W) + ops.w(self.pooler.b))
+                pooled = run.site(self.hook_pooled, pooled)
+                return pooled @ ops.w(self.classifier.W) + ops.w(self.classifier.b)
+            h = F.gelu(x @ ops.w(self.mlm_head.W) + ops.w(self.mlm_head.b))
+            h = self.mlm_head.ln.run(h, run)
+            return h @ ops.w(self.unembed.W_U) + ops.w(self.unembed.b_U)
+        except _StopForward:
+            return None
+
+    def run_capture(self, tokens, names, truncate: bool = True, base_plan: Optional[RunPlan] = None, **kw):
+        plan = RunPlan.capture_only(list(names), truncate=truncate)
+        if base_plan is not None:
+            plan = base_plan.merged(plan)
+        with torch.no_grad():
+            self.forward(tokens, plan=plan, **kw)
+        return plan.cache
+
+
+def from_hf_bert(hf_model) -> Dict[str, torch.Tensor]:
+    """TL-layout parameters from HF ``BertForSequenceClassification`` / ``BertForMaskedLM`` / ``BertModel``."""
+    bert = getattr(hf_model, "bert", hf_model)
+    cfg = bert.config
+    d, H = cfg.hidden_size, cfg.num_attention_heads
+    dh = d // H
+    t = lambda x: x.detach().clone().float()  # noqa: E731
+    emb = bert.embeddings
+    sd = {"embed.embed.W_E": t(emb.word_embeddings.weight), "embed.pos_embed.W_pos": t(emb.position_embeddings.weight),
+          "embed.token_type_embed.W_token_type": t(emb.token_type_embeddings.weight),
+          "embed.ln.w": t(emb.LayerNorm.weight), "embed.ln.b": t(emb.LayerNorm.bias)}
+    for l, layer in enumerate(bert.encoder.layer):
+        p = f"blocks.{l}."
+        s = layer.attention.self
+        for n, lin in (("Q", s.query), ("K", s.key), ("V", s.value)):
+            sd[p + f"attn.W_{n}"] = t(lin.weight).reshape(H, dh, d).permute(0, 2, 1).contiguous()
+            sd[p + f"attn.b_{n}"] = t(lin.bias).reshape(H, dh)
+        o = layer.attention.output
+        sd[p + "attn.W_O"] = t(o.dense.weight).reshape(d, H, dh).permute(1, 2, 0).contiguous()
+        sd[p + "attn.b_O"] = t(o.dense.bias)
+        sd[p + "ln1.w"], sd[p + "ln1.b"] = t(o.LayerNorm.weight), t(o.LayerNorm.bias)
+        sd[p + "mlp.W_in"] = t(layer.intermediate.dense.weight).t().contiguous()
+        sd[p + "mlp.b_in"] = t(layer.intermediate.dense.bias)
+        sd[p + "mlp.W_out"] = t(layer.output.dense.weight).t().contiguous()
+        sd[p + "mlp.b_out"] = t(layer.output.dense.bias)
+        sd[p + "ln2.w"], sd[p + "ln2.b"] = t(layer.output.LayerNorm.weight), t(layer.output.LayerNorm.bias)
+    if getattr(bert, "pooler", None) is not None and hasattr(hf_model, "classifier"):
+        sd["pooler.W"] = t(bert.pooler.dense.weight).t().contiguous()
+        sd["pooler.b"] = t(bert.pooler.dense.bias)
+        sd["classifier.W"] = t(hf_model.classifier.weight).t().contiguous()
+        sd["classifier.b"] = t(hf_model.classifier.bias)
+    if hasattr(hf_model, "cls"):
+        tr = hf_model.cls.predictions.transform
+        sd["mlm_head.W"] = t(tr.dense.weight).t().contiguous()
+        sd["mlm_head.b"] = t(tr.dense.bias)
+        sd["mlm_head.ln.w"], sd["mlm_head.ln.b"] = t(tr.LayerNorm.weight), t(tr.LayerNorm.bias)
+        sd["unembed.W_U"] = t(hf_model.cls.predictions.decoder.weight).t().contiguous()
+        sd["unembed.b_U"] = t(hf_model.cls.predictions.bias if hasattr(hf_model.cls.predictions, "bias")
+                              else hf_model.cls.predictions.decoder.bias)
+    return sd

@@ -67,3 +67,27 @@ def test_llama_presets_and_iit_intervention_on_llama():
         return z
     ref = m.run_with_hooks(base, fwd_hooks=[("blocks.0.attn.hook_z", hook)])[:, -1]
     assert torch.allclose(out, ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("head", ["cls", "mlm"])
+def test_bert_matches_hf(head):
+    from iit_amd.models.bert import HookedEncoder, bert_config_dict, from_hf_bert
+    torch.manual_seed(0)
+    hcfg = transformers.BertConfig(hidden_size=64, num_hidden_layers=2, num_attention_heads=4, intermediate_size=128,
+                                   vocab_size=120, max_position_embeddings=64, num_labels=3,
+                                   hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    hf = (transformers.BertForSequenceClassification(hcfg) if head == "cls" else transformers.BertForMaskedLM(hcfg))
+    hf = hf.eval()
+    cfg = bert_config_dict("bert-tiny", d_vocab=120, device="cpu")
+    model = HookedEncoder(cfg, n_classes=3 if head == "cls" else None)
+    convert.load_converted(model, from_hf_bert(hf))
+    tok = torch.randint(0, 120, (3, 10))
+    tt = torch.cat([torch.zeros(3, 5, dtype=torch.long), torch.ones(3, 5, dtype=torch.long)], dim=1)
+    am = torch.ones(3, 10, dtype=torch.long)
+    am[1, 8:] = 0
+    with torch.no_grad():
+        ref = hf(input_ids=tok, token_type_ids=tt, attention_mask=am).logits
+        out = model(tok, token_type_ids=tt, attention_mask=am)
+    if head == "mlm":
+        ref, out = ref[am.bool()], out[am.bool()]
+    assert torch.allclose(out, ref, atol=1e-4, rtol=1e-4), (out - ref).abs().max()
