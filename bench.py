@@ -79,7 +79,7 @@ def setup(args, dev):
     pair = IOI_ModelPair(ll_model=ll, hl_model=hl, corr=make_ioi_corr(cfg["n_layers"]), training_args=training_args)
     pdist.broadcast_module(ll)
     opt = pair.make_optimizer(training_args["lr"])
-    pair.restrict_embedding_reduce(train_set)  # DP: reduce only W_E rows of dataset tokens (exact)
+    pair.restrict_sparse_rows(train_set)  # reduce / update only embedding rows the data can reach (exact)
     loss_fn = pair.loss_fn
     loader = train_set.make_loader(args.batch, 0)
 

@@ -43,8 +43,26 @@ __global__ void embed_bwd_kernel(const long* __restrict__ tok, const float* __re
   for (int i = threadIdx.x; i < d; i += blockDim.x) atomicAdd(dWE + v * (long)d + i, g[(long)t * d + i]);
 }
 
-// dW_pos[s] += sum_b g[b, s]
-__global__ void pos_bwd_kernel(const float* __restrict__ g, float* __restrict__ dWpos, int B, int S, int d) {
+// dW_pos[s] += sum_b g[b, s].  Block = (position s, 256-column slab); 4 waves split the batch, LDS combine.
+__global__ __launch_bounds__(256) void pos_bwd_kernel(const float* __restrict__ g, float* __restrict__ dWpos, int B,
+                                                      int S, int d) {
+  __shared__ float part[4][64 * 4];
+  const int s = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = blockIdx.y * 256 + lane * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < d)
+    for (int b = w; b < B; b += 4) {
+      const float4 v = *(const float4*)(g + ((long)b * S + s) * d + c);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  *(float4*)&part[w][lane * 4] = acc;
+  __syncthreads();
+  const int col = blockIdx.y * 256 + threadIdx.x;
+  if (col < d)
+    dWpos[(long)s * d + col] += part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+}
+
+__global__ void pos_bwd_scalar_kernel(const float* __restrict__ g, float* __restrict__ dWpos, int B, int S, int d) {
   const int s = blockIdx.x;
   for (int i = threadIdx.x; i < d; i += blockDim.x) {
     float acc = 0.f;
@@ -57,12 +75,69 @@ IIT_EXPORT int iit_embed_pos_bwd(const long* tok, const float* g, float* dWE, fl
                                  void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (dWE) hipLaunchKernelGGL(embed_bwd_kernel, dim3(B * S), dim3(256), 0, st, tok, g, dWE, B * S, d);
-  if (dWpos) hipLaunchKernelGGL(pos_bwd_kernel, dim3(S), dim3(256), 0, st, g, dWpos, B, S, d);
+  if (dWpos) {
+    if (d % 4 == 0 && (((uintptr_t)g) & 15) == 0)
+      hipLaunchKernelGGL(pos_bwd_kernel, dim3(S, (d + 255) / 256), dim3(256), 0, st, g, dWpos, B, S, d);
+    else
+      hipLaunchKernelGGL(pos_bwd_scalar_kernel, dim3(S), dim3(256), 0, st, g, dWpos, B, S, d);
+  }
   return hipGetLastError();
 }
 
 // ============================================================================ layer norm
-// y = (x - mean) * rstd  (* w + b);   one wave per row, up to 32 floats per lane (d <= 2048)
+// One wave per row; each lane owns V4 float4 column groups (c4 = lane + 64*i), so every load is a 16-B
+// vector and a wave instruction moves 1 KB (fp32) / 512 B (bf16).  Requires d % 4 == 0 and 16-B aligned
+// rows; the scalar kernels below cover everything else.  Stats in fp32.
+template <int V4>
+__global__ __launch_bounds__(256) void ln_fwd_vec_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ b, __bf16* __restrict__ y,
+                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                         int T, int d, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const int d4 = d >> 2;
+  const float4* xr = (const float4*)(x + (long)row * d);
+  float4 v[V4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V4; ++i) {
+    const int c = lane + i * 64;
+    v[i] = c < d4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+  const float mu = wave_sum(s) / d;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < V4; ++i) {
+    const int c = lane + i * 64;
+    if (c < d4) {
+      v[i].x -= mu; v[i].y -= mu; v[i].z -= mu; v[i].w -= mu;
+      s2 += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(s2) / d + eps);
+  bf16x4* yr = (bf16x4*)(y + (long)row * d);
+#pragma unroll
+  for (int i = 0; i < V4; ++i) {
+    const int c = lane + i * 64;
+    if (c < d4) {
+      float4 o = make_float4(v[i].x * rstd, v[i].y * rstd, v[i].z * rstd, v[i].w * rstd);
+      if (w) {
+        const float4 ww = ((const float4*)w)[c], bb = ((const float4*)b)[c];
+        o = make_float4(o.x * ww.x + bb.x, o.y * ww.y + bb.y, o.z * ww.z + bb.z, o.w * ww.w + bb.w);
+      }
+      bf16x4 ob = {f2bf(o.x), f2bf(o.y), f2bf(o.z), f2bf(o.w)};
+      yr[c] = ob;
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mu;
+    rstd_out[row] = rstd;
+  }
+}
+
+// scalar fallback: y = (x - mean) * rstd  (* w + b);   one wave per row, up to VPL floats per lane
 template <int VPL>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ b, __bf16* __restrict__ y,
@@ -106,10 +181,21 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
+static inline bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+
 IIT_EXPORT int iit_ln_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd, int T,
                           int d, float eps, void* stream) {
   dim3 grid((T + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
+  const bool vec = d % 4 == 0 && aligned16(x) && (((uintptr_t)y) & 7) == 0 && (!w || (aligned16(w) && aligned16(b)));
+  if (vec && d <= 4096) {
+#define LNF(V) hipLaunchKernelGGL((ln_fwd_vec_kernel<V>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps)
+    const int v4 = (d / 4 + 63) / 64;
+    if (v4 <= 1) LNF(1); else if (v4 <= 2) LNF(2); else if (v4 <= 3) LNF(3); else if (v4 <= 4) LNF(4);
+    else if (v4 <= 6) LNF(6); else if (v4 <= 8) LNF(8); else if (v4 <= 12) LNF(12); else LNF(16);
+#undef LNF
+    return hipGetLastError();
+  }
   if (d <= 256) hipLaunchKernelGGL((ln_fwd_kernel<4>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps);
   else if (d <= 1024) hipLaunchKernelGGL((ln_fwd_kernel<16>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps);
   else if (d <= 2048) hipLaunchKernelGGL((ln_fwd_kernel<32>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps);
@@ -118,16 +204,108 @@ IIT_EXPORT int iit_ln_fwd(const float* x, const float* w, const float* b, void* 
   return hipGetLastError();
 }
 
-// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) (+ dres),  g = dy * w;  dw += dy * xhat, db += dy
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) (+ dres),  g = dy * w.
 // ``dres`` (nullable) is the residual stream's skip-connection gradient: fusing it here saves autograd's
-// separate gradient-sum pass over the fp32 residual.
+// separate gradient-sum pass over the fp32 residual.  ``dx16`` (nullable) receives a bf16 copy of dx: the
+// next backward GEMMs (W_O / W_out dX and dW) read bf16, so the cast rides along with this pass.
+// The affine gradients dw/db are NOT done here (see ln_dwdb_kernel: per-block partial sums, few atomics).
+template <int V4, bool DY_F32>
+__global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
+                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                         const float* __restrict__ w, float* __restrict__ dx,
+                                                         const float* __restrict__ dres, __bf16* __restrict__ dx16,
+                                                         int T, int d, int accumulate) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const int d4 = d >> 2;
+  const float mu = mean[row], rs = rstd[row];
+  float4 g[V4], xh[V4];
+  float sg = 0.f, sgx = 0.f;
+#pragma unroll
+  for (int i = 0; i < V4; ++i) {
+    const int c = lane + i * 64;
+    float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xv = dy;
+    if (c < d4) {
+      if (DY_F32) {
+        dy = ((const float4*)dy_)[(long)row * d4 + c];
+      } else {
+        const bf16x4 t = ((const bf16x4*)dy_)[(long)row * d4 + c];
+        dy = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
+      }
+      const float4 xx = ((const float4*)x)[(long)row * d4 + c];
+      xv = make_float4((xx.x - mu) * rs, (xx.y - mu) * rs, (xx.z - mu) * rs, (xx.w - mu) * rs);
+      if (w) {
+        const float4 ww = ((const float4*)w)[c];
+        dy.x *= ww.x; dy.y *= ww.y; dy.z *= ww.z; dy.w *= ww.w;
+      }
+    }
+    g[i] = dy;
+    xh[i] = xv;
+    sg += (dy.x + dy.y) + (dy.z + dy.w);
+    sgx += (dy.x * xv.x + dy.y * xv.y) + (dy.z * xv.z + dy.w * xv.w);
+  }
+  sg = wave_sum(sg) / d;
+  sgx = wave_sum(sgx) / d;
+#pragma unroll
+  for (int i = 0; i < V4; ++i) {
+    const int c = lane + i * 64;
+    if (c < d4) {
+      float4 o = make_float4(rs * (g[i].x - sg - xh[i].x * sgx), rs * (g[i].y - sg - xh[i].y * sgx),
+                             rs * (g[i].z - sg - xh[i].z * sgx), rs * (g[i].w - sg - xh[i].w * sgx));
+      if (dres) {
+        const float4 r = ((const float4*)dres)[(long)row * d4 + c];
+        o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+      }
+      float4* p = (float4*)dx + (long)row * d4 + c;
+      if (accumulate) {
+        const float4 q = *p;
+        o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+      }
+      *p = o;
+      if (dx16) {
+        bf16x4 ob = {f2bf(o.x), f2bf(o.y), f2bf(o.z), f2bf(o.w)};
+        ((bf16x4*)dx16)[(long)row * d4 + c] = ob;
+      }
+    }
+  }
+}
+
+// Affine LN parameter gradients: dw[c] += sum_t dy[t][c] * xhat[t][c], db[c] += sum_t dy[t][c].
+// Block = 64 columns x 256 rows (4 waves x 64 rows), LDS combine, one atomic per column per block.
+template <bool DY_F32>
+__global__ __launch_bounds__(256) void ln_dwdb_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
+                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                      float* __restrict__ dw, float* __restrict__ db, int T, int d) {
+  __shared__ float pw[4][64], pb[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), wv = threadIdx.x >> 6;
+  const int t0 = blockIdx.y * 256;
+  float sw = 0.f, sb = 0.f;
+  if (c < d)
+    for (int i = 0; i < 64; ++i) {
+      const int t = t0 + wv * 64 + i;
+      if (t >= T) break;
+      const float dy = DY_F32 ? ((const float*)dy_)[(long)t * d + c] : bf2f(((const __bf16*)dy_)[(long)t * d + c]);
+      sw += dy * (x[(long)t * d + c] - mean[t]) * rstd[t];
+      sb += dy;
+    }
+  pw[wv][threadIdx.x & 63] = sw;
+  pb[wv][threadIdx.x & 63] = sb;
+  __syncthreads();
+  if (wv == 0 && c < d) {
+    const int l = threadIdx.x;
+    atomicAdd(dw + c, pw[0][l] + pw[1][l] + pw[2][l] + pw[3][l]);
+    atomicAdd(db + c, pb[0][l] + pb[1][l] + pb[2][l] + pb[3][l]);
+  }
+}
+
+// scalar fallback (any d <= 4096, any alignment)
 template <int VPL, bool DY_F32>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ w, float* __restrict__ dx,
-                                                     const float* __restrict__ dres,
-                                                     float* __restrict__ dw, float* __restrict__ db, int T, int d,
-                                                     int accumulate) {
+                                                     const float* __restrict__ dres, __bf16* __restrict__ dx16,
+                                                     int T, int d, int accumulate) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= T) return;
@@ -141,10 +319,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
     if (c < d) {
       dy = DY_F32 ? ((const float*)dy_)[(long)row * d + c] : bf2f(((const __bf16*)dy_)[(long)row * d + c]);
       xv = (x[(long)row * d + c] - mu) * rs;
-      if (dw) {
-        atomicAdd(dw + c, dy * xv);
-        atomicAdd(db + c, dy);
-      }
       if (w) dy *= w[c];
     }
     g[i] = dy;
@@ -161,25 +335,46 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
       float o = rs * (g[i] - sg - xh[i] * sgx);
       if (dres) o += dres[(long)row * d + c];
       float* p = dx + (long)row * d + c;
-      *p = accumulate ? *p + o : o;
+      o = accumulate ? *p + o : o;
+      *p = o;
+      if (dx16) dx16[(long)row * d + c] = f2bf(o);
     }
   }
 }
 
 IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
-                          const float* w, float* dx, const float* dres, float* dw, float* db, int T, int d,
+                          const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db, int T, int d,
                           int accumulate, void* stream) {
   dim3 grid((T + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
+  __bf16* d16 = (__bf16*)dx16;
+  const bool vec = d % 4 == 0 && d <= 4096 && aligned16(x) && aligned16(dx) && (!dres || aligned16(dres)) &&
+                   (!w || aligned16(w)) && (dy_f32 ? aligned16(dy) : (((uintptr_t)dy) & 7) == 0) &&
+                   (((uintptr_t)dx16) & 7) == 0;
+  if (vec) {
+#define LNBV(V)                                                                                                   \
+  if (dy_f32) hipLaunchKernelGGL((ln_bwd_vec_kernel<V, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate); \
+  else hipLaunchKernelGGL((ln_bwd_vec_kernel<V, false>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate);
+    const int v4 = (d / 4 + 63) / 64;
+    if (v4 <= 1) { LNBV(1) } else if (v4 <= 2) { LNBV(2) } else if (v4 <= 3) { LNBV(3) } else if (v4 <= 4) { LNBV(4) }
+    else if (v4 <= 6) { LNBV(6) } else if (v4 <= 8) { LNBV(8) } else if (v4 <= 12) { LNBV(12) } else { LNBV(16) }
+#undef LNBV
+  } else {
 #define LNB(V)                                                                                                   \
-  if (dy_f32) hipLaunchKernelGGL((ln_bwd_kernel<V, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, dw, db, T, d, accumulate); \
-  else hipLaunchKernelGGL((ln_bwd_kernel<V, false>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, dw, db, T, d, accumulate);
-  if (d <= 256) { LNB(4) }
-  else if (d <= 1024) { LNB(16) }
-  else if (d <= 2048) { LNB(32) }
-  else if (d <= 4096) { LNB(64) }
-  else return (int)hipErrorInvalidValue;
+  if (dy_f32) hipLaunchKernelGGL((ln_bwd_kernel<V, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate); \
+  else hipLaunchKernelGGL((ln_bwd_kernel<V, false>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate);
+    if (d <= 256) { LNB(4) }
+    else if (d <= 1024) { LNB(16) }
+    else if (d <= 2048) { LNB(32) }
+    else if (d <= 4096) { LNB(64) }
+    else return (int)hipErrorInvalidValue;
 #undef LNB
+  }
+  if (dw) {
+    dim3 g2((d + 63) / 64, (T + 255) / 256);
+    if (dy_f32) hipLaunchKernelGGL(ln_dwdb_kernel<true>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d);
+    else hipLaunchKernelGGL(ln_dwdb_kernel<false>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d);
+  }
   return hipGetLastError();
 }
 
@@ -444,16 +639,30 @@ IIT_EXPORT int iit_ce_bwd(const float* logits, long ld, const long* labels, cons
 // partial sums of g^2 per block (grid-stride over float4)
 // Stage 1 of the fused clip+Adam: per-block partial sums of g^2 (skipped when clip == 0) and the
 // device-side step counter bump (block 0), so a captured graph replays with the right bias corrections.
-__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ g, long n4, float* __restrict__ part,
-                                                            int do_norm, int* __restrict__ step) {
+// The optimizer walks a table of spans (start, length in float4 units, <= 1024 float4 each) over the arena
+// instead of [0, n): rows that can never receive gradient (embedding rows of tokens absent from the dataset,
+// positions past the sequence length) are left out -- with zero gradient and zero moments, Adam leaves them
+// bit-identical, so skipping them is exact and saves their 30 B/element of HBM traffic.
+struct Span {
+  long start4;
+  int len4;
+  int pad;
+};
+
+__global__ __launch_bounds__(256) void sumsq_span_kernel(const float* __restrict__ g, const Span* __restrict__ spans,
+                                                         int nspans, float* __restrict__ part, int do_norm,
+                                                         int* __restrict__ step) {
   __shared__ float sm[4];
   if (blockIdx.x == 0 && threadIdx.x == 0 && step) step[0] += 1;
   if (!do_norm) return;
   float s = 0.f;
   const float4* g4 = (const float4*)g;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    const float4 v = g4[i];
-    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  for (int e = blockIdx.x; e < nspans; e += gridDim.x) {
+    const Span sp = spans[e];
+    for (int i = threadIdx.x; i < sp.len4; i += 256) {
+      const float4 v = g4[sp.start4 + i];
+      s += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+    }
   }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
@@ -464,11 +673,11 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restr
 // Adam (torch semantics, amsgrad=False) with the clip coefficient computed on device from the partial sums,
 // the bias corrections from the device step counter, and the bf16 mirror of the updated weights written in
 // the same pass.  Streams: read g, p, m, v; write p, m, v, mirror (the clipped gradient is not written back).
-__global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
+__global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
-                                                        __bf16* __restrict__ mirror, long n4,
-                                                        const float* __restrict__ part, int nparts, float clip,
-                                                        float lr, float b1, float b2, float eps, float wd,
+                                                        __bf16* __restrict__ mirror, const Span* __restrict__ spans,
+                                                        int nspans, const float* __restrict__ part, int nparts,
+                                                        float clip, float lr, float b1, float b2, float eps, float wd,
                                                         int* __restrict__ step, int* __restrict__ skipped) {
   __shared__ float coef_s;
   __shared__ int bad_s;
@@ -499,44 +708,52 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p, c
   float4* p4 = (float4*)p;
   float4* m4 = (float4*)m;
   float4* v4 = (float4*)v;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    float4 gg = g4[i], pp = p4[i], mm = m4[i], vv = v4[i];
-    float* gs = (float*)&gg;
-    float* ps = (float*)&pp;
-    float* ms = (float*)&mm;
-    float* vs = (float*)&vv;
+  for (int e = blockIdx.x; e < nspans; e += gridDim.x) {
+    const Span sp = spans[e];
+    for (int j = threadIdx.x; j < sp.len4; j += 256) {
+      const long i = sp.start4 + j;
+      float4 gg = g4[i], pp = p4[i], mm = m4[i], vv = v4[i];
+      float* gs = (float*)&gg;
+      float* ps = (float*)&pp;
+      float* ms = (float*)&mm;
+      float* vs = (float*)&vv;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float gr = gs[e] * coef;
-      if (wd != 0.f) gr += wd * ps[e];
-      ms[e] = b1 * ms[e] + (1.f - b1) * gr;
-      vs[e] = b2 * vs[e] + (1.f - b2) * gr * gr;
-      ps[e] -= stepsz * ms[e] / (sqrtf(vs[e]) / bc2_sqrt + eps);
-    }
-    p4[i] = pp;
-    m4[i] = mm;
-    v4[i] = vv;
-    if (mirror) {
-      bf16x4 o = {f2bf(ps[0]), f2bf(ps[1]), f2bf(ps[2]), f2bf(ps[3])};
-      ((bf16x4*)mirror)[i] = o;
+      for (int k = 0; k < 4; ++k) {
+        float gr = gs[k] * coef;
+        if (wd != 0.f) gr += wd * ps[k];
+        ms[k] = b1 * ms[k] + (1.f - b1) * gr;
+        vs[k] = b2 * vs[k] + (1.f - b2) * gr * gr;
+        ps[k] -= stepsz * ms[k] / (sqrtf(vs[k]) / bc2_sqrt + eps);
+      }
+      p4[i] = pp;
+      m4[i] = mm;
+      v4[i] = vv;
+      if (mirror) {
+        bf16x4 o = {f2bf(ps[0]), f2bf(ps[1]), f2bf(ps[2]), f2bf(ps[3])};
+        ((bf16x4*)mirror)[i] = o;
+      }
     }
   }
 }
 
-// ``skipped`` (nullable) enables the non-finite-gradient guard: the global norm is then always computed and a
-// step whose gradient contains inf/nan leaves weights, moments and the step counter untouched.
-IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, void* mirror, long n, float* part, int nparts,
-                             float clip, float lr, float b1, float b2, float eps, float wd, int* step, int* skipped,
-                             void* stream) {
+// ``spans`` is a device array of ``nspans`` Span records (iit_adam_span_size() bytes each).  ``skipped``
+// (nullable) enables the non-finite-gradient guard: the global norm is then always computed and a step whose
+// gradient contains inf/nan leaves weights, moments and the step counter untouched.
+IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, void* mirror, const void* spans, int nspans,
+                             float* part, int nparts, float clip, float lr, float b1, float b2, float eps, float wd,
+                             int* step, int* skipped, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const long n4 = n / 4;
   const bool norm = clip > 0.f || skipped != nullptr;
-  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(norm ? nparts : 1), dim3(256), 0, s, g, n4, part, (int)norm, step);
-  const int blocks = (int)min((n4 + 255) / 256, 8192L);
-  hipLaunchKernelGGL(adam_flat_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, n4, part, nparts,
-                     clip, lr, b1, b2, eps, wd, step, skipped);
+  const Span* sp = (const Span*)spans;
+  hipLaunchKernelGGL(sumsq_span_kernel, dim3(norm ? nparts : 1), dim3(256), 0, s, g, sp, nspans, part, (int)norm,
+                     step);
+  const int blocks = min(nspans, 4096);
+  hipLaunchKernelGGL(adam_span_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, sp, nspans, part,
+                     nparts, clip, lr, b1, b2, eps, wd, step, skipped);
   return hipGetLastError();
 }
+
+IIT_EXPORT int iit_adam_span_size() { return (int)sizeof(Span); }
 
 // ============================================================================ shadow weights
 // dst (bf16) = src (fp32) viewed as [rows][cols]; transpose -> dst[c][r] with leading dim ld.
@@ -626,39 +843,37 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x,
 }
 
 // Vectorised variant: 256 threads = 32 column groups (16 B each: 8 bf16 / 4 fp32 columns) x 8 row groups,
-// 128 rows per block; LDS combine over row groups, one fp32 atomic per column per block.
+// R rows per block (R % 8 == 0, chosen so the grid fills the 256 CUs); LDS combine over row groups, one fp32
+// atomic per column per block.
 template <bool F32>
 __global__ __launch_bounds__(256) void colsum_vec_kernel(const void* __restrict__ x, long ld, float* __restrict__ out,
-                                                         int T, int N) {
+                                                         int T, int N, int R) {
   constexpr int CPT = F32 ? 4 : 8;  // columns per thread
   __shared__ float part[8][32 * CPT];
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int c0 = (blockIdx.x * 32 + cg) * CPT;
-  const int t0 = blockIdx.y * 128;
+  const int t0 = blockIdx.y * R;
+  const int t1 = min(T, t0 + R);
   float acc[CPT];
 #pragma unroll
   for (int e = 0; e < CPT; ++e) acc[e] = 0.f;
   if (c0 < N) {
 #pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-      const int t = t0 + rg + 8 * i;
-      if (t < T) {
-        if (F32) {
-          const float4 v = *(const float4*)((const float*)x + (long)t * ld + c0);
-          acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
-        } else {
-          const bf16x8 v = *(const bf16x8*)((const __bf16*)x + (long)t * ld + c0);
+    for (int t = t0 + rg; t < t1; t += 8) {
+      if (F32) {
+        const float4 v = *(const float4*)((const float*)x + (long)t * ld + c0);
+        acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+      } else {
+        const bf16x8 v = *(const bf16x8*)((const __bf16*)x + (long)t * ld + c0);
 #pragma unroll
-          for (int e = 0; e < CPT; ++e) acc[e] += bf2f(v[e]);
-        }
+        for (int e = 0; e < CPT; ++e) acc[e] += bf2f(v[e]);
       }
     }
   }
 #pragma unroll
   for (int e = 0; e < CPT; ++e) part[rg][cg * CPT + e] = acc[e];
   __syncthreads();
-  const int col = threadIdx.x;  // 256 threads cover the block's 32*CPT columns (CPT=8) or twice (CPT=4)
-  if (col < 32 * CPT) {
+  for (int col = threadIdx.x; col < 32 * CPT; col += 256) {
     float s = 0.f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) s += part[r][col];
@@ -671,14 +886,62 @@ IIT_EXPORT int iit_colsum_accum(const void* x, int f32, long ld, float* out, int
   const int cpt = f32 ? 4 : 8;
   const bool vec = (N % cpt == 0) && (ld % cpt == 0) && ((((uintptr_t)x) & 15) == 0);
   if (vec) {
-    dim3 grid((N + 32 * cpt - 1) / (32 * cpt), (T + 127) / 128);
-    if (f32) hipLaunchKernelGGL(colsum_vec_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
-    else hipLaunchKernelGGL(colsum_vec_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
+    const int gx = (N + 32 * cpt - 1) / (32 * cpt);
+    // rows per block: aim for >= ~1024 blocks (4 per CU) without dropping below 32 rows per block
+    int R = 256;
+    while (R > 32 && (long)gx * ((T + R - 1) / R) < 1024) R >>= 1;
+    dim3 grid(gx, (T + R - 1) / R);
+    if (f32) hipLaunchKernelGGL(colsum_vec_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N, R);
+    else hipLaunchKernelGGL(colsum_vec_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N, R);
     return hipGetLastError();
   }
   dim3 grid((N + 63) / 64, (T + 63) / 64);
   if (f32) hipLaunchKernelGGL(colsum_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
   else hipLaunchKernelGGL(colsum_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, out, T, N);
+  return hipGetLastError();
+}
+
+// out = gelu_new(pre)  (bf16 -> bf16, strided rows; 8 elements / 16 B per thread when aligned)
+__device__ __forceinline__ float gelu_new_fast(float x) {
+  // tanh(u) = 1 - 2 / (exp(2u) + 1): one exp + one fast reciprocal instead of libm tanhf
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  const float t = 1.f - 2.f * __frcp_rn(__expf(2.f * u) + 1.f);
+  return 0.5f * x * (1.f + t);
+}
+
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const __bf16* __restrict__ pre, long ldp, __bf16* __restrict__ out,
+                                                       long ldo, int M, int N) {
+  const int n8 = N >> 3;
+  const long total = (long)M * n8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int m = (int)(i / n8), c = (int)(i % n8) * 8;
+    const bf16x8 x = *(const bf16x8*)(pre + m * ldp + c);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_new_fast(bf2f(x[e])));
+    *(bf16x8*)(out + m * ldo + c) = o;
+  }
+}
+
+__global__ void gelu_fwd_scalar_kernel(const __bf16* __restrict__ pre, long ldp, __bf16* __restrict__ out, long ldo,
+                                       int M, int N) {
+  const long total = (long)M * N;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int m = (int)(i / N), n = (int)(i % N);
+    out[m * ldo + n] = f2bf(gelu_new_fast(bf2f(pre[m * ldp + n])));
+  }
+}
+
+IIT_EXPORT int iit_gelu_fwd(const void* pre, long ldp, void* out, long ldo, int M, int N, void* stream) {
+  const bool vec = N % 8 == 0 && ldp % 8 == 0 && ldo % 8 == 0 && ((((uintptr_t)pre) | ((uintptr_t)out)) & 15) == 0;
+  const long work = vec ? (long)M * (N / 8) : (long)M * N;
+  const int blocks = (int)min((work + 255) / 256, 8192L);
+  if (vec)
+    hipLaunchKernelGGL(gelu_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const __bf16*)pre, ldp,
+                       (__bf16*)out, ldo, M, N);
+  else
+    hipLaunchKernelGGL(gelu_fwd_scalar_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const __bf16*)pre,
+                       ldp, (__bf16*)out, ldo, M, N);
   return hipGetLastError();
 }
 

@@ -88,6 +88,9 @@ class FlatParams:
         self.index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
         self.version = 0
         self.mirror_version = -1
+        self._inactive: Dict[int, Tuple[int, int, torch.Tensor]] = {}  # param index -> (offset, row_len, live rows)
+        self.restrict_version = 0
+        self._span_cache = None
         self._listeners = []
         module._flat_params = self
         if with_bf16_shadow:
@@ -106,6 +109,78 @@ class FlatParams:
     def owns(self, p: torch.Tensor) -> bool:
         base = self.data.data_ptr()
         return base <= p.data_ptr() < base + self.numel * 4
+
+    # ---------------------------------------------------------------- sparse rows
+    def restrict_rows(self, p: torch.Tensor, live_rows: Optional[torch.Tensor]) -> bool:
+        """Declare that only ``live_rows`` of the 2-D parameter ``p`` can ever receive gradient (embedding rows
+        of the tokens a dataset contains, positional rows below its sequence length).  The fused optimizer then
+        skips the other rows: with zero gradient and zero Adam moments (and no weight decay) an Adam step leaves
+        them bit-identical, so this is exact.  ``live_rows=None`` lifts the restriction.  Returns whether the
+        restriction applies (it needs a plain, non-grouped slot whose rows are whole float4 groups)."""
+        i = self.index.get(id(p))
+        if i is None:
+            return False
+        if live_rows is None:
+            self._inactive.pop(i, None)
+        else:
+            if p.dim() != 2 or not p.is_contiguous() or p.shape[1] % 4:
+                return False
+            off = self.offset_of(p)
+            if off % 4:
+                return False
+            rows = torch.unique(live_rows.detach().long().cpu())
+            rows = rows[(rows >= 0) & (rows < p.shape[0])]
+            self._inactive[i] = (off, int(p.shape[1]), rows)
+        self.restrict_version += 1
+        self._span_cache = None
+        return True
+
+    def inactive_ranges(self) -> List[Tuple[int, int]]:
+        """Sorted (start, end) element ranges the optimizer may skip."""
+        out = []
+        for i, (off, d, rows) in self._inactive.items():
+            n = self.params[i].shape[0]
+            live = torch.zeros(n, dtype=torch.bool)
+            live[rows] = True
+            r = 0
+            while r < n:
+                if live[r]:
+                    r += 1
+                    continue
+                r0 = r
+                while r < n and not live[r]:
+                    r += 1
+                out.append((off + r0 * d, off + r * d))
+        return sorted(out)
+
+    def span_table(self, span_bytes: int = 16, max_len4: int = 1024, restricted: bool = True):
+        """Device table of (start4, len4) spans covering the active arena (``restricted=False``: all of it), as
+        read by the fused optimizer kernels.  Cached until the restriction changes."""
+        key = (restricted, max_len4)
+        if self._span_cache is not None and self._span_cache[0] == key:
+            return self._span_cache[1], self._span_cache[2]
+        assert span_bytes == 16
+        n4 = self.numel // 4
+        gaps = [(a // 4, b // 4) for a, b in self.inactive_ranges()] if restricted else []
+        spans = []
+        pos = 0
+        for a, b in gaps + [(n4, n4)]:
+            while pos < a:
+                ln = min(max_len4, a - pos)
+                spans.append((pos, ln))
+                pos += ln
+            pos = max(pos, b)
+        tab = torch.tensor(spans if spans else [(0, 0)], dtype=torch.int64).view(-1, 2).to(self.data.device)
+        self._span_cache = (key, tab, len(spans))
+        return tab, len(spans)
+
+    def check_inactive_zero(self, *tensors: torch.Tensor) -> bool:
+        """True when every skipped range is zero in each given arena-shaped tensor (default: the gradient)."""
+        for t in tensors or (self.grad,):
+            for a, b in self.inactive_ranges():
+                if bool(t[a:b].any()):
+                    return False
+        return True
 
     # ---------------------------------------------------------------- grads
     def zero_grad(self) -> None:

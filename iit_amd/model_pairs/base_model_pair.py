@@ -66,6 +66,19 @@ def dataset_token_ids(dataset) -> Optional[Tensor]:
     return None
 
 
+def dataset_seq_len(dataset) -> Optional[int]:
+    """Input sequence length of a token dataset (``x`` of its first item is ``[S]``), or None."""
+    try:
+        x = dataset[0][0]
+    except Exception:  # noqa: BLE001 - any dataset shape
+        return None
+    if isinstance(x, (tuple, list)):
+        x = x[0]
+    if isinstance(x, Tensor) and x.dim() == 1 and not x.dtype.is_floating_point:
+        return int(x.shape[0])
+    return None
+
+
 def _ll_nodes_of(corr, hl_node) -> List[LLNode]:
     v = corr[hl_node]
     if isinstance(v, LLNode):
@@ -270,17 +283,38 @@ class BaseModelPair(ABC):
             self._reducer = GradReducer(flat, bucket_mb=self.training_args.get("bucket_mb", 64.0),
                                         overlap=self.training_args.get("overlap_allreduce", True))
 
-    def restrict_embedding_reduce(self, dataset) -> None:
-        """Data parallel: all-reduce only the embedding rows of tokens the dataset contains (exact: no
-        other row can receive gradient).  No-op without a reducer or a token-id source."""
-        reducer = getattr(self, "_reducer", None)
+    def restrict_sparse_rows(self, dataset, optimizer_rows: bool = True) -> None:
+        """Exploit the gradient sparsity of the embedding tables for ``dataset``:
+
+        * only the ``W_E`` rows of tokens the dataset contains and the ``W_pos`` rows below its sequence
+          length can receive gradient, so data parallelism all-reduces just those rows, and
+        * (``optimizer_rows``) the fused optimizer skips the other rows -- zero gradient and zero moments
+          make their Adam update the identity (checked on the first step; no weight decay), so both are
+          exact.  Training on inputs outside the dataset afterwards needs ``restrict_sparse_rows(None)``.
+        """
         module = self._ll_module()
+        flat = getattr(module, "_flat_params", None)
+        reducer = getattr(self, "_reducer", None)
         embed = getattr(getattr(module, "embed", None), "W_E", None)
-        if reducer is None or embed is None or id(embed) not in reducer.flat.index:
-            return
-        ids = dataset_token_ids(dataset)
-        if ids is not None:
-            reducer.set_row_subset(embed, ids)
+        pos = getattr(getattr(module, "pos_embed", None), "W_pos", None)
+        ids = dataset_token_ids(dataset) if dataset is not None else None
+        seq = dataset_seq_len(dataset) if dataset is not None else None
+        rows = []
+        if embed is not None and ids is not None:
+            rows.append((embed, ids))
+        if pos is not None and seq is not None:
+            rows.append((pos, torch.arange(min(seq, pos.shape[0]))))
+        if dataset is None:
+            rows = [(p, None) for p in (embed, pos) if p is not None]
+        for p, r in rows:
+            if reducer is not None and id(p) in reducer.flat.index and r is not None:
+                reducer.set_row_subset(p, r.to(p.device))
+            if optimizer_rows and flat is not None:
+                flat.restrict_rows(p, r)
+
+    def restrict_embedding_reduce(self, dataset) -> None:
+        """Data-parallel part of :meth:`restrict_sparse_rows` only (reduce just the live embedding rows)."""
+        self.restrict_sparse_rows(dataset, optimizer_rows=False)
 
     def backward(self, loss: Tensor) -> None:
         """``loss.backward()`` + data-parallel gradient averaging + reference grad semantics."""

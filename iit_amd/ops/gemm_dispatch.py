@@ -98,7 +98,10 @@ def _addmm_f32(c, base, a, b) -> None:
 
 
 def _gelu_into(pre, out) -> None:
-    torch._C._nn.gelu(pre, approximate="tanh", out=out)
+    if pre.is_cuda and pre.dtype == BF16 and out.dtype == BF16 and pre.dim() == 2:
+        K.gelu_fwd(pre, out, pre.shape[0], pre.shape[1])
+    else:
+        torch._C._nn.gelu(pre, approximate="tanh", out=out)
 
 
 def _blas(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, C2, C3, bias0, bias1, bias2, resid, ldr, aux, ldc2, bias_cols,

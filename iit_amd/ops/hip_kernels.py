@@ -29,7 +29,7 @@ _SIGS = {
     "iit_embed_pos_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_embed_pos_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_ln_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
-    "iit_ln_bwd": [c_void_p, c_int] + [c_void_p] * 8 + [c_int, c_int, c_int, c_void_p],
+    "iit_ln_bwd": [c_void_p, c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_void_p],
     "iit_attn_small_fwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float, c_int,
                                             c_void_p],
     "iit_attn_small_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
@@ -39,7 +39,9 @@ _SIGS = {
     "iit_ce_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "iit_ce_bwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_long, c_int, c_int, c_int,
                    c_void_p],
-    "iit_adam_flat": [c_void_p] * 5 + [c_long, c_void_p, c_int] + [c_float] * 6 + [c_void_p, c_void_p, c_void_p],
+    "iit_adam_flat": [c_void_p] * 6 + [c_int, c_void_p, c_int] + [c_float] * 6 + [c_void_p, c_void_p, c_void_p],
+    "iit_adam_span_size": [],
+    "iit_gelu_fwd": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_void_p],
     "iit_shadow_refresh": [c_void_p, c_int, c_void_p],
     "iit_shadow_desc_size": [],
     "iit_colsum_accum": [c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_void_p],
@@ -130,10 +132,10 @@ def ln_fwd(x, w, b, y, mean, rstd, T, d, eps):
     _check(lib().iit_ln_fwd(_p(x), _p(w), _p(b), _p(y), _p(mean), _p(rstd), T, d, eps, _stream()), "ln_fwd")
 
 
-def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False, dres=None):
-    """dx = LN'(dy) (+ dres, the skip-connection gradient, fp32 [T, d])."""
+def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False, dres=None, dx16=None):
+    """dx = LN'(dy) (+ dres, the skip-connection gradient, fp32 [T, d]); ``dx16`` (optional) gets a bf16 copy."""
     _check(lib().iit_ln_bwd(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx),
-                            _p(dres), _p(dw), _p(db), T, d, int(accumulate), _stream()), "ln_bwd")
+                            _p(dres), _p(dx16), _p(dw), _p(db), T, d, int(accumulate), _stream()), "ln_bwd")
 
 
 def heads_to_mask(heads: Optional[Sequence[int]]) -> int:
@@ -186,6 +188,11 @@ def colsum3_accum(x, ld, outs, T, N):
         colsum_accum(x[:, i * N:], ld, o, T, N)
 
 
+def gelu_fwd(pre, out, M, N):
+    """out = gelu_new(pre), bf16 [M, N] views with unit column stride (any row strides)."""
+    _check(lib().iit_gelu_fwd(_p(pre), pre.stride(0), _p(out), out.stride(0), M, N, _stream()), "gelu_fwd")
+
+
 def dgelu(dpost, pre, out):
     _check(lib().iit_dgelu(_p(dpost), _p(pre), _p(out), dpost.numel(), _stream()), "dgelu")
 
@@ -216,14 +223,15 @@ def make_shadow_descs(entries, device) -> torch.Tensor:
 
 
 def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_norm, skipped=None):
-    """Fused clip + Adam over the arena; bumps the device step counter ``step_dev`` (int32[1]) and writes the
-    bf16 mirror (``flat.shadow``) when present.  No host scalars depend on the step: graph-capturable."""
-    n = flat.numel
+    """Fused clip + Adam over the arena's active spans (``flat.active_spans``); bumps the device step counter
+    ``step_dev`` (int32[1]) and writes the bf16 mirror (``flat.shadow``) when present.  No host scalars depend
+    on the step: graph-capturable."""
     nparts = 1024
     part = getattr(flat, "_norm_parts", None)
     if part is None or part.numel() < nparts:
         part = flat._norm_parts = torch.zeros(nparts, dtype=torch.float32, device=flat.data.device)
-    _check(lib().iit_adam_flat(_p(flat.data), _p(flat.grad), _p(exp_avg), _p(exp_avg_sq), _p(flat.shadow), n,
-                               _p(part), nparts, float(clip_norm or 0.0), lr, b1, b2, eps, wd, _p(step_dev),
-                               _p(skipped), _stream()), "adam_flat")
+    spans, nspans = flat.span_table(lib().iit_adam_span_size())
+    _check(lib().iit_adam_flat(_p(flat.data), _p(flat.grad), _p(exp_avg), _p(exp_avg_sq), _p(flat.shadow),
+                               _p(spans), nspans, _p(part), nparts, float(clip_norm or 0.0), lr, b1, b2, eps, wd,
+                               _p(step_dev), _p(skipped), _stream()), "adam_flat")
     flat.after_step(mirror_written=flat.shadow is not None)

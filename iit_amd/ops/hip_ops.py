@@ -291,12 +291,32 @@ class LayerNormFn(Function):
         w, b = ctx.params
         T, d = x2.shape
         dx = torch.empty(T, d, dtype=F32, device=x2.device)
+        dx16 = torch.empty(T, d, dtype=BF16, device=x2.device) if ctx.in_dtype == F32 else None
         dw = _grad_slot(w) if w is not None else None
         db = _grad_slot(b) if b is not None else None
-        K.ln_bwd(_flat2(dy.contiguous()), x2, mean, rstd, w, dx, dw, db, T, d)
+        K.ln_bwd(_flat2(dy.contiguous()), x2, mean, rstd, w, dx, dw, db, T, d, dx16=dx16)
         _done(w, b)
         dx = dx.view(*dy.shape[:-1], d)
-        return (dx if ctx.in_dtype == F32 else dx.to(ctx.in_dtype)), None, None, None
+        if dx16 is None:
+            return dx.to(ctx.in_dtype), None, None, None
+        _set_bf16_twin(dx, dx16)
+        return dx, None, None, None
+
+
+def _set_bf16_twin(t: torch.Tensor, t16: torch.Tensor) -> None:
+    """Attach a bf16 copy to an fp32 gradient: its producer wrote both in one pass, so the consuming
+    backward GEMMs skip a separate cast.  Tensor attributes survive autograd hand-off when the gradient
+    has a single consumer; when autograd sums several gradients the twin is simply absent."""
+    t._iit_bf16 = (t.data_ptr(), t._version, t16)
+
+
+def _bf16_of(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype == BF16:
+        return t
+    twin = getattr(t, "_iit_bf16", None)
+    if twin is not None and twin[0] == t.data_ptr() and twin[1] == t._version and twin[2].numel() == t.numel():
+        return twin[2].view(t.shape)
+    return t.to(BF16)
 
 
 class LayerNormForkFn(Function):
@@ -330,12 +350,16 @@ class LayerNormForkFn(Function):
         if dpass is not None:
             dres = _flat2(dpass.float().contiguous())
         dx = torch.empty(T, d, dtype=F32, device=x2.device)
+        dx16 = torch.empty(T, d, dtype=BF16, device=x2.device) if ctx.in_dtype == F32 else None
         dw = _grad_slot(w) if w is not None else None
         db = _grad_slot(b) if b is not None else None
-        K.ln_bwd(_flat2(dy.contiguous()), x2, mean, rstd, w, dx, dw, db, T, d, dres=dres)
+        K.ln_bwd(_flat2(dy.contiguous()), x2, mean, rstd, w, dx, dw, db, T, d, dres=dres, dx16=dx16)
         _done(w, b)
         dx = dx.view(*dy.shape[:-1], d)
-        return (dx if ctx.in_dtype == F32 else dx.to(ctx.in_dtype)), None, None, None
+        if dx16 is None:
+            return dx.to(ctx.in_dtype), None, None, None
+        _set_bf16_twin(dx, dx16)
+        return dx, None, None, None
 
 
 def _packed3(a: Optional[torch.Tensor], b: Optional[torch.Tensor], c: Optional[torch.Tensor], n: int) -> bool:
@@ -479,7 +503,7 @@ class LinearFn(Function):
         # one bf16 copy of an fp32 gradient (residual-stream outputs) serves both GEMMs and the bias sum;
         # the skip connection keeps the fp32 gradient
         gres = gy if out_kind == "resid" else None
-        g16 = gy if gy.dtype == BF16 else gy.to(BF16)
+        g16 = _bf16_of(gy)
         g2 = _aligned_rows(g16, T, N)
         ldg = g2.stride(0)
         dx = None

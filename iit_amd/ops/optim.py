@@ -69,6 +69,7 @@ class FusedAdam(torch.optim.Optimizer):
         if self._hip is not None:
             from . import hip_kernels
             self.step_count += 1
+            self._validate_restriction(wd)
             hip_kernels.adam_step(self.flat, self.exp_avg, self.exp_avg_sq, self._step_dev, lr=lr, b1=b1, b2=b2,
                                   eps=eps, wd=wd, clip_norm=clip_norm,
                                   skipped=self._skipped_dev if self.nan_guard else None)
@@ -91,6 +92,21 @@ class FusedAdam(torch.optim.Optimizer):
         denom = (self.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(eps)
         self.flat.data.addcdiv_(self.exp_avg, denom, value=-lr / bc1)
         self.flat.after_step()
+
+    def _validate_restriction(self, wd: float) -> None:
+        """Row restriction (``FlatParams.restrict_rows``) is exact only without weight decay and with zero
+        moments on the skipped rows; checked once per restriction change (outside graph capture)."""
+        flat = self.flat
+        if not flat._inactive or getattr(self, "_restrict_ok_version", None) == flat.restrict_version:
+            return
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return
+        ok = wd == 0 and flat.check_inactive_zero(self.exp_avg, self.exp_avg_sq, flat.grad)
+        if not ok:
+            flat._inactive.clear()
+            flat._span_cache = None
+            flat.restrict_version += 1
+        self._restrict_ok_version = flat.restrict_version
 
     # ---------------------------------------------------------------- checkpointing
     def state_dict(self):

@@ -108,3 +108,29 @@ def test_frozen_attention_falls_back_to_contiguous():
     FlatParams(m)
     a = m.blocks[0].attn
     assert a.W_Q.is_contiguous() and a.W_V.is_contiguous()
+
+
+def test_row_restriction_span_table():
+    """Span table covers the arena minus the dead embedding rows, in <= max_len4 float4 pieces."""
+    m = torch.nn.ModuleDict({"emb": torch.nn.Embedding(100, 8), "lin": torch.nn.Linear(8, 3)})
+    flat = FlatParams(m)
+    full, nfull = flat.span_table(max_len4=16, restricted=False)
+    assert int(full[:, 1].sum()) * 4 == flat.numel and nfull == full.shape[0]
+    assert flat.restrict_rows(m["emb"].weight, torch.tensor([0, 1, 2, 50, 99, 99]))
+    tab, n = flat.span_table(max_len4=16)
+    covered = torch.zeros(flat.numel, dtype=torch.bool)
+    for st, ln in tab.tolist():
+        assert 0 < ln <= 16
+        covered[st * 4:(st + ln) * 4] = True
+    off = flat.offset_of(m["emb"].weight)
+    live = torch.zeros(100, dtype=torch.bool)
+    live[[0, 1, 2, 50, 99]] = True
+    for r in range(100):
+        assert bool(covered[off + r * 8:off + (r + 1) * 8].all()) == bool(live[r])
+    rest = torch.ones(flat.numel, dtype=torch.bool)
+    rest[off:off + 800] = False
+    assert bool(covered[rest].all())
+    assert flat.check_inactive_zero()
+    flat.grad[off + 3 * 8] = 1.0
+    assert not flat.check_inactive_zero()
+    assert flat.restrict_rows(m["emb"].weight, None) and not flat.inactive_ranges()

@@ -95,25 +95,60 @@ def test_gemm_fp32_a_residual_gelu(K):
     assert rel_err(post, gelu_new(ref_pre)) < 1e-2
 
 
-def test_layernorm(K):
+@pytest.mark.parametrize("d,affine,bf16_dy", [(768, False, False), (768, True, True), (130, True, False),
+                                              (4096, False, True), (66, False, False)])
+def test_layernorm(K, d, affine, bf16_dy):
+    """Vector (d % 4 == 0) and scalar kernels; affine dw/db reduction; fused skip gradient + bf16 twin."""
     torch.manual_seed(4)
-    T, d = 1000, 768
+    T = 1000
     x = torch.randn(T, d, device=dev) * 3 + 1
+    w = torch.randn(d, device=dev) if affine else None
+    b = torch.randn(d, device=dev) if affine else None
     y = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
     mean = torch.empty(T, device=dev)
     rstd = torch.empty(T, device=dev)
-    K.ln_fwd(x, None, None, y, mean, rstd, T, d, 1e-5)
-    xc = x - x.mean(-1, keepdim=True)
-    ref = xc / (xc.pow(2).mean(-1, keepdim=True) + 1e-5).sqrt()
-    assert rel_err(y, ref) < 1e-2
+    K.ln_fwd(x, w, b, y, mean, rstd, T, d, 1e-5)
     xr = x.clone().requires_grad_(True)
-    xc = xr - xr.mean(-1, keepdim=True)
-    out = xc / (xc.pow(2).mean(-1, keepdim=True) + 1e-5).sqrt()
+    wr = w.clone().requires_grad_(True) if affine else None
+    br = b.clone().requires_grad_(True) if affine else None
+    ref = torch.nn.functional.layer_norm(xr, (d,), wr, br, 1e-5)
+    assert rel_err(y, ref) < 1e-2
     g = torch.randn(T, d, device=dev)
-    out.backward(g)
+    if bf16_dy:
+        g = bf(g)
+    ref.backward(g.float())
+    dres = torch.randn(T, d, device=dev)
     dx = torch.empty(T, d, device=dev)
-    K.ln_bwd(g, x, mean, rstd, None, dx, None, None, T, d)
-    assert rel_err(dx, xr.grad) < 1e-3
+    dx16 = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
+    dw = torch.zeros(d, device=dev) if affine else None
+    db = torch.zeros(d, device=dev) if affine else None
+    K.ln_bwd(g, x, mean, rstd, w, dx, dw, db, T, d, dres=dres, dx16=dx16)
+    assert rel_err(dx, xr.grad + dres) < 1e-3
+    assert torch.equal(dx16, dx.to(torch.bfloat16))
+    if affine:
+        assert rel_err(dw, wr.grad) < 1e-4 and rel_err(db, br.grad) < 1e-4
+
+
+def test_gelu_fwd_and_pos_bwd(K):
+    from iit_amd.ops.torch_ops import gelu_new
+    torch.manual_seed(12)
+    pre = bf(torch.randn(300, 1032, device=dev) * 3)
+    out = torch.empty(300, 1040, dtype=torch.bfloat16, device=dev)[:, :1024]
+    K.gelu_fwd(pre[:, :1024], out, 300, 1024)
+    assert rel_err(out, gelu_new(pre[:, :1024].float())) < 4e-3
+    out2 = torch.empty(300, 7, dtype=torch.bfloat16, device=dev)
+    K.gelu_fwd(pre[:, :7], out2, 300, 7)  # scalar path
+    assert rel_err(out2, gelu_new(pre[:, :7].float())) < 4e-3
+    B, S, d = 33, 16, 768
+    g = torch.randn(B * S, d, device=dev)
+    tok = torch.randint(0, 50, (B * S,), device=dev)
+    dWE = torch.zeros(50, d, device=dev)
+    dWpos = torch.randn(S + 3, d, device=dev)
+    ref_pos = dWpos.clone()
+    ref_pos[:S] += g.view(B, S, d).sum(0)
+    K.embed_pos_bwd(tok, g, dWE, dWpos, B, S, d)
+    assert torch.allclose(dWpos, ref_pos, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(dWE, torch.zeros(50, d, device=dev).index_add_(0, tok, g), atol=1e-4)
 
 
 @pytest.mark.parametrize("S,H,dh,causal", [(16, 12, 64, True), (16, 4, 16, True), (33, 3, 32, True), (5, 12, 64, True),
@@ -191,6 +226,32 @@ def test_flat_adam_matches_torch(K):
         opt2.step()
     for p1, p2 in zip(m1.parameters(), m2.parameters()):
         assert torch.allclose(p1, p2, atol=1e-5, rtol=1e-4)
+
+
+def test_flat_adam_row_restriction_is_exact(K):
+    """Skipping embedding rows that never get gradient leaves the update bit-identical to the full pass."""
+    torch.manual_seed(13)
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.ops.optim import FusedAdam
+
+    def make():
+        torch.manual_seed(13)
+        return torch.nn.ModuleDict({"emb": torch.nn.Embedding(5000, 64), "lin": torch.nn.Linear(64, 7)}).to(dev)
+
+    m1, m2 = make(), make()
+    f1, f2 = FlatParams(m1, with_bf16_shadow=True), FlatParams(m2, with_bf16_shadow=True)
+    live = torch.tensor([3, 4, 5, 900, 4999, 17])
+    assert f1.restrict_rows(m1["emb"].weight, live)
+    o1, o2 = FusedAdam(f1, lr=1e-2), FusedAdam(f2, lr=1e-2)
+    for _ in range(4):
+        idx = live[torch.randint(0, len(live), (32,))].to(dev)
+        for m, o in ((m1, o1), (m2, o2)):
+            o.zero_grad()
+            m["lin"](m["emb"](idx)).pow(2).sum().backward()
+            o.step(clip_norm=1.0)
+    assert f1._inactive, "restriction must survive the first-step validation"
+    assert torch.equal(f1.data, f2.data) and torch.equal(f1.shadow, f2.shadow)
+    assert torch.equal(o1.exp_avg, o2.exp_avg)
 
 
 def test_add_bf16_and_vector_dgelu(K):
