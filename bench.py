@@ -125,6 +125,8 @@ def main():
         torch.cuda.synchronize()
     pdist.barrier()
     dt = time.perf_counter() - t0
+    executed = getattr(step_fn, "calls", None) or (args.warmup + args.steps)
+    print(f"[bench] train steps executed in this process: {executed}", file=sys.stderr)
     dt_t = torch.tensor([dt], dtype=torch.float64, device=dev if distributed and dev.type == "cuda" else "cpu")
     if distributed:
         torch.distributed.all_reduce(dt_t, op=torch.distributed.ReduceOp.MAX)

@@ -24,11 +24,14 @@ pair's own ``run_train_step`` -- this class only swaps the phase executor.
 Batches whose shapes differ from the captured ones (e.g. a short final batch)
 run eagerly.
 
-Data parallel: collectives are never captured.  Each phase becomes two graphs
-around an eager gradient all-reduce -- ``[forward + backward]`` -> bucketed
-RCCL all-reduce of the gradient arena -> ``[clip + Adam]`` -- so every rank issues
-the identical collective sequence whatever gets captured, and the launch-bound
-compute still runs as replays.  (``IIT_GRAPHS_DP=0`` keeps DP runs fully eager.)
+Data parallel: collectives are never captured.  Each phase becomes graphs
+around eager gradient all-reduces -- ``[forward + backward of the top layers]``,
+then one graph per lower stage of layers, each followed by the bucketed RCCL
+all-reduce of the arena range it finished (overlapping the next stage, see
+:mod:`iit_amd.engine.staged`; ``IIT_DP_STAGES``, default 4), then ``[clip +
+Adam]`` -- so every rank issues the identical collective sequence whatever gets
+captured, and the launch-bound compute still runs as replays.
+(``IIT_GRAPHS_DP=0`` keeps DP runs fully eager.)
 """
 from __future__ import annotations
 
@@ -66,9 +69,16 @@ class GraphedTrainStep:
                 enabled = False
         self.enabled = enabled
         self.split = ws > 1  # DP: graphs around the (eager) gradient all-reduce
+        self.staged = None
+        if self.split and enabled:
+            from .staged import staged_for
+            self.staged = staged_for(pair)
+            reducer = getattr(pair, "_reducer", None)
+            if self.staged is not None and reducer is not None:
+                reducer.segment_buckets(self.staged.edges)
         self.graphs: Dict[Tuple, Tuple[torch.cuda.CUDAGraph, object]] = {}
         self.seen: Dict[Tuple, int] = {}
-        self.pool = torch.cuda.graph_pool_handle() if enabled else None
+        self.pool = None  # shared graph memory pool, created at the first capture
         if enabled:
             from ..ops.gemm_dispatch import select_graph_safe_blas
             select_graph_safe_blas()
@@ -76,6 +86,7 @@ class GraphedTrainStep:
         self._sig = None
         self.captures = 0
         self.replays = 0
+        self.calls = 0
         self.failed: Dict[Tuple, str] = {}
         pair._phase_runner = self._run_phase
 
@@ -109,12 +120,22 @@ class GraphedTrainStep:
         return getattr(step_fn, "__func__", None) is IITBehaviorModelPair.step_on_loss
 
     def _run_split_phase(self, full, key, compute_loss, optimizer):
-        """DP phase: graph(forward + backward) -> eager all-reduce -> graph(clip + Adam)."""
+        """DP phase: graph(forward + backward) -> eager all-reduce -> graph(clip + Adam).
+
+        With a :class:`~iit_amd.engine.staged.StagedBackward` the backward is several graphs (one per stage
+        of layers) and each stage's gradient range is all-reduced while the next stage computes."""
         pair = self.pair
         reducer = getattr(pair, "_reducer", None)
+        stg = self.staged if reducer is not None and reducer.enabled else None
 
         def fwd_bwd():
-            out = compute_loss()
+            if stg is not None:
+                stg.arm()
+            try:
+                out = compute_loss()
+            finally:
+                if stg is not None:
+                    stg.disarm()
             loss = out[0] if isinstance(out, tuple) else out
             optimizer.zero_grad()
             if reducer is not None:
@@ -130,37 +151,65 @@ class GraphedTrainStep:
             pair.clip_grad_fn(optimizer)
             pair.optimizer_step(optimizer)
 
+        def reduce_eagerly(run_stage):
+            """Host side of the collective schedule (identical on every rank); ``run_stage(i, k)`` computes stage i."""
+            if reducer is None:
+                for i, k in enumerate(stg.stages() if stg is not None else ()):
+                    run_stage(i, k)
+                return
+            reducer.start()
+            if stg is None:
+                reducer.launch_range(0, reducer.flat.numel)
+            else:
+                rng = stg.ranges()
+                reducer.launch_range(*rng[0])
+                for i, k in enumerate(stg.stages()):
+                    run_stage(i, k)
+                    reducer.launch_range(*rng[i + 1])
+            reducer.finish()
+
+        def eager_phase():
+            out = fwd_bwd()
+            reduce_eagerly(lambda i, k: stg.run_stage(k))
+            if stg is not None:
+                stg.release()
+            update()
+            return out
+
         ent = self.graphs.get(full)
         if ent is None:
             n = self.seen.get(full, 0)
             if n < self.warmup or full in self.failed:
                 self.seen[full] = n + 1
-                out = fwd_bwd()
-                if reducer is not None:
-                    reducer.reduce_all()
-                update()
-                return out
+                return eager_phase()
+            if self.pool is None:
+                self.pool = torch.cuda.graph_pool_handle()
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            gs = []
             try:
                 with torch.cuda.graph(ga, pool=self.pool):
                     static_out = fwd_bwd()
+                for k in (stg.stages() if stg is not None else ()):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=self.pool):
+                        stg.run_stage(k)
+                    gs.append(g)
+                if stg is not None:
+                    stg.release()
                 with torch.cuda.graph(gb, pool=self.pool):
                     update()
             except Exception as e:
                 self.failed[full] = repr(e)
                 print(f"[iit graphs] DP phase {key} not captured ({type(e).__name__}: {str(e)[:160]}); eager")
                 torch.cuda.synchronize()
-                out = fwd_bwd()
-                if reducer is not None:
-                    reducer.reduce_all()
-                update()
-                return out
-            ent = self.graphs[full] = ((ga, gb), static_out)
+                if stg is not None:
+                    stg.release()
+                return eager_phase()
+            ent = self.graphs[full] = ((ga, gs, gb), static_out)
             self.captures += 1
-        (ga, gb), static_out = ent
+        (ga, gs, gb), static_out = ent
         ga.replay()
-        if reducer is not None:
-            reducer.reduce_all()
+        reduce_eagerly(lambda i, k: gs[i].replay())
         gb.replay()
         self.replays += 1
         return _clone_out(static_out)
@@ -181,6 +230,8 @@ class GraphedTrainStep:
                 return self._eager(compute_loss, optimizer, step_fn)
             if full in self.failed:
                 return self._eager(compute_loss, optimizer, step_fn)
+            if self.pool is None:
+                self.pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
             try:
                 with torch.cuda.graph(g, pool=self.pool):
@@ -207,6 +258,7 @@ class GraphedTrainStep:
     def __call__(self, base_input, ablation_input, loss_fn=None, optimizer=None):
         loss_fn = loss_fn or self.loss_fn
         optimizer = optimizer or self.optimizer
+        self.calls += 1
         sb, sa, eager = self._stage(base_input, ablation_input)
         self._current_eager = eager
         try:

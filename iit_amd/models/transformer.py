@@ -490,7 +490,13 @@ class HookedTransformer(HookedRootModule):
         try:
             resid = self._embed(tokens, run)
             n_blocks = len(self.blocks) if stop_at_layer is None else stop_at_layer
-            for block in self.blocks[:n_blocks]:
+            cuts = self.__dict__.get("_grad_cuts") if torch.is_grad_enabled() else None
+            for li, block in enumerate(self.blocks[:n_blocks]):
+                if cuts and li in cuts and resid.requires_grad:
+                    # staged backward (engine.graphs): the backward stops here and resumes as its own segment
+                    leaf = resid.detach().requires_grad_(True)
+                    self._cut_log.append((li, resid, leaf))
+                    resid = leaf
                 resid = block(resid, run)
             if stop_at_layer is not None:
                 return resid

@@ -33,7 +33,8 @@ class GradReducer:
         self.world = pdist.world_size()
         self.enabled = self.world > 1
         self.overlap = overlap and self.enabled
-        self.buckets = flat.buckets(int(bucket_mb * (1 << 20)))
+        self._bucket_bytes = int(bucket_mb * (1 << 20))
+        self.buckets = flat.buckets(self._bucket_bytes)
         self._use_avg = self.enabled and dist.get_backend() == "nccl"
         # parameter -> bucket id; bucket -> number of params
         self._param_bucket: List[int] = []
@@ -81,8 +82,11 @@ class GradReducer:
             return
         self._launched[b] = True
         s, e = self.buckets[b]
+        self._launch_span(s, e)
+
+    def _launch_span(self, s: int, e: int) -> None:
+        """Async all-reduce of arena elements [s, e): rows-restricted parameters compactly, the rest in place."""
         op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
-        # a parameter with a row subset is reduced compactly; the rest of the bucket in contiguous pieces
         pieces, cur = [], s
         for i, (o, n, width, rows) in sorted(self._subsets.items(), key=lambda kv: kv[1][0]):
             if o >= s and o + n <= e:
@@ -101,6 +105,46 @@ class GradReducer:
                 full = self.flat.grad[o:o + n].view(-1, width)
                 buf = full.index_select(0, rows)
                 self._works.append((dist.all_reduce(buf, op=op, async_op=True), buf, (full, rows)))
+
+    def launch_range(self, s: int, e: int) -> None:
+        """Start reducing every bucket inside arena range [s, e) now (async; ``finish`` waits).  The staged
+        graph-captured backward calls this after each backward segment so the segment's gradients travel
+        while the next segment computes.  Ranges must fall on bucket boundaries of :meth:`segment_buckets`."""
+        if not self.enabled:
+            return
+        for b, (bs, be) in enumerate(self.buckets):
+            if bs >= s and be <= e:
+                self._launch(b)
+
+    def segment_buckets(self, cuts) -> None:
+        """Re-bucket so every arena offset in ``cuts`` is a bucket edge (segment ranges reduce exactly)."""
+        edges = sorted({0, self.flat.numel, *[int(c) for c in cuts]})
+        per = max(64, int(self._bucket_bytes) // 4)
+        out = []
+        for a, b in zip(edges[:-1], edges[1:]):
+            pieces, end = [], b  # slot-aligned pieces of <= bucket size, back to front
+            while end > a:
+                start = max(a, end - per)
+                for o, n in self.flat.slots:
+                    if o <= start < o + ((n + 63) // 64) * 64:
+                        start = max(a, o)
+                        break
+                if start >= end:
+                    start = a
+                pieces.append((start, end))
+                end = start
+            out.extend(pieces)
+        self.buckets = out
+        self._param_bucket = []
+        self._bucket_count = [0] * len(self.buckets)
+        for o, n in self.flat.offsets:
+            for bi, (s, e) in enumerate(self.buckets):
+                if s <= o < e:
+                    self._param_bucket.append(bi)
+                    self._bucket_count[bi] += 1
+                    break
+        self._pending = list(self._bucket_count)
+        self._launched = [False] * len(self.buckets)
 
     def start(self):
         """Call before ``backward``: every gradient must live in the arena the buckets reduce."""

@@ -140,3 +140,71 @@ def test_dp2_embedding_row_subset_reduce_is_exact(tmp_path):
         got = torch.load(tmp_path / f"subset{i}.pt", weights_only=True)
         for n, p in ref.items():
             assert torch.allclose(got[n], p, atol=2e-5, rtol=1e-4), (i, n)
+
+
+def _worker_staged(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from iit_amd.engine.graphs import GraphedTrainStep
+    from iit_amd.parallel import dist as pdist
+    pdist.init_distributed("gloo")
+    torch.set_num_threads(2)
+    pair, train = _make(64)
+    pdist.broadcast_module(pair.ll_model)
+    opt = pair.make_optimizer(1e-3)
+    pair.restrict_sparse_rows(train)
+    # the graph runner's DP schedule, kept eager (no GPU): staged backward + per-stage range all-reduce
+    step = GraphedTrainStep(pair, opt, pair.loss_fn, warmup=10 ** 9, enabled=True)
+    assert step.split and step.staged is not None and step.staged.cuts == [1]
+    rng = step.staged.ranges()
+    assert rng[0][1] == pair._reducer.flat.numel and rng[-1][0] == 0
+    assert all(a[0] == b[1] for a, b in zip(rng, rng[1:]))  # contiguous, top to bottom
+    edges = {e for b in pair._reducer.buckets for e in b}
+    assert all(s in edges and e in edges for s, e in rng)
+    torch.manual_seed(5)
+    for i, (base, abl) in enumerate(train.make_loader(32, 0)):
+        if i >= 3:
+            break
+        step(base, abl)
+    assert not getattr(pair.ll_model, "_cut_log", [])
+    torch.save({n: p.detach().clone() for n, p in pair.ll_model.named_parameters()},
+               os.path.join(out_dir, f"staged{rank}.pt"))
+    pdist.destroy()
+
+
+def test_dp2_staged_backward_range_reduce_equals_single_process(tmp_path):
+    pair, train = _make(64)
+    _train(pair, train, per_rank_batch=64, steps=3)
+    ref = {n: p.detach().clone() for n, p in pair.ll_model.named_parameters()}
+    mp.spawn(_worker_staged, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for i in range(2):
+        got = torch.load(tmp_path / f"staged{i}.pt", weights_only=True)
+        for n, p in ref.items():
+            assert torch.allclose(got[n], p, atol=2e-5, rtol=1e-4), (i, n)
+
+
+def test_grad_cut_backward_is_exact():
+    """Cutting the residual stream and resuming the backward per stage gives plain autograd's gradients."""
+    from iit_amd.engine.staged import StagedBackward
+    from iit_amd.models.config import gpt2_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    cfg = gpt2_config_dict()
+    cfg.update(n_layers=4, d_model=16, n_heads=2, d_head=8, d_mlp=32, d_vocab=50, n_ctx=16, device="cpu")
+    torch.manual_seed(0)
+    m = HookedTransformer(cfg)
+    tok = torch.randint(0, 50, (3, 7))
+    m(tok).pow(2).mean().backward()
+    ref = {n: p.grad.clone() for n, p in m.named_parameters()}
+    m.zero_grad()
+    st = StagedBackward(m, 4)
+    assert st.cuts == [1, 2, 3] and st.flat is None
+    st.arm()
+    loss = m(tok).pow(2).mean()
+    st.disarm()
+    loss.backward()
+    assert m.blocks[0].attn.W_Q.grad is None or not m.blocks[0].attn.W_Q.grad.any()
+    for k in st.stages():
+        st.run_stage(k)
+    st.release()
+    for n, p in m.named_parameters():
+        assert torch.allclose(p.grad, ref[n], atol=1e-6, rtol=1e-5), n
