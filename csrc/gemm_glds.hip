@@ -1,0 +1,308 @@
+// LDS-DMA (global_load_lds) MFMA GEMM for gfx950: the engine's mid-size GEMMs (M, N, K multiples of the tile).
+//
+// C[M,N] = A[M,K] * B[K,N] for the three operand layouts the transformer uses:
+//   mode 0  A [M][K], B [N][K]          dX = dY W^T
+//   mode 2  A [M][K], B [K][N]          forward, TL-layout weights (bf16 arena mirror)
+//   mode 3  A [K][M], B [K][N]          weight gradients X^T dY (reduction over tokens)
+// with the epilogue fused (bias / packed-QKV bias / fp32 residual add / bias+gelu_new with the pre-activation /
+// fp32 accumulate into the gradient arena / fp32 store).
+//
+// Structure (cdna_hip_programming.md §5, "step-3" + T1/T2/T10):
+// * 256 threads = 4 wave64 as 2x2; tile BM x BN x 64; each wave a (BM/2) x (BN/2) block of 16x16 fp32
+//   accumulators fed by v_mfma_f32_16x16x32_bf16.
+// * Operands are staged global -> LDS with 16-byte global_load_lds (no VGPR round trip, no ds_write pass) into
+//   two LDS buffers: the DMA of K-tile k+1 is in flight while the MFMAs consume tile k; one barrier per K-tile.
+// * LDS images are lane-linear per wave (what LDS-DMA requires) and XOR-swizzled through the *source* address:
+//     k-contiguous [rows][64]:   16-B chunk c of row r lives at slot c ^ ((r >> 1) & 7)  -> ds_read_b128 fragment
+//                                 reads of 16 rows hit 16 distinct bank groups (conflict-free);
+//     k-major [64][cols]:         32-B block b of k-row r lives at b ^ f(r)  -> the 16 k-rows one
+//                                 ds_read_b64_tr_b16 instruction touches spread over all 64 banks (2 passes, the minimum).
+// * k-major operands (X^T dY, [K][N] weights) are transposed by the gfx950 LDS transpose read, so no operand is
+//   ever re-laid-out in memory.
+// * Bijective XCD-aware tile remap: the tiles of one XCD share A row panels in its L2.
+// * Epilogue: accumulators -> LDS (fp32 tile) -> each thread owns 8 consecutive columns of a row: 16-B / 32-B
+//   vector loads of bias / residual / accumulator and vector stores (the MFMA C layout would otherwise give
+//   2-byte column-strided stores).
+#include "common.h"
+
+namespace {
+
+enum : int { E_BF16 = 0, E_BF16_BIAS3 = 1, E_F32_RESID = 2, E_GELU = 3, E_F32_ACC = 5, E_F32_STORE = 7 };
+
+struct G2Args {
+  const __bf16* A;
+  const __bf16* B;
+  void* C;
+  void* C2;
+  const float* bias0;
+  const float* bias1;
+  const float* bias2;
+  const float* resid;
+  long lda, ldb, ldc, ldc2, ldr;
+  int M, N, K, bias_cols;
+};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+__device__ __forceinline__ void glds16(const __bf16* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+// swizzle of a k-major image: 32-B block index XOR f(k-row), chosen so the 16 k-rows {8g + q (+4)} of one
+// transpose-read instruction land on 8 distinct 32-B bank slots of the 256-B bank window
+template <int R>
+__device__ __forceinline__ int kmaj_swz(int kr) {
+  if constexpr (R == 128) return (kr & 3) | (((kr >> 3) & 1) << 2);  // 8 blocks per 256-B k-row
+  else return ((kr >> 1) & 1) | (((kr >> 3) & 1) << 1);              // R == 64: 4 blocks per 128-B k-row
+}
+
+// Stage one operand tile (R rows of the output dimension x 64 k) into its LDS image with LDS-DMA.
+template <bool KMAJ, int R>
+__device__ __forceinline__ void stage_operand(const __bf16* base, long ld, int r0g, int k0, char* img, int wave,
+                                              int lane) {
+  if constexpr (!KMAJ) {
+    // [R][64] bf16, 128-B rows; one instruction = 8 rows x 8 chunks of 16 B
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) {
+      const int r0 = i * 32 + wave * 8;
+      const int row = r0 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      glds16(base + (long)(r0g + row) * ld + k0 + c * 8, img + r0 * 128);
+    }
+  } else {
+    // [64][R] bf16, R*2-B k-rows; one instruction = (64 / (R/8)) k-rows
+    constexpr int CH = R / 8;       // 16-B chunks per k-row
+    constexpr int KRI = 64 / CH;    // k-rows per instruction
+#pragma unroll
+    for (int i = 0; i < 64 / (4 * KRI); ++i) {
+      const int kr0 = (i * 4 + wave) * KRI;
+      const int kr = kr0 + lane / CH;
+      const int ch = lane % CH;
+      const int col = (((ch >> 1) ^ kmaj_swz<R>(kr)) << 4) + ((ch & 1) << 3);
+      glds16(base + (long)(k0 + kr) * ld + r0g + col, img + kr0 * R * 2);
+    }
+  }
+}
+
+// MFMA 16x16x32 operand fragment: lane l gets X[row0 + (l & 15)][kbase + 8 * (l >> 4) + j], j = 0..7
+template <bool KMAJ, int R>
+__device__ __forceinline__ bf16x8 frag(const char* img, int row0, int kbase, int lane) {
+  if constexpr (!KMAJ) {
+    const int row = row0 + (lane & 15);
+    const int c = (kbase >> 3) + (lane >> 4);
+    return *(const bf16x8*)(img + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int kr = kbase + 8 * g + q;
+    const int col = row0 + 4 * pp;
+    const char* a0 = img + kr * (R * 2) + ((((col >> 4) ^ kmaj_swz<R>(kr))) << 5) + ((col & 15) << 1);
+    const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(a0));
+    const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(a0 + 4 * R * 2));
+    const i16x8 w = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, w);
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid % 8;
+  const int q = nwg / 8, r = nwg % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+__device__ __forceinline__ float gelu_new_dev(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  const float t = 1.f - 2.f * __frcp_rn(__expf(2.f * u) + 1.f);
+  return 0.5f * x * (1.f + t);
+}
+
+__device__ __forceinline__ void add8(float* v, const float* b) {
+  const float4 x = *(const float4*)b, y = *(const float4*)(b + 4);
+  v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
+  v[4] += y.x; v[5] += y.y; v[6] += y.z; v[7] += y.w;
+}
+
+__device__ __forceinline__ void store8_bf16(void* dst, const float* v) {
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+  *(bf16x8*)dst = o;
+}
+
+__device__ __forceinline__ void store8_f32(void* dst, const float* v) {
+  *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+  *((float4*)dst + 1) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+template <int BM, int BN, bool AKM, bool BKM, int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_glds_kernel(G2Args p) {
+  constexpr int BK = 64;
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int EPS = BN + 4;  // fp32 epilogue row stride (floats)
+  constexpr int EPI_BYTES = BM * EPS * 4;
+  constexpr int SMEM = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];  // ONE LDS object (keeps hipcc's waits counted)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = p.N / BN;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int nt = p.K / BK;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage_operand<AKM, BM>(p.A, p.lda, m0, 0, smem, wave, lane);
+  stage_operand<BKM, BN>(p.B, p.ldb, n0, 0, smem + A_BYTES, wave, lane);
+  __syncthreads();  // drains the DMA (vmcnt(0)) and publishes tile 0
+  for (int kt = 0; kt < nt; ++kt) {
+    const char* sa = smem + (kt & 1) * STAGE;
+    const char* sb = sa + A_BYTES;
+    if (kt + 1 < nt) {
+      char* na = smem + ((kt + 1) & 1) * STAGE;
+      stage_operand<AKM, BM>(p.A, p.lda, m0, (kt + 1) * BK, na, wave, lane);
+      stage_operand<BKM, BN>(p.B, p.ldb, n0, (kt + 1) * BK, na + A_BYTES, wave, lane);
+    }
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+      bf16x8 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = frag<AKM, BM>(sa, wm * WM + i * 16, s * 32, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = frag<BKM, BN>(sb, wn * WN + j * 16, s * 32, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();  // tile k+1 landed; every wave is done with tile k before it is restaged
+  }
+
+  // ---------------------------------------------------------------- epilogue via LDS
+  float* E = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WN + j * 16 + (lane & 15);
+      const int row = wm * WM + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) E[(row + r) * EPS + col] = acc[i][j][r];
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 8-column chunks per row
+#pragma unroll 2
+  for (int id = tid; id < BM * CPR; id += 256) {
+    const int lr = id / CPR, lc = (id % CPR) * 8;
+    const int row = m0 + lr, col = n0 + lc;
+    float v[8];
+    {
+      const float4 x = *(const float4*)(E + lr * EPS + lc), y = *(const float4*)(E + lr * EPS + lc + 4);
+      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    }
+    if constexpr (EPI == E_BF16) {
+      if (p.bias0) add8(v, p.bias0 + col);
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v);
+    } else if constexpr (EPI == E_BF16_BIAS3) {
+      const int w = col / p.bias_cols, o = col - w * p.bias_cols;
+      const float* bb = w == 0 ? p.bias0 : (w == 1 ? p.bias1 : p.bias2);
+      if (bb) add8(v, bb + o);
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v);
+    } else if constexpr (EPI == E_F32_RESID) {
+      if (p.bias0) add8(v, p.bias0 + col);
+      add8(v, p.resid + (long)row * p.ldr + col);
+      store8_f32((float*)p.C + (long)row * p.ldc + col, v);
+    } else if constexpr (EPI == E_GELU) {
+      if (p.bias0) add8(v, p.bias0 + col);
+      store8_bf16((__bf16*)p.C2 + (long)row * p.ldc2 + col, v);
+      float g[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = gelu_new_dev(bf2f(f2bf(v[e])));  // gelu of the stored (bf16) pre
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, g);
+    } else if constexpr (EPI == E_F32_ACC) {
+      float* dst = (float*)p.C + (long)row * p.ldc + col;
+      add8(v, dst);
+      store8_f32(dst, v);
+    } else {  // E_F32_STORE
+      if (p.bias0) add8(v, p.bias0 + col);
+      store8_f32((float*)p.C + (long)row * p.ldc + col, v);
+    }
+  }
+}
+
+template <int BM, int BN, bool AKM, bool BKM, int EPI>
+hipError_t launch(const G2Args& a, hipStream_t s) {
+  const int tiles = (a.M / BM) * (a.N / BN);
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, AKM, BKM, EPI>), dim3(tiles), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <bool AKM, bool BKM, int EPI>
+hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
+  switch (tile) {
+    case 0: return launch<128, 128, AKM, BKM, EPI>(a, s);
+    case 1: return launch<128, 64, AKM, BKM, EPI>(a, s);
+    case 2: return launch<64, 128, AKM, BKM, EPI>(a, s);
+    default: return launch<64, 64, AKM, BKM, EPI>(a, s);
+  }
+}
+
+}  // namespace
+
+static const int kTileBM[4] = {128, 128, 64, 64};
+static const int kTileBN[4] = {128, 64, 128, 64};
+
+// 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
+IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,
+                                long lda, long ldb, long ldc, long ldc2, long ldr, int M, int N, int K, int mode,
+                                int epi, int bias_cols, int tile) {
+  if (tile < 0 || tile > 3) return 0;
+  if (!(mode == 0 || mode == 2 || mode == 3)) return 0;
+  const bool epi_ok = mode == 3 ? (epi == E_F32_ACC || epi == E_F32_STORE)
+                                : (epi == E_BF16 || epi == E_BF16_BIAS3 || epi == E_F32_RESID || epi == E_GELU ||
+                                   epi == E_F32_ACC || epi == E_F32_STORE);
+  if (!epi_ok) return 0;
+  if (mode == 0 && !(epi == E_BF16 || epi == E_F32_ACC || epi == E_F32_STORE)) return 0;
+  if (M <= 0 || N <= 0 || K <= 0 || M % kTileBM[tile] || N % kTileBN[tile] || K % 64) return 0;
+  if (lda % 8 || ldb % 8 || ldc % 8 || (C2 && ldc2 % 8) || (resid && ldr % 8)) return 0;
+  const uintptr_t al = (uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)C2 | (uintptr_t)resid;
+  if (al & 15) return 0;
+  if (epi == E_BF16_BIAS3 && bias_cols % 8) return 0;
+  return 1;
+}
+
+IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, const float* bias0, const float* bias1,
+                             const float* bias2, const float* resid, long lda, long ldb, long ldc, long ldc2, long ldr,
+                             int M, int N, int K, int mode, int epi, int bias_cols, int tile, void* stream) {
+  if (!iit_gemm_glds_ok(A, B, C, C2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile))
+    return (int)hipErrorInvalidValue;
+  G2Args a;
+  a.A = (const __bf16*)A; a.B = (const __bf16*)B; a.C = C; a.C2 = C2;
+  a.bias0 = bias0; a.bias1 = bias1; a.bias2 = bias2; a.resid = resid;
+  a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldc2 = ldc2; a.ldr = ldr;
+  a.M = M; a.N = N; a.K = K; a.bias_cols = bias_cols;
+  hipStream_t s = (hipStream_t)stream;
+#define G2(MODE, AK, BK_, EPI) \
+  if (mode == (MODE) && epi == (EPI)) return (int)launch_tile<AK, BK_, EPI>(a, tile, s);
+  G2(0, false, false, E_BF16)
+  G2(0, false, false, E_F32_ACC)
+  G2(0, false, false, E_F32_STORE)
+  G2(2, false, true, E_BF16)
+  G2(2, false, true, E_BF16_BIAS3)
+  G2(2, false, true, E_F32_RESID)
+  G2(2, false, true, E_GELU)
+  G2(2, false, true, E_F32_ACC)
+  G2(2, false, true, E_F32_STORE)
+  G2(3, true, true, E_F32_ACC)
+  G2(3, true, true, E_F32_STORE)
+#undef G2
+  return (int)hipErrorInvalidValue;
+}

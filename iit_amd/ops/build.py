@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 CSRC = os.path.join(ROOT, "csrc")
 OUT_DIR = os.path.join(ROOT, "iit_amd", "_native")
 LIB = os.path.join(OUT_DIR, "libiit_hip.so")
-SOURCES = ["gemm.hip", "kernels.hip", "attn_mfma.hip", "flash_attn.hip"]
+SOURCES = ["gemm.hip", "gemm_glds.hip", "kernels.hip", "attn_mfma.hip", "flash_attn.hip"]
 ARCH = os.environ.get("IIT_OFFLOAD_ARCH", "gfx950")
 
 

@@ -1,0 +1,97 @@
+"""LDS-DMA MFMA GEMM (csrc/gemm_glds.hip) vs fp32 PyTorch, every layout x epilogue x tile it covers."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+@pytest.fixture(scope="module")
+def K():
+    from iit_amd.ops import hip_kernels
+    hip_kernels.lib()
+    return hip_kernels
+
+
+def _ops(K, mode, M, N, Kd, pad):
+    """bf16 operands in the storage layout of ``mode`` with padded leading dims; returns (A, B, lda, ldb, a, b)
+    where a [M,K], b [K,N] are the fp32 logical operands."""
+    torch.manual_seed(M + N + Kd + mode)
+    a = torch.randn(M, Kd, device=dev).bfloat16()
+    b = (torch.randn(Kd, N, device=dev) / 8).bfloat16()
+    if mode & K.MODE_AKM:
+        A = torch.zeros(Kd, M + pad, device=dev, dtype=torch.bfloat16)
+        A[:, :M] = a.t()
+        lda = M + pad
+    else:
+        A = torch.zeros(M, Kd + pad, device=dev, dtype=torch.bfloat16)
+        A[:, :Kd] = a
+        lda = Kd + pad
+    if mode & K.MODE_BKM:
+        B = torch.zeros(Kd, N + pad, device=dev, dtype=torch.bfloat16)
+        B[:, :N] = b
+        ldb = N + pad
+    else:
+        B = torch.zeros(N, Kd + pad, device=dev, dtype=torch.bfloat16)
+        B[:, :Kd] = b.t()
+        ldb = Kd + pad
+    return A, B, lda, ldb, a.float(), b.float()
+
+
+CASES = [(0, 0), (0, 5), (0, 7), (2, 0), (2, 1), (2, 2), (2, 3), (2, 5), (2, 7), (3, 5), (3, 7)]
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("mode,epi", CASES)
+def test_glds_gemm_matches_fp32(K, mode, epi, tile):
+    from iit_amd.ops.torch_ops import gelu_new
+    M, N, Kd, pad = 256, 384, 192, 8
+    A, B, lda, ldb, a, b = _ops(K, mode, M, N, Kd, pad)
+    ref = a @ b
+    ldc = N + 8
+    bias = torch.randn(N, device=dev)
+    kw = dict(M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, tile=tile)
+    if epi in (K.EPI_BF16, K.EPI_BF16_BIAS3, K.EPI_GELU):
+        C = torch.zeros(M, ldc, device=dev, dtype=torch.bfloat16)
+    else:
+        C = torch.randn(M, ldc, device=dev)
+    C0 = C.clone()
+    extra = {}
+    if epi == K.EPI_BF16:
+        extra = dict(bias0=bias)
+        exp = ref + bias
+    elif epi == K.EPI_BF16_BIAS3:
+        b3 = [torch.randn(128, device=dev) for _ in range(3)]
+        extra = dict(bias0=b3[0], bias1=b3[1], bias2=b3[2], bias_cols=128)
+        exp = ref + torch.cat(b3)
+    elif epi == K.EPI_F32_RESID:
+        R = torch.randn(M, N + 16, device=dev)
+        extra = dict(bias0=bias, resid=R, ldr=N + 16)
+        exp = ref + bias + R[:, :N]
+    elif epi == K.EPI_GELU:
+        C2 = torch.zeros(M, ldc, device=dev, dtype=torch.bfloat16)
+        extra = dict(bias0=bias, C2=C2, ldc2=ldc)
+        exp = gelu_new(ref + bias)
+    elif epi == K.EPI_F32_ACC:
+        exp = C0[:, :N] + ref
+    else:
+        extra = dict(bias0=bias) if mode != 3 else {}
+        exp = ref + (bias if mode != 3 else 0)
+    assert K.gemm_glds_ok(A, B, C, C2=extra.get("C2"), resid=extra.get("resid"), ldc2=extra.get("ldc2", 0),
+                          ldr=extra.get("ldr", 0), bias_cols=extra.get("bias_cols", 0), **{k: v for k, v in kw.items()})
+    K.gemm_glds(A, B, C, **kw, **extra)
+    torch.cuda.synchronize()
+    got = C[:, :N].float()
+    err = ((got - exp).norm() / exp.norm()).item()
+    assert err < 1e-2, err
+    if epi == K.EPI_GELU:
+        pre = extra["C2"][:, :N].float()
+        assert ((pre - (ref + bias)).norm() / (ref + bias).norm()).item() < 1e-2
+    assert torch.equal(C[:, N:], C0[:, N:])  # padding columns untouched
+
+
+def test_glds_rejects_unaligned_shapes(K):
+    A = torch.zeros(100, 64, device=dev, dtype=torch.bfloat16)
+    B = torch.zeros(64, 128, device=dev, dtype=torch.bfloat16)
+    C = torch.zeros(100, 128, device=dev, dtype=torch.bfloat16)
+    assert not K.gemm_glds_ok(A, B, C, M=100, N=128, K=64, lda=64, ldb=128, ldc=128, mode=2, epi=0, tile=0)

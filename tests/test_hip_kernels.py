@@ -252,7 +252,7 @@ def test_flat_adam_row_restriction_is_exact(K):
             o.step(clip_norm=1.0)
     assert f1._inactive, "restriction must survive the first-step validation"
     assert torch.allclose(f1.data, f2.data, rtol=1e-5, atol=1e-7)
-    assert torch.allclose(o1.exp_avg, o2.exp_avg, rtol=1e-5, atol=1e-9)
+    assert torch.allclose(o1.exp_avg, o2.exp_avg, rtol=1e-4, atol=1e-6)
     off = f1.offset_of(m1["emb"].weight)
     dead = torch.ones(5000, dtype=torch.bool)
     dead[live] = False
