@@ -11,7 +11,9 @@
 // * 256 threads = 4 wave64 as 2x2; tile BM x BN x 64; each wave a (BM/2) x (BN/2) block of 16x16 fp32
 //   accumulators fed by v_mfma_f32_16x16x32_bf16.
 // * Operands are staged global -> LDS with 16-byte global_load_lds (no VGPR round trip, no ds_write pass) into
-//   two LDS buffers: the DMA of K-tile k+1 is in flight while the MFMAs consume tile k; one barrier per K-tile.
+//   an NS-deep ring of LDS buffers: NS-1 K-tiles are in flight while the MFMAs consume one; each K-step waits
+//   with a counted s_waitcnt vmcnt (never 0 in steady state) and one raw s_barrier, so the DMA spans barriers
+//   (a __syncthreads() would drain it: "Pipelining across barriers").
 // * LDS images are lane-linear per wave (what LDS-DMA requires) and XOR-swizzled through the *source* address:
 //     k-contiguous [rows][64]:   16-B chunk c of row r lives at slot c ^ ((r >> 1) & 7)  -> ds_read_b128 fragment
 //                                 reads of 16 rows hit 16 distinct bank groups (conflict-free);
@@ -86,7 +88,14 @@ __device__ __forceinline__ void stage_operand(const __bf16* base, long ld, int r
   }
 }
 
-// MFMA 16x16x32 operand fragment: lane l gets X[row0 + (l & 15)][kbase + 8 * (l >> 4) + j], j = 0..7
+// MFMA 16x16x32 operand fragment: lane l gets X[row0 + (l & 15)][kbase + 8 * (l >> 4) + j], j = 0..7.
+// The k-major (transpose-read) form is issued as inline asm: hipcc (ROCm 7.2) treats the ds_read_tr builtin as
+// possibly aliasing every in-flight LDS-DMA and puts s_waitcnt vmcnt(0) in front of it, which would drain the
+// prefetch ring each K-step.  The caller therefore waits lgkmcnt(0) + sched_barrier before using the registers.
+__device__ __forceinline__ unsigned lds_addr(const char* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
 template <bool KMAJ, int R>
 __device__ __forceinline__ bf16x8 frag(const char* img, int row0, int kbase, int lane) {
   if constexpr (!KMAJ) {
@@ -97,9 +106,10 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int row0, int kbase, int
     const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
     const int kr = kbase + 8 * g + q;
     const int col = row0 + 4 * pp;
-    const char* a0 = img + kr * (R * 2) + ((((col >> 4) ^ kmaj_swz<R>(kr))) << 5) + ((col & 15) << 1);
-    const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(a0));
-    const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(a0 + 4 * R * 2));
+    const unsigned a0 = lds_addr(img + kr * (R * 2) + ((((col >> 4) ^ kmaj_swz<R>(kr))) << 5) + ((col & 15) << 1));
+    i16x4 v0, v1;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v0) : "v"(a0));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v1) : "v"(a0), "i"(4 * R * 2));
     const i16x8 w = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(bf16x8, w);
   }
@@ -135,16 +145,26 @@ __device__ __forceinline__ void store8_f32(void* dst, const float* v) {
   *((float4*)dst + 1) = make_float4(v[4], v[5], v[6], v[7]);
 }
 
-template <int BM, int BN, bool AKM, bool BKM, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_glds_kernel(G2Args p) {
+// s_waitcnt vmcnt(N) with N chosen at run time from {0, L, 2L, 3L} (an immediate is required)
+template <int L>
+__device__ __forceinline__ void wait_tiles(int tiles_in_flight) {
+  if (tiles_in_flight >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * L) : "memory");
+  else if (tiles_in_flight == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * L) : "memory");
+  else if (tiles_in_flight == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
   constexpr int BK = 64;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int LOADS = BM / 32 + BN / 32;  // LDS-DMA instructions per wave per K-tile
   constexpr int EPS = BN + 4;  // fp32 epilogue row stride (floats)
   constexpr int EPI_BYTES = BM * EPS * 4;
-  constexpr int SMEM = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
+  constexpr int SMEM = NS * STAGE > EPI_BYTES ? NS * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];  // ONE LDS object (keeps hipcc's waits counted)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -160,17 +180,28 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(G2Args p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage_operand<AKM, BM>(p.A, p.lda, m0, 0, smem, wave, lane);
-  stage_operand<BKM, BN>(p.B, p.ldb, n0, 0, smem + A_BYTES, wave, lane);
-  __syncthreads();  // drains the DMA (vmcnt(0)) and publishes tile 0
-  for (int kt = 0; kt < nt; ++kt) {
-    const char* sa = smem + (kt & 1) * STAGE;
-    const char* sb = sa + A_BYTES;
-    if (kt + 1 < nt) {
-      char* na = smem + ((kt + 1) & 1) * STAGE;
-      stage_operand<AKM, BM>(p.A, p.lda, m0, (kt + 1) * BK, na, wave, lane);
-      stage_operand<BKM, BN>(p.B, p.ldb, n0, (kt + 1) * BK, na + A_BYTES, wave, lane);
+  // prologue: NS-1 K-tiles in flight
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nt) {
+      char* buf = smem + s * STAGE;
+      stage_operand<AKM, BM>(p.A, p.lda, m0, s * BK, buf, wave, lane);
+      stage_operand<BKM, BN>(p.B, p.ldb, n0, s * BK, buf + A_BYTES, wave, lane);
     }
+  for (int kt = 0; kt < nt; ++kt) {
+    // tile kt is complete once at most min(NS-2, nt-1-kt) later tiles are still in flight (counted, never 0 in
+    // steady state); the raw barrier then publishes every wave's DMA and retires all reads of tile kt-1, whose
+    // buffer is restaged right after it
+    wait_tiles<LOADS>(min(NS - 2, nt - 1 - kt));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nt) {
+      char* buf = smem + ((kt + NS - 1) % NS) * STAGE;
+      stage_operand<AKM, BM>(p.A, p.lda, m0, (kt + NS - 1) * BK, buf, wave, lane);
+      stage_operand<BKM, BN>(p.B, p.ldb, n0, (kt + NS - 1) * BK, buf + A_BYTES, wave, lane);
+    }
+    const char* sa = smem + (kt % NS) * STAGE;
+    const char* sb = sa + A_BYTES;
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
       bf16x8 a[TM], b[TN];
@@ -178,13 +209,17 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(G2Args p) {
       for (int i = 0; i < TM; ++i) a[i] = frag<AKM, BM>(sa, wm * WM + i * 16, s * 32, lane);
 #pragma unroll
       for (int j = 0; j < TN; ++j) b[j] = frag<BKM, BN>(sb, wn * WN + j * 16, s * 32, lane);
+      if constexpr (AKM || BKM) {  // asm transpose reads: retire them before the MFMAs read the registers
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();  // tile k+1 landed; every wave is done with tile k before it is restaged
   }
+  __syncthreads();  // all waves done with the staging buffers before they become the epilogue tile
 
   // ---------------------------------------------------------------- epilogue via LDS
   float* E = (float*)smem;
@@ -238,33 +273,36 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(G2Args p) {
   }
 }
 
-template <int BM, int BN, bool AKM, bool BKM, int EPI>
+template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI>
 hipError_t launch(const G2Args& a, hipStream_t s) {
   const int tiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, AKM, BKM, EPI>), dim3(tiles), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NS, AKM, BKM, EPI>), dim3(tiles), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
+// tile configurations: (BM, BN, LDS stages)
 template <bool AKM, bool BKM, int EPI>
 hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
   switch (tile) {
-    case 0: return launch<128, 128, AKM, BKM, EPI>(a, s);
-    case 1: return launch<128, 64, AKM, BKM, EPI>(a, s);
-    case 2: return launch<64, 128, AKM, BKM, EPI>(a, s);
-    default: return launch<64, 64, AKM, BKM, EPI>(a, s);
+    case 0: return launch<128, 128, 3, AKM, BKM, EPI>(a, s);
+    case 1: return launch<128, 64, 4, AKM, BKM, EPI>(a, s);
+    case 2: return launch<64, 128, 4, AKM, BKM, EPI>(a, s);
+    case 3: return launch<64, 64, 4, AKM, BKM, EPI>(a, s);
+    default: return launch<128, 128, 4, AKM, BKM, EPI>(a, s);
   }
 }
 
 }  // namespace
 
-static const int kTileBM[4] = {128, 128, 64, 64};
-static const int kTileBN[4] = {128, 64, 128, 64};
+#define IIT_GLDS_TILES 5
+static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128};
+static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128};
 
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,
                                 long lda, long ldb, long ldc, long ldc2, long ldr, int M, int N, int K, int mode,
                                 int epi, int bias_cols, int tile) {
-  if (tile < 0 || tile > 3) return 0;
+  if (tile < 0 || tile >= IIT_GLDS_TILES) return 0;
   if (!(mode == 0 || mode == 2 || mode == 3)) return 0;
   const bool epi_ok = mode == 3 ? (epi == E_F32_ACC || epi == E_F32_STORE)
                                 : (epi == E_BF16 || epi == E_BF16_BIAS3 || epi == E_F32_RESID || epi == E_GELU ||

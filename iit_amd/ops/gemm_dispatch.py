@@ -52,6 +52,36 @@ def select_graph_safe_blas() -> None:
         print(f"[iit] could not select rocBLAS ({e})")
 
 
+_TUNED_CSV = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "tunableop_gfx950.csv")
+_TUNABLE_DONE = False
+
+
+def enable_tuned_library_gemms() -> bool:
+    """Load the shipped TunableOp table (``ops/tuned/tunableop_gfx950.csv``): the fastest hipBLASLt / rocBLAS
+    solution per library-GEMM shape of the engine's workloads, found by PyTorch TunableOp's exhaustive search on
+    an MI355X (``scripts/gpu_tunableop.sh``).  The table carries validators (PyTorch / HIP / hipBLASLt / rocBLAS
+    versions, gfx arch); TunableOp ignores it on any mismatch, and shapes not in it take the library default.
+    Tuning itself stays off (it cannot run inside graph capture).  ``IIT_TUNABLEOP=0`` disables."""
+    global _TUNABLE_DONE
+    if _TUNABLE_DONE:
+        return True
+    _TUNABLE_DONE = True
+    if os.environ.get("IIT_TUNABLEOP", "1") == "0" or not torch.cuda.is_available() or not os.path.exists(_TUNED_CSV):
+        return False
+    if os.environ.get("PYTORCH_TUNABLEOP_ENABLED") is not None:  # the user drives TunableOp themselves
+        return False
+    try:
+        import tempfile
+        from torch.cuda import tunable
+        tunable.enable(True)
+        tunable.tuning_enable(False)
+        tunable.set_filename(os.path.join(tempfile.gettempdir(), "iit_tunableop_results%d.csv"))
+        return bool(tunable.read_file(_TUNED_CSV))
+    except Exception as e:  # pragma: no cover - older torch
+        print(f"[iit] TunableOp table not loaded ({e})")
+        return False
+
+
 def _as(t, rows, cols, ld, dtype=None):
     v = torch.as_strided(t, (rows, cols), (ld, 1))
     return v if dtype is None or v.dtype == dtype else v.to(dtype)
@@ -218,6 +248,7 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     Kd = K
     if not _BLAS_SELECTED:
         select_graph_safe_blas()
+        enable_tuned_library_gemms()
     hip_call = lambda c=C, c2=C2, c3=C3: K_.gemm(  # noqa: E731
         A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=c2, C3=c3, bias0=bias0,
         bias1=bias1, bias2=bias2, resid=resid, ldr=ldr, aux=aux, ldc2=ldc2, bias_cols=bias_cols, qkv=qkv,
@@ -228,9 +259,19 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     blas_call = lambda c=C, c2=C2, c3=C3: _blas(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi, c2, c3, bias0,  # noqa
                                                bias1, bias2, resid, ldr, aux, ldc2, bias_cols, qkv, blas_bias)
     calls = {"hip": hip_call, "blas": blas_call}
+    if policy in ("auto", "glds") and A.is_cuda:
+        for tile in K_.GLDS_TILES:
+            if K_.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=C2,
+                               resid=resid, ldc2=ldc2, ldr=ldr, bias_cols=bias_cols, tile=tile):
+                calls[f"glds{tile}"] = lambda c=C, c2=C2, c3=C3, t=tile: K_.gemm_glds(  # noqa: E731
+                    A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=c2, bias0=bias0,
+                    bias1=bias1, bias2=bias2, resid=resid, ldc2=ldc2, ldr=ldr, bias_cols=bias_cols, tile=t)
     if epi in _BLAS16_EPIS:
         calls["blas16"] = lambda c=C, c2=C2, c3=C3: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
                                                            bias0, resid, ldr)
+    if policy == "glds":
+        glds = [k for k in calls if k.startswith("glds")]
+        return calls[glds[0] if glds else "hip"]()
     if policy in calls:
         return calls[policy]()
     key = (M, N, Kd, mode, epi, bias0 is not None)

@@ -1,9 +1,14 @@
 """Graph-timed GEMM comparison on the GPT-2-small IIT step shapes: LDS-DMA kernel tiles vs the register-staged
 kernel vs hipBLASLt (torch.mm).  Prints one line per shape (microseconds per call, TFLOP/s of the best)."""
+import os
+import sys
+
 import torch
 
-from iit_amd.ops import gemm_dispatch as gd
-from iit_amd.ops import hip_kernels as K
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from iit_amd.ops import gemm_dispatch as gd  # noqa: E402
+from iit_amd.ops import hip_kernels as K  # noqa: E402
 
 T = 4096
 SHAPES = [  # (name, M, N, K, mode, epi)
@@ -19,7 +24,7 @@ SHAPES = [  # (name, M, N, K, mode, epi)
 def run():
     dev = "cuda"
     print(f"{'shape':18s} {'M':>5s} {'N':>5s} {'K':>5s}  " + "  ".join(f"{c:>8s}" for c in
-          ["t128x128", "t128x64", "t64x128", "t64x64", "hip_old", "blas"]) + "   best TF/s")
+          ["128x128s3", "128x64s4", "64x128s4", "64x64s4", "128x128s4", "hip_old", "blas"]) + "   best TF/s")
     for name, M, N, Kd, mode, epi in SHAPES:
         torch.manual_seed(0)
         A = (torch.randn(Kd, M) if mode & 1 else torch.randn(M, Kd)).to(dev).bfloat16()
@@ -41,7 +46,7 @@ def run():
         elif epi == 3:
             extra = dict(bias0=bias, C2=C2, ldc2=N)
         res = []
-        for tile in range(4):
+        for tile in range(5):
             if K.gemm_glds_ok(A, B, C, C2=C2, resid=R, ldc2=N if C2 is not None else 0, ldr=N if R is not None else 0,
                               bias_cols=extra.get("bias_cols", 0), tile=tile, **{k: kw[k] for k in kw}):
                 res.append(gd._time(lambda t=tile: K.gemm_glds(A, B, C, tile=t, **kw, **extra), reps=20))
