@@ -98,6 +98,11 @@ def setup(args, dev):
     return pair, opt, loss_fn, it, step_fn, train_set, test_set
 
 
+# the reference publishes no throughput; its semantics (fp32, eager hook closures, full-vocab
+# logits, torch Adam) measured on one MI355X with ``--engine reference --dtype fp32 --graphs 0``
+REFERENCE_EAGER_PAIRS_PER_S = 1559.65
+
+
 def main():
     args = parse()
     from iit_amd.parallel import dist as pdist
@@ -156,7 +161,10 @@ def main():
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": (round(value / REFERENCE_EAGER_PAIRS_PER_S, 3)
+                            if args.model == "gpt2-small" and os.environ.get("IIT_BENCH_TINY") != "1" else None),
+            "baseline": "reference-equivalent eager fp32 engine on 1x MI355X (BASELINE.md; the reference "
+                        "publishes no number)",
             "dtype": args.dtype,
             "data": "synthetic (offline IOI prompts, random-init weights)",
             "config": {"model": ("tiny-test 2L/16d (launch rehearsal, not a measurement)"
