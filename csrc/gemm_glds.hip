@@ -22,6 +22,8 @@
 // * k-major operands (X^T dY, [K][N] weights) are transposed by the gfx950 LDS transpose read, so no operand is
 //   ever re-laid-out in memory.
 // * Bijective XCD-aware tile remap: the tiles of one XCD share A row panels in its L2.
+// * Split-K (fp32 accumulate epilogue only): blockIdx.y takes a K range and adds its partial tile with fp32
+//   atomics -- for the weight gradients, whose [d][N] outputs are too few tiles to fill 256 CUs.
 // * Epilogue: accumulators -> LDS (fp32 tile) -> each thread owns 8 consecutive columns of a row: 16-B / 32-B
 //   vector loads of bias / residual / accumulator and vector stores (the MFMA C layout would otherwise give
 //   2-byte column-strided stores).
@@ -42,6 +44,7 @@ struct G2Args {
   const float* resid;
   long lda, ldb, ldc, ldc2, ldr;
   int M, N, K, bias_cols;
+  int k_per_split;  // split-K: blockIdx.y owns [y * k_per_split, (y + 1) * k_per_split); partials added atomically
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -172,7 +175,8 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
   const int tiles_n = p.N / BN;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
-  const int nt = p.K / BK;
+  const int kbeg = blockIdx.y * p.k_per_split;
+  const int nt = p.k_per_split / BK;
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -185,8 +189,8 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
   for (int s = 0; s < NS - 1; ++s)
     if (s < nt) {
       char* buf = smem + s * STAGE;
-      stage_operand<AKM, BM>(p.A, p.lda, m0, s * BK, buf, wave, lane);
-      stage_operand<BKM, BN>(p.B, p.ldb, n0, s * BK, buf + A_BYTES, wave, lane);
+      stage_operand<AKM, BM>(p.A, p.lda, m0, kbeg + s * BK, buf, wave, lane);
+      stage_operand<BKM, BN>(p.B, p.ldb, n0, kbeg + s * BK, buf + A_BYTES, wave, lane);
     }
   for (int kt = 0; kt < nt; ++kt) {
     // tile kt is complete once at most min(NS-2, nt-1-kt) later tiles are still in flight (counted, never 0 in
@@ -197,8 +201,8 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
     __builtin_amdgcn_s_barrier();
     if (kt + NS - 1 < nt) {
       char* buf = smem + ((kt + NS - 1) % NS) * STAGE;
-      stage_operand<AKM, BM>(p.A, p.lda, m0, (kt + NS - 1) * BK, buf, wave, lane);
-      stage_operand<BKM, BN>(p.B, p.ldb, n0, (kt + NS - 1) * BK, buf + A_BYTES, wave, lane);
+      stage_operand<AKM, BM>(p.A, p.lda, m0, kbeg + (kt + NS - 1) * BK, buf, wave, lane);
+      stage_operand<BKM, BN>(p.B, p.ldb, n0, kbeg + (kt + NS - 1) * BK, buf + A_BYTES, wave, lane);
     }
     const char* sa = smem + (kt % NS) * STAGE;
     const char* sb = sa + A_BYTES;
@@ -217,6 +221,21 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  if constexpr (EPI == E_F32_ACC) {
+    if (gridDim.y > 1) {  // split-K partial: atomics straight from the MFMA layout (16 lanes = 16 consecutive
+                          // columns, so each wave instruction hits 4 rows x 64 B)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn * WN + j * 16 + (lane & 15);
+          const int row = m0 + wm * WM + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) unsafeAtomicAdd((float*)p.C + (long)(row + r) * p.ldc + col, acc[i][j][r]);
+        }
+      return;
     }
   }
   __syncthreads();  // all waves done with the staging buffers before they become the epilogue tile
@@ -276,7 +295,8 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
 template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI>
 hipError_t launch(const G2Args& a, hipStream_t s) {
   const int tiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NS, AKM, BKM, EPI>), dim3(tiles), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NS, AKM, BKM, EPI>), dim3(tiles, a.K / a.k_per_split), dim3(256), 0,
+                     s, a);
   return hipGetLastError();
 }
 
@@ -301,8 +321,9 @@ static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128};
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,
                                 long lda, long ldb, long ldc, long ldc2, long ldr, int M, int N, int K, int mode,
-                                int epi, int bias_cols, int tile) {
+                                int epi, int bias_cols, int tile, int splits) {
   if (tile < 0 || tile >= IIT_GLDS_TILES) return 0;
+  if (splits < 1 || (splits > 1 && (epi != E_F32_ACC || K % (64 * splits)))) return 0;
   if (!(mode == 0 || mode == 2 || mode == 3)) return 0;
   const bool epi_ok = mode == 3 ? (epi == E_F32_ACC || epi == E_F32_STORE)
                                 : (epi == E_BF16 || epi == E_BF16_BIAS3 || epi == E_F32_RESID || epi == E_GELU ||
@@ -319,14 +340,15 @@ IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, con
 
 IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, const float* bias0, const float* bias1,
                              const float* bias2, const float* resid, long lda, long ldb, long ldc, long ldc2, long ldr,
-                             int M, int N, int K, int mode, int epi, int bias_cols, int tile, void* stream) {
-  if (!iit_gemm_glds_ok(A, B, C, C2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile))
+                             int M, int N, int K, int mode, int epi, int bias_cols, int tile, int splits,
+                             void* stream) {
+  if (!iit_gemm_glds_ok(A, B, C, C2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits))
     return (int)hipErrorInvalidValue;
   G2Args a;
   a.A = (const __bf16*)A; a.B = (const __bf16*)B; a.C = C; a.C2 = C2;
   a.bias0 = bias0; a.bias1 = bias1; a.bias2 = bias2; a.resid = resid;
   a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldc2 = ldc2; a.ldr = ldr;
-  a.M = M; a.N = N; a.K = K; a.bias_cols = bias_cols;
+  a.M = M; a.N = N; a.K = K; a.bias_cols = bias_cols; a.k_per_split = K / splits;
   hipStream_t s = (hipStream_t)stream;
 #define G2(MODE, AK, BK_, EPI) \
   if (mode == (MODE) && epi == (EPI)) return (int)launch_tile<AK, BK_, EPI>(a, tile, s);

@@ -260,12 +260,16 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
                                                bias1, bias2, resid, ldr, aux, ldc2, bias_cols, qkv, blas_bias)
     calls = {"hip": hip_call, "blas": blas_call}
     if policy in ("auto", "glds") and A.is_cuda:
+        split_opts = (1, 2, 4) if epi == K_.EPI_F32_ACC and (M // 64) * (N // 64) < 1024 else (1,)
         for tile in K_.GLDS_TILES:
-            if K_.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=C2,
-                               resid=resid, ldc2=ldc2, ldr=ldr, bias_cols=bias_cols, tile=tile):
-                calls[f"glds{tile}"] = lambda c=C, c2=C2, c3=C3, t=tile: K_.gemm_glds(  # noqa: E731
-                    A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=c2, bias0=bias0,
-                    bias1=bias1, bias2=bias2, resid=resid, ldc2=ldc2, ldr=ldr, bias_cols=bias_cols, tile=t)
+            for sp in split_opts:
+                if K_.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=C2,
+                                   resid=resid, ldc2=ldc2, ldr=ldr, bias_cols=bias_cols, tile=tile, splits=sp):
+                    calls[f"glds{tile}" + (f"k{sp}" if sp > 1 else "")] = \
+                        lambda c=C, c2=C2, c3=C3, t=tile, sp=sp: K_.gemm_glds(  # noqa: E731
+                            A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=c2,
+                            bias0=bias0, bias1=bias1, bias2=bias2, resid=resid, ldc2=ldc2, ldr=ldr,
+                            bias_cols=bias_cols, tile=t, splits=sp)
     if epi in _BLAS16_EPIS:
         calls["blas16"] = lambda c=C, c2=C2, c3=C3: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
                                                            bias0, resid, ldr)

@@ -26,8 +26,8 @@ _LIB = None
 
 _SIGS = {
     "iit_gemm": [c_void_p] * 10 + [c_long] * 5 + [c_int] * 12 + [c_void_p],
-    "iit_gemm_glds": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 7 + [c_void_p],
-    "iit_gemm_glds_ok": [c_void_p] * 5 + [c_long] * 5 + [c_int] * 7,
+    "iit_gemm_glds": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p],
+    "iit_gemm_glds_ok": [c_void_p] * 5 + [c_long] * 5 + [c_int] * 8,
     "iit_embed_pos_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_embed_pos_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_ln_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
@@ -125,19 +125,20 @@ GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 1
 
 
 def gemm_glds_ok(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, resid=None, ldc2=0, ldr=0, bias_cols=0,
-                 tile=0) -> bool:
-    """Whether the LDS-DMA kernel (``csrc/gemm_glds.hip``) covers this problem with tile ``tile``."""
+                 tile=0, splits=1) -> bool:
+    """Whether the LDS-DMA kernel (``csrc/gemm_glds.hip``) covers this problem with tile ``tile``
+    (and split-K factor ``splits``, fp32-accumulate epilogue only)."""
     if any(t is not None and (not t.is_cuda or t.dtype not in (torch.bfloat16,)) for t in (A, B)):
         return False
     return bool(lib().iit_gemm_glds_ok(_p(A), _p(B), _p(C), _p(C2), _p(resid), lda, ldb, ldc, ldc2, ldr, M, N, K,
-                                       mode, epi, bias_cols, tile))
+                                       mode, epi, bias_cols, tile, splits))
 
 
 def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None, bias1=None, bias2=None, resid=None,
-              ldc2=0, ldr=0, bias_cols=0, tile=0):
+              ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1):
     """C = A @ B (+ epilogue) on the LDS-DMA MFMA kernel; bf16 operands, M/N/K multiples of the tile."""
     _check(lib().iit_gemm_glds(_p(A), _p(B), _p(C), _p(C2), _p(bias0), _p(bias1), _p(bias2), _p(resid), lda, ldb,
-                               ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, _stream()), "iit_gemm_glds")
+                               ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits, _stream()), "iit_gemm_glds")
 
 
 # ------------------------------------------------------------------------------ others

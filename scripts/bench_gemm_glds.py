@@ -52,6 +52,11 @@ def run():
                 res.append(gd._time(lambda t=tile: K.gemm_glds(A, B, C, tile=t, **kw, **extra), reps=20))
             else:
                 res.append(float("nan"))
+        if epi == 5:  # split-K variants of the best tiles for the weight gradients
+            for tile, sp in ((0, 2), (4, 2), (3, 2), (0, 4), (3, 4)):
+                if K.gemm_glds_ok(A, B, C, tile=tile, splits=sp, **{k: kw[k] for k in kw}):
+                    tt = gd._time(lambda t=tile, s_=sp: K.gemm_glds(A, B, C, tile=t, splits=s_, **kw), reps=20)
+                    print(f"    split-K tile {tile} x{sp}: {tt:8.1f} us")
         old_extra = dict(extra)
         res.append(gd._time(lambda: K.gemm(A, B, C, **kw, **old_extra), reps=20))
         a = A.t() if mode & 1 else A

@@ -90,6 +90,20 @@ def test_glds_gemm_matches_fp32(K, mode, epi, tile):
     assert torch.equal(C[:, N:], C0[:, N:])  # padding columns untouched
 
 
+@pytest.mark.parametrize("tile,splits", [(0, 2), (3, 4), (4, 3)])
+def test_glds_split_k_accumulate(K, tile, splits):
+    M, N, Kd = 256, 384, 64 * 12
+    A, B, lda, ldb, a, b = _ops(K, 3, M, N, Kd, 8)
+    C = torch.randn(M, N, device=dev)
+    exp = C + a @ b
+    assert K.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=3, epi=K.EPI_F32_ACC, tile=tile,
+                          splits=splits)
+    assert not K.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=3, epi=K.EPI_F32_STORE,
+                              tile=tile, splits=splits)
+    K.gemm_glds(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=3, epi=K.EPI_F32_ACC, tile=tile, splits=splits)
+    assert ((C - exp).norm() / exp.norm()).item() < 1e-2
+
+
 def test_glds_rejects_unaligned_shapes(K):
     A = torch.zeros(100, 64, device=dev, dtype=torch.bfloat16)
     B = torch.zeros(64, 128, device=dev, dtype=torch.bfloat16)
