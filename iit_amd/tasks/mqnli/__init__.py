@@ -83,8 +83,7 @@ class MQNLI_HL(HookedRootModule, HLModel):
 
     def forward(self, args):
         x = args[0]
-        dev = x.device
-        T_int, T_neg, T_q, lab = (t.to(dev) for t in (self.T_int, self.T_neg, self.T_q, self.label_of))
+        T_int, T_neg, T_q, lab = self._tables(x.device)
         tok = lambda side, k: x[:, (P_POS if side == "p" else H_POS)[k]]  # noqa: E731
         q = self.hook_q((tok("p", "q") - Q0) * 4 + (tok("h", "q") - Q0))
         adj = self.hook_adj(_modifier_relation(tok("p", "adj"), tok("h", "adj")))
@@ -97,6 +96,13 @@ class MQNLI_HL(HookedRootModule, HLModel):
         negvp = self.hook_negvp(T_neg[neg // 2, neg % 2, vp_rel])
         rel = self.hook_rel(T_q[q // 4, q % 4, np_rel, negvp])
         return torch.nn.functional.one_hot(lab[rel], 3).float() * 10.0
+
+    def _tables(self, dev):
+        """Composition tables on ``dev`` (cached: the first, eager call copies them; graph replays never do)."""
+        cache = self.__dict__.setdefault("_dev_tables", {})
+        if dev not in cache:
+            cache[dev] = tuple(t.to(dev) for t in (self.T_int, self.T_neg, self.T_q, self.label_of))
+        return cache[dev]
 
     def get_idx_to_intermediate(self, name: str):
         i = NODES.index(name)

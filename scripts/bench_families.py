@@ -1,0 +1,151 @@
+"""Throughput of the other BASELINE.json configurations (the headline IOI GPT-2-small number is ``bench.py``).
+
+* ``mqnli-bert-base``   -- MQNLI natural-logic causal model <-> BERT-base (12L/768d/12H, post-LN, GELU),
+  ``IITBehaviorModelPair`` (IIT + behaviour: 2 optimizer steps per batch), 15-token sentence pairs;
+* ``llama3-8b-causal``  -- 8-node arithmetic causal graph <-> Llama-3-8B (32L/4096d, 32 q / 8 kv heads, SwiGLU
+  14336, RMSNorm, rotary, V=128256), ``CausalGraphModelPair`` (IIT + strict + behaviour: 3 optimizer steps),
+  6-token prompts.  fp32 master weights + Adam moments + gradients = 128 GB, bf16 compute.
+
+Random-init weights of the named architectures, synthetic task data; same timing contract as ``bench.py``
+(W untimed warmup steps, then K steps bracketed by barrier + synchronize, max over ranks; one JSON line)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--family", required=True, choices=["mqnli-bert-base", "llama3-8b-causal", "llama-tiny-causal",
+                                                         "mqnli-bert-tiny"])
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=None, help="pairs per GPU per step")
+    ap.add_argument("--graphs", type=int, default=None,
+                    help="HIP-graph phases (default: on for BERT; off for Llama, whose strict phase has one graph per "
+                         "non-circuit node -- ~1000 at 32 layers x 32 heads -- and whose GEMMs are not launch-bound)")
+    return ap.parse_args()
+
+
+def setup(args, dev):
+    from iit_amd.data.iit_dataset import IITDataset, train_test_split
+    torch.manual_seed(0)
+    np.random.seed(0)
+    if args.family.startswith("mqnli"):
+        from iit_amd.model_pairs import IITBehaviorModelPair
+        from iit_amd.models.bert import HookedEncoder, bert_config_dict
+        from iit_amd.tasks.mqnli import VOCAB, make_mqnli_task
+        size = "bert-base" if args.family == "mqnli-bert-base" else "bert-tiny"
+        cfg = bert_config_dict(size, d_vocab=max(VOCAB, 64), device=str(dev), dtype=torch.bfloat16)
+        ll = HookedEncoder(cfg, n_classes=3)
+        ds, hl, corr = make_mqnli_task(ll, n_samples=20000, device=dev)
+        args.batch = args.batch or 256
+        pair = IITBehaviorModelPair(hl, ll, corr, training_args={"batch_size": args.batch, "lr": 1e-4,
+                                                                  "lr_scheduler": None, "early_stop": False,
+                                                                  "clip_grad_norm": 1.0})
+        model_name = f"{size} + MQNLI natural-logic HL (10 nodes)"
+        seq = 15
+    else:
+        from iit_amd.models.convert import llama_config_dict
+        from iit_amd.models.transformer import HookedTransformer
+        from iit_amd.tasks.causal_graph import CausalGraphModelPair, make_causal_graph_task
+        size = "llama-3-8b" if args.family == "llama3-8b-causal" else "llama-tiny"
+        cfg = llama_config_dict(size, device=str(dev), dtype=torch.bfloat16)
+        ll = HookedTransformer(cfg)
+        ds, hl, corr = make_causal_graph_task(ll, n_samples=10000, device=dev)
+        args.batch = args.batch or 64
+        pair = CausalGraphModelPair(hl, ll, corr, training_args={"batch_size": args.batch, "lr": 1e-5,
+                                                                  "lr_scheduler": None, "early_stop": False,
+                                                                  "strict_weight": 0.4, "clip_grad_norm": 1.0})
+        model_name = f"{size} + 8-node arithmetic causal graph"
+        seq = 6
+    from iit_amd.parallel import dist as pdist
+    pdist.broadcast_module(ll)
+    tr, te = train_test_split(ds, 0.1, 42)
+    train_set = IITDataset(tr, tr, seed=0, device=dev)
+    test_set = IITDataset(te, te, seed=0, device=dev)
+    opt = pair.make_optimizer(pair.training_args["lr"])
+    pair.restrict_sparse_rows(train_set)
+    loader = train_set.make_loader(args.batch, 0)
+
+    def batches():
+        while True:
+            for b in loader:
+                yield b
+
+    step_fn = pair.run_train_step
+    if args.graphs is None:
+        args.graphs = int(args.family.startswith("mqnli"))
+    if args.graphs and dev.type == "cuda":
+        from iit_amd.engine.graphs import GraphedTrainStep
+        g = GraphedTrainStep(pair, opt, pair.loss_fn)
+        if g.enabled:
+            step_fn = g
+    return pair, opt, batches(), step_fn, test_set, model_name, seq
+
+
+def main():
+    args = parse()
+    from iit_amd.parallel import dist as pdist
+    distributed = pdist.init_distributed()
+    rank, world = pdist.rank(), pdist.world_size()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    t_setup = time.perf_counter()
+    pair, opt, it, step_fn, test_set, model_name, seq = setup(args, dev)
+    t_setup = time.perf_counter() - t_setup
+    for i in range(args.warmup):
+        base, abl = next(it)
+        if i == 0 and hasattr(step_fn, "prime"):
+            step_fn.prime(base, abl, pair.loss_fn, opt)
+        step_fn(base, abl, pair.loss_fn, opt)
+    timed = [next(it) for _ in range(args.steps)]
+    pdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for base, abl in timed:
+        out = step_fn(base, abl, pair.loss_fn, opt)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    pdist.barrier()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev if distributed and dev.type == "cuda" else "cpu")
+    if distributed:
+        torch.distributed.all_reduce(dt_t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    metrics = pair.make_test_metrics()
+    with torch.no_grad():
+        for i, (base, abl) in enumerate(test_set.make_loader(args.batch, 0)):
+            metrics.update(pair.run_eval_step(base, abl, pair.loss_fn))
+            if i >= 1:
+                break
+    vals = metrics.to_dict()
+    if rank == 0:
+        n_params = sum(p.numel() for p in pair._ll_module().parameters())
+        print(json.dumps({
+            "metric": f"IIT (base,source) intervened pairs/sec, {args.family}", "value": round(
+                args.batch * world * args.steps / dt, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "dtype": "bf16", "data": "synthetic task data, random-init weights",
+            "config": {"model": model_name, "params": n_params, "global_batch": args.batch * world, "seq_len": seq,
+                       "parallelism": f"dp{world}", "graphs": bool(getattr(step_fn, "enabled", False))},
+            "val_IIA": round(float(vals.get("val/IIA", float("nan"))), 3),
+            "setup_s": round(t_setup, 1),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1) if dev.type == "cuda" else None,
+            "last_train_losses": {k: round(float(v), 4) for k, v in out.items()} if isinstance(out, dict) else {},
+        }))
+    pdist.destroy()
+
+
+if __name__ == "__main__":
+    main()
