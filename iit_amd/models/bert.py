@@ -11,8 +11,12 @@ head MQNLI's 3-way entailment label is read from.
 Every hook site goes through the same plan executor as the decoder
 (:class:`iit_amd.models.transformer._Run`), so the native intervention engine
 (capture-only truncated source runs, splices, StopGrad scaling) works unchanged.
-Compute runs through :class:`iit_amd.ops.torch_ops.TorchOps` in the model's
-``cfg.dtype`` (bf16 on MI355X with library GEMMs; fp32 oracle on CPU).
+Compute goes through :func:`iit_amd.ops.select_ops`: on an MI355X in bf16 the HIP backend
+(packed-QKV GEMM into the flat arena's bf16 mirror, fused small-S attention with the
+in-kernel head splice, W_O / W_out GEMMs with the residual add in the epilogue, affine
+LayerNorm kernels); anywhere else the fp32 :class:`~iit_amd.ops.torch_ops.TorchOps` oracle.
+A key-padding ``attention_mask`` or a live attention-internal hook takes the
+TorchOps-semantics path for that block.
 
 ``from_hf_bert`` converts an in-memory HF ``BertForSequenceClassification`` /
 ``BertForMaskedLM`` / ``BertModel`` (random-init or local weights; nothing is
@@ -29,17 +33,9 @@ from torch import nn
 
 from ..engine.plan import RunPlan
 from ..hooks.hook_points import HookedRootModule, HookPoint
-from ..ops.torch_ops import TorchOps
+from ..ops import select_ops
 from .config import HookedTransformerConfig, make_config
-from .transformer import MLP, Attention, LayerNormSite, _Run, _StopForward
-
-_OPS = {}
-
-
-def _ops(dtype):
-    if dtype not in _OPS:
-        _OPS[dtype] = TorchOps(dtype)
-    return _OPS[dtype]
+from .transformer import MLP, Attention, LayerNormSite, _Run, _StopForward, qkv_arena_groups
 
 
 def bert_config_dict(size: str = "bert-base", **overrides):
@@ -87,9 +83,27 @@ class BertBlock(nn.Module):
         self.hook_resid_post = HookPoint()
         self.hook_normalized_resid_post = HookPoint()
 
+    def _fused_ok(self, run: _Run, key_mask) -> bool:
+        attn = self.attn
+        return (run.ops.fused and key_mask is None and not any(
+            run.live(h) for h in (self.hook_attn_out, attn.hook_attn_scores, attn.hook_pattern, attn.hook_q,
+                                  attn.hook_k, attn.hook_v, self.hook_mlp_out)))
+
     def forward(self, resid, run: _Run, key_mask: Optional[torch.Tensor]):
         ops, attn = run.ops, self.attn
         resid = run.site(self.hook_resid_pre, resid)
+        if self._fused_ok(run, key_mask):
+            # HIP path: packed-QKV GEMM -> fused attention (in-kernel head splice) -> W_O GEMM with the fp32
+            # residual add in its epilogue -> LN -> W_in GEMM -> W_out GEMM + residual -> LN
+            z, spliced = attn.compute_z(resid, run)
+            z = run.site(attn.hook_z, z, spliced=spliced)
+            resid_mid = run.site(self.hook_resid_mid, ops.o_proj_residual(z, attn.W_O, attn.b_O, resid))
+            x = run.site(self.hook_mlp_in, self.ln1.run(resid_mid, run))
+            pre_hook = (lambda t: run.site(self.mlp.hook_pre, t)) if run.live(self.mlp.hook_pre) else None
+            _, post = ops.mlp_in(x, self.mlp.W_in, self.mlp.b_in, self.cfg.act_fn, hook_pre=pre_hook)
+            post = run.site(self.mlp.hook_post, post)
+            resid_post = run.site(self.hook_resid_post, ops.mlp_out_residual(post, self.mlp.W_out, self.mlp.b_out, x))
+            return run.site(self.hook_normalized_resid_post, self.ln2.run(resid_post, run))
         q, k, v = ops.qkv(resid, attn.W_Q, attn.W_K, attn.W_V, attn.b_Q, attn.b_K, attn.b_V)
         q, k, v = run.site(attn.hook_q, q), run.site(attn.hook_k, k), run.site(attn.hook_v, v)
         scores = torch.einsum("bqhe,bkhe->bhqk", q, k) / attn.attn_scale
@@ -124,6 +138,7 @@ class HookedEncoder(HookedRootModule):
         self.hook_full_embed = HookPoint()
         self.blocks = nn.ModuleList([BertBlock(cfg, l) for l in range(cfg.n_layers)])
         self.n_classes = n_classes
+        self.op_backend: Optional[str] = None  # None = auto (iit_amd.ops.select_ops: HIP on a GPU in bf16)
         self.sep_token_id: Optional[int] = None  # set -> token types derived from [SEP] when not given
         if n_classes:
             self.pooler = nn.Module()
@@ -151,6 +166,17 @@ class HookedEncoder(HookedRootModule):
     def mark_weights_changed(self) -> None:
         self._iit_weights_version = getattr(self, "_iit_weights_version", 0) + 1
 
+    def _iit_arena_groups(self):
+        """Packed-QKV arena layout, as for the decoder (``transformer.qkv_arena_groups``)."""
+        return qkv_arena_groups(self.blocks, self.cfg)
+
+    def set_op_backend(self, backend: Optional[str]) -> "HookedEncoder":
+        self.op_backend = backend
+        return self
+
+    def ops(self):
+        return select_ops(self, self.op_backend)
+
     def forward(self, input, token_type_ids: Optional[torch.Tensor] = None,
                 attention_mask: Optional[torch.Tensor] = None, *, plan: Optional[RunPlan] = None,
                 return_type: Optional[str] = "logits"):
@@ -159,8 +185,11 @@ class HookedEncoder(HookedRootModule):
             tokens = tokens.unsqueeze(0)
         dev = self.embed.embed.W_E.device
         tokens = tokens.to(dev)
-        run = _Run(plan, _ops(self.cfg.dtype))
+        run = _Run(plan, self.ops())
         ops = run.ops
+        begin = getattr(ops, "begin_forward", None)
+        if begin is not None:
+            begin()
         B, S = tokens.shape
         if token_type_ids is None:
             sep = getattr(self, "sep_token_id", None)

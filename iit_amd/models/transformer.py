@@ -375,6 +375,29 @@ class TransformerBlock(nn.Module):
         return run.site(self.hook_resid_post, resid_post)
 
 
+def qkv_arena_groups(blocks, cfg):
+    """Arena groups packing each block's ``W_Q|W_K|W_V`` into one ``[d_model][3*H*d_head]`` matrix (column
+    ``which*H*dh + h*dh + e``) and ``b_Q|b_K|b_V`` into ``[3][H][dh]`` (see ``HookedTransformer._iit_arena_groups``);
+    shared by every model whose blocks carry an :class:`Attention` (GPT-2 / BERT; GQA blocks are skipped)."""
+    H, d, dh = cfg.n_heads, cfg.d_model, cfg.d_head
+    HD = H * dh
+    groups = []
+    for blk in blocks:
+        a = blk.attn
+        if a.gqa or any(getattr(a, n).shape != (H, d, dh) for n in ("W_Q", "W_K", "W_V")):
+            continue
+
+        def w_view(which):
+            return lambda buf: buf.view(d, 3, H, dh)[:, which].permute(1, 0, 2)
+
+        def b_view(which):
+            return lambda buf: buf.view(3, H, dh)[which]
+
+        groups.append((3 * d * HD, [(a.W_Q, w_view(0)), (a.W_K, w_view(1)), (a.W_V, w_view(2))]))
+        groups.append((3 * HD, [(a.b_Q, b_view(0)), (a.b_K, b_view(1)), (a.b_V, b_view(2))]))
+    return groups
+
+
 class HookedTransformer(HookedRootModule):
     def __init__(self, cfg: Union[HookedTransformerConfig, dict], tokenizer=None, move_to_device: bool = True,
                  default_padding_side: str = "right"):
@@ -432,22 +455,8 @@ class HookedTransformer(HookedRootModule):
         Parameters keep their TL shapes; only their strides differ from contiguous.
         """
         cfg = self.cfg
-        H, d, dh = cfg.n_heads, cfg.d_model, cfg.d_head
-        HD = H * dh
-        groups = []
-        for blk in self.blocks:
-            a = blk.attn
-            if a.gqa or any(getattr(a, n).shape != (H, d, dh) for n in ("W_Q", "W_K", "W_V")):
-                continue
-
-            def w_view(which):
-                return lambda buf: buf.view(d, 3, H, dh)[:, which].permute(1, 0, 2)
-
-            def b_view(which):
-                return lambda buf: buf.view(3, H, dh)[which]
-
-            groups.append((3 * d * HD, [(a.W_Q, w_view(0)), (a.W_K, w_view(1)), (a.W_V, w_view(2))]))
-            groups.append((3 * HD, [(a.b_Q, b_view(0)), (a.b_K, b_view(1)), (a.b_V, b_view(2))]))
+        d = cfg.d_model
+        groups = qkv_arena_groups(self.blocks, cfg)
         V = cfg.d_vocab_out
         Vp = (V + 7) // 8 * 8
         if Vp != V:

@@ -27,11 +27,12 @@ def _torch_ops(dtype):
 
 
 def hip_supported(cfg) -> bool:
-    """Architectures the fused HIP backend implements (GPT-2 family); others run TorchOps on the GPU
-    (bf16 compute, library GEMMs) until their kernels exist (RMSNorm / rotary / SwiGLU / GQA)."""
+    """Architectures the fused HIP backend implements (GPT-2 family and BERT encoders); others run TorchOps on
+    the GPU (bf16 compute, library GEMMs) until their kernels exist (RMSNorm / rotary / SwiGLU / GQA)."""
     return (cfg.positional_embedding_type == "standard" and cfg.normalization_type in ("LN", "LNPre", None)
             and not cfg.gated_mlp and (cfg.n_key_value_heads in (None, cfg.n_heads))
-            and not cfg.parallel_attn_mlp and not cfg.final_rms)
+            and not cfg.parallel_attn_mlp and not cfg.final_rms
+            and cfg.act_fn in ("gelu_new", "gelu_fast", "gelu_pytorch_tanh", "gelu", "relu"))
 
 
 def select_ops(model, backend: Optional[str] = None):

@@ -109,10 +109,15 @@ class ModelShadow:
                 return False
             if not m.cfg.attn_only and not (blk.mlp.W_in.is_contiguous() and blk.mlp.W_out.is_contiguous()):
                 return False
-        W_U = m.unembed.W_U
-        if W_U.stride() != (self.Vp, 1):
+        W_U = self._W_U()
+        if W_U is not None and W_U.stride() != (self.Vp, 1):
             return False
         return all(flat.owns(p) for p in self._matrices())
+
+    def _W_U(self):
+        """The unembedding matrix, or None for models with another head (BERT classifier)."""
+        ue = getattr(self.model, "unembed", None)
+        return None if ue is None else ue.W_U
 
     def _bind_mirror(self, flat):
         sh = flat.ensure_shadow()
@@ -132,7 +137,8 @@ class ModelShadow:
                         and a.b_K.data_ptr() == a.b_Q.data_ptr() + HD * 4
                         and a.b_V.data_ptr() == a.b_Q.data_ptr() + 2 * HD * 4)
             self.biases.append(sh.as_strided((3 * HD,), (1,), flat.offset_of(a.b_Q)) if packed_b else None)
-        self.U = sh.as_strided((d, self.Vp), (self.Vp, 1), flat.offset_of(m.unembed.W_U))
+        W_U = self._W_U()
+        self.U = None if W_U is None else sh.as_strided((d, self.Vp), (self.Vp, 1), flat.offset_of(W_U))
         self._descs = None
 
     # ------------------------------------------------------------------ copy mode
@@ -147,7 +153,7 @@ class ModelShadow:
                 L.update({"in": e(d, cfg.d_mlp), "out": e(cfg.d_mlp, d)})
             self.layers.append(L)
             self.biases.append(None)
-        self.U = torch.zeros(d, self.Vp, dtype=BF16, device=self.dev)
+        self.U = torch.zeros(d, self.Vp, dtype=BF16, device=self.dev) if self._W_U() is not None else None
 
     def _entries(self):
         m, cfg = self.model, self.model.cfg
@@ -163,9 +169,10 @@ class ModelShadow:
                 mlp, dm = blk.mlp, cfg.d_mlp
                 out.append((mlp.W_in.data_ptr(), L["in"].data_ptr(), d, dm, dm, 0))
                 out.append((mlp.W_out.data_ptr(), L["out"].data_ptr(), dm, d, d, 0))
-        W_U = m.unembed.W_U
-        # one single-row "head" per row of W_U: handles a padded (arena) row stride on the fp32 side
-        out.append((W_U.data_ptr(), self.U.data_ptr(), 1, self.V, self.Vp, 0, d, W_U.stride(0), self.Vp))
+        W_U = self._W_U()
+        if W_U is not None:
+            # one single-row "head" per row of W_U: handles a padded (arena) row stride on the fp32 side
+            out.append((W_U.data_ptr(), self.U.data_ptr(), 1, self.V, self.Vp, 0, d, W_U.stride(0), self.Vp))
         return out
 
     def _matrices(self):
@@ -176,7 +183,8 @@ class ModelShadow:
             ps += [a.W_Q, a.W_K, a.W_V, a.W_O]
             if not m.cfg.attn_only:
                 ps += [blk.mlp.W_in, blk.mlp.W_out]
-        ps.append(m.unembed.W_U)
+        if self._W_U() is not None:
+            ps.append(self._W_U())
         return ps
 
     # ------------------------------------------------------------------ per forward
@@ -204,7 +212,7 @@ class ModelShadow:
             value = (wv, tuple(p._version for p in self._matrices()))
         if self.mode != "copy" or self._descs is None or layout != self._layout_sig:
             for p in self._matrices():
-                if p.dtype != F32 or p.stride(-1) != 1 or (p is not m.unembed.W_U and not p.is_contiguous()):
+                if p.dtype != F32 or p.stride(-1) != 1 or (p is not self._W_U() and not p.is_contiguous()):
                     raise RuntimeError("HIP backend needs contiguous fp32 master weights (or the flat arena)")
             self.mode = "copy"
             self._alloc_copies()
@@ -653,6 +661,10 @@ class HipOps(TorchOps):
 
     def residual(self, a, b):
         return a.float() + b.float()
+
+    def w(self, p: torch.Tensor) -> torch.Tensor:
+        """Small parameters used outside the fused kernels (BERT token types, pooler, classifier)."""
+        return p.to(BF16)
 
     def layer_norm(self, x, w, b, eps):
         return LayerNormFn.apply(x, w, b, eps)

@@ -149,3 +149,57 @@ def test_arena_mirror_training_matches_fp32_reference():
         # gradient is at bf16 noise level may move differently: compare the update direction in bulk
         assert rel(pf.detach() - p0[n], pr.detach() - p0[n]) < 0.35, n
         assert ((pf - pr).abs() > 2.5e-3).float().mean().item() < 0.05, n
+
+
+def _bert_pair_models():
+    from iit_amd.models.bert import HookedEncoder, bert_config_dict
+    cfg = bert_config_dict("bert-tiny", n_layers=2, d_model=128, n_heads=2, d_head=64, d_mlp=256, d_vocab=64,
+                           n_ctx=32, device=dev)
+    torch.manual_seed(0)
+    ref = HookedEncoder(cfg, n_classes=3)
+    fast = HookedEncoder({**cfg, "dtype": torch.bfloat16}, n_classes=3)
+    fast.load_state_dict(ref.state_dict())
+    ref.set_op_backend("torch")
+    for m in (ref, fast):
+        m.sep_token_id = 2
+    return ref, fast
+
+
+def test_bert_encoder_on_hip_matches_fp32_oracle():
+    """BERT (post-LN, affine LN, bidirectional attention, erf-GELU) on the HIP backend vs the fp32 oracle."""
+    from iit_amd.ops.hip_ops import HipOps
+    ref, fast = _bert_pair_models()
+    assert isinstance(fast.ops(), HipOps)
+    tok = torch.randint(3, 64, (16, 15), device=dev)
+    tok[:, 0], tok[:, 7], tok[:, 14] = 1, 2, 2
+    lr, lf = ref(tok), fast(tok)
+    assert rel(lf, lr) < 3e-2
+    lr.float().pow(2).mean().backward()
+    lf.float().pow(2).mean().backward()
+    scale = max(p.grad.norm().item() for p in ref.parameters())
+    for (n, pr), (_, pf) in zip(ref.named_parameters(), fast.named_parameters()):
+        assert pf.grad is not None, n
+        if pr.grad.norm().item() < 1e-3 * scale:
+            continue
+        assert rel(pf.grad, pr.grad) < 8e-2, n
+
+
+def test_mqnli_bert_pair_trains_on_hip_arena():
+    """IIT + behaviour steps of the MQNLI pair with the flat arena mirror + fused Adam on the HIP backend."""
+    from iit_amd.data.iit_dataset import IITDataset
+    from iit_amd.model_pairs import IITBehaviorModelPair
+    from iit_amd.tasks.mqnli import make_mqnli_task
+    _, fast = _bert_pair_models()
+    ds, hl, corr = make_mqnli_task(fast, n_samples=512, device=dev)
+    pair = IITBehaviorModelPair(hl, fast, corr, training_args={"batch_size": 64, "lr": 1e-3, "lr_scheduler": None,
+                                                                "early_stop": False})
+    opt = pair.make_optimizer(1e-3)
+    loader = IITDataset(ds, ds, seed=0, device=dev).make_loader(64, 0)
+    losses = []
+    for i, (base, abl) in enumerate(loader):
+        if i >= 6:
+            break
+        out = pair.run_train_step(base, abl, pair.loss_fn, opt)
+        losses.append(float(out["train/behavior_loss"]))
+    assert fast.ops().shadow.mode == "mirror"
+    assert all(torch.isfinite(torch.tensor(losses)))
