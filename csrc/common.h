@@ -43,4 +43,10 @@ __device__ __forceinline__ float gelu_new_grad_f(float x) {
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
 }
 
+// exact (erf) GELU, as BERT / torch.nn.functional.gelu
+__device__ __forceinline__ float gelu_erf_f(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
+__device__ __forceinline__ float gelu_erf_grad_f(float x) {
+  return 0.5f * (1.f + erff(x * 0.7071067811865476f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -28,6 +28,7 @@ enum Epi : int {
   EPI_F32_ACC = 5,    // C(f32) += acc   (atomic when p.atomic)
   EPI_F32_ACC_QKV = 6,// head-blocked scatter-accumulate into 3 TL-layout grads
   EPI_F32_STORE = 7,  // C(f32) = acc (+bias)
+  EPI_GELU_ERF = 8,   // as EPI_GELU with the exact (erf) GELU (BERT)
 };
 
 struct GemmArgs {
@@ -238,10 +239,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
         } else if (EPI == EPI_F32_RESID) {
           if (p.bias0) v += p.bias0[col];
           ((float*)p.C)[(long)row * p.ldc + col] = p.resid[(long)row * p.ldr + col] + v;
-        } else if (EPI == EPI_GELU) {
+        } else if (EPI == EPI_GELU || EPI == EPI_GELU_ERF) {
           if (p.bias0) v += p.bias0[col];
           ((__bf16*)p.C2)[(long)row * p.ldc2 + col] = f2bf(v);
-          ((__bf16*)p.C)[(long)row * p.ldc + col] = f2bf(gelu_new_f(v));
+          ((__bf16*)p.C)[(long)row * p.ldc + col] = f2bf(EPI == EPI_GELU ? gelu_new_f(v) : gelu_erf_f(v));
         } else if (EPI == EPI_DGELU) {
           const float pre = bf2f(((const __bf16*)p.aux)[(long)row * p.ldc2 + col]);
           ((__bf16*)p.C)[(long)row * p.ldc + col] = f2bf(v * gelu_new_grad_f(pre));
@@ -309,6 +310,7 @@ IIT_EXPORT int iit_gemm(const void* A, const void* B, void* C, void* C2, void* C
   IIT_GEMM_CASE(0, false, false, false, false, EPI_BF16_BIAS3)
   IIT_GEMM_CASE(0, false, false, false, false, EPI_F32_RESID)
   IIT_GEMM_CASE(0, false, false, false, false, EPI_GELU)
+  IIT_GEMM_CASE(0, false, false, false, false, EPI_GELU_ERF)
   IIT_GEMM_CASE(0, false, false, false, false, EPI_DGELU)
   IIT_GEMM_CASE(0, false, false, false, false, EPI_F32_STORE)
   IIT_GEMM_CASE(0, false, false, false, false, EPI_F32_ACC)
@@ -317,6 +319,7 @@ IIT_EXPORT int iit_gemm(const void* A, const void* B, void* C, void* C2, void* C
   IIT_GEMM_CASE(2, false, true, false, false, EPI_BF16_BIAS3)
   IIT_GEMM_CASE(2, false, true, false, false, EPI_F32_RESID)
   IIT_GEMM_CASE(2, false, true, false, false, EPI_GELU)
+  IIT_GEMM_CASE(2, false, true, false, false, EPI_GELU_ERF)
   IIT_GEMM_CASE(2, false, true, false, false, EPI_F32_STORE)
   // dX from the fp32 residual-stream gradient
   IIT_GEMM_CASE(4, false, false, true, false, EPI_BF16)

@@ -31,7 +31,8 @@
 
 namespace {
 
-enum : int { E_BF16 = 0, E_BF16_BIAS3 = 1, E_F32_RESID = 2, E_GELU = 3, E_F32_ACC = 5, E_F32_STORE = 7 };
+enum : int { E_BF16 = 0, E_BF16_BIAS3 = 1, E_F32_RESID = 2, E_GELU = 3, E_F32_ACC = 5, E_F32_STORE = 7,
+             E_GELU_ERF = 8 };
 
 struct G2Args {
   const __bf16* A;
@@ -274,12 +275,15 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
       if (p.bias0) add8(v, p.bias0 + col);
       add8(v, p.resid + (long)row * p.ldr + col);
       store8_f32((float*)p.C + (long)row * p.ldc + col, v);
-    } else if constexpr (EPI == E_GELU) {
+    } else if constexpr (EPI == E_GELU || EPI == E_GELU_ERF) {
       if (p.bias0) add8(v, p.bias0 + col);
       store8_bf16((__bf16*)p.C2 + (long)row * p.ldc2 + col, v);
       float g[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] = gelu_new_dev(bf2f(f2bf(v[e])));  // gelu of the stored (bf16) pre
+      for (int e = 0; e < 8; ++e) {  // gelu of the stored (bf16) pre, which the backward reads
+        const float x = bf2f(f2bf(v[e]));
+        g[e] = EPI == E_GELU ? gelu_new_dev(x) : gelu_erf_f(x);
+      }
       store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, g);
     } else if constexpr (EPI == E_F32_ACC) {
       float* dst = (float*)p.C + (long)row * p.ldc + col;
@@ -327,7 +331,7 @@ IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, con
   if (!(mode == 0 || mode == 2 || mode == 3)) return 0;
   const bool epi_ok = mode == 3 ? (epi == E_F32_ACC || epi == E_F32_STORE)
                                 : (epi == E_BF16 || epi == E_BF16_BIAS3 || epi == E_F32_RESID || epi == E_GELU ||
-                                   epi == E_F32_ACC || epi == E_F32_STORE);
+                                   epi == E_GELU_ERF || epi == E_F32_ACC || epi == E_F32_STORE);
   if (!epi_ok) return 0;
   if (mode == 0 && !(epi == E_BF16 || epi == E_F32_ACC || epi == E_F32_STORE)) return 0;
   if (M <= 0 || N <= 0 || K <= 0 || M % kTileBM[tile] || N % kTileBN[tile] || K % 64) return 0;
@@ -359,6 +363,7 @@ IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, co
   G2(2, false, true, E_BF16_BIAS3)
   G2(2, false, true, E_F32_RESID)
   G2(2, false, true, E_GELU)
+  G2(2, false, true, E_GELU_ERF)
   G2(2, false, true, E_F32_ACC)
   G2(2, false, true, E_F32_STORE)
   G2(3, true, true, E_F32_ACC)

@@ -909,6 +909,7 @@ __device__ __forceinline__ float gelu_new_fast(float x) {
   return 0.5f * x * (1.f + t);
 }
 
+template <bool ERF>
 __global__ __launch_bounds__(256) void gelu_fwd_kernel(const __bf16* __restrict__ pre, long ldp, __bf16* __restrict__ out,
                                                        long ldo, int M, int N) {
   const int n8 = N >> 3;
@@ -918,34 +919,44 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const __bf16* __restrict_
     const bf16x8 x = *(const bf16x8*)(pre + m * ldp + c);
     bf16x8 o;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_new_fast(bf2f(x[e])));
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(ERF ? gelu_erf_f(bf2f(x[e])) : gelu_new_fast(bf2f(x[e])));
     *(bf16x8*)(out + m * ldo + c) = o;
   }
 }
 
+template <bool ERF>
 __global__ void gelu_fwd_scalar_kernel(const __bf16* __restrict__ pre, long ldp, __bf16* __restrict__ out, long ldo,
                                        int M, int N) {
   const long total = (long)M * N;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const int m = (int)(i / N), n = (int)(i % N);
-    out[m * ldo + n] = f2bf(gelu_new_fast(bf2f(pre[m * ldp + n])));
+    const float x = bf2f(pre[m * ldp + n]);
+    out[m * ldo + n] = f2bf(ERF ? gelu_erf_f(x) : gelu_new_fast(x));
   }
 }
 
-IIT_EXPORT int iit_gelu_fwd(const void* pre, long ldp, void* out, long ldo, int M, int N, void* stream) {
+IIT_EXPORT int iit_gelu_fwd(const void* pre, long ldp, void* out, long ldo, int M, int N, int erf, void* stream) {
   const bool vec = N % 8 == 0 && ldp % 8 == 0 && ldo % 8 == 0 && ((((uintptr_t)pre) | ((uintptr_t)out)) & 15) == 0;
   const long work = vec ? (long)M * (N / 8) : (long)M * N;
   const int blocks = (int)min((work + 255) / 256, 8192L);
-  if (vec)
-    hipLaunchKernelGGL(gelu_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const __bf16*)pre, ldp,
-                       (__bf16*)out, ldo, M, N);
-  else
-    hipLaunchKernelGGL(gelu_fwd_scalar_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const __bf16*)pre,
-                       ldp, (__bf16*)out, ldo, M, N);
+  hipStream_t st = (hipStream_t)stream;
+  const __bf16* pp = (const __bf16*)pre;
+  __bf16* oo = (__bf16*)out;
+  if (vec) {
+    if (erf) hipLaunchKernelGGL(gelu_fwd_kernel<true>, dim3(blocks), dim3(256), 0, st, pp, ldp, oo, ldo, M, N);
+    else hipLaunchKernelGGL(gelu_fwd_kernel<false>, dim3(blocks), dim3(256), 0, st, pp, ldp, oo, ldo, M, N);
+  } else {
+    if (erf) hipLaunchKernelGGL(gelu_fwd_scalar_kernel<true>, dim3(blocks), dim3(256), 0, st, pp, ldp, oo, ldo, M, N);
+    else hipLaunchKernelGGL(gelu_fwd_scalar_kernel<false>, dim3(blocks), dim3(256), 0, st, pp, ldp, oo, ldo, M, N);
+  }
   return hipGetLastError();
 }
 
-// dpre = dpost * gelu_new'(pre)   (bf16, contiguous; 8 elements / 16 B per thread when n % 8 == 0)
+// dpre = dpost * gelu'(pre)   (bf16, contiguous; 8 elements / 16 B per thread when n % 8 == 0); gelu_new or erf
+template <bool ERF>
+__device__ __forceinline__ float dgelu_of(float x) { return ERF ? gelu_erf_grad_f(x) : gelu_new_grad_f(x); }
+
+template <bool ERF>
 __global__ void dgelu_kernel(const __bf16* __restrict__ dpost, const __bf16* __restrict__ pre, __bf16* __restrict__ out, long n) {
   if ((n & 7) == 0) {
     const long n8 = n >> 3;
@@ -953,20 +964,24 @@ __global__ void dgelu_kernel(const __bf16* __restrict__ dpost, const __bf16* __r
       const bf16x8 g = ((const bf16x8*)dpost)[i], x = ((const bf16x8*)pre)[i];
       bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(g[e]) * gelu_new_grad_f(bf2f(x[e])));
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(g[e]) * dgelu_of<ERF>(bf2f(x[e])));
       ((bf16x8*)out)[i] = o;
     }
     return;
   }
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
-    out[i] = f2bf(bf2f(dpost[i]) * gelu_new_grad_f(bf2f(pre[i])));
+    out[i] = f2bf(bf2f(dpost[i]) * dgelu_of<ERF>(bf2f(pre[i])));
 }
 
-IIT_EXPORT int iit_dgelu(const void* dpost, const void* pre, void* out, long n, void* stream) {
+IIT_EXPORT int iit_dgelu(const void* dpost, const void* pre, void* out, long n, int erf, void* stream) {
   const long work = (n & 7) == 0 ? n / 8 : n;
   const int blocks = (int)min((work + 255) / 256, 8192L);
-  hipLaunchKernelGGL(dgelu_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const __bf16*)dpost,
-                     (const __bf16*)pre, (__bf16*)out, n);
+  if (erf)
+    hipLaunchKernelGGL(dgelu_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const __bf16*)dpost,
+                       (const __bf16*)pre, (__bf16*)out, n);
+  else
+    hipLaunchKernelGGL(dgelu_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const __bf16*)dpost,
+                       (const __bf16*)pre, (__bf16*)out, n);
   return hipGetLastError();
 }
 

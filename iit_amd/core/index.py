@@ -19,6 +19,8 @@ from __future__ import annotations
 
 from typing import Iterable, Optional, Tuple, Union
 
+import torch
+
 IndexAtom = Union[None, int, slice, list]
 
 
@@ -38,7 +40,7 @@ def _freeze(atom: IndexAtom):
 class TorchIndex:
     """A hashable, intersectable tensor index."""
 
-    __slots__ = ("as_index", "hashable_tuple", "_atoms")
+    __slots__ = ("as_index", "hashable_tuple", "_atoms", "_dev")
 
     def __init__(self, list_of_things_in_tuple: Iterable[IndexAtom]):
         if not isinstance(list_of_things_in_tuple, (tuple, list)):
@@ -52,6 +54,22 @@ class TorchIndex:
         self._atoms = atoms
         self.as_index: Tuple = tuple(slice(None) if a is None else a for a in atoms)
         self.hashable_tuple = tuple(_freeze(a) for a in atoms)
+        self._dev = None
+
+    def on(self, device) -> Tuple:
+        """``as_index`` with list atoms as cached int64 tensors on ``device``: indexing a GPU tensor with a Python
+        list copies the list host-to-device on every call, which a captured HIP graph cannot contain (and which
+        costs a sync-free but real copy per splice).  The first call per device builds the tensors."""
+        if not any(isinstance(a, list) for a in self._atoms):
+            return self.as_index
+        device = torch.device(device)
+        if self._dev is None:
+            self._dev = {}
+        ix = self._dev.get(device)
+        if ix is None:
+            ix = self._dev[device] = tuple(torch.tensor(a, dtype=torch.long, device=device) if isinstance(a, list)
+                                           else a for a in self.as_index)
+        return ix
 
     # -- identity -----------------------------------------------------------
     def __hash__(self) -> int:

@@ -70,7 +70,7 @@ class Splice:
                 src = src.expand_as(act)
             return src
         out = act.clone()
-        ix = self.index.as_index
+        ix = self.index.on(act.device)
         out[ix] = src[ix] if src.shape == act.shape else src.expand_as(act)[ix]
         return out
 

@@ -79,7 +79,7 @@ class _Run:
                 def _mask(g, _idxs=idxs):
                     g = g.clone()
                     for ix in _idxs:
-                        g[ix.as_index] = 0
+                        g[ix.on(g.device)] = 0
                     return g
 
                 x = x.view_as(x)

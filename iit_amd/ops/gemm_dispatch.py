@@ -127,11 +127,11 @@ def _addmm_f32(c, base, a, b) -> None:
         torch.add(base, _mm_f32(a, b), out=c)
 
 
-def _gelu_into(pre, out) -> None:
+def _gelu_into(pre, out, erf: bool = False) -> None:
     if pre.is_cuda and pre.dtype == BF16 and out.dtype == BF16 and pre.dim() == 2:
-        K.gelu_fwd(pre, out, pre.shape[0], pre.shape[1])
+        K.gelu_fwd(pre, out, pre.shape[0], pre.shape[1], erf=erf)
     else:
-        torch._C._nn.gelu(pre, approximate="tanh", out=out)
+        torch._C._nn.gelu(pre, approximate="none" if erf else "tanh", out=out)
 
 
 def _blas(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, C2, C3, bias0, bias1, bias2, resid, ldr, aux, ldc2, bias_cols,
@@ -154,10 +154,10 @@ def _blas(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, C2, C3, bias0, bias1, bia
         _addmm_f32(c, _as(resid, M, N, ldr), a, b)
         if bias0 is not None:
             c.add_(bias0.reshape(-1))
-    elif epi == K.EPI_GELU:
+    elif epi in (K.EPI_GELU, K.EPI_GELU_ERF):
         pre = _as(C2, M, N, ldc2)
         torch.addmm(bias0.reshape(-1).to(BF16), a, b, out=pre)
-        _gelu_into(pre, _as(C, M, N, ldc))
+        _gelu_into(pre, _as(C, M, N, ldc), erf=epi == K.EPI_GELU_ERF)
     elif epi == K.EPI_DGELU:
         tmp = torch.mm(a, b)
         K.dgelu(tmp, _as(aux, M, N, ldc2).contiguous(), _as(C, M, N, ldc))

@@ -20,6 +20,7 @@ from . import build as _build
 c_void_p, c_long, c_int, c_float, c_ull = ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_float, ctypes.c_ulonglong
 
 EPI_BF16, EPI_BF16_BIAS3, EPI_F32_RESID, EPI_GELU, EPI_DGELU, EPI_F32_ACC, EPI_F32_ACC_QKV, EPI_F32_STORE = range(8)
+EPI_GELU_ERF = 8  # EPI_GELU with the exact (erf) GELU
 MODE_NN, MODE_AKM, MODE_BKM, MODE_AF32, MODE_BF32 = 0, 1, 2, 4, 8
 
 _LIB = None
@@ -43,11 +44,11 @@ _SIGS = {
                    c_void_p],
     "iit_adam_flat": [c_void_p] * 6 + [c_int, c_void_p, c_int] + [c_float] * 6 + [c_void_p, c_void_p, c_void_p],
     "iit_adam_span_size": [],
-    "iit_gelu_fwd": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_void_p],
+    "iit_gelu_fwd": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_void_p],
     "iit_shadow_refresh": [c_void_p, c_int, c_void_p],
     "iit_shadow_desc_size": [],
     "iit_colsum_accum": [c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_void_p],
-    "iit_dgelu": [c_void_p, c_void_p, c_void_p, c_long, c_void_p],
+    "iit_dgelu": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p],
     "iit_add_bf16": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_int, c_void_p],
     "iit_device_sync": [],
 }
@@ -210,13 +211,13 @@ def colsum3_accum(x, ld, outs, T, N):
         colsum_accum(x[:, i * N:], ld, o, T, N)
 
 
-def gelu_fwd(pre, out, M, N):
-    """out = gelu_new(pre), bf16 [M, N] views with unit column stride (any row strides)."""
-    _check(lib().iit_gelu_fwd(_p(pre), pre.stride(0), _p(out), out.stride(0), M, N, _stream()), "gelu_fwd")
+def gelu_fwd(pre, out, M, N, erf=False):
+    """out = gelu(pre) (gelu_new, or the exact erf form), bf16 [M, N] views with unit column stride."""
+    _check(lib().iit_gelu_fwd(_p(pre), pre.stride(0), _p(out), out.stride(0), M, N, int(erf), _stream()), "gelu_fwd")
 
 
-def dgelu(dpost, pre, out):
-    _check(lib().iit_dgelu(_p(dpost), _p(pre), _p(out), dpost.numel(), _stream()), "dgelu")
+def dgelu(dpost, pre, out, erf=False):
+    _check(lib().iit_dgelu(_p(dpost), _p(pre), _p(out), dpost.numel(), int(erf), _stream()), "dgelu")
 
 
 def add_bf16(out, ldo, base, ldb, y, ldy, bias, M, N):

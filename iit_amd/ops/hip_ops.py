@@ -545,8 +545,9 @@ class MLPInFn(Function):
     """(pre, post) = (x @ W_in + b_in, gelu_new(pre)) in one GEMM epilogue."""
 
     @staticmethod
-    def forward(ctx, x, W_in, b_in, w):
+    def forward(ctx, x, W_in, b_in, w, erf=False):
         ctx.set_materialize_grads(False)
+        ctx.erf = erf
         lead = x.shape[:-1]
         d = x.shape[-1]
         dm = W_in.shape[1]
@@ -554,7 +555,7 @@ class MLPInFn(Function):
         T = x2.shape[0]
         post = torch.empty(T, dm, dtype=BF16, device=x.device)
         pre = torch.empty(T, dm, dtype=BF16, device=x.device)
-        gemm(x2, w, post, C2=pre, M=T, N=dm, K=d, lda=d, ldb=dm, ldc=dm, ldc2=dm, mode=K.MODE_BKM, epi=K.EPI_GELU,
+        gemm(x2, w, post, C2=pre, M=T, N=dm, K=d, lda=d, ldb=dm, ldc=dm, ldc2=dm, mode=K.MODE_BKM, epi=K.EPI_GELU_ERF if erf else K.EPI_GELU,
              bias0=b_in)
         ctx.save_for_backward(x2, pre)
         ctx.params = (W_in, b_in)
@@ -565,14 +566,14 @@ class MLPInFn(Function):
     @staticmethod
     def backward(ctx, gpre, gpost):
         if gpre is None and gpost is None:
-            return None, None, None, None
+            return None, None, None, None, None
         x2, pre = ctx.saved_tensors
         W_in, b_in = ctx.params
         lead, d, dm = ctx.meta
         T = x2.shape[0]
         if gpost is not None:
             dpre = torch.empty(T, dm, dtype=BF16, device=x2.device)
-            K.dgelu(gpost.to(BF16).contiguous().view(T, dm), pre, dpre)
+            K.dgelu(gpost.to(BF16).contiguous().view(T, dm), pre, dpre, erf=ctx.erf)
             if gpre is not None:
                 dpre = (dpre.float() + gpre.float().reshape(T, dm)).to(BF16)
         else:
@@ -586,7 +587,7 @@ class MLPInFn(Function):
         if gb is not None:
             K.colsum_accum(dpre, dm, gb, T, dm)
         _done(W_in, b_in)
-        return dx.view(*lead, d), None, None, None
+        return dx.view(*lead, d), None, None, None, None
 
 
 class CrossEntropyFn(Function):
@@ -710,8 +711,8 @@ class HipOps(TorchOps):
     # -- MLP ---------------------------------------------------------------------------
     def mlp_in(self, x, W_in, b_in, act: str, hook_pre=None):
         w = self._L(W_in)["in"]
-        if hook_pre is None and act in ("gelu_new", "gelu_fast", "gelu_pytorch_tanh"):
-            return MLPInFn.apply(x, W_in, b_in, w)
+        if hook_pre is None and act in ("gelu_new", "gelu_fast", "gelu_pytorch_tanh", "gelu"):
+            return MLPInFn.apply(x, W_in, b_in, w, act == "gelu")
         pre = LinearFn.apply(x, W_in, b_in, w, W_in.shape[1], None, "bf16")
         if hook_pre is not None:
             pre = hook_pre(pre)

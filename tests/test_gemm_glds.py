@@ -38,7 +38,7 @@ def _ops(K, mode, M, N, Kd, pad):
     return A, B, lda, ldb, a.float(), b.float()
 
 
-CASES = [(0, 0), (0, 5), (0, 7), (2, 0), (2, 1), (2, 2), (2, 3), (2, 5), (2, 7), (3, 5), (3, 7)]
+CASES = [(0, 0), (0, 5), (0, 7), (2, 0), (2, 1), (2, 2), (2, 3), (2, 8), (2, 5), (2, 7), (3, 5), (3, 7)]
 
 
 @pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
@@ -51,7 +51,7 @@ def test_glds_gemm_matches_fp32(K, mode, epi, tile):
     ldc = N + 8
     bias = torch.randn(N, device=dev)
     kw = dict(M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, tile=tile)
-    if epi in (K.EPI_BF16, K.EPI_BF16_BIAS3, K.EPI_GELU):
+    if epi in (K.EPI_BF16, K.EPI_BF16_BIAS3, K.EPI_GELU, K.EPI_GELU_ERF):
         C = torch.zeros(M, ldc, device=dev, dtype=torch.bfloat16)
     else:
         C = torch.randn(M, ldc, device=dev)
@@ -68,10 +68,10 @@ def test_glds_gemm_matches_fp32(K, mode, epi, tile):
         R = torch.randn(M, N + 16, device=dev)
         extra = dict(bias0=bias, resid=R, ldr=N + 16)
         exp = ref + bias + R[:, :N]
-    elif epi == K.EPI_GELU:
+    elif epi in (K.EPI_GELU, K.EPI_GELU_ERF):
         C2 = torch.zeros(M, ldc, device=dev, dtype=torch.bfloat16)
         extra = dict(bias0=bias, C2=C2, ldc2=ldc)
-        exp = gelu_new(ref + bias)
+        exp = gelu_new(ref + bias) if epi == K.EPI_GELU else torch.nn.functional.gelu(ref + bias)
     elif epi == K.EPI_F32_ACC:
         exp = C0[:, :N] + ref
     else:
@@ -84,7 +84,7 @@ def test_glds_gemm_matches_fp32(K, mode, epi, tile):
     got = C[:, :N].float()
     err = ((got - exp).norm() / exp.norm()).item()
     assert err < 1e-2, err
-    if epi == K.EPI_GELU:
+    if epi in (K.EPI_GELU, K.EPI_GELU_ERF):
         pre = extra["C2"][:, :N].float()
         assert ((pre - (ref + bias)).norm() / (ref + bias).norm()).item() < 1e-2
     assert torch.equal(C[:, N:], C0[:, N:])  # padding columns untouched

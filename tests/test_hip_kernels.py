@@ -139,6 +139,14 @@ def test_gelu_fwd_and_pos_bwd(K):
     out2 = torch.empty(300, 7, dtype=torch.bfloat16, device=dev)
     K.gelu_fwd(pre[:, :7], out2, 300, 7)  # scalar path
     assert rel_err(out2, gelu_new(pre[:, :7].float())) < 4e-3
+    K.gelu_fwd(pre[:, :1024], out, 300, 1024, erf=True)
+    assert rel_err(out, torch.nn.functional.gelu(pre[:, :1024].float())) < 4e-3
+    g = bf(torch.randn(300, 1024, device=dev))
+    x = pre[:, :1024].float().contiguous().requires_grad_(True)
+    torch.nn.functional.gelu(x).backward(g.float())
+    dpre = torch.empty(300, 1024, dtype=torch.bfloat16, device=dev)
+    K.dgelu(g, pre[:, :1024].contiguous(), dpre, erf=True)
+    assert rel_err(dpre, x.grad) < 1e-2
     B, S, d = 33, 16, 768
     g = torch.randn(B * S, d, device=dev)
     tok = torch.randint(0, 50, (B * S,), device=dev)
