@@ -28,7 +28,7 @@ Data parallel: collectives are never captured.  Each phase becomes graphs
 around eager gradient all-reduces -- ``[forward + backward of the top layers]``,
 then one graph per lower stage of layers, each followed by the bucketed RCCL
 all-reduce of the arena range it finished (overlapping the next stage, see
-:mod:`iit_amd.engine.staged`; ``IIT_DP_STAGES``, default 4), then ``[clip +
+:mod:`iit_amd.engine.staged`; ``IIT_DP_STAGES``, default 6), then ``[clip +
 Adam]`` -- so every rank issues the identical collective sequence whatever gets
 captured, and the launch-bound compute still runs as replays.
 (``IIT_GRAPHS_DP=0`` keeps DP runs fully eager.)

@@ -29,7 +29,7 @@ import torch
 
 
 class StagedBackward:
-    def __init__(self, model, n_stages: int = 4):
+    def __init__(self, model, n_stages: int = 6):
         self.model = model
         L = len(getattr(model, "blocks", []))
         n_stages = max(1, min(int(n_stages), L))
@@ -80,7 +80,7 @@ class StagedBackward:
 def staged_for(pair, n_stages: Optional[int] = None) -> Optional[StagedBackward]:
     """A StagedBackward for the pair's LL model, or None when it does not apply."""
     import os
-    n = int(os.environ.get("IIT_DP_STAGES", "4")) if n_stages is None else n_stages
+    n = int(os.environ.get("IIT_DP_STAGES", "6")) if n_stages is None else n_stages
     model = pair._ll_module() if hasattr(pair, "_ll_module") else getattr(pair, "ll_model", None)
     if n <= 1 or model is None or not hasattr(model, "blocks"):
         return None
