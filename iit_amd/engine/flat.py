@@ -85,6 +85,7 @@ class FlatParams:
                 view.copy_(p.detach().float())
                 p.data = view
                 p.grad = fn(self.grad)
+                p._iit_flat = self  # back-reference: bf16 mirror lookup by the torch op backend
         self.index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
         self.version = 0
         self.mirror_version = -1

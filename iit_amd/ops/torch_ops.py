@@ -32,6 +32,70 @@ def act_fn(name: str):
     raise ValueError(f"unknown act_fn {name}")
 
 
+def _arena_mirror(p: torch.Tensor):
+    """(flat arena, bf16 mirror view of ``p``) when ``p`` lives in a :class:`~iit_amd.engine.flat.FlatParams` on
+    a GPU and the mirror holds its current value (else None).  The fused Adam writes the mirror in its update
+    pass, so a bf16 model reads its weights without a per-forward cast."""
+    flat = getattr(p, "_iit_flat", None)
+    if flat is None or not p.is_cuda or not p.requires_grad or not flat.owns(p):
+        return None
+    module = flat.module
+    if flat.shadow is None or flat.mirror_version != getattr(module, "_iit_weights_version", 0):
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        flat.ensure_shadow()
+        flat.refresh_shadow()
+    return flat, flat.shadow_view(p)
+
+
+def _accumulate(p: torch.Tensor, g: torch.Tensor) -> None:
+    """fp32 grad slot += bf16 gradient in one mixed-precision pass; report it to the DP reducer."""
+    from ..engine import grad_hooks
+    slot = p.grad
+    if slot is None:
+        slot = p.grad = torch.zeros_like(p)
+    slot.add_(g)
+    grad_hooks.notify(p)
+
+
+class _MirrorWeight(torch.autograd.Function):
+    """bf16 compute copy of an arena weight: forward returns the mirror view (no cast kernel); backward adds the
+    bf16 gradient straight into the fp32 grad slot (no cast-to-fp32 pass, no AccumulateGrad)."""
+
+    @staticmethod
+    def forward(ctx, p, _flat):
+        ctx.p = p
+        return _flat.shadow_view(p)
+
+    @staticmethod
+    def backward(ctx, g):
+        _accumulate(ctx.p, g)
+        return None, None
+
+
+class _MirrorEmbed(torch.autograd.Function):
+    """``W_E[tokens]`` from the bf16 mirror; backward index-adds the rows into the fp32 grad slot (no dense
+    ``[V, d]`` gradient is ever materialised -- 128k x 4096 for Llama-3)."""
+
+    @staticmethod
+    def forward(ctx, tokens, W_E, _flat):
+        ctx.save_for_backward(tokens)
+        ctx.p = W_E
+        return _flat.shadow_view(W_E)[tokens]
+
+    @staticmethod
+    def backward(ctx, g):
+        (tokens,) = ctx.saved_tensors
+        from ..engine import grad_hooks
+        W_E = ctx.p
+        slot = W_E.grad
+        if slot is None:
+            slot = W_E.grad = torch.zeros_like(W_E)
+        slot.index_add_(0, tokens.reshape(-1), g.reshape(-1, g.shape[-1]).to(slot.dtype))
+        grad_hooks.notify(W_E)
+        return None, None, None
+
+
 class TorchOps:
     name = "torch"
     fused = False
@@ -41,10 +105,26 @@ class TorchOps:
 
     # -- helpers --------------------------------------------------------------
     def w(self, p: torch.Tensor) -> torch.Tensor:
-        return p if p.dtype == self.dtype else p.to(self.dtype)
+        if p.dtype == self.dtype:
+            return p
+        if self.dtype == torch.bfloat16 and torch.is_grad_enabled():
+            m = _arena_mirror(p)
+            if m is not None:
+                return _MirrorWeight.apply(p, m[0])
+        elif self.dtype == torch.bfloat16:
+            m = _arena_mirror(p)
+            if m is not None:
+                return m[1]
+        return p.to(self.dtype)
 
     # -- ops ------------------------------------------------------------------
     def embed(self, tokens, W_E):
+        if self.dtype == torch.bfloat16 and W_E.dtype != self.dtype:
+            m = _arena_mirror(W_E)
+            if m is not None:
+                if torch.is_grad_enabled():
+                    return _MirrorEmbed.apply(tokens, W_E, m[0])
+                return m[1][tokens]
         return self.w(W_E)[tokens]
 
     def pos_embed(self, batch: int, seq: int, W_pos, offset: int = 0):

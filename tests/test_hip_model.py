@@ -203,3 +203,23 @@ def test_mqnli_bert_pair_trains_on_hip_arena():
         losses.append(float(out["train/behavior_loss"]))
     assert fast.ops().shadow.mode == "mirror"
     assert all(torch.isfinite(torch.tensor(losses)))
+
+
+def test_torch_backend_reads_arena_mirror_and_accumulates_in_place():
+    """Llama-family (torch op backend, bf16 on GPU): weights come from the arena's bf16 mirror and gradients land
+    in the fp32 arena in one pass -- same values as the plain cast + AccumulateGrad path."""
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.models.convert import llama_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    cfg = llama_config_dict("llama-tiny", device=dev, dtype=torch.bfloat16)
+    torch.manual_seed(0)
+    a = HookedTransformer(cfg)
+    b = copy.deepcopy(a)
+    flat = FlatParams(a)
+    tok = torch.randint(0, cfg["d_vocab"], (4, 9), device=dev)
+    for m in (a, b):
+        m(tok).float().pow(2).mean().backward()
+    assert flat.shadow is not None  # the mirror was used
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert torch.allclose(pa.grad, pb.grad, rtol=1e-3, atol=1e-6), n
+    assert flat.grad.abs().sum() > 0
