@@ -96,6 +96,44 @@ class _MirrorEmbed(torch.autograd.Function):
         return None, None, None
 
 
+class _MirrorLinear(torch.autograd.Function):
+    """``x @ W (+ b)`` for an arena weight ``W [K, N]``: both GEMMs read the bf16 mirror, and the weight
+    gradient is one fp32-output GEMM accumulating straight into the arena's grad slot (``addmm`` with
+    beta = 1) -- no bf16 ``dW`` tensor, no cast, no separate accumulate pass over the matrix."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, _flat):
+        Wm = _flat.shadow_view(W)
+        lead = x.shape[:-1]
+        x2 = x.reshape(-1, x.shape[-1])
+        y = x2 @ Wm
+        if b is not None:
+            y = y + _flat.shadow_view(b)
+        ctx.save_for_backward(x2)
+        ctx.W, ctx.b, ctx.flat, ctx.lead = W, b, _flat, lead
+        return y.view(*lead, y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, gy):
+        from ..engine import grad_hooks
+        from .gemm_dispatch import _addmm_f32
+        (x2,) = ctx.saved_tensors
+        W, b, flat = ctx.W, ctx.b, ctx.flat
+        g2 = gy.reshape(-1, gy.shape[-1]).to(x2.dtype)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (g2 @ flat.shadow_view(W).t()).view(*ctx.lead, W.shape[0])
+        if W.requires_grad:
+            slot = W.grad
+            if slot is None:
+                slot = W.grad = torch.zeros_like(W)
+            _addmm_f32(slot, slot, x2.t(), g2)
+            grad_hooks.notify(W)
+        if b is not None and b.requires_grad:
+            _accumulate(b, g2.float().sum(0))
+        return dx, None, None, None
+
+
 class TorchOps:
     name = "torch"
     fused = False
@@ -116,6 +154,16 @@ class TorchOps:
             if m is not None:
                 return m[1]
         return p.to(self.dtype)
+
+    def lin(self, x, W, b=None):
+        """``x @ W (+ b)``; arena weights on a GPU in bf16 take :class:`_MirrorLinear`."""
+        if (self.dtype == torch.bfloat16 and W.dim() == 2 and W.dtype != self.dtype and x.is_cuda
+                and torch.is_grad_enabled() and W.is_contiguous()):
+            m = _arena_mirror(W)
+            if m is not None and (b is None or (_arena_mirror(b) is not None and b.is_contiguous())):
+                return _MirrorLinear.apply(x.to(self.dtype), W, b, m[0])
+        y = x @ self.w(W)
+        return y if b is None else y + self.w(b)
 
     # -- ops ------------------------------------------------------------------
     def embed(self, tokens, W_E):
@@ -202,26 +250,26 @@ class TorchOps:
         return torch.einsum("bshe,hed->bshd", z, self.w(W_O))
 
     def mlp_in(self, x, W_in, b_in, act: str, hook_pre=None):
-        pre = x @ self.w(W_in) + self.w(b_in)
+        pre = self.lin(x, W_in, b_in)
         if hook_pre is not None:
             pre = hook_pre(pre)
         return pre, act_fn(act)(pre)
 
     def mlp_gated_in(self, x, W_gate, W_in, b_in, act: str, hook_pre=None, hook_pre_linear=None):
         """TL ``GatedMLP``: ``pre = x W_gate`` (hook_pre), ``pre_linear = x W_in + b_in``, ``post = act(pre) * pre_linear``."""
-        pre = x @ self.w(W_gate)
+        pre = self.lin(x, W_gate)
         if hook_pre is not None:
             pre = hook_pre(pre)
-        pre_linear = x @ self.w(W_in) + self.w(b_in)
+        pre_linear = self.lin(x, W_in, b_in)
         if hook_pre_linear is not None:
             pre_linear = hook_pre_linear(pre_linear)
         return pre, act_fn(act)(pre) * pre_linear
 
     def mlp_out(self, post, W_out, b_out):
-        return post @ self.w(W_out) + self.w(b_out)
+        return self.lin(post, W_out, b_out)
 
     def unembed(self, x, W_U, b_U):
-        return x @ self.w(W_U) + self.w(b_U)
+        return self.lin(x, W_U, b_U)
 
     def unembed_argmax(self, x, W_U, b_U, chunk: int = 16384):
         """``argmax(x @ W_U + b_U, -1)`` with first-index tie-break, vocab-chunked (bounded memory)."""
