@@ -207,7 +207,8 @@ def test_mqnli_bert_pair_trains_on_hip_arena():
 
 def test_torch_backend_reads_arena_mirror_and_accumulates_in_place():
     """Llama-family (torch op backend, bf16 on GPU): weights come from the arena's bf16 mirror and gradients land
-    in the fp32 arena in one pass -- same values as the plain cast + AccumulateGrad path."""
+    in the fp32 arena directly (fp32-output weight-gradient GEMMs, fp32 bias sums) -- the plain cast +
+    AccumulateGrad path agrees to bf16 rounding (it rounds dW and the bias sums to bf16 first)."""
     from iit_amd.engine.flat import FlatParams
     from iit_amd.models.convert import llama_config_dict
     from iit_amd.models.transformer import HookedTransformer
@@ -221,5 +222,5 @@ def test_torch_backend_reads_arena_mirror_and_accumulates_in_place():
         m(tok).float().pow(2).mean().backward()
     assert flat.shadow is not None  # the mirror was used
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
-        assert torch.allclose(pa.grad, pb.grad, rtol=1e-3, atol=1e-6), n
+        assert rel(pa.grad, pb.grad) < 1e-2, n
     assert flat.grad.abs().sum() > 0
