@@ -11,6 +11,7 @@
 //  shadow_refresh                           fp32 master -> bf16 compute copies (+transposes)
 //  colsum_accum, dgelu, add_f32, cast       small elementwise / reduction helpers
 #include "common.h"
+#include <stdlib.h>
 
 // ============================================================================ embedding
 __global__ void embed_pos_fwd_kernel(const long* __restrict__ tok, const float* __restrict__ WE,
@@ -673,6 +674,7 @@ __global__ __launch_bounds__(256) void sumsq_span_kernel(const float* __restrict
 // Adam (torch semantics, amsgrad=False) with the clip coefficient computed on device from the partial sums,
 // the bias corrections from the device step counter, and the bf16 mirror of the updated weights written in
 // the same pass.  Streams: read g, p, m, v; write p, m, v, mirror (the clipped gradient is not written back).
+template <bool NT>
 __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         __bf16* __restrict__ mirror, const Span* __restrict__ spans,
@@ -712,7 +714,17 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
     const Span sp = spans[e];
     for (int j = threadIdx.x; j < sp.len4; j += 256) {
       const long i = sp.start4 + j;
-      float4 gg = g4[i], pp = p4[i], mm = m4[i], vv = v4[i];
+      // NT: the gradient and both moments are touched once per step -- stream them past the caches
+      float4 gg, pp = p4[i], mm, vv;
+      if (NT) {
+        gg = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)g4 + i));
+        mm = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)m4 + i));
+        vv = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)v4 + i));
+      } else {
+        gg = g4[i];
+        mm = m4[i];
+        vv = v4[i];
+      }
       float* gs = (float*)&gg;
       float* ps = (float*)&pp;
       float* ms = (float*)&mm;
@@ -726,8 +738,13 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
         ps[k] -= stepsz * ms[k] / (sqrtf(vs[k]) / bc2_sqrt + eps);
       }
       p4[i] = pp;
-      m4[i] = mm;
-      v4[i] = vv;
+      if (NT) {
+        __builtin_nontemporal_store(__builtin_bit_cast(f32x4, mm), (f32x4*)m4 + i);
+        __builtin_nontemporal_store(__builtin_bit_cast(f32x4, vv), (f32x4*)v4 + i);
+      } else {
+        m4[i] = mm;
+        v4[i] = vv;
+      }
       if (mirror) {
         bf16x4 o = {f2bf(ps[0]), f2bf(ps[1]), f2bf(ps[2]), f2bf(ps[3])};
         ((bf16x4*)mirror)[i] = o;
@@ -748,8 +765,16 @@ IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, void* mirro
   hipLaunchKernelGGL(sumsq_span_kernel, dim3(norm ? nparts : 1), dim3(256), 0, s, g, sp, nspans, part, (int)norm,
                      step);
   const int blocks = min(nspans, 4096);
-  hipLaunchKernelGGL(adam_span_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, sp, nspans, part,
-                     nparts, clip, lr, b1, b2, eps, wd, step, skipped);
+  static const int nt = [] {
+    const char* e = getenv("IIT_ADAM_NT");
+    return e ? atoi(e) : 1;
+  }();
+  if (nt)
+    hipLaunchKernelGGL(adam_span_kernel<true>, dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, sp, nspans,
+                       part, nparts, clip, lr, b1, b2, eps, wd, step, skipped);
+  else
+    hipLaunchKernelGGL(adam_span_kernel<false>, dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, sp,
+                       nspans, part, nparts, clip, lr, b1, b2, eps, wd, step, skipped);
   return hipGetLastError();
 }
 

@@ -70,6 +70,7 @@ class GraphedTrainStep:
         self.enabled = enabled
         self.split = ws > 1  # DP: graphs around the (eager) gradient all-reduce
         self.staged = None
+        self.force_staged = False  # tests: stage the backward graphs even without a data-parallel reducer
         if self.split and enabled:
             from .staged import staged_for
             self.staged = staged_for(pair)
@@ -126,7 +127,7 @@ class GraphedTrainStep:
         of layers) and each stage's gradient range is all-reduced while the next stage computes."""
         pair = self.pair
         reducer = getattr(pair, "_reducer", None)
-        stg = self.staged if reducer is not None and reducer.enabled else None
+        stg = self.staged if (reducer is not None and reducer.enabled) or self.force_staged else None
 
         def fwd_bwd():
             if stg is not None:

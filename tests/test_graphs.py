@@ -69,19 +69,28 @@ def test_prime_captures_all_phase_keys_and_keeps_rng():
     assert pair.rng.random() == before
 
 
-def test_split_graphs_for_data_parallel_match_eager():
-    """The DP form (graph[fwd+bwd] -> eager all-reduce -> graph[clip+Adam]) on one GPU (no-op reduce)."""
+@pytest.mark.parametrize("staged", [False, True])
+def test_split_graphs_for_data_parallel_match_eager(staged):
+    """The DP form (graph[fwd+bwd] -> eager all-reduce -> graph[clip+Adam]) on one GPU (no-op reduce); with
+    ``staged`` the backward is cut into per-stage graphs (engine/staged.py) exactly as data parallelism runs it."""
     from iit_amd.engine.graphs import GraphedTrainStep
+    from iit_amd.engine.staged import staged_for
     le1, _ = _run("eager")
     pair, opt, train = _setup()
     torch.manual_seed(1)
     batches = [b for _, b in zip(range(10), train.make_loader(64, 0))]
     g = GraphedTrainStep(pair, opt, pair.loss_fn)
     g.split = True
+    if staged:
+        g.staged = staged_for(pair, 3)
+        g.force_staged = True
+        assert g.staged is not None and g.staged.cuts == [2, 4]
     losses = []
     for base, abl in batches * 3:
         out = g(base, abl, pair.loss_fn, opt)
         losses.append(torch.stack([out[k] for k in sorted(out)]))
     ls = torch.stack(losses).cpu()
     assert g.captures > 0 and not g.failed, g.failed
+    if staged:
+        assert all(len(ent[0][1]) == 2 for ent in g.graphs.values())  # two lower-stage graphs per phase
     assert torch.allclose(le1[:_TIGHT], ls[:_TIGHT], rtol=2e-3, atol=2e-3), (le1[:_TIGHT] - ls[:_TIGHT]).abs().max()
