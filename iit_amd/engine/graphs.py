@@ -41,6 +41,12 @@ from typing import Dict, Optional, Tuple
 import torch
 
 
+# "thread_local": only this thread's unsafe HIP calls break a capture.  Under data parallelism the RCCL
+# process group's watchdog thread polls its work events (hipEventQuery) while a phase is being captured;
+# in the default "global" mode such a call from another thread can invalidate the capture.
+_CAPTURE_MODE = "thread_local"
+
+
 def _clone_out(out):
     if isinstance(out, tuple):
         loss, extras = out
@@ -68,7 +74,8 @@ class GraphedTrainStep:
             if ws > 1 and os.environ.get("IIT_GRAPHS_DP", "1") == "0":
                 enabled = False
         self.enabled = enabled
-        self.split = ws > 1  # DP: graphs around the (eager) gradient all-reduce
+        from ..parallel.dist import force_reducer
+        self.split = ws > 1 or force_reducer()  # DP: graphs around the (eager) gradient all-reduce
         self.staged = None
         self.force_staged = False  # tests: stage the backward graphs even without a data-parallel reducer
         if self.split and enabled:
@@ -188,16 +195,16 @@ class GraphedTrainStep:
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             gs = []
             try:
-                with torch.cuda.graph(ga, pool=self.pool):
+                with torch.cuda.graph(ga, pool=self.pool, capture_error_mode=_CAPTURE_MODE):
                     static_out = fwd_bwd()
                 for k in (stg.stages() if stg is not None else ()):
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=self.pool):
+                    with torch.cuda.graph(g, pool=self.pool, capture_error_mode=_CAPTURE_MODE):
                         stg.run_stage(k)
                     gs.append(g)
                 if stg is not None:
                     stg.release()
-                with torch.cuda.graph(gb, pool=self.pool):
+                with torch.cuda.graph(gb, pool=self.pool, capture_error_mode=_CAPTURE_MODE):
                     update()
             except Exception as e:
                 self.failed[full] = repr(e)
@@ -235,7 +242,7 @@ class GraphedTrainStep:
                 self.pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(g, pool=self.pool):
+                with torch.cuda.graph(g, pool=self.pool, capture_error_mode=_CAPTURE_MODE):
                     out = compute_loss()
                     loss = out[0] if isinstance(out, tuple) else out
                     step_fn(loss, optimizer)

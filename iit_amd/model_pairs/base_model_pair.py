@@ -272,7 +272,7 @@ class BaseModelPair(ABC):
 
     def _setup_reducer(self, optimizer):
         self._reducer = None
-        if pdist.world_size() > 1:
+        if pdist.world_size() > 1 or pdist.force_reducer():
             from ..engine.flat import FlatParams
             from ..parallel.ddp import GradReducer
             flat = getattr(optimizer, "flat", None)

@@ -200,7 +200,7 @@ def _time(fn, reps: int = 10) -> float:
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     try:
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for _ in range(reps):
                 fn()
         g.replay()

@@ -31,7 +31,7 @@ class GradReducer:
     def __init__(self, flat: FlatParams, bucket_mb: float = 64.0, overlap: bool = True):
         self.flat = flat
         self.world = pdist.world_size()
-        self.enabled = self.world > 1
+        self.enabled = self.world > 1 or pdist.force_reducer()
         self.overlap = overlap and self.enabled
         self._bucket_bytes = int(bucket_mb * (1 << 20))
         self.buckets = flat.buckets(self._bucket_bytes)

@@ -31,12 +31,19 @@ def is_main() -> bool:
     return rank() == 0
 
 
+def force_reducer() -> bool:
+    """``IIT_DP_FORCE_REDUCER=1`` under a one-rank process group: run the full data-parallel machinery (RCCL
+    all-reduces between staged graph replays) on a single GPU -- the rehearsal of the multi-GPU path that a
+    one-GPU box can run (``scripts/dp_rccl_rehearsal.sh``)."""
+    return os.environ.get("IIT_DP_FORCE_REDUCER") == "1" and is_initialized()
+
+
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> bool:
     """Initialise the default process group from torchrun env vars. Returns True if distributed."""
     if is_initialized():
         return True
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws <= 1:
+    if ws <= 1 and not (os.environ.get("IIT_DP_FORCE_REDUCER") == "1" and "RANK" in os.environ):
         return False
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
