@@ -64,33 +64,51 @@ __device__ __forceinline__ int kmaj_swz(int kr) {
   else return ((kr >> 1) & 1) | (((kr >> 3) & 1) << 1);              // R == 64: 4 blocks per 128-B k-row
 }
 
-// Stage one operand tile (R rows of the output dimension x 64 k) into its LDS image with LDS-DMA.
+// Stage one operand tile (R rows of the output dimension x 64 k) into its LDS image with LDS-DMA.  The per-lane
+// source pointers and LDS offsets are computed once per workgroup; staging K-tile kt then costs one 64-bit add per
+// DMA instruction (the k offset is uniform).
 template <bool KMAJ, int R>
-__device__ __forceinline__ void stage_operand(const __bf16* base, long ld, int r0g, int k0, char* img, int wave,
-                                              int lane) {
-  if constexpr (!KMAJ) {
-    // [R][64] bf16, 128-B rows; one instruction = 8 rows x 8 chunks of 16 B
+struct Stager {
+  static constexpr int N = R / 32;  // LDS-DMA instructions per wave per K-tile
+  const __bf16* ptr[N];
+  int off[N];
+  long kstep;  // elements between consecutive K-tiles
+
+  __device__ __forceinline__ void init(const __bf16* base, long ld, int r0g, int kbeg, int wave, int lane) {
+    if constexpr (!KMAJ) {
+      // [R][64] bf16, 128-B rows; one instruction = 8 rows x 8 chunks of 16 B
 #pragma unroll
-    for (int i = 0; i < R / 32; ++i) {
-      const int r0 = i * 32 + wave * 8;
-      const int row = r0 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
-      glds16(base + (long)(r0g + row) * ld + k0 + c * 8, img + r0 * 128);
-    }
-  } else {
-    // [64][R] bf16, R*2-B k-rows; one instruction = (64 / (R/8)) k-rows
-    constexpr int CH = R / 8;       // 16-B chunks per k-row
-    constexpr int KRI = 64 / CH;    // k-rows per instruction
+      for (int i = 0; i < N; ++i) {
+        const int r0 = i * 32 + wave * 8;
+        const int row = r0 + (lane >> 3);
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        ptr[i] = base + (long)(r0g + row) * ld + kbeg + c * 8;
+        off[i] = r0 * 128;
+      }
+      kstep = 64;
+    } else {
+      // [64][R] bf16, R*2-B k-rows; one instruction = (64 / (R/8)) k-rows
+      constexpr int CH = R / 8;     // 16-B chunks per k-row
+      constexpr int KRI = 64 / CH;  // k-rows per instruction
 #pragma unroll
-    for (int i = 0; i < 64 / (4 * KRI); ++i) {
-      const int kr0 = (i * 4 + wave) * KRI;
-      const int kr = kr0 + lane / CH;
-      const int ch = lane % CH;
-      const int col = (((ch >> 1) ^ kmaj_swz<R>(kr)) << 4) + ((ch & 1) << 3);
-      glds16(base + (long)(k0 + kr) * ld + r0g + col, img + kr0 * R * 2);
+      for (int i = 0; i < N; ++i) {
+        const int kr0 = (i * 4 + wave) * KRI;
+        const int kr = kr0 + lane / CH;
+        const int ch = lane % CH;
+        const int col = (((ch >> 1) ^ kmaj_swz<R>(kr)) << 4) + ((ch & 1) << 3);
+        ptr[i] = base + (long)(kbeg + kr) * ld + r0g + col;
+        off[i] = kr0 * R * 2;
+      }
+      kstep = 64 * ld;
     }
   }
-}
+
+  __device__ __forceinline__ void stage(int kt, char* img) const {
+    const long k = kt * kstep;
+#pragma unroll
+    for (int i = 0; i < N; ++i) glds16(ptr[i] + k, img + off[i]);
+  }
+};
 
 // MFMA 16x16x32 operand fragment: lane l gets X[row0 + (l & 15)][kbase + 8 * (l >> 4) + j], j = 0..7.
 // The k-major (transpose-read) form is issued as inline asm: hipcc (ROCm 7.2) treats the ds_read_tr builtin as
@@ -100,21 +118,37 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
+// Fragment reads are split into an *issue* (asm LDS reads into raw registers) and a *use* (combine into the
+// MFMA operand) so the main loop can keep the next sub-step's reads in flight under the current MFMAs.  hipcc
+// does not track asm-issued LDS reads, so the loop waits lgkmcnt(0) (+ sched_barrier) before any use.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+template <bool KMAJ> struct RawFrag;
+template <> struct RawFrag<false> { i32x4 v; };
+template <> struct RawFrag<true> { i16x4 lo, hi; };
+
 template <bool KMAJ, int R>
-__device__ __forceinline__ bf16x8 frag(const char* img, int row0, int kbase, int lane) {
+__device__ __forceinline__ void frag_issue(const char* img, int row0, int kbase, int lane, RawFrag<KMAJ>& f) {
   if constexpr (!KMAJ) {
     const int row = row0 + (lane & 15);
     const int c = (kbase >> 3) + (lane >> 4);
-    return *(const bf16x8*)(img + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+    const unsigned a = lds_addr(img + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+    asm volatile("ds_read_b128 %0, %1" : "=v"(f.v) : "v"(a));
   } else {
     const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
     const int kr = kbase + 8 * g + q;
     const int col = row0 + 4 * pp;
     const unsigned a0 = lds_addr(img + kr * (R * 2) + ((((col >> 4) ^ kmaj_swz<R>(kr))) << 5) + ((col & 15) << 1));
-    i16x4 v0, v1;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v0) : "v"(a0));
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v1) : "v"(a0), "i"(4 * R * 2));
-    const i16x8 w = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.lo) : "v"(a0));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f.hi) : "v"(a0), "i"(4 * R * 2));
+  }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 frag_use(const RawFrag<KMAJ>& f) {
+  if constexpr (!KMAJ) {
+    return __builtin_bit_cast(bf16x8, f.v);
+  } else {
+    const i16x8 w = __builtin_shufflevector(f.lo, f.hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(bf16x8, w);
   }
 }
@@ -123,6 +157,19 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid % 8;
   const int q = nwg / 8, r = nwg % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// Tile order inside an XCD's contiguous range: column-major groups of up to 8 M-tiles, so the (up to) 32 tiles an
+// XCD runs at once form a compact block that shares A row panels and B column panels in that XCD's L2 (a plain
+// row-major order gives e.g. the 768x3072 weight gradient 18 distinct B panels per XCD instead of 3).
+__device__ __forceinline__ void grouped_tile(int t, int tiles_m, int tiles_n, int& tm, int& tn) {
+  constexpr int GM = 8;
+  const int per_group = GM * tiles_n;
+  const int first_m = (t / per_group) * GM;
+  const int gsize = min(tiles_m - first_m, GM);
+  const int r = t % per_group;
+  tm = first_m + r % gsize;
+  tn = r / gsize;
 }
 
 __device__ __forceinline__ float gelu_new_dev(float x) {
@@ -175,7 +222,9 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles_n = p.N / BN;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  int tm, tn;
+  grouped_tile(t, p.M / BM, tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = blockIdx.y * p.k_per_split;
   const int nt = p.k_per_split / BK;
 
@@ -185,44 +234,86 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: NS-1 K-tiles in flight
+  // Software pipeline (one wave per SIMD, so the wave itself must hide the LDS latency):
+  //  * LDS-DMA ring of NS K-tiles: slot kt % NS holds K-tile kt; NS tiles are staged up front and tile kt + NS
+  //    is staged as soon as every wave has finished reading tile kt;
+  //  * register double buffer: the fragments of the next 32-deep sub-step (possibly in the next K-tile) are
+  //    issued before the 16 MFMAs of the current one, so their LDS latency hides under the matrix work;
+  //  * one raw s_barrier per K-tile, placed before the last sub-step's MFMAs: it publishes tile kt+1 (every
+  //    wave's counted vmcnt) and retires all reads of tile kt, so those MFMAs overlap the next DMA issue.
+  RawFrag<AKM> ca[TM], na[TM];
+  RawFrag<BKM> cb[TN], nb[TN];
+  Stager<AKM, BM> stA;
+  Stager<BKM, BN> stB;
+  stA.init(p.A, p.lda, m0, kbeg, wave, lane);
+  stB.init(p.B, p.ldb, n0, kbeg, wave, lane);
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
+  for (int s = 0; s < NS; ++s)
     if (s < nt) {
       char* buf = smem + s * STAGE;
-      stage_operand<AKM, BM>(p.A, p.lda, m0, kbeg + s * BK, buf, wave, lane);
-      stage_operand<BKM, BN>(p.B, p.ldb, n0, kbeg + s * BK, buf + A_BYTES, wave, lane);
+      stA.stage(s, buf);
+      stB.stage(s, buf + A_BYTES);
     }
+  wait_tiles<LOADS>(min(NS - 1, nt - 1));
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < TM; ++i) frag_issue<AKM, BM>(smem, wm * WM + i * 16, 0, lane, ca[i]);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) frag_issue<BKM, BN>(smem + A_BYTES, wn * WN + j * 16, 0, lane, cb[j]);
+
   for (int kt = 0; kt < nt; ++kt) {
-    // tile kt is complete once at most min(NS-2, nt-1-kt) later tiles are still in flight (counted, never 0 in
-    // steady state); the raw barrier then publishes every wave's DMA and retires all reads of tile kt-1, whose
-    // buffer is restaged right after it
-    wait_tiles<LOADS>(min(NS - 2, nt - 1 - kt));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + NS - 1 < nt) {
-      char* buf = smem + ((kt + NS - 1) % NS) * STAGE;
-      stage_operand<AKM, BM>(p.A, p.lda, m0, kbeg + (kt + NS - 1) * BK, buf, wave, lane);
-      stage_operand<BKM, BN>(p.B, p.ldb, n0, kbeg + (kt + NS - 1) * BK, buf + A_BYTES, wave, lane);
-    }
     const char* sa = smem + (kt % NS) * STAGE;
     const char* sb = sa + A_BYTES;
+    // ---- sub-step 0 of tile kt: operands in ca/cb; issue sub-step 1 into na/nb
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int s = 0; s < BK / 32; ++s) {
+    for (int i = 0; i < TM; ++i) frag_issue<AKM, BM>(sa, wm * WM + i * 16, 32, lane, na[i]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) frag_issue<BKM, BN>(sb, wn * WN + j * 16, 32, lane, nb[j]);
+    __builtin_amdgcn_sched_barrier(0);
+    {
       bf16x8 a[TM], b[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = frag<AKM, BM>(sa, wm * WM + i * 16, s * 32, lane);
+      for (int i = 0; i < TM; ++i) a[i] = frag_use<AKM>(ca[i]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = frag<BKM, BN>(sb, wn * WN + j * 16, s * 32, lane);
-      if constexpr (AKM || BKM) {  // asm transpose reads: retire them before the MFMAs read the registers
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      for (int j = 0; j < TN; ++j) b[j] = frag_use<BKM>(cb[j]);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- sub-step 1: operands in na/nb; publish tile kt+1, restage slot kt % NS, issue (kt+1, 0) into ca/cb
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 1 < nt) {
+      wait_tiles<LOADS>(min(NS - 2, nt - 2 - kt));
+      __builtin_amdgcn_s_barrier();
+      if (kt + NS < nt) {
+        char* buf = smem + (kt % NS) * STAGE;
+        stA.stage(kt + NS, buf);
+        stB.stage(kt + NS, buf + A_BYTES);
+      }
+      const char* ta = smem + ((kt + 1) % NS) * STAGE;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) frag_issue<AKM, BM>(ta, wm * WM + i * 16, 0, lane, ca[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) frag_issue<BKM, BN>(ta + A_BYTES, wn * WN + j * 16, 0, lane, cb[j]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      bf16x8 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = frag_use<AKM>(na[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = frag_use<BKM>(nb[j]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (EPI == E_F32_ACC) {
     if (gridDim.y > 1) {  // split-K partial: atomics straight from the MFMA layout (16 lanes = 16 consecutive

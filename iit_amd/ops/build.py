@@ -18,7 +18,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 CSRC = os.path.join(ROOT, "csrc")
 OUT_DIR = os.path.join(ROOT, "iit_amd", "_native")
 LIB = os.path.join(OUT_DIR, "libiit_hip.so")
-SOURCES = ["gemm.hip", "gemm_glds.hip", "kernels.hip", "attn_mfma.hip", "flash_attn.hip"]
+SOURCES = ["gemm.hip", "gemm_glds.hip", "kernels.hip", "attn_mfma.hip"]
+# per-source compiler flags: the pipelined LDS-DMA GEMM keeps its accumulators in VGPRs (MFMA VGPR form), which
+# avoids the AGPR shuffles hipcc otherwise emits around its register double buffer
+EXTRA_FLAGS = {"gemm_glds.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 ARCH = os.environ.get("IIT_OFFLOAD_ARCH", "gfx950")
 
 
@@ -39,6 +42,7 @@ def source_hash() -> str:
         with open(p, "rb") as f:
             h.update(f.read())
     h.update(ARCH.encode())
+    h.update(repr(sorted(EXTRA_FLAGS.items())).encode())
     return h.hexdigest()[:16]
 
 
@@ -56,7 +60,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for src in sources():
         obj = os.path.join(OUT_DIR, os.path.basename(src) + ".o")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
-               "-I", CSRC, "-c", src, "-o", obj]
+               "-I", CSRC, "-c", src, "-o", obj] + EXTRA_FLAGS.get(os.path.basename(src), [])
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
         objs.append(obj)
     for cmd, p in procs:
