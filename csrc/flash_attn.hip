@@ -1,0 +1,424 @@
+// Tiled (flash-style) attention for long sequences on gfx950 MFMA: forward + backward, causal or bidirectional,
+// grouped-query heads (Hkv divides Hq), head dims 64 and 128, and the interchange-splice head mask of the
+// short-sequence kernel (csrc/attn_mfma.hip): heads in ``head_mask`` take z := src and get zero q/k/v gradients.
+//
+// Never materialises [S, S]: 64x64 score tiles live in registers, the softmax is the online (running max / sum)
+// form, and the backward recomputes P from the saved log-sum-exp (SURVEY.md §2.3 K04, §7.3 kernel 3).
+//
+// All products are v_mfma_f32_16x16x32_bf16 tiles.  Layouts (lane l = 16 g + c):
+//   A fragment  X[m0 + c][k0 + 8g + j]        (16-B LDS row read, or straight from global memory)
+//   B fragment  Y[k0 + 8g + j][n0 + c]
+//   C           lane holds rows m0 + 4g + r (r = 0..3) of column n0 + c
+// A C tile over two consecutive 16-row blocks (rows 4g+r and 16+4g+r) becomes the B operand of the next product
+// with no lane movement when that product's reduction index is permuted the same way, kk(g, j) = 4g + j (j < 4),
+// 16 + 4g + (j - 4) (j >= 4); the partner A operand is read transposed from LDS with ds_read_b64_tr_b16 at exactly
+// those rows (frag_tr_perm).  That keeps P / dS in registers:
+//   forward   S^T = K Q^T (keys x queries), online softmax per query column, O^T += V^T P^T
+//   dK, dV    S = Q K^T, dP = dO V^T (queries x keys), dS = P (dP - D); dV^T += dO^T P, dK^T += Q^T dS
+//   dQ        S^T = K Q^T, dP^T = V dO^T, dS^T = P^T (dP^T - D); dQ^T += K^T dS^T
+// with D = rowsum(dO o O) from a small prep kernel.  dK/dV workgroups own 64 keys of one KV head and loop over every
+// query head of its group (GQA needs no atomics); dQ workgroups own 64 queries.
+#include "common.h"
+
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4_t;
+
+namespace {
+
+struct FaArgs {
+  const __bf16* q; const __bf16* k; const __bf16* v;
+  long qb, qs, qh, kb, ks, kh, vb, vs, vh;           // element strides (batch, position, head); unit stride on d
+  __bf16* z; long zb, zs, zh;                        // forward output
+  float* lse;                                        // [B][Hq][S] (scaled units)
+  const __bf16* src; long sb, ss, sh;                // splice source, z layout
+  unsigned long long head_mask;
+  const __bf16* dz; long db, ds, dh_;                // backward: dO
+  float* dd;                                         // D = rowsum(dO o O), [B][Hq][S]
+  __bf16* dq; __bf16* dk; __bf16* dv;
+  long gqb, gqs, gqh, gkb, gks, gkh, gvb, gvs, gvh;  // gradient strides
+  int B, S, Hq, Hkv, causal;
+  float scale;
+};
+
+constexpr int T64 = 64;
+
+// [64][DH] bf16 LDS image, 16-B chunks XOR-swizzled per row (conflict-free 16-B row reads)
+template <int DH>
+__device__ __forceinline__ int ioff(int row, int col) {
+  const int sw = DH == 64 ? ((row >> 1) & 7) : (row & 15);
+  return row * DH + ((((col >> 3) ^ sw) << 3) | (col & 7));
+}
+
+template <int DH>
+__device__ __forceinline__ void load_tile(__bf16* img, const __bf16* base, long stride, int r0, int S, int tid) {
+  constexpr int CPR = DH / 8;
+#pragma unroll
+  for (int i = tid; i < T64 * CPR; i += 256) {
+    const int r = i / CPR, ch = i % CPR;
+    uint4 val = make_uint4(0u, 0u, 0u, 0u);
+    if (r0 + r < S) val = *(const uint4*)(base + (long)(r0 + r) * stride + ch * 8);
+    *(uint4*)(img + ioff<DH>(r, ch * 8)) = val;
+  }
+}
+
+__device__ __forceinline__ bf16x8 zero8() {
+  const i16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+  return __builtin_bit_cast(bf16x8, z);
+}
+
+__device__ __forceinline__ bf16x8 gload8(const __bf16* p, bool ok) { return ok ? *(const bf16x8*)p : zero8(); }
+
+template <int DH>
+__device__ __forceinline__ bf16x8 frag_rows(const __bf16* img, int m0, int k0, int lane) {
+  return *(const bf16x8*)(img + ioff<DH>(m0 + (lane & 15), k0 + 8 * (lane >> 4)));
+}
+
+// lane receives X[kk(g, j)][n0 + c] of the [64][DH] image X, kk permuted as in the header (rows kb + ...)
+template <int DH>
+__device__ __forceinline__ bf16x8 frag_tr_perm(const __bf16* img, int kb, int n0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int col = n0 + 4 * pp;
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(img + ioff<DH>(kb + 4 * g + q, col)));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(img + ioff<DH>(kb + 16 + 4 * g + q, col)));
+  return __builtin_bit_cast(bf16x8, (i16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__device__ __forceinline__ bf16x8 pack_perm(const float* a, const float* b) {
+  bf16x8 o = {f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
+  return o;
+}
+
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void store4(__bf16* dst, const f32x4 v, float s) {
+  bf16x4 o = {f2bf(v[0] * s), f2bf(v[1] * s), f2bf(v[2] * s), f2bf(v[3] * s)};
+  *(bf16x4*)dst = o;
+}
+
+// ------------------------------------------------------------------------------------------------ forward
+template <int DH>
+__global__ __launch_bounds__(256) void fa_fwd_kernel(FaArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[T64 * DH];
+  __shared__ __attribute__((aligned(16))) __bf16 Vs[T64 * DH];
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, g = l >> 4, c = l & 15;
+  const int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int S = a.S;
+  const int q0 = qblk * T64 + 16 * wave, qi = q0 + c;
+  if ((a.head_mask >> h) & 1ull) {  // spliced head: z := src, lse unused by the backward (zero gradients)
+    constexpr int CPR = DH / 8;
+    for (int i = tid; i < T64 * CPR; i += 256) {
+      const int r = qblk * T64 + i / CPR, ch = i % CPR;
+      if (r < S)
+        *(uint4*)(a.z + b * a.zb + (long)r * a.zs + h * a.zh + ch * 8) =
+            *(const uint4*)(a.src + b * a.sb + (long)r * a.ss + h * a.sh + ch * 8);
+    }
+    return;
+  }
+  const int hk = h / (a.Hq / a.Hkv);
+  const __bf16* kbase = a.k + b * a.kb + hk * a.kh;
+  const __bf16* vbase = a.v + b * a.vb + hk * a.vh;
+  bf16x8 qf[DH / 32];
+#pragma unroll
+  for (int s = 0; s < DH / 32; ++s)
+    qf[s] = gload8(a.q + b * a.qb + (long)qi * a.qs + h * a.qh + 32 * s + 8 * g, qi < S);
+  f32x4 o[DH / 16];
+#pragma unroll
+  for (int t = 0; t < DH / 16; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;  // running max (scaled units) of column qi; this lane's partial sum
+  const int kend = a.causal ? min(S, (qblk + 1) * T64) : S;
+  for (int k0 = 0; k0 < kend; k0 += T64) {
+    __syncthreads();
+    load_tile<DH>(Ks, kbase, a.ks, k0, S, tid);
+    load_tile<DH>(Vs, vbase, a.vs, k0, S, tid);
+    __syncthreads();
+    float p[4][4];
+    float mb = -INFINITY;
+#pragma unroll
+    for (int kb4 = 0; kb4 < 4; ++kb4) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < DH / 32; ++s) acc = mfma(frag_rows<DH>(Ks, 16 * kb4, 32 * s, l), qf[s], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = k0 + 16 * kb4 + 4 * g + r;
+        const bool ok = kj < S && (!a.causal || kj <= qi);
+        p[kb4][r] = ok ? acc[r] * a.scale : -INFINITY;
+        mb = fmaxf(mb, p[kb4][r]);
+      }
+    }
+    mb = fmaxf(mb, __shfl_xor(mb, 16, 64));
+    mb = fmaxf(mb, __shfl_xor(mb, 32, 64));
+    const float mn = fmaxf(m, mb);
+    const float alpha = mn == -INFINITY ? 1.f : __expf(m - mn);
+    m = mn;
+    lsum *= alpha;
+#pragma unroll
+    for (int t = 0; t < DH / 16; ++t) o[t] *= alpha;
+#pragma unroll
+    for (int kb4 = 0; kb4 < 4; ++kb4)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = p[kb4][r] == -INFINITY ? 0.f : __expf(p[kb4][r] - mn);
+        p[kb4][r] = e;
+        lsum += e;
+      }
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      const bf16x8 pb = pack_perm(p[2 * ch], p[2 * ch + 1]);
+#pragma unroll
+      for (int t = 0; t < DH / 16; ++t) o[t] = mfma(frag_tr_perm<DH>(Vs, 32 * ch, 16 * t, l), pb, o[t]);
+    }
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (qi < S) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    __bf16* zr = a.z + b * a.zb + (long)qi * a.zs + h * a.zh;
+#pragma unroll
+    for (int t = 0; t < DH / 16; ++t) store4(zr + 16 * t + 4 * g, o[t], inv);
+    if (g == 0 && a.lse) a.lse[((long)b * a.Hq + h) * S + qi] = m + __logf(lsum);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ backward
+// D[b][h][i] = sum_d dO[i][d] * O[i][d]  (one thread per row)
+template <int DH>
+__global__ __launch_bounds__(256) void fa_bwd_prep_kernel(FaArgs a) {
+  const long row = (long)blockIdx.x * 256 + threadIdx.x;
+  const long rows = (long)a.B * a.Hq * a.S;
+  if (row >= rows) return;
+  const int i = row % a.S;
+  const int h = (row / a.S) % a.Hq;
+  const int b = row / ((long)a.S * a.Hq);
+  const __bf16* o = a.z + b * a.zb + (long)i * a.zs + h * a.zh;
+  const __bf16* g = a.dz + b * a.db + (long)i * a.ds + h * a.dh_;
+  float acc = 0.f;
+#pragma unroll
+  for (int ch = 0; ch < DH / 8; ++ch) {
+    const bf16x8 x = *(const bf16x8*)(o + ch * 8), y = *(const bf16x8*)(g + ch * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc += bf2f(x[e]) * bf2f(y[e]);
+  }
+  a.dd[row] = acc;
+}
+
+template <int DH>
+__global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(FaArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 Qs[T64 * DH];
+  __shared__ __attribute__((aligned(16))) __bf16 Gs[T64 * DH];
+  __shared__ float Ls[T64], Ds[T64];
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, g = l >> 4, c = l & 15;
+  const int kblk = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int S = a.S, rep = a.Hq / a.Hkv;
+  const int kj = kblk * T64 + 16 * wave + c;  // this lane's key (B-operand / C column)
+  bf16x8 kf[DH / 32], vf[DH / 32];
+#pragma unroll
+  for (int s = 0; s < DH / 32; ++s) {
+    kf[s] = gload8(a.k + b * a.kb + (long)kj * a.ks + hk * a.kh + 32 * s + 8 * g, kj < S);
+    vf[s] = gload8(a.v + b * a.vb + (long)kj * a.vs + hk * a.vh + 32 * s + 8 * g, kj < S);
+  }
+  f32x4 dk[DH / 16], dv[DH / 16];
+#pragma unroll
+  for (int t = 0; t < DH / 16; ++t) dk[t] = dv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int qbeg = a.causal ? kblk * T64 : 0;
+  for (int hh = 0; hh < rep; ++hh) {
+    const int h = hk * rep + hh;
+    if ((a.head_mask >> h) & 1ull) continue;  // spliced head: constant z, no gradient
+    const __bf16* qbase = a.q + b * a.qb + h * a.qh;
+    const __bf16* gbase = a.dz + b * a.db + h * a.dh_;
+    const float* lse = a.lse + ((long)b * a.Hq + h) * S;
+    const float* D = a.dd + ((long)b * a.Hq + h) * S;
+    for (int i0 = qbeg; i0 < S; i0 += T64) {
+      __syncthreads();
+      load_tile<DH>(Qs, qbase, a.qs, i0, S, tid);
+      load_tile<DH>(Gs, gbase, a.ds, i0, S, tid);
+      if (tid < T64) {
+        Ls[tid] = i0 + tid < S ? lse[i0 + tid] : 0.f;
+        Ds[tid] = i0 + tid < S ? D[i0 + tid] : 0.f;
+      }
+      __syncthreads();
+      float P[4][4], dS[4][4];
+#pragma unroll
+      for (int qm = 0; qm < 4; ++qm) {
+        f32x4 sa = {0.f, 0.f, 0.f, 0.f}, pa = sa;
+#pragma unroll
+        for (int s = 0; s < DH / 32; ++s) {
+          sa = mfma(frag_rows<DH>(Qs, 16 * qm, 32 * s, l), kf[s], sa);  // S[q][key]
+          pa = mfma(frag_rows<DH>(Gs, 16 * qm, 32 * s, l), vf[s], pa);  // dP[q][key]
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int il = 16 * qm + 4 * g + r, i = i0 + il;
+          const bool ok = i < S && kj < S && (!a.causal || kj <= i);
+          const float pv = ok ? __expf(sa[r] * a.scale - Ls[il]) : 0.f;
+          P[qm][r] = pv;
+          dS[qm][r] = pv * (pa[r] - Ds[il]);
+        }
+      }
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) {
+        const bf16x8 pb = pack_perm(P[2 * ch], P[2 * ch + 1]);
+        const bf16x8 sb = pack_perm(dS[2 * ch], dS[2 * ch + 1]);
+#pragma unroll
+        for (int t = 0; t < DH / 16; ++t) {
+          dv[t] = mfma(frag_tr_perm<DH>(Gs, 32 * ch, 16 * t, l), pb, dv[t]);  // dV^T[d][key] += dO^T P
+          dk[t] = mfma(frag_tr_perm<DH>(Qs, 32 * ch, 16 * t, l), sb, dk[t]);  // dK^T[d][key] += Q^T dS
+        }
+      }
+    }
+  }
+  if (kj < S) {
+    __bf16* dkr = a.dk + b * a.gkb + (long)kj * a.gks + hk * a.gkh;
+    __bf16* dvr = a.dv + b * a.gvb + (long)kj * a.gvs + hk * a.gvh;
+#pragma unroll
+    for (int t = 0; t < DH / 16; ++t) {
+      store4(dkr + 16 * t + 4 * g, dk[t], a.scale);
+      store4(dvr + 16 * t + 4 * g, dv[t], 1.f);
+    }
+  }
+}
+
+template <int DH>
+__global__ __launch_bounds__(256) void fa_bwd_dq_kernel(FaArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[T64 * DH];
+  __shared__ __attribute__((aligned(16))) __bf16 Vs[T64 * DH];
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, g = l >> 4, c = l & 15;
+  const int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int S = a.S;
+  const int qi = qblk * T64 + 16 * wave + c;
+  __bf16* dqr = a.dq + b * a.gqb + (long)qi * a.gqs + h * a.gqh;
+  if ((a.head_mask >> h) & 1ull) {
+    if (qi < S) {
+#pragma unroll
+      for (int t = 0; t < DH / 16; ++t) store4(dqr + 16 * t + 4 * g, f32x4{0.f, 0.f, 0.f, 0.f}, 1.f);
+    }
+    return;
+  }
+  const int hk = h / (a.Hq / a.Hkv);
+  const __bf16* kbase = a.k + b * a.kb + hk * a.kh;
+  const __bf16* vbase = a.v + b * a.vb + hk * a.vh;
+  bf16x8 qf[DH / 32], gf[DH / 32];
+#pragma unroll
+  for (int s = 0; s < DH / 32; ++s) {
+    qf[s] = gload8(a.q + b * a.qb + (long)qi * a.qs + h * a.qh + 32 * s + 8 * g, qi < S);
+    gf[s] = gload8(a.dz + b * a.db + (long)qi * a.ds + h * a.dh_ + 32 * s + 8 * g, qi < S);
+  }
+  const long hrow = ((long)b * a.Hq + h) * S;
+  const float lse_q = qi < S ? a.lse[hrow + qi] : 0.f;
+  const float D_q = qi < S ? a.dd[hrow + qi] : 0.f;
+  f32x4 dq[DH / 16];
+#pragma unroll
+  for (int t = 0; t < DH / 16; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kend = a.causal ? min(S, (qblk + 1) * T64) : S;
+  for (int k0 = 0; k0 < kend; k0 += T64) {
+    __syncthreads();
+    load_tile<DH>(Ks, kbase, a.ks, k0, S, tid);
+    load_tile<DH>(Vs, vbase, a.vs, k0, S, tid);
+    __syncthreads();
+    float dS[4][4];
+#pragma unroll
+    for (int kb4 = 0; kb4 < 4; ++kb4) {
+      f32x4 sa = {0.f, 0.f, 0.f, 0.f}, pa = sa;
+#pragma unroll
+      for (int s = 0; s < DH / 32; ++s) {
+        sa = mfma(frag_rows<DH>(Ks, 16 * kb4, 32 * s, l), qf[s], sa);  // S^T[key][q]
+        pa = mfma(frag_rows<DH>(Vs, 16 * kb4, 32 * s, l), gf[s], pa);  // dP^T[key][q]
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = k0 + 16 * kb4 + 4 * g + r;
+        const bool ok = qi < S && kj < S && (!a.causal || kj <= qi);
+        const float pv = ok ? __expf(sa[r] * a.scale - lse_q) : 0.f;
+        dS[kb4][r] = pv * (pa[r] - D_q);
+      }
+    }
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      const bf16x8 sb = pack_perm(dS[2 * ch], dS[2 * ch + 1]);
+#pragma unroll
+      for (int t = 0; t < DH / 16; ++t) dq[t] = mfma(frag_tr_perm<DH>(Ks, 32 * ch, 16 * t, l), sb, dq[t]);
+    }
+  }
+  if (qi < S) {
+#pragma unroll
+    for (int t = 0; t < DH / 16; ++t) store4(dqr + 16 * t + 4 * g, dq[t], a.scale);
+  }
+}
+
+bool args_ok(const FaArgs& a, int dh) {
+  if (!(dh == 64 || dh == 128) || a.S <= 0 || a.B <= 0 || a.Hq <= 0 || a.Hkv <= 0 || a.Hq % a.Hkv) return false;
+  if (a.head_mask && a.Hq > 64) return false;
+  const long strides[] = {a.qs, a.qh, a.qb, a.ks, a.kh, a.kb, a.vs, a.vh, a.vb};
+  for (long s : strides)
+    if (s % 8) return false;
+  const uintptr_t al = (uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v;
+  return (al & 15) == 0;
+}
+
+}  // namespace
+
+// q [B,S,Hq,dh], k/v [B,S,Hkv,dh] (bf16, any batch/position/head strides that keep 16-B rows), z [B,S,Hq,dh] bf16,
+// lse [B,Hq,S] fp32.  ``scale`` multiplies the scores (1/sqrt(dh) for standard attention).
+IIT_EXPORT int iit_flash_fwd(const void* q, const void* k, const void* v, const long* strides9, void* z,
+                             const long* zstrides3, float* lse, const void* src, const long* sstrides3,
+                             unsigned long long head_mask, int B, int S, int Hq, int Hkv, int dh, float scale,
+                             int causal, void* stream) {
+  FaArgs a = {};
+  a.q = (const __bf16*)q; a.k = (const __bf16*)k; a.v = (const __bf16*)v;
+  a.qb = strides9[0]; a.qs = strides9[1]; a.qh = strides9[2];
+  a.kb = strides9[3]; a.ks = strides9[4]; a.kh = strides9[5];
+  a.vb = strides9[6]; a.vs = strides9[7]; a.vh = strides9[8];
+  a.z = (__bf16*)z; a.zb = zstrides3[0]; a.zs = zstrides3[1]; a.zh = zstrides3[2];
+  a.lse = lse;
+  a.src = (const __bf16*)src;
+  if (src) { a.sb = sstrides3[0]; a.ss = sstrides3[1]; a.sh = sstrides3[2]; }
+  a.head_mask = src ? head_mask : 0ull;
+  a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.scale = scale;
+  if (!args_ok(a, dh) || a.zs % 8 || a.zh % 8 || ((uintptr_t)z & 15)) return (int)hipErrorInvalidValue;
+  dim3 grid((S + T64 - 1) / T64, Hq, B);
+  hipStream_t s = (hipStream_t)stream;
+  if (dh == 64) hipLaunchKernelGGL(fa_fwd_kernel<64>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(fa_fwd_kernel<128>, grid, dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+// dz/z [B,S,Hq,dh] (z = the forward output), dd [B,Hq,S] fp32 scratch; dq/dk/dv with their own strides.
+IIT_EXPORT int iit_flash_bwd(const void* q, const void* k, const void* v, const long* strides9, const void* z,
+                             const long* zstrides3, const void* dz, const long* dzstrides3, const float* lse,
+                             float* dd, void* dq, void* dk, void* dv, const long* gstrides9,
+                             unsigned long long head_mask, int B, int S, int Hq, int Hkv, int dh, float scale,
+                             int causal, void* stream) {
+  FaArgs a = {};
+  a.q = (const __bf16*)q; a.k = (const __bf16*)k; a.v = (const __bf16*)v;
+  a.qb = strides9[0]; a.qs = strides9[1]; a.qh = strides9[2];
+  a.kb = strides9[3]; a.ks = strides9[4]; a.kh = strides9[5];
+  a.vb = strides9[6]; a.vs = strides9[7]; a.vh = strides9[8];
+  a.z = (__bf16*)z; a.zb = zstrides3[0]; a.zs = zstrides3[1]; a.zh = zstrides3[2];
+  a.dz = (const __bf16*)dz; a.db = dzstrides3[0]; a.ds = dzstrides3[1]; a.dh_ = dzstrides3[2];
+  a.lse = (float*)lse; a.dd = dd;
+  a.dq = (__bf16*)dq; a.dk = (__bf16*)dk; a.dv = (__bf16*)dv;
+  a.gqb = gstrides9[0]; a.gqs = gstrides9[1]; a.gqh = gstrides9[2];
+  a.gkb = gstrides9[3]; a.gks = gstrides9[4]; a.gkh = gstrides9[5];
+  a.gvb = gstrides9[6]; a.gvs = gstrides9[7]; a.gvh = gstrides9[8];
+  a.head_mask = head_mask;
+  a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.scale = scale;
+  if (!args_ok(a, dh) || a.ds % 8 || a.dh_ % 8 || a.zs % 8 || a.zh % 8 || ((uintptr_t)dz & 15) || ((uintptr_t)z & 15))
+    return (int)hipErrorInvalidValue;
+  for (int i = 0; i < 9; ++i)
+    if (gstrides9[i] % 4) return (int)hipErrorInvalidValue;  // 8-byte stores
+  hipStream_t s = (hipStream_t)stream;
+  const long rows = (long)B * Hq * S;
+  dim3 gp((rows + 255) / 256);
+  dim3 gkv((S + T64 - 1) / T64, Hkv, B), gq((S + T64 - 1) / T64, Hq, B);
+  if (dh == 64) {
+    hipLaunchKernelGGL(fa_bwd_prep_kernel<64>, gp, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<64>, gkv, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<64>, gq, dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(fa_bwd_prep_kernel<128>, gp, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<128>, gkv, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<128>, gq, dim3(256), 0, s, a);
+  }
+  return (int)hipGetLastError();
+}

@@ -37,6 +37,15 @@ from ..ops.torch_ops import TorchOps
 from .config import HookedTransformerConfig, make_config
 
 
+def _hip_ops():
+    from ..ops import hip_ops
+    return hip_ops
+
+
+def _flash_ok(q: torch.Tensor) -> bool:
+    return q.is_cuda and q.dtype == torch.bfloat16 and _hip_ops().flash_supported(q)
+
+
 class _StopForward(Exception):
     pass
 
@@ -245,11 +254,15 @@ class Attention(nn.Module):
                                                           self.cfg.rotary_adjacent_pairs))
             k = run.site(self.hook_rot_k, TorchOps.rotary(ops, k, self.rotary_cos, self.rotary_sin, self.rotary_dim,
                                                           self.cfg.rotary_adjacent_pairs))
+        causal = self.cfg.attention_dir == "causal"
+        if not ops.fused and q.shape[1] > 16 and _flash_ok(q) and \
+                not (run.live(self.hook_attn_scores) or run.live(self.hook_pattern)):
+            # torch op backend on the GPU (Llama family): tiled MFMA attention, GQA-native (no k/v expansion)
+            return _hip_ops().flash_attention(q, k, v, causal, self.attn_scale), False
         if self.gqa:
             rep = self.cfg.n_heads // self.n_kv
             k = k.repeat_interleave(rep, dim=2)
             v = v.repeat_interleave(rep, dim=2)
-        causal = self.cfg.attention_dir == "causal"
         z_spl = run.plan.splice.get(self.hook_z.name) if run.plan is not None else None
         if ops.fused and not (run.live(self.hook_attn_scores) or run.live(self.hook_pattern)):
             heads = z_spl[0].head_mask(self.cfg.n_heads) if (z_spl and len(z_spl) == 1) else None

@@ -51,6 +51,9 @@ _SIGS = {
     "iit_dgelu": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p],
     "iit_add_bf16": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_int, c_void_p],
     "iit_device_sync": [],
+    "iit_flash_fwd": [c_void_p] * 3 + [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ull] + [c_int] * 5
+                     + [c_float, c_int, c_void_p],
+    "iit_flash_bwd": [c_void_p] * 3 + [c_void_p] * 11 + [c_ull] + [c_int] * 5 + [c_float, c_int, c_void_p],
 }
 
 
@@ -189,6 +192,41 @@ def attn_small_bwd(qkv, dz, lse, dqkv, head_mask, B, S, H, dh, ld_qkv, ld_dz, sc
         return
     _check(lib().iit_attn_small_bwd(_p(qkv), _p(dz), _p(lse), _p(dqkv), head_mask, B, S, H, dh, ld_qkv, ld_dz, scale,
                                     int(causal), _stream()), "attn_small_bwd")
+
+
+def _bsh(t: torch.Tensor):
+    """(batch, position, head) element strides of a [B, S, H, dh] view with unit stride on dh."""
+    assert t.stride(-1) == 1 and t.dtype == torch.bfloat16, "flash attention takes bf16 [B,S,H,dh] with unit d stride"
+    return [t.stride(0), t.stride(1), t.stride(2)]
+
+
+def _longs(vals):
+    return (c_long * len(vals))(*vals)
+
+
+def flash_fwd(q, k, v, z, lse, src, head_mask: int, scale: float, causal: bool):
+    """Tiled attention forward (csrc/flash_attn.hip): q/z [B,S,Hq,dh], k/v [B,S,Hkv,dh], lse [B,Hq,S] fp32."""
+    B, S, Hq, dh = q.shape
+    Hkv = k.shape[2]
+    st = _longs(_bsh(q) + _bsh(k) + _bsh(v))
+    zs = _longs(_bsh(z))
+    ss = _longs(_bsh(src)) if src is not None else None
+    _check(lib().iit_flash_fwd(_p(q), _p(k), _p(v), ctypes.cast(st, c_void_p), _p(z), ctypes.cast(zs, c_void_p),
+                               _p(lse), _p(src), None if ss is None else ctypes.cast(ss, c_void_p),
+                               head_mask if src is not None else 0, B, S, Hq, Hkv, dh, scale, int(causal), _stream()),
+           "flash_fwd")
+
+
+def flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, head_mask: int, scale: float, causal: bool):
+    B, S, Hq, dh = q.shape
+    Hkv = k.shape[2]
+    st = _longs(_bsh(q) + _bsh(k) + _bsh(v))
+    gs = _longs(_bsh(dq) + _bsh(dk) + _bsh(dv))
+    zs, ds = _longs(_bsh(z)), _longs(_bsh(dz))
+    _check(lib().iit_flash_bwd(_p(q), _p(k), _p(v), ctypes.cast(st, c_void_p), _p(z), ctypes.cast(zs, c_void_p),
+                               _p(dz), ctypes.cast(ds, c_void_p), _p(lse), _p(dd), _p(dq), _p(dk), _p(dv),
+                               ctypes.cast(gs, c_void_p), head_mask, B, S, Hq, Hkv, dh, scale, int(causal), _stream()),
+           "flash_bwd")
 
 
 def ce_fwd(logits, ld, labels, loss, lse, amax, R, V):

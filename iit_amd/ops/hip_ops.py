@@ -24,6 +24,7 @@ clone + index-put hook.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -462,6 +463,85 @@ class AttnFn(Function):
         return dqkv, None, None, None, None
 
 
+def _flash_grads(ctx, dz, q, k, v, dq, dk, dv):
+    z, lse = ctx.saved_tensors[-2:]
+    mask, causal, scale = ctx.cfg
+    B, S, Hq, _ = q.shape
+    dz = dz.to(BF16)
+    if dz.stride(-1) != 1 or dz.stride(1) % 8 or dz.stride(2) % 8:
+        dz = dz.contiguous()
+    dd = torch.empty(B, Hq, S, dtype=F32, device=q.device)
+    K.flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, mask, scale, causal)
+
+
+class FlashPackedFn(Function):
+    """Tiled MFMA attention (csrc/flash_attn.hip) over a packed qkv [B,S,3,H,dh] bf16 -> z [B,S,H,dh] bf16.
+    Heads in ``mask`` take ``zsrc`` (interchange splice) and get zero q/k/v gradients."""
+
+    @staticmethod
+    def forward(ctx, qkv, zsrc, mask, causal, scale):
+        ctx.set_materialize_grads(False)
+        B, S, _, H, dh = qkv.shape
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        z = torch.empty(B, S, H, dh, dtype=BF16, device=qkv.device)
+        lse = torch.empty(B, H, S, dtype=F32, device=qkv.device)
+        src = zsrc.to(BF16).contiguous() if mask else None
+        K.flash_fwd(q, k, v, z, lse, src, mask, scale, causal)
+        ctx.save_for_backward(qkv, z, lse)
+        ctx.cfg = (mask, causal, scale)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        if dz is None:
+            return None, None, None, None, None
+        qkv = ctx.saved_tensors[0]
+        dqkv = torch.empty_like(qkv)
+        _flash_grads(ctx, dz, qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2])
+        return dqkv, None, None, None, None
+
+
+class FlashFn(Function):
+    """Tiled MFMA attention over separate q [B,S,Hq,dh] and grouped k/v [B,S,Hkv,dh] (bf16, GQA-native)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        ctx.set_materialize_grads(False)
+        B, S, Hq, dh = q.shape
+        z = torch.empty(B, S, Hq, dh, dtype=BF16, device=q.device)
+        lse = torch.empty(B, Hq, S, dtype=F32, device=q.device)
+        K.flash_fwd(q, k, v, z, lse, None, 0, scale, causal)
+        ctx.save_for_backward(q, k, v, z, lse)
+        ctx.cfg = (0, causal, scale)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        if dz is None:
+            return None, None, None, None, None
+        q, k, v = ctx.saved_tensors[:3]
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        _flash_grads(ctx, dz, q, k, v, dq, dk, dv)
+        return dq, dk, dv, None, None
+
+
+def _flash_view(t: torch.Tensor) -> torch.Tensor:
+    t = t.to(BF16)
+    if t.stride(-1) != 1 or t.stride(1) % 8 or t.stride(2) % 8 or t.stride(0) % 8 or t.data_ptr() % 16:
+        t = t.contiguous()
+    return t
+
+
+def flash_supported(q: torch.Tensor) -> bool:
+    """The tiled kernel covers bf16-able [B,S,H,dh] inputs on the GPU with dh 64 / 128."""
+    return q.is_cuda and q.shape[-1] in (64, 128) and os.environ.get("IIT_FLASH", "1") != "0"
+
+
+def flash_attention(q, k, v, causal: bool, attn_scale: float) -> torch.Tensor:
+    """softmax(q k^T / attn_scale) v for q [B,S,Hq,dh], k/v [B,S,Hkv,dh] (Hkv | Hq), never materialising [S,S]."""
+    return FlashFn.apply(_flash_view(q), _flash_view(k), _flash_view(v), causal, 1.0 / attn_scale)
+
+
 class LinearFn(Function):
     """y = x @ W + b, TL-layout master W [K, N] with bf16 shadow ``w`` (row stride ``ldw``).
 
@@ -685,6 +765,16 @@ class HipOps(TorchOps):
     def attention(self, q, k, v, causal, attn_scale, patch_heads: Optional[Sequence[int]] = None, patch_src=None,
                   hook_scores=None, hook_pattern=None, ignore=float("-inf")):
         S, dh = q.shape[1], q.shape[-1]
+        if S > 16 and flash_supported(q):
+            packed = getattr(q, "_iit_packed", None)
+            if packed is not None and getattr(k, "_iit_packed", None) is packed and \
+                    getattr(v, "_iit_packed", None) is packed and packed.is_contiguous():
+                return FlashPackedFn.apply(packed, patch_src, K.heads_to_mask(patch_heads), causal, 1.0 / attn_scale)
+            z = flash_attention(q, k, v, causal, attn_scale)
+            if patch_heads:
+                z = z.clone()
+                z[:, :, list(patch_heads)] = patch_src[:, :, list(patch_heads)].to(z.dtype)
+            return z
         if S > 64 or dh > 128:
             z = TorchOps.attention(self, q, k, v, causal, attn_scale)
             if patch_heads:
