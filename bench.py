@@ -84,9 +84,12 @@ def setup(args, dev):
     loader = train_set.make_loader(args.batch, 0)
 
     def batches():
+        # full batches only: an epoch's short last batch would run eagerly (new shapes) inside the timed window
+        # and carry fewer pairs than the rate counts
         while True:
             for b in loader:
-                yield b
+                if b[0][0].shape[0] == args.batch:
+                    yield b
 
     it = batches()
     step_fn = pair.run_train_step

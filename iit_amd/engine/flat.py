@@ -87,6 +87,7 @@ class FlatParams:
                 p.grad = fn(self.grad)
                 p._iit_flat = self  # back-reference: bf16 mirror lookup by the torch op backend
         self.index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
+        self._grad_views = None  # (grad arena, cached per-parameter grad views) for rebind_grads
         self.version = 0
         self.mirror_version = -1
         self._inactive: Dict[int, Tuple[int, int, torch.Tensor]] = {}  # param index -> (offset, row_len, live rows)
@@ -194,15 +195,19 @@ class FlatParams:
         A replaced gradient is copied into its slot; with ``zero_missing`` a ``None``
         gradient (``optimizer.zero_grad(set_to_none=True)``) gets its slot zeroed, so
         the arena equals the gradients autograd is about to accumulate."""
-        for p, fn in zip(self.params, self._view_fns):
+        views = self._grad_views
+        if views is None or views[0] is not self.grad:
+            views = self._grad_views = (self.grad, [fn(self.grad) for fn in self._view_fns])
+        for p, view in zip(self.params, views[1]):
             g = p.grad
-            view = fn(self.grad)
+            if g is view:  # the common case (host cost matters: the DP schedule calls this twice per phase)
+                continue
             if g is None or g.data_ptr() != view.data_ptr() or g.stride() != view.stride():
                 if g is not None:
                     view.copy_(g)
                 elif zero_missing:
                     view.zero_()
-                p.grad = view
+            p.grad = view
 
     def grad_view(self, p: torch.Tensor) -> torch.Tensor:
         return self._view_fns[self.index[id(p)]](self.grad)
