@@ -88,6 +88,8 @@ class FlatParams:
                 p._iit_flat = self  # back-reference: bf16 mirror lookup by the torch op backend
         self.index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
         self._grad_views = None  # (grad arena, cached per-parameter grad views) for rebind_grads
+        self._claimed = set()    # parameter indices whose gradient a store-producer wrote (see ``claim``)
+        self._zero_plan = None
         self.version = 0
         self.mirror_version = -1
         self._inactive: Dict[int, Tuple[int, int, torch.Tensor]] = {}  # param index -> (offset, row_len, live rows)
@@ -186,27 +188,97 @@ class FlatParams:
 
     # ---------------------------------------------------------------- grads
     def zero_grad(self) -> None:
-        self.grad.zero_()
+        """Zero every gradient -- lazily for *store-claimed* parameters.
+
+        A parameter whose gradient the previous backward produced with a single overwriting GEMM (``claim``) gets
+        ``.grad = None`` instead of a memset: its producer stores into the slot (beta = 0, no read of the old
+        gradient) and whatever is still ``None`` when the gradients are consumed is zeroed then
+        (``rebind_grads(zero_missing=True)``: the optimizer step / the DP reducer).  Everything else -- biases,
+        norms, embeddings, autograd-accumulated parameters -- is memset here as before.  For the GPT-2 / Llama
+        matrices this removes one write pass (zero) and one read pass (accumulate) over the gradient arena per
+        optimizer step."""
+        if not self._claimed:
+            self.grad.zero_()
+            self.rebind_grads()
+            return
+        key = frozenset(self._claimed)
+        if self._zero_plan is None or self._zero_plan[0] != key:
+            lazy = set()
+            for o, n in self.slots:  # a slot is lazy only when every parameter in it is claimed
+                members = [i for i, p in enumerate(self.params) if o <= self.offset_of(p) < o + max(n, 1)]
+                if members and all(i in key for i in members):
+                    lazy.add(o)
+            ranges = []
+            for o, n in self.slots:  # memset runs over the non-lazy slots (arena order)
+                if o in lazy:
+                    continue
+                end = o + _align(n)
+                if ranges and ranges[-1][1] == o:
+                    ranges[-1] = (ranges[-1][0], end)
+                else:
+                    ranges.append((o, end))
+            none_ids = [i for i, p in enumerate(self.params)
+                        if any(o <= self.offset_of(p) < o + max(n, 1) and o in lazy for o, n in self.slots)]
+            self._zero_plan = (key, ranges, none_ids)
+        _, ranges, none_ids = self._zero_plan
+        for a, b in ranges:
+            self.grad[a:b].zero_()
         self.rebind_grads()
+        for i in none_ids:
+            self.params[i].grad = None
+
+    def claim(self, *ps: torch.Tensor) -> bool:
+        """Called by a producer that writes the *complete* gradient of ``ps`` (one slot, e.g. the packed
+        ``W_Q|W_K|W_V`` group) with a single GEMM: True -> store (the slot holds garbage, overwrite it); False
+        -> accumulate (the gradients are live).  Binds ``.grad`` to the arena views either way."""
+        idx = [self.index.get(id(p)) for p in ps]
+        if any(i is None for i in idx):
+            return False
+        self._claimed.update(idx)  # a store-capable producer: lazily zero these from the next zero_grad on
+        fresh = all(p.grad is None for p in ps)
+        if not fresh:
+            for p in ps:
+                if p.grad is None:
+                    self.bind_zero(p)
+            return False
+        views = self._views()
+        for i, p in zip(idx, ps):
+            p.grad = views[i]
+        return True
+
+    def bind_zero(self, p: torch.Tensor) -> torch.Tensor:
+        """``p.grad`` := its (zeroed) arena view, for producers that accumulate into a ``None`` gradient."""
+        i = self.index[id(p)]
+        v = self._views()[i]
+        if p.grad is None:
+            v.zero_()
+        elif p.grad is not v:
+            v.copy_(p.grad)
+        p.grad = v
+        return v
+
+    def _views(self):
+        views = self._grad_views
+        if views is None or views[0] is not self.grad:
+            views = self._grad_views = (self.grad, [fn(self.grad) for fn in self._view_fns])
+        return views[1]
 
     def rebind_grads(self, zero_missing: bool = False) -> None:
         """Re-attach ``.grad`` views (after someone set them to None / replaced them).
 
-        A replaced gradient is copied into its slot; with ``zero_missing`` a ``None``
-        gradient (``optimizer.zero_grad(set_to_none=True)``) gets its slot zeroed, so
-        the arena equals the gradients autograd is about to accumulate."""
-        views = self._grad_views
-        if views is None or views[0] is not self.grad:
-            views = self._grad_views = (self.grad, [fn(self.grad) for fn in self._view_fns])
-        for p, view in zip(self.params, views[1]):
+        A replaced gradient is copied into its slot and a ``None`` gradient
+        (``optimizer.zero_grad(set_to_none=True)``, or a lazily zeroed slot no producer
+        claimed) gets its slot zeroed, so the arena equals the gradients.  (``zero_missing``
+        is kept for callers; ``None`` slots are always zeroed.)"""
+        for p, view in zip(self.params, self._views()):
             g = p.grad
             if g is view:  # the common case (host cost matters: the DP schedule calls this twice per phase)
                 continue
-            if g is None or g.data_ptr() != view.data_ptr() or g.stride() != view.stride():
-                if g is not None:
-                    view.copy_(g)
-                elif zero_missing:
-                    view.zero_()
+            if g is None:
+                # a None gradient is zero (set_to_none / lazy zero_grad): the arena slot may hold stale values
+                view.zero_()
+            elif g.data_ptr() != view.data_ptr() or g.stride() != view.stride():
+                view.copy_(g)
             p.grad = view
 
     def grad_view(self, p: torch.Tensor) -> torch.Tensor:

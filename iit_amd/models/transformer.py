@@ -389,25 +389,33 @@ class TransformerBlock(nn.Module):
 
 
 def qkv_arena_groups(blocks, cfg):
-    """Arena groups packing each block's ``W_Q|W_K|W_V`` into one ``[d_model][3*H*d_head]`` matrix (column
-    ``which*H*dh + h*dh + e``) and ``b_Q|b_K|b_V`` into ``[3][H][dh]`` (see ``HookedTransformer._iit_arena_groups``);
-    shared by every model whose blocks carry an :class:`Attention` (GPT-2 / BERT; GQA blocks are skipped)."""
+    """Arena groups packing each block's ``W_Q|W_K|W_V`` into one ``[d_model][(H + 2*H_kv)*d_head]`` matrix
+    (query heads, then key heads, then value heads; column ``head*dh + e``) and ``b_Q|b_K|b_V`` into
+    ``[H + 2*H_kv][dh]`` (see ``HookedTransformer._iit_arena_groups``).  Without grouped-query heads this is the
+    ``[d][3][H][dh]`` layout the HIP backend's fused QKV GEMM reads; with them (Llama: ``_W_K`` / ``_W_V`` hold
+    the ``H_kv`` heads) the torch backend's packed projection (``TorchOps.qkv``) runs one GEMM per block."""
     H, d, dh = cfg.n_heads, cfg.d_model, cfg.d_head
-    HD = H * dh
     groups = []
     for blk in blocks:
         a = blk.attn
-        if a.gqa or any(getattr(a, n).shape != (H, d, dh) for n in ("W_Q", "W_K", "W_V")):
+        Hkv = a.n_kv
+        Wq = a.W_Q
+        Wk, Wv = (a._W_K, a._W_V) if a.gqa else (a.W_K, a.W_V)
+        bq = a.b_Q
+        bk, bv = (a._b_K, a._b_V) if a.gqa else (a.b_K, a.b_V)
+        if Wq.shape != (H, d, dh) or Wk.shape != (Hkv, d, dh) or Wv.shape != (Hkv, d, dh):
             continue
+        Ht = H + 2 * Hkv
 
-        def w_view(which):
-            return lambda buf: buf.view(d, 3, H, dh)[:, which].permute(1, 0, 2)
+        def w_view(c0, n):
+            return lambda buf: buf.view(d, Ht, dh)[:, c0:c0 + n].permute(1, 0, 2)
 
-        def b_view(which):
-            return lambda buf: buf.view(3, H, dh)[which]
+        def b_view(c0, n):
+            return lambda buf: buf.view(Ht, dh)[c0:c0 + n]
 
-        groups.append((3 * d * HD, [(a.W_Q, w_view(0)), (a.W_K, w_view(1)), (a.W_V, w_view(2))]))
-        groups.append((3 * HD, [(a.b_Q, b_view(0)), (a.b_K, b_view(1)), (a.b_V, b_view(2))]))
+        spans = ((0, H), (H, Hkv), (H + Hkv, Hkv))
+        groups.append((d * Ht * dh, [(w, w_view(*sp)) for w, sp in zip((Wq, Wk, Wv), spans)]))
+        groups.append((Ht * dh, [(b, b_view(*sp)) for b, sp in zip((bq, bk, bv), spans)]))
     return groups
 
 

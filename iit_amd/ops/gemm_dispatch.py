@@ -112,6 +112,17 @@ def _mm_f32(a, b):
     return torch.mm(a, b).float()
 
 
+def _mm_f32_into(c, a, b) -> None:
+    """c = a @ b (bf16 operands, fp32 output written straight into ``c``: beta = 0, no read of ``c``)."""
+    if _BLAS_OK.get("mm_out_dtype", True) and c.is_contiguous():
+        try:
+            torch.mm(a, b, out_dtype=F32, out=c)
+            return
+        except (RuntimeError, TypeError):
+            _BLAS_OK["mm_out_dtype"] = False
+    c.copy_(_mm_f32(a, b))
+
+
 def _addmm_f32(c, base, a, b) -> None:
     """c = base + a @ b with bf16 operands, fp32 accumulate/output, in one hipBLASLt call when supported
     (``base`` may alias ``c``: the accumulate-into-gradient case)."""
@@ -169,7 +180,7 @@ def _blas(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, C2, C3, bias0, bias1, bia
         if bias0 is not None:
             _addmm_f32(c, bias0.reshape(-1).float(), a, b)
         else:
-            c.copy_(_mm_f32(a, b))
+            _mm_f32_into(c, a, b)
     else:
         raise NotImplementedError(epi)
 

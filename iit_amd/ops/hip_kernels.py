@@ -51,6 +51,11 @@ _SIGS = {
     "iit_dgelu": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p],
     "iit_add_bf16": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_int, c_void_p],
     "iit_device_sync": [],
+    "iit_rms_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
+    "iit_rms_bwd": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "iit_rotary": [c_void_p, c_long, c_long, c_long, c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p],
+    "iit_swiglu_fwd": [c_void_p, c_void_p, c_void_p, c_long, c_void_p],
+    "iit_swiglu_bwd": [c_void_p] * 5 + [c_long, c_void_p],
     "iit_flash_fwd": [c_void_p] * 3 + [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ull] + [c_int] * 5
                      + [c_float, c_int, c_void_p],
     "iit_flash_bwd": [c_void_p] * 3 + [c_void_p] * 11 + [c_ull] + [c_int] * 5 + [c_float, c_int, c_void_p],
@@ -227,6 +232,32 @@ def flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, head_mask: int, scale: float,
                                _p(dz), ctypes.cast(ds, c_void_p), _p(lse), _p(dd), _p(dq), _p(dk), _p(dv),
                                ctypes.cast(gs, c_void_p), head_mask, B, S, Hq, Hkv, dh, scale, int(causal), _stream()),
            "flash_bwd")
+
+
+def rms_fwd(x, w, y, rstd, T: int, d: int, eps: float):
+    _check(lib().iit_rms_fwd(_p(x), int(x.dtype == torch.float32), _p(w), _p(y), _p(rstd), T, d, eps, _stream()),
+           "rms_fwd")
+
+
+def rms_bwd(dy, x, rstd, w, dx, dw, T: int, d: int):
+    _check(lib().iit_rms_bwd(_p(dy), _p(x), int(x.dtype == torch.float32), _p(rstd), _p(w), _p(dx), _p(dw), T, d,
+                             _stream()), "rms_bwd")
+
+
+def rotary(x, out, cos, sin, rd: int, offset: int, adjacent: bool, inverse: bool):
+    """out [B,S,H,D] contiguous = rotary(x) (x any batch/position/head strides, unit d stride), bf16."""
+    B, S, H, D = x.shape
+    _check(lib().iit_rotary(_p(x), x.stride(0), x.stride(1), x.stride(2), _p(out), _p(cos), _p(sin), int(inverse),
+                            B, S, H, D, rd, offset, int(adjacent), _stream()), "rotary")
+
+
+def swiglu_fwd(gate, up, post):
+    _check(lib().iit_swiglu_fwd(_p(gate), _p(up), _p(post), gate.numel(), _stream()), "swiglu_fwd")
+
+
+def swiglu_bwd(dpost, gate, up, dgate, dup):
+    _check(lib().iit_swiglu_bwd(_p(dpost), _p(gate), _p(up), _p(dgate), _p(dup), gate.numel(), _stream()),
+           "swiglu_bwd")
 
 
 def ce_fwd(logits, ld, labels, loss, lse, amax, R, V):

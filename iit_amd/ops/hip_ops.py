@@ -44,13 +44,37 @@ def _pad8(n: int) -> int:
 
 
 def _grad_slot(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """``p.grad`` ready to be accumulated into (an arena parameter's lazily-zeroed slot is zeroed now)."""
     if p is None or not p.requires_grad:
         return None
     g = p.grad
     if g is None:
+        flat = getattr(p, "_iit_flat", None)
+        if flat is not None and flat.owns(p):
+            return flat.bind_zero(p)
         g = torch.zeros_like(p, memory_format=torch.contiguous_format)
         p.grad = g
     return g
+
+
+def _claim_store(*ps, shape=None) -> bool:
+    """True when the caller's single GEMM may *store* the complete gradient of ``ps`` (see FlatParams.claim).
+
+    ``shape=(M, N, K)`` of that weight-gradient GEMM: problems with too few output tiles to fill the chip are
+    better served by split-K, whose partial tiles accumulate atomically -- there the claimed slot is zeroed
+    (one small memset) and the caller accumulates (returns False)."""
+    if any(p is None or not p.requires_grad for p in ps):
+        return False
+    flat = getattr(ps[0], "_iit_flat", None)
+    if flat is None or not all(flat.owns(p) for p in ps):
+        return False
+    if not flat.claim(*ps):
+        return False
+    if shape is not None and K._tiling(*shape, True)[1] > 1:
+        for p in ps:
+            p.grad.zero_()
+        return False
+    return True
 
 
 def _done(*params):
@@ -414,11 +438,16 @@ class QKVFn(Function):
         g = dqkv.to(BF16).contiguous().view(T, 3 * HD)
         dx = torch.empty(T, d, dtype=BF16, device=g.device)
         gemm(g, ctx.layer["qkv"], dx, M=T, N=d, K=3 * HD, lda=3 * HD, ldb=3 * HD, ldc=d, epi=K.EPI_BF16)
-        gq, gk, gv = _grad_slot(W_Q), _grad_slot(W_K), _grad_slot(W_V)
+        store = W_Q.stride() == (dh, 3 * HD, 1) and _packed3(W_Q, W_K, W_V, HD) and \
+            _claim_store(W_Q, W_K, W_V, shape=(d, 3 * HD, T))
+        if store:
+            gq, gk, gv = W_Q.grad, W_K.grad, W_V.grad
+        else:
+            gq, gk, gv = _grad_slot(W_Q), _grad_slot(W_K), _grad_slot(W_V)
         if gq is not None and gk is not None and gv is not None:
             if gq.stride() == (dh, 3 * HD, 1) and _packed3(gq, gk, gv, HD):
                 gemm(x2, g, gq, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=3 * HD, mode=K.MODE_AKM | K.MODE_BKM,
-                     epi=K.EPI_F32_ACC)
+                     epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC)
             else:
                 gemm(x2, g, gq, C2=gk, C3=gv, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=0,
                      mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_ACC_QKV, qkv=(dh, H, d))
@@ -542,6 +571,87 @@ def flash_attention(q, k, v, causal: bool, attn_scale: float) -> torch.Tensor:
     return FlashFn.apply(_flash_view(q), _flash_view(k), _flash_view(v), causal, 1.0 / attn_scale)
 
 
+# ============================================================================ Llama-family fused elementwise ops
+# (used by the torch op backend on the GPU: csrc/llama_ops.hip)
+def _c16(t: torch.Tensor) -> torch.Tensor:
+    t = t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+class RMSNormFn(Function):
+    """``x * rsqrt(mean(x^2) + eps) * w`` -> bf16; ``w``'s gradient accumulates into its fp32 slot."""
+
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        ctx.set_materialize_grads(False)
+        d = x.shape[-1]
+        x2 = _c16(x.reshape(-1, d))
+        T = x2.shape[0]
+        y = torch.empty(T, d, dtype=BF16, device=x.device)
+        rstd = torch.empty(T, dtype=F32, device=x.device)
+        K.rms_fwd(x2, None if w is None else w.detach(), y, rstd, T, d, eps)
+        ctx.save_for_backward(x2, rstd)
+        ctx.w = w
+        ctx.shape = x.shape
+        return y.view(*x.shape[:-1], d)
+
+    @staticmethod
+    def backward(ctx, dy):
+        if dy is None:
+            return None, None, None
+        x2, rstd = ctx.saved_tensors
+        w = ctx.w
+        T, d = x2.shape
+        dx = torch.empty_like(x2)
+        dw = _grad_slot(w) if w is not None else None
+        K.rms_bwd(_c16(dy.to(BF16).reshape(T, d)), x2, rstd, None if w is None else w.detach(), dx, dw, T, d)
+        _done(w)
+        return dx.view(ctx.shape), None, None
+
+
+class RotaryFn(Function):
+    @staticmethod
+    def forward(ctx, x, cos, sin, rd, offset, adjacent):
+        out = torch.empty(x.shape, dtype=BF16, device=x.device)
+        K.rotary(x, out, cos, sin, rd, offset, adjacent, False)
+        ctx.cfg = (cos, sin, rd, offset, adjacent)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin, rd, offset, adjacent = ctx.cfg
+        g = g.to(BF16)
+        if g.stride(-1) != 1:
+            g = g.contiguous()
+        dx = torch.empty(g.shape, dtype=BF16, device=g.device)
+        K.rotary(g, dx, cos, sin, rd, offset, adjacent, True)
+        return dx, None, None, None, None, None
+
+
+class SwiGLUFn(Function):
+    """``silu(gate) * up`` (TL GatedMLP with act_fn silu), bf16."""
+
+    @staticmethod
+    def forward(ctx, gate, up):
+        gate, up = _c16(gate.to(BF16)), _c16(up.to(BF16))
+        post = torch.empty_like(gate)
+        K.swiglu_fwd(gate, up, post)
+        ctx.save_for_backward(gate, up)
+        return post
+
+    @staticmethod
+    def backward(ctx, dpost):
+        gate, up = ctx.saved_tensors
+        dg, du = torch.empty_like(gate), torch.empty_like(up)
+        K.swiglu_bwd(_c16(dpost.to(BF16)), gate, up, dg, du)
+        return dg, du
+
+
+def llama_fused_ok(x: torch.Tensor) -> bool:
+    """The Llama-family fused kernels apply: a bf16 activation on the GPU (``IIT_LLAMA_FUSED=0`` disables)."""
+    return x.is_cuda and x.dtype == BF16 and os.environ.get("IIT_LLAMA_FUSED", "1") != "0"
+
+
 class LinearFn(Function):
     """y = x @ W + b, TL-layout master W [K, N] with bf16 shadow ``w`` (row stride ``ldw``).
 
@@ -608,12 +718,14 @@ class LinearFn(Function):
                      splits=splits)
                 dx = dxf.to(x_dtype)
             dx = dx.view(*lead, Kd)
-        gW = _grad_slot(W)
+        store = _claim_store(W, shape=(Kd, N, T))
+        gW = W.grad if store else _grad_slot(W)
         if gW is not None:
             mode = K.MODE_AKM | K.MODE_BKM
             gW2 = gW.reshape(Kd, N) if gW.is_contiguous() else gW
             assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
-            gemm(x2, g2, gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode, epi=K.EPI_F32_ACC)
+            gemm(x2, g2, gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode,
+                 epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC)
         gb = _grad_slot(b)
         if gb is not None:
             K.colsum_accum(g2, ldg, gb, T, N)
@@ -660,9 +772,11 @@ class MLPInFn(Function):
             dpre = gpre.to(BF16).contiguous().view(T, dm)
         dx = torch.empty(T, d, dtype=BF16, device=x2.device)
         gemm(dpre, ctx.w, dx, M=T, N=d, K=dm, lda=dm, ldb=dm, ldc=d, epi=K.EPI_BF16)
-        gW = _grad_slot(W_in)
+        store = W_in.is_contiguous() and _claim_store(W_in, shape=(d, dm, T))
+        gW = W_in.grad if store else _grad_slot(W_in)
         if gW is not None:
-            gemm(x2, dpre, gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm, mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_ACC)
+            gemm(x2, dpre, gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm, mode=K.MODE_AKM | K.MODE_BKM,
+                 epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC)
         gb = _grad_slot(b_in)
         if gb is not None:
             K.colsum_accum(dpre, dm, gb, T, dm)

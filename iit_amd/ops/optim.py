@@ -62,7 +62,7 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 closure()
-        self.flat.rebind_grads()
+        self.flat.rebind_grads(zero_missing=True)  # gradients no backward produced (lazy zero_grad) are zero
         group = self.param_groups[0]
         lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
         g = self.flat.grad

@@ -53,9 +53,24 @@ def _accumulate(p: torch.Tensor, g: torch.Tensor) -> None:
     from ..engine import grad_hooks
     slot = p.grad
     if slot is None:
-        slot = p.grad = torch.zeros_like(p)
+        flat = getattr(p, "_iit_flat", None)
+        slot = flat.bind_zero(p) if flat is not None and flat.owns(p) else torch.zeros_like(p)
+        p.grad = slot
+    if g.dtype != slot.dtype and g.numel() <= (1 << 20):
+        # small vectors (norm weights): cast + same-dtype add is two ~3 us launches; ROCm's mixed-dtype
+        # add kernel takes ~50 us on a 4096-vector
+        g = g.to(slot.dtype)
     slot.add_(g)
     grad_hooks.notify(p)
+
+
+def _bias_grad_accumulate(slot: torch.Tensor, g2: torch.Tensor) -> None:
+    """fp32 ``slot`` += column sums of the ``[T, N]`` gradient ``g2`` (HIP column-sum kernel on the GPU)."""
+    if g2.is_cuda and slot.is_contiguous() and slot.dtype == torch.float32 and g2.stride(-1) == 1:
+        from . import hip_kernels as K
+        K.colsum_accum(g2, g2.stride(0), slot, g2.shape[0], g2.shape[1])
+    else:
+        slot.add_(g2.float().sum(0))
 
 
 class _MirrorWeight(torch.autograd.Function):
@@ -80,7 +95,7 @@ class _MirrorEmbed(torch.autograd.Function):
     @staticmethod
     def forward(ctx, tokens, W_E, _flat):
         ctx.save_for_backward(tokens)
-        ctx.p = W_E
+        ctx.p, ctx.flat = W_E, _flat
         return _flat.shadow_view(W_E)[tokens]
 
     @staticmethod
@@ -90,7 +105,7 @@ class _MirrorEmbed(torch.autograd.Function):
         W_E = ctx.p
         slot = W_E.grad
         if slot is None:
-            slot = W_E.grad = torch.zeros_like(W_E)
+            slot = ctx.flat.bind_zero(W_E)
         slot.index_add_(0, tokens.reshape(-1), g.reshape(-1, g.shape[-1]).to(slot.dtype))
         grad_hooks.notify(W_E)
         return None, None, None
@@ -124,14 +139,72 @@ class _MirrorLinear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = (g2 @ flat.shadow_view(W).t()).view(*ctx.lead, W.shape[0])
         if W.requires_grad:
-            slot = W.grad
-            if slot is None:
-                slot = W.grad = torch.zeros_like(W)
-            _addmm_f32(slot, slot, x2.t(), g2)
+            from .gemm_dispatch import _mm_f32_into
+            if flat.claim(W):  # lazily-zeroed slot: store (beta = 0)
+                _mm_f32_into(W.grad, x2.t(), g2)
+            else:
+                slot = W.grad
+                if slot is None:
+                    slot = W.grad = torch.zeros_like(W)
+                _addmm_f32(slot, slot, x2.t(), g2)
             grad_hooks.notify(W)
         if b is not None and b.requires_grad:
-            _accumulate(b, g2.float().sum(0))
+            if b.grad is None:
+                flat.bind_zero(b)
+            _bias_grad_accumulate(b.grad, g2)
+            grad_hooks.notify(b)
         return dx, None, None, None
+
+
+class _MirrorMat(torch.autograd.Function):
+    """``y = x @ Wm (+ bm)`` for an arena matrix given as explicit 2-D views: ``wm`` / ``bm`` of the bf16
+    mirror, ``gw`` / ``gb`` of the fp32 gradient arena.  The weight gradient is one fp32-output GEMM
+    accumulating into ``gw`` (``addmm``, beta = 1); ``params`` are reported to the DP reducer.  Used for
+    matrices whose TL shape is not 2-D: the packed ``W_Q|W_K|W_V`` group ``[d][(H + 2 H_kv) dh]`` and
+    ``W_O [H, dh, d]`` as ``[H dh][d]``."""
+
+    @staticmethod
+    def forward(ctx, x, wm, bm, gw, gb, wparams, bparams, *leaves):
+        lead = x.shape[:-1]
+        x2 = x.reshape(-1, x.shape[-1])
+        y = x2 @ wm
+        if bm is not None:
+            y = y + bm
+        ctx.save_for_backward(x2)
+        ctx.wm, ctx.gw, ctx.gb, ctx.lead, ctx.n_leaves = wm, gw, gb, lead, len(leaves)
+        ctx.wparams, ctx.bparams = wparams, bparams
+        return y.view(*lead, y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, gy):
+        from ..engine import grad_hooks
+        from .gemm_dispatch import _addmm_f32
+        (x2,) = ctx.saved_tensors
+        g2 = gy.reshape(-1, gy.shape[-1]).to(x2.dtype)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (g2 @ ctx.wm.t()).view(*ctx.lead, ctx.wm.shape[0])
+        if ctx.gw is not None:
+            flat = ctx.wparams[0]._iit_flat
+            if flat.claim(*ctx.wparams):  # lazily-zeroed slot: store (beta = 0)
+                from .gemm_dispatch import _mm_f32_into
+                _mm_f32_into(ctx.gw, x2.t(), g2)
+            else:
+                _addmm_f32(ctx.gw, ctx.gw, x2.t(), g2)
+        if ctx.gb is not None:
+            for b in ctx.bparams:
+                if b.grad is None:
+                    b._iit_flat.bind_zero(b)
+            _bias_grad_accumulate(ctx.gb, g2)
+        for p in ctx.wparams + ctx.bparams:
+            grad_hooks.notify(p)
+        return (dx, None, None, None, None, None, None) + (None,) * ctx.n_leaves
+
+
+def _bound_to_arena(flat, p: torch.Tensor) -> bool:
+    """``p.grad`` is the arena view at ``p``'s offset (so writing the arena is writing ``p.grad``)."""
+    g = p.grad  # None: lazily zeroed (FlatParams.zero_grad) -- the backward claims / binds the slot itself
+    return g is None or (g.data_ptr() == flat.grad.data_ptr() + flat.offset_of(p) * 4 and g.stride() == p.stride())
 
 
 class TorchOps:
@@ -194,6 +267,13 @@ class TorchOps:
 
     def rms_norm(self, x, w: Optional[torch.Tensor], eps: float, hook_scale=None, hook_normalized=None):
         """TL ``RMSNorm`` / ``RMSNormPre``: ``x / sqrt(mean(x^2) + eps) (* w)``."""
+        if hook_scale is None and hook_normalized is None and self.dtype == torch.bfloat16 and x.is_cuda \
+                and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192 and x.dtype in (torch.bfloat16, torch.float32) \
+                and (w is None or (w.dtype == torch.float32 and w.is_contiguous())):
+            import os
+            if os.environ.get("IIT_LLAMA_FUSED", "1") != "0":
+                from . import hip_ops
+                return hip_ops.RMSNormFn.apply(x, w, eps)  # csrc/llama_ops.hip: one pass fwd, one + dw bwd
         x = x.to(self.dtype)
         scale = (x.pow(2).mean(-1, keepdim=True) + eps).sqrt()
         if hook_scale is not None:
@@ -209,6 +289,11 @@ class TorchOps:
         """Rotary position embedding of ``x [B, S, H, dh]`` on its first ``rotary_dim`` features
         (TL ``apply_rotary``; GPT-NeoX half-split pairs, or adjacent (even, odd) pairs)."""
         S = x.shape[1]
+        if x.is_cuda and x.dtype == torch.bfloat16 and x.stride(-1) == 1 and cos.dtype == torch.float32 \
+                and cos.is_contiguous() and sin.is_contiguous() and rotary_dim % 2 == 0:
+            from . import hip_ops
+            if hip_ops.llama_fused_ok(x):
+                return hip_ops.RotaryFn.apply(x, cos, sin, rotary_dim, offset, adjacent_pairs)
         c = cos[offset:offset + S].to(x.dtype)[None, :, None, :]
         s = sin[offset:offset + S].to(x.dtype)[None, :, None, :]
         xr, xp = x[..., :rotary_dim], x[..., rotary_dim:]
@@ -221,7 +306,57 @@ class TorchOps:
         out = xr * c + flipped * s
         return torch.cat([out, xp], dim=-1) if xp.shape[-1] else out
 
+    def _packed_qkv(self, x, W_Q, W_K, W_V, b_Q, b_K, b_V):
+        """One GEMM over the packed arena group (see ``qkv_arena_groups``) on the bf16 mirror, or None."""
+        if self.dtype != torch.bfloat16 or not x.is_cuda or W_Q.dim() != 3:
+            return None
+        m = _arena_mirror(W_Q)
+        if m is None:
+            return None
+        flat = m[0]
+        H, d, dh = W_Q.shape
+        Hkv = W_K.shape[0]
+        Ht = H + 2 * Hkv
+        N = Ht * dh
+        ws = (W_Q, W_K, W_V)
+        if any(w.stride() != (dh, N, 1) or not flat.owns(w) for w in ws):
+            return None
+        off = flat.offset_of(W_Q)
+        if flat.offset_of(W_K) != off + H * dh or flat.offset_of(W_V) != off + (H + Hkv) * dh:
+            return None
+        bs = (b_Q, b_K, b_V)
+        boff = flat.offset_of(b_Q) if flat.owns(b_Q) else -1
+        packed_b = boff >= 0 and all(b.requires_grad and flat.owns(b) and b.is_contiguous() for b in bs) and \
+            flat.offset_of(b_K) == boff + H * dh and flat.offset_of(b_V) == boff + (H + Hkv) * dh
+        if not packed_b and any(b is not None and b.requires_grad for b in bs):
+            return None
+        grad = torch.is_grad_enabled() and all(w.requires_grad for w in ws)
+        if grad and not all(_bound_to_arena(flat, p) for p in ws + (bs if packed_b else ())):
+            return None
+        sh = flat.shadow
+        wm = sh.as_strided((d, N), (N, 1), off)
+        bm = sh.as_strided((N,), (1,), boff) if packed_b else None
+        xb = x.to(torch.bfloat16)
+        if not grad:
+            y = xb.reshape(-1, d) @ wm
+            if bm is not None:
+                y = y + bm
+            y = y.view(*x.shape[:-1], N)
+        else:
+            gw = flat.grad.as_strided((d, N), (N, 1), off)
+            gb = flat.grad.as_strided((N,), (1,), boff) if packed_b else None
+            bp = bs if packed_b else ()
+            y = _MirrorMat.apply(xb, wm, bm, gw, gb, ws, bp, *(ws + bp))
+        lead = x.shape[:-1]
+        q = y[..., :H * dh].view(*lead, H, dh)
+        k = y[..., H * dh:(H + Hkv) * dh].view(*lead, Hkv, dh)
+        v = y[..., (H + Hkv) * dh:].view(*lead, Hkv, dh)
+        return q, k, v
+
     def qkv(self, x, W_Q, W_K, W_V, b_Q, b_K, b_V):
+        packed = self._packed_qkv(x, W_Q, W_K, W_V, b_Q, b_K, b_V)
+        if packed is not None:
+            return packed
         q = torch.einsum("bsd,hde->bshe", x, self.w(W_Q)) + self.w(b_Q)
         k = torch.einsum("bsd,hde->bshe", x, self.w(W_K)) + self.w(b_K)
         v = torch.einsum("bsd,hde->bshe", x, self.w(W_V)) + self.w(b_V)
@@ -244,6 +379,23 @@ class TorchOps:
         return z
 
     def o_proj(self, z, W_O, b_O):
+        if self.dtype == torch.bfloat16 and z.is_cuda and W_O.is_contiguous():
+            m = _arena_mirror(W_O)
+            mb = _arena_mirror(b_O) if (b_O is not None and b_O.is_contiguous()) else None
+            if m is not None and (b_O is None or mb is not None):
+                flat = m[0]
+                H, dh, d = W_O.shape
+                wm = m[1].view(H * dh, d)
+                grad = torch.is_grad_enabled() and W_O.requires_grad
+                z2 = z.to(torch.bfloat16).reshape(*z.shape[:-2], H * dh)
+                if not grad:
+                    y = z2 @ wm
+                    return y if mb is None else y + mb[1]
+                if _bound_to_arena(flat, W_O) and (b_O is None or _bound_to_arena(flat, b_O)):
+                    bp = () if b_O is None else (b_O,)
+                    gw = flat.grad.as_strided((H * dh, d), (d, 1), flat.offset_of(W_O))
+                    gb = None if b_O is None else flat.grad.as_strided((d,), (1,), flat.offset_of(b_O))
+                    return _MirrorMat.apply(z2, wm, None if mb is None else mb[1], gw, gb, (W_O,), bp, W_O, *bp)
         return torch.einsum("bshe,hed->bsd", z, self.w(W_O)) + self.w(b_O)
 
     def o_result(self, z, W_O):
@@ -258,6 +410,12 @@ class TorchOps:
     def mlp_gated_in(self, x, W_gate, W_in, b_in, act: str, hook_pre=None, hook_pre_linear=None):
         """TL ``GatedMLP``: ``pre = x W_gate`` (hook_pre), ``pre_linear = x W_in + b_in``, ``post = act(pre) * pre_linear``."""
         pre = self.lin(x, W_gate)
+        if act == "silu" and hook_pre is None and hook_pre_linear is None and pre.is_cuda \
+                and pre.dtype == torch.bfloat16 and pre.shape[-1] % 8 == 0:
+            from . import hip_ops
+            if hip_ops.llama_fused_ok(pre):
+                pre_linear = self.lin(x, W_in, b_in)
+                return pre, hip_ops.SwiGLUFn.apply(pre, pre_linear)
         if hook_pre is not None:
             pre = hook_pre(pre)
         pre_linear = self.lin(x, W_in, b_in)

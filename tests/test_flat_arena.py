@@ -134,3 +134,31 @@ def test_row_restriction_span_table():
     flat.grad[off + 3 * 8] = 1.0
     assert not flat.check_inactive_zero()
     assert flat.restrict_rows(m["emb"].weight, None) and not flat.inactive_ranges()
+
+
+def test_lazy_zero_grad_store_claims():
+    """FlatParams.zero_grad leaves store-claimed slots to their producer (grad None, no memset); a claim on a
+    live gradient accumulates; unclaimed None slots read as zero when consumed."""
+    from iit_amd.engine.flat import FlatParams
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Linear(5, 3))
+    flat = FlatParams(m)
+    W0, b0, W1, b1 = m[0].weight, m[0].bias, m[1].weight, m[1].bias
+    flat.grad.fill_(7.0)  # stale values
+    flat.zero_grad()  # nothing claimed yet: full memset
+    assert float(flat.grad.abs().sum()) == 0.0 and W0.grad is not None
+    assert not flat.claim(W1)  # live (zeroed) gradient: accumulate -- but W1 is now known to be store-produced
+    flat.grad.fill_(7.0)
+    flat.zero_grad()
+    assert W1.grad is None and W0.grad is not None  # W1 lazily zeroed, W0 memset
+    assert float(W0.grad.abs().sum()) == 0.0 and float(b1.grad.abs().sum()) == 0.0
+    assert float(flat.grad_view(W1).abs().sum()) > 0  # its slot still holds stale values ...
+    assert flat.claim(W1)  # ... which the producer overwrites (store)
+    W1.grad.copy_(torch.ones_like(W1))
+    assert torch.equal(flat.grad_view(W1), torch.ones_like(W1))
+    # a claimed slot no producer wrote reads as zero once consumed
+    flat.grad.fill_(7.0)
+    flat.zero_grad()
+    assert W1.grad is None
+    flat.rebind_grads(zero_missing=True)
+    assert float(W1.grad.abs().sum()) == 0.0

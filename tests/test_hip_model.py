@@ -212,15 +212,33 @@ def test_torch_backend_reads_arena_mirror_and_accumulates_in_place():
     from iit_amd.engine.flat import FlatParams
     from iit_amd.models.convert import llama_config_dict
     from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.ops import torch_ops
     cfg = llama_config_dict("llama-tiny", device=dev, dtype=torch.bfloat16)
-    torch.manual_seed(0)
-    a = HookedTransformer(cfg)
-    b = copy.deepcopy(a)
-    flat = FlatParams(a)
-    tok = torch.randint(0, cfg["d_vocab"], (4, 9), device=dev)
-    for m in (a, b):
-        m(tok).float().pow(2).mean().backward()
-    assert flat.shadow is not None  # the mirror was used
-    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
-        assert rel(pa.grad, pb.grad) < 1e-2, n
-    assert flat.grad.abs().sum() > 0
+    assert cfg["n_key_value_heads"] < cfg["n_heads"]  # grouped-query heads: packed [d][(H + 2 H_kv) dh] arena group
+    calls = []
+    orig = torch_ops._MirrorMat.apply
+    torch_ops._MirrorMat.apply = lambda *a_: calls.append(1) or orig(*a_)
+    try:
+        for S in (9, 40):  # 40 > 16 with d_head 64: the tiled MFMA attention kernel on the torch backend
+            if S > 16:
+                cfg = llama_config_dict("llama-tiny", device=dev, dtype=torch.bfloat16, d_head=64, rotary_dim=64)
+            torch.manual_seed(0)
+            a = HookedTransformer(cfg)
+            b = copy.deepcopy(a)
+            flat = FlatParams(a)
+            tok = torch.randint(0, cfg["d_vocab"], (4, S), device=dev)
+            with torch.no_grad():
+                assert rel(a(tok), b(tok)) < 1e-2
+            for m in (a, b):
+                m(tok).float().pow(2).mean().backward()
+            assert flat.shadow is not None  # the mirror was used
+            scale = max(pb.grad.float().norm().item() for pb in b.parameters())
+            for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+                # near-cancelling gradients (the key bias: softmax is shift-invariant up to the rotary) are noise
+                # in both paths: relative to the model's gradient scale there
+                err = (pa.grad.float() - pb.grad.float()).norm().item()
+                assert err <= 1e-2 * pb.grad.float().norm().item() + 1e-4 * scale, (S, n)
+            assert flat.grad.abs().sum() > 0
+    finally:
+        torch_ops._MirrorMat.apply = orig
+    assert calls  # packed QKV / 2-D W_O projections ran

@@ -1,0 +1,73 @@
+"""Llama-family fused kernels (csrc/llama_ops.hip) vs plain fp32 PyTorch: RMSNorm (+ weight gradient),
+rotary embedding (NeoX halves and adjacent pairs, partial rotary_dim, strided input), SwiGLU."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("d", [64, 520, 4096])
+@pytest.mark.parametrize("x_dtype", [torch.bfloat16, torch.float32])
+def test_rmsnorm_fwd_bwd(d, x_dtype):
+    from iit_amd.ops import hip_ops
+    torch.manual_seed(d)
+    x = torch.randn(3, 37, d, device=dev).to(x_dtype).requires_grad_()
+    w = (1 + 0.1 * torch.randn(d, device=dev)).requires_grad_()
+    y = hip_ops.RMSNormFn.apply(x, w, 1e-5)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().clone().requires_grad_()
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    assert y.dtype == torch.bfloat16 and rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    assert x.grad.dtype == x_dtype
+    assert rel(x.grad, xr.grad) < 2e-2
+    assert rel(w.grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("adjacent", [False, True])
+@pytest.mark.parametrize("rd", [128, 64])
+def test_rotary_matches_torch_ops(adjacent, rd):
+    from iit_amd.ops import hip_ops
+    from iit_amd.ops.torch_ops import TorchOps
+    from iit_amd.models.config import HookedTransformerConfig
+    from iit_amd.models.transformer import rotary_tables
+    cfg = HookedTransformerConfig.from_dict(dict(n_layers=1, d_model=256, n_heads=2, d_head=128, n_ctx=64,
+                                                 d_vocab=16, act_fn="silu", rotary_dim=rd, rotary_adjacent_pairs=adjacent,
+                                                 positional_embedding_type="rotary"))
+    sin, cos = (t.to(dev) for t in rotary_tables(cfg))
+    torch.manual_seed(0)
+    packed = torch.randn(2, 20, 3, 4, 128, device=dev).bfloat16()
+    x = packed[:, :, 1].detach().requires_grad_()  # strided view, as q/k of a packed QKV projection
+    assert not x.is_contiguous()
+    y = hip_ops.RotaryFn.apply(x, cos, sin, rd, 3, adjacent)
+    ops = TorchOps(torch.float32)
+    xr = x.detach().float().requires_grad_()
+    yr = TorchOps.rotary(ops, xr, cos, sin, rd, adjacent, offset=3)
+    assert rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    assert rel(x.grad, xr.grad) < 1e-2
+
+
+def test_swiglu_fwd_bwd():
+    from iit_amd.ops import hip_ops
+    torch.manual_seed(0)
+    gate = torch.randn(5, 7, 344, device=dev).bfloat16().requires_grad_()
+    up = torch.randn(5, 7, 344, device=dev).bfloat16().requires_grad_()
+    post = hip_ops.SwiGLUFn.apply(gate, up)
+    gr, ur = (t.detach().float().requires_grad_() for t in (gate, up))
+    pr = torch.nn.functional.silu(gr) * ur
+    assert rel(post, pr) < 1e-2
+    g = torch.randn_like(pr)
+    post.backward(g.bfloat16())
+    pr.backward(g)
+    assert rel(gate.grad, gr.grad) < 2e-2 and rel(up.grad, ur.grad) < 2e-2
