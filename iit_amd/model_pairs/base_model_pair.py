@@ -138,6 +138,11 @@ class BaseModelPair(ABC):
         names = sorted({n.name for n in ll_nodes})
         model = self.ll_model
         if self.native():
+            pf = getattr(self, "_source_prefetch", None)
+            if pf is not None:  # evaluation: the double-buffered cache computed ahead on a side stream
+                cached = pf.lookup(x, names)
+                if cached is not None:
+                    return ActivationCache(cached, model)
             return ActivationCache(model.run_capture(x, names), model)
         _, cache = model.run_with_cache(x)
         return cache
@@ -438,8 +443,10 @@ class BaseModelPair(ABC):
     def _run_eval_epoch(self, loader, loss_fn) -> MetricStoreCollection:
         self._ll_module().eval()
         metrics = self.make_test_metrics()
+        from ..engine import prefetch
+        batches = prefetch.prefetched_batches(self, loader) if prefetch.supported(self) else loader
         with torch.no_grad():
-            for base_input, ablation_input in loader:
+            for base_input, ablation_input in batches:
                 metrics.update(self.run_eval_step(base_input, ablation_input, loss_fn))
         return metrics
 
