@@ -67,9 +67,12 @@ __device__ __forceinline__ int kmaj_swz(int kr) {
 // Stage one operand tile (R rows of the output dimension x 64 k) into its LDS image with LDS-DMA.  The per-lane
 // source pointers and LDS offsets are computed once per workgroup; staging K-tile kt then costs one 64-bit add per
 // DMA instruction (the k offset is uniform).
-template <bool KMAJ, int R>
+template <bool KMAJ, int R, int NW = 4>
 struct Stager {
-  static constexpr int N = R / 32;  // LDS-DMA instructions per wave per K-tile
+  // LDS-DMA instructions per wave per K-tile: one instruction moves 8 rows x 128 B (k-contiguous) or
+  // 64 / (R/8) k-rows (k-major); the NW waves of the workgroup split them
+  static constexpr int N = KMAJ ? 64 / (NW * (64 / (R / 8))) : R / (8 * NW);
+  static_assert(N >= 1, "tile too narrow for the workgroup's waves");
   const __bf16* ptr[N];
   int off[N];
   long kstep;  // elements between consecutive K-tiles
@@ -79,7 +82,7 @@ struct Stager {
       // [R][64] bf16, 128-B rows; one instruction = 8 rows x 8 chunks of 16 B
 #pragma unroll
       for (int i = 0; i < N; ++i) {
-        const int r0 = i * 32 + wave * 8;
+        const int r0 = i * 8 * NW + wave * 8;
         const int row = r0 + (lane >> 3);
         const int c = (lane & 7) ^ ((row >> 1) & 7);
         ptr[i] = base + (long)(r0g + row) * ld + kbeg + c * 8;
@@ -92,7 +95,7 @@ struct Stager {
       constexpr int KRI = 64 / CH;  // k-rows per instruction
 #pragma unroll
       for (int i = 0; i < N; ++i) {
-        const int kr0 = (i * 4 + wave) * KRI;
+        const int kr0 = (i * NW + wave) * KRI;
         const int kr = kr0 + lane / CH;
         const int ch = lane % CH;
         const int col = (((ch >> 1) ^ kmaj_swz<R>(kr)) << 4) + ((ch & 1) << 3);
@@ -118,6 +121,26 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
+// Wide k-major operands (R > 128 columns, e.g. the 192-column B tile) are staged as R/64 independent 64-column
+// panels, each its own [64][64] swizzled image (the k-major image layout above needs R/8 | 64).
+template <bool KMAJ, int R, int NW = 4>
+struct OperandStager {
+  static constexpr bool PANELS = KMAJ && R > 128;
+  static constexpr int NP = PANELS ? R / 64 : 1;
+  static constexpr int PR = PANELS ? 64 : R;             // columns per panel
+  static constexpr int N = NP * Stager<KMAJ, PR, NW>::N;  // LDS-DMA instructions per wave per K-tile
+  Stager<KMAJ, PR, NW> st[NP];
+
+  __device__ __forceinline__ void init(const __bf16* base, long ld, int r0g, int kbeg, int wave, int lane) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) st[q].init(base, ld, r0g + q * PR, kbeg, wave, lane);
+  }
+  __device__ __forceinline__ void stage(int kt, char* img) const {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) st[q].stage(kt, img + q * PR * 64 * 2);
+  }
+};
+
 // Fragment reads are split into an *issue* (asm LDS reads into raw registers) and a *use* (combine into the
 // MFMA operand) so the main loop can keep the next sub-step's reads in flight under the current MFMAs.  hipcc
 // does not track asm-issued LDS reads, so the loop waits lgkmcnt(0) (+ sched_barrier) before any use.
@@ -140,6 +163,17 @@ __device__ __forceinline__ void frag_issue(const char* img, int row0, int kbase,
     const unsigned a0 = lds_addr(img + kr * (R * 2) + ((((col >> 4) ^ kmaj_swz<R>(kr))) << 5) + ((col & 15) << 1));
     asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.lo) : "v"(a0));
     asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f.hi) : "v"(a0), "i"(4 * R * 2));
+  }
+}
+
+// fragment of rows/columns [row0, row0 + 16) of an operand tile staged by OperandStager<KMAJ, R>
+template <bool KMAJ, int R>
+__device__ __forceinline__ void frag_issue_t(const char* img, int row0, int kbase, int lane, RawFrag<KMAJ>& f) {
+  using OS = OperandStager<KMAJ, R>;
+  if constexpr (OS::PANELS) {
+    frag_issue<KMAJ, 64>(img + (row0 / 64) * 64 * 64 * 2, row0 % 64, kbase, lane, f);
+  } else {
+    frag_issue<KMAJ, R>(img, row0, kbase, lane, f);
   }
 }
 
@@ -205,21 +239,26 @@ __device__ __forceinline__ void wait_tiles(int tiles_in_flight) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
+template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
   constexpr int BK = 64;
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int NT = NW * 64;                    // threads
+  constexpr int WMR = NW / 2;                    // wave rows (waves form a WMR x 2 grid)
+  constexpr int WM = BM / WMR, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LOADS = BM / 32 + BN / 32;  // LDS-DMA instructions per wave per K-tile
+  constexpr int LOADS = OperandStager<AKM, BM, NW>::N + OperandStager<BKM, BN, NW>::N;  // DMA instrs / wave / K-tile
   constexpr int EPS = BN + 4;  // fp32 epilogue row stride (floats)
-  constexpr int EPI_BYTES = BM * EPS * 4;
+  // the fp32 epilogue tile goes through LDS in row chunks (one per wave row) when the whole tile would not fit
+  constexpr int ECH = BM * EPS * 4 > 160 * 1024 ? 2 : 1;
+  constexpr int EPI_BYTES = BM / ECH * EPS * 4;
   constexpr int SMEM = NS * STAGE > EPI_BYTES ? NS * STAGE : EPI_BYTES;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];  // ONE LDS object (keeps hipcc's waits counted)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave >> 1, wn = wave & 1;  // wave (wm, wn) of the WMR x 2 grid
   const int tiles_n = p.N / BN;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   int tm, tn;
@@ -243,8 +282,8 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
   //    wave's counted vmcnt) and retires all reads of tile kt, so those MFMAs overlap the next DMA issue.
   RawFrag<AKM> ca[TM], na[TM];
   RawFrag<BKM> cb[TN], nb[TN];
-  Stager<AKM, BM> stA;
-  Stager<BKM, BN> stB;
+  OperandStager<AKM, BM, NW> stA;
+  OperandStager<BKM, BN, NW> stB;
   stA.init(p.A, p.lda, m0, kbeg, wave, lane);
   stB.init(p.B, p.ldb, n0, kbeg, wave, lane);
 #pragma unroll
@@ -257,9 +296,9 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
   wait_tiles<LOADS>(min(NS - 1, nt - 1));
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int i = 0; i < TM; ++i) frag_issue<AKM, BM>(smem, wm * WM + i * 16, 0, lane, ca[i]);
+  for (int i = 0; i < TM; ++i) frag_issue_t<AKM, BM>(smem, wm * WM + i * 16, 0, lane, ca[i]);
 #pragma unroll
-  for (int j = 0; j < TN; ++j) frag_issue<BKM, BN>(smem + A_BYTES, wn * WN + j * 16, 0, lane, cb[j]);
+  for (int j = 0; j < TN; ++j) frag_issue_t<BKM, BN>(smem + A_BYTES, wn * WN + j * 16, 0, lane, cb[j]);
 
   for (int kt = 0; kt < nt; ++kt) {
     const char* sa = smem + (kt % NS) * STAGE;
@@ -268,9 +307,9 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) frag_issue<AKM, BM>(sa, wm * WM + i * 16, 32, lane, na[i]);
+    for (int i = 0; i < TM; ++i) frag_issue_t<AKM, BM>(sa, wm * WM + i * 16, 32, lane, na[i]);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) frag_issue<BKM, BN>(sb, wn * WN + j * 16, 32, lane, nb[j]);
+    for (int j = 0; j < TN; ++j) frag_issue_t<BKM, BN>(sb, wn * WN + j * 16, 32, lane, nb[j]);
     __builtin_amdgcn_sched_barrier(0);
     {
       bf16x8 a[TM], b[TN];
@@ -297,9 +336,9 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
       }
       const char* ta = smem + ((kt + 1) % NS) * STAGE;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) frag_issue<AKM, BM>(ta, wm * WM + i * 16, 0, lane, ca[i]);
+      for (int i = 0; i < TM; ++i) frag_issue_t<AKM, BM>(ta, wm * WM + i * 16, 0, lane, ca[i]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) frag_issue<BKM, BN>(ta + A_BYTES, wn * WN + j * 16, 0, lane, cb[j]);
+      for (int j = 0; j < TN; ++j) frag_issue_t<BKM, BN>(ta + A_BYTES, wn * WN + j * 16, 0, lane, cb[j]);
     }
     __builtin_amdgcn_sched_barrier(0);
     {
@@ -330,25 +369,28 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
       return;
     }
   }
-  __syncthreads();  // all waves done with the staging buffers before they become the epilogue tile
-
-  // ---------------------------------------------------------------- epilogue via LDS
+  // ---------------------------------------------------------------- epilogue via LDS (ECH row chunks)
   float* E = (float*)smem;
+  constexpr int ER = BM / ECH;  // rows per chunk: wave rows [ch * WMR / ECH, (ch + 1) * WMR / ECH)
+  for (int ch = 0; ch < ECH; ++ch) {
+  __syncthreads();  // staging buffers / the previous chunk are done before the LDS is (re)written
+  if (wm / (WMR / ECH) == ch) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * WN + j * 16 + (lane & 15);
-      const int row = wm * WM + i * 16 + 4 * (lane >> 4);
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WN + j * 16 + (lane & 15);
+        const int row = (wm % (WMR / ECH)) * WM + i * 16 + 4 * (lane >> 4);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) E[(row + r) * EPS + col] = acc[i][j][r];
-    }
+        for (int r = 0; r < 4; ++r) E[(row + r) * EPS + col] = acc[i][j][r];
+      }
+  }
   __syncthreads();
   constexpr int CPR = BN / 8;  // 8-column chunks per row
 #pragma unroll 2
-  for (int id = tid; id < BM * CPR; id += 256) {
+  for (int id = tid; id < ER * CPR; id += NT) {
     const int lr = id / CPR, lc = (id % CPR) * 8;
-    const int row = m0 + lr, col = n0 + lc;
+    const int row = m0 + ch * ER + lr, col = n0 + lc;
     float v[8];
     {
       const float4 x = *(const float4*)(E + lr * EPS + lc), y = *(const float4*)(E + lr * EPS + lc + 4);
@@ -385,13 +427,14 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(G2Args p) {
       store8_f32((float*)p.C + (long)row * p.ldc + col, v);
     }
   }
+  }  // chunk
 }
 
-template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI>
+template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW = 4>
 hipError_t launch(const G2Args& a, hipStream_t s) {
   const int tiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NS, AKM, BKM, EPI>), dim3(tiles, a.K / a.k_per_split), dim3(256), 0,
-                     s, a);
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NS, AKM, BKM, EPI, NW>), dim3(tiles, a.K / a.k_per_split),
+                     dim3(NW * 64), 0, s, a);
   return hipGetLastError();
 }
 
@@ -403,15 +446,17 @@ hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
     case 1: return launch<128, 64, 4, AKM, BKM, EPI>(a, s);
     case 2: return launch<64, 128, 4, AKM, BKM, EPI>(a, s);
     case 3: return launch<64, 64, 4, AKM, BKM, EPI>(a, s);
+    // 8 waves (two per SIMD, 64 x 96 each): one 256-CU round for 4096 x {2304, 3072}
+    case 5: return launch<256, 192, 2, AKM, BKM, EPI, 8>(a, s);
     default: return launch<128, 128, 4, AKM, BKM, EPI>(a, s);
   }
 }
 
 }  // namespace
 
-#define IIT_GLDS_TILES 5
-static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128};
-static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128};
+#define IIT_GLDS_TILES 6
+static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256};
+static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192};
 
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,

@@ -41,7 +41,7 @@ def _ops(K, mode, M, N, Kd, pad):
 CASES = [(0, 0), (0, 5), (0, 7), (2, 0), (2, 1), (2, 2), (2, 3), (2, 8), (2, 5), (2, 7), (3, 5), (3, 7)]
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("mode,epi", CASES)
 def test_glds_gemm_matches_fp32(K, mode, epi, tile):
     from iit_amd.ops.torch_ops import gelu_new
@@ -109,3 +109,40 @@ def test_glds_rejects_unaligned_shapes(K):
     B = torch.zeros(64, 128, device=dev, dtype=torch.bfloat16)
     C = torch.zeros(100, 128, device=dev, dtype=torch.bfloat16)
     assert not K.gemm_glds_ok(A, B, C, M=100, N=128, K=64, lda=64, ldb=128, ldc=128, mode=2, epi=0, tile=0)
+
+
+@pytest.mark.parametrize("mode,epi", [(2, 3), (2, 1), (0, 0), (2, 7), (3, 7)])
+def test_glds_wide_tile_multi_tile_grid(K, mode, epi):
+    """The 256 x 192 tile (k-major B staged as three 64-column panels, fp32 epilogue in two LDS row chunks) on a
+    grid of several tiles with a longer K loop."""
+    from iit_amd.ops.torch_ops import gelu_new
+    M, N, Kd, pad = 768, 576, 640, 8
+    A, B, lda, ldb, a, b = _ops(K, mode, M, N, Kd, pad)
+    ref = a @ b
+    bias = torch.randn(N, device=dev)
+    kw = dict(M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=mode, epi=epi, tile=5)
+    extra, C2 = {}, None
+    if epi == K.EPI_F32_STORE:
+        C = torch.zeros(M, N, device=dev)
+        if mode != 3:
+            extra = dict(bias0=bias)
+        exp = ref + (bias if mode != 3 else 0)
+    else:
+        C = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+        if epi == K.EPI_GELU:
+            C2 = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+            extra = dict(bias0=bias, C2=C2, ldc2=N)
+            exp = gelu_new(ref + bias)
+        elif epi == K.EPI_BF16_BIAS3:
+            b3 = [torch.randn(N // 3, device=dev) for _ in range(3)]
+            extra = dict(bias0=b3[0], bias1=b3[1], bias2=b3[2], bias_cols=N // 3)
+            exp = ref + torch.cat(b3)
+        else:
+            extra = dict(bias0=bias)
+            exp = ref + bias
+    assert K.gemm_glds_ok(A, B, C, C2=C2, ldc2=N if C2 is not None else 0, bias_cols=extra.get("bias_cols", 0),
+                          **kw)
+    K.gemm_glds(A, B, C, **kw, **extra)
+    torch.cuda.synchronize()
+    err = ((C.float() - exp).norm() / exp.norm()).item()
+    assert err < 1e-2, err
