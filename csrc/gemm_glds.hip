@@ -448,15 +448,17 @@ hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
     case 3: return launch<64, 64, 4, AKM, BKM, EPI>(a, s);
     // 8 waves (two per SIMD, 64 x 96 each): one 256-CU round for 4096 x {2304, 3072}
     case 5: return launch<256, 192, 2, AKM, BKM, EPI, 8>(a, s);
+    case 6: return launch<128, 128, 4, AKM, BKM, EPI, 8>(a, s);  // two waves per SIMD (32 x 64 each)
+    case 7: return launch<256, 128, 2, AKM, BKM, EPI, 8>(a, s);
     default: return launch<128, 128, 4, AKM, BKM, EPI>(a, s);
   }
 }
 
 }  // namespace
 
-#define IIT_GLDS_TILES 6
-static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256};
-static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192};
+#define IIT_GLDS_TILES 8
+static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256};
+static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128};
 
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,

@@ -245,31 +245,19 @@ def _blas16(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, resid, ldr):
 _BLAS16_EPIS = (K.EPI_F32_RESID, K.EPI_F32_ACC)
 
 
-def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=None, bias0=None, bias1=None,
-         bias2=None, resid=None, ldr=0, aux=None, ldc2=0, bias_cols=0, qkv=(0, 0, 0), splits=None, blas_bias=None):
-    """``C = A @ B`` (+ epilogue) on the fastest measured implementation for this problem:
-
-    * ``hip``    -- the hand-written MFMA kernel with the epilogue fused;
-    * ``blas``   -- hipBLASLt (``torch.mm`` / ``addmm``; fp32-output variants for fp32 epilogues);
-    * ``blas16`` -- (fp32 residual / accumulate epilogues) hipBLASLt bf16 output + the fused
-      :func:`iit_amd.ops.hip_kernels.add_bf16` pass.
-
-    ``blas_bias``: optional ready-made bf16 bias row (e.g. a view of the arena's bf16 mirror) for the
-    library path, saving its per-call concatenate/cast."""
-    Kd = K
-    if not _BLAS_SELECTED:
-        select_graph_safe_blas()
-        enable_tuned_library_gemms()
-    hip_call = lambda c=C, c2=C2, c3=C3: K_.gemm(  # noqa: E731
+def _candidates(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, bias2, resid, ldr, aux, ldc2,
+                bias_cols, qkv, splits, blas_bias, policy):
+    """name -> f(c, c2, c3) for every implementation that covers the problem."""
+    hip_call = lambda c=C, c2=C2, c3=None: K_.gemm(  # noqa: E731
         A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=c2, C3=c3, bias0=bias0,
         bias1=bias1, bias2=bias2, resid=resid, ldr=ldr, aux=aux, ldc2=ldc2, bias_cols=bias_cols, qkv=qkv,
         splits=splits)
-    policy = POLICY
-    if policy == "hip" or not _blas_supported(epi, C):
-        return hip_call()
-    blas_call = lambda c=C, c2=C2, c3=C3: _blas(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi, c2, c3, bias0,  # noqa
-                                               bias1, bias2, resid, ldr, aux, ldc2, bias_cols, qkv, blas_bias)
-    calls = {"hip": hip_call, "blas": blas_call}
+    calls = {"hip": hip_call}
+    if not _blas_supported(epi, C):
+        return calls
+    calls["blas"] = lambda c=C, c2=C2, c3=None: _blas(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi, c2, c3,  # noqa
+                                                     bias0, bias1, bias2, resid, ldr, aux, ldc2, bias_cols, qkv,
+                                                     blas_bias)
     if policy in ("auto", "glds") and A.is_cuda:
         split_opts = (1, 2, 4) if epi == K_.EPI_F32_ACC and (M // 64) * (N // 64) < 1024 else (1,)
         for tile in K_.GLDS_TILES:
@@ -277,23 +265,59 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
                 if K_.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=C2,
                                    resid=resid, ldc2=ldc2, ldr=ldr, bias_cols=bias_cols, tile=tile, splits=sp):
                     calls[f"glds{tile}" + (f"k{sp}" if sp > 1 else "")] = \
-                        lambda c=C, c2=C2, c3=C3, t=tile, sp=sp: K_.gemm_glds(  # noqa: E731
+                        lambda c=C, c2=C2, c3=None, t=tile, sp=sp: K_.gemm_glds(  # noqa: E731
                             A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=c2,
                             bias0=bias0, bias1=bias1, bias2=bias2, resid=resid, ldc2=ldc2, ldr=ldr,
                             bias_cols=bias_cols, tile=t, splits=sp)
     if epi in _BLAS16_EPIS:
-        calls["blas16"] = lambda c=C, c2=C2, c3=C3: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
-                                                           bias0, resid, ldr)
+        calls["blas16"] = lambda c=C, c2=C2, c3=None: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
+                                                             bias0, resid, ldr)
+    return calls
+
+
+def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=None, bias0=None, bias1=None,
+         bias2=None, resid=None, ldr=0, aux=None, ldc2=0, bias_cols=0, qkv=(0, 0, 0), splits=None, blas_bias=None,
+         fresh: bool = False):
+    """``C = A @ B`` (+ epilogue) on the fastest measured implementation for this problem:
+
+    * ``hip``    -- the hand-written MFMA kernel with the epilogue fused;
+    * ``glds*``  -- the LDS-DMA MFMA kernel, per tile (and split-K for accumulate epilogues);
+    * ``blas``   -- hipBLASLt (``torch.mm`` / ``addmm``; fp32-output variants for fp32 epilogues);
+    * ``blas16`` -- (fp32 residual / accumulate epilogues) hipBLASLt bf16 output + the fused
+      :func:`iit_amd.ops.hip_kernels.add_bf16` pass.
+
+    ``fresh`` (with ``EPI_F32_STORE``): ``C`` holds garbage (a lazily zeroed gradient slot), so besides
+    storing, "zero ``C`` then accumulate" is also correct -- the split-K accumulate tiles compete too
+    (``z+`` candidates, the memset included in their time).
+    ``blas_bias``: optional ready-made bf16 bias row (e.g. a view of the arena's bf16 mirror) for the
+    library path, saving its per-call concatenate/cast."""
+    Kd = K
+    if not _BLAS_SELECTED:
+        select_graph_safe_blas()
+        enable_tuned_library_gemms()
+    policy = POLICY
+    fresh = fresh and epi == K_.EPI_F32_STORE and bias0 is None
+    args = (A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, bias2, resid, ldr, aux, ldc2, bias_cols,
+            qkv, splits, blas_bias, policy)
+    calls = _candidates(*args)
+    hip_call = calls["hip"]
+    if policy == "hip" or "blas" not in calls:
+        return hip_call(C, C2, C3)
+    if fresh:
+        acc = _candidates(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, K_.EPI_F32_ACC, None, None, None, resid, ldr,
+                          aux, ldc2, bias_cols, qkv, None, blas_bias, policy)
+        for name, f in acc.items():
+            calls["z+" + name] = lambda c=C, c2=C2, c3=None, f=f: (_as(c, M, N, ldc).zero_(), f(c, c2, c3))
     if policy == "glds":
         glds = [k for k in calls if k.startswith("glds")]
-        return calls[glds[0] if glds else "hip"]()
+        return calls[glds[0] if glds else "hip"](C, C2, C3)
     if policy in calls:
-        return calls[policy]()
-    key = (M, N, Kd, mode, epi, bias0 is not None)
+        return calls[policy](C, C2, C3)
+    key = (M, N, Kd, mode, epi, bias0 is not None, fresh)
     choice = DECISIONS.get(key)
     if choice is None:
         if torch.cuda.is_current_stream_capturing():
-            return hip_call()
+            return hip_call(C, C2, C3)
         # time on scratch outputs so accumulate epilogues do not corrupt C
         sc = _scratch(C, M, max(ldc, N))
         sc2 = _scratch(C2, M, max(ldc2, N))
@@ -301,7 +325,7 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         times = {name: min(_time(lambda f=f: f(sc, sc2, sc3)) for _ in range(2)) for name, f in calls.items()}
         best = min(times, key=times.get)
         choice = DECISIONS[key] = (best, times)
-    return calls[choice[0]]()
+    return calls[choice[0]](C, C2, C3)
 
 
 K_ = K  # the kernel module (``K`` is shadowed by the reduction-size keyword above)
@@ -309,7 +333,8 @@ K_ = K  # the kernel module (``K`` is shadowed by the reduction-size keyword abo
 
 def report() -> str:
     lines = [f"library fast paths: {dict(_BLAS_OK) or 'all available'}"]
-    for (M, N, Kd, mode, epi, bias), (c, times) in sorted(DECISIONS.items()):
+    for (M, N, Kd, mode, epi, bias, fresh), (c, times) in sorted(DECISIONS.items()):
         ts = "  ".join(f"{k} {v:8.1f}us" for k, v in times.items())
-        lines.append(f"M={M:6d} N={N:6d} K={Kd:6d} mode={mode:2d} epi={epi} bias={int(bias)} -> {c:6s} {ts}")
+        lines.append(f"M={M:6d} N={N:6d} K={Kd:6d} mode={mode:2d} epi={epi}{'f' if fresh else ''} bias={int(bias)} "
+                     f"-> {c:6s} {ts}")
     return "\n".join(lines)

@@ -131,7 +131,8 @@ def gemm(A, B, C, *, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, mode:
 
 
 GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 128),  # tile 4: 4 LDS stages
-              5: (256, 192)}  # tile 5: 8 x 6 MFMA tiles per wave, 2 stages, epilogue in two row chunks
+              5: (256, 192),  # tiles 5-7: 8 waves (two per SIMD); 5: 4 x 6 MFMA tiles per wave, 2 stages
+              6: (128, 128), 7: (256, 128)}
 
 
 def gemm_glds_ok(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, resid=None, ldc2=0, ldr=0, bias_cols=0,

@@ -57,24 +57,15 @@ def _grad_slot(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return g
 
 
-def _claim_store(*ps, shape=None) -> bool:
-    """True when the caller's single GEMM may *store* the complete gradient of ``ps`` (see FlatParams.claim).
-
-    ``shape=(M, N, K)`` of that weight-gradient GEMM: problems with too few output tiles to fill the chip are
-    better served by split-K, whose partial tiles accumulate atomically -- there the claimed slot is zeroed
-    (one small memset) and the caller accumulates (returns False)."""
+def _claim_store(*ps) -> bool:
+    """True when the caller's single GEMM may *store* the complete gradient of ``ps`` (see FlatParams.claim);
+    the caller then passes ``fresh=True`` so the dispatcher may also pick "zero + split-K accumulate"."""
     if any(p is None or not p.requires_grad for p in ps):
         return False
     flat = getattr(ps[0], "_iit_flat", None)
     if flat is None or not all(flat.owns(p) for p in ps):
         return False
-    if not flat.claim(*ps):
-        return False
-    if shape is not None and K._tiling(*shape, True)[1] > 1:
-        for p in ps:
-            p.grad.zero_()
-        return False
-    return True
+    return flat.claim(*ps)
 
 
 def _done(*params):
@@ -439,7 +430,7 @@ class QKVFn(Function):
         dx = torch.empty(T, d, dtype=BF16, device=g.device)
         gemm(g, ctx.layer["qkv"], dx, M=T, N=d, K=3 * HD, lda=3 * HD, ldb=3 * HD, ldc=d, epi=K.EPI_BF16)
         store = W_Q.stride() == (dh, 3 * HD, 1) and _packed3(W_Q, W_K, W_V, HD) and \
-            _claim_store(W_Q, W_K, W_V, shape=(d, 3 * HD, T))
+            _claim_store(W_Q, W_K, W_V)
         if store:
             gq, gk, gv = W_Q.grad, W_K.grad, W_V.grad
         else:
@@ -447,7 +438,7 @@ class QKVFn(Function):
         if gq is not None and gk is not None and gv is not None:
             if gq.stride() == (dh, 3 * HD, 1) and _packed3(gq, gk, gv, HD):
                 gemm(x2, g, gq, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=3 * HD, mode=K.MODE_AKM | K.MODE_BKM,
-                     epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC)
+                     epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
             else:
                 gemm(x2, g, gq, C2=gk, C3=gv, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=0,
                      mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_ACC_QKV, qkv=(dh, H, d))
@@ -718,14 +709,14 @@ class LinearFn(Function):
                      splits=splits)
                 dx = dxf.to(x_dtype)
             dx = dx.view(*lead, Kd)
-        store = _claim_store(W, shape=(Kd, N, T))
+        store = _claim_store(W)
         gW = W.grad if store else _grad_slot(W)
         if gW is not None:
             mode = K.MODE_AKM | K.MODE_BKM
             gW2 = gW.reshape(Kd, N) if gW.is_contiguous() else gW
             assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
             gemm(x2, g2, gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode,
-                 epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC)
+                 epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
         gb = _grad_slot(b)
         if gb is not None:
             K.colsum_accum(g2, ldg, gb, T, N)
@@ -772,11 +763,11 @@ class MLPInFn(Function):
             dpre = gpre.to(BF16).contiguous().view(T, dm)
         dx = torch.empty(T, d, dtype=BF16, device=x2.device)
         gemm(dpre, ctx.w, dx, M=T, N=d, K=dm, lda=dm, ldb=dm, ldc=d, epi=K.EPI_BF16)
-        store = W_in.is_contiguous() and _claim_store(W_in, shape=(d, dm, T))
+        store = W_in.is_contiguous() and _claim_store(W_in)
         gW = W_in.grad if store else _grad_slot(W_in)
         if gW is not None:
             gemm(x2, dpre, gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm, mode=K.MODE_AKM | K.MODE_BKM,
-                 epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC)
+                 epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
         gb = _grad_slot(b_in)
         if gb is not None:
             K.colsum_accum(dpre, dm, gb, T, dm)
