@@ -1095,3 +1095,23 @@ IIT_EXPORT int iit_probe_tr16b(void* out, void* stream) {
   hipLaunchKernelGGL(probe_tr16b_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (short*)out);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------- multi-span memset
+// Zero many disjoint ranges of one fp32 buffer in a single launch (the flat arena's lazy zero_grad: every
+// gradient slot no store-producer owns).  chunks[i] = (start, len) in elements, len <= 65536; one block each.
+__global__ __launch_bounds__(256) void zero_chunks_kernel(float* __restrict__ base, const long* __restrict__ chunks) {
+  const long start = chunks[2 * blockIdx.x], len = chunks[2 * blockIdx.x + 1];
+  float* p = base + start;
+  const long head = min(len, (long)((4 - (((uintptr_t)p >> 2) & 3)) & 3));  // scalar stores up to 16-B alignment
+  for (long i = threadIdx.x; i < head; i += 256) p[i] = 0.f;
+  float4* q = (float4*)(p + head);
+  const long n4 = (len - head) >> 2;
+  for (long i = threadIdx.x; i < n4; i += 256) q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (long i = head + (n4 << 2) + threadIdx.x; i < len; i += 256) p[i] = 0.f;
+}
+
+IIT_EXPORT int iit_zero_chunks(float* base, const long* chunks, int n_chunks, void* stream) {
+  if (n_chunks <= 0) return 0;
+  hipLaunchKernelGGL(zero_chunks_kernel, dim3(n_chunks), dim3(256), 0, (hipStream_t)stream, base, chunks);
+  return hipGetLastError();
+}

@@ -89,6 +89,7 @@ class FlatParams:
         self.index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
         self._grad_views = None  # (grad arena, cached per-parameter grad views) for rebind_grads
         self._claimed = set()    # parameter indices whose gradient a store-producer wrote (see ``claim``)
+        self._declined = set()   # ... whose producer preferred zero + accumulate (``unclaim``)
         self._zero_plan = None
         self.version = 0
         self.mirror_version = -1
@@ -219,10 +220,23 @@ class FlatParams:
                     ranges.append((o, end))
             none_ids = [i for i, p in enumerate(self.params)
                         if any(o <= self.offset_of(p) < o + max(n, 1) and o in lazy for o, n in self.slots)]
-            self._zero_plan = (key, ranges, none_ids)
-        _, ranges, none_ids = self._zero_plan
-        for a, b in ranges:
-            self.grad[a:b].zero_()
+            chunks = None
+            # one multi-span memset launch instead of one fill per range (its table is uploaded once per plan;
+            # a plan first needed inside a graph capture keeps per-range fills, no host->device copy there)
+            if self.grad.is_cuda and not torch.cuda.is_current_stream_capturing():
+                ch = []
+                for a, b in ranges:
+                    for c in range(a, b, 65536):
+                        ch.append((c, min(65536, b - c)))
+                chunks = (torch.tensor(ch, dtype=torch.int64).view(-1).to(self.grad.device), len(ch))
+            self._zero_plan = (key, ranges, none_ids, chunks)
+        _, ranges, none_ids, chunks = self._zero_plan
+        if chunks is not None:
+            from ..ops import hip_kernels
+            hip_kernels.zero_chunks(self.grad, chunks[0], chunks[1])
+        else:
+            for a, b in ranges:
+                self.grad[a:b].zero_()
         self.rebind_grads()
         for i in none_ids:
             self.params[i].grad = None
@@ -233,6 +247,11 @@ class FlatParams:
         -> accumulate (the gradients are live).  Binds ``.grad`` to the arena views either way."""
         idx = [self.index.get(id(p)) for p in ps]
         if any(i is None for i in idx):
+            return False
+        if any(i in self._declined for i in idx):  # producer chose zero + accumulate: bulk-memset slots
+            for p in ps:
+                if p.grad is None:
+                    self.bind_zero(p)
             return False
         self._claimed.update(idx)  # a store-capable producer: lazily zero these from the next zero_grad on
         fresh = all(p.grad is None for p in ps)
@@ -245,6 +264,15 @@ class FlatParams:
         for i, p in zip(idx, ps):
             p.grad = views[i]
         return True
+
+    def unclaim(self, *ps: torch.Tensor) -> None:
+        """The producer of ``ps`` zero-fills and accumulates after all (e.g. split-K wins): from the next
+        ``zero_grad`` on their slots are part of the bulk memset again."""
+        for p in ps:
+            i = self.index.get(id(p))
+            if i is not None:
+                self._claimed.discard(i)
+                self._declined.add(i)
 
     def bind_zero(self, p: torch.Tensor) -> torch.Tensor:
         """``p.grad`` := its (zeroed) arena view, for producers that accumulate into a ``None`` gradient."""

@@ -290,7 +290,9 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     storing, "zero ``C`` then accumulate" is also correct -- the split-K accumulate tiles compete too
     (``z+`` candidates, the memset included in their time).
     ``blas_bias``: optional ready-made bf16 bias row (e.g. a view of the arena's bf16 mirror) for the
-    library path, saving its per-call concatenate/cast."""
+    library path, saving its per-call concatenate/cast.
+
+    Returns the name of the implementation that ran when the choice was measured (else None)."""
     Kd = K
     if not _BLAS_SELECTED:
         select_graph_safe_blas()
@@ -325,7 +327,8 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         times = {name: min(_time(lambda f=f: f(sc, sc2, sc3)) for _ in range(2)) for name, f in calls.items()}
         best = min(times, key=times.get)
         choice = DECISIONS[key] = (best, times)
-    return calls[choice[0]](C, C2, C3)
+    calls[choice[0]](C, C2, C3)
+    return choice[0]
 
 
 K_ = K  # the kernel module (``K`` is shadowed by the reduction-size keyword above)

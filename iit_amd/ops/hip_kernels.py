@@ -51,6 +51,7 @@ _SIGS = {
     "iit_dgelu": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p],
     "iit_add_bf16": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_int, c_void_p],
     "iit_device_sync": [],
+    "iit_zero_chunks": [c_void_p, c_void_p, c_int, c_void_p],
     "iit_rms_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_rms_bwd": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "iit_rotary": [c_void_p, c_long, c_long, c_long, c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p],
@@ -234,6 +235,11 @@ def flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, head_mask: int, scale: float,
                                _p(dz), ctypes.cast(ds, c_void_p), _p(lse), _p(dd), _p(dq), _p(dk), _p(dv),
                                ctypes.cast(gs, c_void_p), head_mask, B, S, Hq, Hkv, dh, scale, int(causal), _stream()),
            "flash_bwd")
+
+
+def zero_chunks(base, chunks, n: int):
+    """Zero the (start, len) element ranges listed in the int64 device tensor ``chunks`` of fp32 ``base``."""
+    _check(lib().iit_zero_chunks(_p(base), _p(chunks), n, _stream()), "zero_chunks")
 
 
 def rms_fwd(x, w, y, rstd, T: int, d: int, eps: float):

@@ -57,6 +57,13 @@ def _grad_slot(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return g
 
 
+def _settle_claim(choice, *ps) -> None:
+    """The dispatcher served a claimed (fresh) gradient with "zero + accumulate": hand its slot back to the
+    arena's bulk zero_grad memset (one launch for all such slots) instead of a memset per GEMM."""
+    if choice is not None and choice.startswith("z+"):
+        ps[0]._iit_flat.unclaim(*ps)
+
+
 def _claim_store(*ps) -> bool:
     """True when the caller's single GEMM may *store* the complete gradient of ``ps`` (see FlatParams.claim);
     the caller then passes ``fresh=True`` so the dispatcher may also pick "zero + split-K accumulate"."""
@@ -437,8 +444,11 @@ class QKVFn(Function):
             gq, gk, gv = _grad_slot(W_Q), _grad_slot(W_K), _grad_slot(W_V)
         if gq is not None and gk is not None and gv is not None:
             if gq.stride() == (dh, 3 * HD, 1) and _packed3(gq, gk, gv, HD):
-                gemm(x2, g, gq, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=3 * HD, mode=K.MODE_AKM | K.MODE_BKM,
-                     epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+                choice = gemm(x2, g, gq, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=3 * HD,
+                              mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC,
+                              fresh=store)
+                if store:
+                    _settle_claim(choice, W_Q, W_K, W_V)
             else:
                 gemm(x2, g, gq, C2=gk, C3=gv, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=0,
                      mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_ACC_QKV, qkv=(dh, H, d))
@@ -715,8 +725,10 @@ class LinearFn(Function):
             mode = K.MODE_AKM | K.MODE_BKM
             gW2 = gW.reshape(Kd, N) if gW.is_contiguous() else gW
             assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
-            gemm(x2, g2, gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode,
-                 epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+            choice = gemm(x2, g2, gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode,
+                          epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+            if store:
+                _settle_claim(choice, W)
         gb = _grad_slot(b)
         if gb is not None:
             K.colsum_accum(g2, ldg, gb, T, N)
@@ -766,8 +778,10 @@ class MLPInFn(Function):
         store = W_in.is_contiguous() and _claim_store(W_in)
         gW = W_in.grad if store else _grad_slot(W_in)
         if gW is not None:
-            gemm(x2, dpre, gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm, mode=K.MODE_AKM | K.MODE_BKM,
-                 epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+            choice = gemm(x2, dpre, gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm, mode=K.MODE_AKM | K.MODE_BKM,
+                          epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+            if store:
+                _settle_claim(choice, W_in)
         gb = _grad_slot(b_in)
         if gb is not None:
             K.colsum_accum(dpre, dm, gb, T, dm)
