@@ -91,6 +91,8 @@ class FlatParams:
         self._claimed = set()    # parameter indices whose gradient a store-producer wrote (see ``claim``)
         self._declined = set()   # ... whose producer preferred zero + accumulate (``unclaim``)
         self._zero_plan = None
+        self._zero_plans = {}    # claim set -> zero plan; every device table a captured graph may read stays alive
+        self._retired = []       # replaced device tables (span tables) kept alive for the same reason
         self.version = 0
         self.mirror_version = -1
         self._inactive: Dict[int, Tuple[int, int, torch.Tensor]] = {}  # param index -> (offset, row_len, live rows)
@@ -137,8 +139,15 @@ class FlatParams:
             rows = rows[(rows >= 0) & (rows < p.shape[0])]
             self._inactive[i] = (off, int(p.shape[1]), rows)
         self.restrict_version += 1
-        self._span_cache = None
+        self.drop_span_cache()
         return True
+
+    def drop_span_cache(self) -> None:
+        """Forget the optimizer span table; the old device table is retired, not freed (a captured optimizer
+        graph keeps reading its address until it is re-captured)."""
+        if self._span_cache is not None:
+            self._retired.append(self._span_cache[1])
+        self._span_cache = None
 
     def inactive_ranges(self) -> List[Tuple[int, int]]:
         """Sorted (start, end) element ranges the optimizer may skip."""
@@ -176,6 +185,7 @@ class FlatParams:
                 pos += ln
             pos = max(pos, b)
         tab = torch.tensor(spans if spans else [(0, 0)], dtype=torch.int64).view(-1, 2).to(self.data.device)
+        self.drop_span_cache()
         self._span_cache = (key, tab, len(spans))
         return tab, len(spans)
 
@@ -203,6 +213,8 @@ class FlatParams:
             self.rebind_grads()
             return
         key = frozenset(self._claimed)
+        if (self._zero_plan is None or self._zero_plan[0] != key) and key in self._zero_plans:
+            self._zero_plan = self._zero_plans[key]
         if self._zero_plan is None or self._zero_plan[0] != key:
             lazy = set()
             for o, n in self.slots:  # a slot is lazy only when every parameter in it is claimed
@@ -229,7 +241,9 @@ class FlatParams:
                     for c in range(a, b, 65536):
                         ch.append((c, min(65536, b - c)))
                 chunks = (torch.tensor(ch, dtype=torch.int64).view(-1).to(self.grad.device), len(ch))
-            self._zero_plan = (key, ranges, none_ids, chunks)
+            # plans are kept per claim set: a graph captured with this plan's chunk table replays its device
+            # address after the claims change (freeing the table would let the memset read a reused block)
+            self._zero_plan = self._zero_plans[key] = (key, ranges, none_ids, chunks)
         _, ranges, none_ids, chunks = self._zero_plan
         if chunks is not None:
             from ..ops import hip_kernels

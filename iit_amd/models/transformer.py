@@ -333,7 +333,24 @@ class TransformerBlock(nn.Module):
             return self._norm(ln, x, run), x
         return fork(x, ln.w, ln.b, ln.eps)
 
-    def forward(self, resid: torch.Tensor, run: _Run) -> torch.Tensor:
+    def last_position_ok(self, run: _Run) -> bool:
+        """Whether this (final) block may compute only the last position after attention: nothing observes
+        or rewrites a later site of the block at other positions (the logits read position -1 only)."""
+        if self.cfg.use_attn_result:
+            return False
+        sites = [self.hook_attn_out, self.hook_resid_post, self.hook_mlp_out]
+        if not self.cfg.attn_only:
+            sites += [self.hook_resid_mid, self.hook_mlp_in, self.mlp.hook_pre, self.mlp.hook_post]
+            if self.mlp.gated:
+                sites.append(self.mlp.hook_pre_linear)
+            if self.ln2 is not None:
+                sites += [self.ln2.hook_scale, self.ln2.hook_normalized]
+        return not any(run.live(h) for h in sites)
+
+    def forward(self, resid: torch.Tensor, run: _Run, last_only: bool = False) -> torch.Tensor:
+        """``last_only``: after attention (which still sees every position's keys / values) continue with the
+        last position only -- ``[B, 1, d]`` out.  Exact for a loss that reads the last position's logits: the
+        other positions of the final block's W_O / LN2 / MLP never reach it (their gradients are zero)."""
         ops = run.ops
         attn = self.attn
         resid = run.site(self.hook_resid_pre, resid)
@@ -347,6 +364,8 @@ class TransformerBlock(nn.Module):
             x, resid = self._norm_fork(self.ln1, resid, run)
             z, spliced = attn.compute_z(x, run)
             z = run.site(attn.hook_z, z, spliced=spliced)
+        if last_only:
+            z, resid = z[:, -1:].contiguous(), resid[:, -1:].contiguous()
         attn_out_live = run.live(self.hook_attn_out) or self.cfg.use_attn_result
         if self.cfg.use_attn_result:
             result = run.site(attn.hook_result, ops.o_result(z, attn.W_O))
@@ -521,16 +540,20 @@ class HookedTransformer(HookedRootModule):
             resid = self._embed(tokens, run)
             n_blocks = len(self.blocks) if stop_at_layer is None else stop_at_layer
             cuts = self.__dict__.get("_grad_cuts") if torch.is_grad_enabled() else None
+            want = plan.logits if plan is not None else ("last" if logits_at == -1 else "full")
+            # last-position logits: the final block continues past attention at position -1 only
+            last_only = (want == "last" and stop_at_layer is None and return_type is not None
+                         and len(self.blocks) > 0 and getattr(self, "last_position_final_block", True)
+                         and tokens.shape[1] > 1 and self.blocks[-1].last_position_ok(run))
             for li, block in enumerate(self.blocks[:n_blocks]):
                 if cuts and li in cuts and resid.requires_grad:
                     # staged backward (engine.graphs): the backward stops here and resumes as its own segment
                     leaf = resid.detach().requires_grad_(True)
                     self._cut_log.append((li, resid, leaf))
                     resid = leaf
-                resid = block(resid, run)
+                resid = block(resid, run, last_only=last_only and li == len(self.blocks) - 1)
             if stop_at_layer is not None:
                 return resid
-            want = plan.logits if plan is not None else ("last" if logits_at == -1 else "full")
             if plan is not None and plan.logits == "none":
                 return None
             if return_type is None:

@@ -94,6 +94,29 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+CHECK_BOUNDS = os.environ.get("IIT_CHECK_BOUNDS", "0") == "1"
+
+
+def _avail(t: torch.Tensor) -> int:
+    """Elements of ``t``'s storage from its first element to the end."""
+    st = t.untyped_storage()
+    return (st.nbytes() - (t.data_ptr() - st.data_ptr())) // t.element_size()
+
+
+def _bounds(what: str, *spans):
+    """Host-side extent check (``IIT_CHECK_BOUNDS=1``) of raw-pointer kernel operands before a launch: each span
+    ``(name, t, rows, cols, ld)`` must fit inside ``t``'s storage -- a debugging aid that turns an out-of-bounds
+    launch into a Python error instead of a GPU fault."""
+    for name, t, rows, cols, ld in spans:
+        if t is None or rows <= 0 or cols <= 0:
+            continue
+        need = (rows - 1) * ld + cols
+        have = _avail(t)
+        if need > have or ld < cols and rows > 1:
+            raise RuntimeError(f"{what}: operand {name} needs {rows}x{cols} (ld {ld}) = {need} elements, "
+                               f"storage holds {have} (shape {tuple(t.shape)}, stride {t.stride()})")
+
+
 def _check(rc: int, what: str):
     if rc != 0:
         raise RuntimeError(f"{what} failed with hip error {rc}")
@@ -122,9 +145,8 @@ def gemm(A, B, C, *, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, mode:
     big, auto_splits = _tiling(M, N, K, can_split)
     if splits is None:
         splits = auto_splits
-    if K % 8 != 0 and not (mode & MODE_AKM):
-        if any(ld % 8 for ld in (lda,)):
-            pass
+    if CHECK_BOUNDS:
+        _gemm_bounds("iit_gemm", A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode, qkv)
     rc = lib().iit_gemm(_p(A), _p(B), _p(C), _p(C2), _p(C3), _p(bias0), _p(bias1), _p(bias2), _p(resid), _p(aux),
                         lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi, splits, big, bias_cols, qkv[0], qkv[1], qkv[2],
                         int(atomic), _stream())
@@ -134,6 +156,13 @@ def gemm(A, B, C, *, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, mode:
 GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 128),  # tile 4: 4 LDS stages
               5: (256, 192),  # tiles 5-7: 8 waves (two per SIMD); 5: 4 x 6 MFMA tiles per wave, 2 stages
               6: (128, 128), 7: (256, 128)}
+
+
+def _gemm_bounds(what, A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode, qkv=(0, 0, 0)):
+    a = ("A", A, K, M, lda) if mode & MODE_AKM else ("A", A, M, K, lda)
+    b = ("B", B, K, N, ldb) if mode & MODE_BKM else ("B", B, N, K, ldb)
+    c = ("C", C, M, N, ldc) if not qkv[0] else ("C", C, 0, 0, 0)
+    _bounds(what, a, b, c, ("C2", C2, M, N, ldc2 or ldc), ("resid", resid, M, N, ldr or ldc))
 
 
 def gemm_glds_ok(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, resid=None, ldc2=0, ldr=0, bias_cols=0,
@@ -149,6 +178,8 @@ def gemm_glds_ok(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, resid=N
 def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None, bias1=None, bias2=None, resid=None,
               ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1):
     """C = A @ B (+ epilogue) on the LDS-DMA MFMA kernel; bf16 operands, M/N/K multiples of the tile."""
+    if CHECK_BOUNDS:
+        _gemm_bounds("iit_gemm_glds", A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode)
     _check(lib().iit_gemm_glds(_p(A), _p(B), _p(C), _p(C2), _p(bias0), _p(bias1), _p(bias2), _p(resid), lda, ldb,
                                ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits, _stream()), "iit_gemm_glds")
 
@@ -163,11 +194,16 @@ def embed_pos_bwd(tokens, g, dWE, dWpos, B, S, d):
 
 
 def ln_fwd(x, w, b, y, mean, rstd, T, d, eps):
+    if CHECK_BOUNDS:
+        _bounds("ln_fwd", ("x", x, T, d, d), ("y", y, T, d, d), ("mean", mean, 1, T, T), ("rstd", rstd, 1, T, T))
     _check(lib().iit_ln_fwd(_p(x), _p(w), _p(b), _p(y), _p(mean), _p(rstd), T, d, eps, _stream()), "ln_fwd")
 
 
 def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False, dres=None, dx16=None):
     """dx = LN'(dy) (+ dres, the skip-connection gradient, fp32 [T, d]); ``dx16`` (optional) gets a bf16 copy."""
+    if CHECK_BOUNDS:
+        _bounds("ln_bwd", ("dy", dy, T, d, d), ("x", x, T, d, d), ("dx", dx, T, d, d), ("dres", dres, T, d, d),
+                ("dx16", dx16, T, d, d), ("mean", mean, 1, T, T))
     _check(lib().iit_ln_bwd(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx),
                             _p(dres), _p(dx16), _p(dw), _p(db), T, d, int(accumulate), _stream()), "ln_bwd")
 
@@ -185,6 +221,9 @@ def _mfma_attn(S, dh):
 
 def attn_small_fwd(qkv, z, lse, zsrc, head_mask, B, S, H, dh, ld_qkv, ld_z, ld_src, scale, causal):
     """Causal attention for S <= 64 (MFMA one-wave-per-head kernel when S <= 16, csrc/attn_mfma.hip)."""
+    if CHECK_BOUNDS:
+        _bounds("attn_fwd", ("qkv", qkv, B * S, 3 * H * dh, ld_qkv), ("z", z, B * S, H * dh, ld_z),
+                ("zsrc", zsrc, B * S, H * dh, ld_src), ("lse", lse, 1, B * H * S, B * H * S))
     if _mfma_attn(S, dh):
         _check(lib().iit_attn_mfma_fwd(_p(qkv), _p(z), _p(lse), _p(zsrc), head_mask, B, S, H, dh, ld_qkv, ld_z, ld_src,
                                        scale, int(causal), _stream()), "attn_mfma_fwd")
@@ -194,6 +233,9 @@ def attn_small_fwd(qkv, z, lse, zsrc, head_mask, B, S, H, dh, ld_qkv, ld_z, ld_s
 
 
 def attn_small_bwd(qkv, dz, lse, dqkv, head_mask, B, S, H, dh, ld_qkv, ld_dz, scale, causal):
+    if CHECK_BOUNDS:
+        _bounds("attn_bwd", ("qkv", qkv, B * S, 3 * H * dh, ld_qkv), ("dz", dz, B * S, H * dh, ld_dz),
+                ("dqkv", dqkv, B * S, 3 * H * dh, ld_qkv))
     if _mfma_attn(S, dh):
         _check(lib().iit_attn_mfma_bwd(_p(qkv), _p(dz), _p(lse), _p(dqkv), head_mask, B, S, H, dh, ld_qkv, ld_dz, scale,
                                        int(causal), _stream()), "attn_mfma_bwd")
@@ -269,16 +311,22 @@ def swiglu_bwd(dpost, gate, up, dgate, dup):
 
 
 def ce_fwd(logits, ld, labels, loss, lse, amax, R, V):
+    if CHECK_BOUNDS:
+        _bounds("ce_fwd", ("logits", logits, R, V, ld))
     _check(lib().iit_ce_fwd(_p(logits), ld, _p(labels), _p(loss), _p(lse), _p(amax), R, V, _stream()), "ce_fwd")
 
 
 def ce_bwd(logits, ld, labels, lse, gscale, inv_rows, out, ld_out, R, V):
     """dlogits into ``out`` (fp32 or bf16, row stride ``ld_out``; pad columns zeroed)."""
+    if CHECK_BOUNDS:
+        _bounds("ce_bwd", ("logits", logits, R, V, ld), ("out", out, R, V, ld_out))
     _check(lib().iit_ce_bwd(_p(logits), ld, _p(labels), _p(lse), _p(gscale), inv_rows, _p(out), ld_out, R, V,
                             int(out.dtype == torch.bfloat16), _stream()), "ce_bwd")
 
 
 def colsum_accum(x, ld, out, T, N):
+    if CHECK_BOUNDS:
+        _bounds("colsum", ("x", x, T, N, ld), ("out", out, 1, N, N))
     _check(lib().iit_colsum_accum(_p(x), int(x.dtype == torch.float32), ld, _p(out), T, N, _stream()), "colsum")
 
 
@@ -299,6 +347,8 @@ def dgelu(dpost, pre, out, erf=False):
 
 def add_bf16(out, ldo, base, ldb, y, ldy, bias, M, N):
     """out = base + y + bias (fp32 out/base, bf16 y, fp32 bias or None); base may alias out."""
+    if CHECK_BOUNDS:
+        _bounds("add_bf16", ("out", out, M, N, ldo), ("base", base, M, N, ldb), ("y", y, M, N, ldy))
     _check(lib().iit_add_bf16(_p(out), ldo, _p(base), ldb, _p(y), ldy, _p(bias), M, N, _stream()), "add_bf16")
 
 

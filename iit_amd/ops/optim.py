@@ -104,7 +104,7 @@ class FusedAdam(torch.optim.Optimizer):
         ok = wd == 0 and flat.check_inactive_zero(self.exp_avg, self.exp_avg_sq, flat.grad)
         if not ok:
             flat._inactive.clear()
-            flat._span_cache = None
+            flat.drop_span_cache()
             flat.restrict_version += 1
         self._restrict_ok_version = flat.restrict_version
 

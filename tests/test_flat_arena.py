@@ -4,6 +4,7 @@ The arena re-binds every parameter as a (possibly strided) view: W_Q|W_K|W_V
 interleaved into one [d][3HD] matrix, b_Q|b_K|b_V into [3][H][dh], W_U with padded
 rows.  Public shapes, values, forward results, gradients and state_dict are unchanged.
 """
+import pytest
 import torch
 
 from iit_amd.engine.flat import FlatParams
@@ -162,3 +163,26 @@ def test_lazy_zero_grad_store_claims():
     assert W1.grad is None
     flat.rebind_grads(zero_missing=True)
     assert float(W1.grad.abs().sum()) == 0.0
+
+
+@pytest.mark.gpu
+def test_zero_plans_outlive_claim_changes():
+    """A graph captured with one claim set's multi-span memset table replays that table's device address after
+    the claims change: every plan's table stays alive (freeing it let the memset read a reused block)."""
+    from iit_amd.engine.flat import FlatParams
+    m = torch.nn.Sequential(torch.nn.Linear(64, 64), torch.nn.Linear(64, 64)).cuda()
+    flat = FlatParams(m)
+    flat.claim(m[1].weight)
+    flat.zero_grad()
+    key1, _, _, chunks1 = flat._zero_plan
+    assert chunks1 is not None
+    table1 = chunks1[0].clone()
+    flat.claim(m[0].weight)
+    flat.zero_grad()
+    assert flat._zero_plan[0] != key1
+    assert flat._zero_plans[key1][3][0] is chunks1[0] and torch.equal(chunks1[0], table1)
+    flat.grad.fill_(3.0)
+    flat.unclaim(m[0].weight)
+    flat.zero_grad()  # back to the first claim set: its plan (and table) is reused
+    assert flat._zero_plan[3][0] is chunks1[0]
+    assert float(flat.grad_view(m[0].weight).abs().sum()) == 0.0 and m[1].weight.grad is None

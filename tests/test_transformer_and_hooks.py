@@ -132,6 +132,37 @@ def test_last_position_logits_and_argmax_cpu():
     assert torch.equal(m(x, plan=RunPlan(logits="argmax")), full.argmax(-1))
 
 
+def test_last_position_final_block_exact_with_gradients():
+    """With last-position logits the final block runs W_O / LN2 / MLP on position -1 only; losses and every
+    parameter gradient equal the full-width forward's."""
+    m = tiny()
+    x = torch.randint(0, 21, (3, 6))
+    src = torch.randint(0, 21, (3, 6))
+    cache = m.run_capture(src, ["blocks.0.mlp.hook_post"])
+    spl = [("blocks.0.mlp.hook_post", Ix[:, 2:4, :], cache["blocks.0.mlp.hook_post"])]
+    grads = []
+    for fast in (True, False):
+        m.last_position_final_block = fast
+        m.zero_grad(set_to_none=True)
+        out = m(x, plan=RunPlan.with_splices(spl, logits="last"))
+        assert out.shape == (3, 21)
+        (out.square().sum() + out[:, 3].sum()).backward()
+        grads.append({n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys()
+    for n in grads[0]:
+        assert torch.allclose(grads[0][n], grads[1][n], atol=1e-5), n
+    # a live site after attention in the final block keeps the full-width path
+    last = str(len(m.blocks) - 1)
+    plan = RunPlan.with_splices([(f"blocks.{last}.hook_resid_mid", Ix[:, 1:2, :],
+                                  m.run_capture(src, [f"blocks.{last}.hook_resid_mid"])[f"blocks.{last}.hook_resid_mid"])],
+                                logits="last")
+    m.last_position_final_block = True
+    a = m(x, plan=plan)
+    m.last_position_final_block = False
+    assert torch.allclose(a, m(x, plan=plan), atol=1e-6)
+    del m.last_position_final_block
+
+
 def test_attn_only_and_result_hooks():
     m = tiny(attn_only=True, use_attn_result=True)
     x = torch.randint(0, 21, (2, 5))
