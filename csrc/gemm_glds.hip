@@ -27,12 +27,15 @@
 // * Epilogue: accumulators -> LDS (fp32 tile) -> each thread owns 8 consecutive columns of a row: 16-B / 32-B
 //   vector loads of bias / residual / accumulator and vector stores (the MFMA C layout would otherwise give
 //   2-byte column-strided stores).
+// * E_DGELU (mode 0, the MLP backward dpre = (dY W_out^T) * gelu_new'(pre)): reads the saved pre-activation in the
+//   epilogue and, with ``csum``, also reduces the stored dpre tile over its rows in LDS into the b_in gradient
+//   (one atomic per column per tile) -- the separate dgelu pass and the bias column-sum pass disappear.
 #include "common.h"
 
 namespace {
 
-enum : int { E_BF16 = 0, E_BF16_BIAS3 = 1, E_F32_RESID = 2, E_GELU = 3, E_F32_ACC = 5, E_F32_STORE = 7,
-             E_GELU_ERF = 8 };
+enum : int { E_BF16 = 0, E_BF16_BIAS3 = 1, E_F32_RESID = 2, E_GELU = 3, E_DGELU = 4, E_F32_ACC = 5,
+             E_F32_STORE = 7, E_GELU_ERF = 8 };
 
 struct G2Args {
   const __bf16* A;
@@ -46,6 +49,7 @@ struct G2Args {
   long lda, ldb, ldc, ldc2, ldr;
   int M, N, K, bias_cols;
   int k_per_split;  // split-K: blockIdx.y owns [y * k_per_split, (y + 1) * k_per_split); partials added atomically
+  float* csum;      // E_DGELU: optional column sums of the stored output (the MLP input-bias gradient), += atomically
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -61,7 +65,8 @@ __device__ __forceinline__ void glds16(const __bf16* g, char* lds_wave_base) {
 template <int R>
 __device__ __forceinline__ int kmaj_swz(int kr) {
   if constexpr (R == 128) return (kr & 3) | (((kr >> 3) & 1) << 2);  // 8 blocks per 256-B k-row
-  else return ((kr >> 1) & 1) | (((kr >> 3) & 1) << 1);              // R == 64: 4 blocks per 128-B k-row
+  else if constexpr (R == 64) return ((kr >> 1) & 1) | (((kr >> 3) & 1) << 1);  // 4 blocks per 128-B k-row
+  else return (kr >> 3) & 1;  // R == 32: 2 blocks per 64-B k-row; k-rows 8g+q of one read -> 2 per bank slot
 }
 
 // Stage one operand tile (R rows of the output dimension x 64 k) into its LDS image with LDS-DMA.  The per-lane
@@ -122,12 +127,20 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
 }
 
 // Wide k-major operands (R > 128 columns, e.g. the 192-column B tile) are staged as R/64 independent 64-column
-// panels, each its own [64][64] swizzled image (the k-major image layout above needs R/8 | 64).
+// panels, each its own [64][64] swizzled image (the k-major image layout above needs R/8 | 64); a k-major operand
+// whose width is an odd multiple of 32 (the 96-column tiles) as R/32 panels of [64][32].
+template <bool KMAJ, int R>
+struct Panels {
+  static constexpr bool ON = KMAJ && (R > 128 || R % 64 != 0);
+  static constexpr int PR = !ON ? R : (R % 64 == 0 ? 64 : 32);  // columns per panel
+  static constexpr int NP = R / PR;
+};
+
 template <bool KMAJ, int R, int NW = 4>
 struct OperandStager {
-  static constexpr bool PANELS = KMAJ && R > 128;
-  static constexpr int NP = PANELS ? R / 64 : 1;
-  static constexpr int PR = PANELS ? 64 : R;             // columns per panel
+  static constexpr bool PANELS = Panels<KMAJ, R>::ON;
+  static constexpr int NP = Panels<KMAJ, R>::NP;
+  static constexpr int PR = Panels<KMAJ, R>::PR;        // columns per panel
   static constexpr int N = NP * Stager<KMAJ, PR, NW>::N;  // LDS-DMA instructions per wave per K-tile
   Stager<KMAJ, PR, NW> st[NP];
 
@@ -169,9 +182,9 @@ __device__ __forceinline__ void frag_issue(const char* img, int row0, int kbase,
 // fragment of rows/columns [row0, row0 + 16) of an operand tile staged by OperandStager<KMAJ, R>
 template <bool KMAJ, int R>
 __device__ __forceinline__ void frag_issue_t(const char* img, int row0, int kbase, int lane, RawFrag<KMAJ>& f) {
-  using OS = OperandStager<KMAJ, R>;
-  if constexpr (OS::PANELS) {
-    frag_issue<KMAJ, 64>(img + (row0 / 64) * 64 * 64 * 2, row0 % 64, kbase, lane, f);
+  using PN = Panels<KMAJ, R>;
+  if constexpr (PN::ON) {
+    frag_issue<KMAJ, PN::PR>(img + (row0 / PN::PR) * PN::PR * 64 * 2, row0 % PN::PR, kbase, lane, f);
   } else {
     frag_issue<KMAJ, R>(img, row0, kbase, lane, f);
   }
@@ -206,10 +219,11 @@ __device__ __forceinline__ void grouped_tile(int t, int tiles_m, int tiles_n, in
   tn = r / gsize;
 }
 
-__device__ __forceinline__ float gelu_new_dev(float x) {
-  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-  const float t = 1.f - 2.f * __frcp_rn(__expf(2.f * u) + 1.f);
-  return 0.5f * x * (1.f + t);
+__device__ __forceinline__ float gelu_new_dev(float x) { return gelu_new_f(x); }
+
+__device__ __forceinline__ void add8v(float* v, const float4 x, const float4 y) {
+  v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
+  v[4] += y.x; v[5] += y.y; v[6] += y.z; v[7] += y.w;
 }
 
 __device__ __forceinline__ void add8(float* v, const float* b) {
@@ -372,7 +386,33 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
   // ---------------------------------------------------------------- epilogue via LDS (ECH row chunks)
   float* E = (float*)smem;
   constexpr int ER = BM / ECH;  // rows per chunk: wave rows [ch * WMR / ECH, (ch + 1) * WMR / ECH)
+  constexpr int CPR = BN / 8;                      // 8-column chunks per row
+  constexpr int ITEMS = (ER * CPR + NT - 1) / NT;  // chunks per thread per row chunk
+  // the epilogue's streamed global operand (residual, accumulator, saved pre-activation) is loaded for all of a
+  // thread's items up front, before the LDS tile is complete: ITEMS loads in flight instead of one per round trip
+  constexpr bool PF32 = EPI == E_F32_RESID || EPI == E_F32_ACC;
+  constexpr bool PF16 = EPI == E_DGELU;
   for (int ch = 0; ch < ECH; ++ch) {
+  float4 pf[PF32 ? 2 * ITEMS : 1];
+  bf16x8 pb[PF16 ? ITEMS : 1];
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int id = tid + k * NT;
+    if (id < ER * CPR) {
+      const int row = m0 + ch * ER + id / CPR, col = n0 + (id % CPR) * 8;
+      if constexpr (EPI == E_F32_RESID) {
+        const float* src = p.resid + (long)row * p.ldr + col;
+        pf[2 * k] = *(const float4*)src;
+        pf[2 * k + 1] = *(const float4*)(src + 4);
+      } else if constexpr (EPI == E_F32_ACC) {
+        const float* src = (const float*)p.C + (long)row * p.ldc + col;
+        pf[2 * k] = *(const float4*)src;
+        pf[2 * k + 1] = *(const float4*)(src + 4);
+      } else if constexpr (PF16) {
+        pb[k] = *(const bf16x8*)((const __bf16*)p.C2 + (long)row * p.ldc2 + col);
+      }
+    }
+  }
   __syncthreads();  // staging buffers / the previous chunk are done before the LDS is (re)written
   if (wm / (WMR / ECH) == ch) {
 #pragma unroll
@@ -386,9 +426,10 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
       }
   }
   __syncthreads();
-  constexpr int CPR = BN / 8;  // 8-column chunks per row
-#pragma unroll 2
-  for (int id = tid; id < ER * CPR; id += NT) {
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int id = tid + k * NT;
+    if (id >= ER * CPR) break;
     const int lr = id / CPR, lc = (id % CPR) * 8;
     const int row = m0 + ch * ER + lr, col = n0 + lc;
     float v[8];
@@ -406,7 +447,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
       store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v);
     } else if constexpr (EPI == E_F32_RESID) {
       if (p.bias0) add8(v, p.bias0 + col);
-      add8(v, p.resid + (long)row * p.ldr + col);
+      add8v(v, pf[2 * k], pf[2 * k + 1]);
       store8_f32((float*)p.C + (long)row * p.ldc + col, v);
     } else if constexpr (EPI == E_GELU || EPI == E_GELU_ERF) {
       if (p.bias0) add8(v, p.bias0 + col);
@@ -418,13 +459,38 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
         g[e] = EPI == E_GELU ? gelu_new_dev(x) : gelu_erf_f(x);
       }
       store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, g);
+    } else if constexpr (EPI == E_DGELU) {
+      const bf16x8 pr = pb[k];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(v[e] * gelu_new_grad_f(bf2f(pr[e]))));  // the stored value
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v);
+      if (p.csum) {  // this thread's own chunk of E: no other thread touches it before the barrier below
+        *(float4*)(E + lr * EPS + lc) = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)(E + lr * EPS + lc + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
     } else if constexpr (EPI == E_F32_ACC) {
       float* dst = (float*)p.C + (long)row * p.ldc + col;
-      add8(v, dst);
+      add8v(v, pf[2 * k], pf[2 * k + 1]);
       store8_f32(dst, v);
     } else {  // E_F32_STORE
       if (p.bias0) add8(v, p.bias0 + col);
       store8_f32((float*)p.C + (long)row * p.ldc + col, v);
+    }
+  }
+  if constexpr (EPI == E_DGELU) {
+    if (p.csum) {  // column sums of this chunk's ER rows: G row groups per column, one atomic each
+      __syncthreads();
+      constexpr int G = NT / BN > 0 ? NT / BN : 1;
+      for (int c = tid; c < BN * G; c += NT) {
+        const int col = c % BN, g = c / BN;
+        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent chains: the LDS reads pipeline
+#pragma unroll
+        for (int r0 = g; r0 < ER; r0 += 8 * G)
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (r0 + u * G < ER) s[u] += E[(r0 + u * G) * EPS + col];
+        atomicAdd(p.csum + n0 + col, ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7])));
+      }
     }
   }
   }  // chunk
@@ -450,15 +516,18 @@ hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
     case 5: return launch<256, 192, 2, AKM, BKM, EPI, 8>(a, s);
     case 6: return launch<128, 128, 4, AKM, BKM, EPI, 8>(a, s);  // two waves per SIMD (32 x 64 each)
     case 7: return launch<256, 128, 2, AKM, BKM, EPI, 8>(a, s);
+    // 96 x 96: the [768][3072] / [3072][768] weight gradients are exactly 256 tiles (one per CU) where 128 x 128
+    // leaves 112 CUs idle; 2 x 2 waves of 48 x 48 (3 x 3 MFMA blocks)
+    case 8: return launch<96, 96, 4, AKM, BKM, EPI>(a, s);
     default: return launch<128, 128, 4, AKM, BKM, EPI>(a, s);
   }
 }
 
 }  // namespace
 
-#define IIT_GLDS_TILES 8
-static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256};
-static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128};
+#define IIT_GLDS_TILES 9
+static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256, 96};
+static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128, 96};
 
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,
@@ -469,9 +538,10 @@ IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, con
   if (!(mode == 0 || mode == 2 || mode == 3)) return 0;
   const bool epi_ok = mode == 3 ? (epi == E_F32_ACC || epi == E_F32_STORE)
                                 : (epi == E_BF16 || epi == E_BF16_BIAS3 || epi == E_F32_RESID || epi == E_GELU ||
-                                   epi == E_GELU_ERF || epi == E_F32_ACC || epi == E_F32_STORE);
+                                   epi == E_GELU_ERF || epi == E_F32_ACC || epi == E_F32_STORE || epi == E_DGELU);
   if (!epi_ok) return 0;
-  if (mode == 0 && !(epi == E_BF16 || epi == E_F32_ACC || epi == E_F32_STORE)) return 0;
+  if (mode == 0 && !(epi == E_BF16 || epi == E_F32_ACC || epi == E_F32_STORE || epi == E_DGELU)) return 0;
+  if (epi == E_DGELU && (mode != 0 || !C2)) return 0;
   if (M <= 0 || N <= 0 || K <= 0 || M % kTileBM[tile] || N % kTileBN[tile] || K % 64) return 0;
   if (lda % 8 || ldb % 8 || ldc % 8 || (C2 && ldc2 % 8) || (resid && ldr % 8)) return 0;
   const uintptr_t al = (uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)C2 | (uintptr_t)resid;
@@ -483,7 +553,7 @@ IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, con
 IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, const float* bias0, const float* bias1,
                              const float* bias2, const float* resid, long lda, long ldb, long ldc, long ldc2, long ldr,
                              int M, int N, int K, int mode, int epi, int bias_cols, int tile, int splits,
-                             void* stream) {
+                             float* csum, void* stream) {
   if (!iit_gemm_glds_ok(A, B, C, C2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits))
     return (int)hipErrorInvalidValue;
   G2Args a;
@@ -491,12 +561,14 @@ IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, co
   a.bias0 = bias0; a.bias1 = bias1; a.bias2 = bias2; a.resid = resid;
   a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldc2 = ldc2; a.ldr = ldr;
   a.M = M; a.N = N; a.K = K; a.bias_cols = bias_cols; a.k_per_split = K / splits;
+  a.csum = epi == E_DGELU ? csum : nullptr;
   hipStream_t s = (hipStream_t)stream;
 #define G2(MODE, AK, BK_, EPI) \
   if (mode == (MODE) && epi == (EPI)) return (int)launch_tile<AK, BK_, EPI>(a, tile, s);
   G2(0, false, false, E_BF16)
   G2(0, false, false, E_F32_ACC)
   G2(0, false, false, E_F32_STORE)
+  G2(0, false, false, E_DGELU)
   G2(2, false, true, E_BF16)
   G2(2, false, true, E_BF16_BIAS3)
   G2(2, false, true, E_F32_RESID)

@@ -389,6 +389,13 @@ class TransformerBlock(nn.Module):
         pre_lin_live = mlp.gated and run.live(mlp.hook_pre_linear)
         if spl is not None and not run.live(mlp.hook_pre) and not ln2_live and not pre_lin_live:
             post = run.site(mlp.hook_post, spl.src.to(ops.dtype), spliced=True)
+        elif (not mlp.gated and getattr(ops, "mlp_gelu_residual", None) is not None
+              and self.cfg.act_fn in ("gelu_new", "gelu_fast", "gelu_pytorch_tanh")
+              and not (ln2_live or run.live(mlp.hook_pre) or run.live(mlp.hook_post) or run.live(self.hook_mlp_out))):
+            # no MLP site observed: one fused op whose backward forms dpre in the dX GEMM epilogue
+            x, resid_mid = self._norm_fork(self.ln2, resid_mid, run)
+            resid_post = ops.mlp_gelu_residual(x, mlp.W_in, mlp.b_in, mlp.W_out, mlp.b_out, resid_mid)
+            return run.site(self.hook_resid_post, resid_post)
         else:
             x, resid_mid = self._norm_fork(self.ln2, resid_mid, run)
             pre_hook = (lambda t: run.site(mlp.hook_pre, t)) if run.live(mlp.hook_pre) else None

@@ -246,8 +246,23 @@ _BLAS16_EPIS = (K.EPI_F32_RESID, K.EPI_F32_ACC)
 
 
 def _candidates(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, bias2, resid, ldr, aux, ldc2,
-                bias_cols, qkv, splits, blas_bias, policy):
-    """name -> f(c, c2, c3) for every implementation that covers the problem."""
+                bias_cols, qkv, splits, blas_bias, policy, csum_box=None):
+    """name -> f(c, c2, c3) for every implementation that covers the problem.
+
+    ``csum_box`` ([fp32 tensor] or None): every candidate also adds the column sums of its (bf16) output into
+    ``csum_box[0]`` -- fused in the LDS-DMA kernel's DGELU epilogue, a column-sum pass after the others."""
+    calls = _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, bias2, resid, ldr, aux,
+                              ldc2, bias_cols, qkv, splits, blas_bias, policy, csum_box)
+    if csum_box is not None:
+        for name in list(calls):
+            if not name.startswith("glds"):
+                calls[name] = lambda c=C, c2=C2, c3=None, f=calls[name]: (  # noqa: E731
+                    f(c, c2, c3), K_.colsum_accum(c, ldc, csum_box[0], M, N))
+    return calls
+
+
+def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, bias2, resid, ldr, aux, ldc2,
+                      bias_cols, qkv, splits, blas_bias, policy, csum_box):
     hip_call = lambda c=C, c2=C2, c3=None: K_.gemm(  # noqa: E731
         A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=c2, C3=c3, bias0=bias0,
         bias1=bias1, bias2=bias2, resid=resid, ldr=ldr, aux=aux, ldc2=ldc2, bias_cols=bias_cols, qkv=qkv,
@@ -260,15 +275,18 @@ def _candidates(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, b
                                                      blas_bias)
     if policy in ("auto", "glds") and A.is_cuda:
         split_opts = (1, 2, 4) if epi == K_.EPI_F32_ACC and (M // 64) * (N // 64) < 1024 else (1,)
+        dg = epi == K_.EPI_DGELU  # the LDS-DMA kernel reads the pre-activation through its C2 operand
         for tile in K_.GLDS_TILES:
             for sp in split_opts:
-                if K_.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=C2,
-                                   resid=resid, ldc2=ldc2, ldr=ldr, bias_cols=bias_cols, tile=tile, splits=sp):
+                if K_.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi,
+                                   C2=aux if dg else C2, resid=resid, ldc2=ldc2, ldr=ldr, bias_cols=bias_cols,
+                                   tile=tile, splits=sp):
                     calls[f"glds{tile}" + (f"k{sp}" if sp > 1 else "")] = \
                         lambda c=C, c2=C2, c3=None, t=tile, sp=sp: K_.gemm_glds(  # noqa: E731
-                            A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=c2,
-                            bias0=bias0, bias1=bias1, bias2=bias2, resid=resid, ldc2=ldc2, ldr=ldr,
-                            bias_cols=bias_cols, tile=t, splits=sp)
+                            A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi,
+                            C2=aux if dg else c2, bias0=bias0, bias1=bias1, bias2=bias2, resid=resid, ldc2=ldc2,
+                            ldr=ldr, bias_cols=bias_cols, tile=t, splits=sp,
+                            csum=csum_box[0] if csum_box is not None else None)
     if epi in _BLAS16_EPIS:
         calls["blas16"] = lambda c=C, c2=C2, c3=None: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
                                                              bias0, resid, ldr)
@@ -277,7 +295,7 @@ def _candidates(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, b
 
 def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=None, bias0=None, bias1=None,
          bias2=None, resid=None, ldr=0, aux=None, ldc2=0, bias_cols=0, qkv=(0, 0, 0), splits=None, blas_bias=None,
-         fresh: bool = False):
+         fresh: bool = False, colsum=None):
     """``C = A @ B`` (+ epilogue) on the fastest measured implementation for this problem:
 
     * ``hip``    -- the hand-written MFMA kernel with the epilogue fused;
@@ -291,6 +309,8 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     (``z+`` candidates, the memset included in their time).
     ``blas_bias``: optional ready-made bf16 bias row (e.g. a view of the arena's bf16 mirror) for the
     library path, saving its per-call concatenate/cast.
+    ``colsum`` (``EPI_DGELU`` only): fp32 [N] that also receives the column sums of the bf16 output (the MLP
+    input-bias gradient), fused into the LDS-DMA kernel's epilogue or as a pass after the other candidates.
 
     Returns the name of the implementation that ran when the choice was measured (else None)."""
     Kd = K
@@ -299,9 +319,11 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         enable_tuned_library_gemms()
     policy = POLICY
     fresh = fresh and epi == K_.EPI_F32_STORE and bias0 is None
+    assert colsum is None or epi == K_.EPI_DGELU, "fused column sums need the DGELU epilogue"
+    box = [colsum] if colsum is not None else None
     args = (A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, bias2, resid, ldr, aux, ldc2, bias_cols,
             qkv, splits, blas_bias, policy)
-    calls = _candidates(*args)
+    calls = _candidates(*args, csum_box=box)
     hip_call = calls["hip"]
     if policy == "hip" or "blas" not in calls:
         return hip_call(C, C2, C3)
@@ -315,16 +337,23 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         return calls[glds[0] if glds else "hip"](C, C2, C3)
     if policy in calls:
         return calls[policy](C, C2, C3)
-    key = (M, N, Kd, mode, epi, bias0 is not None, fresh)
+    # the last key field marks the variant: a fresh store (EPI_F32_STORE) or fused column sums (EPI_DGELU)
+    key = (M, N, Kd, mode, epi, bias0 is not None, fresh or (colsum is not None))
     choice = DECISIONS.get(key)
     if choice is None:
         if torch.cuda.is_current_stream_capturing():
             return hip_call(C, C2, C3)
-        # time on scratch outputs so accumulate epilogues do not corrupt C
+        # time on scratch outputs so accumulate epilogues (and column sums) do not corrupt C
         sc = _scratch(C, M, max(ldc, N))
         sc2 = _scratch(C2, M, max(ldc2, N))
         sc3 = _scratch(C3, M, max(ldc, N))
-        times = {name: min(_time(lambda f=f: f(sc, sc2, sc3)) for _ in range(2)) for name, f in calls.items()}
+        if box is not None:
+            box[0] = torch.zeros_like(colsum)
+        try:
+            times = {name: min(_time(lambda f=f: f(sc, sc2, sc3)) for _ in range(2)) for name, f in calls.items()}
+        finally:
+            if box is not None:
+                box[0] = colsum
         best = min(times, key=times.get)
         choice = DECISIONS[key] = (best, times)
     calls[choice[0]](C, C2, C3)

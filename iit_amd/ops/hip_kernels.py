@@ -27,7 +27,7 @@ _LIB = None
 
 _SIGS = {
     "iit_gemm": [c_void_p] * 10 + [c_long] * 5 + [c_int] * 12 + [c_void_p],
-    "iit_gemm_glds": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p],
+    "iit_gemm_glds": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p, c_void_p],
     "iit_gemm_glds_ok": [c_void_p] * 5 + [c_long] * 5 + [c_int] * 8,
     "iit_embed_pos_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_embed_pos_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
@@ -155,7 +155,8 @@ def gemm(A, B, C, *, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, mode:
 
 GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 128),  # tile 4: 4 LDS stages
               5: (256, 192),  # tiles 5-7: 8 waves (two per SIMD); 5: 4 x 6 MFMA tiles per wave, 2 stages
-              6: (128, 128), 7: (256, 128)}
+              6: (128, 128), 7: (256, 128),
+              8: (96, 96)}  # 96 x 96: 256 tiles for the [768][3072] weight gradients
 
 
 def _gemm_bounds(what, A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode, qkv=(0, 0, 0)):
@@ -176,12 +177,16 @@ def gemm_glds_ok(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, resid=N
 
 
 def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None, bias1=None, bias2=None, resid=None,
-              ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1):
-    """C = A @ B (+ epilogue) on the LDS-DMA MFMA kernel; bf16 operands, M/N/K multiples of the tile."""
+              ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1, csum=None):
+    """C = A @ B (+ epilogue) on the LDS-DMA MFMA kernel; bf16 operands, M/N/K multiples of the tile.
+    ``EPI_DGELU`` (mode 0): ``C2`` is the saved bf16 pre-activation (row stride ``ldc2``); ``csum`` (fp32 [N],
+    optional) accumulates the column sums of the stored bf16 output."""
     if CHECK_BOUNDS:
         _gemm_bounds("iit_gemm_glds", A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode)
+        _bounds("iit_gemm_glds", ("csum", csum, 1, N, N))
     _check(lib().iit_gemm_glds(_p(A), _p(B), _p(C), _p(C2), _p(bias0), _p(bias1), _p(bias2), _p(resid), lda, ldb,
-                               ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits, _stream()), "iit_gemm_glds")
+                               ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits, _p(csum), _stream()),
+           "iit_gemm_glds")
 
 
 # ------------------------------------------------------------------------------ others

@@ -783,10 +783,81 @@ class MLPInFn(Function):
             if store:
                 _settle_claim(choice, W_in)
         gb = _grad_slot(b_in)
-        if gb is not None:
+        if gb is not None and not _bias_sum_done(gpre if gpost is None else None, b_in):
             K.colsum_accum(dpre, dm, gb, T, dm)
         _done(W_in, b_in)
         return dx.view(*lead, d), None, None, None, None
+
+
+def _bias_sum_done(g: Optional[torch.Tensor], b: Optional[torch.Tensor]) -> bool:
+    """Whether ``g``'s producer already added its column sums into ``b``'s gradient (MLPOutGeluFn's fused
+    epilogue); the tag is checked against the tensor's storage and version, like the bf16 twin."""
+    tag = getattr(g, "_iit_bias_sum", None) if g is not None else None
+    return tag is not None and b is not None and tag == (g.data_ptr(), g._version, id(b))
+
+
+class MLPOutGeluFn(Function):
+    """``resid + gelu_new(pre) @ W_out + b_out`` with the gradient taken w.r.t. ``pre`` (``post`` comes in as
+    data: ``post = gelu_new(pre)`` from :class:`MLPInFn`'s epilogue, the block's only use of it).
+
+    The backward's dX GEMM runs with the DGELU epilogue -- ``dpre = (g W_out^T) * gelu_new'(pre)`` in one pass --
+    and, on the LDS-DMA kernel, reduces dpre into the b_in gradient in the same epilogue (tagged on dpre so
+    MLPInFn skips its column sum).  Used only when neither ``hook_pre``, ``hook_post`` nor ``hook_mlp_out`` is
+    live, so ``pre`` has no other consumer whose gradient autograd could add to the tagged tensor."""
+
+    @staticmethod
+    def forward(ctx, pre, post, W, b, w, ldw, resid, b_in):
+        ctx.set_materialize_grads(False)
+        lead = post.shape[:-1]
+        Kd = post.shape[-1]
+        N = W.shape[-1]
+        x2 = _flat2(post)
+        T = x2.shape[0]
+        r2 = _flat2(resid.float().contiguous())
+        out = torch.empty(T, N, dtype=F32, device=post.device)
+        gemm(x2, w, out, M=T, N=N, K=Kd, lda=Kd, ldb=ldw, ldc=N, mode=K.MODE_BKM, epi=K.EPI_F32_RESID, bias0=b,
+             resid=r2, ldr=N)
+        ctx.save_for_backward(x2, _flat2(pre))
+        ctx.params = (W, b, b_in)
+        ctx.w = w
+        ctx.ldw = ldw
+        ctx.meta = (lead, Kd, N)
+        return out.view(*lead, N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        if gy is None:
+            return (None,) * 8
+        x2, pre2 = ctx.saved_tensors
+        W, b, b_in = ctx.params
+        lead, Kd, N = ctx.meta
+        T = x2.shape[0]
+        g16 = _bf16_of(gy)
+        g2 = _aligned_rows(g16, T, N)
+        ldg = g2.stride(0)
+        dpre = None
+        if ctx.needs_input_grad[0]:
+            dpre = torch.empty(T, Kd, dtype=BF16, device=g2.device)
+            gbi = _grad_slot(b_in)
+            gemm(g2, ctx.w, dpre, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ldw, ldc=Kd, mode=K.MODE_NN, epi=K.EPI_DGELU,
+                 aux=pre2, ldc2=pre2.stride(0), colsum=gbi)
+            dpre = dpre.view(*lead, Kd)
+            if gbi is not None:
+                dpre._iit_bias_sum = (dpre.data_ptr(), dpre._version, id(b_in))
+        store = _claim_store(W)
+        gW = W.grad if store else _grad_slot(W)
+        if gW is not None:
+            gW2 = gW.reshape(Kd, N) if gW.is_contiguous() else gW
+            assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
+            choice = gemm(x2, g2, gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0),
+                          mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+            if store:
+                _settle_claim(choice, W)
+        gb = _grad_slot(b)
+        if gb is not None:
+            K.colsum_accum(g2, ldg, gb, T, N)
+        _done(W, b)
+        return dpre, None, None, None, None, None, gy, None
 
 
 class CrossEntropyFn(Function):
@@ -926,6 +997,13 @@ class HipOps(TorchOps):
         if hook_pre is not None:
             pre = hook_pre(pre)
         return pre, act_fn(act)(pre)
+
+    def mlp_gelu_residual(self, x, W_in, b_in, W_out, b_out, resid):
+        """``resid + gelu_new(x W_in + b_in) W_out + b_out`` for a block whose MLP sites are all dead: the
+        backward forms dpre in the dX GEMM's epilogue (see :class:`MLPOutGeluFn`)."""
+        pre, post = MLPInFn.apply(x, W_in, b_in, self._L(W_in)["in"], False)
+        return MLPOutGeluFn.apply(pre, post.detach(), W_out, b_out, self._L(W_out)["out"], W_out.shape[1], resid,
+                                  b_in)
 
     def mlp_out(self, post, W_out, b_out):
         return LinearFn.apply(post, W_out, b_out, self._L(W_out)["out"], W_out.shape[1], None, "bf16")

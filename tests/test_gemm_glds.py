@@ -41,11 +41,11 @@ def _ops(K, mode, M, N, Kd, pad):
 CASES = [(0, 0), (0, 5), (0, 7), (2, 0), (2, 1), (2, 2), (2, 3), (2, 8), (2, 5), (2, 7), (3, 5), (3, 7)]
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("mode,epi", CASES)
 def test_glds_gemm_matches_fp32(K, mode, epi, tile):
     from iit_amd.ops.torch_ops import gelu_new
-    M, N, Kd, pad = 256, 384, 192, 8
+    M, N, Kd, pad = (288 if tile == 8 else 256), 384, 192, 8
     A, B, lda, ldb, a, b = _ops(K, mode, M, N, Kd, pad)
     ref = a @ b
     ldc = N + 8
@@ -104,6 +104,19 @@ def test_glds_split_k_accumulate(K, tile, splits):
     assert ((C - exp).norm() / exp.norm()).item() < 1e-2
 
 
+@pytest.mark.parametrize("epi", [5, 7])
+def test_glds_96_tile_weight_gradient_shape(K, epi):
+    """The 96 x 96 tile (k-major operands staged as three 32-column panels) on the GPT-2 W_in weight-gradient
+    shape it exists for: [768][3072] = 256 tiles, K = 4096 tokens."""
+    M, N, Kd = 768, 3072, 4096
+    A, B, lda, ldb, a, b = _ops(K, 3, M, N, Kd, 0)
+    C = torch.randn(M, N, device=dev)
+    exp = a @ b + (C if epi == K.EPI_F32_ACC else 0)
+    assert K.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=3, epi=epi, tile=8)
+    K.gemm_glds(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=3, epi=epi, tile=8)
+    assert ((C - exp).norm() / exp.norm()).item() < 1e-2
+
+
 def test_glds_rejects_unaligned_shapes(K):
     A = torch.zeros(100, 64, device=dev, dtype=torch.bfloat16)
     B = torch.zeros(64, 128, device=dev, dtype=torch.bfloat16)
@@ -146,3 +159,26 @@ def test_glds_wide_tile_multi_tile_grid(K, mode, epi):
     torch.cuda.synchronize()
     err = ((C.float() - exp).norm() / exp.norm()).item()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("policy", ["auto", "hip", "blas", "glds"])
+def test_dgelu_epilogue_with_fused_column_sums(K, policy, monkeypatch):
+    """dpre = (dY W^T) * gelu_new'(pre) (mode 0, DGELU epilogue) plus the column sums of the stored dpre into the
+    bias gradient, on every dispatcher path (fused in the LDS-DMA epilogue, a column-sum pass after the others)."""
+    from iit_amd.ops import gemm_dispatch as gd
+    from iit_amd.ops.torch_ops import gelu_new
+    monkeypatch.setattr(gd, "POLICY", policy)
+    M, N, Kd = 512, 384, 256
+    A, B, lda, ldb, a, b = _ops(K, 0, M, N, Kd, 0)
+    pre = torch.randn(M, N, device=dev).bfloat16()
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    cs = torch.randn(N, device=dev)
+    cs0 = cs.clone()
+    p = pre.float().requires_grad_()
+    (gp,) = torch.autograd.grad(gelu_new(p).sum(), p)
+    exp = (a @ b) * gp
+    gd.gemm(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=0, epi=K.EPI_DGELU, aux=pre, ldc2=N, colsum=cs)
+    torch.cuda.synchronize()
+    assert ((C.float() - exp).norm() / exp.norm()).item() < 1e-2
+    ds = cs - cs0
+    assert ((ds - C.float().sum(0)).norm() / C.float().sum(0).norm()).item() < 1e-3  # sums of the stored values
