@@ -19,6 +19,7 @@
 // with D = rowsum(dO o O) from a small prep kernel.  dK/dV workgroups own 64 keys of one KV head and loop over every
 // query head of its group (GQA needs no atomics); dQ workgroups own 64 queries.
 #include "common.h"
+#include <stdlib.h>
 
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4_t;
 
@@ -97,18 +98,26 @@ __device__ __forceinline__ void store4(__bf16* dst, const f32x4 v, float s) {
 }
 
 // ------------------------------------------------------------------------------------------------ forward
-template <int DH>
-__global__ __launch_bounds__(256) void fa_fwd_kernel(FaArgs a) {
+// Each wave owns QB blocks of 16 queries (QB * 64 queries per workgroup): every K / V fragment read from LDS feeds
+// QB MFMAs, halving (QB = 2) the LDS traffic per FLOP -- with one 16-query block per wave the kernel is LDS-bound
+// (16 x 64 x DH MACs per 2 x 64 x DH x 2 bytes read).  Softmax runs in the log2 domain (scale * log2(e) folded
+// into one multiply, exp2 on the hardware v_exp_f32); the saved log-sum-exp is converted back to natural units.
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+template <int DH, int QB>
+__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FaArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 Ks[T64 * DH];
   __shared__ __attribute__((aligned(16))) __bf16 Vs[T64 * DH];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, g = l >> 4, c = l & 15;
   const int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int S = a.S;
-  const int q0 = qblk * T64 + 16 * wave, qi = q0 + c;
+  constexpr int QW = T64 * QB;  // queries per workgroup
+  const int q0 = qblk * QW + 16 * QB * wave;  // this wave's first query; block j covers q0 + 16 j + [0, 16)
   if ((a.head_mask >> h) & 1ull) {  // spliced head: z := src, lse unused by the backward (zero gradients)
     constexpr int CPR = DH / 8;
-    for (int i = tid; i < T64 * CPR; i += 256) {
-      const int r = qblk * T64 + i / CPR, ch = i % CPR;
+    for (int i = tid; i < QW * CPR; i += 256) {
+      const int r = qblk * QW + i / CPR, ch = i % CPR;
       if (r < S)
         *(uint4*)(a.z + b * a.zb + (long)r * a.zs + h * a.zh + ch * 8) =
             *(const uint4*)(a.src + b * a.sb + (long)r * a.ss + h * a.sh + ch * 8);
@@ -118,66 +127,100 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(FaArgs a) {
   const int hk = h / (a.Hq / a.Hkv);
   const __bf16* kbase = a.k + b * a.kb + hk * a.kh;
   const __bf16* vbase = a.v + b * a.vb + hk * a.vh;
-  bf16x8 qf[DH / 32];
+  const float sl2 = a.scale * kLog2e;
+  bf16x8 qf[QB][DH / 32];
+  f32x4 o[QB][DH / 16];
+  float m[QB], lsum[QB];  // running max (log2 units) of column qi; this lane's partial sum
 #pragma unroll
-  for (int s = 0; s < DH / 32; ++s)
-    qf[s] = gload8(a.q + b * a.qb + (long)qi * a.qs + h * a.qh + 32 * s + 8 * g, qi < S);
-  f32x4 o[DH / 16];
+  for (int j = 0; j < QB; ++j) {
+    const int qi = q0 + 16 * j + c;
 #pragma unroll
-  for (int t = 0; t < DH / 16; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, lsum = 0.f;  // running max (scaled units) of column qi; this lane's partial sum
-  const int kend = a.causal ? min(S, (qblk + 1) * T64) : S;
+    for (int s = 0; s < DH / 32; ++s)
+      qf[j][s] = gload8(a.q + b * a.qb + (long)qi * a.qs + h * a.qh + 32 * s + 8 * g, qi < S);
+#pragma unroll
+    for (int t = 0; t < DH / 16; ++t) o[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m[j] = -INFINITY;
+    lsum[j] = 0.f;
+  }
+  const int kend = a.causal ? min(S, (qblk + 1) * QW) : S;
   for (int k0 = 0; k0 < kend; k0 += T64) {
     __syncthreads();
     load_tile<DH>(Ks, kbase, a.ks, k0, S, tid);
     load_tile<DH>(Vs, vbase, a.vs, k0, S, tid);
     __syncthreads();
-    float p[4][4];
-    float mb = -INFINITY;
+    if (a.causal && k0 > q0 + 16 * QB - 1) continue;  // every key of this tile is after this wave's queries
+    float p[QB][4][4];
+    float mb[QB];
+#pragma unroll
+    for (int j = 0; j < QB; ++j) mb[j] = -INFINITY;
 #pragma unroll
     for (int kb4 = 0; kb4 < 4; ++kb4) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      f32x4 acc[QB];
 #pragma unroll
-      for (int s = 0; s < DH / 32; ++s) acc = mfma(frag_rows<DH>(Ks, 16 * kb4, 32 * s, l), qf[s], acc);
+      for (int j = 0; j < QB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kj = k0 + 16 * kb4 + 4 * g + r;
-        const bool ok = kj < S && (!a.causal || kj <= qi);
-        p[kb4][r] = ok ? acc[r] * a.scale : -INFINITY;
-        mb = fmaxf(mb, p[kb4][r]);
+      for (int s = 0; s < DH / 32; ++s) {
+        const bf16x8 kf = frag_rows<DH>(Ks, 16 * kb4, 32 * s, l);
+#pragma unroll
+        for (int j = 0; j < QB; ++j) acc[j] = mfma(kf, qf[j][s], acc[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < QB; ++j) {
+        const int qi = q0 + 16 * j + c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kj = k0 + 16 * kb4 + 4 * g + r;
+          const bool ok = kj < S && (!a.causal || kj <= qi);
+          p[j][kb4][r] = ok ? acc[j][r] * sl2 : -INFINITY;
+          mb[j] = fmaxf(mb[j], p[j][kb4][r]);
+        }
       }
     }
-    mb = fmaxf(mb, __shfl_xor(mb, 16, 64));
-    mb = fmaxf(mb, __shfl_xor(mb, 32, 64));
-    const float mn = fmaxf(m, mb);
-    const float alpha = mn == -INFINITY ? 1.f : __expf(m - mn);
-    m = mn;
-    lsum *= alpha;
 #pragma unroll
-    for (int t = 0; t < DH / 16; ++t) o[t] *= alpha;
+    for (int j = 0; j < QB; ++j) {
+      mb[j] = fmaxf(mb[j], __shfl_xor(mb[j], 16, 64));
+      mb[j] = fmaxf(mb[j], __shfl_xor(mb[j], 32, 64));
+      const float mn = fmaxf(m[j], mb[j]);
+      const float alpha = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m[j] - mn);
+      m[j] = mn;
+      lsum[j] *= alpha;
 #pragma unroll
-    for (int kb4 = 0; kb4 < 4; ++kb4)
+      for (int t = 0; t < DH / 16; ++t) o[j][t] *= alpha;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = p[kb4][r] == -INFINITY ? 0.f : __expf(p[kb4][r] - mn);
-        p[kb4][r] = e;
-        lsum += e;
-      }
+      for (int kb4 = 0; kb4 < 4; ++kb4)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = p[j][kb4][r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(p[j][kb4][r] - mn);
+          p[j][kb4][r] = e;
+          lsum[j] += e;
+        }
+    }
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) {
-      const bf16x8 pb = pack_perm(p[2 * ch], p[2 * ch + 1]);
+      bf16x8 pb[QB];
 #pragma unroll
-      for (int t = 0; t < DH / 16; ++t) o[t] = mfma(frag_tr_perm<DH>(Vs, 32 * ch, 16 * t, l), pb, o[t]);
+      for (int j = 0; j < QB; ++j) pb[j] = pack_perm(p[j][2 * ch], p[j][2 * ch + 1]);
+#pragma unroll
+      for (int t = 0; t < DH / 16; ++t) {
+        const bf16x8 vf = frag_tr_perm<DH>(Vs, 32 * ch, 16 * t, l);
+#pragma unroll
+        for (int j = 0; j < QB; ++j) o[j][t] = mfma(vf, pb[j], o[j][t]);
+      }
     }
   }
-  lsum += __shfl_xor(lsum, 16, 64);
-  lsum += __shfl_xor(lsum, 32, 64);
-  if (qi < S) {
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-    __bf16* zr = a.z + b * a.zb + (long)qi * a.zs + h * a.zh;
 #pragma unroll
-    for (int t = 0; t < DH / 16; ++t) store4(zr + 16 * t + 4 * g, o[t], inv);
-    if (g == 0 && a.lse) a.lse[((long)b * a.Hq + h) * S + qi] = m + __logf(lsum);
+  for (int j = 0; j < QB; ++j) {
+    float ls = lsum[j];
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    const int qi = q0 + 16 * j + c;
+    if (qi < S) {
+      const float inv = ls > 0.f ? 1.f / ls : 0.f;
+      __bf16* zr = a.z + b * a.zb + (long)qi * a.zs + h * a.zh;
+#pragma unroll
+      for (int t = 0; t < DH / 16; ++t) store4(zr + 16 * t + 4 * g, o[j][t], inv);
+      if (g == 0 && a.lse) a.lse[((long)b * a.Hq + h) * S + qi] = (m[j] + __log2f(ls)) * kLn2;
+    }
   }
 }
 
@@ -376,10 +419,20 @@ IIT_EXPORT int iit_flash_fwd(const void* q, const void* k, const void* v, const 
   a.head_mask = src ? head_mask : 0ull;
   a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.scale = scale;
   if (!args_ok(a, dh) || a.zs % 8 || a.zh % 8 || ((uintptr_t)z & 15)) return (int)hipErrorInvalidValue;
-  dim3 grid((S + T64 - 1) / T64, Hq, B);
+  // query blocks per wave: 2 halves the LDS traffic per FLOP but halves the workgroup count -- taken when that
+  // still leaves >= 2 workgroups per CU (IIT_FLASH_QB=1|2 forces a choice)
+  static const int qb_env = getenv("IIT_FLASH_QB") ? atoi(getenv("IIT_FLASH_QB")) : 0;
+  const long wg2 = (long)((S + 2 * T64 - 1) / (2 * T64)) * Hq * B;
+  const int QB = qb_env == 1 ? 1 : (qb_env == 2 ? 2 : (wg2 >= 512 ? 2 : 1));
+  dim3 grid((S + T64 * QB - 1) / (T64 * QB), Hq, B);
   hipStream_t s = (hipStream_t)stream;
-  if (dh == 64) hipLaunchKernelGGL(fa_fwd_kernel<64>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(fa_fwd_kernel<128>, grid, dim3(256), 0, s, a);
+  if (dh == 64) {
+    if (QB == 2) hipLaunchKernelGGL((fa_fwd_kernel<64, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((fa_fwd_kernel<64, 1>), grid, dim3(256), 0, s, a);
+  } else {
+    if (QB == 2) hipLaunchKernelGGL((fa_fwd_kernel<128, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((fa_fwd_kernel<128, 1>), grid, dim3(256), 0, s, a);
+  }
   return (int)hipGetLastError();
 }
 

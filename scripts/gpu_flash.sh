@@ -1,0 +1,11 @@
+# Flash-attention check on the GPU box: parity tests, then the microbenchmark with the automatic and the forced
+# query-block policies (IIT_FLASH_QB).
+set -u
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_flash_attn.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pt_flash.log 2>&1 || { tail -30 gpurun_out/pt_flash.log; exit 1; }
+tail -1 gpurun_out/pt_flash.log
+for qb in 0 1 2; do
+  IIT_FLASH_QB=$qb timeout -k 10 200 python scripts/bench_flash.py > gpurun_out/flash_qb$qb.txt 2>&1 || exit 3
+  echo "IIT_FLASH_QB=$qb"; cat gpurun_out/flash_qb$qb.txt
+done
