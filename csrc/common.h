@@ -28,16 +28,17 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp_f32 + one v_rcp_f32 instead of libm tanhf's ~40-instruction
+// tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp_f32 + one v_rcp_f32 (the raw 1-ulp reciprocal, not the IEEE
+// division sequence __frcp_rn compiles to) instead of libm tanhf's ~40-instruction
 // branchy sequence (which made the fused dgelu epilogue VALU-bound); saturates correctly at +-inf
-__device__ __forceinline__ float tanh_fast(float u) { return 1.f - 2.f * __frcp_rn(__expf(2.f * u) + 1.f); }
+__device__ __forceinline__ float tanh_fast(float u) { return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * u) + 1.f); }
 
 // gelu_new (tanh approximation, as TransformerLens / GPT-2) in its sigmoid form: 0.5 (1 + tanh(u)) = sigmoid(2u),
 // u = sqrt(2/pi) (x + 0.044715 x^3), with log2(e) folded into the constants -> one v_exp_f32 + one v_rcp_f32 and
 // a handful of FMAs per element (the GEMM epilogues that apply it are VALU-bound)
 __device__ __forceinline__ float gelu_sig2u(float x, float x2) {  // sigmoid(2u)
   const float m = x * __builtin_fmaf(0.10294324f, x2, 2.3022082f);  // 2u * log2(e)
-  return __frcp_rn(1.f + __builtin_amdgcn_exp2f(-m));
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-m));
 }
 __device__ __forceinline__ float gelu_new_f(float x) { return x * gelu_sig2u(x, x * x); }
 __device__ __forceinline__ float gelu_new_grad_f(float x) {

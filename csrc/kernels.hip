@@ -930,7 +930,7 @@ IIT_EXPORT int iit_colsum_accum(const void* x, int f32, long ld, float* out, int
 __device__ __forceinline__ float gelu_new_fast(float x) {
   // tanh(u) = 1 - 2 / (exp(2u) + 1): one exp + one fast reciprocal instead of libm tanhf
   const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-  const float t = 1.f - 2.f * __frcp_rn(__expf(2.f * u) + 1.f);
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * u) + 1.f);
   return 0.5f * x * (1.f + t);
 }
 

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void rotary_kernel(const __bf16* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------------------------ SwiGLU
-__device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
+__device__ __forceinline__ float silu_f(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const __bf16* __restrict__ gate, const __bf16* __restrict__ up,
                                                          __bf16* __restrict__ post, long n8) {
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const __bf16* __restric
   ld8(up + i * 8, false, u);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const float sg = 1.f / (1.f + __expf(-g[e]));
+    const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-g[e]));
     du[e] = dp[e] * g[e] * sg;
     dg[e] = dp[e] * u[e] * sg * (1.f + g[e] * (1.f - sg));
   }
