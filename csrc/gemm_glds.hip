@@ -519,15 +519,17 @@ hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
     // 96 x 96: the [768][3072] / [3072][768] weight gradients are exactly 256 tiles (one per CU) where 128 x 128
     // leaves 112 CUs idle; 2 x 2 waves of 48 x 48 (3 x 3 MFMA blocks)
     case 8: return launch<96, 96, 4, AKM, BKM, EPI>(a, s);
+    // 128 x 96: the 4096 x 768 outputs (W_O / W_out forward, dX of QKV / W_O / W_in) are exactly 256 tiles
+    case 9: return launch<128, 96, 4, AKM, BKM, EPI>(a, s);
     default: return launch<128, 128, 4, AKM, BKM, EPI>(a, s);
   }
 }
 
 }  // namespace
 
-#define IIT_GLDS_TILES 9
-static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256, 96};
-static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128, 96};
+#define IIT_GLDS_TILES 10
+static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256, 96, 128};
+static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128, 96, 96};
 
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,

@@ -156,7 +156,8 @@ def gemm(A, B, C, *, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, mode:
 GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 128),  # tile 4: 4 LDS stages
               5: (256, 192),  # tiles 5-7: 8 waves (two per SIMD); 5: 4 x 6 MFMA tiles per wave, 2 stages
               6: (128, 128), 7: (256, 128),
-              8: (96, 96)}  # 96 x 96: 256 tiles for the [768][3072] weight gradients
+              8: (96, 96),  # 96 x 96: 256 tiles for the [768][3072] weight gradients
+              9: (128, 96)}  # 128 x 96: 256 tiles for the [4096][768] outputs
 
 
 def _gemm_bounds(what, A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode, qkv=(0, 0, 0)):

@@ -24,7 +24,7 @@ SHAPES = [  # (name, M, N, K, mode, epi)
 def run():
     dev = "cuda"
     print(f"{'shape':18s} {'M':>5s} {'N':>5s} {'K':>5s}  " + "  ".join(f"{c:>8s}" for c in
-          ["128x128s3", "128x64s4", "64x128s4", "64x64s4", "128x128s4", "256x192w8", "128x128w8", "256x128w8", "96x96s4", "hip_old", "blas"]) + "   best TF/s")
+          ["128x128s3", "128x64s4", "64x128s4", "64x64s4", "128x128s4", "256x192w8", "128x128w8", "256x128w8", "96x96s4", "128x96s4", "hip_old", "blas"]) + "   best TF/s")
     for name, M, N, Kd, mode, epi in SHAPES:
         torch.manual_seed(0)
         A = (torch.randn(Kd, M) if mode & 1 else torch.randn(M, Kd)).to(dev).bfloat16()
@@ -46,7 +46,7 @@ def run():
         elif epi == 3:
             extra = dict(bias0=bias, C2=C2, ldc2=N)
         res = []
-        for tile in range(9):
+        for tile in range(10):
             if K.gemm_glds_ok(A, B, C, C2=C2, resid=R, ldc2=N if C2 is not None else 0, ldr=N if R is not None else 0,
                               bias_cols=extra.get("bias_cols", 0), tile=tile, **{k: kw[k] for k in kw}):
                 res.append(gd._time(lambda t=tile: K.gemm_glds(A, B, C, tile=t, **kw, **extra), reps=20))

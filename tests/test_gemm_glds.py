@@ -41,7 +41,7 @@ def _ops(K, mode, M, N, Kd, pad):
 CASES = [(0, 0), (0, 5), (0, 7), (2, 0), (2, 1), (2, 2), (2, 3), (2, 8), (2, 5), (2, 7), (3, 5), (3, 7)]
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("mode,epi", CASES)
 def test_glds_gemm_matches_fp32(K, mode, epi, tile):
     from iit_amd.ops.torch_ops import gelu_new
