@@ -246,25 +246,32 @@ __global__ __launch_bounds__(256) void fa_bwd_prep_kernel(FaArgs a) {
   a.dd[row] = acc;
 }
 
-template <int DH>
-__global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(FaArgs a) {
+// dK / dV: each wave owns NB blocks of 16 keys, so every Q / dO fragment read from LDS feeds NB MFMAs (NB = 2 halves
+// the LDS traffic per FLOP, as in the forward).
+template <int DH, int NB>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(FaArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 Qs[T64 * DH];
   __shared__ __attribute__((aligned(16))) __bf16 Gs[T64 * DH];
   __shared__ float Ls[T64], Ds[T64];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, g = l >> 4, c = l & 15;
   const int kblk = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int S = a.S, rep = a.Hq / a.Hkv;
-  const int kj = kblk * T64 + 16 * wave + c;  // this lane's key (B-operand / C column)
-  bf16x8 kf[DH / 32], vf[DH / 32];
+  constexpr int KW = T64 * NB;  // keys per workgroup
+  const int k0 = kblk * KW + 16 * NB * wave;  // this wave's first key; block j covers k0 + 16 j + [0, 16)
+  bf16x8 kf[NB][DH / 32], vf[NB][DH / 32];
+  f32x4 dk[NB][DH / 16], dv[NB][DH / 16];
 #pragma unroll
-  for (int s = 0; s < DH / 32; ++s) {
-    kf[s] = gload8(a.k + b * a.kb + (long)kj * a.ks + hk * a.kh + 32 * s + 8 * g, kj < S);
-    vf[s] = gload8(a.v + b * a.vb + (long)kj * a.vs + hk * a.vh + 32 * s + 8 * g, kj < S);
+  for (int j = 0; j < NB; ++j) {
+    const int kj = k0 + 16 * j + c;  // this lane's key (B-operand / C column)
+#pragma unroll
+    for (int s = 0; s < DH / 32; ++s) {
+      kf[j][s] = gload8(a.k + b * a.kb + (long)kj * a.ks + hk * a.kh + 32 * s + 8 * g, kj < S);
+      vf[j][s] = gload8(a.v + b * a.vb + (long)kj * a.vs + hk * a.vh + 32 * s + 8 * g, kj < S);
+    }
+#pragma unroll
+    for (int t = 0; t < DH / 16; ++t) dk[j][t] = dv[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  f32x4 dk[DH / 16], dv[DH / 16];
-#pragma unroll
-  for (int t = 0; t < DH / 16; ++t) dk[t] = dv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int qbeg = a.causal ? kblk * T64 : 0;
+  const int qbeg = a.causal ? kblk * KW : 0;
   for (int hh = 0; hh < rep; ++hh) {
     const int h = hk * rep + hh;
     if ((a.head_mask >> h) & 1ull) continue;  // spliced head: constant z, no gradient
@@ -281,111 +288,167 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(FaArgs a) {
         Ds[tid] = i0 + tid < S ? D[i0 + tid] : 0.f;
       }
       __syncthreads();
-      float P[4][4], dS[4][4];
+      if (a.causal && i0 + T64 - 1 < k0) continue;  // every query of this tile precedes this wave's keys
+      float P[NB][4][4], dS[NB][4][4];
 #pragma unroll
       for (int qm = 0; qm < 4; ++qm) {
-        f32x4 sa = {0.f, 0.f, 0.f, 0.f}, pa = sa;
+        f32x4 sa[NB], pa[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) sa[j] = pa[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < DH / 32; ++s) {
-          sa = mfma(frag_rows<DH>(Qs, 16 * qm, 32 * s, l), kf[s], sa);  // S[q][key]
-          pa = mfma(frag_rows<DH>(Gs, 16 * qm, 32 * s, l), vf[s], pa);  // dP[q][key]
+          const bf16x8 qfr = frag_rows<DH>(Qs, 16 * qm, 32 * s, l), gfr = frag_rows<DH>(Gs, 16 * qm, 32 * s, l);
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            sa[j] = mfma(qfr, kf[j][s], sa[j]);  // S[q][key]
+            pa[j] = mfma(gfr, vf[j][s], pa[j]);  // dP[q][key]
+          }
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int il = 16 * qm + 4 * g + r, i = i0 + il;
-          const bool ok = i < S && kj < S && (!a.causal || kj <= i);
-          const float pv = ok ? __expf(sa[r] * a.scale - Ls[il]) : 0.f;
-          P[qm][r] = pv;
-          dS[qm][r] = pv * (pa[r] - Ds[il]);
+        for (int j = 0; j < NB; ++j) {
+          const int kj = k0 + 16 * j + c;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int il = 16 * qm + 4 * g + r, i = i0 + il;
+            const bool ok = i < S && kj < S && (!a.causal || kj <= i);
+            const float pv = ok ? __expf(sa[j][r] * a.scale - Ls[il]) : 0.f;
+            P[j][qm][r] = pv;
+            dS[j][qm][r] = pv * (pa[j][r] - Ds[il]);
+          }
         }
       }
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch) {
-        const bf16x8 pb = pack_perm(P[2 * ch], P[2 * ch + 1]);
-        const bf16x8 sb = pack_perm(dS[2 * ch], dS[2 * ch + 1]);
+        bf16x8 pb[NB], sb[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          pb[j] = pack_perm(P[j][2 * ch], P[j][2 * ch + 1]);
+          sb[j] = pack_perm(dS[j][2 * ch], dS[j][2 * ch + 1]);
+        }
 #pragma unroll
         for (int t = 0; t < DH / 16; ++t) {
-          dv[t] = mfma(frag_tr_perm<DH>(Gs, 32 * ch, 16 * t, l), pb, dv[t]);  // dV^T[d][key] += dO^T P
-          dk[t] = mfma(frag_tr_perm<DH>(Qs, 32 * ch, 16 * t, l), sb, dk[t]);  // dK^T[d][key] += Q^T dS
+          const bf16x8 gtr = frag_tr_perm<DH>(Gs, 32 * ch, 16 * t, l), qtr = frag_tr_perm<DH>(Qs, 32 * ch, 16 * t, l);
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            dv[j][t] = mfma(gtr, pb[j], dv[j][t]);  // dV^T[d][key] += dO^T P
+            dk[j][t] = mfma(qtr, sb[j], dk[j][t]);  // dK^T[d][key] += Q^T dS
+          }
         }
       }
     }
   }
-  if (kj < S) {
-    __bf16* dkr = a.dk + b * a.gkb + (long)kj * a.gks + hk * a.gkh;
-    __bf16* dvr = a.dv + b * a.gvb + (long)kj * a.gvs + hk * a.gvh;
 #pragma unroll
-    for (int t = 0; t < DH / 16; ++t) {
-      store4(dkr + 16 * t + 4 * g, dk[t], a.scale);
-      store4(dvr + 16 * t + 4 * g, dv[t], 1.f);
+  for (int j = 0; j < NB; ++j) {
+    const int kj = k0 + 16 * j + c;
+    if (kj < S) {
+      __bf16* dkr = a.dk + b * a.gkb + (long)kj * a.gks + hk * a.gkh;
+      __bf16* dvr = a.dv + b * a.gvb + (long)kj * a.gvs + hk * a.gvh;
+#pragma unroll
+      for (int t = 0; t < DH / 16; ++t) {
+        store4(dkr + 16 * t + 4 * g, dk[j][t], a.scale);
+        store4(dvr + 16 * t + 4 * g, dv[j][t], 1.f);
+      }
     }
   }
 }
 
-template <int DH>
-__global__ __launch_bounds__(256) void fa_bwd_dq_kernel(FaArgs a) {
+// dQ: each wave owns NB blocks of 16 queries (K / V fragment reads shared by NB MFMAs).
+template <int DH, int NB>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(FaArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 Ks[T64 * DH];
   __shared__ __attribute__((aligned(16))) __bf16 Vs[T64 * DH];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, g = l >> 4, c = l & 15;
   const int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int S = a.S;
-  const int qi = qblk * T64 + 16 * wave + c;
-  __bf16* dqr = a.dq + b * a.gqb + (long)qi * a.gqs + h * a.gqh;
+  constexpr int QW = T64 * NB;
+  const int q0 = qblk * QW + 16 * NB * wave;
   if ((a.head_mask >> h) & 1ull) {
-    if (qi < S) {
 #pragma unroll
-      for (int t = 0; t < DH / 16; ++t) store4(dqr + 16 * t + 4 * g, f32x4{0.f, 0.f, 0.f, 0.f}, 1.f);
+    for (int j = 0; j < NB; ++j) {
+      const int qi = q0 + 16 * j + c;
+      if (qi < S) {
+        __bf16* dqr = a.dq + b * a.gqb + (long)qi * a.gqs + h * a.gqh;
+#pragma unroll
+        for (int t = 0; t < DH / 16; ++t) store4(dqr + 16 * t + 4 * g, f32x4{0.f, 0.f, 0.f, 0.f}, 1.f);
+      }
     }
     return;
   }
   const int hk = h / (a.Hq / a.Hkv);
   const __bf16* kbase = a.k + b * a.kb + hk * a.kh;
   const __bf16* vbase = a.v + b * a.vb + hk * a.vh;
-  bf16x8 qf[DH / 32], gf[DH / 32];
-#pragma unroll
-  for (int s = 0; s < DH / 32; ++s) {
-    qf[s] = gload8(a.q + b * a.qb + (long)qi * a.qs + h * a.qh + 32 * s + 8 * g, qi < S);
-    gf[s] = gload8(a.dz + b * a.db + (long)qi * a.ds + h * a.dh_ + 32 * s + 8 * g, qi < S);
-  }
   const long hrow = ((long)b * a.Hq + h) * S;
-  const float lse_q = qi < S ? a.lse[hrow + qi] : 0.f;
-  const float D_q = qi < S ? a.dd[hrow + qi] : 0.f;
-  f32x4 dq[DH / 16];
+  bf16x8 qf[NB][DH / 32], gf[NB][DH / 32];
+  float lse_q[NB], D_q[NB];
+  f32x4 dq[NB][DH / 16];
 #pragma unroll
-  for (int t = 0; t < DH / 16; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int kend = a.causal ? min(S, (qblk + 1) * T64) : S;
+  for (int j = 0; j < NB; ++j) {
+    const int qi = q0 + 16 * j + c;
+#pragma unroll
+    for (int s = 0; s < DH / 32; ++s) {
+      qf[j][s] = gload8(a.q + b * a.qb + (long)qi * a.qs + h * a.qh + 32 * s + 8 * g, qi < S);
+      gf[j][s] = gload8(a.dz + b * a.db + (long)qi * a.ds + h * a.dh_ + 32 * s + 8 * g, qi < S);
+    }
+    lse_q[j] = qi < S ? a.lse[hrow + qi] : 0.f;
+    D_q[j] = qi < S ? a.dd[hrow + qi] : 0.f;
+#pragma unroll
+    for (int t = 0; t < DH / 16; ++t) dq[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int kend = a.causal ? min(S, (qblk + 1) * QW) : S;
   for (int k0 = 0; k0 < kend; k0 += T64) {
     __syncthreads();
     load_tile<DH>(Ks, kbase, a.ks, k0, S, tid);
     load_tile<DH>(Vs, vbase, a.vs, k0, S, tid);
     __syncthreads();
-    float dS[4][4];
+    if (a.causal && k0 > q0 + 16 * NB - 1) continue;  // every key of this tile is after this wave's queries
+    float dS[NB][4][4];
 #pragma unroll
     for (int kb4 = 0; kb4 < 4; ++kb4) {
-      f32x4 sa = {0.f, 0.f, 0.f, 0.f}, pa = sa;
+      f32x4 sa[NB], pa[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) sa[j] = pa[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < DH / 32; ++s) {
-        sa = mfma(frag_rows<DH>(Ks, 16 * kb4, 32 * s, l), qf[s], sa);  // S^T[key][q]
-        pa = mfma(frag_rows<DH>(Vs, 16 * kb4, 32 * s, l), gf[s], pa);  // dP^T[key][q]
+        const bf16x8 kfr = frag_rows<DH>(Ks, 16 * kb4, 32 * s, l), vfr = frag_rows<DH>(Vs, 16 * kb4, 32 * s, l);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          sa[j] = mfma(kfr, qf[j][s], sa[j]);  // S^T[key][q]
+          pa[j] = mfma(vfr, gf[j][s], pa[j]);  // dP^T[key][q]
+        }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kj = k0 + 16 * kb4 + 4 * g + r;
-        const bool ok = qi < S && kj < S && (!a.causal || kj <= qi);
-        const float pv = ok ? __expf(sa[r] * a.scale - lse_q) : 0.f;
-        dS[kb4][r] = pv * (pa[r] - D_q);
+      for (int j = 0; j < NB; ++j) {
+        const int qi = q0 + 16 * j + c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kj = k0 + 16 * kb4 + 4 * g + r;
+          const bool ok = qi < S && kj < S && (!a.causal || kj <= qi);
+          const float pv = ok ? __expf(sa[j][r] * a.scale - lse_q[j]) : 0.f;
+          dS[j][kb4][r] = pv * (pa[j][r] - D_q[j]);
+        }
       }
     }
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) {
-      const bf16x8 sb = pack_perm(dS[2 * ch], dS[2 * ch + 1]);
+      bf16x8 sb[NB];
 #pragma unroll
-      for (int t = 0; t < DH / 16; ++t) dq[t] = mfma(frag_tr_perm<DH>(Ks, 32 * ch, 16 * t, l), sb, dq[t]);
+      for (int j = 0; j < NB; ++j) sb[j] = pack_perm(dS[j][2 * ch], dS[j][2 * ch + 1]);
+#pragma unroll
+      for (int t = 0; t < DH / 16; ++t) {
+        const bf16x8 ktr = frag_tr_perm<DH>(Ks, 32 * ch, 16 * t, l);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) dq[j][t] = mfma(ktr, sb[j], dq[j][t]);
+      }
     }
   }
-  if (qi < S) {
 #pragma unroll
-    for (int t = 0; t < DH / 16; ++t) store4(dqr + 16 * t + 4 * g, dq[t], a.scale);
+  for (int j = 0; j < NB; ++j) {
+    const int qi = q0 + 16 * j + c;
+    if (qi < S) {
+      __bf16* dqr = a.dq + b * a.gqb + (long)qi * a.gqs + h * a.gqh;
+#pragma unroll
+      for (int t = 0; t < DH / 16; ++t) store4(dqr + 16 * t + 4 * g, dq[j][t], a.scale);
+    }
   }
 }
 
@@ -463,15 +526,24 @@ IIT_EXPORT int iit_flash_bwd(const void* q, const void* k, const void* v, const 
   hipStream_t s = (hipStream_t)stream;
   const long rows = (long)B * Hq * S;
   dim3 gp((rows + 255) / 256);
-  dim3 gkv((S + T64 - 1) / T64, Hkv, B), gq((S + T64 - 1) / T64, Hq, B);
+  // blocks per wave as in the forward: 2 when the grid keeps >= 2 workgroups per CU (IIT_FLASH_QB forces);
+  // the dK/dV kernel keeps one block per wave at dh 128 (its accumulators would not fit two waves per SIMD)
+  static const int qb_env = getenv("IIT_FLASH_QB") ? atoi(getenv("IIT_FLASH_QB")) : 0;
+  const int tiles2 = (S + 2 * T64 - 1) / (2 * T64);
+  const int nbq = qb_env == 1 ? 1 : (qb_env == 2 ? 2 : ((long)tiles2 * Hq * B >= 512 ? 2 : 1));
+  const int nbk = dh == 128 ? 1 : (qb_env == 1 ? 1 : (qb_env == 2 ? 2 : ((long)tiles2 * Hkv * B >= 512 ? 2 : 1)));
+  dim3 gkv((S + T64 * nbk - 1) / (T64 * nbk), Hkv, B), gq((S + T64 * nbq - 1) / (T64 * nbq), Hq, B);
   if (dh == 64) {
     hipLaunchKernelGGL(fa_bwd_prep_kernel<64>, gp, dim3(256), 0, s, a);
-    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<64>, gkv, dim3(256), 0, s, a);
-    hipLaunchKernelGGL(fa_bwd_dq_kernel<64>, gq, dim3(256), 0, s, a);
+    if (nbk == 2) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<64, 2>), gkv, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((fa_bwd_dkdv_kernel<64, 1>), gkv, dim3(256), 0, s, a);
+    if (nbq == 2) hipLaunchKernelGGL((fa_bwd_dq_kernel<64, 2>), gq, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((fa_bwd_dq_kernel<64, 1>), gq, dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL(fa_bwd_prep_kernel<128>, gp, dim3(256), 0, s, a);
-    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<128>, gkv, dim3(256), 0, s, a);
-    hipLaunchKernelGGL(fa_bwd_dq_kernel<128>, gq, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, 1>), gkv, dim3(256), 0, s, a);
+    if (nbq == 2) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, 2>), gq, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((fa_bwd_dq_kernel<128, 1>), gq, dim3(256), 0, s, a);
   }
   return (int)hipGetLastError();
 }
