@@ -112,7 +112,7 @@ def main():
     distributed = pdist.init_distributed()
     rank, world = pdist.rank(), pdist.world_size()
     if torch.cuda.is_available():
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(pdist.local_device_index())
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
     pair, opt, loss_fn, it, step_fn, train_set, test_set = setup(args, dev)

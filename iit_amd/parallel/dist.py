@@ -38,6 +38,15 @@ def force_reducer() -> bool:
     return os.environ.get("IIT_DP_FORCE_REDUCER") == "1" and is_initialized()
 
 
+def local_device_index() -> int:
+    """GPU of this rank: ``LOCAL_RANK``, or 0 for every rank under ``IIT_REHEARSE_ONE_GPU=1`` -- the rehearsal of the
+    multi-rank data-parallel schedule on a one-GPU box (ranks share the card; pair it with
+    ``IIT_DIST_BACKEND=gloo``, since RCCL refuses two ranks on one device)."""
+    if os.environ.get("IIT_REHEARSE_ONE_GPU") == "1":
+        return 0
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> bool:
     """Initialise the default process group from torchrun env vars. Returns True if distributed."""
     if is_initialized():
@@ -48,9 +57,10 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> boo
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("IIT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_device_index())
     if backend == "nccl":
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
     return True

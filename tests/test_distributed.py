@@ -208,3 +208,13 @@ def test_grad_cut_backward_is_exact():
     st.release()
     for n, p in m.named_parameters():
         assert torch.allclose(p.grad, ref[n], atol=1e-6, rtol=1e-5), n
+
+
+def test_rehearsal_device_mapping(monkeypatch):
+    """IIT_REHEARSE_ONE_GPU maps every rank to cuda:0 (the one-GPU multi-rank rehearsal); otherwise LOCAL_RANK."""
+    from iit_amd.parallel import dist as pdist
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    monkeypatch.delenv("IIT_REHEARSE_ONE_GPU", raising=False)
+    assert pdist.local_device_index() == 3
+    monkeypatch.setenv("IIT_REHEARSE_ONE_GPU", "1")
+    assert pdist.local_device_index() == 0
