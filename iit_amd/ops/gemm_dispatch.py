@@ -153,9 +153,9 @@ def _blas(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, C2, C3, bias0, bias1, bia
         if blas_bias is not None:
             bias = blas_bias
         elif epi == K.EPI_BF16_BIAS3:
-            bias = torch.cat([bias0.reshape(-1), bias1.reshape(-1), bias2.reshape(-1)]).to(BF16)
+            bias = torch.cat([bias0.reshape(-1)[:N], bias1.reshape(-1), bias2.reshape(-1)]).to(BF16)
         else:
-            bias = None if bias0 is None else bias0.reshape(-1).to(BF16)
+            bias = None if bias0 is None else bias0.reshape(-1)[:N].to(BF16)
         if bias is None:
             torch.mm(a, b, out=c)
         else:
@@ -164,10 +164,10 @@ def _blas(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, C2, C3, bias0, bias1, bia
         c = _as(C, M, N, ldc)
         _addmm_f32(c, _as(resid, M, N, ldr), a, b)
         if bias0 is not None:
-            c.add_(bias0.reshape(-1))
+            c.add_(bias0.reshape(-1)[:N])
     elif epi in (K.EPI_GELU, K.EPI_GELU_ERF):
         pre = _as(C2, M, N, ldc2)
-        torch.addmm(bias0.reshape(-1).to(BF16), a, b, out=pre)
+        torch.addmm(bias0.reshape(-1)[:N].to(BF16), a, b, out=pre)
         _gelu_into(pre, _as(C, M, N, ldc), erf=epi == K.EPI_GELU_ERF)
     elif epi == K.EPI_DGELU:
         tmp = torch.mm(a, b)
@@ -178,7 +178,7 @@ def _blas(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, C2, C3, bias0, bias1, bia
     elif epi == K.EPI_F32_STORE:
         c = _as(C, M, N, ldc)
         if bias0 is not None:
-            _addmm_f32(c, bias0.reshape(-1).float(), a, b)
+            _addmm_f32(c, bias0.reshape(-1)[:N].float(), a, b)
         else:
             _mm_f32_into(c, a, b)
     else:
@@ -235,7 +235,7 @@ def _blas16(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, resid, ldr):
     (hipBLASLt's bf16-in/fp32-out kernels are markedly slower than its bf16-out ones on gfx950)."""
     a, b = _operands(A, B, M, N, Kd, lda, ldb, mode)
     y = torch.mm(a, b)
-    bias = None if bias0 is None else bias0.reshape(-1).float().contiguous()
+    bias = None if bias0 is None else bias0.reshape(-1)[:N].float().contiguous()
     if epi == K.EPI_F32_RESID:
         K.add_bf16(C, ldc, resid, ldr, y, N, bias, M, N)
     else:  # EPI_F32_ACC: C += y
@@ -274,7 +274,9 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
                                                      bias0, bias1, bias2, resid, ldr, aux, ldc2, bias_cols, qkv,
                                                      blas_bias)
     if policy in ("auto", "glds") and A.is_cuda:
-        split_opts = (1, 2, 4) if epi == K_.EPI_F32_ACC and (M // 64) * (N // 64) < 1024 else (1,)
+        split_opts = (1,)
+        if epi == K_.EPI_F32_ACC and (M // 64) * (N // 64) < 1024:
+            split_opts = (1, 2, 4, 8, 16) if (M // 64) * (N // 64) < 64 else (1, 2, 4)
         dg = epi == K_.EPI_DGELU  # the LDS-DMA kernel reads the pre-activation through its C2 operand
         for tile in K_.GLDS_TILES:
             for sp in split_opts:
@@ -293,9 +295,41 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
     return calls
 
 
+def _shift(t, off: int):
+    """1-D view of ``t``'s storage starting ``off`` elements after ``t``'s first element (operand sub-blocks for
+    the raw-pointer kernels; the library path re-strides it with ``_as``)."""
+    if t is None:
+        return None
+    n = t.untyped_storage().nbytes() // t.element_size() - t.storage_offset() - off
+    return torch.as_strided(t, (n,), (1,), t.storage_offset() + off)
+
+
+RAGGED = {}  # ragged problem key -> (split wins, whole time, [bulk time, tail time])
+
+
+def _ragged_split(A, B, C, *, M, N, K, lda, ldb, mode, epi, C2, bias0, resid, aux):
+    """Problem pieces ``[kwargs, ...]`` for a GEMM whose N (any column-wise epilogue) or K (fp32 accumulate) is
+    large but not tile-aligned: a bulk of N // 128 * 128 columns (resp. K // 1024 * 1024 reduction steps, so
+    split-K factors up to 16 divide it) plus the remainder.  None when the problem is aligned or small."""
+    if epi in (K_.EPI_BF16, K_.EPI_F32_STORE, K_.EPI_F32_ACC) and N >= 4096 and N % 128:
+        n0 = N // 128 * 128
+        boff = n0 if mode & K_.MODE_BKM else n0 * ldb
+        return [dict(A=A, B=B, C=C, M=M, N=n0, K=K, C2=C2, bias0=bias0, resid=resid, aux=aux),
+                dict(A=A, B=_shift(B, boff), C=_shift(C, n0), M=M, N=N - n0, K=K, C2=_shift(C2, n0),
+                     bias0=_shift(bias0, n0), resid=_shift(resid, n0), aux=_shift(aux, n0))]
+    if epi == K_.EPI_F32_ACC and K >= 16384 and K % 1024:
+        k0 = K // 1024 * 1024
+        aoff = k0 * lda if mode & K_.MODE_AKM else k0
+        boff = k0 * ldb if mode & K_.MODE_BKM else k0
+        return [dict(A=A, B=B, C=C, M=M, N=N, K=k0, C2=C2, bias0=bias0, resid=resid, aux=aux),
+                dict(A=_shift(A, aoff), B=_shift(B, boff), C=C, M=M, N=N, K=K - k0, C2=C2, bias0=None,
+                     resid=resid, aux=aux)]
+    return None
+
+
 def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=None, bias0=None, bias1=None,
          bias2=None, resid=None, ldr=0, aux=None, ldc2=0, bias_cols=0, qkv=(0, 0, 0), splits=None, blas_bias=None,
-         fresh: bool = False, colsum=None):
+         fresh: bool = False, colsum=None, _decide_only: bool = False, _no_split: bool = False):
     """``C = A @ B`` (+ epilogue) on the fastest measured implementation for this problem:
 
     * ``hip``    -- the hand-written MFMA kernel with the epilogue fused;
@@ -312,12 +346,41 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     ``colsum`` (``EPI_DGELU`` only): fp32 [N] that also receives the column sums of the bf16 output (the MLP
     input-bias gradient), fused into the LDS-DMA kernel's epilogue or as a pass after the other candidates.
 
+    Ragged problems (the vocabulary-sized unembed GEMMs: N or K = 50257) are split into a tile-aligned bulk, which
+    the LDS-DMA kernel can serve, and a narrow tail (see :func:`_ragged_split`).
+
     Returns the name of the implementation that ran when the choice was measured (else None)."""
     Kd = K
     if not _BLAS_SELECTED:
         select_graph_safe_blas()
         enable_tuned_library_gemms()
     policy = POLICY
+    if policy in ("auto", "glds") and A.is_cuda and qkv[0] == 0 and colsum is None and not _no_split:
+        parts = _ragged_split(A, B, C, M=M, N=N, K=K, lda=lda, ldb=ldb, mode=mode, epi=epi, C2=C2, bias0=bias0,
+                              resid=resid, aux=aux)
+        if parts is not None:
+            bulk, tail = parts
+
+            def run(kw, decide=False):
+                kw = dict(kw)
+                return gemm(kw.pop("A"), kw.pop("B"), kw.pop("C"), lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi,
+                            ldr=ldr, ldc2=ldc2, blas_bias=None, fresh=fresh, _decide_only=decide, **kw)
+
+            rkey = (M, N, K, mode, epi, bias0 is not None, fresh, "ragged")
+            split = RAGGED.get(rkey)
+            if split is None and not torch.cuda.is_current_stream_capturing():
+                # the split is one more candidate: bulk + tail against the whole problem, each at its best
+                whole = gemm(A, B, C, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=C2, C3=C3,
+                             bias0=bias0, bias1=bias1, bias2=bias2, resid=resid, ldr=ldr, aux=aux, ldc2=ldc2,
+                             bias_cols=bias_cols, qkv=qkv, splits=splits, blas_bias=blas_bias, fresh=fresh,
+                             _decide_only=True, _no_split=True)
+                pieces = [run(bulk, True), run(tail, True)]
+                split = RAGGED[rkey] = (None not in pieces and whole is not None and sum(pieces) < whole,
+                                        whole, pieces)
+            if split is not None and split[0]:
+                choice = run(bulk)
+                run(tail)
+                return choice
     fresh = fresh and epi == K_.EPI_F32_STORE and bias0 is None
     assert colsum is None or epi == K_.EPI_DGELU, "fused column sums need the DGELU epilogue"
     box = [colsum] if colsum is not None else None
@@ -325,6 +388,8 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
             qkv, splits, blas_bias, policy)
     calls = _candidates(*args, csum_box=box)
     hip_call = calls["hip"]
+    if _decide_only and (policy != "auto" or "blas" not in calls):
+        return None  # nothing to measure: a forced policy or a single candidate
     if policy == "hip" or "blas" not in calls:
         return hip_call(C, C2, C3)
     if fresh:
@@ -342,7 +407,7 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     choice = DECISIONS.get(key)
     if choice is None:
         if torch.cuda.is_current_stream_capturing():
-            return hip_call(C, C2, C3)
+            return None if _decide_only else hip_call(C, C2, C3)
         # time on scratch outputs so accumulate epilogues (and column sums) do not corrupt C
         sc = _scratch(C, M, max(ldc, N))
         sc2 = _scratch(C2, M, max(ldc2, N))
@@ -356,6 +421,8 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
                 box[0] = colsum
         best = min(times, key=times.get)
         choice = DECISIONS[key] = (best, times)
+    if _decide_only:  # the measured time of the best implementation; nothing runs on C
+        return choice[1][choice[0]]
     calls[choice[0]](C, C2, C3)
     return choice[0]
 
@@ -369,4 +436,7 @@ def report() -> str:
         ts = "  ".join(f"{k} {v:8.1f}us" for k, v in times.items())
         lines.append(f"M={M:6d} N={N:6d} K={Kd:6d} mode={mode:2d} epi={epi}{'f' if fresh else ''} bias={int(bias)} "
                      f"-> {c:6s} {ts}")
+    for (M, N, Kd, mode, epi, bias, fresh, _), (split, whole, pieces) in sorted(RAGGED.items()):
+        lines.append(f"M={M:6d} N={N:6d} K={Kd:6d} mode={mode:2d} epi={epi}{'f' if fresh else ''} bias={int(bias)} "
+                     f"-> {'bulk+tail' if split else 'whole'}  whole {whole}us  bulk+tail {pieces}us")
     return "\n".join(lines)

@@ -182,3 +182,40 @@ def test_dgelu_epilogue_with_fused_column_sums(K, policy, monkeypatch):
     assert ((C.float() - exp).norm() / exp.norm()).item() < 1e-2
     ds = cs - cs0
     assert ((ds - C.float().sum(0)).norm() / C.float().sum(0).norm()).item() < 1e-3  # sums of the stored values
+
+
+@pytest.mark.parametrize("case", ["fwd", "dx", "dw"])
+def test_ragged_vocab_gemms_split_bulk_and_tail(K, case):
+    """The unembed GEMMs (N or K = 50257) run as a tile-aligned bulk + a narrow tail; results match fp32."""
+    from iit_amd.ops import gemm_dispatch as gd
+    V, Vp, d, T = 50257, 50264, 768, 256
+    torch.manual_seed(0)
+    if case == "fwd":  # logits = x @ W_U + b_U (fp32 store, padded rows)
+        x = torch.randn(T, d, device=dev).bfloat16()
+        U = torch.zeros(d, Vp, device=dev, dtype=torch.bfloat16)
+        U[:, :V] = (torch.randn(d, V, device=dev) / 16).bfloat16()
+        b = torch.randn(V, device=dev)
+        C = torch.full((T, Vp), 7.0, device=dev)
+        gd.gemm(x, U, C, M=T, N=V, K=d, lda=d, ldb=Vp, ldc=Vp, mode=K.MODE_BKM, epi=K.EPI_F32_STORE, bias0=b)
+        exp = x.float() @ U[:, :V].float() + b
+        got = C[:, :V]
+        assert torch.all(C[:, V:] == 7.0)
+    elif case == "dx":  # dX += G @ W_U^T (K = vocab, fp32 accumulate)
+        G = torch.zeros(T, Vp, device=dev, dtype=torch.bfloat16)
+        G[:, :V] = (torch.randn(T, V, device=dev) / 64).bfloat16()
+        U = (torch.randn(d, Vp, device=dev) / 16).bfloat16()
+        C = torch.randn(T, d, device=dev)
+        exp = C + G[:, :V].float() @ U[:, :V].float().t()
+        gd.gemm(G, U, C, M=T, N=d, K=V, lda=Vp, ldb=Vp, ldc=d, mode=K.MODE_NN, epi=K.EPI_F32_ACC)
+        got = C
+    else:  # dW_U = x^T G (fp32 store into the padded gradient rows)
+        x = torch.randn(T, d, device=dev).bfloat16()
+        G = (torch.randn(T, Vp, device=dev) / 64).bfloat16()
+        C = torch.full((d, Vp), 7.0, device=dev)
+        gd.gemm(x, G, C, M=d, N=V, K=T, lda=d, ldb=Vp, ldc=Vp, mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE,
+                fresh=True)
+        exp = x.float().t() @ G[:, :V].float()
+        got = C[:, :V]
+        assert torch.all(C[:, V:] == 7.0)
+    torch.cuda.synchronize()
+    assert ((got - exp).norm() / exp.norm()).item() < 1e-2
