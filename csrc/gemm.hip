@@ -29,6 +29,7 @@ enum Epi : int {
   EPI_F32_ACC_QKV = 6,// head-blocked scatter-accumulate into 3 TL-layout grads
   EPI_F32_STORE = 7,  // C(f32) = acc (+bias)
   EPI_GELU_ERF = 8,   // as EPI_GELU with the exact (erf) GELU (BERT)
+  EPI_DGELU_ERF = 9,  // as EPI_DGELU with the exact (erf) GELU's derivative
 };
 
 struct GemmArgs {
@@ -243,9 +244,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
           if (p.bias0) v += p.bias0[col];
           ((__bf16*)p.C2)[(long)row * p.ldc2 + col] = f2bf(v);
           ((__bf16*)p.C)[(long)row * p.ldc + col] = f2bf(EPI == EPI_GELU ? gelu_new_f(v) : gelu_erf_f(v));
-        } else if (EPI == EPI_DGELU) {
+        } else if (EPI == EPI_DGELU || EPI == EPI_DGELU_ERF) {
           const float pre = bf2f(((const __bf16*)p.aux)[(long)row * p.ldc2 + col]);
-          ((__bf16*)p.C)[(long)row * p.ldc + col] = f2bf(v * gelu_new_grad_f(pre));
+          const float gp = EPI == EPI_DGELU ? gelu_new_grad_f(pre) : gelu_erf_grad_f(pre);
+          ((__bf16*)p.C)[(long)row * p.ldc + col] = f2bf(v * gp);
         } else if (EPI == EPI_F32_ACC) {
           float* dst = (float*)p.C + (long)row * p.ldc + col;
           if (p.atomic) atomicAdd(dst, v);
@@ -312,6 +314,7 @@ IIT_EXPORT int iit_gemm(const void* A, const void* B, void* C, void* C2, void* C
   IIT_GEMM_CASE(0, false, false, false, false, EPI_GELU)
   IIT_GEMM_CASE(0, false, false, false, false, EPI_GELU_ERF)
   IIT_GEMM_CASE(0, false, false, false, false, EPI_DGELU)
+  IIT_GEMM_CASE(0, false, false, false, false, EPI_DGELU_ERF)
   IIT_GEMM_CASE(0, false, false, false, false, EPI_F32_STORE)
   IIT_GEMM_CASE(0, false, false, false, false, EPI_F32_ACC)
   // forward GEMMs straight from TL-layout ([K][N]) bf16 weights: B k-major (tr16 reads)

@@ -35,7 +35,7 @@
 namespace {
 
 enum : int { E_BF16 = 0, E_BF16_BIAS3 = 1, E_F32_RESID = 2, E_GELU = 3, E_DGELU = 4, E_F32_ACC = 5,
-             E_F32_STORE = 7, E_GELU_ERF = 8 };
+             E_F32_STORE = 7, E_GELU_ERF = 8, E_DGELU_ERF = 9 };
 
 struct G2Args {
   const __bf16* A;
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
   // the epilogue's streamed global operand (residual, accumulator, saved pre-activation) is loaded for all of a
   // thread's items up front, before the LDS tile is complete: ITEMS loads in flight instead of one per round trip
   constexpr bool PF32 = EPI == E_F32_RESID || EPI == E_F32_ACC;
-  constexpr bool PF16 = EPI == E_DGELU;
+  constexpr bool PF16 = EPI == E_DGELU || EPI == E_DGELU_ERF;
   for (int ch = 0; ch < ECH; ++ch) {
   float4 pf[PF32 ? 2 * ITEMS : 1];
   bf16x8 pb[PF16 ? ITEMS : 1];
@@ -459,10 +459,13 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
         g[e] = EPI == E_GELU ? gelu_new_dev(x) : gelu_erf_f(x);
       }
       store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, g);
-    } else if constexpr (EPI == E_DGELU) {
+    } else if constexpr (EPI == E_DGELU || EPI == E_DGELU_ERF) {
       const bf16x8 pr = pb[k];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(v[e] * gelu_new_grad_f(bf2f(pr[e]))));  // the stored value
+      for (int e = 0; e < 8; ++e) {  // the stored value
+        const float x = bf2f(pr[e]);
+        v[e] = bf2f(f2bf(v[e] * (EPI == E_DGELU ? gelu_new_grad_f(x) : gelu_erf_grad_f(x))));
+      }
       store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v);
       if (p.csum) {  // this thread's own chunk of E: no other thread touches it before the barrier below
         *(float4*)(E + lr * EPS + lc) = make_float4(v[0], v[1], v[2], v[3]);
@@ -477,7 +480,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
       store8_f32((float*)p.C + (long)row * p.ldc + col, v);
     }
   }
-  if constexpr (EPI == E_DGELU) {
+  if constexpr (EPI == E_DGELU || EPI == E_DGELU_ERF) {
     if (p.csum) {  // column sums of this chunk's ER rows: G row groups per column, one atomic each
       __syncthreads();
       constexpr int G = NT / BN > 0 ? NT / BN : 1;
@@ -540,10 +543,12 @@ IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, con
   if (!(mode == 0 || mode == 2 || mode == 3)) return 0;
   const bool epi_ok = mode == 3 ? (epi == E_F32_ACC || epi == E_F32_STORE)
                                 : (epi == E_BF16 || epi == E_BF16_BIAS3 || epi == E_F32_RESID || epi == E_GELU ||
-                                   epi == E_GELU_ERF || epi == E_F32_ACC || epi == E_F32_STORE || epi == E_DGELU);
+                                   epi == E_GELU_ERF || epi == E_F32_ACC || epi == E_F32_STORE || epi == E_DGELU ||
+                                   epi == E_DGELU_ERF);
   if (!epi_ok) return 0;
-  if (mode == 0 && !(epi == E_BF16 || epi == E_F32_ACC || epi == E_F32_STORE || epi == E_DGELU)) return 0;
-  if (epi == E_DGELU && (mode != 0 || !C2)) return 0;
+  const bool dg = epi == E_DGELU || epi == E_DGELU_ERF;
+  if (mode == 0 && !(epi == E_BF16 || epi == E_F32_ACC || epi == E_F32_STORE || dg)) return 0;
+  if (dg && (mode != 0 || !C2)) return 0;
   if (M <= 0 || N <= 0 || K <= 0 || M % kTileBM[tile] || N % kTileBN[tile] || K % 64) return 0;
   if (lda % 8 || ldb % 8 || ldc % 8 || (C2 && ldc2 % 8) || (resid && ldr % 8)) return 0;
   const uintptr_t al = (uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)C2 | (uintptr_t)resid;
@@ -563,7 +568,7 @@ IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, co
   a.bias0 = bias0; a.bias1 = bias1; a.bias2 = bias2; a.resid = resid;
   a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldc2 = ldc2; a.ldr = ldr;
   a.M = M; a.N = N; a.K = K; a.bias_cols = bias_cols; a.k_per_split = K / splits;
-  a.csum = epi == E_DGELU ? csum : nullptr;
+  a.csum = (epi == E_DGELU || epi == E_DGELU_ERF) ? csum : nullptr;
   hipStream_t s = (hipStream_t)stream;
 #define G2(MODE, AK, BK_, EPI) \
   if (mode == (MODE) && epi == (EPI)) return (int)launch_tile<AK, BK_, EPI>(a, tile, s);
@@ -571,6 +576,7 @@ IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, co
   G2(0, false, false, E_F32_ACC)
   G2(0, false, false, E_F32_STORE)
   G2(0, false, false, E_DGELU)
+  G2(0, false, false, E_DGELU_ERF)
   G2(2, false, true, E_BF16)
   G2(2, false, true, E_BF16_BIAS3)
   G2(2, false, true, E_F32_RESID)

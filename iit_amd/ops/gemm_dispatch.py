@@ -169,9 +169,9 @@ def _blas(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, C2, C3, bias0, bias1, bia
         pre = _as(C2, M, N, ldc2)
         torch.addmm(bias0.reshape(-1)[:N].to(BF16), a, b, out=pre)
         _gelu_into(pre, _as(C, M, N, ldc), erf=epi == K.EPI_GELU_ERF)
-    elif epi == K.EPI_DGELU:
+    elif epi in (K.EPI_DGELU, K.EPI_DGELU_ERF):
         tmp = torch.mm(a, b)
-        K.dgelu(tmp, _as(aux, M, N, ldc2).contiguous(), _as(C, M, N, ldc))
+        K.dgelu(tmp, _as(aux, M, N, ldc2).contiguous(), _as(C, M, N, ldc), erf=epi == K.EPI_DGELU_ERF)
     elif epi == K.EPI_F32_ACC:
         c = _as(C, M, N, ldc)
         _addmm_f32(c, c, a, b)
@@ -188,7 +188,7 @@ def _blas(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, C2, C3, bias0, bias1, bia
 def _blas_supported(epi, C) -> bool:
     if epi == K.EPI_F32_ACC_QKV:
         return False
-    if epi == K.EPI_DGELU:
+    if epi in (K.EPI_DGELU, K.EPI_DGELU_ERF):
         return True
     return True
 
@@ -277,7 +277,7 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
         split_opts = (1,)
         if epi == K_.EPI_F32_ACC and (M // 64) * (N // 64) < 1024:
             split_opts = (1, 2, 4, 8, 16) if (M // 64) * (N // 64) < 64 else (1, 2, 4)
-        dg = epi == K_.EPI_DGELU  # the LDS-DMA kernel reads the pre-activation through its C2 operand
+        dg = epi in (K_.EPI_DGELU, K_.EPI_DGELU_ERF)  # the LDS-DMA kernel reads pre through its C2 operand
         for tile in K_.GLDS_TILES:
             for sp in split_opts:
                 if K_.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi,
@@ -382,7 +382,7 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
                 run(tail)
                 return choice
     fresh = fresh and epi == K_.EPI_F32_STORE and bias0 is None
-    assert colsum is None or epi == K_.EPI_DGELU, "fused column sums need the DGELU epilogue"
+    assert colsum is None or epi in (K_.EPI_DGELU, K_.EPI_DGELU_ERF), "fused column sums need a DGELU epilogue"
     box = [colsum] if colsum is not None else None
     args = (A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, bias2, resid, ldr, aux, ldc2, bias_cols,
             qkv, splits, blas_bias, policy)

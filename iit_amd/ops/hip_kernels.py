@@ -21,6 +21,7 @@ c_void_p, c_long, c_int, c_float, c_ull = ctypes.c_void_p, ctypes.c_long, ctypes
 
 EPI_BF16, EPI_BF16_BIAS3, EPI_F32_RESID, EPI_GELU, EPI_DGELU, EPI_F32_ACC, EPI_F32_ACC_QKV, EPI_F32_STORE = range(8)
 EPI_GELU_ERF = 8  # EPI_GELU with the exact (erf) GELU
+EPI_DGELU_ERF = 9  # EPI_DGELU with the exact (erf) GELU's derivative
 MODE_NN, MODE_AKM, MODE_BKM, MODE_AF32, MODE_BF32 = 0, 1, 2, 4, 8
 
 _LIB = None

@@ -797,8 +797,9 @@ def _bias_sum_done(g: Optional[torch.Tensor], b: Optional[torch.Tensor]) -> bool
 
 
 class MLPOutGeluFn(Function):
-    """``resid + gelu_new(pre) @ W_out + b_out`` with the gradient taken w.r.t. ``pre`` (``post`` comes in as
-    data: ``post = gelu_new(pre)`` from :class:`MLPInFn`'s epilogue, the block's only use of it).
+    """``resid + gelu(pre) @ W_out + b_out`` with the gradient taken w.r.t. ``pre`` (``post`` comes in as
+    data: ``post = gelu(pre)`` from :class:`MLPInFn`'s epilogue, the block's only use of it; gelu_new, or the
+    exact erf form with ``erf``).
 
     The backward's dX GEMM runs with the DGELU epilogue -- ``dpre = (g W_out^T) * gelu_new'(pre)`` in one pass --
     and, on the LDS-DMA kernel, reduces dpre into the b_in gradient in the same epilogue (tagged on dpre so
@@ -806,8 +807,9 @@ class MLPOutGeluFn(Function):
     live, so ``pre`` has no other consumer whose gradient autograd could add to the tagged tensor."""
 
     @staticmethod
-    def forward(ctx, pre, post, W, b, w, ldw, resid, b_in):
+    def forward(ctx, pre, post, W, b, w, ldw, resid, b_in, erf=False):
         ctx.set_materialize_grads(False)
+        ctx.erf = erf
         lead = post.shape[:-1]
         Kd = post.shape[-1]
         N = W.shape[-1]
@@ -827,7 +829,7 @@ class MLPOutGeluFn(Function):
     @staticmethod
     def backward(ctx, gy):
         if gy is None:
-            return (None,) * 8
+            return (None,) * 9
         x2, pre2 = ctx.saved_tensors
         W, b, b_in = ctx.params
         lead, Kd, N = ctx.meta
@@ -839,8 +841,8 @@ class MLPOutGeluFn(Function):
         if ctx.needs_input_grad[0]:
             dpre = torch.empty(T, Kd, dtype=BF16, device=g2.device)
             gbi = _grad_slot(b_in)
-            gemm(g2, ctx.w, dpre, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ldw, ldc=Kd, mode=K.MODE_NN, epi=K.EPI_DGELU,
-                 aux=pre2, ldc2=pre2.stride(0), colsum=gbi)
+            gemm(g2, ctx.w, dpre, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ldw, ldc=Kd, mode=K.MODE_NN,
+                 epi=K.EPI_DGELU_ERF if ctx.erf else K.EPI_DGELU, aux=pre2, ldc2=pre2.stride(0), colsum=gbi)
             dpre = dpre.view(*lead, Kd)
             if gbi is not None:
                 dpre._iit_bias_sum = (dpre.data_ptr(), dpre._version, id(b_in))
@@ -857,7 +859,7 @@ class MLPOutGeluFn(Function):
         if gb is not None:
             K.colsum_accum(g2, ldg, gb, T, N)
         _done(W, b)
-        return dpre, None, None, None, None, None, gy, None
+        return dpre, None, None, None, None, None, gy, None, None
 
 
 class CrossEntropyFn(Function):
@@ -998,12 +1000,12 @@ class HipOps(TorchOps):
             pre = hook_pre(pre)
         return pre, act_fn(act)(pre)
 
-    def mlp_gelu_residual(self, x, W_in, b_in, W_out, b_out, resid):
-        """``resid + gelu_new(x W_in + b_in) W_out + b_out`` for a block whose MLP sites are all dead: the
-        backward forms dpre in the dX GEMM's epilogue (see :class:`MLPOutGeluFn`)."""
-        pre, post = MLPInFn.apply(x, W_in, b_in, self._L(W_in)["in"], False)
+    def mlp_gelu_residual(self, x, W_in, b_in, W_out, b_out, resid, erf: bool = False):
+        """``resid + gelu(x W_in + b_in) W_out + b_out`` (gelu_new, or the exact erf GELU) for a block whose MLP
+        sites are all dead: the backward forms dpre in the dX GEMM's epilogue (see :class:`MLPOutGeluFn`)."""
+        pre, post = MLPInFn.apply(x, W_in, b_in, self._L(W_in)["in"], erf)
         return MLPOutGeluFn.apply(pre, post.detach(), W_out, b_out, self._L(W_out)["out"], W_out.shape[1], resid,
-                                  b_in)
+                                  b_in, erf)
 
     def mlp_out(self, post, W_out, b_out):
         return LinearFn.apply(post, W_out, b_out, self._L(W_out)["out"], W_out.shape[1], None, "bf16")

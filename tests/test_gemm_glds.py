@@ -161,8 +161,9 @@ def test_glds_wide_tile_multi_tile_grid(K, mode, epi):
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("erf", [False, True])
 @pytest.mark.parametrize("policy", ["auto", "hip", "blas", "glds"])
-def test_dgelu_epilogue_with_fused_column_sums(K, policy, monkeypatch):
+def test_dgelu_epilogue_with_fused_column_sums(K, policy, erf, monkeypatch):
     """dpre = (dY W^T) * gelu_new'(pre) (mode 0, DGELU epilogue) plus the column sums of the stored dpre into the
     bias gradient, on every dispatcher path (fused in the LDS-DMA epilogue, a column-sum pass after the others)."""
     from iit_amd.ops import gemm_dispatch as gd
@@ -175,9 +176,11 @@ def test_dgelu_epilogue_with_fused_column_sums(K, policy, monkeypatch):
     cs = torch.randn(N, device=dev)
     cs0 = cs.clone()
     p = pre.float().requires_grad_()
-    (gp,) = torch.autograd.grad(gelu_new(p).sum(), p)
+    act = torch.nn.functional.gelu(p) if erf else gelu_new(p)
+    (gp,) = torch.autograd.grad(act.sum(), p)
     exp = (a @ b) * gp
-    gd.gemm(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=0, epi=K.EPI_DGELU, aux=pre, ldc2=N, colsum=cs)
+    gd.gemm(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=0, epi=K.EPI_DGELU_ERF if erf else K.EPI_DGELU,
+            aux=pre, ldc2=N, colsum=cs)
     torch.cuda.synchronize()
     assert ((C.float() - exp).norm() / exp.norm()).item() < 1e-2
     ds = cs - cs0
