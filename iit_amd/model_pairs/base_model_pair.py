@@ -285,8 +285,10 @@ class BaseModelPair(ABC):
                 module = self._ll_module()
                 flat = getattr(module, "_flat_params", None) or FlatParams(module)
                 module._flat_params = flat
+            wire = self.training_args.get("grad_wire_dtype")  # "bf16" halves the all-reduce bytes (opt-in)
             self._reducer = GradReducer(flat, bucket_mb=self.training_args.get("bucket_mb", 64.0),
-                                        overlap=self.training_args.get("overlap_allreduce", True))
+                                        overlap=self.training_args.get("overlap_allreduce", True),
+                                        wire_dtype=torch.bfloat16 if wire == "bf16" else None)
 
     def restrict_sparse_rows(self, dataset, optimizer_rows: bool = True) -> None:
         """Exploit the gradient sparsity of the embedding tables for ``dataset``:

@@ -218,3 +218,26 @@ def test_rehearsal_device_mapping(monkeypatch):
     assert pdist.local_device_index() == 3
     monkeypatch.setenv("IIT_REHEARSE_ONE_GPU", "1")
     assert pdist.local_device_index() == 0
+
+
+def _worker_bf16_wire(rank, world, port, out_dir):
+    os.environ["IIT_DP_GRAD_DTYPE"] = "bf16"
+    _worker(rank, world, port, out_dir)
+
+
+def test_dp2_bf16_wire_gradients(tmp_path):
+    """IIT_DP_GRAD_DTYPE=bf16: gradients travel as bf16 -- the ranks stay bit-identical to each other and close
+    to the single-process (fp32) run."""
+    pair, train = _make(64)
+    ref_losses, _ = _train(pair, train, per_rank_batch=64)
+    ref_params = {n: p.detach().clone() for n, p in pair.ll_model.named_parameters()}
+    mp.spawn(_worker_bf16_wire, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r = [torch.load(tmp_path / f"rank{i}.pt", weights_only=True) for i in range(2)]
+    for n, p in ref_params.items():
+        assert torch.equal(r[0]["params"][n], r[1]["params"][n]), n
+        if n.endswith("b_K"):  # exactly-zero gradient in exact arithmetic: Adam turns rounding noise into +-lr steps
+            continue
+        err = float((r[0]["params"][n] - p).norm() / (p.norm() + 1e-12))
+        assert err < 5e-2, (n, err)
+    avg = torch.tensor(r[0]["losses"]) / 2 + torch.tensor(r[1]["losses"]) / 2
+    assert torch.allclose(avg, torch.tensor(ref_losses), atol=2e-2, rtol=2e-2)
