@@ -44,10 +44,6 @@ __device__ __forceinline__ i16x4 tr_block(const __bf16* img, int g, int lane_in_
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(img + (4 * g + q) * LDSR + col0 + 4 * p));
 }
 
-__device__ __forceinline__ void store4(__bf16* dst, const f32x4 v) {
-  bf16x4 o = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-  *(bf16x4*)dst = o;
-}
 
 template <int DH>
 __global__ __launch_bounds__(256) void attn_mfma_fwd_kernel(const __bf16* __restrict__ qkv, __bf16* __restrict__ z,
@@ -112,12 +108,23 @@ __global__ __launch_bounds__(256) void attn_mfma_fwd_kernel(const __bf16* __rest
   const float inv = sum > 0.f ? 1.f / sum : 0.f;
   if (lse && g == 0 && c < S) lse[(long)bh * S + c] = m + __logf(sum);
   const bf16x8 bp = regs_frag(p[0] * inv, p[1] * inv, p[2] * inv, p[3] * inv);
+  f32x4 o[DH / 16];
 #pragma unroll
   for (int t = 0; t < DH / 16; ++t) {
     const bf16x8 av = half_frag(tr_block<LDSR>(Vs, g, c, 16 * t));
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-    const f32x4 o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bp, zero, 0, 0, 0);
-    if (c < S) store4(z + (row0 + c) * ld_z + h * DH + 16 * t + 4 * g, o);
+    o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bp, zero, 0, 0, 0);  // Z^T[e][qi=c]
+  }
+  // z rows out through this wave's LDS image (V is consumed) as 16-byte chunks, as in the backward
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int t = 0; t < DH / 16; ++t)
+    *(bf16x4*)(Vs + c * LDSR + 16 * t + 4 * g) = bf16x4{f2bf(o[t][0]), f2bf(o[t][1]), f2bf(o[t][2]), f2bf(o[t][3])};
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = l; i < 16 * DH / 8; i += 64) {
+    const int r = i / (DH / 8), ch = i % (DH / 8);
+    if (r < S) *(bf16x8*)(z + (row0 + r) * ld_z + h * DH + ch * 8) = *(const bf16x8*)(Vs + r * LDSR + ch * 8);
   }
 }
 
@@ -211,19 +218,37 @@ __global__ __launch_bounds__(256) void attn_mfma_bwd_kernel(const __bf16* __rest
   const bf16x8 bdS = regs_frag(dS[0], dS[1], dS[2], dS[3]);
   const bf16x8 bdST = regs_frag(dST[0], dST[1], dST[2], dST[3]);
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  f32x4 dvT[DH / 16], dkT[DH / 16], dqT[DH / 16];
 #pragma unroll
   for (int t = 0; t < DH / 16; ++t) {
     const bf16x8 aG = half_frag(tr_block<LDSR>(Gs, g, c, 16 * t));  // dZ^T[e][qi=4g+j]
     const bf16x8 aQ = half_frag(tr_block<LDSR>(Qs, g, c, 16 * t));  // Q^T[e][qi=4g+j]
     const bf16x8 aK = half_frag(tr_block<LDSR>(Ks, g, c, 16 * t));  // K^T[e][kj=4g+j]
-    const f32x4 dvT = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aG, bP, zero, 0, 0, 0);   // dV^T[e][kj=c]
-    const f32x4 dkT = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aQ, bdS, zero, 0, 0, 0);  // dK^T[e][kj=c]
-    const f32x4 dqT = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aK, bdST, zero, 0, 0, 0); // dQ^T[e][qi=c]
-    if (c < S) {
-      const long o = (row0 + c) * ld_qkv + 16 * t + 4 * g;
-      store4(dv + o, dvT);
-      store4(dk + o, dkT);
-      store4(dq + o, dqT);
+    dvT[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aG, bP, zero, 0, 0, 0);   // dV^T[e][kj=c]
+    dkT[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aQ, bdS, zero, 0, 0, 0);  // dK^T[e][kj=c]
+    dqT[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aK, bdST, zero, 0, 0, 0); // dQ^T[e][qi=c]
+  }
+  // Coalesced writes: the transposed results go through this wave's (now free) LDS images as [16][DH] rows, then
+  // out as 16-byte row chunks (the MFMA layout would give 8-byte stores scattered over 16 rows per instruction).
+  // Only this wave touches its images, so an lgkmcnt drain orders its LDS writes before its reads.
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int t = 0; t < DH / 16; ++t) {
+    const int o = c * LDSR + 16 * t + 4 * g;
+    *(bf16x4*)(Gs + o) = bf16x4{f2bf(dvT[t][0]), f2bf(dvT[t][1]), f2bf(dvT[t][2]), f2bf(dvT[t][3])};
+    *(bf16x4*)(Ks + o) = bf16x4{f2bf(dkT[t][0]), f2bf(dkT[t][1]), f2bf(dkT[t][2]), f2bf(dkT[t][3])};
+    *(bf16x4*)(Qs + o) = bf16x4{f2bf(dqT[t][0]), f2bf(dqT[t][1]), f2bf(dqT[t][2]), f2bf(dqT[t][3])};
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  constexpr int CPR = DH / 8;  // 16-byte chunks per row
+#pragma unroll
+  for (int i = l; i < 16 * CPR; i += 64) {
+    const int r = i / CPR, ch = i % CPR;
+    if (r < S) {
+      const long o = (row0 + r) * ld_qkv + ch * 8;
+      *(bf16x8*)(dv + o) = *(const bf16x8*)(Gs + r * LDSR + ch * 8);
+      *(bf16x8*)(dk + o) = *(const bf16x8*)(Ks + r * LDSR + ch * 8);
+      *(bf16x8*)(dq + o) = *(const bf16x8*)(Qs + r * LDSR + ch * 8);
     }
   }
 }
