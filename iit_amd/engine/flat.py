@@ -312,16 +312,47 @@ class FlatParams:
         (``optimizer.zero_grad(set_to_none=True)``, or a lazily zeroed slot no producer
         claimed) gets its slot zeroed, so the arena equals the gradients.  (``zero_missing``
         is kept for callers; ``None`` slots are always zeroed.)"""
-        for p, view in zip(self.params, self._views()):
+        missing = []
+        for i, (p, view) in enumerate(zip(self.params, self._views())):
             g = p.grad
             if g is view:  # the common case (host cost matters: the DP schedule calls this twice per phase)
                 continue
             if g is None:
                 # a None gradient is zero (set_to_none / lazy zero_grad): the arena slot may hold stale values
-                view.zero_()
+                missing.append(i)
             elif g.data_ptr() != view.data_ptr() or g.stride() != view.stride():
                 view.copy_(g)
             p.grad = view
+        if missing:  # one multi-tensor launch: whole slots whose members are all missing, else the single views
+            views = self._views()
+            by_slot = {}
+            for i in missing:
+                by_slot.setdefault(self._slot_of(i), []).append(i)
+            parts = []
+            for (o, n), idx in sorted(by_slot.items()):
+                if len(idx) == len(self._slot_members()[(o, n)]):
+                    parts.append(self.grad[o:o + n])
+                else:
+                    parts.extend(views[i] for i in idx)
+            torch._foreach_zero_(parts)
+
+    def _slot_of(self, i: int) -> Tuple[int, int]:
+        """(offset, numel) of the arena slot holding parameter ``i``."""
+        slots = self.__dict__.get("_slot_index")
+        if slots is None:
+            slots = self._slot_index = {}
+        if i not in slots:
+            off = self.offset_of(self.params[i])
+            slots[i] = next((o, n) for o, n in self.slots if o <= off < o + max(n, 1))
+        return slots[i]
+
+    def _slot_members(self) -> Dict[Tuple[int, int], List[int]]:
+        members = self.__dict__.get("_members")
+        if members is None:
+            members = self._members = {}
+            for i in range(len(self.params)):
+                members.setdefault(self._slot_of(i), []).append(i)
+        return members
 
     def grad_view(self, p: torch.Tensor) -> torch.Tensor:
         return self._view_fns[self.index[id(p)]](self.grad)

@@ -186,3 +186,23 @@ def test_zero_plans_outlive_claim_changes():
     flat.zero_grad()  # back to the first claim set: its plan (and table) is reused
     assert flat._zero_plan[3][0] is chunks1[0]
     assert float(flat.grad_view(m[0].weight).abs().sum()) == 0.0 and m[1].weight.grad is None
+
+
+def test_rebind_zeroes_missing_slots_only():
+    """rebind_grads zeroes the slots of missing gradients in one batched launch, never a live member's values."""
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.models.transformer import HookedTransformer
+    torch.manual_seed(0)
+    m = HookedTransformer(dict(n_layers=1, n_heads=2, d_model=8, d_head=4, d_mlp=16, n_ctx=8, act_fn="gelu",
+                               d_vocab=11, device="cpu"))
+    flat = FlatParams(m)
+    a = m.blocks[0].attn
+    flat.grad.fill_(3.0)
+    a.W_Q.grad = a.W_K.grad = a.W_V.grad = None  # a whole packed QKV slot missing
+    m.blocks[0].mlp.W_in.grad = None              # a plain slot missing
+    a.b_Q.grad = None                             # one member of the packed bias slot missing
+    flat.rebind_grads()
+    assert float(a.W_Q.grad.abs().sum() + a.W_K.grad.abs().sum() + a.W_V.grad.abs().sum()) == 0.0
+    assert float(m.blocks[0].mlp.W_in.grad.abs().sum()) == 0.0
+    assert float(a.b_Q.grad.abs().sum()) == 0.0 and bool((a.b_K.grad == 3.0).all()) and bool((a.b_V.grad == 3.0).all())
+    assert bool((m.blocks[0].mlp.W_out.grad == 3.0).all())
