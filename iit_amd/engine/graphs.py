@@ -48,8 +48,14 @@ _CAPTURE_MODE = "thread_local"
 
 
 def _clone_out(out):
+    """Copies of a replayed phase's outputs (the captured buffers are overwritten by the next replay).  Scalar
+    losses are packed by one ``stack`` -- a single copy kernel instead of one per metric."""
     if isinstance(out, tuple):
         loss, extras = out
+        ts = [loss] + list(extras.values())
+        if all(t.dim() == 0 and t.dtype == loss.dtype and t.device == loss.device for t in ts):
+            vals = torch.stack(ts).unbind(0)
+            return vals[0], dict(zip(extras.keys(), vals[1:]))
         return loss.clone(), {k: v.clone() for k, v in extras.items()}
     return out.clone()
 
