@@ -88,3 +88,30 @@ def test_gemm_entry_point_forced_blas_on_cpu(monkeypatch):
     gd.gemm(A, B, C, M=M, N=N, K=Kd, lda=Kd, ldb=Kd, ldc=N, mode=K.MODE_NN, epi=K.EPI_BF16)
     assert torch.allclose(C.float(), A.float() @ B.float().T, atol=0.1, rtol=0.02)
     assert isinstance(gd.DECISIONS, dict) and "library fast paths" in gd.report()
+
+
+def test_ragged_split_pieces_cover_the_problem():
+    """_ragged_split: an N-ragged problem becomes a 128-aligned bulk + tail over disjoint columns (operand / output
+    offsets per layout); a K-ragged accumulate becomes a 1024-aligned bulk + tail over disjoint reduction steps."""
+    V, d, T = 50257, 768, 256
+    A = torch.zeros(T, d, dtype=BF)
+    B = torch.zeros(d, 50264, dtype=BF)
+    C = torch.zeros(T, 50264)
+    bias = torch.zeros(V)
+    parts = gd._ragged_split(A, B, C, M=T, N=V, K=d, lda=d, ldb=50264, mode=K.MODE_BKM, epi=K.EPI_F32_STORE,
+                             C2=None, bias0=bias, resid=None, aux=None)
+    bulk, tail = parts
+    assert bulk["N"] == 50176 and tail["N"] == V - 50176
+    assert tail["B"].data_ptr() == B.data_ptr() + 50176 * 2  # k-major B: column offset
+    assert tail["C"].data_ptr() == C.data_ptr() + 50176 * 4 and tail["bias0"].data_ptr() == bias.data_ptr() + 50176 * 4
+    # K-ragged fp32 accumulate (the unembed input gradient, K = vocab)
+    G = torch.zeros(T, 50264, dtype=BF)
+    U = torch.zeros(d, 50264, dtype=BF)
+    X = torch.zeros(T, d)
+    bulk, tail = gd._ragged_split(G, U, X, M=T, N=d, K=V, lda=50264, ldb=50264, mode=K.MODE_NN, epi=K.EPI_F32_ACC,
+                                  C2=None, bias0=None, resid=None, aux=None)
+    assert bulk["K"] == 50176 and tail["K"] == V - 50176 and tail["C"] is X
+    assert tail["A"].data_ptr() == G.data_ptr() + 50176 * 2 and tail["B"].data_ptr() == U.data_ptr() + 50176 * 2
+    # aligned or small problems are left whole
+    assert gd._ragged_split(A, B, C, M=T, N=4096, K=d, lda=d, ldb=50264, mode=K.MODE_BKM, epi=K.EPI_F32_STORE,
+                            C2=None, bias0=None, resid=None, aux=None) is None

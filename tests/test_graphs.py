@@ -94,3 +94,4 @@ def test_split_graphs_for_data_parallel_match_eager(staged):
     if staged:
         assert all(len(ent[0][1]) == 2 for ent in g.graphs.values())  # two lower-stage graphs per phase
     assert torch.allclose(le1[:_TIGHT], ls[:_TIGHT], rtol=2e-3, atol=2e-3), (le1[:_TIGHT] - ls[:_TIGHT]).abs().max()
+
