@@ -292,16 +292,24 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
     if epi in _BLAS16_EPIS:
         calls["blas16"] = lambda c=C, c2=C2, c3=None: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
                                                              bias0, resid, ldr)
-    if (epi == K_.EPI_F32_STORE and A.is_cuda and mode in (0, 2, 3) and Kd >= 256 and Kd % 64 == 0
-            and ((M + 63) // 64) * ((N + 63) // 64) < 64):
-        # a store with too few output tiles to fill the chip (the narrow tail of a ragged vocab GEMM): write the
-        # bias (or zeros), then accumulate with split-K -- many workgroups instead of a handful of long K loops
+    if (epi in (K_.EPI_F32_STORE, K_.EPI_F32_RESID) and A.is_cuda and mode in (0, 2, 3) and Kd >= 256
+            and Kd % 64 == 0 and ((M + 63) // 64) * ((N + 63) // 64) < 64):
+        # an fp32 store with too few output tiles to fill the chip (the narrow tail of a ragged vocab GEMM, the
+        # last-position-only final block): write the bias (+ residual, or zeros) first, then accumulate with
+        # split-K -- many workgroups instead of a handful of long K loops
         sp = min(16, Kd // 64)
 
         def split_store(c=C, c2=C2, c3=None):
             cv = _as(c, M, N, ldc)
-            if bias0 is not None:
-                cv.copy_(bias0.reshape(-1)[:N].float().expand(M, N))
+            b = None if bias0 is None else bias0.reshape(-1)[:N].float()
+            if epi == K_.EPI_F32_RESID:
+                r = _as(resid, M, N, ldr)
+                if b is None:
+                    cv.copy_(r)
+                else:
+                    torch.add(r, b, out=cv)
+            elif b is not None:
+                cv.copy_(b.expand(M, N))
             else:
                 cv.zero_()
             K_.gemm(A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=K_.EPI_F32_ACC, splits=sp)

@@ -224,8 +224,9 @@ def test_ragged_vocab_gemms_split_bulk_and_tail(K, case):
     assert ((got - exp).norm() / exp.norm()).item() < 1e-2
 
 
+@pytest.mark.parametrize("resid", [False, True])
 @pytest.mark.parametrize("bias", [True, False])
-def test_split_store_candidate_for_narrow_outputs(K, bias):
+def test_split_store_candidate_for_narrow_outputs(K, bias, resid):
     """The "s+hip" candidate (bias / zero fill, then split-K accumulate) equals the fp32 store it replaces on a
     narrow, few-tile output (the ragged unembed tail: 256 x 81, K = 768)."""
     from iit_amd.ops import gemm_dispatch as gd
@@ -233,11 +234,13 @@ def test_split_store_candidate_for_narrow_outputs(K, bias):
     A, B, lda, ldb, a, b = _ops(K, K.MODE_BKM, M, N, Kd, 8)
     b0 = torch.randn(N, device=dev) if bias else None
     C = torch.full((M, N + 7), 5.0, device=dev)
-    calls = gd._candidates(A, B, C, None, M, N, Kd, lda, ldb, N + 7, K.MODE_BKM, K.EPI_F32_STORE, b0, None, None,
-                           None, 0, None, 0, 0, (0, 0, 0), None, None, "auto")
+    R = torch.randn(M, N + 3, device=dev) if resid else None
+    epi = K.EPI_F32_RESID if resid else K.EPI_F32_STORE
+    calls = gd._candidates(A, B, C, None, M, N, Kd, lda, ldb, N + 7, K.MODE_BKM, epi, b0, None, None,
+                           R, N + 3 if resid else 0, None, 0, 0, (0, 0, 0), None, None, "auto")
     assert "s+hip" in calls
     calls["s+hip"](C, None, None)
     torch.cuda.synchronize()
-    exp = a @ b + (b0 if bias else 0)
+    exp = a @ b + (b0 if bias else 0) + (R[:, :N] if resid else 0)
     assert ((C[:, :N] - exp).norm() / exp.norm()).item() < 1e-2
     assert torch.all(C[:, N:] == 5.0)
