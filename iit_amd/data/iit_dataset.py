@@ -17,7 +17,9 @@ returns a :class:`DeviceIITLoader` that keeps the pair table and the samples in
 HBM and assembles each batch with two ``index_select`` launches - no per-sample
 Python, no host->device copies.  Other datasets use a regular ``DataLoader``
 with the reference collate.  Under ``torch.distributed`` each rank takes its
-contiguous shard of every *global* batch (``batch_size`` is per rank).
+contiguous shard of every *global* batch (``batch_size`` is per rank).  The
+epoch tail is split into balanced shards (sizes differ by at most one row); a
+tail smaller than the world size is skipped, so no rank ever sees an empty batch.
 """
 from __future__ import annotations
 
@@ -164,7 +166,9 @@ class DeviceIITLoader:
     def __len__(self) -> int:
         n = len(self.dataset)
         gb = self.global_batch
-        return n // gb if self.drop_last else (n + gb - 1) // gb
+        if self.drop_last or (self.world > 1 and 0 < n % gb < self.world):
+            return n // gb
+        return (n + gb - 1) // gb
 
     def __iter__(self) -> Iterator:
         n = len(self.dataset)
@@ -176,8 +180,13 @@ class DeviceIITLoader:
             chunk = perm[start:start + gb]
             if chunk.numel() < gb and self.drop_last:
                 break
-            per = (chunk.numel() + self.world - 1) // self.world
-            chunk = chunk[self.rank * per:(self.rank + 1) * per]
+            if self.world > 1:
+                if chunk.numel() < self.world:
+                    # a tail that cannot give every rank a row: an empty shard would average NaN losses and
+                    # accuracies into every rank's metrics (and trip the early stop), so all ranks skip it
+                    break
+                # balanced shards (sizes differ by at most one row), never empty
+                chunk = torch.tensor_split(chunk, self.world)[self.rank]
             if self._unique:
                 yield self._base_gather(chunk)
             else:

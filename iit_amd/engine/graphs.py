@@ -172,14 +172,20 @@ class GraphedTrainStep:
                     run_stage(i, k)
                 return
             reducer.start()
-            if stg is None:
-                reducer.launch_range(0, reducer.flat.numel)
-            else:
-                rng = stg.ranges()
-                reducer.launch_range(*rng[0])
-                for i, k in enumerate(stg.stages()):
-                    run_stage(i, k)
-                    reducer.launch_range(*rng[i + 1])
+            # launches come only from the explicit ranges: a stage's backward may cover several forwards (a
+            # single combined loss), so a parameter's first gradient report inside it is not its final value
+            reducer.paused = True
+            try:
+                if stg is None:
+                    reducer.launch_range(0, reducer.flat.numel)
+                else:
+                    rng = stg.ranges()
+                    reducer.launch_range(*rng[0])
+                    for i, k in enumerate(stg.stages()):
+                        run_stage(i, k)
+                        reducer.launch_range(*rng[i + 1])
+            finally:
+                reducer.paused = False
             reducer.finish()
 
         def eager_phase():

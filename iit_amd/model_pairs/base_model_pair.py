@@ -288,7 +288,8 @@ class BaseModelPair(ABC):
             wire = self.training_args.get("grad_wire_dtype")  # "bf16" halves the all-reduce bytes (opt-in)
             self._reducer = GradReducer(flat, bucket_mb=self.training_args.get("bucket_mb", 64.0),
                                         overlap=self.training_args.get("overlap_allreduce", True),
-                                        wire_dtype=torch.bfloat16 if wire == "bf16" else None)
+                                        wire_dtype=torch.bfloat16 if wire == "bf16" else None,
+                                        module=self._ll_module())
 
     def restrict_sparse_rows(self, dataset, optimizer_rows: bool = True) -> None:
         """Exploit the gradient sparsity of the embedding tables for ``dataset``:
@@ -387,7 +388,9 @@ class BaseModelPair(ABC):
                                                       training_args["num_workers"])
         early_stop = training_args["early_stop"]
         optimizer = self.make_optimizer(training_args["lr"])
-        self.restrict_embedding_reduce(train_set)
+        # only the embedding rows the training data can reach get gradient: reduce (DP) and update just those
+        # (exact, see restrict_sparse_rows); evaluation reads the other rows unchanged
+        self.restrict_sparse_rows(train_set)
         loss_fn = self.loss_fn
         scheduler_cls = training_args.get("lr_scheduler", None)
         lr_scheduler = None
@@ -432,12 +435,35 @@ class BaseModelPair(ABC):
     def make_loaders(dataset: IITDataset, test_dataset: IITDataset, batch_size: int, num_workers: int):
         return dataset.make_loader(batch_size, num_workers), test_dataset.make_loader(batch_size, num_workers)
 
+    def train_step_fn(self, optimizer, loss_fn) -> Callable:
+        """The per-batch step the training loop calls: :class:`iit_amd.engine.graphs.GraphedTrainStep` (every
+        optimizer phase captured once per sampled node as a HIP graph, then replayed) for a native LL model on
+        the GPU, else the plain ``run_train_step``.  ``training_args["graphs"]`` (default: on when the LL model
+        is on a GPU; ``IIT_GRAPHS=0`` turns it off) selects; batches of other shapes (a short epoch tail) and
+        phases that cannot be captured run eagerly inside the runner."""
+        runner = getattr(self, "_graph_step", None)
+        if runner is not None and runner.optimizer is optimizer:
+            return runner
+        import os
+        use = self.training_args.get("graphs", None)
+        if use is None:
+            use = (os.environ.get("IIT_GRAPHS", "1") != "0" and self.native()
+                   and next(self._ll_module().parameters()).is_cuda)
+        if use:
+            from ..engine.graphs import GraphedTrainStep
+            g = GraphedTrainStep(self, optimizer, loss_fn)
+            if g.enabled:
+                self._graph_step = g
+                return g
+        return self.run_train_step
+
     def _run_train_epoch(self, loader, loss_fn, optimizer, max_steps: Optional[int] = None) -> MetricStoreCollection:
         self._ll_module().train()
         metrics = self.make_train_metrics()
+        step = self.train_step_fn(optimizer, loss_fn)
         for i, (base_input, ablation_input) in enumerate(progress(loader, total=len(loader),
                                                                   disable=not pdist.is_main(), leave=False)):
-            metrics.update(self.run_train_step(base_input, ablation_input, loss_fn, optimizer))
+            metrics.update(step(base_input, ablation_input, loss_fn, optimizer))
             if max_steps is not None and i + 1 >= max_steps:
                 break
         return metrics

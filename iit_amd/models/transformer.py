@@ -274,9 +274,21 @@ class Attention(nn.Module):
             ops, q, k, v, causal, self.attn_scale,
             hook_scores=lambda t: run.site(self.hook_attn_scores, t),
             hook_pattern=lambda t: run.site(self.hook_pattern, t),
-            ignore=float(self.IGNORE),
+            ignore=self.ignore_value(),
         )
         return z, False
+
+    def ignore_value(self) -> float:
+        """The masked-score fill (the ``IGNORE`` buffer) as a host float, read once: a device read inside a
+        graph-captured phase is a synchronising copy, which capture forbids.  ``load_state_dict`` re-reads it."""
+        v = self.__dict__.get("_ignore_f")
+        if v is None:
+            v = self.__dict__["_ignore_f"] = float(self.IGNORE)
+        return v
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self.__dict__.pop("_ignore_f", None)
+        return super()._load_from_state_dict(*args, **kwargs)
 
 
 class MLP(nn.Module):

@@ -82,6 +82,16 @@ def enable_tuned_library_gemms() -> bool:
         return False
 
 
+def deterministic() -> bool:
+    """Run-to-run reproducible GEMMs: ``IIT_DETERMINISTIC=1`` or ``torch.use_deterministic_algorithms(True)``.
+
+    The split-K candidates (fp32 atomics into the output: the weight-gradient accumulate tiles and the few-tile
+    fp32 store / residual ``s+hip`` path used by the last-position logits and the final-block residual adds) sum
+    their partial products in arrival order, so two runs can differ in the last bits.  In deterministic mode the
+    dispatcher drops them and every candidate has a fixed reduction order."""
+    return os.environ.get("IIT_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
+
+
 def _as(t, rows, cols, ld, dtype=None):
     v = torch.as_strided(t, (rows, cols), (ld, 1))
     return v if dtype is None or v.dtype == dtype else v.to(dtype)
@@ -263,6 +273,9 @@ def _candidates(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, b
 
 def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, bias2, resid, ldr, aux, ldc2,
                       bias_cols, qkv, splits, blas_bias, policy, csum_box):
+    det = deterministic()
+    if det:
+        splits = 1
     hip_call = lambda c=C, c2=C2, c3=None: K_.gemm(  # noqa: E731
         A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=c2, C3=c3, bias0=bias0,
         bias1=bias1, bias2=bias2, resid=resid, ldr=ldr, aux=aux, ldc2=ldc2, bias_cols=bias_cols, qkv=qkv,
@@ -275,7 +288,7 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
                                                      blas_bias)
     if policy in ("auto", "glds") and A.is_cuda:
         split_opts = (1,)
-        if epi == K_.EPI_F32_ACC and (M // 64) * (N // 64) < 1024:
+        if epi == K_.EPI_F32_ACC and (M // 64) * (N // 64) < 1024 and not det:
             split_opts = (1, 2, 4, 8, 16) if (M // 64) * (N // 64) < 64 else (1, 2, 4)
         dg = epi in (K_.EPI_DGELU, K_.EPI_DGELU_ERF)  # the LDS-DMA kernel reads pre through its C2 operand
         for tile in K_.GLDS_TILES:
@@ -292,7 +305,7 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
     if epi in _BLAS16_EPIS:
         calls["blas16"] = lambda c=C, c2=C2, c3=None: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
                                                              bias0, resid, ldr)
-    if (epi in (K_.EPI_F32_STORE, K_.EPI_F32_RESID) and A.is_cuda and mode in (0, 2, 3) and Kd >= 256
+    if (not det and epi in (K_.EPI_F32_STORE, K_.EPI_F32_RESID) and A.is_cuda and mode in (0, 2, 3) and Kd >= 256
             and Kd % 64 == 0 and ((M + 63) // 64) * ((N + 63) // 64) < 64):
         # an fp32 store with too few output tiles to fill the chip (the narrow tail of a ragged vocab GEMM, the
         # last-position-only final block): write the bias (+ residual, or zeros) first, then accumulate with
@@ -389,7 +402,7 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
                 return gemm(kw.pop("A"), kw.pop("B"), kw.pop("C"), lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi,
                             ldr=ldr, ldc2=ldc2, blas_bias=None, fresh=fresh, _decide_only=decide, **kw)
 
-            rkey = (M, N, K, mode, epi, bias0 is not None, fresh, "ragged")
+            rkey = (M, N, K, mode, epi, bias0 is not None, fresh, deterministic())
             split = RAGGED.get(rkey)
             if split is None and not torch.cuda.is_current_stream_capturing():
                 # the split is one more candidate: bulk + tail against the whole problem, each at its best
@@ -426,7 +439,7 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     if policy in calls:
         return calls[policy](C, C2, C3)
     # the last key field marks the variant: a fresh store (EPI_F32_STORE) or fused column sums (EPI_DGELU)
-    key = (M, N, Kd, mode, epi, bias0 is not None, fresh or (colsum is not None))
+    key = (M, N, Kd, mode, epi, bias0 is not None, fresh or (colsum is not None), deterministic())
     choice = DECISIONS.get(key)
     if choice is None:
         if torch.cuda.is_current_stream_capturing():
@@ -455,7 +468,7 @@ K_ = K  # the kernel module (``K`` is shadowed by the reduction-size keyword abo
 
 def report() -> str:
     lines = [f"library fast paths: {dict(_BLAS_OK) or 'all available'}"]
-    for (M, N, Kd, mode, epi, bias, fresh), (c, times) in sorted(DECISIONS.items()):
+    for (M, N, Kd, mode, epi, bias, fresh, _det), (c, times) in sorted(DECISIONS.items()):
         ts = "  ".join(f"{k} {v:8.1f}us" for k, v in times.items())
         lines.append(f"M={M:6d} N={N:6d} K={Kd:6d} mode={mode:2d} epi={epi}{'f' if fresh else ''} bias={int(bias)} "
                      f"-> {c:6s} {ts}")

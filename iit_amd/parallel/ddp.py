@@ -11,6 +11,12 @@ never completed by autograd (dead compute skipped by the engine) are flushed in
 ``finish()``.  Reduction is in place on the arena (no pack/unpack copies), as an
 average (``ReduceOp.AVG`` on RCCL, SUM + scale on gloo).
 
+A loss may span several grad-enabled forwards (``use_single_loss``: the IIT, strict and behaviour forwards feed one
+backward), and then every weight gradient is written once *per forward*: the first report of a parameter is not
+its final value.  A forward hook on the LL module counts the grad-enabled forwards since the last backward; when
+there was more than one, ``start`` turns the per-parameter launches off for that backward and ``finish`` reduces
+every bucket after autograd is done (correct for any number of writes; only the overlap is lost).
+
 Bucket size default 64 MiB: per xGMI ring link (~150 GB/s) that is ~0.4 ms per
 bucket, large enough to amortise RCCL launch latency, small enough that the last
 bucket's exposed tail is short.
@@ -36,7 +42,7 @@ from . import dist as pdist
 
 class GradReducer:
     def __init__(self, flat: FlatParams, bucket_mb: float = 64.0, overlap: bool = True,
-                 wire_dtype: Optional[torch.dtype] = None):
+                 wire_dtype: Optional[torch.dtype] = None, module: Optional[torch.nn.Module] = None):
         self.flat = flat
         if wire_dtype is None and os.environ.get("IIT_DP_GRAD_DTYPE", "fp32") == "bf16":
             wire_dtype = torch.bfloat16
@@ -64,6 +70,11 @@ class GradReducer:
         self._listener = None
         self._subsets = {}
         self.paused = False  # True while a graph-captured backward runs (reduction happens after it)
+        self.deferred = False  # this backward: no per-parameter launches (several forwards wrote each gradient)
+        self._grad_forwards = 0
+        self._fwd_hook = None
+        if module is not None:
+            self._fwd_hook = module.register_forward_pre_hook(self._count_forward)
         if self.overlap:
             for i, p in enumerate(flat.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -72,10 +83,15 @@ class GradReducer:
             self._listener = grad_hooks.add_listener(
                 lambda p, _index=index: self._mark_ready(_index[id(p)]) if id(p) in _index else None)
 
+    def _count_forward(self, _module, _args) -> None:
+        if torch.is_grad_enabled():
+            self._grad_forwards += 1
+
     def _mark_ready(self, i: int) -> None:
-        # each parameter's gradient is final when first reported within a backward (the engine writes every
-        # weight gradient exactly once per backward); repeats are ignored
-        if self.paused or self._ready[i]:
+        # with one grad-enabled forward each parameter's gradient is final when first reported within a backward
+        # (the engine writes every weight gradient exactly once per backward pass); repeats are ignored.  With
+        # several forwards behind the loss the reports are not final: ``deferred`` leaves everything to finish()
+        if self.paused or self.deferred or self._ready[i]:
             return
         self._ready[i] = True
         b = self._param_bucket[i]
@@ -161,7 +177,12 @@ class GradReducer:
         self._launched = [False] * len(self.buckets)
 
     def start(self):
-        """Call before ``backward``: every gradient must live in the arena the buckets reduce."""
+        """Call before ``backward``: every gradient must live in the arena the buckets reduce.
+
+        Per-parameter launches stay on only if exactly one grad-enabled forward of the module (or an unknown
+        number, when no module was given) produced the loss."""
+        self.deferred = self._fwd_hook is not None and self._grad_forwards != 1
+        self._grad_forwards = 0
         self.flat.rebind_grads(zero_missing=True)
         self._pending = list(self._bucket_count)
         self._launched = [False] * len(self.buckets)
@@ -186,6 +207,7 @@ class GradReducer:
                 full, rows = scatter
                 full.index_copy_(0, rows, buf)
         self._works = []
+        self.deferred = False
         self.flat.rebind_grads()
 
     def reduce_all(self) -> None:
@@ -208,6 +230,9 @@ class GradReducer:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        if self._fwd_hook is not None:
+            self._fwd_hook.remove()
+            self._fwd_hook = None
         if self._listener is not None:
             grad_hooks.remove_listener(self._listener)
             self._listener = None

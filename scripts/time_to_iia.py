@@ -1,0 +1,107 @@
+"""Training wall-clock to the reference's convergence criterion on IOI (BASELINE.json: "match or beat the
+reference's IIA and training wall-clock on the IOI task").
+
+Runs ``IOI_ModelPair.train`` exactly as ``train_ioi.py`` does (reference ``train_ioi.py:12-48``: 12,000 samples,
+80/20 split, batch 256, Adam lr 1e-4, iit/behaviour/strict weights 1/1/0.4, clip 1.0, no scheduler, early stop
+when every validation ACCURACY metric reaches 100 %, at most ``--epochs`` epochs) and prints one JSON line with the
+epochs run, the wall-clock, whether the early-stop criterion was met, and the final validation metrics.
+
+    python scripts/time_to_iia.py --model ioi-6l --engine native            # this engine (fp32, graphs)
+    python scripts/time_to_iia.py --model ioi-6l --engine reference         # reference-semantics eager fp32
+    python scripts/time_to_iia.py --model gpt2-small --dtype bf16 --epochs 20
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="ioi-6l", choices=["ioi-6l", "gpt2-small"])
+    ap.add_argument("--engine", default="native", choices=["native", "reference"])
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--epochs", type=int, default=1000)
+    ap.add_argument("--num-samples", type=int, default=12000)
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--graphs", type=int, default=1)
+    args = ap.parse_args()
+
+    from iit_amd.data.iit_dataset import IITDataset, train_test_split
+    from iit_amd.model_pairs import IOI_ModelPair
+    from iit_amd.models.config import gpt2_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.parallel import dist as pdist
+    from iit_amd.tasks.ioi import NAMES, ioi_cfg, make_ioi_corr, make_ioi_dataset_and_hl
+
+    pdist.init_distributed()
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    torch.manual_seed(0)
+    np.random.seed(0)
+    cfg = gpt2_config_dict()
+    if args.model == "ioi-6l":
+        cfg.update(ioi_cfg)
+    cfg.update(init_weights=True, device=str(dev), dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32)
+    ll = HookedTransformer(cfg)
+    if args.dtype == "fp32" or args.engine == "reference":
+        ll.set_op_backend("torch")
+    ds, hl = make_ioi_dataset_and_hl(args.num_samples, ll, NAMES, device=dev,
+                                     label_format="onehot" if args.engine == "reference" else "index")
+    train_ds, test_ds = train_test_split(ds, test_size=0.2, random_state=42)
+    train_set = IITDataset(train_ds, train_ds, seed=0, device=dev)
+    test_set = IITDataset(test_ds, test_ds, seed=0, device=dev)
+    training_args = {"batch_size": 256, "lr": args.lr, "iit_weight": 1.0, "behavior_weight": 1.0,
+                     "strict_weight": 0.4, "next_token": False, "lr_scheduler": None, "clip_grad_norm": 1.0,
+                     "early_stop": True, "use_single_loss": False, "engine": args.engine,
+                     "graphs": bool(args.graphs) and args.engine == "native" and dev.type == "cuda"}
+    pair = IOI_ModelPair(ll_model=ll, hl_model=hl, corr=make_ioi_corr(cfg["n_layers"]), training_args=training_args)
+
+    epochs_seen = []
+    orig = pair._print_and_log_metrics
+    t_start = [None]
+
+    def log(epoch, metrics, sink=None):
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        epochs_seen.append((epoch, time.perf_counter() - t_start[0], {m.get_name(): m.get_value() for m in metrics
+                                                                       if m.get_name() != "val/per_token_accuracy"}))
+        if epoch % 10 == 0 or epoch < 3:
+            orig(epoch, metrics, sink)
+            sys.stdout.flush()
+
+    pair._print_and_log_metrics = log
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t_start[0] = time.perf_counter()
+    pair.train(train_set, test_set, epochs=args.epochs)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    wall = time.perf_counter() - t_start[0]
+    last_epoch, _, last = epochs_seen[-1]
+    converged = bool(pair._check_early_stop_condition(pair.test_metrics.metrics))
+    first_100 = next((e for e, _, m in epochs_seen if m.get("val/IIA", 0) >= 100), None)
+    steps = (last_epoch + 1) * len(train_set.make_loader(256, 0))
+    rec = {"metric": "IOI training wall-clock to the reference's early-stop criterion (val/IIA = val/accuracy = 100)",
+           "model": args.model, "engine": args.engine, "dtype": args.dtype, "graphs": training_args["graphs"],
+           "epochs_run": last_epoch + 1, "converged": converged, "first_epoch_IIA_100": first_100,
+           "wall_s": round(wall, 2), "s_per_epoch": round(wall / (last_epoch + 1), 3),
+           "train_pairs_per_s": round(steps * 256 / wall, 1),
+           "final": {k: round(float(v), 3) for k, v in last.items()},
+           "device": torch.cuda.get_device_name() if dev.type == "cuda" else "cpu",
+           "data": "synthetic (offline IOI prompts, random-init weights)"}
+    if pdist.is_main():
+        print(json.dumps(rec))
+    pdist.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -241,3 +241,67 @@ def test_dp2_bf16_wire_gradients(tmp_path):
         assert err < 5e-2, (n, err)
     avg = torch.tensor(r[0]["losses"]) / 2 + torch.tensor(r[1]["losses"]) / 2
     assert torch.allclose(avg, torch.tensor(ref_losses), atol=2e-2, rtol=2e-2)
+
+
+def _train_single_loss(pair, train, per_rank_batch, steps=3):
+    pair.training_args["use_single_loss"] = True
+    return _train(pair, train, per_rank_batch, steps=steps)
+
+
+def _worker_single_loss(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from iit_amd.parallel import dist as pdist
+    pdist.init_distributed("gloo")
+    torch.set_num_threads(2)
+    pair, train = _make(64)
+    pdist.broadcast_module(pair.ll_model)
+    losses, nodes = _train_single_loss(pair, train, per_rank_batch=32)
+    assert pair._reducer.overlap and not pair._reducer.deferred
+    torch.save({"losses": losses, "nodes": nodes,
+                "params": {n: p.detach().clone() for n, p in pair.ll_model.named_parameters()}},
+               os.path.join(out_dir, f"single{rank}.pt"))
+    pdist.destroy()
+
+
+def test_dp2_single_loss_equals_single_process(tmp_path):
+    """use_single_loss: one backward through the IIT, strict and behaviour forwards writes every weight gradient
+    three times; the overlapped reducer must reduce only the final sums (launching a bucket at the first
+    report raced the later accumulations and left the ranks with different weights)."""
+    pair, train = _make(64)
+    ref_losses, ref_nodes = _train_single_loss(pair, train, per_rank_batch=64)
+    ref_params = {n: p.detach().clone() for n, p in pair.ll_model.named_parameters()}
+    mp.spawn(_worker_single_loss, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r = [torch.load(tmp_path / f"single{i}.pt", weights_only=True) for i in range(2)]
+    assert r[0]["nodes"] == r[1]["nodes"] == ref_nodes
+    for n, p in ref_params.items():
+        assert torch.equal(r[0]["params"][n], r[1]["params"][n]), n
+        assert torch.allclose(r[0]["params"][n], p, atol=2e-5, rtol=1e-4), n
+    avg = torch.tensor(r[0]["losses"]) / 2 + torch.tensor(r[1]["losses"]) / 2
+    assert torch.allclose(avg, torch.tensor(ref_losses), atol=1e-4)
+
+
+def test_reducer_defers_launches_for_multi_forward_losses():
+    """The forward counter: one grad-enabled forward keeps per-parameter launches; two defer them to finish()."""
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.parallel.ddp import GradReducer
+    pair, train = _make(64)
+    red = GradReducer(FlatParams(pair.ll_model), module=pair.ll_model)
+    red.enabled = True  # no process group: only the bookkeeping is exercised (nothing is launched below)
+    x = next(iter(train.make_loader(8, 0)))[0][0]
+    pair.ll_model(x)
+    red.start()
+    assert not red.deferred
+    pair.ll_model(x)
+    pair.ll_model(x)
+    red.start()
+    assert red.deferred
+    from iit_amd.engine import grad_hooks
+    for p in pair.ll_model.parameters():  # the fused kernels' per-write reports launch nothing while deferred
+        grad_hooks.notify(p)
+    assert not any(red._launched)
+    with torch.no_grad():
+        pair.ll_model(x)
+    red.start()
+    assert red.deferred  # zero grad-enabled forwards: unknown producer count, stay conservative
+    red.remove()
