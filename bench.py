@@ -93,7 +93,8 @@ def setup(args, dev):
 
     it = batches()
     step_fn = pair.run_train_step
-    if args.graphs and dev.type == "cuda" and args.engine == "native":
+    # graphs on the fused HIP backend (bf16); the fp32 torch-op backend runs eagerly (see train_step_fn)
+    if args.graphs and dev.type == "cuda" and args.engine == "native" and args.dtype == "bf16":
         from iit_amd.engine.graphs import GraphedTrainStep
         g = GraphedTrainStep(pair, opt, loss_fn)
         if g.enabled:

@@ -45,6 +45,8 @@ import torch
 # process group's watchdog thread polls its work events (hipEventQuery) while a phase is being captured;
 # in the default "global" mode such a call from another thread can invalidate the capture.
 _CAPTURE_MODE = "thread_local"
+_SYNC_BEFORE_REPLAY = os.environ.get("IIT_GRAPH_SYNC_BEFORE_REPLAY") == "1"  # diagnostics
+_RECAPTURE_ALL = os.environ.get("IIT_GRAPH_RECAPTURE_ALL") == "1"  # diagnostics
 
 
 def _clone_out(out):
@@ -93,6 +95,11 @@ class GraphedTrainStep:
         self.graphs: Dict[Tuple, Tuple[torch.cuda.CUDAGraph, object]] = {}
         self.seen: Dict[Tuple, int] = {}
         self.pool = None  # shared graph memory pool, created at the first capture
+        # every step -- eager warm-up phases, captures and replays -- runs on this one stream: autograd's
+        # AccumulateGrad nodes run on the stream they were created on, so a node made by an eager phase on the
+        # default stream and kept alive would accumulate *outside* a later capture (silently missing from the
+        # graph); one stream for everything keeps them inside
+        self.stream = torch.cuda.Stream() if (enabled and torch.cuda.is_available()) else None
         if enabled:
             from ..ops.gemm_dispatch import select_graph_safe_blas
             select_graph_safe_blas()
@@ -202,24 +209,25 @@ class GraphedTrainStep:
             if n < self.warmup or full in self.failed:
                 self.seen[full] = n + 1
                 return eager_phase()
-            if self.pool is None:
+            if self.pool is None or os.environ.get("IIT_GRAPH_POOL") == "private":
                 self.pool = torch.cuda.graph_pool_handle()
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             gs = []
             try:
-                with torch.cuda.graph(ga, pool=self.pool, capture_error_mode=_CAPTURE_MODE):
+                with torch.cuda.graph(ga, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                     static_out = fwd_bwd()
                 for k in (stg.stages() if stg is not None else ()):
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=self.pool, capture_error_mode=_CAPTURE_MODE):
+                    with torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                         stg.run_stage(k)
                     gs.append(g)
                 if stg is not None:
                     stg.release()
-                with torch.cuda.graph(gb, pool=self.pool, capture_error_mode=_CAPTURE_MODE):
+                with torch.cuda.graph(gb, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                     update()
             except Exception as e:
                 self.failed[full] = repr(e)
+                self.pool = None  # see _run_phase: the aborted capture's pool is not reusable
                 print(f"[iit graphs] DP phase {key} not captured ({type(e).__name__}: {str(e)[:160]}); eager")
                 torch.cuda.synchronize()
                 if stg is not None:
@@ -250,26 +258,33 @@ class GraphedTrainStep:
                 return self._eager(compute_loss, optimizer, step_fn)
             if full in self.failed:
                 return self._eager(compute_loss, optimizer, step_fn)
-            if self.pool is None:
+            if self.pool is None or os.environ.get("IIT_GRAPH_POOL") == "private":
                 self.pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(g, pool=self.pool, capture_error_mode=_CAPTURE_MODE):
+                with torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                     out = compute_loss()
                     loss = out[0] if isinstance(out, tuple) else out
                     step_fn(loss, optimizer)
                     static_out = _detach_out(out)
             except Exception as e:  # something in the phase is not capturable: keep it eager
                 self.failed[full] = repr(e)
+                # an aborted capture leaves its private memory pool unusable for the next capture (the caching
+                # allocator asserts on it): later captures get a fresh pool (graphs already captured keep theirs)
+                self.pool = None
                 import traceback
                 tb = "".join(traceback.format_exc(limit=12)) if len(self.failed) == 1 else ""
                 print(f"[iit graphs] phase {key} not captured ({type(e).__name__}: {str(e)[:160]}); "
                       f"running it eagerly\n{tb}")
                 torch.cuda.synchronize()
                 return self._eager(compute_loss, optimizer, step_fn)
+            if _RECAPTURE_ALL:  # diagnostics: a new capture drops every other graph (recaptured at next use)
+                self.graphs.clear()
             ent = self.graphs[full] = (g, static_out)
             self.captures += 1
         g, static_out = ent
+        if _SYNC_BEFORE_REPLAY:
+            torch.cuda.current_stream().synchronize()
         g.replay()
         self.replays += 1
         return _clone_out(static_out)
@@ -279,6 +294,22 @@ class GraphedTrainStep:
         loss_fn = loss_fn or self.loss_fn
         optimizer = optimizer or self.optimizer
         self.calls += 1
+        if self.stream is None:
+            return self._step(base_input, ablation_input, loss_fn, optimizer)
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        # the batch was produced on the caller's stream and is read on ours: without this the caller's next
+        # allocation (the loader's next batch) could reuse its memory while our copies / eager phases still read it
+        for t in tuple(base_input) + tuple(ablation_input):
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(self.stream)
+        try:
+            with torch.cuda.stream(self.stream):
+                return self._step(base_input, ablation_input, loss_fn, optimizer)
+        finally:
+            cur.wait_stream(self.stream)
+
+    def _step(self, base_input, ablation_input, loss_fn, optimizer):
         sb, sa, eager = self._stage(base_input, ablation_input)
         self._current_eager = eager
         try:

@@ -447,8 +447,14 @@ class BaseModelPair(ABC):
         import os
         use = self.training_args.get("graphs", None)
         if use is None:
-            use = (os.environ.get("IIT_GRAPHS", "1") != "0" and self.native()
-                   and next(self._ll_module().parameters()).is_cuda)
+            module = self._ll_module()
+            ops = getattr(module, "ops", None)
+            fused = bool(getattr(ops() if callable(ops) else ops, "fused", False))
+            # default: the fused HIP backend (bf16), whose captured phases track eager training (tests/test_graphs.py,
+            # scripts/time_to_iia.py); the torch-op backend stays eager -- with several phase graphs of it captured,
+            # a replay can go stale after a later capture (scripts/diag_graph_node.py), so it is opt-in only
+            use = (os.environ.get("IIT_GRAPHS", "1") != "0" and self.native() and fused
+                   and next(module.parameters()).is_cuda)
         if use:
             from ..engine.graphs import GraphedTrainStep
             g = GraphedTrainStep(self, optimizer, loss_fn)

@@ -368,7 +368,8 @@ class TorchOps:
         if causal:
             S = q.shape[1]
             mask = torch.ones(S, S, dtype=torch.bool, device=q.device).tril()
-            scores = torch.where(mask, scores, torch.tensor(ignore, dtype=scores.dtype, device=scores.device))
+            # a python-scalar fill (no host->device tensor copy, so the op is capturable in a HIP graph)
+            scores = scores.masked_fill(~mask, ignore)
         if hook_scores is not None:
             scores = hook_scores(scores)
         pattern = F.softmax(scores, dim=-1)

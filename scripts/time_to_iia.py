@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--num-samples", type=int, default=12000)
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--graphs", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=0, help="torch / numpy seed (the reference uses 0)")
     args = ap.parse_args()
 
     from iit_amd.data.iit_dataset import IITDataset, train_test_split
@@ -45,8 +46,8 @@ def main():
 
     pdist.init_distributed()
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
-    torch.manual_seed(0)
-    np.random.seed(0)
+    torch.manual_seed(args.seed)
+    np.random.seed(args.seed)
     cfg = gpt2_config_dict()
     if args.model == "ioi-6l":
         cfg.update(ioi_cfg)
@@ -62,7 +63,7 @@ def main():
     training_args = {"batch_size": 256, "lr": args.lr, "iit_weight": 1.0, "behavior_weight": 1.0,
                      "strict_weight": 0.4, "next_token": False, "lr_scheduler": None, "clip_grad_norm": 1.0,
                      "early_stop": True, "use_single_loss": False, "engine": args.engine,
-                     "graphs": bool(args.graphs) and args.engine == "native" and dev.type == "cuda"}
+                     "graphs": None if (args.graphs and args.engine == "native") else False}
     pair = IOI_ModelPair(ll_model=ll, hl_model=hl, corr=make_ioi_corr(cfg["n_layers"]), training_args=training_args)
 
     epochs_seen = []
@@ -79,6 +80,21 @@ def main():
             sys.stdout.flush()
 
     pair._print_and_log_metrics = log
+    if os.environ.get("TTI_NO_EVAL") == "1":  # diagnostics: no evaluation epochs between training epochs
+        def no_eval(loader, loss_fn):
+            m = pair.make_test_metrics()
+            m.update({k.get_name(): (torch.zeros(16) if k.get_name().endswith("per_token_accuracy") else 0.0)
+                      for k in m.metrics})
+            return m
+        pair._run_eval_epoch = no_eval
+    if os.environ.get("TTI_DROP_LAST") == "1":  # diagnostics: full batches only
+        orig_ml = train_set.make_loader
+
+        def ml(bs, nw=0, **kw):
+            ld = orig_ml(bs, nw, **kw)
+            ld.drop_last = True
+            return ld
+        train_set.make_loader = ml
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t_start[0] = time.perf_counter()
@@ -91,7 +107,7 @@ def main():
     first_100 = next((e for e, _, m in epochs_seen if m.get("val/IIA", 0) >= 100), None)
     steps = (last_epoch + 1) * len(train_set.make_loader(256, 0))
     rec = {"metric": "IOI training wall-clock to the reference's early-stop criterion (val/IIA = val/accuracy = 100)",
-           "model": args.model, "engine": args.engine, "dtype": args.dtype, "graphs": training_args["graphs"],
+           "model": args.model, "engine": args.engine, "dtype": args.dtype, "graphs": getattr(pair, "_graph_step", None) is not None,
            "epochs_run": last_epoch + 1, "converged": converged, "first_epoch_IIA_100": first_100,
            "wall_s": round(wall, 2), "s_per_epoch": round(wall / (last_epoch + 1), 3),
            "train_pairs_per_s": round(steps * 256 / wall, 1),
