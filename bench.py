@@ -118,22 +118,26 @@ def main():
 
     pair, opt, loss_fn, it, step_fn, train_set, test_set = setup(args, dev)
 
-    for i in range(args.warmup):
-        base, abl = next(it)
-        if i == 0 and hasattr(step_fn, "prime"):
-            step_fn.prime(base, abl, loss_fn, opt)  # capture every phase graph before timing
-        step_fn(base, abl, loss_fn, opt)
-    batches_timed = [next(it) for _ in range(args.steps)]
-    pdist.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for base, abl in batches_timed:
-        out = step_fn(base, abl, loss_fn, opt)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    pdist.barrier()
-    dt = time.perf_counter() - t0
+    import contextlib
+    # the whole loop runs on the graph runner's stream (batches included): no per-step stream handoff
+    ctx = step_fn.stream_context() if hasattr(step_fn, "stream_context") else contextlib.nullcontext()
+    with ctx:
+        for i in range(args.warmup):
+            base, abl = next(it)
+            if i == 0 and hasattr(step_fn, "prime"):
+                step_fn.prime(base, abl, loss_fn, opt)  # capture every phase graph before timing
+            step_fn(base, abl, loss_fn, opt)
+        batches_timed = [next(it) for _ in range(args.steps)]
+        pdist.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for base, abl in batches_timed:
+            out = step_fn(base, abl, loss_fn, opt)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        pdist.barrier()
+        dt = time.perf_counter() - t0
     executed = getattr(step_fn, "calls", None) or (args.warmup + args.steps)
     print(f"[bench] train steps executed in this process: {executed}", file=sys.stderr)
     dt_t = torch.tensor([dt], dtype=torch.float64, device=dev if distributed and dev.type == "cuda" else "cpu")

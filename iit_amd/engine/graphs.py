@@ -294,7 +294,9 @@ class GraphedTrainStep:
         loss_fn = loss_fn or self.loss_fn
         optimizer = optimizer or self.optimizer
         self.calls += 1
-        if self.stream is None:
+        if self.stream is None or torch.cuda.current_stream() == self.stream:
+            # (callers running their whole loop on ``self.stream`` -- bench.py, BaseModelPair.train -- skip the
+            # per-step stream handoff)
             return self._step(base_input, ablation_input, loss_fn, optimizer)
         cur = torch.cuda.current_stream()
         self.stream.wait_stream(cur)
@@ -318,6 +320,24 @@ class GraphedTrainStep:
             self._current_eager = False
 
     _current_eager = False
+
+    def stream_context(self):
+        """``with step.stream_context(): ...`` runs a whole training loop on the runner's stream (no per-step
+        stream handoff); a no-op context when graphs are off."""
+        import contextlib
+        if self.stream is None:
+            return contextlib.nullcontext()
+
+        @contextlib.contextmanager
+        def ctx():
+            cur = torch.cuda.current_stream()
+            self.stream.wait_stream(cur)
+            try:
+                with torch.cuda.stream(self.stream):
+                    yield
+            finally:
+                cur.wait_stream(self.stream)
+        return ctx()
 
     def prime(self, base_input, ablation_input, loss_fn=None, optimizer=None) -> int:
         """Capture every phase key up front (untimed warmup): force each HL / strict node in turn.

@@ -467,11 +467,15 @@ class BaseModelPair(ABC):
         self._ll_module().train()
         metrics = self.make_train_metrics()
         step = self.train_step_fn(optimizer, loss_fn)
-        for i, (base_input, ablation_input) in enumerate(progress(loader, total=len(loader),
-                                                                  disable=not pdist.is_main(), leave=False)):
-            metrics.update(step(base_input, ablation_input, loss_fn, optimizer))
-            if max_steps is not None and i + 1 >= max_steps:
-                break
+        import contextlib
+        # a graphed step runs on its own stream; the epoch's batches are produced there too (no per-step handoff)
+        ctx = step.stream_context() if hasattr(step, "stream_context") else contextlib.nullcontext()
+        with ctx:
+            for i, (base_input, ablation_input) in enumerate(progress(loader, total=len(loader),
+                                                                      disable=not pdist.is_main(), leave=False)):
+                metrics.update(step(base_input, ablation_input, loss_fn, optimizer))
+                if max_steps is not None and i + 1 >= max_steps:
+                    break
         return metrics
 
     def _run_eval_epoch(self, loader, loss_fn) -> MetricStoreCollection:

@@ -110,6 +110,9 @@ def main():
            "model": args.model, "engine": args.engine, "dtype": args.dtype, "graphs": getattr(pair, "_graph_step", None) is not None,
            "epochs_run": last_epoch + 1, "converged": converged, "first_epoch_IIA_100": first_100,
            "wall_s": round(wall, 2), "s_per_epoch": round(wall / (last_epoch + 1), 3),
+           # epoch 0 carries one-time work (GEMM autotuning, graph captures): the steady epoch is the median of the rest
+           "steady_s_per_epoch": (round(float(np.median(np.diff([t for _, t, _ in epochs_seen]))), 3)
+                                  if len(epochs_seen) > 2 else None),
            "train_pairs_per_s": round(steps * 256 / wall, 1),
            "final": {k: round(float(v), 3) for k, v in last.items()},
            "device": torch.cuda.get_device_name() if dev.type == "cuda" else "cpu",
