@@ -1110,6 +1110,50 @@ __global__ __launch_bounds__(256) void zero_chunks_kernel(float* __restrict__ ba
   for (long i = head + (n4 << 2) + threadIdx.x; i < len; i += 256) p[i] = 0.f;
 }
 
+// Zero up to 64 element ranges of ``base`` in one launch with the ranges passed BY VALUE (kernel arguments are
+// copied at launch, and at graph capture): unlike a device range table no host->device copy is needed, so a zero
+// plan first built inside a HIP-graph capture is one node instead of a fill per range.  Block b zeroes chunk
+// b - cum[r] (ZR_CHUNK floats) of the range r with cum[r] <= b < cum[r + 1].
+#define ZR_MAX 64
+#define ZR_CHUNK 16384
+struct ZeroRanges {
+  long start[ZR_MAX];
+  long len[ZR_MAX];
+  int cum[ZR_MAX + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void zero_ranges_kernel(float* __restrict__ base, const ZeroRanges zr) {
+  const int b = blockIdx.x;
+  int r = 0;
+  while (r + 1 < zr.n && zr.cum[r + 1] <= b) ++r;
+  const long off = (long)(b - zr.cum[r]) * ZR_CHUNK;
+  const long len = min((long)ZR_CHUNK, zr.len[r] - off);
+  float* p = base + zr.start[r] + off;
+  const long head = min(len, (long)((4 - (((uintptr_t)p >> 2) & 3)) & 3));
+  for (long i = threadIdx.x; i < head; i += 256) p[i] = 0.f;
+  float4* q = (float4*)(p + head);
+  const long n4 = (len - head) >> 2;
+  for (long i = threadIdx.x; i < n4; i += 256) q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (long i = head + (n4 << 2) + threadIdx.x; i < len; i += 256) p[i] = 0.f;
+}
+
+IIT_EXPORT int iit_zero_ranges(float* base, const long* starts, const long* lens, int n, void* stream) {
+  for (int i0 = 0; i0 < n; i0 += ZR_MAX) {
+    ZeroRanges zr;
+    zr.n = min(ZR_MAX, n - i0);
+    zr.cum[0] = 0;
+    for (int r = 0; r < zr.n; ++r) {
+      zr.start[r] = starts[i0 + r];
+      zr.len[r] = lens[i0 + r];
+      zr.cum[r + 1] = zr.cum[r] + (int)((lens[i0 + r] + ZR_CHUNK - 1) / ZR_CHUNK);
+    }
+    if (zr.cum[zr.n] > 0)
+      hipLaunchKernelGGL(zero_ranges_kernel, dim3(zr.cum[zr.n]), dim3(256), 0, (hipStream_t)stream, base, zr);
+  }
+  return hipGetLastError();
+}
+
 IIT_EXPORT int iit_zero_chunks(float* base, const long* chunks, int n_chunks, void* stream) {
   if (n_chunks <= 0) return 0;
   hipLaunchKernelGGL(zero_chunks_kernel, dim3(n_chunks), dim3(256), 0, (hipStream_t)stream, base, chunks);

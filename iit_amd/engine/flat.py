@@ -27,6 +27,7 @@ from __future__ import annotations
 
 from typing import Callable, Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 from torch import nn
 
@@ -35,6 +36,26 @@ _ALIGN = 64
 
 def _align(n: int) -> int:
     return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+def _subtract_ranges(ranges, holes):
+    """Sorted disjoint ``ranges`` minus sorted disjoint ``holes`` (both lists of half-open (start, end))."""
+    out = []
+    hi = 0
+    for a, b in ranges:
+        cur = a
+        while hi < len(holes) and holes[hi][1] <= cur:
+            hi += 1
+        j = hi
+        while j < len(holes) and holes[j][0] < b:
+            ha, hb = holes[j]
+            if ha > cur:
+                out.append((cur, ha))
+            cur = max(cur, hb)
+            j += 1
+        if cur < b:
+            out.append((cur, b))
+    return out
 
 
 class FlatParams:
@@ -199,27 +220,28 @@ class FlatParams:
 
     # ---------------------------------------------------------------- grads
     def zero_grad(self) -> None:
-        """Zero every gradient -- lazily for *store-claimed* parameters.
+        """Zero every gradient -- lazily for *store-claimed* parameters, and never the restricted rows.
 
         A parameter whose gradient the previous backward produced with a single overwriting GEMM (``claim``) gets
         ``.grad = None`` instead of a memset: its producer stores into the slot (beta = 0, no read of the old
         gradient) and whatever is still ``None`` when the gradients are consumed is zeroed then
         (``rebind_grads(zero_missing=True)``: the optimizer step / the DP reducer).  Everything else -- biases,
-        norms, embeddings, autograd-accumulated parameters -- is memset here as before.  For the GPT-2 / Llama
-        matrices this removes one write pass (zero) and one read pass (accumulate) over the gradient arena per
-        optimizer step."""
-        if not self._claimed:
-            self.grad.zero_()
-            self.rebind_grads()
-            return
-        key = frozenset(self._claimed)
-        if (self._zero_plan is None or self._zero_plan[0] != key) and key in self._zero_plans:
-            self._zero_plan = self._zero_plans[key]
-        if self._zero_plan is None or self._zero_plan[0] != key:
+        norms, embeddings, autograd-accumulated parameters -- is memset here.  For the GPT-2 / Llama matrices this
+        removes one write pass (zero) and one read pass (accumulate) over the gradient arena per optimizer step.
+
+        Rows excluded by :meth:`restrict_rows` (embedding rows of tokens the data never contains) are never written
+        by a backward over that data, so they stay zero without a memset (GPT-2's 50k x 768 ``W_E`` slot shrinks
+        to its ~100 live rows).  On the GPU the memset is one launch per 64 ranges with the ranges passed as kernel
+        arguments: no device table, so a plan first needed inside a graph capture is still a single node.  Plans
+        are cached per (claim set, restriction)."""
+        key = (frozenset(self._claimed), self.restrict_version)
+        plan = self._zero_plans.get(key)
+        if plan is None:
+            claimed = key[0]
             lazy = set()
             for o, n in self.slots:  # a slot is lazy only when every parameter in it is claimed
                 members = [i for i, p in enumerate(self.params) if o <= self.offset_of(p) < o + max(n, 1)]
-                if members and all(i in key for i in members):
+                if members and all(i in claimed for i in members):
                     lazy.add(o)
             ranges = []
             for o, n in self.slots:  # memset runs over the non-lazy slots (arena order)
@@ -230,24 +252,17 @@ class FlatParams:
                     ranges[-1] = (ranges[-1][0], end)
                 else:
                     ranges.append((o, end))
+            ranges = _subtract_ranges(ranges, self.inactive_ranges())
             none_ids = [i for i, p in enumerate(self.params)
                         if any(o <= self.offset_of(p) < o + max(n, 1) and o in lazy for o, n in self.slots)]
-            chunks = None
-            # one multi-span memset launch instead of one fill per range (its table is uploaded once per plan;
-            # a plan first needed inside a graph capture keeps per-range fills, no host->device copy there)
-            if self.grad.is_cuda and not torch.cuda.is_current_stream_capturing():
-                ch = []
-                for a, b in ranges:
-                    for c in range(a, b, 65536):
-                        ch.append((c, min(65536, b - c)))
-                chunks = (torch.tensor(ch, dtype=torch.int64).view(-1).to(self.grad.device), len(ch))
-            # plans are kept per claim set: a graph captured with this plan's chunk table replays its device
-            # address after the claims change (freeing the table would let the memset read a reused block)
-            self._zero_plan = self._zero_plans[key] = (key, ranges, none_ids, chunks)
-        _, ranges, none_ids, chunks = self._zero_plan
-        if chunks is not None:
+            starts = np.array([a for a, _ in ranges], dtype=np.int64)
+            lens = np.array([b - a for a, b in ranges], dtype=np.int64)
+            plan = self._zero_plans[key] = (ranges, none_ids, starts, lens)
+        self._zero_plan = plan
+        ranges, none_ids, starts, lens = plan
+        if self.grad.is_cuda:
             from ..ops import hip_kernels
-            hip_kernels.zero_chunks(self.grad, chunks[0], chunks[1])
+            hip_kernels.zero_ranges(self.grad, starts, lens)
         else:
             for a, b in ranges:
                 self.grad[a:b].zero_()

@@ -53,6 +53,7 @@ _SIGS = {
     "iit_add_bf16": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_int, c_void_p],
     "iit_device_sync": [],
     "iit_zero_chunks": [c_void_p, c_void_p, c_int, c_void_p],
+    "iit_zero_ranges": [c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "iit_rms_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_rms_bwd": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "iit_rotary": [c_void_p, c_long, c_long, c_long, c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p],
@@ -284,6 +285,18 @@ def flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, head_mask: int, scale: float,
                                _p(dz), ctypes.cast(ds, c_void_p), _p(lse), _p(dd), _p(dq), _p(dk), _p(dv),
                                ctypes.cast(gs, c_void_p), head_mask, B, S, Hq, Hkv, dh, scale, int(causal), _stream()),
            "flash_bwd")
+
+
+def zero_ranges(base, starts, lens):
+    """Zero the element ranges ``[starts[i], starts[i] + lens[i])`` of fp32 ``base``; ``starts`` / ``lens`` are
+    host int64 numpy arrays, passed to the kernel by value (capturable: no device table, no host->device copy)."""
+    import numpy as np
+    starts = np.ascontiguousarray(starts, dtype=np.int64)
+    lens = np.ascontiguousarray(lens, dtype=np.int64)
+    if CHECK_BOUNDS and len(lens):
+        assert int((starts + lens).max()) <= _avail(base) and int(starts.min()) >= 0, "zero_ranges out of bounds"
+    _check(lib().iit_zero_ranges(_p(base), starts.ctypes.data, lens.ctypes.data, len(lens), _stream()),
+           "zero_ranges")
 
 
 def zero_chunks(base, chunks, n: int):

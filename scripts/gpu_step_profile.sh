@@ -9,5 +9,5 @@ rc=$?
 echo "rocprof rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 f=$(find gpurun_out/stepprof -name "*kernel_trace.csv" | head -n 1)
-python scripts/step_breakdown.py "$f" --steps 15 --top 40 --gaps 6 > gpurun_out/stepprof/breakdown.txt && cat gpurun_out/stepprof/breakdown.txt
+python scripts/step_breakdown.py "$f" --steps 15 --top 40 --gaps 6 --dump-step gpurun_out/stepprof/one_step.txt > gpurun_out/stepprof/breakdown.txt && cat gpurun_out/stepprof/breakdown.txt
 rm -f "$f"

@@ -15,6 +15,7 @@ def main():
     ap.add_argument("--per-step-adam", type=int, default=3)
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--gaps", type=int, default=0, help="also list the N largest idle gaps (with neighbours)")
+    ap.add_argument("--dump-step", default=None, help="write the last steady step's kernel sequence to this file")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
@@ -72,6 +73,13 @@ def main():
         print(f"idle gaps: {len(gaps)} totalling {sum(g for g, _, _ in gaps) / n / 1e6:.3f} ms/step; by neighbours:")
         for (before, after), gp in tot.most_common(a.gaps):
             print(f"  {gp / n / 1e3:8.1f} us/step  after {before}  |  before {after}")
+    if a.dump_step:
+        s0, s1 = spans[-1]
+        with open(a.dump_step, "w") as f:
+            f.write("# start_us  dur_us  kernel (one steady-state step)\n")
+            for s, e, name in rows:
+                if s0 <= s < s1:
+                    f.write(f"{(s - s0) / 1e3:9.1f} {(e - s) / 1e3:8.1f}  {name[:110]}\n")
     print(f"{'ms/step':>8s} {'calls':>6s} {'avg us':>8s}  kernel")
     for name, t in per.most_common(a.top):
         print(f"{t / n / 1e6:8.3f} {calls[name] / n:6.1f} {t / calls[name] / 1e3:8.1f}  {name[:100]}")

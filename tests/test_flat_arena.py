@@ -166,26 +166,56 @@ def test_lazy_zero_grad_store_claims():
 
 
 @pytest.mark.gpu
-def test_zero_plans_outlive_claim_changes():
-    """A graph captured with one claim set's multi-span memset table replays that table's device address after
-    the claims change: every plan's table stays alive (freeing it let the memset read a reused block)."""
+def test_zero_plans_by_value_ranges_and_claim_changes():
+    """The multi-range memset passes its ranges as kernel arguments (no device table: capturable anywhere); plans
+    are cached per claim set and a plan reused after the claims change zeroes exactly its slots."""
     from iit_amd.engine.flat import FlatParams
     m = torch.nn.Sequential(torch.nn.Linear(64, 64), torch.nn.Linear(64, 64)).cuda()
     flat = FlatParams(m)
     flat.claim(m[1].weight)
+    flat.grad.fill_(3.0)
     flat.zero_grad()
-    key1, _, _, chunks1 = flat._zero_plan
-    assert chunks1 is not None
-    table1 = chunks1[0].clone()
+    plan1 = flat._zero_plan
+    assert m[1].weight.grad is None and float(flat.grad_view(m[0].weight).abs().sum()) == 0.0
+    assert float(flat.grad_view(m[1].weight).abs().sum()) > 0  # lazy slot untouched
     flat.claim(m[0].weight)
     flat.zero_grad()
-    assert flat._zero_plan[0] != key1
-    assert flat._zero_plans[key1][3][0] is chunks1[0] and torch.equal(chunks1[0], table1)
+    assert flat._zero_plan is not plan1
     flat.grad.fill_(3.0)
     flat.unclaim(m[0].weight)
-    flat.zero_grad()  # back to the first claim set: its plan (and table) is reused
-    assert flat._zero_plan[3][0] is chunks1[0]
+    flat.zero_grad()  # back to the first claim set: its plan is reused
+    assert flat._zero_plan is plan1
     assert float(flat.grad_view(m[0].weight).abs().sum()) == 0.0 and m[1].weight.grad is None
+    # inside a capture: one node, replayed
+    flat.grad.fill_(5.0)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        flat.zero_grad()
+    flat.grad.fill_(5.0)
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(flat.grad_view(m[0].weight).abs().sum()) == 0.0 and float(flat.grad_view(m[0].bias).abs().sum()) == 0.0
+
+
+def test_zero_grad_skips_restricted_rows():
+    """Rows excluded by restrict_rows (never written by a backward over the data) are left out of the memset;
+    every other element is zeroed, and lifting the restriction zeroes them again."""
+    from iit_amd.engine.flat import FlatParams
+    emb = torch.nn.Embedding(10, 8)
+    lin = torch.nn.Linear(8, 4)
+    m = torch.nn.ModuleDict({"e": emb, "l": lin})
+    flat = FlatParams(m)
+    assert flat.restrict_rows(emb.weight, torch.tensor([1, 4, 5]))
+    flat.grad.fill_(2.0)
+    flat.zero_grad()
+    g = flat.grad_view(emb.weight)
+    live = torch.zeros(10, dtype=torch.bool)
+    live[[1, 4, 5]] = True
+    assert float(g[live].abs().sum()) == 0.0 and bool((g[~live] == 2.0).all())
+    assert float(flat.grad_view(lin.weight).abs().sum()) == 0.0 and float(flat.grad_view(lin.bias).abs().sum()) == 0.0
+    flat.restrict_rows(emb.weight, None)
+    flat.zero_grad()
+    assert float(flat.grad.abs().sum()) == 0.0
 
 
 def test_rebind_zeroes_missing_slots_only():
