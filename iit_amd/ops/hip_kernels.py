@@ -54,6 +54,7 @@ _SIGS = {
     "iit_device_sync": [],
     "iit_zero_chunks": [c_void_p, c_void_p, c_int, c_void_p],
     "iit_zero_ranges": [c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "iit_colsum_multi": [c_void_p] * 6 + [c_int, c_void_p],
     "iit_rms_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_rms_bwd": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "iit_rotary": [c_void_p, c_long, c_long, c_long, c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p],
@@ -348,6 +349,32 @@ def colsum_accum(x, ld, out, T, N):
     if CHECK_BOUNDS:
         _bounds("colsum", ("x", x, T, N, ld), ("out", out, 1, N, N))
     _check(lib().iit_colsum_accum(_p(x), int(x.dtype == torch.float32), ld, _p(out), T, N, _stream()), "colsum")
+
+
+def colsum_vec_ok(x, ld, out, N) -> bool:
+    """Whether ``colsum_multi`` can take this sum (vector-aligned rows of a bf16 / fp32 operand)."""
+    cpt = 4 if x.dtype == torch.float32 else 8
+    return (x.dtype in (torch.float32, torch.bfloat16) and out.dtype == torch.float32 and N % cpt == 0
+            and ld % cpt == 0 and x.data_ptr() % 16 == 0)
+
+
+def colsum_multi(items):
+    """``out_i[n] += sum_t x_i[t][n]`` for every ``(x, ld, out, T, N)`` in ``items`` -- one launch per 32 sums,
+    descriptors passed by value (capturable).  Every item must satisfy :func:`colsum_vec_ok`."""
+    import numpy as np
+    if not items:
+        return
+    xs = np.array([it[0].data_ptr() for it in items], dtype=np.int64)
+    outs = np.array([it[2].data_ptr() for it in items], dtype=np.int64)
+    lds = np.array([it[1] for it in items], dtype=np.int64)
+    Ts = np.array([it[3] for it in items], dtype=np.int32)
+    Ns = np.array([it[4] for it in items], dtype=np.int32)
+    f32s = np.array([int(it[0].dtype == torch.float32) for it in items], dtype=np.int32)
+    if CHECK_BOUNDS:
+        for x, ld, out, T, N in items:
+            _bounds("colsum_multi", ("x", x, T, N, ld), ("out", out, 1, N, N))
+    _check(lib().iit_colsum_multi(xs.ctypes.data, outs.ctypes.data, lds.ctypes.data, Ts.ctypes.data, Ns.ctypes.data,
+                                  f32s.ctypes.data, len(items), _stream()), "colsum_multi")
 
 
 def colsum3_accum(x, ld, outs, T, N):

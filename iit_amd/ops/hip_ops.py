@@ -81,6 +81,50 @@ def _done(*params):
             grad_hooks.notify(p)
 
 
+class _BiasSums:
+    """Bias-gradient column sums of one backward pass, batched.
+
+    Each fused backward adds ``colsum(dY)`` into its bias gradient; as separate launches these are ~36 small
+    kernels per backward (one per bias).  Here they are queued -- the bf16 / fp32 operands stay referenced, and
+    no kernel writes them after their producer -- and summed by ONE launch per 32 biases at the end of the
+    autograd backward pass (an engine final callback, so every ``backward()`` -- eager, graph-captured, a staged
+    DP segment -- ends with its biases complete).  The biases are reported to the data-parallel reducer when
+    their sums land.  ``IIT_DEFER_BIAS_SUMS=0`` restores one launch per bias."""
+
+    def __init__(self):
+        self.items, self.params, self.stream = [], [], None
+
+    def add(self, x, ld, out, T, N, *params):
+        if (_DEFER_BIAS_SUMS and x.is_cuda and K.colsum_vec_ok(x, ld, out, N)
+                and (self.items or self._arm())):
+            self.items.append((x, ld, out, T, N))
+            self.params.extend(params)
+            return
+        K.colsum_accum(x, ld, out, T, N)
+        _done(*params)
+
+    def _arm(self) -> bool:
+        try:  # only inside an autograd backward pass; elsewhere the sum runs immediately
+            torch.autograd.Variable._execution_engine.queue_callback(self.flush)
+        except RuntimeError:
+            return False
+        self.stream = torch.cuda.current_stream()
+        return True
+
+    def flush(self) -> None:
+        if not self.items:
+            return
+        items, params, stream = self.items, self.params, self.stream
+        self.items, self.params, self.stream = [], [], None
+        with torch.cuda.stream(stream):
+            K.colsum_multi(items)
+        _done(*params)
+
+
+_DEFER_BIAS_SUMS = os.environ.get("IIT_DEFER_BIAS_SUMS", "1") != "0"
+_BIAS_SUMS = _BiasSums()
+
+
 # ============================================================================ shadow weights
 class ModelShadow:
     """bf16 compute copies of a HookedTransformer's matrices, in the layouts the GEMMs read.
@@ -455,10 +499,11 @@ class QKVFn(Function):
         gbs = [_grad_slot(bp) for bp in (b_Q, b_K, b_V)]
         if all(gb is not None for gb in gbs):
             if all(gb.is_contiguous() for gb in gbs) and _packed3(*gbs, HD):
-                K.colsum_accum(g, 3 * HD, gbs[0], T, 3 * HD)
+                _BIAS_SUMS.add(g, 3 * HD, gbs[0], T, 3 * HD, b_Q, b_K, b_V)
             else:
                 K.colsum3_accum(g, 3 * HD, gbs, T, HD)
-        _done(W_Q, W_K, W_V, b_Q, b_K, b_V)
+                _done(b_Q, b_K, b_V)
+        _done(W_Q, W_K, W_V)
         return (dx.view(B, S, d),) + (None,) * 8
 
 
@@ -731,8 +776,8 @@ class LinearFn(Function):
                 _settle_claim(choice, W)
         gb = _grad_slot(b)
         if gb is not None:
-            K.colsum_accum(g2, ldg, gb, T, N)
-        _done(W, b)
+            _BIAS_SUMS.add(g2, ldg, gb, T, N, b)
+        _done(W)
         return dx, None, None, None, None, gres, None
 
 
@@ -784,8 +829,10 @@ class MLPInFn(Function):
                 _settle_claim(choice, W_in)
         gb = _grad_slot(b_in)
         if gb is not None and not _bias_sum_done(gpre if gpost is None else None, b_in):
-            K.colsum_accum(dpre, dm, gb, T, dm)
-        _done(W_in, b_in)
+            _BIAS_SUMS.add(dpre, dm, gb, T, dm, b_in)
+        else:
+            _done(b_in)
+        _done(W_in)
         return dx.view(*lead, d), None, None, None, None
 
 
@@ -857,8 +904,8 @@ class MLPOutGeluFn(Function):
                 _settle_claim(choice, W)
         gb = _grad_slot(b)
         if gb is not None:
-            K.colsum_accum(g2, ldg, gb, T, N)
-        _done(W, b)
+            _BIAS_SUMS.add(g2, ldg, gb, T, N, b)
+        _done(W)
         return dpre, None, None, None, None, None, gy, None, None
 
 
