@@ -298,6 +298,11 @@ class GraphedTrainStep:
             # (callers running their whole loop on ``self.stream`` -- bench.py, BaseModelPair.train -- skip the
             # per-step stream handoff)
             return self._step(base_input, ablation_input, loss_fn, optimizer)
+        if not self._handoff_warned:
+            self._handoff_warned = True
+            print("[iit graphs] train step called from another stream: run the loop (and any evaluation between "
+                  "steps) inside `with step.stream_context():` -- mixing streams between captured phases and other "
+                  "work has been seen to corrupt later replays (scripts/diag_graph_node.py)")
         cur = torch.cuda.current_stream()
         self.stream.wait_stream(cur)
         # the batch was produced on the caller's stream and is read on ours: without this the caller's next
@@ -320,6 +325,7 @@ class GraphedTrainStep:
             self._current_eager = False
 
     _current_eager = False
+    _handoff_warned = False
 
     def stream_context(self):
         """``with step.stream_context(): ...`` runs a whole training loop on the runner's stream (no per-step

@@ -409,7 +409,12 @@ class BaseModelPair(ABC):
         epoch = start_epoch
         for epoch in progress(range(start_epoch, epochs), disable=not pdist.is_main()):
             train_metrics = self._run_train_epoch(train_loader, loss_fn, optimizer, max_steps=max_steps)
-            test_metrics = self._run_eval_epoch(test_loader, loss_fn)
+            # evaluation on the same stream as the (graphed) training steps: every kernel of the run is ordered on
+            # one stream, so the caching allocator never hands memory across streams between epochs
+            step = getattr(self, "_graph_step", None)
+            import contextlib
+            with (step.stream_context() if step is not None else contextlib.nullcontext()):
+                test_metrics = self._run_eval_epoch(test_loader, loss_fn)
             self._reduce_metrics(train_metrics)
             self._reduce_metrics(test_metrics)
             if lr_scheduler is not None:
@@ -448,13 +453,11 @@ class BaseModelPair(ABC):
         use = self.training_args.get("graphs", None)
         if use is None:
             module = self._ll_module()
-            ops = getattr(module, "ops", None)
-            fused = bool(getattr(ops() if callable(ops) else ops, "fused", False))
-            # default: the fused HIP backend (bf16), whose captured phases track eager training (tests/test_graphs.py,
-            # scripts/time_to_iia.py); the torch-op backend stays eager -- with several phase graphs of it captured,
-            # a replay can go stale after a later capture (scripts/diag_graph_node.py), so it is opt-in only
-            use = (os.environ.get("IIT_GRAPHS", "1") != "0" and self.native() and fused
-                   and next(module.parameters()).is_cuda)
+            # default on for native GPU models up to a few billion parameters (each phase graph keeps its
+            # activations in the graph memory pool; the 8B Llama runs its phases eagerly unless asked)
+            n_params = sum(p.numel() for p in module.parameters())
+            use = (os.environ.get("IIT_GRAPHS", "1") != "0" and self.native()
+                   and next(module.parameters()).is_cuda and n_params < 2_000_000_000)
         if use:
             from ..engine.graphs import GraphedTrainStep
             g = GraphedTrainStep(self, optimizer, loss_fn)

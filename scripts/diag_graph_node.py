@@ -48,9 +48,12 @@ def run(mode, hl_name, only_iit):
             pair._phase_runner = sel
     out_l = []
     nsteps = int(os.environ.get("NSTEPS", "12"))
-    for base, abl in (batches * 2)[:nsteps]:
-        out = step(base, abl, pair.loss_fn, opt)
-        out_l.append(torch.stack([out[k] for k in sorted(out)]))
+    import contextlib
+    ctx = step.stream_context() if (mode == "graphs" and os.environ.get("CTX") == "1") else contextlib.nullcontext()
+    with ctx:
+        for base, abl in (batches * 2)[:nsteps]:
+            out = step(base, abl, pair.loss_fn, opt)
+            out_l.append(torch.stack([out[k] for k in sorted(out)]))
     torch.cuda.synchronize()
     if os.environ.get("PARAMS"):
         return torch.stack(out_l).cpu(), {n: p.detach().clone() for n, p in pair.ll_model.named_parameters()}

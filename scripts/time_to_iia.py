@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--epochs", type=int, default=1000)
     ap.add_argument("--num-samples", type=int, default=12000)
     ap.add_argument("--lr", type=float, default=1e-4)
-    ap.add_argument("--graphs", type=int, default=1)
+    ap.add_argument("--graphs", type=int, default=1, help="1: engine default, 2: force graphs, 0: eager")
     ap.add_argument("--seed", type=int, default=0, help="torch / numpy seed (the reference uses 0)")
     args = ap.parse_args()
 
@@ -63,7 +63,7 @@ def main():
     training_args = {"batch_size": 256, "lr": args.lr, "iit_weight": 1.0, "behavior_weight": 1.0,
                      "strict_weight": 0.4, "next_token": False, "lr_scheduler": None, "clip_grad_norm": 1.0,
                      "early_stop": True, "use_single_loss": False, "engine": args.engine,
-                     "graphs": None if (args.graphs and args.engine == "native") else False}
+                     "graphs": (None if args.graphs == 1 else bool(args.graphs)) if args.engine == "native" else False}
     pair = IOI_ModelPair(ll_model=ll, hl_model=hl, corr=make_ioi_corr(cfg["n_layers"]), training_args=training_args)
 
     epochs_seen = []
