@@ -120,7 +120,8 @@ def main():
 
     import contextlib
     # the whole loop runs on the graph runner's stream (batches included): no per-step stream handoff
-    ctx = step_fn.stream_context() if hasattr(step_fn, "stream_context") else contextlib.nullcontext()
+    ctx = (step_fn.stream_context() if hasattr(step_fn, "stream_context") and os.environ.get("IIT_BENCH_STREAM_CTX") != "0"
+           else contextlib.nullcontext())
     with ctx:
         for i in range(args.warmup):
             base, abl = next(it)

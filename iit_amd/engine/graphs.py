@@ -69,6 +69,16 @@ def _detach_out(out):
     return out.detach()
 
 
+def _fused_backend(pair) -> bool:
+    """Whether the pair's LL model runs on the fused HIP op backend (its backward writes arena gradients itself)."""
+    module = pair._ll_module() if hasattr(pair, "_ll_module") else getattr(pair, "ll_model", None)
+    ops = getattr(module, "ops", None)
+    try:
+        return bool(getattr(ops() if callable(ops) else ops, "fused", False))
+    except Exception:  # noqa: BLE001 - models without an op backend
+        return False
+
+
 class GraphedTrainStep:
     def __init__(self, pair, optimizer=None, loss_fn=None, warmup: int = 1, enabled: Optional[bool] = None):
         self.pair = pair
@@ -95,11 +105,17 @@ class GraphedTrainStep:
         self.graphs: Dict[Tuple, Tuple[torch.cuda.CUDAGraph, object]] = {}
         self.seen: Dict[Tuple, int] = {}
         self.pool = None  # shared graph memory pool, created at the first capture
-        # every step -- eager warm-up phases, captures and replays -- runs on this one stream: autograd's
-        # AccumulateGrad nodes run on the stream they were created on, so a node made by an eager phase on the
-        # default stream and kept alive would accumulate *outside* a later capture (silently missing from the
-        # graph); one stream for everything keeps them inside
-        self.stream = torch.cuda.Stream() if (enabled and torch.cuda.is_available()) else None
+        # torch-op backend: every step -- eager warm-ups, captures and replays -- runs on one dedicated stream.
+        # Autograd's AccumulateGrad nodes run on the stream they were created on, so a node made by an eager phase
+        # on the default stream and kept alive would accumulate *outside* a later capture (silently missing from
+        # the graph).  The fused HIP backend writes every arena gradient from its own backward functions (no
+        # AccumulateGrad) and keeps the plain arrangement -- eager on the caller's stream, captures on torch's
+        # capture stream -- which also keeps the stream count low: a dedicated stream next to gloo's pool streams
+        # deadlocked the two-rank gloo rehearsal on one GPU (scripts/gpu_dp_rehearsal_debug.sh).
+        # ``IIT_GRAPH_STREAM=1|0`` forces it on / off.
+        mode = os.environ.get("IIT_GRAPH_STREAM", "auto")
+        dedicated = mode == "1" or (mode == "auto" and not _fused_backend(pair))
+        self.stream = torch.cuda.Stream() if (enabled and torch.cuda.is_available() and dedicated) else None
         if enabled:
             from ..ops.gemm_dispatch import select_graph_safe_blas
             select_graph_safe_blas()
