@@ -38,3 +38,34 @@ def test_pvr_scripts(tmp_path):
          "--hook-points", *hp, "--out-dir", str(tmp_path / "plots")])
     assert correct.shape == (1, 4) and leaky.shape == (1, 4) and leaky_all.shape == (1, 12)
     assert (tmp_path / "plots" / "bin" / "leaky_accs_all.npy").exists()
+
+
+def test_time_to_iia_script_runs_and_reports(tmp_path, capsys, monkeypatch):
+    """scripts/time_to_iia.py: the train_ioi.py loop with per-epoch timing and one JSON record (tiny CPU run)."""
+    import json
+    import runpy
+    monkeypatch.setattr(sys, "argv", ["time_to_iia.py", "--model", "ioi-6l", "--epochs", "3", "--num-samples", "80",
+                                      "--graphs", "0"])
+    monkeypatch.chdir(tmp_path)
+    runpy.run_path(os.path.join(ROOT, "scripts", "time_to_iia.py"), run_name="__main__")
+    rec = json.loads([l for l in capsys.readouterr().out.splitlines() if l.startswith("{")][-1])
+    assert rec["epochs_run"] == 3 and rec["engine"] == "native" and not rec["graphs"]
+    assert rec["steady_s_per_epoch"] is not None and rec["wall_s"] > 0
+    assert {"train/iit_loss", "val/IIA", "val/accuracy"} <= set(rec["final"])
+
+
+def test_train_step_fn_is_plain_on_cpu():
+    """Graph capture is a GPU feature: on CPU the training loop calls run_train_step directly."""
+    import torch
+    from iit_amd.model_pairs import IOI_ModelPair
+    from iit_amd.models.config import gpt2_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.tasks.ioi import make_ioi_corr, make_ioi_dataset_and_hl
+    cfg = gpt2_config_dict()
+    cfg.update(n_layers=2, d_model=16, n_heads=2, d_head=8, d_mlp=32, device="cpu")
+    ll = HookedTransformer(cfg)
+    ds, hl = make_ioi_dataset_and_hl(64, ll, device="cpu")
+    pair = IOI_ModelPair(hl, ll, make_ioi_corr(2), training_args={"lr_scheduler": None})
+    opt = torch.optim.Adam(ll.parameters(), lr=1e-3)
+    step = pair.train_step_fn(opt, pair.loss_fn)
+    assert step == pair.run_train_step
