@@ -115,7 +115,11 @@ class GradReducer:
         """Async all-reduce of arena elements [s, e): rows-restricted parameters compactly, the rest in place."""
         op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
         pieces, cur = [], s
-        for i, (o, n, width, rows) in sorted(self._subsets.items(), key=lambda kv: kv[1][0]):
+        subsets = self.__dict__.get("_subsets_sorted")
+        if subsets is None or subsets[0] != len(self._subsets):
+            subsets = self._subsets_sorted = (len(self._subsets),
+                                              sorted(self._subsets.items(), key=lambda kv: kv[1][0]))
+        for i, (o, n, width, rows) in subsets[1]:
             if o >= s and o + n <= e:
                 if o > cur:
                     pieces.append(("dense", cur, o))
@@ -146,12 +150,20 @@ class GradReducer:
             if bs >= s and be <= e:
                 self._launch(b)
 
-    def segment_buckets(self, cuts) -> None:
-        """Re-bucket so every arena offset in ``cuts`` is a bucket edge (segment ranges reduce exactly)."""
+    def segment_buckets(self, cuts, whole_segments: bool = True) -> None:
+        """Re-bucket so every arena offset in ``cuts`` is a bucket edge (segment ranges reduce exactly).
+
+        ``whole_segments`` (the staged backward's default): one bucket per segment.  Every bucket of a segment is
+        launched at the same moment (``launch_range`` after the segment's graph), so splitting a segment only adds
+        collective calls -- host time between the segment graphs -- without adding overlap; one large all-reduce
+        per segment is also RCCL's most efficient message size on xGMI."""
         edges = sorted({0, self.flat.numel, *[int(c) for c in cuts]})
         per = max(64, int(self._bucket_bytes) // 4)
         out = []
         for a, b in zip(edges[:-1], edges[1:]):
+            if whole_segments:
+                out.append((a, b))
+                continue
             pieces, end = [], b  # slot-aligned pieces of <= bucket size, back to front
             while end > a:
                 start = max(a, end - per)
@@ -164,6 +176,7 @@ class GradReducer:
                 pieces.append((start, end))
                 end = start
             out.extend(pieces)
+        out.sort(key=lambda r: -r[0])  # reverse arena order, like ``FlatParams.buckets``
         self.buckets = out
         self._param_bucket = []
         self._bucket_count = [0] * len(self.buckets)
@@ -225,6 +238,7 @@ class GradReducer:
         n = param.numel()
         width = param.shape[-1]
         self._subsets[i] = (o, n, width, rows.to(self.flat.grad.device).long().unique())
+        self.__dict__.pop("_subsets_sorted", None)
 
     def remove(self):
         for h in self._hooks:
