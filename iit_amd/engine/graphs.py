@@ -396,3 +396,89 @@ class GraphedTrainStep:
         if getattr(self.pair, "_phase_runner", None) == self._run_phase:
             self.pair._phase_runner = None
         self.graphs.clear()
+
+
+class GraphedEvalStep:
+    """Evaluation steps (``pair.run_eval_step``) captured as HIP graphs, one per sampled HL node.
+
+    An eval step is a fixed kernel sequence for a given HL node (the source / base interventions and the
+    behaviour forward, no autograd, no optimizer), so -- like :class:`GraphedTrainStep` -- the node is drawn from
+    the pair's RNG first (the same single draw ``run_eval_step`` makes), the batch is copied into static
+    buffers, and the step for that node is captured once (after ``warmup`` eager runs) and replayed.  The metric
+    outputs are cloned after each replay.  Batches of another shape (an epoch's short tail) run eagerly; a pair
+    whose eval step does not draw exactly one HL node stays eager."""
+
+    def __init__(self, pair, loss_fn, warmup: int = 1, stream=None):
+        self.pair = pair
+        self.loss_fn = loss_fn
+        self.warmup = warmup
+        self.stream = stream  # capture stream (the training runner's dedicated stream, or torch's default)
+        self.graphs: Dict[Tuple, Tuple[torch.cuda.CUDAGraph, dict]] = {}
+        self.seen: Dict[Tuple, int] = {}
+        self.failed: Dict[Tuple, str] = {}
+        self.pool = None
+        self._static = None
+        self._sig = None
+        self.ok = True  # False once a step draws a number of HL nodes other than one
+        self.replays = 0
+
+    def _eager(self, base, abl):
+        return self.pair.run_eval_step(base, abl, self.loss_fn)
+
+    def __call__(self, base, abl):
+        pair = self.pair
+        if not self.ok:
+            return self._eager(base, abl)
+        node = pair.sample_hl_name()
+        draws = [0]
+
+        def fixed(_node=node):
+            draws[0] += 1
+            return _node
+        own = pair.__dict__.get("sample_hl_name")  # an instance-level sampler (tests, prime) is restored after
+        pair.sample_hl_name = fixed
+        try:
+            out = self._run(node, base, abl)
+        finally:
+            if own is None:
+                del pair.sample_hl_name
+            else:
+                pair.sample_hl_name = own
+        if draws[0] != 1:  # the step's sampling is not the single draw this runner replays: go eager from now on
+            self.ok = False
+        return out
+
+    def _run(self, node, base, abl):
+        sig = tuple((tuple(t.shape), t.dtype, t.device) for t in tuple(base) + tuple(abl))
+        if self._static is None:
+            self._static = (tuple(t.clone() for t in base), tuple(t.clone() for t in abl))
+            self._sig = sig
+        if sig != self._sig:
+            return self._eager(base, abl)
+        sb, sa = self._static
+        for d, src in zip(sb + sa, tuple(base) + tuple(abl)):
+            d.copy_(src, non_blocking=True)
+        key = (node.name, sig)
+        ent = self.graphs.get(key)
+        if ent is None:
+            n = self.seen.get(key, 0)
+            if n < self.warmup or key in self.failed:
+                self.seen[key] = n + 1
+                return self._eager(sb, sa)
+            if self.pool is None:
+                self.pool = torch.cuda.graph_pool_handle()
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
+                    static_out = self._eager(sb, sa)
+            except Exception as e:  # not capturable: keep this node eager
+                self.failed[key] = repr(e)
+                self.pool = None
+                print(f"[iit graphs] eval step for {node.name} not captured ({type(e).__name__}: {str(e)[:160]}); eager")
+                torch.cuda.synchronize()
+                return self._eager(sb, sa)
+            ent = self.graphs[key] = (g, static_out)
+        g, static_out = ent
+        g.replay()
+        self.replays += 1
+        return {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in static_out.items()}

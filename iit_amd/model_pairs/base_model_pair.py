@@ -485,11 +485,29 @@ class BaseModelPair(ABC):
         self._ll_module().eval()
         metrics = self.make_test_metrics()
         from ..engine import prefetch
-        batches = prefetch.prefetched_batches(self, loader) if prefetch.supported(self) else loader
+        use_prefetch = prefetch.supported(self)
+        batches = prefetch.prefetched_batches(self, loader) if use_prefetch else loader
+        step = self.eval_step_fn(loss_fn) if not use_prefetch else None
         with torch.no_grad():
             for base_input, ablation_input in batches:
-                metrics.update(self.run_eval_step(base_input, ablation_input, loss_fn))
+                if step is not None:
+                    metrics.update(step(base_input, ablation_input))
+                else:
+                    metrics.update(self.run_eval_step(base_input, ablation_input, loss_fn))
         return metrics
+
+    def eval_step_fn(self, loss_fn):
+        """The graphed evaluation step (:class:`iit_amd.engine.graphs.GraphedEvalStep`) when training runs graphed
+        phases (``train_step_fn``), else None (plain ``run_eval_step``).  ``training_args["eval_graphs"]=False``
+        keeps evaluation eager."""
+        train_step = getattr(self, "_graph_step", None)
+        if train_step is None or not self.training_args.get("eval_graphs", True):
+            return None
+        ev = getattr(self, "_graph_eval", None)
+        if ev is None or ev.loss_fn is not loss_fn:
+            from ..engine.graphs import GraphedEvalStep
+            ev = self._graph_eval = GraphedEvalStep(self, loss_fn, stream=train_step.stream)
+        return ev
 
     @staticmethod
     def _reduce_metrics(collection: MetricStoreCollection) -> None:
