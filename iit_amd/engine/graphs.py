@@ -69,6 +69,31 @@ def _detach_out(out):
     return out.detach()
 
 
+class _CaptureGC:
+    """Context for a graph capture: collect cyclic garbage first, keep the collector off during the capture.
+
+    Objects holding CUDA graphs or graph memory pools (earlier runners, pairs referencing them in a cycle) may be
+    cyclic garbage; destroying one *inside* another capture is an illegal HIP call that aborts the process, and
+    the collector can run at any allocation.  So it runs before, never during, a capture."""
+
+    def __init__(self, collect: bool = True):
+        self.collect = collect
+
+    def __enter__(self):
+        import gc
+        if self.collect:
+            gc.collect()
+        self._was = gc.isenabled()
+        gc.disable()
+        return self
+
+    def __exit__(self, *exc):
+        import gc
+        if self._was:
+            gc.enable()
+        return False
+
+
 def _fused_backend(pair) -> bool:
     """Whether the pair's LL model runs on the fused HIP op backend (its backward writes arena gradients itself)."""
     module = pair._ll_module() if hasattr(pair, "_ll_module") else getattr(pair, "ll_model", None)
@@ -230,16 +255,16 @@ class GraphedTrainStep:
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             gs = []
             try:
-                with torch.cuda.graph(ga, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
+                with _CaptureGC(), torch.cuda.graph(ga, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                     static_out = fwd_bwd()
                 for k in (stg.stages() if stg is not None else ()):
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
+                    with _CaptureGC(), torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                         stg.run_stage(k)
                     gs.append(g)
                 if stg is not None:
                     stg.release()
-                with torch.cuda.graph(gb, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
+                with _CaptureGC(), torch.cuda.graph(gb, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                     update()
             except Exception as e:
                 self.failed[full] = repr(e)
@@ -278,7 +303,7 @@ class GraphedTrainStep:
                 self.pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
+                with _CaptureGC(), torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                     out = compute_loss()
                     loss = out[0] if isinstance(out, tuple) else out
                     step_fn(loss, optimizer)
@@ -469,7 +494,7 @@ class GraphedEvalStep:
                 self.pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
+                with _CaptureGC(), torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                     static_out = self._eager(sb, sa)
             except Exception as e:  # not capturable: keep this node eager
                 self.failed[key] = repr(e)

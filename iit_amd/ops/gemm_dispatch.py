@@ -220,8 +220,9 @@ def _time(fn, reps: int = 10) -> float:
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     try:
+        from ..engine.graphs import _CaptureGC
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        with _CaptureGC(collect=False), torch.cuda.graph(g, capture_error_mode="thread_local"):
             for _ in range(reps):
                 fn()
         g.replay()
