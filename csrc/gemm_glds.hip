@@ -50,6 +50,11 @@ struct G2Args {
   int M, N, K, bias_cols;
   int k_per_split;  // split-K: blockIdx.y owns [y * k_per_split, (y + 1) * k_per_split); partials added atomically
   float* csum;      // E_DGELU: optional column sums of the stored output (the MLP input-bias gradient), += atomically
+  // reduction split-K (fp32 accumulate / store epilogues, gridDim.y > 1): every split stores its partial tile to
+  // ws[(split * tiles + tile) * BM * BN] and takes a ticket on counters[tile]; the last arriver sums the partials
+  // in split order (deterministic) and runs the normal epilogue, then resets the ticket for the next launch
+  float* ws;
+  int* counters;
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -368,8 +373,65 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  if constexpr (EPI == E_F32_ACC || EPI == E_F32_STORE) {
+    if (p.ws != nullptr) {
+      // Partial tile in MFMA register order (one 16-B chunk per lane per accumulator: 1 KiB coalesced per wave),
+      // published without any L2 writeback / invalidate: write-through (sc1) stores, drained with vmcnt(0) before
+      // the ticket, and sc1 loads on the reading side (the XCDs' L2s are not coherent with each other; a
+      // device-scope fence here would write back / invalidate whole L2s under every other tile's main loop).
+      const long tile_elems = (long)BM * BN;
+      f32x4* mine = (f32x4*)(p.ws + ((long)blockIdx.y * gridDim.x + t) * tile_elems);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(mine + (i * TN + j) * NT + tid), "v"(acc[i][j])
+                       : "memory");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // every thread's partial has landed; also retires the main loop's LDS use
+      int* flag = (int*)smem;
+      if (tid == 0) {
+        const int last = atomicAdd(p.counters + t, 1) == (int)gridDim.y - 1;
+        if (last) p.counters[t] = 0;  // every split has arrived: re-arm the ticket for the next launch
+        flag[0] = last;
+      }
+      __syncthreads();
+      if (!flag[0]) return;
+      f32x4 sum[TM][TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) sum[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int sp = 0; sp < (int)gridDim.y; ++sp) {  // fixed order: bit-identical whoever arrives last
+        if (sp == (int)blockIdx.y) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) sum[i][j] += acc[i][j];
+          continue;
+        }
+        const f32x4* other = (const f32x4*)(p.ws + ((long)sp * gridDim.x + t) * tile_elems);
+        f32x4 v[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[i][j]) : "v"(other + (i * TN + j) * NT + tid)
+                         : "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) sum[i][j] += v[i][j];
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = sum[i][j];
+    }
+  }
   if constexpr (EPI == E_F32_ACC) {
-    if (gridDim.y > 1) {  // split-K partial: atomics straight from the MFMA layout (16 lanes = 16 consecutive
+    if (gridDim.y > 1 && p.ws == nullptr) {  // split-K partial: atomics straight from the MFMA layout (16 lanes = 16 consecutive
                           // columns, so each wave instruction hits 4 rows x 64 B)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -524,22 +586,29 @@ hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
     case 8: return launch<96, 96, 4, AKM, BKM, EPI>(a, s);
     // 128 x 96: the 4096 x 768 outputs (W_O / W_out forward, dX of QKV / W_O / W_in) are exactly 256 tiles
     case 9: return launch<128, 96, 4, AKM, BKM, EPI>(a, s);
+    // 96 x 192 / 192 x 96 (2 x 2 waves of 48 x 96 / 96 x 48): the weight gradients with a 2-way reduction split
+    // -- 256 workgroups for [768][3072] / [3072][768], a third fewer operand bytes per CU than 96 x 96
+    case 10: return launch<96, 192, 4, AKM, BKM, EPI>(a, s);
+    case 11: return launch<192, 96, 4, AKM, BKM, EPI>(a, s);
     default: return launch<128, 128, 4, AKM, BKM, EPI>(a, s);
   }
 }
 
 }  // namespace
 
-#define IIT_GLDS_TILES 10
-static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256, 96, 128};
-static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128, 96, 96};
+#define IIT_GLDS_TILES 12
+static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256, 96, 128, 96, 192};
+static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128, 96, 96, 192, 96};
 
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,
                                 long lda, long ldb, long ldc, long ldc2, long ldr, int M, int N, int K, int mode,
-                                int epi, int bias_cols, int tile, int splits) {
+                                int epi, int bias_cols, int tile, int splits, int reduce) {
   if (tile < 0 || tile >= IIT_GLDS_TILES) return 0;
-  if (splits < 1 || (splits > 1 && (epi != E_F32_ACC || K % (64 * splits)))) return 0;
+  // atomic split-K: fp32 accumulate only; reduction split-K (``reduce``): fp32 accumulate or store
+  const bool split_epi = epi == E_F32_ACC || (reduce && epi == E_F32_STORE);
+  if (splits < 1 || (splits > 1 && (!split_epi || K % (64 * splits)))) return 0;
+  if (reduce && splits < 2) return 0;
   if (!(mode == 0 || mode == 2 || mode == 3)) return 0;
   const bool epi_ok = mode == 3 ? (epi == E_F32_ACC || epi == E_F32_STORE)
                                 : (epi == E_BF16 || epi == E_BF16_BIAS3 || epi == E_F32_RESID || epi == E_GELU ||
@@ -560,15 +629,20 @@ IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, con
 IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, const float* bias0, const float* bias1,
                              const float* bias2, const float* resid, long lda, long ldb, long ldc, long ldc2, long ldr,
                              int M, int N, int K, int mode, int epi, int bias_cols, int tile, int splits,
-                             float* csum, void* stream) {
-  if (!iit_gemm_glds_ok(A, B, C, C2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits))
+                             float* csum, float* ws, int* counters, void* stream) {
+  const int reduce = ws != nullptr;
+  if (!iit_gemm_glds_ok(A, B, C, C2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits,
+                        reduce))
     return (int)hipErrorInvalidValue;
+  if (reduce && !counters) return (int)hipErrorInvalidValue;
   G2Args a;
   a.A = (const __bf16*)A; a.B = (const __bf16*)B; a.C = C; a.C2 = C2;
   a.bias0 = bias0; a.bias1 = bias1; a.bias2 = bias2; a.resid = resid;
   a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldc2 = ldc2; a.ldr = ldr;
   a.M = M; a.N = N; a.K = K; a.bias_cols = bias_cols; a.k_per_split = K / splits;
   a.csum = (epi == E_DGELU || epi == E_DGELU_ERF) ? csum : nullptr;
+  a.ws = reduce ? ws : nullptr;  // workspace >= splits * M * N floats, counters >= tiles ints (zero when idle)
+  a.counters = reduce ? counters : nullptr;
   hipStream_t s = (hipStream_t)stream;
 #define G2(MODE, AK, BK_, EPI) \
   if (mode == (MODE) && epi == (EPI)) return (int)launch_tile<AK, BK_, EPI>(a, tile, s);

@@ -88,7 +88,8 @@ def deterministic() -> bool:
     The split-K candidates (fp32 atomics into the output: the weight-gradient accumulate tiles and the few-tile
     fp32 store / residual ``s+hip`` path used by the last-position logits and the final-block residual adds) sum
     their partial products in arrival order, so two runs can differ in the last bits.  In deterministic mode the
-    dispatcher drops them and every candidate has a fixed reduction order."""
+    dispatcher drops them and every candidate has a fixed reduction order.  The reduction split-K candidates
+    (``glds*r*``: partial tiles summed in split order by the last-arriving workgroup) are deterministic and stay."""
     return os.environ.get("IIT_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
 
 
@@ -303,6 +304,18 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
                             C2=aux if dg else c2, bias0=bias0, bias1=bias1, bias2=bias2, resid=resid, ldc2=ldc2,
                             ldr=ldr, bias_cols=bias_cols, tile=t, splits=sp,
                             csum=csum_box[0] if csum_box is not None else None)
+            # the weight gradients (X^T dY, reduction over the tokens) also get the deterministic reduction split:
+            # larger tiles per CU (fewer operand bytes per flop) without fp32 atomics; they only run in backward
+            # passes, which are serial on one stream
+            if mode == 3 and epi in (K_.EPI_F32_ACC, K_.EPI_F32_STORE):
+                for sp in (2, 4):
+                    if Kd // sp < 256 or not K_.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc,
+                                                             mode=mode, epi=epi, resid=resid, ldr=ldr, tile=tile,
+                                                             splits=sp, reduce=True):
+                        continue
+                    calls[f"glds{tile}r{sp}"] = lambda c=C, c2=C2, c3=None, t=tile, sp=sp: K_.gemm_glds(  # noqa
+                        A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, bias0=bias0,
+                        resid=resid, ldr=ldr, tile=t, splits=sp, reduce=True)
     if epi in _BLAS16_EPIS:
         calls["blas16"] = lambda c=C, c2=C2, c3=None: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
                                                              bias0, resid, ldr)

@@ -28,8 +28,8 @@ _LIB = None
 
 _SIGS = {
     "iit_gemm": [c_void_p] * 10 + [c_long] * 5 + [c_int] * 12 + [c_void_p],
-    "iit_gemm_glds": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p, c_void_p],
-    "iit_gemm_glds_ok": [c_void_p] * 5 + [c_long] * 5 + [c_int] * 8,
+    "iit_gemm_glds": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p] * 4,
+    "iit_gemm_glds_ok": [c_void_p] * 5 + [c_long] * 5 + [c_int] * 9,
     "iit_embed_pos_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_embed_pos_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_ln_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
@@ -160,7 +160,8 @@ GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 1
               5: (256, 192),  # tiles 5-7: 8 waves (two per SIMD); 5: 4 x 6 MFMA tiles per wave, 2 stages
               6: (128, 128), 7: (256, 128),
               8: (96, 96),  # 96 x 96: 256 tiles for the [768][3072] weight gradients
-              9: (128, 96)}  # 128 x 96: 256 tiles for the [4096][768] outputs
+              9: (128, 96),  # 128 x 96: 256 tiles for the [4096][768] outputs
+              10: (96, 192), 11: (192, 96)}  # 2-way reduction split: 256 workgroups for the [768][3072] gradients
 
 
 def _gemm_bounds(what, A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode, qkv=(0, 0, 0)):
@@ -171,25 +172,51 @@ def _gemm_bounds(what, A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mo
 
 
 def gemm_glds_ok(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, resid=None, ldc2=0, ldr=0, bias_cols=0,
-                 tile=0, splits=1) -> bool:
-    """Whether the LDS-DMA kernel (``csrc/gemm_glds.hip``) covers this problem with tile ``tile``
-    (and split-K factor ``splits``, fp32-accumulate epilogue only)."""
+                 tile=0, splits=1, reduce=False) -> bool:
+    """Whether the LDS-DMA kernel (``csrc/gemm_glds.hip``) covers this problem with tile ``tile`` and split-K
+    factor ``splits`` (atomic split-K: fp32-accumulate epilogue only; ``reduce``: the deterministic reduction
+    split, fp32 accumulate or store)."""
     if any(t is not None and (not t.is_cuda or t.dtype not in (torch.bfloat16,)) for t in (A, B)):
         return False
     return bool(lib().iit_gemm_glds_ok(_p(A), _p(B), _p(C), _p(C2), _p(resid), lda, ldb, ldc, ldc2, ldr, M, N, K,
-                                       mode, epi, bias_cols, tile, splits))
+                                       mode, epi, bias_cols, tile, splits, int(reduce)))
+
+
+_SPLIT_WS = {}  # (device, stream, M, N, tile, splits) -> (fp32 partial-tile workspace, int32 tickets)
+
+
+def split_workspace(M: int, N: int, tile: int, splits: int, device) -> tuple:
+    """Workspace of the reduction split-K for one problem: ``splits * M * N`` fp32 partials and one ticket per
+    output tile (zeroed once; the kernel's last arriver re-arms it).  Keyed by the current stream too, so launches
+    on different streams never share partial tiles; allocated on first use (the dispatcher measures candidates --
+    and so allocates -- outside graph capture)."""
+    stream = torch.cuda.current_stream(device).cuda_stream
+    key = (str(device), stream, M, N, tile, splits)
+    ws = _SPLIT_WS.get(key)
+    if ws is None:
+        bm, bn = GLDS_TILES[tile]
+        ws = _SPLIT_WS[key] = (torch.empty(splits * M * N, dtype=torch.float32, device=device),
+                               torch.zeros((M // bm) * (N // bn), dtype=torch.int32, device=device))
+    return ws
 
 
 def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None, bias1=None, bias2=None, resid=None,
-              ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1, csum=None):
+              ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1, csum=None, reduce=False):
     """C = A @ B (+ epilogue) on the LDS-DMA MFMA kernel; bf16 operands, M/N/K multiples of the tile.
     ``EPI_DGELU`` (mode 0): ``C2`` is the saved bf16 pre-activation (row stride ``ldc2``); ``csum`` (fp32 [N],
-    optional) accumulates the column sums of the stored bf16 output."""
+    optional) accumulates the column sums of the stored bf16 output.
+    ``splits > 1``: split-K.  By default the partial tiles are added into C with fp32 atomics (accumulate
+    epilogue); with ``reduce`` they go to a workspace and the last-arriving split sums them in a fixed order
+    (run-to-run deterministic, no atomics, and valid for fp32 stores too)."""
+    ws = cnt = None
+    if reduce:
+        ws, cnt = split_workspace(M, N, tile, splits, A.device)
     if CHECK_BOUNDS:
         _gemm_bounds("iit_gemm_glds", A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode)
         _bounds("iit_gemm_glds", ("csum", csum, 1, N, N))
     _check(lib().iit_gemm_glds(_p(A), _p(B), _p(C), _p(C2), _p(bias0), _p(bias1), _p(bias2), _p(resid), lda, ldb,
-                               ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits, _p(csum), _stream()),
+                               ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits, _p(csum), _p(ws), _p(cnt),
+                               _stream()),
            "iit_gemm_glds")
 
 

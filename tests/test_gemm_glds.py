@@ -41,11 +41,11 @@ def _ops(K, mode, M, N, Kd, pad):
 CASES = [(0, 0), (0, 5), (0, 7), (2, 0), (2, 1), (2, 2), (2, 3), (2, 8), (2, 5), (2, 7), (3, 5), (3, 7)]
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("mode,epi", CASES)
 def test_glds_gemm_matches_fp32(K, mode, epi, tile):
     from iit_amd.ops.torch_ops import gelu_new
-    M, N, Kd, pad = (288 if tile == 8 else 256), 384, 192, 8
+    M, N, Kd, pad = {8: 288, 10: 288, 11: 384}.get(tile, 256), 384, 192, 8
     A, B, lda, ldb, a, b = _ops(K, mode, M, N, Kd, pad)
     ref = a @ b
     ldc = N + 8
@@ -102,6 +102,43 @@ def test_glds_split_k_accumulate(K, tile, splits):
                               tile=tile, splits=splits)
     K.gemm_glds(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=3, epi=K.EPI_F32_ACC, tile=tile, splits=splits)
     assert ((C - exp).norm() / exp.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("tile,splits", [(8, 2), (8, 4), (10, 2), (11, 2), (0, 4), (3, 2)])
+@pytest.mark.parametrize("epi", [5, 7])
+def test_glds_reduction_split_k(K, tile, splits, epi):
+    """Deterministic split-K: partial tiles to a workspace, summed in split order by the last-arriving workgroup.
+    Matches fp32, is bit-identical run to run, re-arms its tickets (back-to-back launches and graph replays), and
+    serves fp32 stores as well as accumulates (which atomic split-K cannot)."""
+    bm, bn = K.GLDS_TILES[tile]
+    M, N, Kd = 2 * bm * 2, bn * 3, 64 * 8 * splits
+    A, B, lda, ldb, a, b = _ops(K, 3, M, N, Kd, 8)
+    C0 = torch.randn(M, N + 8, device=dev)
+    bias = torch.randn(N, device=dev) if epi == K.EPI_F32_STORE else None
+    exp = a @ b + (C0[:, :N] if epi == K.EPI_F32_ACC else bias)
+    kw = dict(M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N + 8, mode=3, epi=epi, tile=tile, splits=splits)
+    assert K.gemm_glds_ok(A, B, C0, **kw, reduce=True)
+    outs = []
+    for _ in range(3):
+        C = C0.clone()
+        K.gemm_glds(A, B, C, **kw, bias0=bias, reduce=True)
+        outs.append(C)
+    torch.cuda.synchronize()
+    err = ((outs[0][:, :N] - exp).norm() / exp.norm()).item()
+    assert err < 1e-2, err
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert torch.equal(outs[0][:, N:], C0[:, N:])  # padding columns untouched
+    _, cnt = K.split_workspace(M, N, tile, splits, A.device)
+    assert int(cnt.abs().sum()) == 0  # every ticket re-armed
+    C = C0.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        K.gemm_glds(A, B, C, **kw, bias0=bias, reduce=True)
+    for _ in range(2):
+        C.copy_(C0)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(C, outs[0])
 
 
 @pytest.mark.parametrize("epi", [5, 7])
