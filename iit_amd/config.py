@@ -19,6 +19,13 @@ import torch
 
 WANDB_ENTITY = os.environ.get("IIT_WANDB_ENTITY", "cybershiptrooper")
 
+if os.environ.get("IIT_DEBUG_SYNC", "0") == "1":
+    # race-debug mode: the HIP runtime serialises kernel launches (read when HIP initialises, i.e. only if this
+    # module is imported before the first GPU call -- ``import iit_amd`` does that); iit_amd.utils.tracing adds a
+    # device drain at every phase boundary
+    os.environ.setdefault("HIP_LAUNCH_BLOCKING", "1")
+    os.environ.setdefault("AMD_SERIALIZE_KERNEL", "3")
+
 
 def _local_device() -> torch.device:
     if torch.cuda.is_available():

@@ -40,6 +40,8 @@ from typing import Dict, Optional, Tuple
 
 import torch
 
+from ..utils.tracing import sync_point, trace_range
+
 
 # "thread_local": only this thread's unsafe HIP calls break a capture.  Under data parallelism the RCCL
 # process group's watchdog thread polls its work events (hipEventQuery) while a phase is being captured;
@@ -277,9 +279,15 @@ class GraphedTrainStep:
             ent = self.graphs[full] = ((ga, gs, gb), static_out)
             self.captures += 1
         (ga, gs, gb), static_out = ent
-        ga.replay()
-        reduce_eagerly(lambda i, k: gs[i].replay())
-        gb.replay()
+        with trace_range("graph:fwd_bwd"):
+            ga.replay()
+        sync_point()
+        with trace_range("grad_allreduce"):
+            reduce_eagerly(lambda i, k: gs[i].replay())
+        sync_point()
+        with trace_range("graph:clip_adam"):
+            gb.replay()
+        sync_point()
         self.replays += 1
         return _clone_out(static_out)
 
@@ -326,7 +334,9 @@ class GraphedTrainStep:
         g, static_out = ent
         if _SYNC_BEFORE_REPLAY:
             torch.cuda.current_stream().synchronize()
-        g.replay()
+        with trace_range("graph:phase"):
+            g.replay()
+        sync_point()
         self.replays += 1
         return _clone_out(static_out)
 
@@ -504,6 +514,8 @@ class GraphedEvalStep:
                 return self._eager(sb, sa)
             ent = self.graphs[key] = (g, static_out)
         g, static_out = ent
-        g.replay()
+        with trace_range("graph:eval_step"):
+            g.replay()
+        sync_point()
         self.replays += 1
         return {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in static_out.items()}

@@ -44,6 +44,7 @@ from ..hooks.hook_points import ActivationCache, HookPoint
 from ..parallel import dist as pdist
 from ..utils.progress import progress
 from ..utils.sinks import make_sink
+from ..utils.tracing import StepTimer, sync_point, trace_range
 
 
 def _is_native(model) -> bool:
@@ -172,12 +173,18 @@ class BaseModelPair(ABC):
         ablation_x = ablation_input[0]
         base_x = base_input[0]
         hl_kw = self.hl_run_kwargs()
-        hl_ablation_output, self.hl_cache = self.hl_model.run_with_cache(ablation_input, **hl_kw)
+        with trace_range("hl_source_cache"):
+            hl_ablation_output, self.hl_cache = self.hl_model.run_with_cache(ablation_input, **hl_kw)
         ll_nodes = _ll_nodes_of(self.corr, hl_node)
-        self.ll_cache = self.ll_source_cache(ablation_x, ll_nodes)
-        hl_output = self.hl_model.run_with_hooks(
-            base_input, fwd_hooks=[(hl_node.name, self.make_hl_ablation_hook(hl_node))], **hl_kw)
-        ll_output = self.ll_intervened_forward(base_x, ll_nodes)
+        with trace_range("ll_source_cache"):
+            self.ll_cache = self.ll_source_cache(ablation_x, ll_nodes)
+        sync_point()
+        with trace_range("hl_intervened_fwd"):
+            hl_output = self.hl_model.run_with_hooks(
+                base_input, fwd_hooks=[(hl_node.name, self.make_hl_ablation_hook(hl_node))], **hl_kw)
+        with trace_range("ll_spliced_fwd"):
+            ll_output = self.ll_intervened_forward(base_x, ll_nodes)
+        sync_point()
         if verbose:
             print(f"{hl_node=}, {ll_nodes=}\n{hl_output=}")
         return hl_output, ll_output
@@ -240,7 +247,8 @@ class BaseModelPair(ABC):
         phase once as a HIP graph and replay it; without a runner it runs eagerly."""
         runner = getattr(self, "_phase_runner", None)
         if runner is not None:
-            return runner(key, compute_loss, optimizer, step_fn)
+            with trace_range(f"phase:{key[0]}"):
+                return runner(key, compute_loss, optimizer, step_fn)
         out = compute_loss()
         if isinstance(out, tuple):  # (loss, {name: tensor}) -> (loss, detached extras)
             loss, extras = out
@@ -329,9 +337,13 @@ class BaseModelPair(ABC):
         reducer = getattr(self, "_reducer", None)
         if reducer is not None:
             reducer.start()
-        loss.backward()
+        with trace_range("backward"):
+            loss.backward()
+        sync_point()
         if reducer is not None:
-            reducer.finish()
+            with trace_range("grad_allreduce"):
+                reducer.finish()
+            sync_point()
         # the reference's hook-based splices leave every LL parameter on the autograd
         # graph (zero gradients for dead paths); the native engine skips dead compute,
         # so give untouched parameters an explicit zero gradient (Adam still steps them).
@@ -351,11 +363,13 @@ class BaseModelPair(ABC):
 
     def optimizer_step(self, optimizer):
         clip = getattr(optimizer, "pending_clip", None)
-        if clip is not None and hasattr(optimizer, "flat"):
-            optimizer.pending_clip = None
-            optimizer.step(clip_norm=clip)
-        else:
-            optimizer.step()
+        with trace_range("clip_adam"):
+            if clip is not None and hasattr(optimizer, "flat"):
+                optimizer.pending_clip = None
+                optimizer.step(clip_norm=clip)
+            else:
+                optimizer.step()
+        sync_point()
 
     def step_scheduler(self, lr_scheduler, test_metrics):
         if isinstance(lr_scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
@@ -423,6 +437,7 @@ class BaseModelPair(ABC):
             self.train_metrics = train_metrics
             if pdist.is_main():
                 self._print_and_log_metrics(epoch, train_metrics.metrics + test_metrics.metrics, sink)
+                self._log_throughput(epoch, sink)
             if checkpoint_dir:
                 from ..utils.checkpoint import save_resume_state
                 save_resume_state(checkpoint_dir, self, optimizer, lr_scheduler, epoch + 1)
@@ -434,6 +449,19 @@ class BaseModelPair(ABC):
         if sink is not None:
             sink.log({"final epoch": epoch})
             sink.close()
+
+    def _log_throughput(self, epoch: int, sink) -> None:
+        """The epoch's training throughput (``self.throughput``): to the metric sink when there is one, and to
+        stdout with ``IIT_PROFILE=1`` (the default stdout stays the reference's metric lines)."""
+        tp = getattr(self, "throughput", None)
+        if not tp:
+            return
+        if sink is not None:
+            sink.log({"perf/pairs_per_s": tp["pairs_per_s"], "perf/ms_per_step": tp["ms_per_step"]})
+        from ..utils import tracing
+        if tracing.PROFILE:
+            print(f"[perf] epoch {epoch}: {tp['ms_per_step']:.2f} ms/step, {tp['pairs_per_s']:.0f} pairs/s "
+                  f"({int(tp['steps'])} timed steps, {pdist.world_size()} rank(s))")
 
     @final
     @staticmethod
@@ -473,12 +501,19 @@ class BaseModelPair(ABC):
         import contextlib
         # a graphed step runs on its own stream; the epoch's batches are produced there too (no per-step handoff)
         ctx = step.stream_context() if hasattr(step, "stream_context") else contextlib.nullcontext()
+        timer = StepTimer(pdist.world_size())
         with ctx:
             for i, (base_input, ablation_input) in enumerate(progress(loader, total=len(loader),
                                                                       disable=not pdist.is_main(), leave=False)):
-                metrics.update(step(base_input, ablation_input, loss_fn, optimizer))
+                timer.start()
+                with trace_range("train_step"):
+                    out = step(base_input, ablation_input, loss_fn, optimizer)
+                timer.stop(len(base_input[0]))
+                metrics.update(out)
                 if max_steps is not None and i + 1 >= max_steps:
                     break
+            # ms/step and whole-job intervened pairs/s of this epoch (device time, HIP events)
+            self.throughput = timer.summary()
         return metrics
 
     def _run_eval_epoch(self, loader, loss_fn) -> MetricStoreCollection:
@@ -488,7 +523,7 @@ class BaseModelPair(ABC):
         use_prefetch = prefetch.supported(self)
         batches = prefetch.prefetched_batches(self, loader) if use_prefetch else loader
         step = self.eval_step_fn(loss_fn) if not use_prefetch else None
-        with torch.no_grad():
+        with torch.no_grad(), trace_range("eval_epoch"):
             for base_input, ablation_input in batches:
                 if step is not None:
                     metrics.update(step(base_input, ablation_input))

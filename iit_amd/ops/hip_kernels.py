@@ -182,22 +182,33 @@ def gemm_glds_ok(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, resid=N
                                        mode, epi, bias_cols, tile, splits, int(reduce)))
 
 
-_SPLIT_WS = {}  # (device, stream, M, N, tile, splits) -> (fp32 partial-tile workspace, int32 tickets)
+_SPLIT_WS = {}  # (device, stream) -> [fp32 partial-tile workspace, int32 tickets, retired buffers]
 
 
 def split_workspace(M: int, N: int, tile: int, splits: int, device) -> tuple:
-    """Workspace of the reduction split-K for one problem: ``splits * M * N`` fp32 partials and one ticket per
-    output tile (zeroed once; the kernel's last arriver re-arms it).  Keyed by the current stream too, so launches
-    on different streams never share partial tiles; allocated on first use (the dispatcher measures candidates --
-    and so allocates -- outside graph capture)."""
+    """Workspace of the reduction split-K: ``splits * M * N`` fp32 partials and one ticket per output tile.
+
+    One buffer pair per (device, stream), shared by every problem launched on that stream (launches on one
+    stream are serial, and every launch leaves its tickets at zero), grown on demand.  A grown-out buffer is
+    retired, never freed: a captured graph keeps using the address it was captured with.  Launches on different
+    streams never share partial tiles.  The dispatcher measures the candidates -- and so sizes the buffers --
+    outside graph capture."""
     stream = torch.cuda.current_stream(device).cuda_stream
-    key = (str(device), stream, M, N, tile, splits)
-    ws = _SPLIT_WS.get(key)
-    if ws is None:
-        bm, bn = GLDS_TILES[tile]
-        ws = _SPLIT_WS[key] = (torch.empty(splits * M * N, dtype=torch.float32, device=device),
-                               torch.zeros((M // bm) * (N // bn), dtype=torch.int32, device=device))
-    return ws
+    key = (str(device), stream)
+    ent = _SPLIT_WS.get(key)
+    bm, bn = GLDS_TILES[tile]
+    need_ws, need_cnt = splits * M * N, (M // bm) * (N // bn)
+    if ent is None:
+        ent = _SPLIT_WS[key] = [None, None, []]
+    if ent[0] is None or ent[0].numel() < need_ws:
+        if ent[0] is not None:
+            ent[2].append(ent[0])
+        ent[0] = torch.empty(need_ws, dtype=torch.float32, device=device)
+    if ent[1] is None or ent[1].numel() < need_cnt:
+        if ent[1] is not None:
+            ent[2].append(ent[1])
+        ent[1] = torch.zeros(max(need_cnt, 1024), dtype=torch.int32, device=device)
+    return ent[0], ent[1]
 
 
 def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None, bias1=None, bias2=None, resid=None,
