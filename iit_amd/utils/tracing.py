@@ -78,8 +78,9 @@ def set_debug_sync(on: bool) -> None:
 
 def sync_point() -> None:
     """Phase boundary: in race-debug mode (``IIT_DEBUG_SYNC=1``) wait for all device work, so phases on different
-    streams never overlap; otherwise nothing."""
-    if DEBUG_SYNC and torch.cuda.is_available():
+    streams never overlap; otherwise nothing.  Inside a graph capture it does nothing (a device sync would abort
+    the capture; the captured phases replay in stream order anyway)."""
+    if DEBUG_SYNC and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
         torch.cuda.synchronize()
 
 

@@ -3,6 +3,7 @@ import os
 import subprocess
 import sys
 
+import pytest
 import torch
 
 from iit_amd.data.iit_dataset import IITDataset, train_test_split
@@ -76,3 +77,37 @@ def test_debug_sync_mode_serialises_hip_launches():
     out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.split() == ["1", "3", "True"]
+
+
+@pytest.mark.gpu
+def test_debug_sync_and_ranges_keep_graph_capture_working():
+    """Race-debug drains and roctx ranges around graph-captured phases: captures still succeed (no device sync
+    inside a capture) and the ranges reach roctx without error."""
+    from iit_amd.engine.graphs import GraphedTrainStep
+    from iit_amd.model_pairs import IOI_ModelPair
+    from iit_amd.models.config import gpt2_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.ops import hip_kernels
+    hip_kernels.lib()
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    cfg = gpt2_config_dict()
+    cfg.update(n_layers=2, d_model=128, n_heads=4, d_head=32, d_mlp=512, device="cuda:0", dtype=torch.bfloat16)
+    ll = HookedTransformer(cfg)
+    ll.set_op_backend("hip")
+    ds, hl = make_ioi_dataset_and_hl(256, ll, device=dev)
+    train = IITDataset(ds, ds, seed=0, device=dev)
+    pair = IOI_ModelPair(hl, ll, make_ioi_corr(2), training_args={"batch_size": 64, "lr": 1e-3, "lr_scheduler": None})
+    opt = pair.make_optimizer(1e-3)
+    runner = GraphedTrainStep(pair, opt, pair.loss_fn)
+    tracing.set_profiling(True)
+    tracing.set_debug_sync(True)
+    try:
+        for i, (base, abl) in enumerate(train.make_loader(64, 0)):
+            out = runner(base, abl, pair.loss_fn, opt)
+        torch.cuda.synchronize()
+    finally:
+        tracing.set_profiling(False)
+        tracing.set_debug_sync(False)
+    assert runner.captures > 0 and not runner.failed, runner.failed
+    assert all(torch.isfinite(torch.as_tensor(v)).all() for v in out.values())
