@@ -9,17 +9,21 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from iit_amd.ops import hip_kernels as K  # noqa: E402
 
 T = 4096
-CASES = [  # name, M, N, K, mode, epi, tile
+CASES = [  # name, M, N, K, mode, epi, tile[, splits, reduce]
     ("W_in fwd+gelu", T, 3072, 768, 2, K.EPI_GELU, 5),
     ("qkv fwd", T, 2304, 768, 2, K.EPI_BF16_BIAS3, 5),
     ("dX W_out + dgelu", T, 3072, 768, 0, K.EPI_DGELU, 5),
     ("dW W_in (X^T dY)", 768, 3072, T, 3, K.EPI_F32_STORE, 8),
+    # the deterministic reduction split-K the dispatcher now picks for the weight gradients
+    ("dW W_in 96x192 r2", 768, 3072, T, 3, K.EPI_F32_STORE, 10, 2, True),
+    ("dW W_O 64x64 r2", 768, 768, T, 3, K.EPI_F32_STORE, 3, 2, True),
 ]
 
 
 def main():
     dev = "cuda"
-    for name, M, N, Kd, mode, epi, tile in CASES:
+    for name, M, N, Kd, mode, epi, tile, *sk in CASES:
+        splits, reduce = (sk + [1, False])[:2] if sk else (1, False)
         A = (torch.randn(Kd, M) if mode & 1 else torch.randn(M, Kd)).to(dev).bfloat16()
         B = (torch.randn(Kd, N) if mode & 2 else torch.randn(N, Kd)).to(dev).bfloat16() / 16
         lda = M if mode & 1 else Kd
@@ -35,7 +39,7 @@ def main():
             extra = dict(bias0=bias)
         for _ in range(5):
             K.gemm_glds(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=mode, epi=epi, C2=C2,
-                        ldc2=N if C2 is not None else 0, tile=tile, **extra)
+                        ldc2=N if C2 is not None else 0, tile=tile, splits=splits, reduce=reduce, **extra)
         torch.cuda.synchronize()
         print(name, "ok", flush=True)
 
