@@ -249,10 +249,17 @@ __device__ __forceinline__ void store8_f32(void* dst, const float* v) {
   *((float4*)dst + 1) = make_float4(v[4], v[5], v[6], v[7]);
 }
 
-// s_waitcnt vmcnt(N) with N chosen at run time from {0, L, 2L, 3L} (an immediate is required)
+// s_waitcnt vmcnt(N) with N chosen at run time from {0, L, ..., 7L} (an immediate is required; deep rings keep up
+// to NS - 1 K-tiles in flight, capped by the 6-bit vmcnt)
 template <int L>
 __device__ __forceinline__ void wait_tiles(int tiles_in_flight) {
-  if (tiles_in_flight >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * L) : "memory");
+  constexpr int CAP = 63 / L;
+  if (tiles_in_flight > CAP) tiles_in_flight = CAP;
+  if (tiles_in_flight >= 7) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((7 * L) < 63 ? 7 * L : 63) : "memory");
+  else if (tiles_in_flight == 6) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((6 * L) < 63 ? 6 * L : 63) : "memory");
+  else if (tiles_in_flight == 5) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((5 * L) < 63 ? 5 * L : 63) : "memory");
+  else if (tiles_in_flight == 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((4 * L) < 63 ? 4 * L : 63) : "memory");
+  else if (tiles_in_flight == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((3 * L) < 63 ? 3 * L : 63) : "memory");
   else if (tiles_in_flight == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * L) : "memory");
   else if (tiles_in_flight == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -590,15 +597,19 @@ hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
     // -- 256 workgroups for [768][3072] / [3072][768], a third fewer operand bytes per CU than 96 x 96
     case 10: return launch<96, 192, 4, AKM, BKM, EPI>(a, s);
     case 11: return launch<192, 96, 4, AKM, BKM, EPI>(a, s);
+    // deep LDS rings (5-8 K-tiles, up to 144 KiB): more operand bytes in flight per CU for the intake-bound tiles
+    case 12: return launch<96, 96, 6, AKM, BKM, EPI>(a, s);
+    case 13: return launch<128, 96, 5, AKM, BKM, EPI>(a, s);
+    case 14: return launch<64, 64, 8, AKM, BKM, EPI>(a, s);
     default: return launch<128, 128, 4, AKM, BKM, EPI>(a, s);
   }
 }
 
 }  // namespace
 
-#define IIT_GLDS_TILES 12
-static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256, 96, 128, 96, 192};
-static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128, 96, 96, 192, 96};
+#define IIT_GLDS_TILES 15
+static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256, 96, 128, 96, 192, 96, 128, 64};
+static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128, 96, 96, 192, 96, 96, 96, 64};
 
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,

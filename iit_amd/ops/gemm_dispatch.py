@@ -293,7 +293,7 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
         if epi == K_.EPI_F32_ACC and (M // 64) * (N // 64) < 1024 and not det:
             split_opts = (1, 2, 4, 8, 16) if (M // 64) * (N // 64) < 64 else (1, 2, 4)
         dg = epi in (K_.EPI_DGELU, K_.EPI_DGELU_ERF)  # the LDS-DMA kernel reads pre through its C2 operand
-        for tile in K_.GLDS_TILES:
+        for tile in K_.GLDS_DISPATCH_TILES:
             for sp in split_opts:
                 if K_.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi,
                                    C2=aux if dg else C2, resid=resid, ldc2=ldc2, ldr=ldr, bias_cols=bias_cols,

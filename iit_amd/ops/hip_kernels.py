@@ -161,7 +161,11 @@ GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 1
               6: (128, 128), 7: (256, 128),
               8: (96, 96),  # 96 x 96: 256 tiles for the [768][3072] weight gradients
               9: (128, 96),  # 128 x 96: 256 tiles for the [4096][768] outputs
-              10: (96, 192), 11: (192, 96)}  # 2-way reduction split: 256 workgroups for the [768][3072] gradients
+              10: (96, 192), 11: (192, 96),  # 2-way reduction split: 256 workgroups for the [768][3072] gradients
+              12: (96, 96), 13: (128, 96), 14: (64, 64)}  # deep LDS rings (6 / 5 / 8 K-tiles)
+# measured slower than their 4-deep twins on every step shape (profiles/gemm_ring_depth_r2.txt: the tiles are
+# intake-bandwidth-bound, not latency-bound), so the dispatcher does not offer them; kept for the experiment
+GLDS_DISPATCH_TILES = tuple(t for t in GLDS_TILES if t not in (12, 13, 14))
 
 
 def _gemm_bounds(what, A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode, qkv=(0, 0, 0)):

@@ -1,0 +1,55 @@
+"""LDS ring depth vs operand intake: the step's intake-bound GEMM shapes on the standard tiles and on their deep-ring
+twins (tiles 12-14: 6 / 5 / 8 K-tiles in flight instead of 4), graph-timed (device time), best of 3."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from iit_amd.ops import gemm_dispatch as gd  # noqa: E402
+from iit_amd.ops import hip_kernels as K  # noqa: E402
+
+T = 4096
+CASES = [  # name, M, N, K, mode, epi, [(tile, splits, reduce), ...]
+    ("dW W_in [768][3072] store", 768, 3072, T, 3, K.EPI_F32_STORE, [(8, 1, False), (12, 1, False), (10, 2, True)]),
+    ("dW W_O [768][768] store", 768, 768, T, 3, K.EPI_F32_STORE, [(3, 2, True), (14, 2, True), (3, 1, False),
+                                                                    (14, 1, False), (8, 4, True), (12, 4, True)]),
+    ("dW QKV [768][2304] store", 768, 2304, T, 3, K.EPI_F32_STORE, [(3, 1, False), (14, 1, False)]),
+    ("fwd W_out [4096][768] resid", T, 768, 3072, 2, K.EPI_F32_RESID, [(9, 1, False), (13, 1, False)]),
+    ("dX W_in [4096][768] bf16", T, 768, 3072, 0, K.EPI_BF16, [(9, 1, False), (13, 1, False)]),
+    ("fwd W_O [4096][768] resid", T, 768, 768, 2, K.EPI_F32_RESID, [(9, 1, False), (13, 1, False)]),
+]
+
+
+def main():
+    dev = "cuda"
+    for name, M, N, Kd, mode, epi, variants in CASES:
+        torch.manual_seed(0)
+        A = (torch.randn(Kd, M) if mode & 1 else torch.randn(M, Kd)).to(dev).bfloat16()
+        B = (torch.randn(Kd, N) if mode & 2 else torch.randn(N, Kd)).to(dev).bfloat16() / 16
+        lda = M if mode & 1 else Kd
+        ldb = N if mode & 2 else Kd
+        f32 = epi in (K.EPI_F32_STORE, K.EPI_F32_ACC, K.EPI_F32_RESID)
+        C = torch.zeros(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
+        R = torch.randn(M, N, device=dev) if epi == K.EPI_F32_RESID else None
+        kw = dict(M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=mode, epi=epi)
+        ex = dict(resid=R, ldr=N) if R is not None else {}
+        ref = None
+        out = []
+        for tile, sp, red in variants:
+            if not K.gemm_glds_ok(A, B, C, tile=tile, splits=sp, reduce=red, **kw, **ex):
+                out.append(f"t{tile}{'r' if red else 'k'}{sp}: n/a")
+                continue
+            f = lambda: K.gemm_glds(A, B, C, tile=tile, splits=sp, reduce=red, **kw, **ex)  # noqa: E731
+            f()
+            torch.cuda.synchronize()
+            ref = C.clone() if ref is None else ref
+            err = float(((C.float() - ref.float()).norm() / ref.float().norm()))
+            us = min(gd._time(f, reps=20) for _ in range(3))
+            tf = 2 * M * N * Kd / (us * 1e-6) / 1e12
+            out.append(f"t{tile}{'r' if red else 'k'}{sp}: {us:6.1f} us {tf:5.0f} TF/s (rel diff {err:.1e})")
+        print(f"{name:28s} " + " | ".join(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
