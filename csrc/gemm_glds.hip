@@ -74,14 +74,23 @@ __device__ __forceinline__ int kmaj_swz(int kr) {
   else return (kr >> 3) & 1;  // R == 32: 2 blocks per 64-B k-row; k-rows 8g+q of one read -> 2 per bank slot
 }
 
-// Stage one operand tile (R rows of the output dimension x 64 k) into its LDS image with LDS-DMA.  The per-lane
+// swizzle of a k-contiguous image: the 16-B chunk slot XOR f(row), so the 16 rows one ds_read_b128 fragment read
+// touches land on distinct 16-B bank slots (128-B rows: two rows per 256-B bank window; 256-B rows: one)
+template <int BK>
+__device__ __forceinline__ int kcont_swz(int row) {
+  if constexpr (BK == 128) return row & 15;
+  else return (row >> 1) & 7;
+}
+
+// Stage one operand tile (R rows of the output dimension x BK k) into its LDS image with LDS-DMA.  The per-lane
 // source pointers and LDS offsets are computed once per workgroup; staging K-tile kt then costs one 64-bit add per
 // DMA instruction (the k offset is uniform).
-template <bool KMAJ, int R, int NW = 4>
+template <bool KMAJ, int R, int NW = 4, int BK = 64>
 struct Stager {
-  // LDS-DMA instructions per wave per K-tile: one instruction moves 8 rows x 128 B (k-contiguous) or
-  // 64 / (R/8) k-rows (k-major); the NW waves of the workgroup split them
-  static constexpr int N = KMAJ ? 64 / (NW * (64 / (R / 8))) : R / (8 * NW);
+  // LDS-DMA instructions per wave per K-tile: one instruction moves 8 rows x 128 B (k-contiguous, BK = 64), 4 rows x
+  // 256 B (BK = 128) or 64 / (R/8) k-rows (k-major); the NW waves of the workgroup split them
+  static constexpr int RPI = 1024 / (BK * 2);  // k-contiguous rows per instruction
+  static constexpr int N = KMAJ ? BK / (NW * (64 / (R / 8))) : R / (RPI * NW);
   static_assert(N >= 1, "tile too narrow for the workgroup's waves");
   const __bf16* ptr[N];
   int off[N];
@@ -89,16 +98,18 @@ struct Stager {
 
   __device__ __forceinline__ void init(const __bf16* base, long ld, int r0g, int kbeg, int wave, int lane) {
     if constexpr (!KMAJ) {
-      // [R][64] bf16, 128-B rows; one instruction = 8 rows x 8 chunks of 16 B
+      // [R][BK] bf16; BK = 64: 128-B rows, one instruction = 8 rows x 8 chunks of 16 B, chunk c of row r at slot
+      // c ^ ((r >> 1) & 7); BK = 128: 256-B rows, 4 rows x 16 chunks, chunk c at slot c ^ (r & 15)
+      constexpr int CPR = BK / 8;  // 16-B chunks per row
 #pragma unroll
       for (int i = 0; i < N; ++i) {
-        const int r0 = i * 8 * NW + wave * 8;
-        const int row = r0 + (lane >> 3);
-        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        const int r0 = i * RPI * NW + wave * RPI;
+        const int row = r0 + lane / CPR;
+        const int c = (lane % CPR) ^ kcont_swz<BK>(row);
         ptr[i] = base + (long)(r0g + row) * ld + kbeg + c * 8;
-        off[i] = r0 * 128;
+        off[i] = r0 * BK * 2;
       }
-      kstep = 64;
+      kstep = BK;
     } else {
       // [64][R] bf16, R*2-B k-rows; one instruction = (64 / (R/8)) k-rows
       constexpr int CH = R / 8;     // 16-B chunks per k-row
@@ -112,7 +123,7 @@ struct Stager {
         ptr[i] = base + (long)(kbeg + kr) * ld + r0g + col;
         off[i] = kr0 * R * 2;
       }
-      kstep = 64 * ld;
+      kstep = (long)BK * ld;
     }
   }
 
@@ -141,13 +152,13 @@ struct Panels {
   static constexpr int NP = R / PR;
 };
 
-template <bool KMAJ, int R, int NW = 4>
+template <bool KMAJ, int R, int NW = 4, int BK = 64>
 struct OperandStager {
   static constexpr bool PANELS = Panels<KMAJ, R>::ON;
   static constexpr int NP = Panels<KMAJ, R>::NP;
   static constexpr int PR = Panels<KMAJ, R>::PR;        // columns per panel
-  static constexpr int N = NP * Stager<KMAJ, PR, NW>::N;  // LDS-DMA instructions per wave per K-tile
-  Stager<KMAJ, PR, NW> st[NP];
+  static constexpr int N = NP * Stager<KMAJ, PR, NW, BK>::N;  // LDS-DMA instructions per wave per K-tile
+  Stager<KMAJ, PR, NW, BK> st[NP];
 
   __device__ __forceinline__ void init(const __bf16* base, long ld, int r0g, int kbeg, int wave, int lane) {
 #pragma unroll
@@ -155,7 +166,7 @@ struct OperandStager {
   }
   __device__ __forceinline__ void stage(int kt, char* img) const {
 #pragma unroll
-    for (int q = 0; q < NP; ++q) st[q].stage(kt, img + q * PR * 64 * 2);
+    for (int q = 0; q < NP; ++q) st[q].stage(kt, img + q * PR * BK * 2);
   }
 };
 
@@ -167,12 +178,12 @@ template <bool KMAJ> struct RawFrag;
 template <> struct RawFrag<false> { i32x4 v; };
 template <> struct RawFrag<true> { i16x4 lo, hi; };
 
-template <bool KMAJ, int R>
+template <bool KMAJ, int R, int BK = 64>
 __device__ __forceinline__ void frag_issue(const char* img, int row0, int kbase, int lane, RawFrag<KMAJ>& f) {
   if constexpr (!KMAJ) {
     const int row = row0 + (lane & 15);
     const int c = (kbase >> 3) + (lane >> 4);
-    const unsigned a = lds_addr(img + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+    const unsigned a = lds_addr(img + row * (BK * 2) + ((c ^ kcont_swz<BK>(row)) << 4));
     asm volatile("ds_read_b128 %0, %1" : "=v"(f.v) : "v"(a));
   } else {
     const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
@@ -185,13 +196,13 @@ __device__ __forceinline__ void frag_issue(const char* img, int row0, int kbase,
 }
 
 // fragment of rows/columns [row0, row0 + 16) of an operand tile staged by OperandStager<KMAJ, R>
-template <bool KMAJ, int R>
+template <bool KMAJ, int R, int BK = 64>
 __device__ __forceinline__ void frag_issue_t(const char* img, int row0, int kbase, int lane, RawFrag<KMAJ>& f) {
   using PN = Panels<KMAJ, R>;
   if constexpr (PN::ON) {
-    frag_issue<KMAJ, PN::PR>(img + (row0 / PN::PR) * PN::PR * 64 * 2, row0 % PN::PR, kbase, lane, f);
+    frag_issue<KMAJ, PN::PR, BK>(img + (row0 / PN::PR) * PN::PR * BK * 2, row0 % PN::PR, kbase, lane, f);
   } else {
-    frag_issue<KMAJ, R>(img, row0, kbase, lane, f);
+    frag_issue<KMAJ, R, BK>(img, row0, kbase, lane, f);
   }
 }
 
@@ -265,16 +276,16 @@ __device__ __forceinline__ void wait_tiles(int tiles_in_flight) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW>
+template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW, int BK = 64>
 __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
-  constexpr int BK = 64;
+  constexpr int HALVES = BK / 64;  // a 128-deep K-tile is two 64-deep halves of two 32-deep MFMA sub-steps each
   constexpr int NT = NW * 64;                    // threads
   constexpr int WMR = NW / 2;                    // wave rows (waves form a WMR x 2 grid)
   constexpr int WM = BM / WMR, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LOADS = OperandStager<AKM, BM, NW>::N + OperandStager<BKM, BN, NW>::N;  // DMA instrs / wave / K-tile
+  constexpr int LOADS = OperandStager<AKM, BM, NW, BK>::N + OperandStager<BKM, BN, NW, BK>::N;  // DMA / wave / K-tile
   constexpr int EPS = BN + 4;  // fp32 epilogue row stride (floats)
   // the fp32 epilogue tile goes through LDS in row chunks (one per wave row) when the whole tile would not fit
   constexpr int ECH = BM * EPS * 4 > 160 * 1024 ? 2 : 1;
@@ -308,8 +319,8 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
   //    wave's counted vmcnt) and retires all reads of tile kt, so those MFMAs overlap the next DMA issue.
   RawFrag<AKM> ca[TM], na[TM];
   RawFrag<BKM> cb[TN], nb[TN];
-  OperandStager<AKM, BM, NW> stA;
-  OperandStager<BKM, BN, NW> stB;
+  OperandStager<AKM, BM, NW, BK> stA;
+  OperandStager<BKM, BN, NW, BK> stB;
   stA.init(p.A, p.lda, m0, kbeg, wave, lane);
   stB.init(p.B, p.ldb, n0, kbeg, wave, lane);
 #pragma unroll
@@ -322,20 +333,22 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
   wait_tiles<LOADS>(min(NS - 1, nt - 1));
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int i = 0; i < TM; ++i) frag_issue_t<AKM, BM>(smem, wm * WM + i * 16, 0, lane, ca[i]);
+  for (int i = 0; i < TM; ++i) frag_issue_t<AKM, BM, BK>(smem, wm * WM + i * 16, 0, lane, ca[i]);
 #pragma unroll
-  for (int j = 0; j < TN; ++j) frag_issue_t<BKM, BN>(smem + A_BYTES, wn * WN + j * 16, 0, lane, cb[j]);
+  for (int j = 0; j < TN; ++j) frag_issue_t<BKM, BN, BK>(smem + A_BYTES, wn * WN + j * 16, 0, lane, cb[j]);
 
   for (int kt = 0; kt < nt; ++kt) {
     const char* sa = smem + (kt % NS) * STAGE;
     const char* sb = sa + A_BYTES;
-    // ---- sub-step 0 of tile kt: operands in ca/cb; issue sub-step 1 into na/nb
+#pragma unroll
+    for (int h = 0; h < HALVES; ++h) {
+    // ---- sub-step 0 of half h of tile kt: operands in ca/cb; issue sub-step 1 into na/nb
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) frag_issue_t<AKM, BM>(sa, wm * WM + i * 16, 32, lane, na[i]);
+    for (int i = 0; i < TM; ++i) frag_issue_t<AKM, BM, BK>(sa, wm * WM + i * 16, h * 64 + 32, lane, na[i]);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) frag_issue_t<BKM, BN>(sb, wn * WN + j * 16, 32, lane, nb[j]);
+    for (int j = 0; j < TN; ++j) frag_issue_t<BKM, BN, BK>(sb, wn * WN + j * 16, h * 64 + 32, lane, nb[j]);
     __builtin_amdgcn_sched_barrier(0);
     {
       bf16x8 a[TM], b[TN];
@@ -349,10 +362,16 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    // ---- sub-step 1: operands in na/nb; publish tile kt+1, restage slot kt % NS, issue (kt+1, 0) into ca/cb
+    // ---- sub-step 1: operands in na/nb; issue the next half of this tile into ca/cb, or (last half) publish tile
+    // kt+1, restage slot kt % NS and issue (kt+1, 0) into ca/cb
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + 1 < nt) {
+    if (h + 1 < HALVES) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) frag_issue_t<AKM, BM, BK>(sa, wm * WM + i * 16, (h + 1) * 64, lane, ca[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) frag_issue_t<BKM, BN, BK>(sb, wn * WN + j * 16, (h + 1) * 64, lane, cb[j]);
+    } else if (kt + 1 < nt) {
       wait_tiles<LOADS>(min(NS - 2, nt - 2 - kt));
       __builtin_amdgcn_s_barrier();
       if (kt + NS < nt) {
@@ -362,9 +381,9 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
       }
       const char* ta = smem + ((kt + 1) % NS) * STAGE;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) frag_issue_t<AKM, BM>(ta, wm * WM + i * 16, 0, lane, ca[i]);
+      for (int i = 0; i < TM; ++i) frag_issue_t<AKM, BM, BK>(ta, wm * WM + i * 16, 0, lane, ca[i]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) frag_issue_t<BKM, BN>(ta + A_BYTES, wn * WN + j * 16, 0, lane, cb[j]);
+      for (int j = 0; j < TN; ++j) frag_issue_t<BKM, BN, BK>(ta + A_BYTES, wn * WN + j * 16, 0, lane, cb[j]);
     }
     __builtin_amdgcn_sched_barrier(0);
     {
@@ -379,6 +398,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
+    }  // half
   }
   if constexpr (EPI == E_F32_ACC || EPI == E_F32_STORE) {
     if (p.ws != nullptr) {
@@ -568,10 +588,10 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
   }  // chunk
 }
 
-template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW = 4>
+template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW = 4, int BK = 64>
 hipError_t launch(const G2Args& a, hipStream_t s) {
   const int tiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NS, AKM, BKM, EPI, NW>), dim3(tiles, a.K / a.k_per_split),
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NS, AKM, BKM, EPI, NW, BK>), dim3(tiles, a.K / a.k_per_split),
                      dim3(NW * 64), 0, s, a);
   return hipGetLastError();
 }
@@ -601,15 +621,24 @@ hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
     case 12: return launch<96, 96, 6, AKM, BKM, EPI>(a, s);
     case 13: return launch<128, 96, 5, AKM, BKM, EPI>(a, s);
     case 14: return launch<64, 64, 8, AKM, BKM, EPI>(a, s);
+    // 128-deep K-tiles (256-B row segments per DMA, half the K-tiles / barriers per K): the intake experiment
+    case 15: return launch<128, 96, 2, AKM, BKM, EPI, 4, 128>(a, s);
+    case 16: return launch<96, 96, 3, AKM, BKM, EPI, 4, 128>(a, s);
+    case 17: return launch<64, 64, 4, AKM, BKM, EPI, 4, 128>(a, s);
+    case 18: return launch<128, 128, 2, AKM, BKM, EPI, 4, 128>(a, s);
     default: return launch<128, 128, 4, AKM, BKM, EPI>(a, s);
   }
 }
 
 }  // namespace
 
-#define IIT_GLDS_TILES 15
-static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256, 96, 128, 96, 192, 96, 128, 64};
-static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128, 96, 96, 192, 96, 96, 96, 64};
+#define IIT_GLDS_TILES 19
+static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256, 96, 128, 96, 192, 96, 128, 64,
+                                            128, 96, 64, 128};
+static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128, 96, 96, 192, 96, 96, 96, 64,
+                                            96, 96, 64, 128};
+static const int kTileBK[IIT_GLDS_TILES] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64,
+                                            128, 128, 128, 128};
 
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,
@@ -618,7 +647,8 @@ IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, con
   if (tile < 0 || tile >= IIT_GLDS_TILES) return 0;
   // atomic split-K: fp32 accumulate only; reduction split-K (``reduce``): fp32 accumulate or store
   const bool split_epi = epi == E_F32_ACC || (reduce && epi == E_F32_STORE);
-  if (splits < 1 || (splits > 1 && (!split_epi || K % (64 * splits)))) return 0;
+  const int bk = kTileBK[tile];
+  if (splits < 1 || (splits > 1 && (!split_epi || K % (bk * splits)))) return 0;
   if (reduce && splits < 2) return 0;
   if (!(mode == 0 || mode == 2 || mode == 3)) return 0;
   const bool epi_ok = mode == 3 ? (epi == E_F32_ACC || epi == E_F32_STORE)
@@ -629,7 +659,7 @@ IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, con
   const bool dg = epi == E_DGELU || epi == E_DGELU_ERF;
   if (mode == 0 && !(epi == E_BF16 || epi == E_F32_ACC || epi == E_F32_STORE || dg)) return 0;
   if (dg && (mode != 0 || !C2)) return 0;
-  if (M <= 0 || N <= 0 || K <= 0 || M % kTileBM[tile] || N % kTileBN[tile] || K % 64) return 0;
+  if (M <= 0 || N <= 0 || K <= 0 || M % kTileBM[tile] || N % kTileBN[tile] || K % bk) return 0;
   if (lda % 8 || ldb % 8 || ldc % 8 || (C2 && ldc2 % 8) || (resid && ldr % 8)) return 0;
   const uintptr_t al = (uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)C2 | (uintptr_t)resid;
   if (al & 15) return 0;

@@ -162,9 +162,11 @@ GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 1
               8: (96, 96),  # 96 x 96: 256 tiles for the [768][3072] weight gradients
               9: (128, 96),  # 128 x 96: 256 tiles for the [4096][768] outputs
               10: (96, 192), 11: (192, 96),  # 2-way reduction split: 256 workgroups for the [768][3072] gradients
-              12: (96, 96), 13: (128, 96), 14: (64, 64)}  # deep LDS rings (6 / 5 / 8 K-tiles)
-# measured slower than their 4-deep twins on every step shape (profiles/gemm_ring_depth_r2.txt: the tiles are
-# intake-bandwidth-bound, not latency-bound), so the dispatcher does not offer them; kept for the experiment
+              12: (96, 96), 13: (128, 96), 14: (64, 64),  # deep LDS rings (6 / 5 / 8 K-tiles)
+              15: (128, 96), 16: (96, 96), 17: (64, 64), 18: (128, 128)}  # 128-deep K-tiles (K % 128 == 0)
+# tiles 12-14 measured slower than their 4-deep twins on every step shape (profiles/gemm_ring_depth_r2.txt: the tiles
+# are intake-bandwidth-bound, not latency-bound), so the dispatcher does not offer them; kept for the experiment.
+# Tiles 15-18 (128-deep K-tiles) are within a few % of the 64-deep tiles and compete per shape.
 GLDS_DISPATCH_TILES = tuple(t for t in GLDS_TILES if t not in (12, 13, 14))
 
 

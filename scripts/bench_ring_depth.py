@@ -11,13 +11,14 @@ from iit_amd.ops import hip_kernels as K  # noqa: E402
 
 T = 4096
 CASES = [  # name, M, N, K, mode, epi, [(tile, splits, reduce), ...]
-    ("dW W_in [768][3072] store", 768, 3072, T, 3, K.EPI_F32_STORE, [(8, 1, False), (12, 1, False), (10, 2, True)]),
-    ("dW W_O [768][768] store", 768, 768, T, 3, K.EPI_F32_STORE, [(3, 2, True), (14, 2, True), (3, 1, False),
-                                                                    (14, 1, False), (8, 4, True), (12, 4, True)]),
-    ("dW QKV [768][2304] store", 768, 2304, T, 3, K.EPI_F32_STORE, [(3, 1, False), (14, 1, False)]),
-    ("fwd W_out [4096][768] resid", T, 768, 3072, 2, K.EPI_F32_RESID, [(9, 1, False), (13, 1, False)]),
-    ("dX W_in [4096][768] bf16", T, 768, 3072, 0, K.EPI_BF16, [(9, 1, False), (13, 1, False)]),
-    ("fwd W_O [4096][768] resid", T, 768, 768, 2, K.EPI_F32_RESID, [(9, 1, False), (13, 1, False)]),
+    ("dW W_in [768][3072] store", 768, 3072, T, 3, K.EPI_F32_STORE, [(8, 1, False), (12, 1, False), (16, 1, False), (10, 2, True)]),
+    ("dW W_O [768][768] store", 768, 768, T, 3, K.EPI_F32_STORE, [(3, 2, True), (14, 2, True), (17, 2, True), (3, 1, False),
+                                                                    (17, 1, False), (8, 4, True), (16, 4, True)]),
+    ("dW QKV [768][2304] store", 768, 2304, T, 3, K.EPI_F32_STORE, [(3, 1, False), (17, 1, False)]),
+    ("fwd W_out [4096][768] resid", T, 768, 3072, 2, K.EPI_F32_RESID, [(9, 1, False), (15, 1, False)]),
+    ("fwd W_in [4096][3072] bf16", T, 3072, 768, 2, K.EPI_BF16, [(5, 1, False), (0, 1, False), (18, 1, False)]),
+    ("dX W_in [4096][768] bf16", T, 768, 3072, 0, K.EPI_BF16, [(9, 1, False), (15, 1, False)]),
+    ("fwd W_O [4096][768] resid", T, 768, 768, 2, K.EPI_F32_RESID, [(9, 1, False), (15, 1, False)]),
 ]
 
 

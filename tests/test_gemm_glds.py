@@ -41,11 +41,11 @@ def _ops(K, mode, M, N, Kd, pad):
 CASES = [(0, 0), (0, 5), (0, 7), (2, 0), (2, 1), (2, 2), (2, 3), (2, 8), (2, 5), (2, 7), (3, 5), (3, 7)]
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18])
 @pytest.mark.parametrize("mode,epi", CASES)
 def test_glds_gemm_matches_fp32(K, mode, epi, tile):
     from iit_amd.ops.torch_ops import gelu_new
-    M, N, Kd, pad = {8: 288, 10: 288, 11: 384, 12: 288}.get(tile, 256), 384, 64 * 9, 8
+    M, N, Kd, pad = {8: 288, 10: 288, 11: 384, 12: 288, 16: 288}.get(tile, 256), 384, 64 * 10, 8
     A, B, lda, ldb, a, b = _ops(K, mode, M, N, Kd, pad)
     ref = a @ b
     ldc = N + 8
@@ -104,7 +104,7 @@ def test_glds_split_k_accumulate(K, tile, splits):
     assert ((C - exp).norm() / exp.norm()).item() < 1e-2
 
 
-@pytest.mark.parametrize("tile,splits", [(8, 2), (8, 4), (10, 2), (11, 2), (0, 4), (3, 2), (12, 2), (14, 2)])
+@pytest.mark.parametrize("tile,splits", [(8, 2), (8, 4), (10, 2), (11, 2), (0, 4), (3, 2), (12, 2), (14, 2), (16, 2), (17, 2)])
 @pytest.mark.parametrize("epi", [5, 7])
 def test_glds_reduction_split_k(K, tile, splits, epi):
     """Deterministic split-K: partial tiles to a workspace, summed in split order by the last-arriving workgroup.
