@@ -102,6 +102,9 @@ def main():
     if dev.type == "cuda":
         torch.cuda.synchronize()
     wall = time.perf_counter() - t_start[0]
+    if not pdist.is_main():  # only rank 0 logs epochs (and writes the record)
+        pdist.destroy()
+        return
     last_epoch, _, last = epochs_seen[-1]
     converged = bool(pair._check_early_stop_condition(pair.test_metrics.metrics))
     first_100 = next((e for e, _, m in epochs_seen if m.get("val/IIA", 0) >= 100), None)
