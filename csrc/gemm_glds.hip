@@ -419,7 +419,8 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
       int* flag = (int*)smem;
       if (tid == 0) {
         const int last = atomicAdd(p.counters + t, 1) == (int)gridDim.y - 1;
-        if (last) p.counters[t] = 0;  // every split has arrived: re-arm the ticket for the next launch
+        // every split has arrived: re-arm the ticket for the next launch (a device-coherent store, like the ticket)
+        if (last) __hip_atomic_store(p.counters + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         flag[0] = last;
       }
       __syncthreads();
