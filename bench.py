@@ -192,6 +192,9 @@ def main():
             from iit_amd.ops import gemm_dispatch
             with open(os.environ["IIT_GEMM_REPORT"], "w") as f:
                 f.write(gemm_dispatch.report())
+        if os.environ.get("IIT_GEMM_TABLE_EXPORT"):  # regenerate iit_amd/ops/tuned/gemm_decisions_gfx950.json
+            from iit_amd.ops import gemm_dispatch
+            gemm_dispatch.export_table(os.environ["IIT_GEMM_TABLE_EXPORT"])
     pdist.destroy()
 
 

@@ -456,6 +456,10 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     key = (M, N, Kd, mode, epi, bias0 is not None, fresh or (colsum is not None), deterministic())
     choice = DECISIONS.get(key)
     if choice is None:
+        shipped = None if _decide_only else _table().get(repr(key))  # ragged bulk/tail splits compare real times
+        if shipped in calls:
+            choice = DECISIONS[key] = (shipped, {shipped: float("nan")})
+    if choice is None:
         if torch.cuda.is_current_stream_capturing():
             return None if _decide_only else hip_call(C, C2, C3)
         # time on scratch outputs so accumulate epilogues (and column sums) do not corrupt C
@@ -483,6 +487,41 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
 
 
 K_ = K  # the kernel module (``K`` is shadowed by the reduction-size keyword above)
+
+# Shipped decision table: the measured choice per problem key from an MI355X run (``export_table``), so a fresh
+# process skips the autotuning of known shapes (the first training epoch / the bench warm-up).  Entries are only
+# used when the named implementation is among the problem's candidates; anything else is measured as before.
+# ``IIT_GEMM_TABLE=0`` disables it, ``IIT_GEMM_TABLE=<path>`` reads another file.
+_TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "gemm_decisions_gfx950.json")
+_TABLE = None
+
+
+def _table() -> Dict[str, str]:
+    global _TABLE
+    if _TABLE is None:
+        _TABLE = {}
+        path = os.environ.get("IIT_GEMM_TABLE", _TABLE_PATH)
+        if path != "0" and os.path.exists(path) and torch.cuda.is_available():
+            import json
+            try:
+                with open(path) as f:
+                    data = json.load(f)
+                arch = getattr(torch.cuda.get_device_properties(0), "gcnArchName", "").split(":")[0]
+                if data.get("arch") == arch:  # decisions measured on this GPU architecture only
+                    _TABLE = dict(data.get("decisions", {}))
+            except (OSError, ValueError) as e:  # pragma: no cover - a corrupt table only costs autotuning
+                print(f"[iit] GEMM decision table not loaded ({e})")
+    return _TABLE
+
+
+def export_table(path: str) -> int:
+    """Write the measured decisions of this process (``DECISIONS``) as a decision table; returns the entry count."""
+    import json
+    dec = {repr(k): v[0] for k, v in DECISIONS.items()}
+    with open(path, "w") as f:
+        json.dump({"arch": "gfx950", "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else None,
+                   "decisions": dec}, f, indent=0, sort_keys=True)
+    return len(dec)
 
 
 def report() -> str:
