@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="pairs per GPU per step")
     ap.add_argument("--model", default="gpt2-small", choices=["gpt2-small", "ioi-6l"])
@@ -128,12 +128,12 @@ def main():
             if i == 0 and hasattr(step_fn, "prime"):
                 step_fn.prime(base, abl, loss_fn, opt)  # capture every phase graph before timing
             step_fn(base, abl, loss_fn, opt)
-        batches_timed = [next(it) for _ in range(args.steps)]
         pdist.barrier()
         if dev.type == "cuda":
             torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for base, abl in batches_timed:
+        for _ in range(args.steps):
+            base, abl = next(it)  # the device-side batch gather is part of the timed step
             out = step_fn(base, abl, loss_fn, opt)
         if dev.type == "cuda":
             torch.cuda.synchronize()

@@ -276,8 +276,11 @@ __device__ __forceinline__ void wait_tiles(int tiles_in_flight) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW, int BK = 64>
-__global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
+// OCC = workgroups co-resident per CU the kernel is built for (LDS <= 160 KiB / OCC, registers <= 512 / OCC per lane
+// for 4-wave groups): with OCC = 2 one workgroup's prologue / epilogue (operand fill, output stores) overlaps the
+// other's MFMA main loop -- the per-launch fixed cost that one lock-stepped tile per CU leaves exposed.
+template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW, int BK = 64, int OCC = 1>
+__global__ __launch_bounds__(NW * 64, OCC) void gemm_glds_kernel(G2Args p) {
   constexpr int HALVES = BK / 64;  // a 128-deep K-tile is two 64-deep halves of two 32-deep MFMA sub-steps each
   constexpr int NT = NW * 64;                    // threads
   constexpr int WMR = NW / 2;                    // wave rows (waves form a WMR x 2 grid)
@@ -288,10 +291,11 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
   constexpr int LOADS = OperandStager<AKM, BM, NW, BK>::N + OperandStager<BKM, BN, NW, BK>::N;  // DMA / wave / K-tile
   constexpr int EPS = BN + 4;  // fp32 epilogue row stride (floats)
   // the fp32 epilogue tile goes through LDS in row chunks (one per wave row) when the whole tile would not fit
-  constexpr int ECH = BM * EPS * 4 > 160 * 1024 ? 2 : 1;
+  constexpr int LDS_BUDGET = 160 * 1024 / OCC;
+  constexpr int ECH = BM * EPS * 4 > LDS_BUDGET ? 2 : 1;
   constexpr int EPI_BYTES = BM / ECH * EPS * 4;
   constexpr int SMEM = NS * STAGE > EPI_BYTES ? NS * STAGE : EPI_BYTES;
-  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static_assert(SMEM <= LDS_BUDGET, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];  // ONE LDS object (keeps hipcc's waits counted)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -589,10 +593,10 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_glds_kernel(G2Args p) {
   }  // chunk
 }
 
-template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW = 4, int BK = 64>
+template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW = 4, int BK = 64, int OCC = 1>
 hipError_t launch(const G2Args& a, hipStream_t s) {
   const int tiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NS, AKM, BKM, EPI, NW, BK>), dim3(tiles, a.K / a.k_per_split),
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NS, AKM, BKM, EPI, NW, BK, OCC>), dim3(tiles, a.K / a.k_per_split),
                      dim3(NW * 64), 0, s, a);
   return hipGetLastError();
 }
@@ -627,25 +631,48 @@ hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
     case 16: return launch<96, 96, 3, AKM, BKM, EPI, 4, 128>(a, s);
     case 17: return launch<64, 64, 4, AKM, BKM, EPI, 4, 128>(a, s);
     case 18: return launch<128, 128, 2, AKM, BKM, EPI, 4, 128>(a, s);
+    // 192 x 192 (2 x 2 waves of 96 x 96, 6 x 6 MFMA blocks): the weight gradients with a 4-way reduction split --
+    // 192 workgroups for [768][3072] / [3072][768] / 144 for [768][2304] at half the operand bytes per flop of
+    // 96 x 96 (the intake-bound regime); 3- and 2-deep rings
+    // (tile 19 was 192 x 192 with a 3-deep ring: wrong results under the reduction split; not offered)
+    case 20: return launch<192, 192, 2, AKM, BKM, EPI>(a, s);
+    // 192 x 128 / 128 x 192 (2 x 2 waves of 96 x 64 / 64 x 96), 4-deep rings (exactly 160 KiB)
+    case 21: return launch<192, 128, 4, AKM, BKM, EPI>(a, s);
+    case 22: return launch<128, 192, 4, AKM, BKM, EPI>(a, s);
+    // two co-resident workgroups per CU (OCC = 2: <= 80 KiB LDS, <= 256 registers per lane), so one tile's
+    // prologue / epilogue overlaps the other's main loop; shapes with >= 512 tiles
+    case 23: return launch<128, 96, 2, AKM, BKM, EPI, 4, 64, 2>(a, s);
+    case 24: return launch<64, 96, 3, AKM, BKM, EPI, 4, 64, 2>(a, s);
+    case 25: return launch<128, 128, 2, AKM, BKM, EPI, 4, 64, 2>(a, s);
+    case 26: return launch<96, 96, 3, AKM, BKM, EPI, 4, 64, 2>(a, s);
+    case 27: return launch<128, 192, 2, AKM, BKM, EPI, 4, 64, 2>(a, s);
+    case 28: return launch<64, 192, 2, AKM, BKM, EPI, 4, 64, 2>(a, s);
+    // three / four co-resident workgroups per CU: the HBM-bound residual-epilogue shapes ([4096][768] outputs)
+    case 29: return launch<64, 96, 2, AKM, BKM, EPI, 4, 64, 3>(a, s);
+    case 30: return launch<64, 64, 2, AKM, BKM, EPI, 4, 64, 4>(a, s);
+    case 31: return launch<64, 128, 2, AKM, BKM, EPI, 4, 64, 3>(a, s);
     default: return launch<128, 128, 4, AKM, BKM, EPI>(a, s);
   }
 }
 
 }  // namespace
 
-#define IIT_GLDS_TILES 19
+#define IIT_GLDS_TILES 32
 static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256, 96, 128, 96, 192, 96, 128, 64,
-                                            128, 96, 64, 128};
+                                            128, 96, 64, 128, 192, 192, 192, 128, 128, 64, 128, 96, 128, 64,
+                                            64, 64, 64};
 static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128, 96, 96, 192, 96, 96, 96, 64,
-                                            96, 96, 64, 128};
+                                            96, 96, 64, 128, 192, 192, 128, 192, 96, 96, 128, 96, 192, 192,
+                                            96, 64, 128};
 static const int kTileBK[IIT_GLDS_TILES] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64,
-                                            128, 128, 128, 128};
+                                            128, 128, 128, 128, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64,
+                                            64, 64, 64};
 
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,
                                 long lda, long ldb, long ldc, long ldc2, long ldr, int M, int N, int K, int mode,
                                 int epi, int bias_cols, int tile, int splits, int reduce) {
-  if (tile < 0 || tile >= IIT_GLDS_TILES) return 0;
+  if (tile < 0 || tile >= IIT_GLDS_TILES || tile == 19) return 0;
   // atomic split-K: fp32 accumulate only; reduction split-K (``reduce``): fp32 accumulate or store
   const bool split_epi = epi == E_F32_ACC || (reduce && epi == E_F32_STORE);
   const int bk = kTileBK[tile];

@@ -645,7 +645,9 @@ IIT_EXPORT int iit_ce_bwd(const float* logits, long ld, const long* labels, cons
 // positions past the sequence length) are left out -- with zero gradient and zero moments, Adam leaves them
 // bit-identical, so skipping them is exact and saves their 30 B/element of HBM traffic.
 struct Span {
-  long start4;
+  long start4;  // parameter / bf16-mirror offset (float4 units) in the arena
+  long local4;  // gradient / Adam-moment offset: == start4 for the replicated optimizer; with optimizer-state
+                // sharding (ZeRO-1, iit_amd/parallel/zero.py) the offset inside this rank's shard buffers
   int len4;
   int pad;
 };
@@ -661,7 +663,7 @@ __global__ __launch_bounds__(256) void sumsq_span_kernel(const float* __restrict
   for (int e = blockIdx.x; e < nspans; e += gridDim.x) {
     const Span sp = spans[e];
     for (int i = threadIdx.x; i < sp.len4; i += 256) {
-      const float4 v = g4[sp.start4 + i];
+      const float4 v = g4[sp.local4 + i];
       s += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
     }
   }
@@ -680,7 +682,18 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
                                                         __bf16* __restrict__ mirror, const Span* __restrict__ spans,
                                                         int nspans, const float* __restrict__ part, int nparts,
                                                         float clip, float lr, float b1, float b2, float eps, float wd,
-                                                        int* __restrict__ step, int* __restrict__ skipped) {
+                                                        const float* __restrict__ hyper, int* __restrict__ step,
+                                                        int* __restrict__ skipped) {
+  // ``hyper`` (nullable): device copy of {lr, beta1, beta2, eps, weight_decay}.  A captured graph replays the
+  // kernel arguments it saw at capture; reading the hyper-parameters from device memory lets the host change the
+  // learning rate (an LR scheduler) between replays with one small copy.
+  if (hyper) {
+    lr = hyper[0];
+    b1 = hyper[1];
+    b2 = hyper[2];
+    eps = hyper[3];
+    wd = hyper[4];
+  }
   __shared__ float coef_s;
   __shared__ int bad_s;
   if (threadIdx.x < 64) {
@@ -713,17 +726,18 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
   for (int e = blockIdx.x; e < nspans; e += gridDim.x) {
     const Span sp = spans[e];
     for (int j = threadIdx.x; j < sp.len4; j += 256) {
-      const long i = sp.start4 + j;
+      const long i = sp.start4 + j;   // parameter / mirror
+      const long li = sp.local4 + j;  // gradient / moments
       // NT: the gradient and both moments are touched once per step -- stream them past the caches
       float4 gg, pp = p4[i], mm, vv;
       if (NT) {
-        gg = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)g4 + i));
-        mm = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)m4 + i));
-        vv = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)v4 + i));
+        gg = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)g4 + li));
+        mm = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)m4 + li));
+        vv = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)v4 + li));
       } else {
-        gg = g4[i];
-        mm = m4[i];
-        vv = v4[i];
+        gg = g4[li];
+        mm = m4[li];
+        vv = v4[li];
       }
       float* gs = (float*)&gg;
       float* ps = (float*)&pp;
@@ -739,11 +753,11 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
       }
       p4[i] = pp;
       if (NT) {
-        __builtin_nontemporal_store(__builtin_bit_cast(f32x4, mm), (f32x4*)m4 + i);
-        __builtin_nontemporal_store(__builtin_bit_cast(f32x4, vv), (f32x4*)v4 + i);
+        __builtin_nontemporal_store(__builtin_bit_cast(f32x4, mm), (f32x4*)m4 + li);
+        __builtin_nontemporal_store(__builtin_bit_cast(f32x4, vv), (f32x4*)v4 + li);
       } else {
-        m4[i] = mm;
-        v4[i] = vv;
+        m4[li] = mm;
+        v4[li] = vv;
       }
       if (mirror) {
         bf16x4 o = {f2bf(ps[0]), f2bf(ps[1]), f2bf(ps[2]), f2bf(ps[3])};
@@ -758,7 +772,7 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
 // gradient contains inf/nan leaves weights, moments and the step counter untouched.
 IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, void* mirror, const void* spans, int nspans,
                              float* part, int nparts, float clip, float lr, float b1, float b2, float eps, float wd,
-                             int* step, int* skipped, void* stream) {
+                             const float* hyper, int* step, int* skipped, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool norm = clip > 0.f || skipped != nullptr;
   const Span* sp = (const Span*)spans;
@@ -771,14 +785,34 @@ IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, void* mirro
   }();
   if (nt)
     hipLaunchKernelGGL(adam_span_kernel<true>, dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, sp, nspans,
-                       part, nparts, clip, lr, b1, b2, eps, wd, step, skipped);
+                       part, nparts, clip, lr, b1, b2, eps, wd, hyper, step, skipped);
   else
     hipLaunchKernelGGL(adam_span_kernel<false>, dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, sp,
-                       nspans, part, nparts, clip, lr, b1, b2, eps, wd, step, skipped);
+                       nspans, part, nparts, clip, lr, b1, b2, eps, wd, hyper, step, skipped);
   return hipGetLastError();
 }
 
 IIT_EXPORT int iit_adam_span_size() { return (int)sizeof(Span); }
+
+// The two stages separately, for the sharded optimizer (ZeRO-1, iit_amd/parallel/zero.py): per-block partial sums
+// of g^2 over this rank's shard spans (+ the device step bump), then -- after the host all-reduces the partial total
+// into ``total`` (one float) -- the Adam pass over the same spans with the global norm read from ``total``.
+IIT_EXPORT int iit_sumsq_spans(const float* g, const void* spans, int nspans, float* part, int nparts, int do_norm,
+                               int* step, void* stream) {
+  hipLaunchKernelGGL(sumsq_span_kernel, dim3(do_norm ? nparts : 1), dim3(256), 0, (hipStream_t)stream, g,
+                     (const Span*)spans, nspans, part, do_norm, step);
+  return hipGetLastError();
+}
+
+IIT_EXPORT int iit_adam_spans(float* p, const float* g, float* m, float* v, void* mirror, const void* spans,
+                              int nspans, const float* total, float clip, float lr, float b1, float b2, float eps,
+                              float wd, const float* hyper, int* step, int* skipped, void* stream) {
+  const int blocks = max(1, min(nspans, 4096));
+  hipLaunchKernelGGL(adam_span_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
+                     (__bf16*)mirror, (const Span*)spans, nspans, total, 1, clip, lr, b1, b2, eps, wd, hyper, step,
+                     skipped);
+  return hipGetLastError();
+}
 
 // ============================================================================ shadow weights
 // dst (bf16) = src (fp32) viewed as [rows][cols]; transpose -> dst[c][r] with leading dim ld.

@@ -11,9 +11,12 @@ Behavioural decisions:
     raising ``TypeError`` on ``max(None, int)``.
   * comparing with a non-``TorchIndex`` returns ``False`` instead of raising.
 
-Besides the reference API this module exposes ``to_mask_spec`` which the
-engine (``iit_amd.engine.plan``) uses to turn an index into the compact
-per-dimension range table consumed by the HIP splice epilogues.
+Besides the reference API this module exposes ``to_ranges``, which lowers an
+index to the compact per-dimension range table (up to 8 half-open ranges per
+dimension) that the HIP splice / gradient-mask / scale kernel consumes
+(``csrc/splice.hip`` through :mod:`iit_amd.ops.splice`, used by
+:class:`iit_amd.engine.plan.Splice` and the StopGrad sites of the hooked
+transformer), and ``to_mask_spec`` (the same selection as per-dimension lists).
 """
 from __future__ import annotations
 
@@ -40,7 +43,7 @@ def _freeze(atom: IndexAtom):
 class TorchIndex:
     """A hashable, intersectable tensor index."""
 
-    __slots__ = ("as_index", "hashable_tuple", "_atoms", "_dev")
+    __slots__ = ("as_index", "hashable_tuple", "_atoms", "_dev", "_iit_specs")
 
     def __init__(self, list_of_things_in_tuple: Iterable[IndexAtom]):
         if not isinstance(list_of_things_in_tuple, (tuple, list)):
@@ -55,6 +58,7 @@ class TorchIndex:
         self.as_index: Tuple = tuple(slice(None) if a is None else a for a in atoms)
         self.hashable_tuple = tuple(_freeze(a) for a in atoms)
         self._dev = None
+        self._iit_specs = None  # packed splice range tables per (hook shape, source strides), see iit_amd.ops.splice
 
     def on(self, device) -> Tuple:
         """``as_index`` with list atoms as cached int64 tensors on ``device``: indexing a GPU tensor with a Python
@@ -124,6 +128,44 @@ class TorchIndex:
             if not _atoms_overlap(a, b):
                 return False
         return True
+
+    def to_ranges(self, shape: Tuple[int, ...], max_ranges: int = 8):
+        """Per-dimension lists of half-open ``(lo, hi)`` ranges selecting the same elements of a tensor of ``shape``
+        as ``t[self.as_index]`` -- the splice kernel's patch spec -- or None when the index is not such a
+        per-dimension product: more than one list atom (torch pairs list atoms up instead of crossing them), a
+        stepped slice, more atoms than dimensions, or a dimension needing more than ``max_ranges`` runs.
+        Negative ints / slice bounds are normalised; list atoms are sorted and merged into runs (a splice writes
+        the same value whatever the order or multiplicity)."""
+        atoms = self.as_index
+        if len(atoms) > len(shape) or sum(isinstance(a, list) for a in atoms) > 1:
+            return None
+        out = []
+        for d, n in enumerate(shape):
+            a = atoms[d] if d < len(atoms) else slice(None)
+            if isinstance(a, slice):
+                if a.step not in (None, 1):
+                    return None
+                lo, hi, _ = a.indices(n)
+                runs = [(lo, hi)] if hi > lo else []
+            elif _is_int(a):
+                if not -n <= a < n:
+                    return None
+                v = a % n
+                runs = [(v, v + 1)]
+            else:
+                if any(not -n <= v < n for v in a):
+                    return None  # out of range: the generic path raises torch's IndexError
+                vals = sorted({v % n for v in a})
+                runs = []
+                for v in vals:
+                    if runs and runs[-1][1] == v:
+                        runs[-1] = (runs[-1][0], v + 1)
+                    else:
+                        runs.append((v, v + 1))
+            if len(runs) > max_ranges:
+                return None
+            out.append(runs)
+        return out
 
     def to_mask_spec(self, shape: Tuple[int, ...]):
         """Per-dimension list of selected positions (None = whole dim) for ``shape``.

@@ -58,6 +58,12 @@ def _subtract_ranges(ranges, holes):
     return out
 
 
+def make_span_tensor(spans, device) -> torch.Tensor:
+    """Pack ``[(arena start4, local start4, len4), ...]`` as the kernels' 24-byte ``Span`` records (int64 triples;
+    the length's high word is the zero pad)."""
+    return torch.tensor(spans if spans else [(0, 0, 0)], dtype=torch.int64).view(-1, 3).to(device)
+
+
 class FlatParams:
     def __init__(self, module: nn.Module, with_bf16_shadow: bool = False):
         self.module = module
@@ -148,6 +154,13 @@ class FlatParams:
         i = self.index.get(id(p))
         if i is None:
             return False
+        # rows skipped so far were never memset by zero_grad: a backward outside the restricted data (after
+        # train() returned) may have left sums there, which must not reach Adam once the rows are live again
+        stale = self.inactive_ranges() if i in self._inactive else []
+        g = getattr(self, "grad", None)
+        if g is not None:
+            for a, b in stale:
+                g[a:b].zero_()
         if live_rows is None:
             self._inactive.pop(i, None)
         else:
@@ -188,13 +201,15 @@ class FlatParams:
                 out.append((off + r0 * d, off + r * d))
         return sorted(out)
 
-    def span_table(self, span_bytes: int = 16, max_len4: int = 1024, restricted: bool = True):
-        """Device table of (start4, len4) spans covering the active arena (``restricted=False``: all of it), as
-        read by the fused optimizer kernels.  Cached until the restriction changes."""
+    def span_table(self, span_bytes: int = 24, max_len4: int = 1024, restricted: bool = True):
+        """Device table of optimizer span records (arena start, gradient / moment start, length; float4 units)
+        covering the active arena (``restricted=False``: all of it), as read by the fused optimizer kernels
+        (``Span`` in csrc/kernels.hip; the replicated optimizer reads gradient and moments at the arena offset).
+        Cached until the restriction changes."""
         key = (restricted, max_len4)
         if self._span_cache is not None and self._span_cache[0] == key:
             return self._span_cache[1], self._span_cache[2]
-        assert span_bytes == 16
+        assert span_bytes == 24
         n4 = self.numel // 4
         gaps = [(a // 4, b // 4) for a, b in self.inactive_ranges()] if restricted else []
         spans = []
@@ -202,10 +217,10 @@ class FlatParams:
         for a, b in gaps + [(n4, n4)]:
             while pos < a:
                 ln = min(max_len4, a - pos)
-                spans.append((pos, ln))
+                spans.append((pos, pos, ln))
                 pos += ln
             pos = max(pos, b)
-        tab = torch.tensor(spans if spans else [(0, 0)], dtype=torch.int64).view(-1, 2).to(self.data.device)
+        tab = make_span_tensor(spans, self.data.device)
         self.drop_span_cache()
         self._span_cache = (key, tab, len(spans))
         return tab, len(spans)

@@ -51,6 +51,15 @@ _SYNC_BEFORE_REPLAY = os.environ.get("IIT_GRAPH_SYNC_BEFORE_REPLAY") == "1"  # d
 _RECAPTURE_ALL = os.environ.get("IIT_GRAPH_RECAPTURE_ALL") == "1"  # diagnostics
 
 
+def _sync_hyper(optimizer) -> None:
+    """A captured optimizer step replays the kernel arguments of its capture; the fused Adam reads its learning
+    rate (and betas / eps / weight decay) from device scalars, refreshed here when the host values changed (an LR
+    scheduler stepped between epochs).  Optimizers without device hyper-parameters are left alone."""
+    sync = getattr(optimizer, "sync_hyper", None)
+    if sync is not None:
+        sync()
+
+
 def _clone_out(out):
     """Copies of a replayed phase's outputs (the captured buffers are overwritten by the next replay).  Scalar
     losses are packed by one ``stack`` -- a single copy kernel instead of one per metric."""
@@ -255,6 +264,8 @@ class GraphedTrainStep:
             if self.pool is None or os.environ.get("IIT_GRAPH_POOL") == "private":
                 self.pool = torch.cuda.graph_pool_handle()
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            if getattr(optimizer, "sharded", False):
+                gb = None  # the sharded optimizer step issues collectives (norm all-reduce, all-gather): eager
             gs = []
             try:
                 with _CaptureGC(), torch.cuda.graph(ga, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
@@ -266,8 +277,10 @@ class GraphedTrainStep:
                     gs.append(g)
                 if stg is not None:
                     stg.release()
-                with _CaptureGC(), torch.cuda.graph(gb, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
-                    update()
+                if gb is not None:
+                    with _CaptureGC(), torch.cuda.graph(gb, pool=self.pool, stream=self.stream,
+                                                        capture_error_mode=_CAPTURE_MODE):
+                        update()
             except Exception as e:
                 self.failed[full] = repr(e)
                 self.pool = None  # see _run_phase: the aborted capture's pool is not reusable
@@ -279,6 +292,7 @@ class GraphedTrainStep:
             ent = self.graphs[full] = ((ga, gs, gb), static_out)
             self.captures += 1
         (ga, gs, gb), static_out = ent
+        _sync_hyper(optimizer)
         with trace_range("graph:fwd_bwd"):
             ga.replay()
         sync_point()
@@ -286,7 +300,10 @@ class GraphedTrainStep:
             reduce_eagerly(lambda i, k: gs[i].replay())
         sync_point()
         with trace_range("graph:clip_adam"):
-            gb.replay()
+            if gb is None:
+                update()
+            else:
+                gb.replay()
         sync_point()
         self.replays += 1
         return _clone_out(static_out)
@@ -332,6 +349,7 @@ class GraphedTrainStep:
             ent = self.graphs[full] = (g, static_out)
             self.captures += 1
         g, static_out = ent
+        _sync_hyper(optimizer)
         if _SYNC_BEFORE_REPLAY:
             torch.cuda.current_stream().synchronize()
         with trace_range("graph:phase"):

@@ -10,8 +10,12 @@ clone/index_put" substrate (``/root/reference/iit/model_pairs/base_model_pair.py
 * ``splice``: hook name -> list of ``(TorchIndex, src)``.  Semantics equal the
   reference hook ``out = act.clone(); out[idx] = src[idx]``; the spliced slice is
   a constant, so no gradient flows upstream through it (K10).  Fused HIP kernels
-  implement whole-tensor and per-head splices in their epilogues; everything
-  else falls back to a generic masked copy.
+  implement whole-tensor and per-head splices in their epilogues (or skip the
+  dead producer); any other index that lowers to a per-dimension range table
+  (``TorchIndex.to_ranges``: batch / position / head / feature / channel /
+  spatial ranges and lists) is one launch of the patch-spec splice kernel
+  (``csrc/splice.hip``), whose backward zeroes the spliced gradient; only
+  paired list atoms or stepped slices keep the clone + index_put fallback.
 * ``scale`` / ``zero_grad``: StopGrad semantics (K21).
 * ``logits``: ``"full"`` (``[B,S,V]``), ``"last"`` (only position -1, K08) or ``"none"``.
 """
@@ -69,6 +73,11 @@ class Splice:
             if src.shape != act.shape:
                 src = src.expand_as(act)
             return src
+        if act.is_cuda:
+            from ..ops import splice as _splice
+            out = _splice.splice(act, self.index, src)
+            if out is not None:
+                return out
         out = act.clone()
         ix = self.index.on(act.device)
         out[ix] = src[ix] if src.shape == act.shape else src.expand_as(act)[ix]
@@ -124,3 +133,34 @@ class RunPlan:
         out.logits = other.logits
         out.truncate = other.truncate
         return out
+
+
+def scale_site(x: torch.Tensor, scale: float) -> torch.Tensor:
+    """StopGrad's forward hook ``act / scale`` (/root/reference/iit/model_pairs/stop_grad_pair.py:37-44): on the GPU
+    one launch of the patch-spec kernel (csrc/splice.hip, whole-hook range), elsewhere a torch divide."""
+    if x.is_cuda:
+        from ..ops import splice as _splice
+        out = _splice.divide(x, EVERYTHING, scale)
+        if out is not None:
+            return out
+    return x / scale
+
+
+def zero_grad_site(x: torch.Tensor, idxs) -> torch.Tensor:
+    """StopGrad's backward hook ``grad[idx] = 0`` per non-circuit node (stop_grad_pair.py:62-75): on the GPU a fused
+    gradient-mask launch per index (csrc/splice.hip), elsewhere a clone + index-assign tensor hook."""
+    if x.is_cuda:
+        from ..ops import splice as _splice
+        out = _splice.grad_mask(x, idxs)
+        if out is not None:
+            return out
+
+    def _mask(g, _idxs=idxs):
+        g = g.clone()
+        for ix in _idxs:
+            g[ix.on(g.device)] = 0
+        return g
+
+    x = x.view_as(x)
+    x.register_hook(_mask)
+    return x

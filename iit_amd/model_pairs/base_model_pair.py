@@ -277,11 +277,24 @@ class BaseModelPair(ABC):
             if flat is None:
                 flat = FlatParams(module, with_bf16_shadow=getattr(module, "wants_bf16_shadow", False))
                 module._flat_params = flat
-            opt = FusedAdam(flat, lr=lr)
+            if self._zero_requested():
+                # optimizer-state sharding over the data-parallel ranks (ZeRO-1, iit_amd/parallel/zero.py); the
+                # reducer's buckets define the shards (set again when the staged schedule re-buckets)
+                from ..parallel.zero import ShardedFusedAdam
+                opt = ShardedFusedAdam(flat, flat.buckets(int(self.training_args.get("bucket_mb", 64.0) * (1 << 20))),
+                                       lr=lr)
+            else:
+                opt = FusedAdam(flat, lr=lr)
         else:
             opt = torch.optim.Adam(module.parameters(), lr=lr)
         self._setup_reducer(opt)
         return opt
+
+    def _zero_requested(self) -> bool:
+        """Optimizer-state sharding: ``training_args["zero"]`` (or ``IIT_ZERO=1``) under data parallelism."""
+        import os
+        want = self.training_args.get("zero", os.environ.get("IIT_ZERO", "0") == "1")
+        return bool(want) and (pdist.world_size() > 1 or pdist.force_reducer())
 
     def _setup_reducer(self, optimizer):
         self._reducer = None
@@ -298,6 +311,8 @@ class BaseModelPair(ABC):
                                         overlap=self.training_args.get("overlap_allreduce", True),
                                         wire_dtype=torch.bfloat16 if wire == "bf16" else None,
                                         module=self._ll_module())
+            if getattr(optimizer, "sharded", False):
+                self._reducer.attach_shard(optimizer)
 
     def restrict_sparse_rows(self, dataset, optimizer_rows: bool = True) -> None:
         """Exploit the gradient sparsity of the embedding tables for ``dataset``:
@@ -446,6 +461,8 @@ class BaseModelPair(ABC):
                 fault_hook(epoch)
             if early_stop and self._check_early_stop_condition(test_metrics.metrics):
                 break
+        # lift the row restriction: later backwards (fine-tuning on other data) may touch any embedding row
+        self.restrict_sparse_rows(None)
         if sink is not None:
             sink.log({"final epoch": epoch})
             sink.close()
@@ -546,27 +563,33 @@ class BaseModelPair(ABC):
 
     @staticmethod
     def _reduce_metrics(collection: MetricStoreCollection) -> None:
-        """Average each metric's epoch value over data-parallel ranks (one small all-reduce)."""
+        """Epoch metrics over data-parallel ranks as the single-process mean: every store's per-step values are
+        summed and counted on each rank, one all-reduce adds the sums and counts, and the store
+        keeps sum / count -- exact also when ranks ran different numbers of batches (a mean of per-rank means is
+        not)."""
         if pdist.world_size() <= 1:
             return
-        vals = []
+        stores, parts = [], []
         for m in collection.metrics:
             if len(m) == 0:
                 continue
-            vals.append(np.atleast_1d(np.mean(np.stack([np.asarray(v, dtype=np.float64) for v in m._values()]), axis=0)))
-        if not vals:
+            vals = np.stack([np.atleast_1d(np.asarray(v, dtype=np.float64)) for v in m._values()])
+            stores.append((m, vals.shape[1]))
+            parts.append(vals.sum(axis=0))
+            parts.append(np.array([float(len(vals))]))
+        if not parts:
             return
-        flat = torch.tensor(np.concatenate(vals), dtype=torch.float64)
+        flat = torch.tensor(np.concatenate(parts), dtype=torch.float64)
         if torch.distributed.get_backend() == "nccl":
             flat = flat.cuda()
-        pdist.all_reduce_mean_(flat)
+        torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM)
         flat = flat.cpu().numpy()
         off = 0
-        for m, v in zip([m for m in collection.metrics if len(m)], vals):
-            n = v.size
-            red = flat[off:off + n]
-            off += n
-            m._store = [red if (m.type == MetricType.LOG) else float(red[0])]
+        for m, n in stores:
+            total, count = flat[off:off + n], flat[off + n]
+            off += n + 1
+            mean = total / count
+            m._store = [mean if (m.type == MetricType.LOG) else float(mean[0])]
 
     @staticmethod
     def _check_early_stop_condition(test_metrics) -> bool:

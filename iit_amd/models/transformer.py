@@ -30,7 +30,7 @@ from typing import List, Optional, Union
 import torch
 from torch import nn
 
-from ..engine.plan import RunPlan
+from ..engine.plan import RunPlan, scale_site as _scale_site, zero_grad_site as _zero_grad_site
 from ..hooks.hook_points import HookedRootModule, HookPoint
 from ..ops import select_ops
 from ..ops.torch_ops import TorchOps
@@ -81,18 +81,9 @@ class _Run:
                 for s in plan.splice[name]:
                     x = s.apply(x)
             if name in plan.scale:
-                x = x / plan.scale[name]
+                x = _scale_site(x, plan.scale[name])
             if name in plan.zero_grad and isinstance(x, torch.Tensor) and x.requires_grad:
-                idxs = plan.zero_grad[name]
-
-                def _mask(g, _idxs=idxs):
-                    g = g.clone()
-                    for ix in _idxs:
-                        g[ix.on(g.device)] = 0
-                    return g
-
-                x = x.view_as(x)
-                x.register_hook(_mask)
+                x = _zero_grad_site(x, plan.zero_grad[name])
         x = hp(x)
         if plan is not None and name in plan.capture:
             plan.cache[name] = x.detach()

@@ -28,6 +28,10 @@ from . import hip_kernels as K
 
 POLICY = os.environ.get("IIT_GEMM", "auto")
 DECISIONS: Dict[Tuple, Tuple[str, Dict[str, float]]] = {}
+# in-context tuning (scripts/tune_gemm_in_situ.py): per problem key a forced candidate, and a list that receives
+# (key, candidate, start event, end event) for every GEMM launched while it is set
+FORCE: Dict[Tuple, str] = {}
+TIMING = None
 BF16, F32 = torch.bfloat16, torch.float32
 _BLAS_OK = {}
 _BLAS_SELECTED = False
@@ -482,8 +486,18 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         choice = DECISIONS[key] = (best, times)
     if _decide_only:  # the measured time of the best implementation; nothing runs on C
         return choice[1][choice[0]]
-    calls[choice[0]](C, C2, C3)
-    return choice[0]
+    name = FORCE.get(key, choice[0])
+    if name not in calls:
+        name = choice[0]
+    if TIMING is not None:
+        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s_ev.record()
+        calls[name](C, C2, C3)
+        e_ev.record()
+        TIMING.append((key, name, s_ev, e_ev))
+        return name
+    calls[name](C, C2, C3)
+    return name
 
 
 K_ = K  # the kernel module (``K`` is shadowed by the reduction-size keyword above)
@@ -518,8 +532,10 @@ def export_table(path: str) -> int:
     """Write the measured decisions of this process (``DECISIONS``) as a decision table; returns the entry count."""
     import json
     dec = {repr(k): v[0] for k, v in DECISIONS.items()}
+    arch = getattr(torch.cuda.get_device_properties(0), "gcnArchName", "").split(":")[0] \
+        if torch.cuda.is_available() else None
     with open(path, "w") as f:
-        json.dump({"arch": "gfx950", "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else None,
+        json.dump({"arch": arch, "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else None,
                    "decisions": dec}, f, indent=0, sort_keys=True)
     return len(dec)
 

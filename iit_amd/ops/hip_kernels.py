@@ -43,8 +43,10 @@ _SIGS = {
     "iit_ce_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "iit_ce_bwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_long, c_int, c_int, c_int,
                    c_void_p],
-    "iit_adam_flat": [c_void_p] * 6 + [c_int, c_void_p, c_int] + [c_float] * 6 + [c_void_p, c_void_p, c_void_p],
+    "iit_adam_flat": [c_void_p] * 6 + [c_int, c_void_p, c_int] + [c_float] * 6 + [c_void_p] * 4,
     "iit_adam_span_size": [],
+    "iit_sumsq_spans": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "iit_adam_spans": [c_void_p] * 6 + [c_int, c_void_p] + [c_float] * 6 + [c_void_p] * 4,
     "iit_gelu_fwd": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_void_p],
     "iit_shadow_refresh": [c_void_p, c_int, c_void_p],
     "iit_shadow_desc_size": [],
@@ -63,6 +65,8 @@ _SIGS = {
     "iit_flash_fwd": [c_void_p] * 3 + [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ull] + [c_int] * 5
                      + [c_float, c_int, c_void_p],
     "iit_flash_bwd": [c_void_p] * 3 + [c_void_p] * 11 + [c_ull] + [c_int] * 5 + [c_float, c_int, c_void_p],
+    "iit_splice": [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_int, c_int, c_float, c_void_p],
+    "iit_splice_spec_size": [],
 }
 
 
@@ -163,7 +167,12 @@ GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 1
               9: (128, 96),  # 128 x 96: 256 tiles for the [4096][768] outputs
               10: (96, 192), 11: (192, 96),  # 2-way reduction split: 256 workgroups for the [768][3072] gradients
               12: (96, 96), 13: (128, 96), 14: (64, 64),  # deep LDS rings (6 / 5 / 8 K-tiles)
-              15: (128, 96), 16: (96, 96), 17: (64, 64), 18: (128, 128)}  # 128-deep K-tiles (K % 128 == 0)
+              15: (128, 96), 16: (96, 96), 17: (64, 64), 18: (128, 128),  # 128-deep K-tiles (K % 128 == 0)
+              20: (192, 192),  # weight gradients with a 4-way reduction split (2-deep ring)
+              21: (192, 128), 22: (128, 192),
+              # two co-resident workgroups per CU (<= 80 KiB LDS each): prologue / epilogue overlap
+              23: (128, 96), 24: (64, 96), 25: (128, 128), 26: (96, 96), 27: (128, 192), 28: (64, 192),
+              29: (64, 96), 30: (64, 64), 31: (64, 128)}  # three / four workgroups per CU
 # tiles 12-14 measured slower than their 4-deep twins on every step shape (profiles/gemm_ring_depth_r2.txt: the tiles
 # are intake-bandwidth-bound, not latency-bound), so the dispatcher does not offer them; kept for the experiment.
 # Tiles 15-18 (128-deep K-tiles) are within a few % of the 64-deep tiles and compete per shape.
@@ -237,7 +246,32 @@ def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None
            "iit_gemm_glds")
 
 
+def sumsq_spans(g, spans, nspans, part, step_dev, do_norm: bool):
+    """Sharded optimizer stage 1: per-block partial sums of g^2 over ``spans`` into ``part`` (1024 floats) and the
+    device step-counter bump."""
+    _check(lib().iit_sumsq_spans(_p(g), _p(spans), nspans, _p(part), part.numel(), int(do_norm), _p(step_dev),
+                                 _stream()), "sumsq_spans")
+
+
+def adam_spans(flat, g, m, v, spans, nspans, total, step_dev, *, lr, b1, b2, eps, wd, clip_norm, skipped=None,
+               hyper=None):
+    """Sharded optimizer stage 2: fused clip + Adam over ``spans`` (arena offsets for weights / mirror, shard offsets
+    for gradient / moments) with the global g^2 sum in ``total`` (fp32[1])."""
+    _check(lib().iit_adam_spans(_p(flat.data), _p(g), _p(m), _p(v), _p(flat.shadow), _p(spans), nspans, _p(total),
+                                float(clip_norm or 0.0), lr, b1, b2, eps, wd, _p(hyper), _p(step_dev), _p(skipped),
+                                _stream()), "adam_spans")
+
+
 # ------------------------------------------------------------------------------ others
+def splice(act, src, out, n, spec_ptr, f32, mode, scale=1.0):
+    """``csrc/splice.hip``: out = splice / zero-mask / scale of ``act`` over the packed range table at host address
+    ``spec_ptr`` (see :mod:`iit_amd.ops.splice`); act / out contiguous with ``n`` elements."""
+    if CHECK_BOUNDS:
+        _bounds("iit_splice", ("act", act, 1, n, n), ("out", out, 1, n, n))
+    _check(lib().iit_splice(_p(act), _p(src), _p(out), n, spec_ptr, int(f32), int(mode), float(scale), _stream()),
+           "iit_splice")
+
+
 def embed_pos_fwd(tokens, W_E, W_pos, out, B, S, d):
     _check(lib().iit_embed_pos_fwd(_p(tokens), _p(W_E), _p(W_pos), _p(out), B * S, S, d, _stream()), "embed_pos_fwd")
 
@@ -463,10 +497,11 @@ def make_shadow_descs(entries, device) -> torch.Tensor:
     return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
 
 
-def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_norm, skipped=None):
+def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_norm, skipped=None, hyper=None):
     """Fused clip + Adam over the arena's active spans (``flat.active_spans``); bumps the device step counter
     ``step_dev`` (int32[1]) and writes the bf16 mirror (``flat.shadow``) when present.  No host scalars depend
-    on the step: graph-capturable."""
+    on the step: graph-capturable.  ``hyper`` (fp32[5] on the device: lr, beta1, beta2, eps, weight decay)
+    overrides the scalar arguments, so a captured replay follows later learning-rate changes."""
     nparts = 1024
     part = getattr(flat, "_norm_parts", None)
     if part is None or part.numel() < nparts:
@@ -474,5 +509,5 @@ def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_
     spans, nspans = flat.span_table(lib().iit_adam_span_size())
     _check(lib().iit_adam_flat(_p(flat.data), _p(flat.grad), _p(exp_avg), _p(exp_avg_sq), _p(flat.shadow),
                                _p(spans), nspans, _p(part), nparts, float(clip_norm or 0.0), lr, b1, b2, eps, wd,
-                               _p(step_dev), _p(skipped), _stream()), "adam_flat")
+                               _p(hyper), _p(step_dev), _p(skipped), _stream()), "adam_flat")
     flat.after_step(mirror_written=flat.shadow is not None)

@@ -93,29 +93,42 @@ class _BiasSums:
 
     def __init__(self):
         self.items, self.params, self.stream = [], [], None
+        self.task = None  # autograd graph task whose final callback will flush the queue
 
     def add(self, x, ld, out, T, N, *params):
-        if (_DEFER_BIAS_SUMS and x.is_cuda and K.colsum_vec_ok(x, ld, out, N)
-                and (self.items or self._arm())):
+        if _DEFER_BIAS_SUMS and x.is_cuda and K.colsum_vec_ok(x, ld, out, N) and self._armed():
             self.items.append((x, ld, out, T, N))
             self.params.extend(params)
             return
         K.colsum_accum(x, ld, out, T, N)
         _done(*params)
 
-    def _arm(self) -> bool:
-        try:  # only inside an autograd backward pass; elsewhere the sum runs immediately
+    def _armed(self) -> bool:
+        """True when this backward pass's final callback is queued.  The queue is keyed by the autograd graph
+        task: a backward that raised after queueing (e.g. an aborted graph capture) never ran its callback, and
+        its stale items -- tensors of the failed pass -- are dropped instead of being summed into a later one."""
+        task = torch._C._current_graph_task_id()
+        if task < 0:
+            return False  # not inside an autograd backward pass: the sum runs immediately
+        if task == self.task:
+            return True
+        self.reset()
+        try:
             torch.autograd.Variable._execution_engine.queue_callback(self.flush)
         except RuntimeError:
             return False
+        self.task = task
         self.stream = torch.cuda.current_stream()
         return True
 
+    def reset(self) -> None:
+        self.items, self.params, self.stream, self.task = [], [], None, None
+
     def flush(self) -> None:
-        if not self.items:
-            return
         items, params, stream = self.items, self.params, self.stream
-        self.items, self.params, self.stream = [], [], None
+        self.reset()
+        if not items:
+            return
         with torch.cuda.stream(stream):
             K.colsum_multi(items)
         _done(*params)

@@ -31,24 +31,47 @@ class FusedAdam(torch.optim.Optimizer):
     """
 
     def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, use_hip: Optional[bool] = None, nan_guard: bool = True):
+                 weight_decay: float = 0.0, use_hip: Optional[bool] = None, nan_guard: bool = True,
+                 alloc_moments: bool = True):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(flat.params, defaults)
         self.flat = flat
-        self.exp_avg = torch.zeros_like(flat.data)
-        self.exp_avg_sq = torch.zeros_like(flat.data)
+        # (the sharded subclass allocates shard-sized moments itself: no transient arena-sized pair)
+        self.exp_avg = torch.zeros_like(flat.data) if alloc_moments else None
+        self.exp_avg_sq = torch.zeros_like(flat.data) if alloc_moments else None
         self.step_count = 0
         self.pending_clip = None
         self.nan_guard = nan_guard
         dev = flat.data.device
         self._step_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # device-side step counter
         self._skipped_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        # device copy of (lr, beta1, beta2, eps, weight_decay): the fused kernel reads it, so a graph-captured
+        # step follows hyper-parameter changes (an LR scheduler) made between replays -- see sync_hyper
+        self._hyper_dev = torch.zeros(5, dtype=torch.float32, device=dev)
+        self._hyper_host = None
         if use_hip is None:
             use_hip = flat.data.is_cuda
         self._hip = None
         if use_hip:
             from . import hip_kernels
             self._hip = hip_kernels.lib()
+
+    def _hyper(self):
+        group = self.param_groups[0]
+        (b1, b2) = group["betas"]
+        return (float(group["lr"]), float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]))
+
+    def sync_hyper(self) -> None:
+        """Copy changed hyper-parameters to the device scalars the fused kernel reads.  Called by every eager
+        ``step`` and by the graph runners before each replay of a captured phase (a replay does not run ``step``'s
+        host code); a no-op while capturing and when nothing changed."""
+        h = self._hyper()
+        if h == self._hyper_host:
+            return
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return  # the eager warm-up before the capture has already synchronised them
+        self._hyper_dev.copy_(torch.tensor(h, dtype=torch.float32))
+        self._hyper_host = h
 
     @property
     def skipped_steps(self) -> int:
@@ -70,9 +93,14 @@ class FusedAdam(torch.optim.Optimizer):
             from . import hip_kernels
             self.step_count += 1
             self._validate_restriction(wd)
+            self.sync_hyper()
+            capturing = torch.cuda.is_current_stream_capturing()
+            if capturing and self._hyper_host != self._hyper():
+                raise RuntimeError("FusedAdam: hyper-parameters changed since the last eager step; run one eager "
+                                   "step (or sync_hyper()) before capturing")
             hip_kernels.adam_step(self.flat, self.exp_avg, self.exp_avg_sq, self._step_dev, lr=lr, b1=b1, b2=b2,
                                   eps=eps, wd=wd, clip_norm=clip_norm,
-                                  skipped=self._skipped_dev if self.nan_guard else None)
+                                  skipped=self._skipped_dev if self.nan_guard else None, hyper=self._hyper_dev)
             return
         norm = torch.linalg.vector_norm(g) if (clip_norm or self.nan_guard) else None
         if self.nan_guard and not bool(torch.isfinite(norm)):

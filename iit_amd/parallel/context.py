@@ -63,7 +63,7 @@ class _GatherSeq(torch.autograd.Function):
             out = torch.empty_like(chunks[:n])
             dist.reduce_scatter_tensor(out, chunks, group=ctx.group)
             return out.movedim(0, dim), None, None
-        g = g.contiguous()
+        g = g.clone(memory_format=torch.contiguous_format)  # never reduce in place into an autograd-owned buffer
         dist.all_reduce(g, group=ctx.group)  # gloo: no reduce-scatter
         return g.narrow(dim, r * n, n), None, None
 

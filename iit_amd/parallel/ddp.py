@@ -69,6 +69,7 @@ class GradReducer:
         self._hooks = []
         self._listener = None
         self._subsets = {}
+        self.shard = None  # ShardedFusedAdam (ZeRO-1): buckets are reduce-scattered into its shard buffers
         self.paused = False  # True while a graph-captured backward runs (reduction happens after it)
         self.deferred = False  # this backward: no per-parameter launches (several forwards wrote each gradient)
         self._grad_forwards = 0
@@ -104,12 +105,41 @@ class GradReducer:
             self._mark_ready(_i)
         return hook
 
+    def attach_shard(self, optimizer) -> None:
+        """Optimizer-state sharding (iit_amd.parallel.zero): reduce-scatter every bucket into ``optimizer``'s shard
+        buffers instead of all-reducing it in place; the optimizer all-gathers the updated weights."""
+        self.shard = optimizer
+        optimizer.set_buckets(self.buckets)
+
     def _launch(self, b: int):
         if self._launched[b]:
             return
         self._launched[b] = True
         s, e = self.buckets[b]
+        if self.shard is not None:
+            self._launch_reduce_scatter(b, s, e)
+            return
         self._launch_span(s, e)
+
+    def _launch_reduce_scatter(self, b: int, s: int, e: int) -> None:
+        """Bucket ``b`` -> the averaged gradient of this rank's piece in the shard buffer (async)."""
+        sh = self.shard
+        world, rank, piece = sh.plan.world, sh.plan.rank, sh.plan.piece[b]
+        out = sh.shard_view(b)
+        src = self.flat.grad[s:e]
+        if self.wire_dtype is not None:
+            src = src.to(self.wire_dtype)
+        inp = sh.padded_input(b, src)
+        if self._use_avg:  # RCCL: reduce-scatter with AVG
+            dst = out if self.wire_dtype is None else torch.empty(piece, dtype=self.wire_dtype, device=out.device)
+            work = dist.reduce_scatter_tensor(dst, inp, op=dist.ReduceOp.AVG, async_op=True)
+            post = None if dst is out else (lambda d=dst, o=out: o.copy_(d))
+        else:  # gloo (no reduce-scatter): all-reduce the padded bucket, keep this rank's piece
+            if inp is src:
+                inp = inp.clone()
+            work = dist.all_reduce(inp, op=dist.ReduceOp.SUM, async_op=True)
+            post = lambda i=inp, o=out: o.copy_(i[rank * piece:(rank + 1) * piece]).div_(world)  # noqa: E731
+        self._works.append((work, None, None, None, post))
 
     def _launch_span(self, s: int, e: int) -> None:
         """Async all-reduce of arena elements [s, e): rows-restricted parameters compactly, the rest in place."""
@@ -138,7 +168,7 @@ class GradReducer:
                 scatter = (full, rows)
             buf = dst if self.wire_dtype is None else dst.to(self.wire_dtype)
             home = None if self.wire_dtype is None else dst  # fp32 destination of the bf16 wire buffer
-            self._works.append((dist.all_reduce(buf, op=op, async_op=True), buf, scatter, home))
+            self._works.append((dist.all_reduce(buf, op=op, async_op=True), buf, scatter, home, None))
 
     def launch_range(self, s: int, e: int) -> None:
         """Start reducing every bucket inside arena range [s, e) now (async; ``finish`` waits).  The staged
@@ -178,6 +208,8 @@ class GradReducer:
             out.extend(pieces)
         out.sort(key=lambda r: -r[0])  # reverse arena order, like ``FlatParams.buckets``
         self.buckets = out
+        if self.shard is not None:
+            self.shard.set_buckets(self.buckets)
         self._param_bucket = []
         self._bucket_count = [0] * len(self.buckets)
         for o, n in self.flat.offsets:
@@ -209,8 +241,11 @@ class GradReducer:
         for b in range(len(self.buckets)):
             if not self._launched[b]:
                 self._launch(b)
-        for work, buf, scatter, home in self._works:
+        for work, buf, scatter, home, post in self._works:
             work.wait()
+            if post is not None:  # reduce-scatter into the optimizer shard
+                post()
+                continue
             if home is not None:  # bf16 wire buffer back into its fp32 destination
                 home.copy_(buf)
                 buf = home

@@ -1,0 +1,257 @@
+"""Optimizer-state sharding (ZeRO stage 1) for data parallelism over RCCL/xGMI.
+
+Replicated data parallelism (:class:`iit_amd.parallel.ddp.GradReducer` + :class:`iit_amd.ops.optim.FusedAdam`)
+keeps, on every rank, the fp32 master weights, the fp32 gradient and both Adam moments of the whole model, and runs
+clip + Adam over all of it: for Llama-3-8B that is 32 GB of moments per moment and a 126 ms optimizer pass per step
+on every GPU (``profiles/llama3_8b_kernel_stats_v3.txt``).  With ``ShardedFusedAdam`` each optimizer phase is
+
+  1. **reduce-scatter** per gradient bucket (in the staged schedule: per backward stage, overlapped with the next
+     stage's backward exactly like the all-reduce it replaces): bucket ``[s, e)`` is split into ``N`` equal pieces of
+     ``P = ceil((e - s) / N)`` (rounded to 64 elements); rank ``r`` receives the averaged gradient of piece ``r`` in
+     its shard buffer;
+  2. **sharded global-norm clip**: every rank sums g^2 over its pieces (the fused sumsq kernel over a shard span
+     table), one 4-byte all-reduce gives the global norm, and the clip coefficient is formed on device;
+  3. **sharded Adam**: the fused kernel updates only this rank's pieces -- master weights and bf16 mirror at their
+     arena offsets, gradient and moments at their shard offsets -- so moments take ``8/N`` bytes per parameter
+     instead of 8 and the pass is ``N`` times shorter;
+  4. **all-gather** of the updated fp32 pieces per bucket back into every rank's arena, then the bf16 mirror of the
+     bucket is re-derived locally (a cast pass), so the next phase's forward reads identical weights on every rank.
+
+Bytes on xGMI per optimizer phase equal a ring all-reduce of the gradient (reduce-scatter + all-gather of the same
+size: ``2 (N-1)/N * 4 B`` per parameter); what changes is memory (moments ``/N``) and optimizer time (``/N``).
+``bf16`` wire (``IIT_DP_GRAD_DTYPE=bf16``) halves the reduce-scatter bytes as for the all-reduce.
+
+Semantics equal the replicated optimizer up to the summation order of the gradient average: every rank applies the
+Adam math of ``torch.optim.Adam`` to the averaged, globally clipped gradient (``/root/reference/iit/model_pairs/
+iit_behavior_model_pair.py:60-64``: zero_grad -> backward -> clip -> step).  gloo (CPU tests) has no reduce-scatter:
+there the bucket is all-reduced and each rank keeps its piece.
+
+Per-rank memory model (fp32 master + fp32 gradient + bf16 mirror replicated, moments sharded):
+``P * (4 + 4 + 2) + 8 P / N`` bytes for ``P`` parameters -- Llama-3-8B at N = 8: 80.3 GB + 8.0 GB = 88.3 GB
+(replicated: 144.5 GB), see :func:`memory_model`.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..engine.flat import FlatParams, make_span_tensor
+from ..ops.optim import FusedAdam
+from . import dist as pdist
+
+_ALIGN = 64
+
+
+def _piece(n: int, world: int) -> int:
+    p = (n + world - 1) // world
+    return (p + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+class ShardPlan:
+    """Which arena elements this rank owns: piece ``rank`` of every bucket ``[s, e)`` (arena order of buckets is
+    irrelevant; the local shard buffers concatenate this rank's pieces bucket by bucket)."""
+
+    def __init__(self, buckets: Sequence[Tuple[int, int]], world: int, rank: int):
+        self.world, self.rank = world, rank
+        self.buckets: List[Tuple[int, int]] = [(int(s), int(e)) for s, e in buckets]
+        self.piece: List[int] = []     # piece length per bucket (same on every rank)
+        self.local: List[int] = []     # offset of this rank's piece in the shard buffers
+        self.own: List[Tuple[int, int]] = []  # owned arena range per bucket (may be empty / shorter than the piece)
+        off = 0
+        for s, e in self.buckets:
+            p = _piece(e - s, world)
+            a = min(e, s + rank * p)
+            b = min(e, s + (rank + 1) * p)
+            self.piece.append(p)
+            self.local.append(off)
+            self.own.append((a, b))
+            off += p
+        self.numel = off  # shard buffer length (elements)
+        self.index: Dict[Tuple[int, int], int] = {bk: i for i, bk in enumerate(self.buckets)}
+
+    def spans(self, max_len4: int = 1024) -> List[Tuple[int, int, int]]:
+        """Optimizer span records (arena start4, shard start4, len4) over the owned pieces."""
+        out = []
+        for (a, b), loc in zip(self.own, self.local):
+            pos, n = a // 4, (b - a) // 4
+            lpos = loc // 4
+            while n > 0:
+                ln = min(max_len4, n)
+                out.append((pos, lpos, ln))
+                pos += ln
+                lpos += ln
+                n -= ln
+        return out
+
+
+class ShardedFusedAdam(FusedAdam):
+    """:class:`FusedAdam` with optimizer state sharded over the data-parallel ranks (see the module docstring).
+
+    The gradient reducer (``GradReducer(..., shard=optimizer)``) fills :attr:`shard_grad` by reduce-scatter; ``step``
+    clips with the global norm, updates this rank's pieces and all-gathers them.  ``step`` issues collectives, so a
+    graph-captured phase runs it eagerly (``sharded = True``)."""
+
+    sharded = True
+
+    def __init__(self, flat: FlatParams, buckets: Sequence[Tuple[int, int]], lr: float = 1e-3, betas=(0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 0.0, use_hip: Optional[bool] = None, nan_guard: bool = True):
+        super().__init__(flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, use_hip=use_hip,
+                         nan_guard=nan_guard, alloc_moments=False)
+        dev = flat.data.device
+        self._total = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._part = torch.zeros(1024, dtype=torch.float32, device=dev)
+        self.plan = None
+        self.set_buckets(buckets)
+
+    def set_buckets(self, buckets: Sequence[Tuple[int, int]]) -> None:
+        """(Re)build the shard plan over the reducer's gradient buckets (the staged schedule re-buckets the arena
+        once, before training).  The moments live in the plan's layout, so this is only allowed before the first
+        step (or with an unchanged layout)."""
+        plan = ShardPlan(buckets, pdist.world_size(), pdist.rank())
+        if self.plan is not None and plan.buckets == self.plan.buckets:
+            return
+        if self.plan is not None and self.step_count:
+            raise RuntimeError("optimizer-state sharding: the gradient buckets changed after the first step")
+        dev = self.flat.data.device
+        self.plan = plan
+        # shard-sized moments and gradient (the replicated optimizer's arena-sized ones are dropped)
+        self.exp_avg = torch.zeros(plan.numel, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(plan.numel, dtype=torch.float32, device=dev)
+        self.shard_grad = torch.zeros(plan.numel, dtype=torch.float32, device=dev)
+        spans = plan.spans()
+        self._spans = make_span_tensor(spans, dev)
+        self._nspans = len(spans)
+        self._gather_bufs: Dict[tuple, torch.Tensor] = {}
+
+    # ------------------------------------------------------------------ gradient side (called by the reducer)
+    def shard_view(self, bucket: int) -> torch.Tensor:
+        p = self.plan.piece[bucket]
+        loc = self.plan.local[bucket]
+        return self.shard_grad[loc:loc + p]
+
+    def padded_input(self, bucket: int, src: torch.Tensor) -> torch.Tensor:
+        """``src`` (bucket ``[s, e)`` of the gradient arena) padded with zeros to ``N * piece`` elements."""
+        s, e = self.plan.buckets[bucket]
+        full = self.plan.piece[bucket] * self.plan.world
+        if full == e - s:
+            return src
+        buf = self._gather_bufs.get(("in", bucket))
+        if buf is None or buf.dtype != src.dtype:
+            buf = self._gather_bufs[("in", bucket)] = torch.zeros(full, dtype=src.dtype, device=src.device)
+        buf[:e - s].copy_(src)
+        return buf
+
+    # ------------------------------------------------------------------ optimizer
+    @torch.no_grad()
+    def step(self, closure=None, clip_norm: Optional[float] = None):
+        if closure is not None:
+            with torch.enable_grad():
+                closure()
+        group = self.param_groups[0]
+        lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+        self.step_count += 1
+        self.sync_hyper()
+        need_norm = bool(clip_norm) or self.nan_guard
+        if self._hip is not None:
+            from ..ops import hip_kernels as K
+            K.sumsq_spans(self.shard_grad, self._spans, self._nspans, self._part, self._step_dev, need_norm)
+            if need_norm:
+                torch.sum(self._part, dim=0, keepdim=True, out=self._total)
+                if pdist.world_size() > 1:
+                    dist.all_reduce(self._total, op=dist.ReduceOp.SUM)
+            K.adam_spans(self.flat, self.shard_grad, self.exp_avg, self.exp_avg_sq, self._spans, self._nspans,
+                         self._total, self._step_dev, lr=lr, b1=b1, b2=b2, eps=eps, wd=wd, clip_norm=clip_norm,
+                         skipped=self._skipped_dev if self.nan_guard else None, hyper=self._hyper_dev)
+        else:
+            self._step_torch(clip_norm, lr, b1, b2, eps, wd, need_norm)
+        self._all_gather()
+
+    def _owned_views(self):
+        """(arena view, shard view) per bucket for this rank's owned elements."""
+        for (a, b), loc in zip(self.plan.own, self.plan.local):
+            if b > a:
+                yield self.flat.data[a:b], loc, b - a
+
+    def _step_torch(self, clip_norm, lr, b1, b2, eps, wd, need_norm):
+        g = self.shard_grad
+        if need_norm:
+            tot = (g.double() ** 2).sum().reshape(1)
+            if pdist.world_size() > 1:
+                dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+            norm = tot.sqrt().float()
+            if self.nan_guard and not bool(torch.isfinite(norm)):
+                self._skipped_dev += 1
+                self.step_count -= 1
+                return
+        self._step_dev += 1
+        t = int(self._step_dev.item())
+        bc1 = 1.0 - b1 ** t
+        bc2 = 1.0 - b2 ** t
+        coef = 1.0
+        if clip_norm:
+            coef = float(torch.clamp(clip_norm / (norm + 1e-6), max=1.0))
+        for p, loc, n in self._owned_views():
+            gg = g[loc:loc + n] * coef
+            if wd:
+                gg = gg.add(p, alpha=wd)
+            m = self.exp_avg[loc:loc + n]
+            v = self.exp_avg_sq[loc:loc + n]
+            m.mul_(b1).add_(gg, alpha=1 - b1)
+            v.mul_(b2).addcmul_(gg, gg, value=1 - b2)
+            denom = (v.sqrt() / (bc2 ** 0.5)).add_(eps)
+            p.addcdiv_(m, denom, value=-lr / bc1)
+
+    def _all_gather(self) -> None:
+        """Every rank's updated pieces back into every arena; the bf16 mirror of each bucket re-derived locally."""
+        flat = self.flat
+        world = self.plan.world
+        for bi, (s, e) in enumerate(self.plan.buckets):
+            p = self.plan.piece[bi]
+            a, b = self.plan.own[bi]
+            if world > 1:
+                full = p * world
+                exact = full == e - s
+                out = flat.data[s:e] if exact else self._gather_bufs.get(("out", bi))
+                if out is None:
+                    out = self._gather_bufs[("out", bi)] = torch.zeros(full, dtype=torch.float32,
+                                                                     device=flat.data.device)
+                piece = out[self.plan.rank * p:(self.plan.rank + 1) * p]
+                if not exact:
+                    piece.zero_()
+                    if b > a:
+                        piece[:b - a].copy_(flat.data[a:b])
+                parts = list(out.split(p))
+                if dist.get_backend() == "nccl":
+                    dist.all_gather_into_tensor(out, piece.clone() if exact else piece)
+                else:
+                    dist.all_gather(parts, piece.clone())
+                if not exact:
+                    flat.data[s:e].copy_(out[:e - s])
+            if flat.shadow is not None:
+                flat.shadow[s:e].copy_(flat.data[s:e])
+        flat.after_step(mirror_written=flat.shadow is not None)
+
+    # ------------------------------------------------------------------ checkpointing
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["shard"] = {"world": self.plan.world, "rank": self.plan.rank, "buckets": self.plan.buckets}
+        return sd
+
+    def load_state_dict(self, sd):
+        shard = sd.get("shard")
+        if shard is None or shard["world"] != self.plan.world or [tuple(b) for b in shard["buckets"]] != \
+                self.plan.buckets:
+            raise ValueError("sharded optimizer state was saved with another data-parallel layout")
+        super().load_state_dict(sd)
+
+
+def memory_model(n_params: int, world: int, mirror: bool = True) -> Dict[str, float]:
+    """Per-rank bytes of the training state for ``n_params`` parameters (activations excluded): replicated
+    data parallelism vs optimizer-state sharding."""
+    master, grad, mom = 4 * n_params, 4 * n_params, 8 * n_params
+    shadow = 2 * n_params if mirror else 0
+    return {"replicated_GB": (master + grad + mom + shadow) / 1e9,
+            "sharded_GB": (master + grad + shadow + mom / world) / 1e9,
+            "moments_per_rank_GB": mom / world / 1e9}

@@ -1,7 +1,9 @@
 """Eight-node arithmetic causal graph (the HL side of ``BASELINE.json`` config 5).
 
 Input ``[BOS, a, b, c, d, =]`` (digit tokens), the answer token is predicted at the
-last position.  HL graph, 8 hooked nodes::
+last position; ``seq_len > 6`` puts a context of random filler tokens between BOS and
+the operands (long-context runs: the operands stay the last five positions).  HL
+graph, 8 hooked nodes::
 
     a   b   c   d            leaves   (hook_a .. hook_d)
      \\ /     \\ /
@@ -36,6 +38,7 @@ from ...model_pairs.strict_iit_model_pair import StrictIITModelPair
 from ..hl_model import HLModel
 
 BOS, EQ, DIGIT0 = 1, 2, 10
+FILLER = (3, 10)  # filler token range of long-context prompts (never a digit, BOS or "=")
 NODES = ("hook_a", "hook_b", "hook_c", "hook_d", "hook_s1", "hook_s2", "hook_p", "hook_out")
 SEQ = 6
 
@@ -57,8 +60,9 @@ class CausalGraphHL(HookedRootModule, HLModel):
 
     def forward(self, args):
         x = args[0]
-        a, b, c, d = (self.hook_a(x[:, 1] - DIGIT0), self.hook_b(x[:, 2] - DIGIT0), self.hook_c(x[:, 3] - DIGIT0),
-                      self.hook_d(x[:, 4] - DIGIT0))
+        # the operands are the four positions before the final "=" (positions 1..4 of the 6-token prompt)
+        a, b, c, d = (self.hook_a(x[:, -5] - DIGIT0), self.hook_b(x[:, -4] - DIGIT0), self.hook_c(x[:, -3] - DIGIT0),
+                      self.hook_d(x[:, -2] - DIGIT0))
         s1 = self.hook_s1((a + b) % 10)
         s2 = self.hook_s2((c + d) % 10)
         p = self.hook_p((s1 * s2) % 10)
@@ -67,9 +71,12 @@ class CausalGraphHL(HookedRootModule, HLModel):
 
 
 class CausalGraphDataset(torch.utils.data.Dataset):
-    """``(x [6], y, iv [8])`` items; all 10^4 inputs are distinct, ``n`` of them drawn by ``seed``."""
+    """``(x [seq_len], y, iv [8])`` items; all 10^4 operand tuples are distinct, ``n`` of them drawn by ``seed``;
+    ``seq_len > 6`` inserts ``seq_len - 6`` random filler tokens after BOS."""
 
-    def __init__(self, n: int = 10000, seed: int = 0, device=None):
+    def __init__(self, n: int = 10000, seed: int = 0, device=None, seq_len: int = SEQ):
+        if seq_len < SEQ:
+            raise ValueError(f"seq_len must be >= {SEQ}")
         rng = np.random.default_rng(seed)
         codes = rng.permutation(10 ** 4)[:n] if n <= 10 ** 4 else rng.integers(0, 10 ** 4, n)
         dig = np.stack([(codes // 10 ** k) % 10 for k in (3, 2, 1, 0)], axis=1)
@@ -80,6 +87,9 @@ class CausalGraphDataset(torch.utils.data.Dataset):
         dev = torch.device(device) if device is not None else torch.device(DEVICE)
         x = torch.stack([torch.full_like(a, BOS), a + DIGIT0, b + DIGIT0, c + DIGIT0, d + DIGIT0,
                          torch.full_like(a, EQ)], dim=1)
+        if seq_len > SEQ:
+            fill = torch.as_tensor(rng.integers(FILLER[0], FILLER[1], (x.shape[0], seq_len - SEQ)))
+            x = torch.cat([x[:, :1], fill, x[:, 1:]], dim=1)
         self.x = x.long().to(dev)
         self.y = (out + DIGIT0).long().to(dev)
         self.iv = torch.stack([a, b, c, d, s1, s2, p, out], dim=1).long().to(dev)
@@ -98,15 +108,15 @@ class CausalGraphDataset(torch.utils.data.Dataset):
         return torch.unique(self.x)
 
 
-def make_causal_graph_corr(n_layers: int, n_heads: int, d_mlp: int) -> Correspondence:
-    """Default alignment of the 8 HL nodes with an ``n_layers`` hooked transformer."""
+def make_causal_graph_corr(n_layers: int, n_heads: int, d_mlp: int, seq_len: int = SEQ) -> Correspondence:
+    """Default alignment of the 8 HL nodes with an ``n_layers`` hooked transformer (prompts of ``seq_len``)."""
     early = max(0, n_layers // 4)
     mid = min(n_layers - 1, max(early + 1, n_layers // 2)) if n_layers > 1 else 0
     last = n_layers - 1
     h = max(1, n_heads // 2)
     corr: Dict[HLNode, set] = {}
     for i, n in enumerate(NODES[:4]):
-        corr[HLNode(n, 10)] = {LLNode("hook_embed", Ix[:, i + 1])}
+        corr[HLNode(n, 10)] = {LLNode("hook_embed", Ix[:, seq_len - 5 + i])}
     corr[HLNode("hook_s1", 10)] = {LLNode(f"blocks.{early}.attn.hook_z", Ix[:, -1, :h, :])}
     corr[HLNode("hook_s2", 10)] = {LLNode(f"blocks.{early}.attn.hook_z", Ix[:, -1, h:, :])}
     if mid == last:  # shallow models: p and out share the last MLP, split by neurons
@@ -169,10 +179,10 @@ class CausalGraphModelPair(StrictIITModelPair):
         return {"val/iit_loss": loss_fn(ll_last, hl_output).detach(), "val/IIA": iia, "val/accuracy": acc}
 
 
-def make_causal_graph_task(ll_model, n_samples: int = 10000, seed: int = 0, device=None):
+def make_causal_graph_task(ll_model, n_samples: int = 10000, seed: int = 0, device=None, seq_len: int = SEQ):
     """(dataset, HL model, corr) for a hooked-transformer LL model."""
     cfg = ll_model.cfg
-    ds = CausalGraphDataset(n_samples, seed, device=device)
+    ds = CausalGraphDataset(n_samples, seed, device=device, seq_len=seq_len)
     hl = CausalGraphHL(cfg.d_vocab_out)
-    corr = make_causal_graph_corr(cfg.n_layers, cfg.n_heads, cfg.d_mlp)
+    corr = make_causal_graph_corr(cfg.n_layers, cfg.n_heads, cfg.d_mlp, seq_len=seq_len)
     return ds, hl, corr

@@ -12,12 +12,16 @@ For every candidate LL node (all / in-circuit / not-in-circuit, via
 * **mean / zero ablation** — replace the node by its dataset mean (or 0) and count
   the fraction of correctly-predicted base inputs whose prediction flips.
 
-MI355X-native execution: with a plan-capable LL model the source activation is
-captured by a truncated ``run_capture`` and the patch is an in-kernel splice
-(:class:`iit_amd.engine.plan.RunPlan`); the per-node sweep never builds hook
-closures, computes only the logits the metric reads, and accumulates scores on
-device (one host read per sweep instead of one per node per batch).  Any other
-LL model takes the reference hook path.
+MI355X-native execution: with a plan-capable LL model each batch costs ONE
+truncated source capture of every candidate node's hook (the reference re-runs
+the source forward for every node), ONE HL base output and -- for mean / zero
+ablation -- ONE unablated base forward, all shared by the node loop; each node is
+then a single spliced forward (:class:`iit_amd.engine.plan.RunPlan`: in-kernel or
+patch-spec-kernel splices, a broadcast mean as the source), computing only the
+logits the metric reads, with scores accumulated on device (one host read per
+sweep instead of one per node per batch).  The scores are the per-node path's
+bit for bit (tests/test_eval_ablations.py).  Any other LL model takes the
+reference hook path.
 """
 from __future__ import annotations
 
@@ -92,15 +96,10 @@ def do_intervention(model_pair, base_input, ablation_input, node: LLNode, hooker
     return model_pair.ll_model.run_with_hooks(base_input, fwd_hooks=[(node.name, hooker)])
 
 
-def resample_ablate_node(model_pair, base_in, ablation_in, node: LLNode, results: Dict, hooker: Optional[Callable] = None,
-                         atol: float = 5e-2, verbose: bool = False,
-                         categorical_metric: Categorical_Metric = Categorical_Metric.KL) -> None:
-    """Adds this batch's score for ``node`` to ``results[node]`` (a device scalar; summed over batches)."""
-    base_x, base_y = base_in[0], base_in[1]
-    ablation_y = ablation_in[1]
+def _resample_score(model_pair, base_in, ablation_in, ll_out, base_hl_out, hl_reduced, atol: float = 5e-2,
+                    verbose: bool = False, node=None, categorical_metric: Categorical_Metric = Categorical_Metric.KL):
+    base_y, ablation_y = base_in[1], ablation_in[1]
     reduced = _reduced_logits(model_pair)
-    ll_out = do_intervention(model_pair, base_x, ablation_in[0], node, hooker)
-    base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
     if model_pair.hl_model.is_categorical():
         label_idx = model_pair.get_label_idxs()
         label_unchanged = _labels_at(base_y, label_idx) == _labels_at(ablation_y, label_idx)
@@ -122,19 +121,48 @@ def resample_ablate_node(model_pair, base_in, ablation_in, node: LLNode, results
                                      atol=atol)
         changed = (~label_unchanged).float().reshape(ll_unchanged.shape) * (~ll_unchanged).float()
         score = changed.sum() / (~label_unchanged).float().sum()
-    results[node] = results[node] + score.detach()
+    return score.detach()
+
+
+def resample_ablate_node(model_pair, base_in, ablation_in, node: LLNode, results: Dict, hooker: Optional[Callable] = None,
+                         atol: float = 5e-2, verbose: bool = False,
+                         categorical_metric: Categorical_Metric = Categorical_Metric.KL) -> None:
+    """Adds this batch's score for ``node`` to ``results[node]`` (a device scalar; summed over batches)."""
+    ll_out = do_intervention(model_pair, base_in[0], ablation_in[0], node, hooker)
+    base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
+    results[node] = results[node] + _resample_score(model_pair, base_in, ablation_in, ll_out, base_hl_out, hl_reduced,
+                                                    atol, verbose, node, categorical_metric)
+
+
+def resample_ablate_nodes(model_pair, base_in, ablation_in, nodes, results: Dict, atol: float = 5e-2,
+                          verbose: bool = False, categorical_metric: Categorical_Metric = Categorical_Metric.KL) -> None:
+    """Native batched form of :func:`resample_ablate_node` over ``nodes``: one source capture of every node's hook
+    and one HL base output for the batch, then one spliced base forward per node."""
+    with torch.no_grad():
+        cache = model_pair.ll_source_cache(ablation_in[0], nodes)
+        model_pair.ll_cache = cache
+        base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
+        for node in nodes:
+            ll_out = model_pair.ll_intervened_forward(base_in[0], [node])
+            results[node] = results[node] + _resample_score(model_pair, base_in, ablation_in, ll_out, base_hl_out,
+                                                            hl_reduced, atol, verbose, node, categorical_metric)
 
 
 def check_causal_effect(model_pair, dataset, batch_size: int = 256, node_type: str = "a", verbose: bool = False,
                         categorical_metric: Categorical_Metric = Categorical_Metric.KL) -> Dict[LLNode, float]:
     """Mean resample-ablation score per node over the dataset (``eval_ablations.py:128-161``)."""
     nodes = _nodes(model_pair, node_type)
-    hookers = {} if _native(model_pair) else {n: model_pair.make_ll_ablation_hook(n) for n in nodes}
+    native = _native(model_pair)
+    hookers = {} if native else {n: model_pair.make_ll_ablation_hook(n) for n in nodes}
     results = {n: 0 for n in nodes}
     loader = dataset.make_loader(batch_size=batch_size, num_workers=0)
     nb = 0
     for base_in, ablation_in in progress(loader, desc="resample ablation"):
         nb += 1
+        if native:
+            resample_ablate_nodes(model_pair, base_in, ablation_in, nodes, results, verbose=verbose,
+                                  categorical_metric=categorical_metric)
+            continue
         for node in nodes:
             resample_ablate_node(model_pair, base_in, ablation_in, node, results, hookers.get(node), verbose=verbose,
                                  categorical_metric=categorical_metric)
@@ -185,24 +213,8 @@ def _ablation_value(node: LLNode, mean_cache, use_mean_cache: bool, like: torch.
     return torch.zeros_like(like)
 
 
-def ablate_node(model_pair, base_in, node: LLNode, results: Dict, hook: Optional[Callable] = None, atol: float = 5e-2,
-                verbose: bool = False, mean_cache=None, use_mean_cache: bool = True, shapes=None) -> None:
-    base_x, base_y = base_in[0], base_in[1]
-    model = model_pair.ll_model
+def _ablation_score(model_pair, ll_out, base_ll_out, base_hl_out, hl_reduced, atol: float = 5e-2):
     reduced = _reduced_logits(model_pair)
-    with torch.no_grad():
-        if _native(model_pair):
-            like = shapes[node.name] if shapes is not None else model.run_capture(base_x, [node.name])[node.name]
-            if like.shape[0] != base_x.shape[0]:
-                like = like[:1].expand(base_x.shape[0], *like.shape[1:])
-            val = _ablation_value(node, mean_cache, use_mean_cache, like)
-            plan = RunPlan.with_splices([(node.name, node.index, val)], logits=model_pair.ll_logits_mode())
-            ll_out = model(base_x, plan=plan)
-            base_ll_out = model_pair.ll_forward(base_x)
-        else:
-            ll_out = model.run_with_hooks(base_x, fwd_hooks=[(node.name, hook)])
-            base_ll_out = model(base_x)
-        base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
     if model_pair.hl_model.is_categorical():
         label_idx = model_pair.get_label_idxs()
         ll_pred = torch.argmax(_at(ll_out.squeeze() if not reduced else ll_out, label_idx, reduced), dim=-1)
@@ -216,7 +228,45 @@ def ablate_node(model_pair, base_in, node: LLNode, results: Dict, hook: Optional
         ll_unchanged = torch.isclose(ll_out.float().squeeze(), base_hl_out.float().squeeze(), atol=atol)
         accuracy = torch.isclose(base_ll_out.float().squeeze(), base_hl_out.float().squeeze(), atol=atol).float()
         changed = (~ll_unchanged).float() * accuracy
-    results[node] = results[node] + changed.sum() / (accuracy.sum() + 1e-6)
+    return changed.sum() / (accuracy.sum() + 1e-6)
+
+
+def ablate_node(model_pair, base_in, node: LLNode, results: Dict, hook: Optional[Callable] = None, atol: float = 5e-2,
+                verbose: bool = False, mean_cache=None, use_mean_cache: bool = True, shapes=None) -> None:
+    base_x = base_in[0]
+    model = model_pair.ll_model
+    with torch.no_grad():
+        if _native(model_pair):
+            like = shapes[node.name] if shapes is not None else model.run_capture(base_x, [node.name])[node.name]
+            if like.shape[0] != base_x.shape[0]:
+                like = like[:1].expand(base_x.shape[0], *like.shape[1:])
+            val = _ablation_value(node, mean_cache, use_mean_cache, like)
+            plan = RunPlan.with_splices([(node.name, node.index, val)], logits=model_pair.ll_logits_mode())
+            ll_out = model(base_x, plan=plan)
+            base_ll_out = model_pair.ll_forward(base_x)
+        else:
+            ll_out = model.run_with_hooks(base_x, fwd_hooks=[(node.name, hook)])
+            base_ll_out = model(base_x)
+        base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
+    results[node] = results[node] + _ablation_score(model_pair, ll_out, base_ll_out, base_hl_out, hl_reduced, atol)
+
+
+def ablate_nodes(model_pair, base_in, nodes, results: Dict, values: Dict[str, torch.Tensor], atol: float = 5e-2) -> None:
+    """Native batched form of :func:`ablate_node` over ``nodes``: one unablated base forward and one HL base output
+    per batch, then one spliced forward per node with its [1, ...] ablation value broadcast over the batch."""
+    model = model_pair.ll_model
+    base_x = base_in[0]
+    with torch.no_grad():
+        base_ll_out = model_pair.ll_forward(base_x)
+        base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
+        B = base_x.shape[0]
+        for node in nodes:
+            v = values[node.name]
+            v = v.expand(B, *v.shape[1:]) if v.shape[0] != B else v  # a view: no per-batch copy
+            plan = RunPlan.with_splices([(node.name, node.index, v)], logits=model_pair.ll_logits_mode())
+            ll_out = model(base_x, plan=plan)
+            results[node] = results[node] + _ablation_score(model_pair, ll_out, base_ll_out, base_hl_out,
+                                                            hl_reduced, atol)
 
 
 def check_causal_effect_on_ablation(model_pair, dataset, batch_size: int = 256, node_type: str = "a",
@@ -230,15 +280,24 @@ def check_causal_effect_on_ablation(model_pair, dataset, batch_size: int = 256, 
     results = {n: 0 for n in nodes}
     loader = dataset.make_loader(batch_size=batch_size, num_workers=0)
     nb = 0
+    values = None
     for base_in in progress(loader, desc="ablation"):
         nb += 1
-        shapes = None
         if native:
-            with torch.no_grad():
-                shapes = model_pair.ll_model.run_capture(base_in[0], sorted({n.name for n in nodes}))
+            if values is None:  # [1, ...] ablation values, broadcast over every batch (shapes probed once)
+                names = sorted({n.name for n in nodes})
+                if use_mean_cache and all(nm in mean_cache for nm in names):
+                    values = {nm: mean_cache[nm] for nm in names}
+                else:
+                    with torch.no_grad():
+                        probe = model_pair.ll_model.run_capture(base_in[0][:1], names)
+                    values = {nm: (mean_cache[nm] if use_mean_cache else torch.zeros_like(probe[nm]))
+                              for nm in names}
+            ablate_nodes(model_pair, base_in, nodes, results, values)
+            continue
         for node in nodes:
             ablate_node(model_pair, base_in, node, results, hookers.get(node), verbose=verbose, mean_cache=mean_cache,
-                        use_mean_cache=use_mean_cache, shapes=shapes)
+                        use_mean_cache=use_mean_cache)
     return {n: float(v) / max(nb, 1) for n, v in results.items()}
 
 

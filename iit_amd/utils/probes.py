@@ -44,7 +44,8 @@ def construct_probe(high_level_node: HLNode, ll_nodes, dummy_cache, bias: bool =
 def construct_probes(model_pair, input_shape, bias: bool = False, input_dtype: Optional[torch.dtype] = None):
     dtype = input_dtype
     if dtype is None:
-        dtype = torch.long if getattr(model_pair.ll_model, "supports_run_plan", False) else torch.float32
+        # token models (hooked transformer / encoder) take ids; wrapped CNNs (also plan-capable) take images
+        dtype = torch.long if hasattr(model_pair.ll_model, "cfg") else torch.float32
     names = [n.name for v in model_pair.corr.values() for n in _nodes(v)]
     with torch.no_grad():
         dummy = capture_hooks(model_pair.ll_model, torch.zeros(input_shape, dtype=dtype, device=DEVICE), names)

@@ -4,7 +4,13 @@
   ``IITBehaviorModelPair`` (IIT + behaviour: 2 optimizer steps per batch), 15-token sentence pairs;
 * ``llama3-8b-causal``  -- 8-node arithmetic causal graph <-> Llama-3-8B (32L/4096d, 32 q / 8 kv heads, SwiGLU
   14336, RMSNorm, rotary, V=128256), ``CausalGraphModelPair`` (IIT + strict + behaviour: 3 optimizer steps),
-  6-token prompts.  fp32 master weights + Adam moments + gradients = 128 GB, bf16 compute.
+  6-token prompts (``--seq 512``: a 506-token filler context before the operands, so the captured source
+  activations -- ``attn.hook_z`` / ``mlp.hook_post`` over B x S tokens -- are GB-scale).  fp32 master weights + Adam
+  moments + gradients = 128 GB, bf16 compute;
+* ``pvr-resnet18``      -- MNIST-PVR pointer-value-retrieval HL <-> ResNet-18 (torchvision layout, fc 512->10),
+  ``IITBehaviorModelPair`` exactly as ``train.py`` (lr 1e-3, batch 256), 84 x 84 RGB 2 x 2 digit tiles, spatial
+  quadrant splice at ``mod.layer3.mod.1.mod.conv2.hook_point``; fp32 (the reference precision; MIOpen convolutions)
+  or ``--dtype bf16`` (channels-last bf16 autocast).
 
 Random-init weights of the named architectures, synthetic task data; same timing contract as ``bench.py``
 (W untimed warmup steps, then K steps bracketed by barrier + synchronize, max over ranks; one JSON line)."""
@@ -25,7 +31,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--family", required=True, choices=["mqnli-bert-base", "llama3-8b-causal", "llama-tiny-causal",
-                                                         "mqnli-bert-tiny"])
+                                                         "mqnli-bert-tiny", "pvr-resnet18"])
+    ap.add_argument("--seq", type=int, default=6, help="causal-graph prompt length (>= 6; Llama families)")
+    ap.add_argument("--zero", type=int, default=0, help="optimizer-state sharding (ZeRO-1) under data parallelism")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None, help="pairs per GPU per step")
@@ -53,6 +61,19 @@ def setup(args, dev):
                                                                   "clip_grad_norm": 1.0})
         model_name = f"{size} + MQNLI natural-logic HL (10 nodes)"
         seq = 15
+    elif args.family == "pvr-resnet18":
+        from iit_amd.model_pairs import IITBehaviorModelPair
+        from iit_amd.tasks.task_loader import get_alignment, get_dataset
+        n = 20000
+        tr_set, te_set = get_dataset("mnist_pvr", {"train_size": n, "test_size": 2048, "device": dev})
+        ll, hl, corr = get_alignment("mnist_pvr", {"input_shape": te_set.base_data.get_input_shape(), "device": dev})
+        args.batch = args.batch or 256
+        pair = IITBehaviorModelPair(hl, ll, corr, training_args={"batch_size": args.batch, "lr": 1e-3,
+                                                                  "lr_scheduler": None, "early_stop": False,
+                                                                  "zero": bool(args.zero)})
+        model_name = "resnet18 (fc 512->10) + MNIST-PVR HL, quadrant splice at layer3.1.conv2"
+        seq = 84
+        ds = tr_set.base_data
     else:
         from iit_amd.models.convert import llama_config_dict
         from iit_amd.models.transformer import HookedTransformer
@@ -60,18 +81,22 @@ def setup(args, dev):
         size = "llama-3-8b" if args.family == "llama3-8b-causal" else "llama-tiny"
         cfg = llama_config_dict(size, device=str(dev), dtype=torch.bfloat16)
         ll = HookedTransformer(cfg)
-        ds, hl, corr = make_causal_graph_task(ll, n_samples=10000, device=dev)
-        args.batch = args.batch or 64
+        ds, hl, corr = make_causal_graph_task(ll, n_samples=10000, device=dev, seq_len=args.seq)
+        args.batch = args.batch or (64 if args.seq <= 16 else max(1, 8192 // args.seq))
         pair = CausalGraphModelPair(hl, ll, corr, training_args={"batch_size": args.batch, "lr": 1e-5,
                                                                   "lr_scheduler": None, "early_stop": False,
                                                                   "strict_weight": 0.4, "clip_grad_norm": 1.0})
         model_name = f"{size} + 8-node arithmetic causal graph"
-        seq = 6
+        seq = args.seq
+        pair.training_args["zero"] = bool(args.zero)
     from iit_amd.parallel import dist as pdist
     pdist.broadcast_module(ll)
-    tr, te = train_test_split(ds, 0.1, 42)
-    train_set = IITDataset(tr, tr, seed=0, device=dev)
-    test_set = IITDataset(te, te, seed=0, device=dev)
+    if args.family == "pvr-resnet18":
+        train_set, test_set = tr_set, te_set
+    else:
+        tr, te = train_test_split(ds, 0.1, 42)
+        train_set = IITDataset(tr, tr, seed=0, device=dev)
+        test_set = IITDataset(te, te, seed=0, device=dev)
     opt = pair.make_optimizer(pair.training_args["lr"])
     pair.restrict_sparse_rows(train_set)
     loader = train_set.make_loader(args.batch, 0)
@@ -83,7 +108,7 @@ def setup(args, dev):
 
     step_fn = pair.run_train_step
     if args.graphs is None:
-        args.graphs = int(args.family.startswith("mqnli"))
+        args.graphs = int(args.family.startswith("mqnli") or args.family.startswith("pvr"))
     if args.graphs and dev.type == "cuda":
         from iit_amd.engine.graphs import GraphedTrainStep
         g = GraphedTrainStep(pair, opt, pair.loss_fn)

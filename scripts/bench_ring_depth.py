@@ -10,6 +10,32 @@ from iit_amd.ops import gemm_dispatch as gd  # noqa: E402
 from iit_amd.ops import hip_kernels as K  # noqa: E402
 
 T = 4096
+CASES_R3 = [  # round 3: two co-resident workgroups per CU (tiles 23-28) against the shipped choices
+    ("fwd QKV [4096][2304] bf16", T, 2304, 768, 2, K.EPI_BF16, [(5, 1, False), (23, 1, False), (25, 1, False),
+                                                                 (27, 1, False), (24, 1, False)]),
+    ("fwd W_in [4096][3072] gelu", T, 3072, 768, 2, K.EPI_GELU, [(5, 1, False), (23, 1, False), (25, 1, False),
+                                                                  (27, 1, False), (28, 1, False)]),
+    ("fwd W_O [4096][768] resid", T, 768, 768, 2, K.EPI_F32_RESID, [(9, 1, False), (24, 1, False), (29, 1, False),
+                                                                     (30, 1, False), (31, 1, False)]),
+    ("fwd W_out [4096][768] resid", T, 768, 3072, 2, K.EPI_F32_RESID, [(9, 1, False), (24, 1, False),
+                                                                        (29, 1, False), (30, 1, False), (31, 1, False)]),
+    ("dX W_in [4096][768] bf16", T, 768, 3072, 0, K.EPI_BF16, [(9, 1, False), (24, 1, False), (29, 1, False),
+                                                                (30, 1, False), (31, 1, False)]),
+    ("dX QKV [4096][768] bf16", T, 768, 2304, 0, K.EPI_BF16, [(9, 1, False), (24, 1, False), (29, 1, False),
+                                                               (30, 1, False), (31, 1, False)]),
+    ("dX W_O [4096][768] bf16", T, 768, 768, 0, K.EPI_BF16, [(9, 1, False), (24, 1, False), (29, 1, False),
+                                                              (30, 1, False), (31, 1, False)]),
+    ("dX W_out [4096][3072] dgelu", T, 3072, 768, 0, K.EPI_DGELU, [(5, 1, False), (23, 1, False), (25, 1, False),
+                                                                    (27, 1, False)]),
+    ("dW W_in [768][3072] store", 768, 3072, T, 3, K.EPI_F32_STORE,
+     [(11, 2, True), (10, 2, True), (26, 2, True), (23, 2, True), (25, 4, True), (26, 1, False), (24, 1, False)]),
+    ("dW W_out [3072][768] store", 3072, 768, T, 3, K.EPI_F32_STORE,
+     [(10, 2, True), (11, 2, True), (26, 2, True), (23, 2, True), (25, 4, True), (24, 1, False)]),
+    ("dW QKV [768][2304] store", 768, 2304, T, 3, K.EPI_F32_STORE, [(3, 1, False), (26, 2, True), (23, 2, True),
+                                                                     (24, 2, True), (25, 4, True)]),
+    ("dW W_O [768][768] store", 768, 768, T, 3, K.EPI_F32_STORE, [(3, 2, True), (8, 4, True), (26, 4, True),
+                                                                   (24, 4, True), (23, 4, True)]),
+]
 CASES = [  # name, M, N, K, mode, epi, [(tile, splits, reduce), ...]
     ("dW W_in [768][3072] store", 768, 3072, T, 3, K.EPI_F32_STORE, [(8, 1, False), (12, 1, False), (16, 1, False), (10, 2, True)]),
     ("dW W_O [768][768] store", 768, 768, T, 3, K.EPI_F32_STORE, [(3, 2, True), (14, 2, True), (17, 2, True), (3, 1, False),
@@ -24,7 +50,7 @@ CASES = [  # name, M, N, K, mode, epi, [(tile, splits, reduce), ...]
 
 def main():
     dev = "cuda"
-    for name, M, N, Kd, mode, epi, variants in CASES:
+    for name, M, N, Kd, mode, epi, variants in (CASES_R3 if os.environ.get("R3", "1") == "1" else CASES):
         torch.manual_seed(0)
         A = (torch.randn(Kd, M) if mode & 1 else torch.randn(M, Kd)).to(dev).bfloat16()
         B = (torch.randn(Kd, N) if mode & 2 else torch.randn(N, Kd)).to(dev).bfloat16() / 16
@@ -35,6 +61,8 @@ def main():
         R = torch.randn(M, N, device=dev) if epi == K.EPI_F32_RESID else None
         kw = dict(M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=N, mode=mode, epi=epi)
         ex = dict(resid=R, ldr=N) if R is not None else {}
+        if epi in (K.EPI_GELU, K.EPI_DGELU):  # pre-activation: written (GELU) or read (DGELU)
+            ex = dict(C2=torch.randn(M, N, device=dev).bfloat16(), ldc2=N)
         ref = None
         out = []
         for tile, sp, red in variants:

@@ -14,4 +14,4 @@ torch.cuda.synchronize()
 print("after steps inactive:", list(flat._inactive.keys()), "restrict_version", flat.restrict_version,
       "ok_version", getattr(opt, "_restrict_ok_version", None))
 tab, n = flat.span_table()
-print("spans", n, "active elems", int(tab[:, 1].sum()) * 4, "of", flat.numel)
+print("spans", n, "active elems", int(tab[:, 2].sum()) * 4, "of", flat.numel)

@@ -1,0 +1,108 @@
+"""In-context GEMM selection for the headline step (writes the shipped decision table).
+
+The dispatcher's autotuner times each candidate alone, back to back on L2-hot operands.  Inside the step a GEMM
+reads activations a previous kernel just wrote and weights that are not cache-resident, and the multi-workgroup-
+per-CU tiles (2-4 co-resident groups) that win in isolation lose there (round-3 profile: the 64 x 128 QKV tile 22.5 us
+alone, 29.8 us in the step).  This script measures every candidate where it runs: full training steps are issued
+eagerly behind a device sleep (the host enqueues the whole step, the GPU then runs it back to back exactly as a graph
+replay would), each GEMM bracketed by HIP events; candidates rotate over the rounds, and per problem the candidate with
+the lowest median in-context time is kept.  Output: the decision table (``--out``) and a per-problem report.
+
+    python scripts/tune_gemm_in_situ.py --out iit_amd/ops/tuned/gemm_decisions_gfx950.json
+"""
+import argparse
+import collections
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "gemm_decisions_in_situ.json"))
+    ap.add_argument("--report", default=os.path.join(ROOT, "gpurun_out", "gemm_in_situ_report.txt"))
+    ap.add_argument("--top", type=int, default=4, help="candidates per problem (by isolated time)")
+    ap.add_argument("--rounds", type=int, default=16)
+    ap.add_argument("--min-us", type=float, default=6.0, help="only problems whose best isolated time exceeds this")
+    a = ap.parse_args()
+
+    import bench
+    from iit_amd.ops import gemm_dispatch as gd
+
+    args = argparse.Namespace(gpus=1, steps=1, warmup=1, batch=256, model="gpt2-small", engine="native", dtype="bf16",
+                              graphs=0, profile_dir=None)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    pair, opt, loss_fn, it, step_fn, _, _ = bench.setup(args, dev)
+    # settle the isolated decisions of every phase kind (each HL node, each strict node, behaviour)
+    hl_nodes = list(pair.corr.keys())
+    ll_nodes = list(pair.nodes_not_in_circuit)
+    base, abl = next(it)
+    for i in range(max(len(hl_nodes), len(ll_nodes))):
+        pair.sample_hl_name = lambda i=i: hl_nodes[i % len(hl_nodes)]
+        pair.sample_ll_node = lambda i=i: ll_nodes[i % len(ll_nodes)]
+        pair.run_train_step(base, abl, loss_fn, opt)
+    torch.cuda.synchronize()
+    del pair.sample_hl_name, pair.sample_ll_node
+
+    cands = {}
+    for key, (choice, times) in gd.DECISIONS.items():
+        finite = {k: v for k, v in times.items() if v == v}
+        if len(finite) < 2 or min(finite.values()) < a.min_us:
+            continue
+        cands[key] = sorted(finite, key=finite.get)[:a.top]
+    print(f"{len(cands)} problems to tune in context", flush=True)
+
+    samples = collections.defaultdict(list)  # (key, cand) -> [us]
+    for r in range(a.rounds):
+        gd.FORCE.clear()
+        for key, cs in cands.items():
+            gd.FORCE[key] = cs[r % len(cs)]
+        gd.TIMING = []
+        base, abl = next(it)
+        torch.cuda.synchronize()
+        torch.cuda._sleep(int(1.5e9))  # ~0.6 s of GPU spin: the host enqueues the whole step meanwhile
+        pair.run_train_step(base, abl, loss_fn, opt)
+        torch.cuda.synchronize()
+        for key, name, s_ev, e_ev in gd.TIMING:
+            samples[(key, name)].append(s_ev.elapsed_time(e_ev) * 1e3)
+        gd.TIMING = None
+        print(f"round {r}: {sum(len(v) for v in samples.values())} samples", flush=True)
+    gd.FORCE.clear()
+
+    lines = []
+    table = {}
+    for key, cs in cands.items():
+        med = {}
+        for c in cs:
+            v = sorted(samples.get((key, c), []))
+            if v:
+                med[c] = v[len(v) // 2]
+        if not med:
+            continue
+        best = min(med, key=med.get)
+        iso = gd.DECISIONS[key][1]
+        gd.DECISIONS[key] = (best, iso)
+        lines.append(f"{key}: in-context " + "  ".join(f"{c} {med[c]:.1f}us(iso {iso[c]:.1f})" for c in med)
+                     + f"  -> {best}")
+    for key, (choice, _) in gd.DECISIONS.items():
+        table[repr(key)] = choice
+    arch = torch.cuda.get_device_properties(0).gcnArchName.split(":")[0]
+    with open(a.out, "w") as f:
+        json.dump({"arch": arch, "device": torch.cuda.get_device_name(0), "decisions": table,
+                   "method": "in-context (scripts/tune_gemm_in_situ.py)"}, f, indent=0, sort_keys=True)
+    with open(a.report, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    t0 = time.time()
+    main()
+    print(f"done in {time.time() - t0:.0f} s")

@@ -305,3 +305,89 @@ def test_reducer_defers_launches_for_multi_forward_losses():
     red.start()
     assert red.deferred  # zero grad-enabled forwards: unknown producer count, stay conservative
     red.remove()
+
+
+def _worker_zero(rank, world, port, out_dir, staged=False):
+    """Optimizer-state sharding (iit_amd/parallel/zero.py): reduce-scatter -> sharded clip + Adam -> all-gather."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from iit_amd.parallel import dist as pdist
+    from iit_amd.parallel.zero import ShardedFusedAdam
+    pdist.init_distributed("gloo")
+    torch.set_num_threads(2)
+    pair, train = _make(64)
+    pair.training_args.update(zero=True, fused_optimizer=True)
+    pdist.broadcast_module(pair.ll_model)
+    per_rank = 64 // world
+    if staged:
+        from iit_amd.engine.graphs import GraphedTrainStep
+        opt = pair.make_optimizer(1e-3)
+        step = GraphedTrainStep(pair, opt, pair.loss_fn, warmup=10 ** 9, enabled=True)
+        assert step.split and step.staged is not None
+        torch.manual_seed(5)
+        for i, (base, abl) in enumerate(train.make_loader(per_rank, 0)):
+            if i >= 3:
+                break
+            step(base, abl)
+    else:
+        opt = pair.make_optimizer(1e-3)
+        torch.manual_seed(5)
+        for i, (base, abl) in enumerate(train.make_loader(per_rank, 0)):
+            if i >= 3:
+                break
+            pair.run_train_step(base, abl, pair.loss_fn, opt)
+    assert isinstance(opt, ShardedFusedAdam) and pair._reducer.shard is opt
+    flat = opt.flat
+    assert opt.exp_avg.numel() <= flat.numel // world + 64 * len(opt.plan.buckets)  # moments are sharded
+    torch.save({n: p.detach().clone() for n, p in pair.ll_model.named_parameters()},
+               os.path.join(out_dir, f"zero{rank}.pt"))
+    pdist.destroy()
+
+
+def _worker_zero_staged(rank, world, port, out_dir):
+    _worker_zero(rank, world, port, out_dir, staged=True)
+
+
+@pytest.mark.parametrize("world,staged", [(2, False), (4, False), (2, True)])
+def test_zero1_sharded_optimizer_equals_single_process(tmp_path, world, staged):
+    """ZeRO-1 at world 2 and 4 (and under the staged DP schedule) reproduces the single-process run to fp32 tolerance
+    -- every rank ends with identical weights."""
+    pair, train = _make(64)
+    _train(pair, train, per_rank_batch=64, steps=3)
+    ref = {n: p.detach().clone() for n, p in pair.ll_model.named_parameters()}
+    mp.spawn(_worker_zero_staged if staged else _worker_zero, args=(world, _free_port(), str(tmp_path)),
+             nprocs=world, join=True)
+    got = [torch.load(tmp_path / f"zero{i}.pt", weights_only=True) for i in range(world)]
+    for n, p in ref.items():
+        for i in range(world):
+            assert torch.equal(got[i][n], got[0][n]), (i, n)
+            assert torch.allclose(got[i][n], p, atol=3e-5, rtol=2e-4), (i, n, float((got[i][n] - p).abs().max()))
+
+
+def _worker_metrics(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from iit_amd.core.metric import MetricStore, MetricStoreCollection, MetricType, PerTokenMetricStore
+    from iit_amd.model_pairs.base_model_pair import BaseModelPair
+    from iit_amd.parallel import dist as pdist
+    pdist.init_distributed("gloo")
+    mc = MetricStoreCollection([MetricStore("val/IIA", MetricType.ACCURACY), MetricStore("val/loss", MetricType.LOSS),
+                                PerTokenMetricStore("val/per_token_accuracy")])
+    # unequal batch counts per rank: rank 0 three batches, rank 1 one
+    vals = [(1.0, 2.0), (1.0, 4.0), (0.0, 6.0)] if rank == 0 else [(0.0, 10.0)]
+    for a, l in vals:
+        mc.update({"val/IIA": a, "val/loss": l, "val/per_token_accuracy": torch.tensor([a, 1.0 - a]).numpy()})
+    BaseModelPair._reduce_metrics(mc)
+    torch.save({m.get_name(): torch.as_tensor(m.get_value()) for m in mc.metrics}, os.path.join(out_dir, f"m{rank}.pt"))
+    pdist.destroy()
+
+
+def test_metric_reduction_weights_by_batch_counts(tmp_path):
+    """epoch metrics are all-reduced as sums and counts, so ranks with unequal numbers of
+    batches give the single-process mean (4 batches in all), not a mean of per-rank means."""
+    mp.spawn(_worker_metrics, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        m = torch.load(tmp_path / f"m{r}.pt", weights_only=True)
+        assert float(m["val/IIA"]) == pytest.approx(50.0)  # (1 + 1 + 0 + 0) / 4 x 100
+        assert float(m["val/loss"]) == pytest.approx(5.5)  # (2 + 4 + 6 + 10) / 4
+        assert torch.allclose(m["val/per_token_accuracy"].double(), torch.tensor([0.5, 0.5], dtype=torch.float64))

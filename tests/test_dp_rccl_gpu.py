@@ -17,7 +17,7 @@ def _free_port():
     return port
 
 
-def _train(steps=4):
+def _train(steps=4, zero=False):
     from iit_amd.data.iit_dataset import IITDataset
     from iit_amd.engine.graphs import GraphedTrainStep
     from iit_amd.model_pairs import IOI_ModelPair
@@ -32,7 +32,8 @@ def _train(steps=4):
     ds, hl = make_ioi_dataset_and_hl(512, ll, device=dev)
     train = IITDataset(ds, ds, seed=0, device=dev)
     pair = IOI_ModelPair(hl, ll, make_ioi_corr(6), training_args={"batch_size": 64, "lr": 1e-3,
-                                                                   "lr_scheduler": None, "strict_weight": 0.4})
+                                                                   "lr_scheduler": None, "strict_weight": 0.4,
+                                                                   "zero": zero})
     opt = pair.make_optimizer(1e-3)
     step = GraphedTrainStep(pair, opt, pair.loss_fn)
     it = iter(train.make_loader(64, 0, shuffle=False))
@@ -45,16 +46,23 @@ def _train(steps=4):
     return ll, losses, step, pair
 
 
-def test_one_rank_rccl_dp_schedule_matches_single_gpu(monkeypatch):
+@pytest.mark.parametrize("zero", [False, True])
+def test_one_rank_rccl_dp_schedule_matches_single_gpu(monkeypatch, zero):
+    """``zero``: optimizer-state sharding (iit_amd/parallel/zero.py) -- per-stage RCCL reduce-scatter into the shard,
+    sharded sumsq + 4-byte norm all-reduce, sharded fused Adam, RCCL all-gather + mirror refresh."""
     import torch.distributed as dist
     ref_model, ref_losses, ref_step, _ = _train()
     assert ref_step.staged is None
     monkeypatch.setenv("IIT_DP_FORCE_REDUCER", "1")
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
     try:
-        dp_model, dp_losses, dp_step, pair = _train()
+        dp_model, dp_losses, dp_step, pair = _train(zero=zero)
         assert pair._reducer is not None and pair._reducer.enabled
         assert dp_step.staged is not None and dp_step.replays > 0
+        if zero:
+            from iit_amd.parallel.zero import ShardedFusedAdam
+            assert isinstance(pair.optimizer if hasattr(pair, "optimizer") else dp_step.optimizer, ShardedFusedAdam)
+            assert pair._reducer.shard is not None
     finally:
         dist.destroy_process_group()
     for a, b in zip(ref_losses, dp_losses):

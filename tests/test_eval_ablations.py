@@ -81,3 +81,32 @@ def test_mean_and_zero_ablation_native_equals_reference(tmp_path):
     ea.save_result(df, str(tmp_path / "results"), pair)
     assert (tmp_path / "results" / "results.csv").exists()
     assert (tmp_path / "results" / "meta.log").read_text().startswith("{")
+
+
+def test_batched_sweeps_equal_the_per_node_path():
+    """the native sweeps share one source capture / HL output / base forward per batch across
+    all nodes; the scores equal the per-node native path (``resample_ablate_node`` / ``ablate_node``) exactly."""
+    pair, ds = _pair()
+    pair.training_args["engine"] = "native"
+    iit_set = IITDataset(ds, ds, seed=0, device="cpu")
+    nodes = list(ea._nodes(pair, "n")) + list(ea._nodes(pair, "c"))
+    torch.manual_seed(0)
+    base_in, abl_in = next(iter(iit_set.make_loader(32, 0)))
+    per_node = {n: 0 for n in nodes}
+    for n in nodes:
+        ea.resample_ablate_node(pair, base_in, abl_in, n, per_node)
+    batched = {n: 0 for n in nodes}
+    ea.resample_ablate_nodes(pair, base_in, abl_in, nodes, batched)
+    for n in nodes:
+        assert torch.equal(torch.as_tensor(per_node[n]), torch.as_tensor(batched[n])), n
+    uni = IITUniqueDataset(ds, ds, seed=0, device="cpu")
+    mean_cache = ea.get_mean_cache(pair, uni, batch_size=32)
+    (b,) = [next(iter(uni.make_loader(32, 0)))]
+    nodes = ea._nodes(pair, "a", with_suffixes=True)
+    per_node = {n: 0 for n in nodes}
+    for n in nodes:
+        ea.ablate_node(pair, b, n, per_node, mean_cache=mean_cache, use_mean_cache=True)
+    batched = {n: 0 for n in nodes}
+    ea.ablate_nodes(pair, b, nodes, batched, {nm: mean_cache[nm] for nm in {n.name for n in nodes}})
+    for n in nodes:
+        assert torch.equal(torch.as_tensor(per_node[n]), torch.as_tensor(batched[n])), n

@@ -116,11 +116,12 @@ def test_row_restriction_span_table():
     m = torch.nn.ModuleDict({"emb": torch.nn.Embedding(100, 8), "lin": torch.nn.Linear(8, 3)})
     flat = FlatParams(m)
     full, nfull = flat.span_table(max_len4=16, restricted=False)
-    assert int(full[:, 1].sum()) * 4 == flat.numel and nfull == full.shape[0]
+    assert int(full[:, 2].sum()) * 4 == flat.numel and nfull == full.shape[0]
+    assert torch.equal(full[:, 0], full[:, 1])  # replicated optimizer: gradient / moments at the arena offset
     assert flat.restrict_rows(m["emb"].weight, torch.tensor([0, 1, 2, 50, 99, 99]))
     tab, n = flat.span_table(max_len4=16)
     covered = torch.zeros(flat.numel, dtype=torch.bool)
-    for st, ln in tab.tolist():
+    for st, _loc, ln in tab.tolist():
         assert 0 < ln <= 16
         covered[st * 4:(st + ln) * 4] = True
     off = flat.offset_of(m["emb"].weight)

@@ -114,3 +114,37 @@ def test_split_graphs_for_data_parallel_match_eager(staged):
         assert all(len(ent[0][1]) == 2 for ent in g.graphs.values())  # two lower-stage graphs per phase
     assert torch.allclose(le1[:_TIGHT], ls[:_TIGHT], rtol=2e-3, atol=2e-3), (le1[:_TIGHT] - ls[:_TIGHT]).abs().max()
 
+
+
+def _run_lr_change(mode, change_at=9, n_batches=6, reps=3):
+    """fp32 torch-op backend (bit-exact graphs), the learning rate lowered 10x mid-run as ReduceLROnPlateau would."""
+    from iit_amd.engine.graphs import GraphedTrainStep
+    pair, opt, train = _setup(dtype=torch.float32)
+    torch.manual_seed(1)
+    batches = [b for _, b in zip(range(n_batches), train.make_loader(64, 0))]
+    step, g = pair.run_train_step, None
+    import contextlib
+    ctx = contextlib.nullcontext()
+    if mode == "graphs":
+        g = step = GraphedTrainStep(pair, opt, pair.loss_fn)
+        ctx = g.stream_context()
+    losses = []
+    with ctx:
+        for i, (base, abl) in enumerate(batches * reps):
+            if i == change_at:
+                for grp in opt.param_groups:
+                    grp["lr"] *= 0.1
+            out = step(base, abl, pair.loss_fn, opt)
+            losses.append(torch.stack([out[k] for k in sorted(out)]))
+    torch.cuda.synchronize()
+    return torch.stack(losses).cpu(), g
+
+
+def test_graphed_steps_follow_lr_changes():
+    """a captured Adam step must not keep the learning rate it saw at capture.  The fused kernel
+    reads lr from a device scalar the runner refreshes before each replay, so a mid-run lr change (an LR scheduler
+    between epochs) gives the eager trajectory bit for bit."""
+    le, _ = _run_lr_change("eager")
+    lg, g = _run_lr_change("graphs")
+    assert g.captures > 0 and g.replays > 0 and not g.failed, g.failed
+    assert torch.equal(le, lg), (le - lg).abs().max(dim=1).values

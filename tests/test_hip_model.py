@@ -242,3 +242,34 @@ def test_torch_backend_reads_arena_mirror_and_accumulates_in_place():
     finally:
         torch_ops._MirrorMat.apply = orig
     assert calls  # packed QKV / 2-D W_O projections ran
+
+
+def test_bias_sums_survive_a_failed_backward():
+    """the batched bias column sums are flushed by the backward pass's final callback.  A
+    backward that raises after queueing a bias (an aborted graph capture) never runs it; the next backward must
+    still produce complete bias gradients (stale items of the failed pass are dropped, not summed)."""
+    ref, fast = make_models()
+    tok = torch.randint(0, 1000, (8, 16), device=dev)
+
+    def grads(model, fail):
+        model.zero_grad(set_to_none=True)
+        if fail:
+            # block 0's input gradient arrives last: by then every block has queued its bias sums
+            def boom(g, hook):
+                raise RuntimeError("injected backward failure")
+            model.add_hook(model.blocks[0].hook_resid_pre.name, boom, dir="bwd")
+        out = model(tok)
+        try:
+            out.float().pow(2).mean().backward()
+        finally:
+            model.reset_hooks()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().clone() for n, p in model.named_parameters() if n.endswith(("b_in", "b_out", "b_O"))}
+
+    with pytest.raises(RuntimeError, match="injected"):
+        grads(fast, fail=True)
+    gf = grads(fast, fail=False)
+    gr = grads(ref, fail=False)
+    for n in gr:
+        assert gf[n].abs().sum() > 0, n
+        assert rel(gf[n], gr[n]) < 3e-2, (n, rel(gf[n], gr[n]))
