@@ -55,6 +55,9 @@ struct G2Args {
   // in split order (deterministic) and runs the normal epilogue, then resets the ticket for the next launch
   float* ws;
   int* counters;
+  // epilogue store flavour of the output tiles: 0 plain, 1 non-temporal (streamed past the caches), 2 write-through
+  // (sc1: written to memory and dropped from the XCD's L2, so the kernel boundary has no dirty lines to write back)
+  int store_mode;
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -248,16 +251,26 @@ __device__ __forceinline__ void add8(float* v, const float* b) {
   v[4] += y.x; v[5] += y.y; v[6] += y.z; v[7] += y.w;
 }
 
-__device__ __forceinline__ void store8_bf16(void* dst, const float* v) {
+__device__ __forceinline__ void store16(void* dst, const f32x4 x, int mode) {
+  if (mode == 1) {
+    __builtin_nontemporal_store(x, (f32x4*)dst);
+  } else if (mode == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(x) : "memory");
+  } else {
+    *(f32x4*)dst = x;
+  }
+}
+
+__device__ __forceinline__ void store8_bf16(void* dst, const float* v, int mode = 0) {
   bf16x8 o;
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
-  *(bf16x8*)dst = o;
+  store16(dst, __builtin_bit_cast(f32x4, o), mode);
 }
 
-__device__ __forceinline__ void store8_f32(void* dst, const float* v) {
-  *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
-  *((float4*)dst + 1) = make_float4(v[4], v[5], v[6], v[7]);
+__device__ __forceinline__ void store8_f32(void* dst, const float* v, int mode = 0) {
+  store16(dst, f32x4{v[0], v[1], v[2], v[3]}, mode);
+  store16((float*)dst + 4, f32x4{v[4], v[5], v[6], v[7]}, mode);
 }
 
 // s_waitcnt vmcnt(N) with N chosen at run time from {0, L, ..., 7L} (an immediate is required; deep rings keep up
@@ -533,26 +546,26 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_glds_kernel(G2Args p) {
     }
     if constexpr (EPI == E_BF16) {
       if (p.bias0) add8(v, p.bias0 + col);
-      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v);
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v, p.store_mode);
     } else if constexpr (EPI == E_BF16_BIAS3) {
       const int w = col / p.bias_cols, o = col - w * p.bias_cols;
       const float* bb = w == 0 ? p.bias0 : (w == 1 ? p.bias1 : p.bias2);
       if (bb) add8(v, bb + o);
-      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v);
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v, p.store_mode);
     } else if constexpr (EPI == E_F32_RESID) {
       if (p.bias0) add8(v, p.bias0 + col);
       add8v(v, pf[2 * k], pf[2 * k + 1]);
-      store8_f32((float*)p.C + (long)row * p.ldc + col, v);
+      store8_f32((float*)p.C + (long)row * p.ldc + col, v, p.store_mode);
     } else if constexpr (EPI == E_GELU || EPI == E_GELU_ERF) {
       if (p.bias0) add8(v, p.bias0 + col);
-      store8_bf16((__bf16*)p.C2 + (long)row * p.ldc2 + col, v);
+      store8_bf16((__bf16*)p.C2 + (long)row * p.ldc2 + col, v, p.store_mode);
       float g[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {  // gelu of the stored (bf16) pre, which the backward reads
         const float x = bf2f(f2bf(v[e]));
         g[e] = EPI == E_GELU ? gelu_new_dev(x) : gelu_erf_f(x);
       }
-      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, g);
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, g, p.store_mode);
     } else if constexpr (EPI == E_DGELU || EPI == E_DGELU_ERF) {
       const bf16x8 pr = pb[k];
 #pragma unroll
@@ -560,7 +573,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_glds_kernel(G2Args p) {
         const float x = bf2f(pr[e]);
         v[e] = bf2f(f2bf(v[e] * (EPI == E_DGELU ? gelu_new_grad_f(x) : gelu_erf_grad_f(x))));
       }
-      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v);
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v, p.store_mode);
       if (p.csum) {  // this thread's own chunk of E: no other thread touches it before the barrier below
         *(float4*)(E + lr * EPS + lc) = make_float4(v[0], v[1], v[2], v[3]);
         *(float4*)(E + lr * EPS + lc + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -568,10 +581,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_glds_kernel(G2Args p) {
     } else if constexpr (EPI == E_F32_ACC) {
       float* dst = (float*)p.C + (long)row * p.ldc + col;
       add8v(v, pf[2 * k], pf[2 * k + 1]);
-      store8_f32(dst, v);
+      store8_f32(dst, v, p.store_mode);
     } else {  // E_F32_STORE
       if (p.bias0) add8(v, p.bias0 + col);
-      store8_f32((float*)p.C + (long)row * p.ldc + col, v);
+      store8_f32((float*)p.C + (long)row * p.ldc + col, v, p.store_mode);
     }
   }
   if constexpr (EPI == E_DGELU || EPI == E_DGELU_ERF) {
@@ -695,10 +708,24 @@ IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, con
   return 1;
 }
 
+IIT_EXPORT int iit_gemm_glds_sm(const void* A, const void* B, void* C, void* C2, const float* bias0,
+                                const float* bias1, const float* bias2, const float* resid, long lda, long ldb, long ldc,
+                                long ldc2, long ldr, int M, int N, int K, int mode, int epi, int bias_cols, int tile,
+                                int splits, float* csum, float* ws, int* counters, int store_mode, void* stream);
+
 IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, const float* bias0, const float* bias1,
                              const float* bias2, const float* resid, long lda, long ldb, long ldc, long ldc2, long ldr,
                              int M, int N, int K, int mode, int epi, int bias_cols, int tile, int splits,
                              float* csum, float* ws, int* counters, void* stream) {
+  return iit_gemm_glds_sm(A, B, C, C2, bias0, bias1, bias2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi,
+                          bias_cols, tile, splits, csum, ws, counters, 0, stream);
+}
+
+// the same with the epilogue store flavour (G2Args::store_mode)
+IIT_EXPORT int iit_gemm_glds_sm(const void* A, const void* B, void* C, void* C2, const float* bias0,
+                                const float* bias1, const float* bias2, const float* resid, long lda, long ldb, long ldc,
+                                long ldc2, long ldr, int M, int N, int K, int mode, int epi, int bias_cols, int tile,
+                                int splits, float* csum, float* ws, int* counters, int store_mode, void* stream) {
   const int reduce = ws != nullptr;
   if (!iit_gemm_glds_ok(A, B, C, C2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits,
                         reduce))
@@ -712,6 +739,7 @@ IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, co
   a.csum = (epi == E_DGELU || epi == E_DGELU_ERF) ? csum : nullptr;
   a.ws = reduce ? ws : nullptr;  // workspace >= splits * M * N floats, counters >= tiles ints (zero when idle)
   a.counters = reduce ? counters : nullptr;
+  a.store_mode = store_mode;
   hipStream_t s = (hipStream_t)stream;
 #define G2(MODE, AK, BK_, EPI) \
   if (mode == (MODE) && epi == (EPI)) return (int)launch_tile<AK, BK_, EPI>(a, tile, s);

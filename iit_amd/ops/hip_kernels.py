@@ -30,6 +30,7 @@ _SIGS = {
     "iit_gemm": [c_void_p] * 10 + [c_long] * 5 + [c_int] * 12 + [c_void_p],
     "iit_gemm_glds": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p] * 4,
     "iit_gemm_glds_ok": [c_void_p] * 5 + [c_long] * 5 + [c_int] * 9,
+    "iit_gemm_glds_sm": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p] * 3 + [c_int, c_void_p],
     "iit_embed_pos_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_embed_pos_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_ln_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
@@ -226,8 +227,11 @@ def split_workspace(M: int, N: int, tile: int, splits: int, device) -> tuple:
     return ent[0], ent[1]
 
 
+GLDS_STORE_MODE = int(os.environ.get("IIT_GEMM_STORE", "0"))  # epilogue stores: 0 plain, 1 non-temporal, 2 write-through
+
+
 def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None, bias1=None, bias2=None, resid=None,
-              ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1, csum=None, reduce=False):
+              ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1, csum=None, reduce=False, store_mode=None):
     """C = A @ B (+ epilogue) on the LDS-DMA MFMA kernel; bf16 operands, M/N/K multiples of the tile.
     ``EPI_DGELU`` (mode 0): ``C2`` is the saved bf16 pre-activation (row stride ``ldc2``); ``csum`` (fp32 [N],
     optional) accumulates the column sums of the stored bf16 output.
@@ -240,9 +244,10 @@ def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None
     if CHECK_BOUNDS:
         _gemm_bounds("iit_gemm_glds", A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode)
         _bounds("iit_gemm_glds", ("csum", csum, 1, N, N))
-    _check(lib().iit_gemm_glds(_p(A), _p(B), _p(C), _p(C2), _p(bias0), _p(bias1), _p(bias2), _p(resid), lda, ldb,
-                               ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits, _p(csum), _p(ws), _p(cnt),
-                               _stream()),
+    sm = GLDS_STORE_MODE if store_mode is None else store_mode
+    _check(lib().iit_gemm_glds_sm(_p(A), _p(B), _p(C), _p(C2), _p(bias0), _p(bias1), _p(bias2), _p(resid), lda, ldb,
+                                  ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits, _p(csum), _p(ws),
+                                  _p(cnt), int(sm), _stream()),
            "iit_gemm_glds")
 
 

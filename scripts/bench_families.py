@@ -161,7 +161,8 @@ def main():
             "metric": f"IIT (base,source) intervened pairs/sec, {args.family}", "value": round(
                 args.batch * world * args.steps / dt, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "dtype": "bf16", "data": "synthetic task data, random-init weights",
+            "scaling": "weak", "dtype": "fp32" if args.family.startswith("pvr") else "bf16",
+            "data": "synthetic task data, random-init weights",
             "config": {"model": model_name, "params": n_params, "global_batch": args.batch * world, "seq_len": seq,
                        "parallelism": f"dp{world}", "graphs": bool(getattr(step_fn, "enabled", False))},
             "val_IIA": round(float(vals.get("val/IIA", float("nan"))), 3),

@@ -1,0 +1,152 @@
+"""Where the IOI val/IIA ceiling comes from.
+
+1. **Ties.**  For every held-out (base, source) pair and every HL node, the HL's intervened last-position logits
+   (``IOI_HL``, /root/reference/iit/tasks/ioi/ioi_hl.py:54-68) are checked for a tied maximum: with a tie the IIT
+   label is the first maximal vocabulary index (torch.argmax), a deterministic but token-order-dependent target.
+2. **Per-node IIA.**  The reference's eval epoch samples ONE HL node per batch from the pair's RNG
+   (/root/reference/iit/model_pairs/ioi_model_pair.py:71-92), so an epoch's val/IIA is a mix of ~10 node draws.  Every
+   ``--every`` epochs this script also evaluates every HL node on the whole validation split, and logs which nodes
+   the epoch's own eval drew, so an epoch-to-epoch swing can be attributed to the node mix (data / evaluation) or to
+   the model (optimizer).
+
+Training is ``train_ioi.py``'s configuration (BaseModelPair.train: 12k samples, 80/20, batch 256, Adam 1e-4,
+iit/behaviour/strict 1/1/0.4, clip 1.0) on the headline GPT-2-small model.  Prints one JSON line at the end.
+
+    python scripts/iia_ceiling.py --epochs 70 --every 5
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def tie_stats(pair, test_set, batch: int = 512):
+    """Fraction of held-out pairs whose intervened HL last-position max is tied, per HL node."""
+    hl = pair.hl_model
+    out = {}
+    for node in pair.corr.keys():
+        ties = total = 0
+        for base, abl in test_set.make_loader(batch, 0, shuffle=False):
+            with torch.no_grad():
+                _, pair.hl_cache = hl.run_with_cache(abl, **pair.hl_run_kwargs())
+                y = hl.run_with_hooks(base, fwd_hooks=[(node.name, pair.make_hl_ablation_hook(node))],
+                                      **pair.hl_run_kwargs())
+            y = y[:, -1] if y.dim() == 3 else y
+            top = y.max(dim=-1, keepdim=True).values
+            ties += int(((y == top).sum(dim=-1) > 1).sum())
+            total += y.shape[0]
+        out[node.name] = ties / max(total, 1)
+    return out
+
+
+def per_node_iia(pair, test_set, batch: int = 512):
+    """val/IIA of every HL node over the whole validation split (the pair's own eval draws one node per batch)."""
+    res = {}
+    pair._ll_module().eval()
+    for node in pair.corr.keys():
+        hits = n = 0
+        for base, abl in test_set.make_loader(batch, 0, shuffle=False):
+            with torch.no_grad():
+                hl_out, ll_out = pair.do_intervention(base, abl, node)
+            hl_last = hl_out[:, -1] if hl_out.dim() == 3 else hl_out
+            ll_last = ll_out[:, -1] if ll_out.dim() == 3 else ll_out
+            hits += int((ll_last.argmax(-1) == hl_last.argmax(-1)).sum())
+            n += hl_last.shape[0]
+        res[node.name] = 100.0 * hits / max(n, 1)
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="gpt2-small", choices=["gpt2-small", "ioi-6l"])
+    ap.add_argument("--epochs", type=int, default=70)
+    ap.add_argument("--every", type=int, default=5)
+    ap.add_argument("--num-samples", type=int, default=12000)
+    args = ap.parse_args()
+
+    from iit_amd.data.iit_dataset import IITDataset, train_test_split
+    from iit_amd.model_pairs import IOI_ModelPair
+    from iit_amd.models.config import gpt2_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.tasks.ioi import NAMES, ioi_cfg, make_ioi_corr, make_ioi_dataset_and_hl
+
+    dev = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+    torch.manual_seed(0)
+    np.random.seed(0)
+    cfg = gpt2_config_dict()
+    if args.model == "ioi-6l":
+        cfg.update(ioi_cfg)
+    cfg.update(init_weights=True, device=str(dev), dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32)
+    ll = HookedTransformer(cfg)
+    if dev.type != "cuda":
+        ll.set_op_backend("torch")
+    ds, hl = make_ioi_dataset_and_hl(args.num_samples, ll, NAMES, device=dev)
+    train_ds, test_ds = train_test_split(ds, test_size=0.2, random_state=42)
+    train_set = IITDataset(train_ds, train_ds, seed=0, device=dev)
+    test_set = IITDataset(test_ds, test_ds, seed=0, device=dev)
+    training_args = {"batch_size": 256, "lr": 1e-4, "iit_weight": 1.0, "behavior_weight": 1.0, "strict_weight": 0.4,
+                     "next_token": False, "lr_scheduler": None, "clip_grad_norm": 1.0, "early_stop": False,
+                     "use_single_loss": False}
+    pair = IOI_ModelPair(ll_model=ll, hl_model=hl, corr=make_ioi_corr(cfg["n_layers"]), training_args=training_args)
+
+    ties = tie_stats(pair, test_set)
+    print("tied HL maxima per node (fraction of held-out pairs):", json.dumps(ties), flush=True)
+
+    # record the HL node each eval batch draws (the reference's one-node-per-batch eval)
+    drawn = []
+    orig_eval = pair.run_eval_step
+
+    def eval_step(base, abl, loss_fn):
+        orig_sample = pair.sample_hl_name
+
+        def sample():
+            n = orig_sample()
+            drawn.append(n.name)
+            return n
+        pair.sample_hl_name = sample
+        try:
+            return orig_eval(base, abl, loss_fn)
+        finally:
+            del pair.sample_hl_name
+    pair.run_eval_step = eval_step
+    pair.training_args["eval_graphs"] = False  # the draws must go through the recording sampler
+
+    rows = []
+    orig_log = pair._print_and_log_metrics
+    t0 = time.perf_counter()
+
+    def log(epoch, metrics, sink=None):
+        vals = {m.get_name(): m.get_value() for m in metrics if m.get_name() != "val/per_token_accuracy"}
+        mix = collections.Counter(drawn)
+        drawn.clear()
+        row = {"epoch": epoch, "val/IIA": round(float(vals["val/IIA"]), 2), "eval_node_draws": dict(mix)}
+        if epoch % args.every == 0 or epoch == args.epochs - 1:
+            rng_state = pair.rng.bit_generator.state
+            row["per_node_IIA"] = {k: round(v, 2) for k, v in per_node_iia(pair, test_set).items()}
+            pair.rng.bit_generator.state = rng_state  # per-node evaluation draws nothing; keep the RNG anyway
+            pair._ll_module().train()
+            orig_log(epoch, metrics, sink)
+            print(json.dumps(row), flush=True)
+        rows.append(row)
+    pair._print_and_log_metrics = log
+    pair.train(train_set, test_set, epochs=args.epochs)
+    wall = time.perf_counter() - t0
+    best = max(rows, key=lambda r: r["val/IIA"])
+    print(json.dumps({"metric": "IOI val/IIA ceiling analysis", "model": args.model, "epochs": args.epochs,
+                      "wall_s": round(wall, 1), "tie_fraction_per_node": ties,
+                      "best_epoch_val_IIA": best["val/IIA"], "best_epoch": best["epoch"],
+                      "final_per_node_IIA": rows[-1].get("per_node_IIA")}))
+
+
+if __name__ == "__main__":
+    main()

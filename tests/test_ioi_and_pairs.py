@@ -177,3 +177,30 @@ def test_ioi_pair_trains_and_checkpoints(tmp_path):
     names = [m.get_name() for m in pair.test_metrics.metrics]
     assert names == ["val/iit_loss", "val/IIA", "val/accuracy", "val/per_token_accuracy"]
     assert pair.test_metrics.metrics[3].get_value().shape == (16,)
+
+
+def test_oracle_train_step_under_detect_anomaly():
+    """the fp32 oracle's full Strict-IIT step (5 forwards, 3 backwards incl. in-place splices, the
+    fused-optimizer fallback) runs clean under ``torch.autograd.detect_anomaly`` (NaN / in-place-modification checks
+    on every backward node)."""
+    import torch
+
+    from iit_amd.data.iit_dataset import IITDataset
+    from iit_amd.model_pairs import IOI_ModelPair
+    from iit_amd.models.config import gpt2_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.tasks.ioi import make_ioi_corr, make_ioi_dataset_and_hl
+    cfg = gpt2_config_dict()
+    cfg.update(n_layers=6, d_model=32, n_heads=4, d_head=8, d_mlp=64, device="cpu")
+    torch.manual_seed(0)
+    ll = HookedTransformer(cfg)
+    ds, hl = make_ioi_dataset_and_hl(128, ll, device="cpu")
+    train = IITDataset(ds, ds, seed=0, device="cpu")
+    pair = IOI_ModelPair(hl, ll, make_ioi_corr(6), training_args={"batch_size": 32, "lr": 1e-3, "lr_scheduler": None,
+                                                                   "fused_optimizer": True})
+    opt = pair.make_optimizer(1e-3)
+    base, abl = next(iter(train.make_loader(32, 0)))
+    with torch.autograd.detect_anomaly():
+        for _ in range(2):
+            out = pair.run_train_step(base, abl, pair.loss_fn, opt)
+    assert all(torch.isfinite(torch.as_tensor(v)).all() for v in out.values())
