@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--epochs", type=int, default=70)
     ap.add_argument("--every", type=int, default=5)
     ap.add_argument("--num-samples", type=int, default=12000)
+    ap.add_argument("--train-nodes", default="",
+                    help="comma list of HL node names the TRAINING steps sample from (default: all, as the reference)")
     args = ap.parse_args()
 
     from iit_amd.data.iit_dataset import IITDataset, train_test_split
@@ -99,6 +101,11 @@ def main():
                      "use_single_loss": False}
     pair = IOI_ModelPair(ll_model=ll, hl_model=hl, corr=make_ioi_corr(cfg["n_layers"]), training_args=training_args)
 
+    if args.train_nodes:  # learnability probe: train on a subset of nodes, still evaluate every node
+        keep = [n for n in pair.corr.keys() if n.name in args.train_nodes.split(",")]
+        assert keep, args.train_nodes
+        pair.sample_hl_name = lambda: keep[int(pair.rng.integers(len(keep)))]
+
     ties = tie_stats(pair, test_set)
     print("tied HL maxima per node (fraction of held-out pairs):", json.dumps(ties), flush=True)
 
@@ -107,7 +114,8 @@ def main():
     orig_eval = pair.run_eval_step
 
     def eval_step(base, abl, loss_fn):
-        orig_sample = pair.sample_hl_name
+        train_sampler = pair.__dict__.get("sample_hl_name")
+        orig_sample = type(pair).sample_hl_name.__get__(pair)
 
         def sample():
             n = orig_sample()
@@ -117,7 +125,10 @@ def main():
         try:
             return orig_eval(base, abl, loss_fn)
         finally:
-            del pair.sample_hl_name
+            if train_sampler is None:
+                del pair.sample_hl_name
+            else:
+                pair.sample_hl_name = train_sampler
     pair.run_eval_step = eval_step
     pair.training_args["eval_graphs"] = False  # the draws must go through the recording sampler
 
@@ -143,6 +154,7 @@ def main():
     wall = time.perf_counter() - t0
     best = max(rows, key=lambda r: r["val/IIA"])
     print(json.dumps({"metric": "IOI val/IIA ceiling analysis", "model": args.model, "epochs": args.epochs,
+                      "train_nodes": args.train_nodes or "all",
                       "wall_s": round(wall, 1), "tie_fraction_per_node": ties,
                       "best_epoch_val_IIA": best["val/IIA"], "best_epoch": best["epoch"],
                       "final_per_node_IIA": rows[-1].get("per_node_IIA")}))
