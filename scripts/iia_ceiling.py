@@ -72,6 +72,9 @@ def main():
     ap.add_argument("--epochs", type=int, default=70)
     ap.add_argument("--every", type=int, default=5)
     ap.add_argument("--num-samples", type=int, default=12000)
+    ap.add_argument("--graphs", type=int, default=1, help="0: eager phases (no HIP graphs)")
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch"],
+                    help="torch: the fp32 torch-op oracle backend on the same device")
     ap.add_argument("--train-nodes", default="",
                     help="comma list of HL node names the TRAINING steps sample from (default: all, as the reference)")
     args = ap.parse_args()
@@ -88,9 +91,10 @@ def main():
     cfg = gpt2_config_dict()
     if args.model == "ioi-6l":
         cfg.update(ioi_cfg)
-    cfg.update(init_weights=True, device=str(dev), dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32)
+    fast = dev.type == "cuda" and args.backend == "hip"
+    cfg.update(init_weights=True, device=str(dev), dtype=torch.bfloat16 if fast else torch.float32)
     ll = HookedTransformer(cfg)
-    if dev.type != "cuda":
+    if not fast:
         ll.set_op_backend("torch")
     ds, hl = make_ioi_dataset_and_hl(args.num_samples, ll, NAMES, device=dev)
     train_ds, test_ds = train_test_split(ds, test_size=0.2, random_state=42)
@@ -98,7 +102,7 @@ def main():
     test_set = IITDataset(test_ds, test_ds, seed=0, device=dev)
     training_args = {"batch_size": 256, "lr": 1e-4, "iit_weight": 1.0, "behavior_weight": 1.0, "strict_weight": 0.4,
                      "next_token": False, "lr_scheduler": None, "clip_grad_norm": 1.0, "early_stop": False,
-                     "use_single_loss": False}
+                     "use_single_loss": False, "graphs": bool(args.graphs)}
     pair = IOI_ModelPair(ll_model=ll, hl_model=hl, corr=make_ioi_corr(cfg["n_layers"]), training_args=training_args)
 
     if args.train_nodes:  # learnability probe: train on a subset of nodes, still evaluate every node
@@ -154,7 +158,7 @@ def main():
     wall = time.perf_counter() - t0
     best = max(rows, key=lambda r: r["val/IIA"])
     print(json.dumps({"metric": "IOI val/IIA ceiling analysis", "model": args.model, "epochs": args.epochs,
-                      "train_nodes": args.train_nodes or "all",
+                      "train_nodes": args.train_nodes or "all", "graphs": args.graphs, "backend": args.backend,
                       "wall_s": round(wall, 1), "tie_fraction_per_node": ties,
                       "best_epoch_val_IIA": best["val/IIA"], "best_epoch": best["epoch"],
                       "final_per_node_IIA": rows[-1].get("per_node_IIA")}))

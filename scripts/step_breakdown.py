@@ -8,6 +8,23 @@ import collections
 import csv
 
 
+def group_of(k: str) -> str:
+    """Kernel family of a lower-cased kernel name."""
+    if "conv" in k or k.startswith("igemm_") or "im2d2col" in k or "col2im" in k:
+        return "conv"
+    if "gemm" in k or "cijk" in k:
+        return "gemm"
+    if "attn" in k or "flash" in k or "fa_" in k:
+        return "attention"
+    if "ln_" in k or "rms_" in k or "batchnorm" in k:
+        return "norm"
+    if "adam" in k or "sumsq" in k:
+        return "optimizer"
+    if "nccl" in k or "rccl" in k:
+        return "collective"
+    return "elementwise"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
@@ -53,9 +70,7 @@ def main():
     groups = collections.Counter()
     for name, t in per.items():
         k = name.lower()
-        g = ("gemm" if ("gemm" in k or k.startswith("cijk")) else "attention" if "attn" in k or "flash" in k or "fa_" in k
-             else "norm" if "ln_" in k else "optimizer" if ("adam" in k or "sumsq" in k) else "collective"
-             if "nccl" in k or "rccl" in k else "elementwise")
+        g = group_of(k)
         groups[g] += t
     print("groups (ms/step): " + ", ".join(f"{g} {t / n / 1e6:.2f}" for g, t in groups.most_common()))
     if a.gaps:
