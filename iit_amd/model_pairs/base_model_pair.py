@@ -158,6 +158,35 @@ class BaseModelPair(ABC):
         out = model.run_with_hooks(x, fwd_hooks=[(n.name, self.make_ll_ablation_hook(n)) for n in ll_nodes])
         return out[:, -1] if logits == "last" and out.dim() == 3 else out
 
+    def ll_paired_intervention(self, base_x: Tensor, ablation_x: Tensor, ll_nodes: Iterable[LLNode],
+                               logits: Optional[str] = None):
+        """``ll_source_cache`` + ``ll_intervened_forward`` as ONE paired forward of source and base rows
+        (``HookedTransformer.run_paired``; SURVEY.md §7.5 (2a)) when the native engine covers the configuration;
+        sets ``self.ll_cache`` to the source activations at the splice sites.  None = not covered (two forwards).
+        ``training_args["paired"] = False`` turns it off; pairs that customise the two runs (StopGrad) keep them."""
+        if not self.native() or self.training_args.get("paired", True) is False:
+            return None
+        if getattr(self, "_source_prefetch", None) is not None:
+            return None
+        cls = type(self)
+        if (cls.ll_intervened_forward is not BaseModelPair.ll_intervened_forward
+                or cls.ll_source_cache is not BaseModelPair.ll_source_cache):
+            return None
+        fn = getattr(self.ll_model, "run_paired", None)
+        if fn is None:
+            return None
+        sites = {}
+        for n in ll_nodes:
+            if n.subspace is not None:
+                return None
+            sites.setdefault(n.name, []).append(n.index)
+        res = fn(base_x, ablation_x, sites, logits=logits or self.ll_logits_mode())
+        if res is None:
+            return None
+        out, caps = res
+        self.ll_cache = ActivationCache(caps, self.ll_model)
+        return out
+
     def ll_forward(self, x: Tensor, logits: Optional[str] = None):
         logits = logits or self.ll_logits_mode()
         model = self.ll_model
@@ -176,14 +205,18 @@ class BaseModelPair(ABC):
         with trace_range("hl_source_cache"):
             hl_ablation_output, self.hl_cache = self.hl_model.run_with_cache(ablation_input, **hl_kw)
         ll_nodes = _ll_nodes_of(self.corr, hl_node)
-        with trace_range("ll_source_cache"):
-            self.ll_cache = self.ll_source_cache(ablation_x, ll_nodes)
+        with trace_range("ll_paired_fwd"):
+            ll_output = self.ll_paired_intervention(base_x, ablation_x, ll_nodes)
+        if ll_output is None:
+            with trace_range("ll_source_cache"):
+                self.ll_cache = self.ll_source_cache(ablation_x, ll_nodes)
         sync_point()
         with trace_range("hl_intervened_fwd"):
             hl_output = self.hl_model.run_with_hooks(
                 base_input, fwd_hooks=[(hl_node.name, self.make_hl_ablation_hook(hl_node))], **hl_kw)
-        with trace_range("ll_spliced_fwd"):
-            ll_output = self.ll_intervened_forward(base_x, ll_nodes)
+        if ll_output is None:
+            with trace_range("ll_spliced_fwd"):
+                ll_output = self.ll_intervened_forward(base_x, ll_nodes)
         sync_point()
         if verbose:
             print(f"{hl_node=}, {ll_nodes=}\n{hl_output=}")

@@ -42,8 +42,10 @@ class StrictIITModelPair(IITBehaviorModelPair):
 
     def get_strict_loss_over_batch(self, base_input, ablation_input, ll_node: LLNode, loss_fn):
         base_x, base_y = base_input[0], base_input[1]
-        self.ll_cache = self.ll_source_cache(ablation_input[0], [ll_node])
-        out = self.ll_intervened_forward(base_x, [ll_node])
+        out = self.ll_paired_intervention(base_x, ablation_input[0], [ll_node])
+        if out is None:
+            self.ll_cache = self.ll_source_cache(ablation_input[0], [ll_node])
+            out = self.ll_intervened_forward(base_x, [ll_node])
         if out.dim() > 1 and out.shape[0] == 1:
             return loss_fn(out, base_y)
         return loss_fn(out.squeeze(), base_y)

@@ -417,6 +417,90 @@ class TransformerBlock(nn.Module):
         return run.site(self.hook_resid_post, resid_post)
 
 
+    # ------------------------------------------------------------------ paired source + base rows
+    def paired_ok(self, run: _Run) -> bool:
+        """Whether this block can run as part of a paired forward (the fused HIP path, no live hook inside)."""
+        cfg = self.cfg
+        if cfg.use_attn_result or self.attn.rotary or self.attn.gqa:
+            return False
+        if self.ln1 is None or self.ln1.rms or (not cfg.attn_only and (self.ln2 is None or self.ln2.rms)):
+            return False
+        if not cfg.attn_only and (self.mlp.gated or cfg.act_fn not in ("gelu_new", "gelu_fast", "gelu_pytorch_tanh")):
+            return False
+        return True
+
+    def forward_paired(self, p, run: _Run, sites, stop_after: str, captures, last_only: bool = False):
+        """One block over paired rows (``ops.hip_ops.Paired``: base rows with autograd, source rows without).
+
+        ``sites``: hook name -> list of TorchIndex spliced from source into base (only ``attn.hook_z`` and
+        ``mlp.hook_post`` occur); their source values go to ``captures``.  When the block holds ``stop_after`` (the
+        deepest site) the pairing ends right after it and the rest of the block runs on the base rows only.
+        Returns ``(resid, still_paired)``."""
+        ops = run.ops
+        attn = self.attn
+        zname = attn.hook_z.name
+        zs = sites.get(zname)
+        causal = self.cfg.attention_dir == "causal"
+        if zs is not None and any(ix.is_everything() for ix in zs):
+            # the base z is the source z: the base attention is dead, compute the source rows only
+            with torch.no_grad():
+                x = ops.layer_norm(p.src, self.ln1.w, self.ln1.b, self.ln1.eps)
+                q, k, v = ops.qkv(x, attn.W_Q, attn.W_K, attn.W_V, attn.b_Q, attn.b_K, attn.b_V)
+                z_src = ops.attention(q, k, v, causal, attn.attn_scale)
+            zf = torch.cat([z_src, z_src])
+            z = _hip_ops().Paired(zf[:z_src.shape[0]], zf)
+            resid = p
+        else:
+            x, resid = ops.pair_layer_norm_fork(p, self.ln1.w, self.ln1.b, self.ln1.eps)
+            qkv = ops.pair_qkv(x, attn.W_Q, attn.W_K, attn.W_V, attn.b_Q, attn.b_K, attn.b_V)
+            z = ops.pair_attention(qkv, causal, attn.attn_scale)
+            for ix in zs or ():
+                z = ops.pair_splice(z, ix)
+        if zs is not None:
+            captures[zname] = z.src
+        if zname == stop_after:
+            return self._finish_after_attn(z.base, resid.base, run, last_only), False
+        resid_mid = ops.pair_o_proj_residual(z, attn.W_O, attn.b_O, resid)
+        if self.cfg.attn_only:
+            return resid_mid, True
+        mlp = self.mlp
+        pname = mlp.hook_post.name
+        ps = sites.get(pname)
+        erf = False  # gelu_new family only (paired_ok)
+        if ps is None:
+            x, resid2 = ops.pair_layer_norm_fork(resid_mid, self.ln2.w, self.ln2.b, self.ln2.eps)
+            return ops.pair_mlp_gelu_residual(x, mlp.W_in, mlp.b_in, mlp.W_out, mlp.b_out, resid2, erf=erf), True
+        if any(ix.is_everything() for ix in ps):
+            with torch.no_grad():
+                x = ops.layer_norm(resid_mid.src, self.ln2.w, self.ln2.b, self.ln2.eps)
+                _, post_src = ops.mlp_in(x, mlp.W_in, mlp.b_in, self.cfg.act_fn)
+            qf = torch.cat([post_src, post_src])
+            post = _hip_ops().Paired(qf[:post_src.shape[0]], qf)
+            resid2 = resid_mid
+        else:
+            x, resid2 = ops.pair_layer_norm_fork(resid_mid, self.ln2.w, self.ln2.b, self.ln2.eps)
+            _, post = ops.pair_mlp_in(x, mlp.W_in, mlp.b_in, erf=erf)
+            for ix in ps:
+                post = ops.pair_splice(post, ix)
+        captures[pname] = post.src
+        if pname == stop_after:
+            return ops.mlp_out_residual(post.base, mlp.W_out, mlp.b_out, resid2.base), False
+        return ops.pair_mlp_out_residual(post, mlp.W_out, mlp.b_out, resid2), True
+
+    def _finish_after_attn(self, z, resid, run: _Run, last_only: bool):
+        """The rest of the block (O projection + MLP) on base rows, after a paired attention section."""
+        ops = run.ops
+        attn = self.attn
+        if last_only:
+            z, resid = z[:, -1:].contiguous(), resid[:, -1:].contiguous()
+        resid_mid = ops.o_proj_residual(z, attn.W_O, attn.b_O, resid)
+        if self.cfg.attn_only:
+            return resid_mid
+        mlp = self.mlp
+        x, resid_mid = self._norm_fork(self.ln2, resid_mid, run)
+        return ops.mlp_gelu_residual(x, mlp.W_in, mlp.b_in, mlp.W_out, mlp.b_out, resid_mid)
+
+
 def qkv_arena_groups(blocks, cfg):
     """Arena groups packing each block's ``W_Q|W_K|W_V`` into one ``[d_model][(H + 2*H_kv)*d_head]`` matrix
     (query heads, then key heads, then value heads; column ``head*dh + e``) and ``b_Q|b_K|b_V`` into
@@ -596,6 +680,76 @@ class HookedTransformer(HookedRootModule):
         with torch.no_grad():
             self.forward(tokens, plan=plan)
         return plan.cache
+
+    def run_paired(self, tokens: torch.Tensor, src_tokens: torch.Tensor, sites, logits: str = "full"):
+        """Interchange intervention with the source run folded into the base forward.
+
+        ``sites``: ``{hook name: [TorchIndex, ...]}`` spliced from the source run into the base run, as
+        ``ll_source_cache`` + ``ll_intervened_forward`` do with two forwards
+        (/root/reference/iit/model_pairs/base_model_pair.py:80-98).  Up to the deepest site both runs go through
+        every kernel as one batch of 2B rows (``ops.hip_ops.Paired``): the source rows carry no autograd state (the
+        reference's source run is under no_grad) and the base rows are exactly the unpaired intervened forward's.
+        Returns ``(output, {site: source activation})``, or None when the configuration is not covered (fused HIP
+        backend, short-sequence attention, LN models, sites on ``attn.hook_z`` / ``mlp.hook_post``, no live user
+        hook) -- the caller then runs the two forwards.  ``IIT_PAIRED=0`` disables it."""
+        import os
+        if os.environ.get("IIT_PAIRED", "1") == "0" or not sites:
+            return None
+        ops = self.ops()
+        cfg = self.cfg
+        if not getattr(ops, "supports_pairs", False) or self.rotary or cfg.final_rms:
+            return None
+        if tokens.dim() != 2 or tokens.shape != src_tokens.shape or tokens.shape[1] > 16 or tokens.shape[1] < 1:
+            return None
+        if torch.is_grad_enabled() and self.__dict__.get("_grad_cuts"):
+            return None
+        if any(hp.is_live for hp in self.hook_dict.values()):
+            return None
+        B, S = tokens.shape
+        order = []
+        for name, idxs in sites.items():
+            parts = name.split(".")
+            if len(parts) != 4 or parts[0] != "blocks" or (parts[2], parts[3]) not in (("attn", "hook_z"),
+                                                                                        ("mlp", "hook_post")):
+                return None
+            li = int(parts[1])
+            if parts[2] == "mlp" and cfg.attn_only:
+                return None
+            shape = (B, S, cfg.n_heads, cfg.d_head) if parts[2] == "attn" else (B, S, cfg.d_mlp)
+            for ix in idxs:
+                if not ix.is_everything() and ix.to_ranges(shape) is None:
+                    return None
+            order.append((li, 0 if parts[2] == "attn" else 1, name))
+        deepest = max(order)
+        if not all(blk.paired_ok(None) for blk in self.blocks[:deepest[0] + 1]):
+            return None
+        tokens = tokens.to(self.embed.W_E.device)
+        src_tokens = src_tokens.to(self.embed.W_E.device)
+        run = _Run(RunPlan(logits=logits), ops)
+        ops.begin_forward()
+        n = len(self.blocks)
+        final_mlp_site = not cfg.attn_only and self.blocks[-1].mlp.hook_post.name in sites
+        last_only = (logits == "last" and n > 0 and S > 1 and getattr(self, "last_position_final_block", True)
+                     and self.blocks[-1].last_position_ok(run) and not final_mlp_site)
+        captures = {}
+        resid = ops.pair_embed_pos(tokens, src_tokens, self.embed.W_E, self.pos_embed.W_pos)
+        paired = True
+        for li, block in enumerate(self.blocks):
+            lo = last_only and li == n - 1
+            if paired:
+                resid, paired = block.forward_paired(resid, run, sites, deepest[2], captures, last_only=lo)
+            else:
+                resid = block(resid, run, last_only=lo)
+        if paired:  # (cannot happen: the deepest site ends the pairing) -- keep the base rows
+            resid = resid.base
+        if logits == "none":
+            return None, captures
+        if logits == "last":
+            resid = resid[:, -1]
+        x = resid if self.ln_final is None else self.ln_final.run(resid, run)
+        if logits == "argmax":
+            return ops.unembed_argmax(x, self.unembed.W_U, self.unembed.b_U), captures
+        return ops.unembed(x, self.unembed.W_U, self.unembed.b_U), captures
 
     def to_tokens(self, input, prepend_bos: Optional[bool] = None):
         if self.tokenizer is None:

@@ -959,6 +959,247 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     return CrossEntropyFn.apply(logits.float(), labels)
 
 
+# ============================================================================ paired (source + base) rows
+# One launch per op over the rows of BOTH runs of an interchange intervention: the base run (rows [0, B), with
+# autograd) and the no-grad source run (rows [B, 2B)) share every weight, so up to the deepest splice site the two
+# forwards are one M = 2T batch (the reference runs them as two forwards,
+# /root/reference/iit/model_pairs/base_model_pair.py:80-98).  Each paired Function computes over the full rows,
+# returns the base rows as its (differentiable) output, appends the full result to ``box`` for the source side
+# and saves only base-row slices for the backward -- the backward is the unpaired op's, unchanged, so source rows
+# cost no backward work and produce no gradient (the reference's source run is under no_grad).
+
+
+class Paired:
+    """An activation of a paired forward: ``full`` [2B, ...] (rows [0, B) base, [B, 2B) source) and ``base``, the
+    autograd-visible tensor holding the values of ``full[:B]`` (a view of it, or a passthrough of such a view)."""
+
+    __slots__ = ("base", "full")
+
+    def __init__(self, base: torch.Tensor, full: torch.Tensor):
+        self.base, self.full = base, full
+
+    @property
+    def nb(self) -> int:
+        return self.base.shape[0]
+
+    @property
+    def src(self) -> torch.Tensor:
+        return self.full[self.nb:]
+
+
+class EmbedPosPairFn(EmbedPosFn):
+    @staticmethod
+    def forward(ctx, tokens, W_E, W_pos, tokens_full, box):
+        ctx.set_materialize_grads(False)
+        B2, S = tokens_full.shape
+        d = W_E.shape[1]
+        B = tokens.shape[0]
+        out = torch.empty(B2, S, d, dtype=F32, device=tokens.device)
+        K.embed_pos_fwd(tokens_full, W_E, W_pos, out, B2, S, d)
+        ctx.save_for_backward(tokens_full[:B])
+        ctx.params = (W_E, W_pos)
+        box.append(out)
+        return out[:B]
+
+    @staticmethod
+    def backward(ctx, g):
+        return EmbedPosFn.backward(ctx, g) + (None, None)
+
+
+class LayerNormForkPairFn(LayerNormForkFn):
+    @staticmethod
+    def forward(ctx, x, w, b, eps, x_full, box):
+        ctx.set_materialize_grads(False)
+        d = x.shape[-1]
+        B = x.shape[0]
+        x2 = _flat2(x_full)
+        T2 = x2.shape[0]
+        T = T2 * B // x_full.shape[0]
+        y = torch.empty(T2, d, dtype=BF16, device=x.device)
+        mean = torch.empty(T2, dtype=F32, device=x.device)
+        rstd = torch.empty(T2, dtype=F32, device=x.device)
+        K.ln_fwd(x2, w, b, y, mean, rstd, T2, d, eps)
+        ctx.save_for_backward(x2[:T], mean[:T], rstd[:T])
+        ctx.params = (w, b)
+        ctx.in_dtype = x.dtype
+        yf = y.view(*x_full.shape[:-1], d)
+        box.append(yf)
+        return yf[:B], x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dpass):
+        return LayerNormForkFn.backward(ctx, dy, dpass) + (None, None)
+
+
+class QKVPairFn(QKVFn):
+    @staticmethod
+    def forward(ctx, x, layer, bias_bf16, W_Q, W_K, W_V, b_Q, b_K, b_V, x_full, box):
+        ctx.set_materialize_grads(False)
+        B, S, d = x.shape
+        B2 = x_full.shape[0]
+        H, dh = W_Q.shape[0], W_Q.shape[2]
+        HD = H * dh
+        x2 = _flat2(x_full)
+        T2 = x2.shape[0]
+        out = torch.empty(B2, S, 3, H, dh, dtype=BF16, device=x.device)
+        gemm(x2, layer["qkv"], out, M=T2, N=3 * HD, K=d, lda=d, ldb=3 * HD, ldc=3 * HD, mode=K.MODE_BKM,
+             epi=K.EPI_BF16_BIAS3, bias0=b_Q, bias1=b_K, bias2=b_V, bias_cols=HD, blas_bias=bias_bf16)
+        ctx.save_for_backward(x2[:B * S])
+        ctx.layer = layer
+        ctx.params = (W_Q, W_K, W_V, b_Q, b_K, b_V)
+        ctx.dims = (B, S, d, H, dh)
+        box.append(out)
+        return out[:B]
+
+    @staticmethod
+    def backward(ctx, dqkv):
+        return QKVFn.backward(ctx, dqkv) + (None, None)
+
+
+class AttnPairFn(AttnFn):
+    @staticmethod
+    def forward(ctx, qkv, causal, scale, qkv_full, box):
+        ctx.set_materialize_grads(False)
+        B = qkv.shape[0]
+        B2, S, _, H, dh = qkv_full.shape
+        z = torch.empty(B2, S, H, dh, dtype=BF16, device=qkv.device)
+        lse = torch.empty(B2 * H * S, dtype=F32, device=qkv.device)
+        K.attn_small_fwd(qkv_full, z, lse, None, 0, B2, S, H, dh, 3 * H * dh, H * dh, H * dh, scale, causal)
+        ctx.save_for_backward(qkv_full[:B], lse[:B * H * S])  # lse rows are (batch, head)-major
+        ctx.cfg = (0, causal, scale)
+        box.append(z)
+        return z[:B]
+
+    @staticmethod
+    def backward(ctx, dz):
+        g = AttnFn.backward(ctx, dz)
+        return (g[0], None, None, None, None)
+
+
+class LinearPairFn(LinearFn):
+    """bf16 out or fp32 ``resid + xW + b`` out (``resid_full`` paired with the input rows)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, w, ldw, resid, out_kind, x_full, resid_full, box):
+        ctx.set_materialize_grads(False)
+        B = x.shape[0]
+        lead = x.shape[:-1]
+        Kd = x.shape[-1]
+        N = W.shape[-1]
+        x2 = _flat2(x_full)
+        T2 = x2.shape[0]
+        T = T2 * B // x_full.shape[0]
+        if out_kind == "bf16":
+            out = torch.empty(T2, N, dtype=BF16, device=x.device)
+            gemm(x2, w, out, M=T2, N=N, K=Kd, lda=Kd, ldb=ldw, ldc=N, mode=K.MODE_BKM, epi=K.EPI_BF16, bias0=b)
+        else:
+            r2 = _flat2(resid_full)
+            out = torch.empty(T2, N, dtype=F32, device=x.device)
+            gemm(x2, w, out, M=T2, N=N, K=Kd, lda=Kd, ldb=ldw, ldc=N, mode=K.MODE_BKM, epi=K.EPI_F32_RESID, bias0=b,
+                 resid=r2, ldr=N)
+        ctx.save_for_backward(x2[:T])
+        ctx.params = (W, b)
+        ctx.w = w
+        ctx.ldw = ldw
+        ctx.meta = (lead, Kd, N, out_kind, x.dtype)
+        of = out.view(*x_full.shape[:-1], N)
+        box.append(of)
+        return of[:B]
+
+    @staticmethod
+    def backward(ctx, gy):
+        return LinearFn.backward(ctx, gy) + (None, None, None)
+
+
+class MLPInPairFn(MLPInFn):
+    @staticmethod
+    def forward(ctx, x, W_in, b_in, w, erf, x_full, box):
+        ctx.set_materialize_grads(False)
+        ctx.erf = erf
+        B = x.shape[0]
+        lead = x.shape[:-1]
+        d = x.shape[-1]
+        dm = W_in.shape[1]
+        x2 = _flat2(x_full)
+        T2 = x2.shape[0]
+        T = T2 * B // x_full.shape[0]
+        post = torch.empty(T2, dm, dtype=BF16, device=x.device)
+        pre = torch.empty(T2, dm, dtype=BF16, device=x.device)
+        gemm(x2, w, post, C2=pre, M=T2, N=dm, K=d, lda=d, ldb=dm, ldc=dm, ldc2=dm, mode=K.MODE_BKM,
+             epi=K.EPI_GELU_ERF if erf else K.EPI_GELU, bias0=b_in)
+        ctx.save_for_backward(x2[:T], pre[:T])
+        ctx.params = (W_in, b_in)
+        ctx.w = w
+        ctx.meta = (lead, d, dm)
+        pf, qf = pre.view(*x_full.shape[:-1], dm), post.view(*x_full.shape[:-1], dm)
+        box.append((pf, qf))
+        return pf[:B], qf[:B]
+
+    @staticmethod
+    def backward(ctx, gpre, gpost):
+        return MLPInFn.backward(ctx, gpre, gpost) + (None, None)
+
+
+class MLPOutGeluPairFn(MLPOutGeluFn):
+    @staticmethod
+    def forward(ctx, pre, post, W, b, w, ldw, resid, b_in, erf, post_full, resid_full, box):
+        ctx.set_materialize_grads(False)
+        ctx.erf = erf
+        B = post.shape[0]
+        lead = post.shape[:-1]
+        Kd = post.shape[-1]
+        N = W.shape[-1]
+        x2 = _flat2(post_full)
+        T2 = x2.shape[0]
+        T = T2 * B // post_full.shape[0]
+        r2 = _flat2(resid_full)
+        out = torch.empty(T2, N, dtype=F32, device=post.device)
+        gemm(x2, w, out, M=T2, N=N, K=Kd, lda=Kd, ldb=ldw, ldc=N, mode=K.MODE_BKM, epi=K.EPI_F32_RESID, bias0=b,
+             resid=r2, ldr=N)
+        ctx.save_for_backward(x2[:T], _flat2(pre))
+        ctx.params = (W, b, b_in)
+        ctx.w = w
+        ctx.ldw = ldw
+        ctx.meta = (lead, Kd, N)
+        of = out.view(*post_full.shape[:-1], N)
+        box.append(of)
+        return of[:B]
+
+    @staticmethod
+    def backward(ctx, gy):
+        return MLPOutGeluFn.backward(ctx, gy) + (None, None, None)
+
+
+class PairSpliceFn(Function):
+    """Splice at a paired site: ``out_full[:B] = base`` with ``index`` taken from the source rows at the same
+    positions, ``out_full[B:] = source`` -- one launch of the patch-spec kernel over a leading (base, source) axis.
+    Gradient: the base gradient with the spliced elements zeroed (exactly :class:`iit_amd.ops.splice.SpliceFn`)."""
+
+    @staticmethod
+    def forward(ctx, act, act_full, spec_pair, spec_base, box):
+        out = torch.empty_like(act_full)
+        B = act.shape[0]
+        K.splice(act_full, act_full[B:], out, act_full.numel(), spec_pair.ptr, act_full.dtype == F32, 0)
+        ctx.spec = spec_base
+        box.append(out)
+        return out[:B]
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is None:
+            return None, None, None, None, None
+        g = g.contiguous()
+        out = torch.empty_like(g)
+        K.splice(g, None, out, g.numel(), ctx.spec.ptr, g.dtype == F32, 1)
+        return out, None, None, None, None
+
+
+def _one(fn, *args):
+    box = []
+    out = fn.apply(*args, box)
+    return out, box[0]
+
+
 # ============================================================================ op backend
 class HipOps(TorchOps):
     name = "hip"
@@ -1100,6 +1341,77 @@ class HipOps(TorchOps):
                 best_v = torch.where(upd, v, best_v)
                 best_i = torch.where(upd, i, best_i)
         return best_i.view(*lead)
+
+
+    # -- paired (source + base) rows: see Paired ----------------------------------------------------------------
+    supports_pairs = True
+
+    def pair_embed_pos(self, tokens, src_tokens, W_E, W_pos) -> Paired:
+        full_tok = torch.cat([tokens, src_tokens]).contiguous()
+        out, full = _one(EmbedPosPairFn, tokens, W_E, W_pos, full_tok)
+        return Paired(out, full)
+
+    def pair_layer_norm_fork(self, p: Paired, w, b, eps):
+        """(LN of both row sets, residual passthrough): ``(Paired normed, Paired resid)``."""
+        box = []
+        y, x_pass = LayerNormForkPairFn.apply(p.base, w, b, eps, p.full.float().contiguous(), box)
+        return Paired(y, box[0]), Paired(x_pass, p.full)
+
+    def pair_qkv(self, p: Paired, W_Q, W_K, W_V, b_Q, b_K, b_V) -> Paired:
+        i = self._layer_of[id(W_Q)]
+        out, full = _one(QKVPairFn, p.base, self.shadow.layers[i], self.shadow.biases[i], W_Q, W_K, W_V, b_Q, b_K,
+                         b_V, p.full)
+        return Paired(out, full)
+
+    def pair_attention(self, p: Paired, causal: bool, attn_scale: float) -> Paired:
+        out, full = _one(AttnPairFn, p.base, causal, 1.0 / attn_scale, p.full)
+        return Paired(out, full)
+
+    def pair_o_proj_residual(self, z: Paired, W_O, b_O, resid: Paired) -> Paired:
+        B2, S, H, dh = z.full.shape
+        B = z.base.shape[0]
+        out, full = _one(LinearPairFn, z.base.reshape(B, S, H * dh), W_O, b_O, self._L(W_O)["o"], W_O.shape[-1],
+                         resid.base, "resid", z.full.reshape(B2, S, H * dh), resid.full.float().contiguous())
+        return Paired(out, full)
+
+    def pair_mlp_in(self, x: Paired, W_in, b_in, erf: bool = False):
+        (pre, post), (pf, qf) = _one(MLPInPairFn, x.base, W_in, b_in, self._L(W_in)["in"], erf, x.full)
+        return Paired(pre, pf), Paired(post, qf)
+
+    def pair_mlp_out_residual(self, post: Paired, W_out, b_out, resid: Paired) -> Paired:
+        out, full = _one(LinearPairFn, post.base, W_out, b_out, self._L(W_out)["out"], W_out.shape[1], resid.base,
+                         "resid", post.full, resid.full.float().contiguous())
+        return Paired(out, full)
+
+    def pair_mlp_gelu_residual(self, x: Paired, W_in, b_in, W_out, b_out, resid: Paired, erf: bool = False):
+        pre, post = self.pair_mlp_in(x, W_in, b_in, erf)
+        out, full = _one(MLPOutGeluPairFn, pre.base, post.base.detach(), W_out, b_out, self._L(W_out)["out"],
+                         W_out.shape[1], resid.base, b_in, erf, post.full, resid.full.float().contiguous())
+        return Paired(out, full)
+
+    def pair_splice(self, p: Paired, index) -> Optional[Paired]:
+        """Base rows take the source rows' values at ``index`` (None when the range table cannot express it)."""
+        from . import splice as _sp
+        B = p.base.shape[0]
+        shape = tuple(p.base.shape)
+        ranges = index.to_ranges(shape)
+        if ranges is None or not p.full.is_contiguous():
+            return None
+        src = p.full[B:]
+        strides = [0] + list(src.stride())
+        dims = _sp._collapse((2,) + shape, [[(0, 1)]] + ranges, strides)
+        base_spec = _sp.patch_spec(index, shape)
+        if dims is None or base_spec is None:
+            return None
+        key = ("pair",) + shape
+        cache = getattr(index, "_iit_specs", None)
+        if cache is None:
+            cache = index._iit_specs = {}
+        spec = cache.get(key)
+        if spec is None:
+            spec = cache[key] = _sp.PatchSpec(dims)
+        out, full = _one(PairSpliceFn, p.base, p.full, spec, base_spec)
+        return Paired(out, full)
 
 
 def get_hip_ops(model) -> HipOps:

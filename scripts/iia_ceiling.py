@@ -51,19 +51,22 @@ def tie_stats(pair, test_set, batch: int = 512):
 
 def per_node_iia(pair, test_set, batch: int = 512):
     """val/IIA of every HL node over the whole validation split (the pair's own eval draws one node per batch)."""
-    res = {}
+    res, losses = {}, {}
     pair._ll_module().eval()
     for node in pair.corr.keys():
         hits = n = 0
+        loss = 0.0
         for base, abl in test_set.make_loader(batch, 0, shuffle=False):
             with torch.no_grad():
                 hl_out, ll_out = pair.do_intervention(base, abl, node)
             hl_last = hl_out[:, -1] if hl_out.dim() == 3 else hl_out
             ll_last = ll_out[:, -1] if ll_out.dim() == 3 else ll_out
             hits += int((ll_last.argmax(-1) == hl_last.argmax(-1)).sum())
+            loss += float(torch.nn.functional.cross_entropy(ll_last.float(), hl_last.argmax(-1), reduction="sum"))
             n += hl_last.shape[0]
         res[node.name] = 100.0 * hits / max(n, 1)
-    return res
+        losses[node.name] = loss / max(n, 1)
+    return res, losses
 
 
 def main():
@@ -72,6 +75,7 @@ def main():
     ap.add_argument("--epochs", type=int, default=70)
     ap.add_argument("--every", type=int, default=5)
     ap.add_argument("--num-samples", type=int, default=12000)
+    ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--graphs", type=int, default=1, help="0: eager phases (no HIP graphs)")
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"],
                     help="torch: the fp32 torch-op oracle backend on the same device")
@@ -100,7 +104,7 @@ def main():
     train_ds, test_ds = train_test_split(ds, test_size=0.2, random_state=42)
     train_set = IITDataset(train_ds, train_ds, seed=0, device=dev)
     test_set = IITDataset(test_ds, test_ds, seed=0, device=dev)
-    training_args = {"batch_size": 256, "lr": 1e-4, "iit_weight": 1.0, "behavior_weight": 1.0, "strict_weight": 0.4,
+    training_args = {"batch_size": 256, "lr": args.lr, "iit_weight": 1.0, "behavior_weight": 1.0, "strict_weight": 0.4,
                      "next_token": False, "lr_scheduler": None, "clip_grad_norm": 1.0, "early_stop": False,
                      "use_single_loss": False, "graphs": bool(args.graphs)}
     pair = IOI_ModelPair(ll_model=ll, hl_model=hl, corr=make_ioi_corr(cfg["n_layers"]), training_args=training_args)
@@ -147,7 +151,9 @@ def main():
         row = {"epoch": epoch, "val/IIA": round(float(vals["val/IIA"]), 2), "eval_node_draws": dict(mix)}
         if epoch % args.every == 0 or epoch == args.epochs - 1:
             rng_state = pair.rng.bit_generator.state
-            row["per_node_IIA"] = {k: round(v, 2) for k, v in per_node_iia(pair, test_set).items()}
+            iia, ce = per_node_iia(pair, test_set)
+            row["per_node_IIA"] = {k: round(v, 2) for k, v in iia.items()}
+            row["per_node_IIT_loss"] = {k: round(v, 4) for k, v in ce.items()}
             pair.rng.bit_generator.state = rng_state  # per-node evaluation draws nothing; keep the RNG anyway
             pair._ll_module().train()
             orig_log(epoch, metrics, sink)
@@ -158,7 +164,7 @@ def main():
     wall = time.perf_counter() - t0
     best = max(rows, key=lambda r: r["val/IIA"])
     print(json.dumps({"metric": "IOI val/IIA ceiling analysis", "model": args.model, "epochs": args.epochs,
-                      "train_nodes": args.train_nodes or "all", "graphs": args.graphs, "backend": args.backend,
+                      "train_nodes": args.train_nodes or "all", "graphs": args.graphs, "backend": args.backend, "lr": args.lr,
                       "wall_s": round(wall, 1), "tie_fraction_per_node": ties,
                       "best_epoch_val_IIA": best["val/IIA"], "best_epoch": best["epoch"],
                       "final_per_node_IIA": rows[-1].get("per_node_IIA")}))

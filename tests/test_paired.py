@@ -1,0 +1,133 @@
+"""Paired source + base forward (HookedTransformer.run_paired, ops.hip_ops Paired functions): the source run of an
+interchange intervention folded into the base forward as one batch of 2B rows up to the deepest splice site
+(the reference runs two forwards, /root/reference/iit/model_pairs/base_model_pair.py:80-98).
+Oracle: the same model's unpaired path (truncated source capture + spliced forward)."""
+import pytest
+import torch
+
+from iit_amd.core.index import Ix
+
+pytestmark = pytest.mark.gpu
+
+L, D, H, DH, DM, V, S, B = 4, 128, 4, 32, 512, 1000, 16, 32
+
+
+def _model(vocab=V):
+    from iit_amd.models.transformer import HookedTransformer
+    cfg = dict(n_layers=L, d_model=D, n_heads=H, d_head=DH, d_mlp=DM, n_ctx=S, d_vocab=vocab, act_fn="gelu_new",
+               normalization_type="LNPre", device="cuda", dtype=torch.bfloat16, positional_embedding_type="standard")
+    torch.manual_seed(0)
+    m = HookedTransformer(cfg)
+    m.set_op_backend("hip")
+    return m
+
+
+SITES = [
+    {"blocks.0.attn.hook_z": [Ix[[None]]]},                                   # whole z (dead base attention)
+    {"blocks.1.attn.hook_z": [Ix[:, :, 2]]},                                  # one head
+    {"blocks.1.mlp.hook_post": [Ix[[None]]]},                                 # whole MLP post
+    {"blocks.2.mlp.hook_post": [Ix[:, :, :64]]},                              # neuron range
+    {"blocks.0.attn.hook_z": [Ix[[None]]], "blocks.2.attn.hook_z": [Ix[[None]]]},  # two layers
+    {"blocks.3.attn.hook_z": [Ix[:, :, 1]]},                                  # final block: last-position tail
+    {"blocks.3.mlp.hook_post": [Ix[:, -1, :128]]},                            # final block MLP, last position
+    {"blocks.1.attn.hook_z": [Ix[:, [3, 7]]]},                                # position list
+]
+
+
+def _unpaired(m, base, src, sites, logits):
+    from iit_amd.engine.plan import RunPlan
+    cache = m.run_capture(src, list(sites))
+    plan = RunPlan.with_splices([(n, ix, cache[n]) for n, ixs in sites.items() for ix in ixs], logits=logits)
+    return m(base, plan=plan), cache
+
+
+@pytest.mark.parametrize("sites", SITES, ids=[",".join(s) for s in SITES])
+@pytest.mark.parametrize("logits", ["last", "full"])
+def test_paired_matches_two_forwards(sites, logits):
+    m = _model()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    base = torch.randint(0, V, (B, S), device="cuda", generator=g)
+    src = torch.randint(0, V, (B, S), device="cuda", generator=g)
+    w = torch.randn(B, V, device="cuda", generator=g)
+
+    def loss_of(out):
+        o = out[:, -1] if out.dim() == 3 else out
+        return (o.float() * w).sum()
+
+    m.zero_grad(set_to_none=True)
+    ref, ref_cache = _unpaired(m, base, src, sites, logits)
+    loss_of(ref).backward()
+    g_ref = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+
+    m.zero_grad(set_to_none=True)
+    res = m.run_paired(base, src, sites, logits=logits)
+    assert res is not None, "paired path not taken"
+    out, cache = res
+    loss_of(out).backward()
+    g_pair = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+
+    assert out.shape == ref.shape
+    assert torch.allclose(out.float(), ref.float(), rtol=2e-2, atol=2e-2), (out.float() - ref.float()).abs().max()
+    for n in sites:
+        assert torch.allclose(cache[n].float(), ref_cache[n].float(), rtol=1e-2, atol=1e-2), n
+    assert set(g_pair) == set(g_ref)
+    for k in g_ref:
+        err = float((g_pair[k] - g_ref[k]).norm() / (g_ref[k].norm() + 1e-12))
+        assert err < 2e-2, (k, err)
+
+
+def test_paired_source_rows_get_no_gradient_and_no_graph():
+    """The source activations returned by the paired forward are plain tensors (no autograd history)."""
+    m = _model()
+    base = torch.randint(0, V, (B, S), device="cuda")
+    src = torch.randint(0, V, (B, S), device="cuda")
+    out, cache = m.run_paired(base, src, {"blocks.2.attn.hook_z": [Ix[:, :, 0]]}, logits="last")
+    assert out.requires_grad
+    assert not cache["blocks.2.attn.hook_z"].requires_grad
+
+
+def test_paired_declines_what_it_does_not_cover():
+    m = _model()
+    base = torch.randint(0, V, (B, S), device="cuda")
+    src = torch.randint(0, V, (B, S), device="cuda")
+    assert m.run_paired(base, src, {"blocks.1.hook_resid_pre": [Ix[[None]]]}) is None
+    assert m.run_paired(base, src[:, :8], {"blocks.1.attn.hook_z": [Ix[[None]]]}) is None
+    h = m.blocks[0].attn.hook_z.add_hook(lambda x, hook: x)
+    try:
+        assert m.run_paired(base, src, {"blocks.1.attn.hook_z": [Ix[[None]]]}) is None
+    finally:
+        m.reset_hooks()
+
+
+def test_ioi_pair_step_paired_equals_unpaired():
+    """A whole IOI_ModelPair training step (IIT + strict + behaviour phases, eager) with and without pairing."""
+    from iit_amd.data.iit_dataset import IITDataset
+    from iit_amd.model_pairs import IOI_ModelPair
+    from iit_amd.ops import hip_ops
+    from iit_amd.tasks.ioi import NAMES, make_ioi_corr, make_ioi_dataset_and_hl
+
+    calls = []
+    orig = hip_ops.HipOps.pair_embed_pos
+    hip_ops.HipOps.pair_embed_pos = lambda self, *a, **k: (calls.append(1), orig(self, *a, **k))[1]
+    try:
+        losses = {}
+        for paired in (False, True):
+            m = _model(50257)
+            ds, hl = make_ioi_dataset_and_hl(512, m, NAMES, device="cuda")
+            train = IITDataset(ds, ds, seed=0, device="cuda")
+            pair = IOI_ModelPair(hl, m, make_ioi_corr(L), training_args={
+                "batch_size": 64, "lr": 1e-3, "lr_scheduler": None, "paired": paired, "graphs": False})
+            opt = pair.make_optimizer(1e-3)
+            base, abl = next(iter(train.make_loader(64, 0)))
+            out = []
+            for node in list(pair.corr.keys()):
+                pair.sample_hl_name = lambda node=node: node
+                out.append({k: float(v) for k, v in pair.run_train_step(base, abl, pair.loss_fn, opt).items()})
+            losses[paired] = out
+            if paired:
+                assert calls, "the paired path never ran"
+        for a, b in zip(losses[False], losses[True]):
+            for k in a:
+                assert abs(a[k] - b[k]) <= 2e-2 * max(1.0, abs(a[k])), (k, a[k], b[k])
+    finally:
+        hip_ops.HipOps.pair_embed_pos = orig
