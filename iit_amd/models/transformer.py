@@ -717,7 +717,7 @@ class HookedTransformer(HookedRootModule):
                 return None
             shape = (B, S, cfg.n_heads, cfg.d_head) if parts[2] == "attn" else (B, S, cfg.d_mlp)
             for ix in idxs:
-                if not ix.is_everything() and ix.to_ranges(shape) is None:
+                if not ix.is_everything() and _hip_ops().pair_specs(ix, shape) is None:
                     return None
             order.append((li, 0 if parts[2] == "attn" else 1, name))
         deepest = max(order)

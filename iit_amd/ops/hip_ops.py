@@ -1391,27 +1391,49 @@ class HipOps(TorchOps):
 
     def pair_splice(self, p: Paired, index) -> Optional[Paired]:
         """Base rows take the source rows' values at ``index`` (None when the range table cannot express it)."""
-        from . import splice as _sp
-        B = p.base.shape[0]
-        shape = tuple(p.base.shape)
-        ranges = index.to_ranges(shape)
-        if ranges is None or not p.full.is_contiguous():
+        if not p.full.is_contiguous():
             return None
-        src = p.full[B:]
-        strides = [0] + list(src.stride())
-        dims = _sp._collapse((2,) + shape, [[(0, 1)]] + ranges, strides)
-        base_spec = _sp.patch_spec(index, shape)
-        if dims is None or base_spec is None:
+        specs = pair_specs(index, tuple(p.base.shape))
+        if specs is None:
             return None
-        key = ("pair",) + shape
-        cache = getattr(index, "_iit_specs", None)
-        if cache is None:
-            cache = index._iit_specs = {}
-        spec = cache.get(key)
-        if spec is None:
-            spec = cache[key] = _sp.PatchSpec(dims)
-        out, full = _one(PairSpliceFn, p.base, p.full, spec, base_spec)
+        out, full = _one(PairSpliceFn, p.base, p.full, specs[0], specs[1])
         return Paired(out, full)
+
+
+def pair_specs(index, shape):
+    """(paired spec, base spec) of ``index`` on a hook of base shape ``shape`` whose paired activation is the
+    contiguous [2B, ...] tensor: the paired spec selects ``index`` inside rows [0, B) and reads the source from rows
+    [B, 2B) at the same positions (a whole-batch index merges the (base | source) axis into the batch axis: rows
+    [0, B) of 2B), or None when the kernel's 4-dimensional range table cannot express it."""
+    from . import splice as _sp
+    key = ("pair",) + tuple(shape)
+    cache = getattr(index, "_iit_specs", None)
+    if cache is not None and key in cache:
+        return cache[key]
+    ranges = index.to_ranges(tuple(shape))
+    base_spec = _sp.patch_spec(index, tuple(shape))
+    out = None
+    if ranges is not None and base_spec is not None:
+        B = shape[0]
+        rest = list(shape[1:])
+        row = 1
+        for n in rest:
+            row *= n
+        cstr = []  # contiguous strides of the trailing dims
+        acc = 1
+        for n in reversed(rest):
+            cstr.insert(0, acc)
+            acc *= n
+        if ranges[0] == [(0, B)]:
+            dims = _sp._collapse((2 * B,) + tuple(rest), [[(0, B)]] + ranges[1:], [row] + cstr)
+        else:
+            dims = _sp._collapse((2, B) + tuple(rest), [[(0, 1)]] + ranges, [0, row] + cstr)
+        if dims is not None:
+            out = (_sp.PatchSpec(dims), base_spec)
+    if cache is None:
+        cache = index._iit_specs = {}
+    cache[key] = out
+    return out
 
 
 def get_hip_ops(model) -> HipOps:
