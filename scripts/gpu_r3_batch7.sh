@@ -1,5 +1,5 @@
-# Round 3 batch 7: train.py's full MNIST-PVR configuration (60k/10k, 10 epochs) wall clock; eval_ioi sweep timing on
-# the HIP engine (cold + warm) and the fp32 torch-op backend; one-step kernel sequence of the headline bench.
+# Round 3 batch 7: paired/splice GPU tests; train.py's full MNIST-PVR configuration (60k/10k, 10 epochs) wall clock;
+# eval_ioi sweep timing on the HIP engine (cold + warm) and the fp32 torch-op backend; one-step kernel sequence.
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -15,6 +15,7 @@ run() {
   if [ $rc -ge 124 ]; then echo "stopping: $name rc=$rc"; exit $rc; fi
   return 0
 }
+run tests_paired 400 python3 -u -m pytest tests/test_paired.py tests/test_splice.py -x -q --timeout 120 --timeout-method thread
 run train_py_full 900 python3 -u train.py
 run ioi_ckpt 300 python3 -u train_ioi.py --model gpt2-small --dtype bf16 --epochs 2 --num-samples 4000 --save-root /tmp/r3models --no-early-stop
 run eval_ioi_hip 600 python3 -u eval_ioi.py --model gpt2-small -w 100_100_40 --root /tmp/r3models --backend hip --num-samples 4608 --timing-repeats 2
