@@ -45,12 +45,17 @@ __device__ __forceinline__ i16x4 tr_block(const __bf16* img, int g, int lane_in_
 }
 
 
+// Paired source + base rows (iit_amd/ops/hip_ops.py Paired): sequences [0, pair_seqs) are base rows, the rest source
+// rows.  Heads in ``pair_mask`` are spliced from source into base: the base wave of such a head computes nothing (its
+// z is the source's, its gradient zero) and the source wave stores its z into both rows.  ``z2`` (nullable) receives
+// a second copy of every stored z row (a whole-layer splice whose base z is the source z).
 template <int DH>
 __global__ __launch_bounds__(256) void attn_mfma_fwd_kernel(const __bf16* __restrict__ qkv, __bf16* __restrict__ z,
                                                             float* __restrict__ lse, const __bf16* __restrict__ zsrc,
                                                             unsigned long long head_mask, int BH, int S, int H,
                                                             long ld_qkv, long ld_z, long ld_src, float scale,
-                                                            int causal) {
+                                                            int causal, __bf16* __restrict__ z2, int pair_seqs,
+                                                            unsigned long long pair_mask) {
   constexpr int LDSR = DH + 8;
   __shared__ __attribute__((aligned(16))) __bf16 smem[4][16 * LDSR];
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
@@ -60,8 +65,11 @@ __global__ __launch_bounds__(256) void attn_mfma_fwd_kernel(const __bf16* __rest
   const int HD = H * DH;
   const long row0 = (long)b * S;
   const bool patched = valid && ((head_mask >> h) & 1ull);
+  const bool mirrored = valid && pair_seqs > 0 && ((pair_mask >> h) & 1ull);
+  const bool mirror_base = mirrored && b < pair_seqs;  // this base head takes the source's z
+  const bool mirror_src = mirrored && b >= pair_seqs;  // ... which this source wave also stores there
   __bf16* Vs = smem[wave];
-  if (valid && !patched) {
+  if (valid && !patched && !mirror_base) {
     for (int i = l; i < 16 * DH / 8; i += 64) {
       const int r = i / (DH / 8), ch = i % (DH / 8);
       *(bf16x8*)(Vs + r * LDSR + ch * 8) = load8(qkv + (row0 + r) * ld_qkv + 2 * HD + h * DH + ch * 8, r < S);
@@ -69,10 +77,16 @@ __global__ __launch_bounds__(256) void attn_mfma_fwd_kernel(const __bf16* __rest
   }
   __syncthreads();
   if (!valid) return;
+  if (mirror_base) {
+    if (lse && l < S) lse[(long)bh * S + l] = 0.f;
+    return;
+  }
   if (patched) {
     for (int i = l; i < S * DH / 8; i += 64) {
       const int r = i / (DH / 8), ch = i % (DH / 8);
-      *(uint4*)(z + (row0 + r) * ld_z + h * DH + ch * 8) = *(const uint4*)(zsrc + (row0 + r) * ld_src + h * DH + ch * 8);
+      const uint4 v = *(const uint4*)(zsrc + (row0 + r) * ld_src + h * DH + ch * 8);
+      *(uint4*)(z + (row0 + r) * ld_z + h * DH + ch * 8) = v;
+      if (z2) *(uint4*)(z2 + (row0 + r) * ld_z + h * DH + ch * 8) = v;
     }
     if (lse && l < S) lse[(long)bh * S + l] = 0.f;
     return;
@@ -124,7 +138,12 @@ __global__ __launch_bounds__(256) void attn_mfma_fwd_kernel(const __bf16* __rest
 #pragma unroll
   for (int i = l; i < 16 * DH / 8; i += 64) {
     const int r = i / (DH / 8), ch = i % (DH / 8);
-    if (r < S) *(bf16x8*)(z + (row0 + r) * ld_z + h * DH + ch * 8) = *(const bf16x8*)(Vs + r * LDSR + ch * 8);
+    if (r < S) {
+      const bf16x8 v = *(const bf16x8*)(Vs + r * LDSR + ch * 8);
+      *(bf16x8*)(z + (row0 + r) * ld_z + h * DH + ch * 8) = v;
+      if (z2) *(bf16x8*)(z2 + (row0 + r) * ld_z + h * DH + ch * 8) = v;
+      if (mirror_src) *(bf16x8*)(z + (row0 - (long)pair_seqs * S + r) * ld_z + h * DH + ch * 8) = v;
+    }
   }
 }
 
@@ -253,16 +272,33 @@ __global__ __launch_bounds__(256) void attn_mfma_bwd_kernel(const __bf16* __rest
   }
 }
 
+IIT_EXPORT int iit_attn_mfma_fwd_pair(const void* qkv, void* z, float* lse, const void* zsrc,
+                                      unsigned long long head_mask, int B, int S, int H, int dh, long ld_qkv, long ld_z,
+                                      long ld_src, float scale, int causal, void* z2, int pair_seqs,
+                                      unsigned long long pair_mask, void* stream);
+
 IIT_EXPORT int iit_attn_mfma_fwd(const void* qkv, void* z, float* lse, const void* zsrc, unsigned long long head_mask,
                                  int B, int S, int H, int dh, long ld_qkv, long ld_z, long ld_src, float scale,
                                  int causal, void* stream) {
+  return iit_attn_mfma_fwd_pair(qkv, z, lse, zsrc, head_mask, B, S, H, dh, ld_qkv, ld_z, ld_src, scale, causal,
+                                nullptr, 0, 0ull, stream);
+}
+
+// the same with the paired-row options of attn_mfma_fwd_kernel (``z2`` copy, ``pair_mask`` heads of the first
+// ``pair_seqs`` sequences taken from the sequences ``pair_seqs`` later)
+IIT_EXPORT int iit_attn_mfma_fwd_pair(const void* qkv, void* z, float* lse, const void* zsrc,
+                                      unsigned long long head_mask, int B, int S, int H, int dh, long ld_qkv, long ld_z,
+                                      long ld_src, float scale, int causal, void* z2, int pair_seqs,
+                                      unsigned long long pair_mask, void* stream) {
   if (S > 16) return (int)hipErrorInvalidValue;
+  if (pair_seqs < 0 || (pair_seqs > 0 && 2 * pair_seqs != B)) return (int)hipErrorInvalidValue;
   const int BH = B * H;
   dim3 grid((BH + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
 #define AF(D)                                                                                                       \
   hipLaunchKernelGGL(attn_mfma_fwd_kernel<D>, grid, block, 0, s, (const __bf16*)qkv, (__bf16*)z, lse,               \
-                     (const __bf16*)zsrc, head_mask, BH, S, H, ld_qkv, ld_z, ld_src, scale, causal)
+                     (const __bf16*)zsrc, head_mask, BH, S, H, ld_qkv, ld_z, ld_src, scale, causal, (__bf16*)z2,    \
+                     pair_seqs, pair_mask)
   if (dh == 32) AF(32);
   else if (dh == 64) AF(64);
   else if (dh == 96) AF(96);

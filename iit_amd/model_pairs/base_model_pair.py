@@ -394,9 +394,15 @@ class BaseModelPair(ABC):
             sync_point()
         # the reference's hook-based splices leave every LL parameter on the autograd
         # graph (zero gradients for dead paths); the native engine skips dead compute,
-        # so give untouched parameters an explicit zero gradient (Adam still steps them).
-        for p in self._ll_module().parameters():
-            if p.requires_grad and p.grad is None:
+        # so give untouched parameters an explicit zero gradient (Adam still steps them).  Arena parameters keep
+        # ``None``: the fused optimizer zeroes every missing slot in one multi-tensor launch when it binds the
+        # arena (FlatParams.rebind_grads) instead of a fill here plus a copy into the arena there per parameter.
+        module = self._ll_module()
+        flat = getattr(module, "_flat_params", None)
+        if flat is not None and not getattr(flat, "zeroes_missing_on_step", False):
+            flat = None
+        for p in module.parameters():
+            if p.requires_grad and p.grad is None and not (flat is not None and flat.owns(p)):
                 p.grad = torch.zeros_like(p)
 
     def clip_grad_fn(self, optimizer=None):

@@ -30,7 +30,7 @@ from typing import List, Optional, Union
 import torch
 from torch import nn
 
-from ..engine.plan import RunPlan, scale_site as _scale_site, zero_grad_site as _zero_grad_site
+from ..engine.plan import RunPlan, Splice, scale_site as _scale_site, zero_grad_site as _zero_grad_site
 from ..hooks.hook_points import HookedRootModule, HookPoint
 from ..ops import select_ops
 from ..ops.torch_ops import TorchOps
@@ -441,20 +441,30 @@ class TransformerBlock(nn.Module):
         zname = attn.hook_z.name
         zs = sites.get(zname)
         causal = self.cfg.attention_dir == "causal"
+        S, H, dh = p.full.shape[1], self.cfg.n_heads, self.cfg.d_head
+        mirror = ops.pair_heads_ok(S, dh) and H <= 64
         if zs is not None and any(ix.is_everything() for ix in zs):
             # the base z is the source z: the base attention is dead, compute the source rows only
             with torch.no_grad():
                 x = ops.layer_norm(p.src, self.ln1.w, self.ln1.b, self.ln1.eps)
                 q, k, v = ops.qkv(x, attn.W_Q, attn.W_K, attn.W_V, attn.b_Q, attn.b_K, attn.b_V)
-                z_src = ops.attention(q, k, v, causal, attn.attn_scale)
-            zf = torch.cat([z_src, z_src])
-            z = _hip_ops().Paired(zf[:z_src.shape[0]], zf)
+                if mirror:  # stored into both halves by the attention kernel itself
+                    zf = ops.attention_dual(q, causal, attn.attn_scale)
+                else:
+                    z_src = ops.attention(q, k, v, causal, attn.attn_scale)
+                    zf = torch.cat([z_src, z_src])
+            z = _hip_ops().Paired(zf[:p.nb], zf)
             resid = p
         else:
             x, resid = ops.pair_layer_norm_fork(p, self.ln1.w, self.ln1.b, self.ln1.eps)
             qkv = ops.pair_qkv(x, attn.W_Q, attn.W_K, attn.W_V, attn.b_Q, attn.b_K, attn.b_V)
-            z = ops.pair_attention(qkv, causal, attn.attn_scale)
-            for ix in zs or ():
+            heads, rest = None, list(zs or ())
+            if mirror and len(rest) == 1:
+                heads = Splice(rest[0], None).head_mask(H)
+                if heads is not None:
+                    rest = []  # head splice inside the attention kernel
+            z = ops.pair_attention(qkv, causal, attn.attn_scale, heads=heads)
+            for ix in rest:
                 z = ops.pair_splice(z, ix)
         if zs is not None:
             captures[zname] = z.src

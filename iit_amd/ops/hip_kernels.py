@@ -40,6 +40,8 @@ _SIGS = {
     "iit_attn_small_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
     "iit_attn_mfma_fwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float, c_int,
                                            c_void_p],
+    "iit_attn_mfma_fwd_pair": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float,
+                                                c_int, c_void_p, c_int, c_ull, c_void_p],
     "iit_attn_mfma_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
     "iit_ce_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "iit_ce_bwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_long, c_int, c_int, c_int,
@@ -322,6 +324,24 @@ def attn_small_fwd(qkv, z, lse, zsrc, head_mask, B, S, H, dh, ld_qkv, ld_z, ld_s
         return
     _check(lib().iit_attn_small_fwd(_p(qkv), _p(z), _p(lse), _p(zsrc), head_mask, B, S, H, dh, ld_qkv, ld_z, ld_src,
                                     scale, int(causal), _stream()), "attn_small_fwd")
+
+
+def attn_pair_ok(S, dh) -> bool:
+    """Whether the paired-row options (dual store, mirrored heads) of the MFMA attention kernel apply."""
+    return _mfma_attn(S, dh)
+
+
+def attn_pair_fwd(qkv, z, lse, B, S, H, dh, ld_qkv, ld_z, scale, causal, z2=None, pair_seqs=0, pair_mask=0):
+    """MFMA short-sequence attention with ``z2`` (a second copy of z) and / or paired rows: the first ``pair_seqs``
+    of the ``B`` sequences are base rows whose heads in ``pair_mask`` take the z of the sequence ``pair_seqs`` later
+    (computed once, stored twice; see csrc/attn_mfma.hip)."""
+    if not _mfma_attn(S, dh):
+        raise RuntimeError("attn_pair_fwd needs the MFMA short-sequence kernel (S <= 16, dh in 32/64/96/128)")
+    if CHECK_BOUNDS:
+        _bounds("attn_pair_fwd", ("qkv", qkv, B * S, 3 * H * dh, ld_qkv), ("z", z, B * S, H * dh, ld_z),
+                ("z2", z2, B * S, H * dh, ld_z), ("lse", lse, 1, B * H * S, B * H * S))
+    _check(lib().iit_attn_mfma_fwd_pair(_p(qkv), _p(z), _p(lse), None, 0, B, S, H, dh, ld_qkv, ld_z, 0, scale,
+                                        int(causal), _p(z2), pair_seqs, pair_mask, _stream()), "attn_mfma_fwd_pair")
 
 
 def attn_small_bwd(qkv, dz, lse, dqkv, head_mask, B, S, H, dh, ld_qkv, ld_dz, scale, causal):

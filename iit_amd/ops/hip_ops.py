@@ -1057,23 +1057,30 @@ class QKVPairFn(QKVFn):
 
 
 class AttnPairFn(AttnFn):
+    """Paired attention; heads in ``mask`` (an interchange splice of those heads of ``hook_z``) are computed once, by
+    the source rows, and stored into the base rows too -- the base rows of those heads carry no gradient."""
+
     @staticmethod
-    def forward(ctx, qkv, causal, scale, qkv_full, box):
+    def forward(ctx, qkv, causal, scale, mask, qkv_full, box):
         ctx.set_materialize_grads(False)
         B = qkv.shape[0]
         B2, S, _, H, dh = qkv_full.shape
         z = torch.empty(B2, S, H, dh, dtype=BF16, device=qkv.device)
         lse = torch.empty(B2 * H * S, dtype=F32, device=qkv.device)
-        K.attn_small_fwd(qkv_full, z, lse, None, 0, B2, S, H, dh, 3 * H * dh, H * dh, H * dh, scale, causal)
+        if mask:
+            K.attn_pair_fwd(qkv_full, z, lse, B2, S, H, dh, 3 * H * dh, H * dh, scale, causal, pair_seqs=B,
+                            pair_mask=mask)
+        else:
+            K.attn_small_fwd(qkv_full, z, lse, None, 0, B2, S, H, dh, 3 * H * dh, H * dh, H * dh, scale, causal)
         ctx.save_for_backward(qkv_full[:B], lse[:B * H * S])  # lse rows are (batch, head)-major
-        ctx.cfg = (0, causal, scale)
+        ctx.cfg = (mask, causal, scale)
         box.append(z)
         return z[:B]
 
     @staticmethod
     def backward(ctx, dz):
         g = AttnFn.backward(ctx, dz)
-        return (g[0], None, None, None, None)
+        return (g[0], None, None, None, None, None)
 
 
 class LinearPairFn(LinearFn):
@@ -1363,9 +1370,24 @@ class HipOps(TorchOps):
                          b_V, p.full)
         return Paired(out, full)
 
-    def pair_attention(self, p: Paired, causal: bool, attn_scale: float) -> Paired:
-        out, full = _one(AttnPairFn, p.base, causal, 1.0 / attn_scale, p.full)
+    def pair_attention(self, p: Paired, causal: bool, attn_scale: float, heads: Optional[Sequence[int]] = None
+                       ) -> Paired:
+        """Attention over paired rows; ``heads``: the base rows of these heads take the source rows' z."""
+        out, full = _one(AttnPairFn, p.base, causal, 1.0 / attn_scale, K.heads_to_mask(heads) if heads else 0,
+                         p.full)
         return Paired(out, full)
+
+    def attention_dual(self, q, causal: bool, attn_scale: float) -> torch.Tensor:
+        """No-grad attention of the packed qkv behind ``q`` (``qkv`` output) into BOTH halves of a [2B, S, H, dh]
+        tensor: the z of a whole-layer ``hook_z`` splice, whose base rows are the source rows."""
+        packed = q._iit_packed
+        B, S, _, H, dh = packed.shape
+        zf = torch.empty(2 * B, S, H, dh, dtype=BF16, device=packed.device)
+        K.attn_pair_fwd(packed, zf[B:], None, B, S, H, dh, 3 * H * dh, H * dh, 1.0 / attn_scale, causal, z2=zf[:B])
+        return zf
+
+    def pair_heads_ok(self, S: int, dh: int) -> bool:
+        return K.attn_pair_ok(S, dh)
 
     def pair_o_proj_residual(self, z: Paired, W_O, b_O, resid: Paired) -> Paired:
         B2, S, H, dh = z.full.shape

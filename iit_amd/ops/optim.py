@@ -37,6 +37,7 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(flat.params, defaults)
         self.flat = flat
         # (the sharded subclass allocates shard-sized moments itself: no transient arena-sized pair)
+        flat.zeroes_missing_on_step = True  # step() zeroes None-gradient slots (one launch, rebind_grads)
         self.exp_avg = torch.zeros_like(flat.data) if alloc_moments else None
         self.exp_avg_sq = torch.zeros_like(flat.data) if alloc_moments else None
         self.step_count = 0

@@ -33,6 +33,7 @@ SITES = [
     {"blocks.1.attn.hook_z": [Ix[:, [3, 7]]]},                                # position list
     {"blocks.1.attn.hook_z": [Ix[:, -1, :2, :]]},                             # causal graph: last position, heads
     {"blocks.2.mlp.hook_post": [Ix[2:5]]},                                    # batch subset: (base | source) axis
+    {"blocks.2.attn.hook_z": [Ix[:, :, [0, 3]]]},                             # two heads (mirrored in-kernel)
 ]
 
 
