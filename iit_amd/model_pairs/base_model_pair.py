@@ -158,6 +158,21 @@ class BaseModelPair(ABC):
         out = model.run_with_hooks(x, fwd_hooks=[(n.name, self.make_ll_ablation_hook(n)) for n in ll_nodes])
         return out[:, -1] if logits == "last" and out.dim() == 3 else out
 
+    def ll_intervention(self, base_x: Tensor, ablation_x: Tensor, ll_nodes: Iterable[LLNode]) -> Tensor:
+        """The LL side of an interchange intervention: the source run's activations at ``ll_nodes`` (kept in
+        ``self.ll_cache``) spliced into the base run -- one paired forward when the native engine covers it, else
+        the truncated source capture followed by the spliced forward."""
+        with trace_range("ll_paired_fwd"):
+            ll_output = self.ll_paired_intervention(base_x, ablation_x, ll_nodes)
+        if ll_output is None:
+            with trace_range("ll_source_cache"):
+                self.ll_cache = self.ll_source_cache(ablation_x, ll_nodes)
+            sync_point()
+            with trace_range("ll_spliced_fwd"):
+                ll_output = self.ll_intervened_forward(base_x, ll_nodes)
+        sync_point()
+        return ll_output
+
     def ll_paired_intervention(self, base_x: Tensor, ablation_x: Tensor, ll_nodes: Iterable[LLNode],
                                logits: Optional[str] = None):
         """``ll_source_cache`` + ``ll_intervened_forward`` as ONE paired forward of source and base rows
@@ -204,20 +219,10 @@ class BaseModelPair(ABC):
         hl_kw = self.hl_run_kwargs()
         with trace_range("hl_source_cache"):
             hl_ablation_output, self.hl_cache = self.hl_model.run_with_cache(ablation_input, **hl_kw)
-        ll_nodes = _ll_nodes_of(self.corr, hl_node)
-        with trace_range("ll_paired_fwd"):
-            ll_output = self.ll_paired_intervention(base_x, ablation_x, ll_nodes)
-        if ll_output is None:
-            with trace_range("ll_source_cache"):
-                self.ll_cache = self.ll_source_cache(ablation_x, ll_nodes)
-        sync_point()
         with trace_range("hl_intervened_fwd"):
             hl_output = self.hl_model.run_with_hooks(
                 base_input, fwd_hooks=[(hl_node.name, self.make_hl_ablation_hook(hl_node))], **hl_kw)
-        if ll_output is None:
-            with trace_range("ll_spliced_fwd"):
-                ll_output = self.ll_intervened_forward(base_x, ll_nodes)
-        sync_point()
+        ll_output = self.ll_intervention(base_x, ablation_x, _ll_nodes_of(self.corr, hl_node))
         if verbose:
             print(f"{hl_node=}, {ll_nodes=}\n{hl_output=}")
         return hl_output, ll_output

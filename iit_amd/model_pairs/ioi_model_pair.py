@@ -22,6 +22,7 @@ from torch import Tensor
 from ..config import DEVICE
 from ..core import index as index_mod
 from ..core.metric import MetricStore, MetricStoreCollection, MetricType, PerTokenMetricStore
+from .base_model_pair import _ll_nodes_of
 from .strict_iit_model_pair import StrictIITModelPair
 
 
@@ -96,17 +97,49 @@ class IOI_ModelPair(StrictIITModelPair):
     def _hl_label(hl_output: Tensor) -> Tensor:
         return torch.argmax(hl_output[:, -1] if hl_output.dim() == 3 else hl_output, dim=-1)
 
+    def fast_hl_label(self, base_x: Tensor, ablation_x: Tensor, hl_node):
+        """The intervened IOI HL label ``argmax(hl_out[:, -1])`` in one kernel launch (csrc/ioi_hl.hip) instead of
+        two HL forwards and a [B, V] argmax; None when not applicable (another HL model, live hooks on it, CPU
+        tensors, ``training_args["fast_hl"] = False``)."""
+        from ..tasks.ioi.ioi_hl import IOI_HL
+        hl = self.hl_model
+        if not (self.native() and self.training_args.get("fast_hl", True) and type(hl) is IOI_HL
+                and base_x.is_cuda and base_x.dtype == torch.long and ablation_x.dtype == torch.long):
+            return None
+        from ..ops import hip_kernels as K
+        node = K.IOI_HL_NODES.get(hl_node.name)
+        if node is None or not (hl_node.index is None or hl_node.index.is_everything()):
+            return None
+        if base_x.dim() != 2 or base_x.shape != ablation_x.shape or base_x.shape[1] > 64:
+            return None
+        if any(hp.is_live for hp in hl.hook_dict.values()):
+            return None
+        nm = hl.name_mover_head
+        table = nm.name_table
+        if table.device != base_x.device:
+            table = nm.name_table = table.to(base_x.device)
+        out = torch.empty(base_x.shape[0], dtype=torch.long, device=base_x.device)
+        K.ioi_hl_label(base_x.contiguous(), ablation_x.contiguous(), table, nm.d_vocab_out, node, out)
+        return out
+
+    def _label_and_ll(self, base_input, ablation_input, hl_node):
+        """(IIT label [B], LL output) of one interchange intervention."""
+        label = self.fast_hl_label(base_input[0], ablation_input[0], hl_node)
+        if label is None:
+            hl_output, ll_output = self.do_intervention(base_input, ablation_input, hl_node)
+            return self._hl_label(hl_output), ll_output
+        return label, self.ll_intervention(base_input[0], ablation_input[0], _ll_nodes_of(self.corr, hl_node))
+
     def get_IIT_loss_over_batch(self, base_input, ablation_input, hl_node, loss_fn):
-        hl_output, ll_output = self.do_intervention(base_input, ablation_input, hl_node)
+        hl_label, ll_output = self._label_and_ll(base_input, ablation_input, hl_node)
         ll_last = ll_output[:, -1] if ll_output.dim() == 3 else ll_output
-        return loss_fn(ll_last, self._hl_label(hl_output))
+        return loss_fn(ll_last, hl_label)
 
     # ------------------------------------------------------------------ eval
     def run_eval_step(self, base_input, ablation_input, loss_fn):
         hl_node = self.sample_hl_name()
-        hl_output, ll_output = self.do_intervention(base_input, ablation_input, hl_node)
+        hl_label, ll_output = self._label_and_ll(base_input, ablation_input, hl_node)
         ll_last = ll_output[:, -1] if ll_output.dim() == 3 else ll_output
-        hl_label = self._hl_label(hl_output)
         loss = loss_fn(ll_last, hl_label)
         iia = (torch.argmax(ll_last, dim=-1) == hl_label).float().mean()
         base_x, base_y = base_input[0], base_input[1]

@@ -19,7 +19,7 @@ CSRC = os.path.join(ROOT, "csrc")
 OUT_DIR = os.path.join(ROOT, "iit_amd", "_native")
 LIB = os.path.join(OUT_DIR, "libiit_hip.so")
 SOURCES = ["gemm.hip", "gemm_glds.hip", "kernels.hip", "attn_mfma.hip", "flash_attn.hip", "llama_ops.hip",
-           "splice.hip"]
+           "splice.hip", "ioi_hl.hip"]
 # per-source compiler flags: the pipelined LDS-DMA GEMM keeps its accumulators in VGPRs (MFMA VGPR form), which
 # avoids the AGPR shuffles hipcc otherwise emits around its register double buffer
 EXTRA_FLAGS = {"gemm_glds.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}

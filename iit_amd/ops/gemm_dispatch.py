@@ -153,6 +153,25 @@ def _addmm_f32(c, base, a, b) -> None:
         torch.add(base, _mm_f32(a, b), out=c)
 
 
+def wgrad_into(c, x2, g2, store: bool) -> None:
+    """Weight gradient ``c (+)= x2^T @ g2`` (x2 [T, K_in], g2 [T, N] bf16; c [K_in, N] fp32, unit column stride):
+    ``store`` writes it (beta = 0, a lazily-zeroed slot), else accumulates.  On the GPU the dispatcher measures the
+    LDS-DMA kernel's fp32-store / -accumulate epilogues (and its deterministic reduction split) against hipBLASLt
+    per shape -- on the Llama-3-8B weight gradients the repo's kernel wins (profiles/llama3_8b_gemm_study_r3.txt)."""
+    T, Kin = x2.shape
+    N = g2.shape[1]
+    ok = (c.is_cuda and x2.dtype == BF16 and g2.dtype == BF16 and c.dtype == F32 and x2.stride(1) == 1
+          and g2.stride(1) == 1 and c.stride(-1) == 1 and c.dim() == 2 and POLICY in ("auto", "glds"))
+    if ok:
+        gemm(x2, g2, c, M=Kin, N=N, K=T, lda=x2.stride(0), ldb=g2.stride(0), ldc=c.stride(0),
+             mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+        return
+    if store:
+        _mm_f32_into(c, x2.t(), g2)
+    else:
+        _addmm_f32(c, c, x2.t(), g2)
+
+
 def _gelu_into(pre, out, erf: bool = False) -> None:
     if pre.is_cuda and pre.dtype == BF16 and out.dtype == BF16 and pre.dim() == 2:
         K.gelu_fwd(pre, out, pre.shape[0], pre.shape[1], erf=erf)

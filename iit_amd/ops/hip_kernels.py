@@ -70,6 +70,7 @@ _SIGS = {
     "iit_flash_bwd": [c_void_p] * 3 + [c_void_p] * 11 + [c_ull] + [c_int] * 5 + [c_float, c_int, c_void_p],
     "iit_splice": [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_splice_spec_size": [],
+    "iit_ioi_hl_label": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
 
@@ -536,3 +537,14 @@ def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_
                                _p(spans), nspans, _p(part), nparts, float(clip_norm or 0.0), lr, b1, b2, eps, wd,
                                _p(hyper), _p(step_dev), _p(skipped), _stream()), "adam_flat")
     flat.after_step(mirror_written=flat.shadow is not None)
+
+
+IOI_HL_NODES = {"all_nodes_hook": 0, "hook_duplicate": 1, "hook_s_inhibition": 2, "hook_name_mover": 3}
+
+
+def ioi_hl_label(base, src, name_table, V: int, node: int, out):
+    """Intervened IOI HL label per sequence (csrc/ioi_hl.hip): ``base`` / ``src`` int64 [B, S] tokens, ``node`` the
+    interchanged HL node (IOI_HL_NODES), ``out`` int64 [B]."""
+    B, S = base.shape
+    _check(lib().iit_ioi_hl_label(_p(base), _p(src), _p(name_table), name_table.numel(), B, S, V, node, _p(out),
+                                  _stream()), "ioi_hl_label")

@@ -131,7 +131,6 @@ class _MirrorLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         from ..engine import grad_hooks
-        from .gemm_dispatch import _addmm_f32
         (x2,) = ctx.saved_tensors
         W, b, flat = ctx.W, ctx.b, ctx.flat
         g2 = gy.reshape(-1, gy.shape[-1]).to(x2.dtype)
@@ -139,14 +138,14 @@ class _MirrorLinear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = (g2 @ flat.shadow_view(W).t()).view(*ctx.lead, W.shape[0])
         if W.requires_grad:
-            from .gemm_dispatch import _mm_f32_into
+            from .gemm_dispatch import wgrad_into
             if flat.claim(W):  # lazily-zeroed slot: store (beta = 0)
-                _mm_f32_into(W.grad, x2.t(), g2)
+                wgrad_into(W.grad, x2, g2, store=True)
             else:
                 slot = W.grad
                 if slot is None:
                     slot = W.grad = torch.zeros_like(W)
-                _addmm_f32(slot, slot, x2.t(), g2)
+                wgrad_into(slot, x2, g2, store=False)
             grad_hooks.notify(W)
         if b is not None and b.requires_grad:
             if b.grad is None:
@@ -178,19 +177,16 @@ class _MirrorMat(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         from ..engine import grad_hooks
-        from .gemm_dispatch import _addmm_f32
         (x2,) = ctx.saved_tensors
         g2 = gy.reshape(-1, gy.shape[-1]).to(x2.dtype)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = (g2 @ ctx.wm.t()).view(*ctx.lead, ctx.wm.shape[0])
         if ctx.gw is not None:
+            from .gemm_dispatch import wgrad_into
             flat = ctx.wparams[0]._iit_flat
-            if flat.claim(*ctx.wparams):  # lazily-zeroed slot: store (beta = 0)
-                from .gemm_dispatch import _mm_f32_into
-                _mm_f32_into(ctx.gw, x2.t(), g2)
-            else:
-                _addmm_f32(ctx.gw, ctx.gw, x2.t(), g2)
+            # a claimed (lazily-zeroed) slot is stored (beta = 0), else accumulated
+            wgrad_into(ctx.gw, x2, g2, store=flat.claim(*ctx.wparams))
         if ctx.gb is not None:
             for b in ctx.bparams:
                 if b.grad is None:
