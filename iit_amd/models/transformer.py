@@ -711,8 +711,6 @@ class HookedTransformer(HookedRootModule):
             return None
         if tokens.dim() != 2 or tokens.shape != src_tokens.shape or tokens.shape[1] > 16 or tokens.shape[1] < 1:
             return None
-        if torch.is_grad_enabled() and self.__dict__.get("_grad_cuts"):
-            return None
         if any(hp.is_live for hp in self.hook_dict.values()):
             return None
         B, S = tokens.shape
@@ -744,8 +742,16 @@ class HookedTransformer(HookedRootModule):
         captures = {}
         resid = ops.pair_embed_pos(tokens, src_tokens, self.embed.W_E, self.pos_embed.W_pos)
         paired = True
+        cuts = self.__dict__.get("_grad_cuts") if torch.is_grad_enabled() else None
         for li, block in enumerate(self.blocks):
             lo = last_only and li == n - 1
+            base = resid.base if paired else resid
+            if cuts and li in cuts and base.requires_grad:
+                # staged backward (engine.staged): the backward stops here and resumes as its own segment; the
+                # source rows carry no autograd state, so only the base rows are cut
+                leaf = base.detach().requires_grad_(True)
+                self._cut_log.append((li, base, leaf))
+                resid = _hip_ops().Paired(leaf, resid.full) if paired else leaf
             if paired:
                 resid, paired = block.forward_paired(resid, run, sites, deepest[2], captures, last_only=lo)
             else:

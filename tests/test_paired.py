@@ -137,3 +137,39 @@ def test_ioi_pair_step_paired_equals_unpaired():
                 assert abs(a[k] - b[k]) <= 2e-2 * max(1.0, abs(a[k])), (k, a[k], b[k])
     finally:
         hip_ops.HipOps.pair_embed_pos = orig
+
+
+def test_paired_with_staged_backward_cuts():
+    """The data-parallel schedule cuts the residual stream at block boundaries (engine.staged): the paired forward
+    cuts its base rows there, and the staged backward reproduces the uncut gradients."""
+    from iit_amd.engine.staged import StagedBackward
+    m = _model()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    base = torch.randint(0, V, (B, S), device="cuda", generator=g)
+    src = torch.randint(0, V, (B, S), device="cuda", generator=g)
+    w = torch.randn(B, V, device="cuda", generator=g)
+    sites = {"blocks.2.attn.hook_z": [Ix[:, :, 1]], "blocks.0.mlp.hook_post": [Ix[[None]]]}
+
+    def grads():
+        return {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+
+    m.zero_grad(set_to_none=True)
+    out, _ = m.run_paired(base, src, sites, logits="last")
+    (out.float() * w).sum().backward()
+    ref = grads()
+    st = StagedBackward(m, 4)
+    m.zero_grad(set_to_none=True)
+    st.arm()
+    try:
+        out, _ = m.run_paired(base, src, sites, logits="last")
+        assert m._cut_log, "no cut was taken"
+        (out.float() * w).sum().backward()
+        for k in st.stages():
+            st.run_stage(k)
+    finally:
+        st.release()
+        st.disarm()
+    got = grads()
+    assert set(got) == set(ref)
+    for k in ref:
+        assert torch.allclose(got[k], ref[k], rtol=1e-3, atol=1e-5), k
