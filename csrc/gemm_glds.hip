@@ -664,22 +664,27 @@ hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
     case 29: return launch<64, 96, 2, AKM, BKM, EPI, 4, 64, 3>(a, s);
     case 30: return launch<64, 64, 2, AKM, BKM, EPI, 4, 64, 4>(a, s);
     case 31: return launch<64, 128, 2, AKM, BKM, EPI, 4, 64, 3>(a, s);
+    // the in-flight-depth test on the big 8-wave tiles: 3-deep rings (2 K-tiles in flight while one is consumed,
+    // tile 5 / 7 keep one) within 160 KiB, and the 256 x 256 two-stage tile
+    case 32: return launch<256, 128, 3, AKM, BKM, EPI, 8>(a, s);
+    case 33: return launch<128, 256, 3, AKM, BKM, EPI, 8>(a, s);
+    case 34: return launch<256, 256, 2, AKM, BKM, EPI, 8>(a, s);
     default: return launch<128, 128, 4, AKM, BKM, EPI>(a, s);
   }
 }
 
 }  // namespace
 
-#define IIT_GLDS_TILES 32
+#define IIT_GLDS_TILES 35
 static const int kTileBM[IIT_GLDS_TILES] = {128, 128, 64, 64, 128, 256, 128, 256, 96, 128, 96, 192, 96, 128, 64,
                                             128, 96, 64, 128, 192, 192, 192, 128, 128, 64, 128, 96, 128, 64,
-                                            64, 64, 64};
+                                            64, 64, 64, 256, 128, 256};
 static const int kTileBN[IIT_GLDS_TILES] = {128, 64, 128, 64, 128, 192, 128, 128, 96, 96, 192, 96, 96, 96, 64,
                                             96, 96, 64, 128, 192, 192, 128, 192, 96, 96, 128, 96, 192, 192,
-                                            96, 64, 128};
+                                            96, 64, 128, 128, 256, 256};
 static const int kTileBK[IIT_GLDS_TILES] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64,
                                             128, 128, 128, 128, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64,
-                                            64, 64, 64};
+                                            64, 64, 64, 64, 64, 64};
 
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,

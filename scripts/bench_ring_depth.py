@@ -36,6 +36,22 @@ CASES_R3 = [  # round 3: two co-resident workgroups per CU (tiles 23-28) against
     ("dW W_O [768][768] store", 768, 768, T, 3, K.EPI_F32_STORE, [(3, 2, True), (8, 4, True), (26, 4, True),
                                                                    (24, 4, True), (23, 4, True)]),
 ]
+CASES_R3B = [  # round 3: in-flight depth on the big 8-wave tiles (tiles 32-34 vs 5 / 7)
+    ("fwd QKV [4096][2304] bf16", T, 2304, 768, 2, K.EPI_BF16, [(5, 1, False), (7, 1, False), (32, 1, False),
+                                                                 (34, 1, False)]),
+    ("fwd W_in [4096][3072] gelu", T, 3072, 768, 2, K.EPI_GELU, [(5, 1, False), (7, 1, False), (32, 1, False),
+                                                                  (33, 1, False), (34, 1, False)]),
+    ("fwd QKV [8192][2304] bf16", 2 * T, 2304, 768, 2, K.EPI_BF16, [(5, 1, False), (7, 1, False), (32, 1, False),
+                                                                     (34, 1, False)]),
+    ("fwd W_in [8192][3072] gelu", 2 * T, 3072, 768, 2, K.EPI_GELU, [(5, 1, False), (7, 1, False), (32, 1, False),
+                                                                      (33, 1, False), (34, 1, False)]),
+    ("fwd W_out [8192][768] resid", 2 * T, 768, 3072, 2, K.EPI_F32_RESID, [(7, 1, False), (32, 1, False),
+                                                                            (9, 1, False)]),
+    ("dX W_out [4096][3072] dgelu", T, 3072, 768, 0, K.EPI_DGELU, [(5, 1, False), (7, 1, False), (32, 1, False),
+                                                                    (33, 1, False), (34, 1, False)]),
+    ("dW W_in [768][3072] store", 768, 3072, T, 3, K.EPI_F32_STORE, [(10, 2, True), (7, 1, False), (32, 1, False),
+                                                                      (33, 1, False), (33, 2, True)]),
+]
 CASES = [  # name, M, N, K, mode, epi, [(tile, splits, reduce), ...]
     ("dW W_in [768][3072] store", 768, 3072, T, 3, K.EPI_F32_STORE, [(8, 1, False), (12, 1, False), (16, 1, False), (10, 2, True)]),
     ("dW W_O [768][768] store", 768, 768, T, 3, K.EPI_F32_STORE, [(3, 2, True), (14, 2, True), (17, 2, True), (3, 1, False),
@@ -50,7 +66,8 @@ CASES = [  # name, M, N, K, mode, epi, [(tile, splits, reduce), ...]
 
 def main():
     dev = "cuda"
-    for name, M, N, Kd, mode, epi, variants in (CASES_R3 if os.environ.get("R3", "1") == "1" else CASES):
+    which = os.environ.get("R3", "1")
+    for name, M, N, Kd, mode, epi, variants in (CASES_R3B if which == "b" else CASES_R3 if which == "1" else CASES):
         torch.manual_seed(0)
         A = (torch.randn(Kd, M) if mode & 1 else torch.randn(M, Kd)).to(dev).bfloat16()
         B = (torch.randn(Kd, N) if mode & 2 else torch.randn(N, Kd)).to(dev).bfloat16() / 16
