@@ -58,7 +58,15 @@ struct G2Args {
   // epilogue store flavour of the output tiles: 0 plain, 1 non-temporal (streamed past the caches), 2 write-through
   // (sc1: written to memory and dropped from the XCD's L2, so the kernel boundary has no dirty lines to write back)
   int store_mode;
+  // timeline probe (nullable, diagnostic builds of the bench only): wave 0 of every workgroup records the shader
+  // clock at the kernel's phases into prof[wg * 64 + e] -- e 0 start, 1 first K-tile landed, 2.. each later K-tile
+  // landed, 61 main loop done, 62 epilogue stores drained; the 100 MHz wall clock at 63 (start) and 60 (end)
+  long long* prof;
 };
+
+__device__ __forceinline__ void prof_mark(long long* prof, int slot, int e, bool on) {
+  if (on) prof[(long)slot * 64 + e] = clock64();
+}
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4_t;
@@ -320,6 +328,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_glds_kernel(G2Args p) {
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = blockIdx.y * p.k_per_split;
   const int nt = p.k_per_split / BK;
+  const bool prof_on = p.prof != nullptr && tid == 0;
+  const int prof_slot = blockIdx.y * gridDim.x + blockIdx.x;
+  if (prof_on) {
+    p.prof[(long)prof_slot * 64 + 63] = wall_clock64();
+    prof_mark(p.prof, prof_slot, 0, true);
+  }
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -349,6 +363,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_glds_kernel(G2Args p) {
     }
   wait_tiles<LOADS>(min(NS - 1, nt - 1));
   __builtin_amdgcn_s_barrier();
+  prof_mark(p.prof, prof_slot, 1, prof_on);
 #pragma unroll
   for (int i = 0; i < TM; ++i) frag_issue_t<AKM, BM, BK>(smem, wm * WM + i * 16, 0, lane, ca[i]);
 #pragma unroll
@@ -391,6 +406,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_glds_kernel(G2Args p) {
     } else if (kt + 1 < nt) {
       wait_tiles<LOADS>(min(NS - 2, nt - 2 - kt));
       __builtin_amdgcn_s_barrier();
+      if (kt + 2 < 61) prof_mark(p.prof, prof_slot, kt + 2, prof_on);
       if (kt + NS < nt) {
         char* buf = smem + (kt % NS) * STAGE;
         stA.stage(kt + NS, buf);
@@ -417,6 +433,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_glds_kernel(G2Args p) {
     __builtin_amdgcn_sched_barrier(0);
     }  // half
   }
+  prof_mark(p.prof, prof_slot, 61, prof_on);
   if constexpr (EPI == E_F32_ACC || EPI == E_F32_STORE) {
     if (p.ws != nullptr) {
       // Partial tile in MFMA register order (one 16-B chunk per lane per accumulator: 1 KiB coalesced per wave),
@@ -604,6 +621,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_glds_kernel(G2Args p) {
     }
   }
   }  // chunk
+  if (p.prof != nullptr) {  // drain this workgroup's stores, then stamp (diagnostic path only)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    prof_mark(p.prof, prof_slot, 62, prof_on);
+    if (prof_on) p.prof[(long)prof_slot * 64 + 60] = wall_clock64();
+  }
 }
 
 template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW = 4, int BK = 64, int OCC = 1>
@@ -718,6 +741,11 @@ IIT_EXPORT int iit_gemm_glds_sm(const void* A, const void* B, void* C, void* C2,
                                 long ldc2, long ldr, int M, int N, int K, int mode, int epi, int bias_cols, int tile,
                                 int splits, float* csum, float* ws, int* counters, int store_mode, void* stream);
 
+// the timeline probe of the NEXT iit_gemm_glds* launch from this host thread (scripts/gemm_timeline.py): a
+// [workgroups][64] int64 device buffer, consumed by that launch
+static thread_local long long* g_prof_buf = nullptr;
+IIT_EXPORT void iit_gemm_glds_set_prof(void* buf) { g_prof_buf = (long long*)buf; }
+
 IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, const float* bias0, const float* bias1,
                              const float* bias2, const float* resid, long lda, long ldb, long ldc, long ldc2, long ldr,
                              int M, int N, int K, int mode, int epi, int bias_cols, int tile, int splits,
@@ -745,6 +773,8 @@ IIT_EXPORT int iit_gemm_glds_sm(const void* A, const void* B, void* C, void* C2,
   a.ws = reduce ? ws : nullptr;  // workspace >= splits * M * N floats, counters >= tiles ints (zero when idle)
   a.counters = reduce ? counters : nullptr;
   a.store_mode = store_mode;
+  a.prof = g_prof_buf;
+  g_prof_buf = nullptr;
   hipStream_t s = (hipStream_t)stream;
 #define G2(MODE, AK, BK_, EPI) \
   if (mode == (MODE) && epi == (EPI)) return (int)launch_tile<AK, BK_, EPI>(a, tile, s);

@@ -70,6 +70,7 @@ _SIGS = {
     "iit_flash_bwd": [c_void_p] * 3 + [c_void_p] * 11 + [c_ull] + [c_int] * 5 + [c_float, c_int, c_void_p],
     "iit_splice": [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_splice_spec_size": [],
+    "iit_gemm_glds_set_prof": [c_void_p],
     "iit_ioi_hl_label": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
@@ -549,3 +550,9 @@ def ioi_hl_label(base, src, name_table, V: int, node: int, out):
     B, S = base.shape
     _check(lib().iit_ioi_hl_label(_p(base), _p(src), _p(name_table), name_table.numel(), B, S, V, node, _p(out),
                                   _stream()), "ioi_hl_label")
+
+
+def gemm_glds_set_prof(buf) -> None:
+    """Arm the LDS-DMA GEMM's timeline probe for the next ``gemm_glds`` launch on this thread: ``buf`` int64
+    [workgroups * 64] on the device (scripts/gemm_timeline.py)."""
+    lib().iit_gemm_glds_set_prof(_p(buf))
