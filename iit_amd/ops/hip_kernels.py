@@ -71,6 +71,7 @@ _SIGS = {
     "iit_splice": [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_splice_spec_size": [],
     "iit_gemm_glds_set_prof": [c_void_p],
+    "iit_gemm_glds_set_group_m": [c_int],
     "iit_ioi_hl_label": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
@@ -556,3 +557,8 @@ def gemm_glds_set_prof(buf) -> None:
     """Arm the LDS-DMA GEMM's timeline probe for the next ``gemm_glds`` launch on this thread: ``buf`` int64
     [workgroups * 64] on the device (scripts/gemm_timeline.py)."""
     lib().iit_gemm_glds_set_prof(_p(buf))
+
+
+def gemm_glds_set_group_m(gm: int) -> None:
+    """M-tiles per group of the LDS-DMA GEMM's XCD-local tile order for later launches (0 = default 8)."""
+    lib().iit_gemm_glds_set_group_m(int(gm))

@@ -52,6 +52,14 @@ CASES_R3B = [  # round 3: in-flight depth on the big 8-wave tiles (tiles 32-34 v
     ("dW W_in [768][3072] store", 768, 3072, T, 3, K.EPI_F32_STORE, [(10, 2, True), (7, 1, False), (32, 1, False),
                                                                       (33, 1, False), (33, 2, True)]),
 ]
+CASES_GM = [  # round 3: XCD-local tile-order group height (IIT_GM_SWEEP), shipped tiles
+    ("fwd QKV [4096][2304] bf16", T, 2304, 768, 2, K.EPI_BF16, [(5, 1, False)]),
+    ("fwd W_in [4096][3072] gelu", T, 3072, 768, 2, K.EPI_GELU, [(5, 1, False)]),
+    ("fwd W_out [4096][768] resid", T, 768, 3072, 2, K.EPI_F32_RESID, [(9, 1, False), (24, 1, False)]),
+    ("dX W_in [4096][768] bf16", T, 768, 3072, 0, K.EPI_BF16, [(9, 1, False)]),
+    ("fwd QKV [8192][2304] bf16", 2 * T, 2304, 768, 2, K.EPI_BF16, [(5, 1, False)]),
+    ("dW W_in [768][3072] store", 768, 3072, T, 3, K.EPI_F32_STORE, [(8, 1, False), (10, 2, True)]),
+]
 CASES = [  # name, M, N, K, mode, epi, [(tile, splits, reduce), ...]
     ("dW W_in [768][3072] store", 768, 3072, T, 3, K.EPI_F32_STORE, [(8, 1, False), (12, 1, False), (16, 1, False), (10, 2, True)]),
     ("dW W_O [768][768] store", 768, 768, T, 3, K.EPI_F32_STORE, [(3, 2, True), (14, 2, True), (17, 2, True), (3, 1, False),
@@ -67,7 +75,8 @@ CASES = [  # name, M, N, K, mode, epi, [(tile, splits, reduce), ...]
 def main():
     dev = "cuda"
     which = os.environ.get("R3", "1")
-    for name, M, N, Kd, mode, epi, variants in (CASES_R3B if which == "b" else CASES_R3 if which == "1" else CASES):
+    cases = CASES_R3B if which == "b" else CASES_GM if which == "gm" else CASES_R3 if which == "1" else CASES
+    for name, M, N, Kd, mode, epi, variants in cases:
         torch.manual_seed(0)
         A = (torch.randn(Kd, M) if mode & 1 else torch.randn(M, Kd)).to(dev).bfloat16()
         B = (torch.randn(Kd, N) if mode & 2 else torch.randn(N, Kd)).to(dev).bfloat16() / 16
@@ -82,9 +91,12 @@ def main():
             ex = dict(C2=torch.randn(M, N, device=dev).bfloat16(), ldc2=N)
         ref = None
         out = []
-        for tile, sp, red in variants:
+        gms = [int(g) for g in os.environ.get("IIT_GM_SWEEP", "0").split(",")]
+        variants = [(t, sp, red, gm) for t, sp, red in variants for gm in gms]
+        for tile, sp, red, gm in variants:
+            K.gemm_glds_set_group_m(gm)
             if not K.gemm_glds_ok(A, B, C, tile=tile, splits=sp, reduce=red, **kw, **ex):
-                out.append(f"t{tile}{'r' if red else 'k'}{sp}: n/a")
+                out.append(f"t{tile}{'r' if red else 'k'}{sp}g{gm}: n/a")
                 continue
             f = lambda: K.gemm_glds(A, B, C, tile=tile, splits=sp, reduce=red, **kw, **ex)  # noqa: E731
             f()
@@ -93,7 +105,8 @@ def main():
             err = float(((C.float() - ref.float()).norm() / ref.float().norm()))
             us = min(gd._time(f, reps=20) for _ in range(3))
             tf = 2 * M * N * Kd / (us * 1e-6) / 1e12
-            out.append(f"t{tile}{'r' if red else 'k'}{sp}: {us:6.1f} us {tf:5.0f} TF/s (rel diff {err:.1e})")
+            out.append(f"t{tile}{'r' if red else 'k'}{sp}{f'g{gm}' if gm else ''}: {us:6.1f} us {tf:5.0f} TF/s "
+                       f"(rel diff {err:.1e})")
         print(f"{name:28s} " + " | ".join(out), flush=True)
 
 
