@@ -62,7 +62,7 @@ struct G2Args {
   // clock at the kernel's phases into prof[wg * 64 + e] -- e 0 start, 1 first K-tile landed, 2.. each later K-tile
   // landed, 61 main loop done, 62 epilogue stores drained; the 100 MHz wall clock at 63 (start) and 60 (end)
   long long* prof;
-  int group_m;  // M-tiles per column group of the XCD-local tile order (0 = 1, or 8 for K-split launches)
+  int group_m;  // M-tiles per column group of the XCD-local tile order (0 = 8)
 };
 
 __device__ __forceinline__ void prof_mark(long long* prof, int slot, int e, bool on) {
@@ -236,8 +236,8 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 // Tile order inside an XCD's contiguous range: column-major groups of up to GM M-tiles.  GM = 1 is the plain
 // row-major order (an XCD runs whole rows of output tiles: each A row panel lives in one XCD's L2, the B column
-// panels in all of them); larger GM makes each XCD's concurrent tiles a compact block that shares both.  Measured:
-// GM = 1 for single-pass launches, 8 for K-split ones (see the call site).
+// panels in all of them); larger GM makes each XCD's concurrent tiles a compact block that shares both (see the
+// call site for the measured choice).
 __device__ __forceinline__ void grouped_tile(int t, int tiles_m, int tiles_n, int& tm, int& tn, int GM = 8) {
   const int per_group = GM * tiles_n;
   const int first_m = (t / per_group) * GM;
@@ -325,10 +325,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void gemm_glds_kernel(G2Args p) {
   const int tiles_n = p.N / BN;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   int tm, tn;
-  // XCD-local order: whole rows of output tiles per XCD (group height 1) -- each A panel (the activation rows) is
-  // fetched into ONE XCD's L2 and the small weight panels into every XCD; 3-8 % faster than 8-high column groups
-  // on every single-pass shape (profiles/gemm_tile_order_r3.txt).  K-split launches keep 8-high groups.
-  grouped_tile(t, p.M / BM, tiles_n, tm, tn, p.group_m > 0 ? p.group_m : (gridDim.y > 1 ? 8 : 1));
+  // XCD-local order, 8-high column groups.  Whole rows of output tiles per XCD (group height 1: each activation
+  // panel in ONE XCD's L2) are 3-8 % faster in isolation on every single-pass shape but 0.03-0.08 ms/step slower
+  // inside the training step, same box (profiles/gemm_tile_order_r3.txt); ``group_m`` (IIT_GEMM_GROUP_M) overrides.
+  grouped_tile(t, p.M / BM, tiles_n, tm, tn, p.group_m > 0 ? p.group_m : 8);
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = blockIdx.y * p.k_per_split;
   const int nt = p.k_per_split / BK;

@@ -88,6 +88,9 @@ def lib():
             fn.argtypes = argtypes
             fn.restype = c_int
         _LIB = L
+        gm = os.environ.get("IIT_GEMM_GROUP_M")  # XCD-local tile-order group height of the LDS-DMA GEMM (experiment)
+        if gm:
+            L.iit_gemm_glds_set_group_m(int(gm))
     return _LIB
 
 
