@@ -1,0 +1,133 @@
+// Two GEMM problems in ONE launch: a layer's weight gradient dW = X^T dY (mode 3, fp32 store / accumulate, optional
+// K-split) and its input gradient dX = dY W^T (mode 0, bf16 or the fused dgelu epilogue).  The two are independent,
+// and each alone is about one round of tiles on the 256 CUs: run back to back, every launch pays its own ramp,
+// pipeline fill, epilogue drain and tail (profiles/gemm_timeline_r3.txt: 5-13 us of a 20-37 us GEMM), and HIP graph
+// branches on side streams do not overlap them (profiles/graph_branch_concurrency_r3.txt).  Here the workgroups of
+// both problems share one grid, two per CU (4 waves, <= 80 KiB LDS each), so one problem's prologue / epilogue runs
+// under the other's main loop and the launch has one tail instead of two.
+//
+// The per-tile code is gemm_glds_body (csrc/gemm_glds_body.h), unchanged: workgroups [0, w_tiles * w_splits) take
+// the dW tiles (split-major, so the K-splits of a tile are a launch round apart and its reduction ticket is taken
+// late), the rest the dX tiles.  The dW problem comes first because its K (the token count) is the longer loop.
+#include "gemm_glds_body.h"
+
+namespace {
+
+template <int BM_, int BN_, int NS_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, NS = NS_;
+  static constexpr int SMEM = GldsSmem<BM_, BN_, NS_, 4, 64, 2>::BYTES;
+};
+
+template <class TW, int EW, class TX, int EX>
+__global__ __launch_bounds__(256, 2) void gemm_dual_kernel(G2Args pw, G2Args px, int w_tiles, int w_splits,
+                                                           int x_tiles) {
+  __shared__ __attribute__((aligned(16))) char smem[TW::SMEM > TX::SMEM ? TW::SMEM : TX::SMEM];  // ONE LDS object
+  const int b = blockIdx.x;
+  const int nw = w_tiles * w_splits;
+  if (b < nw) {
+    gemm_glds_body<TW::BM, TW::BN, TW::NS, true, true, EW, 4, 64, 2>(pw, b % w_tiles, w_tiles, b / w_tiles, w_splits,
+                                                                      smem);
+  } else {
+    gemm_glds_body<TX::BM, TX::BN, TX::NS, false, false, EX, 4, 64, 2>(px, b - nw, x_tiles, 0, 1, smem);
+  }
+}
+
+// dW tiles (index -> the single-launch tile id of the same shape, for the shape checks): 128x96, 128x128, 96x96,
+// 64x96, 64x64; dX tiles: 128x96, 64x96, 128x192, 128x128
+constexpr int kWTiles = 5, kXTiles = 4;
+const int kWTileId[kWTiles] = {23, 25, 26, 24, 3};
+const int kXTileId[kXTiles] = {23, 24, 27, 25};
+const int kWBM[kWTiles] = {128, 128, 96, 64, 64}, kWBN[kWTiles] = {96, 128, 96, 96, 64};
+const int kXBM[kXTiles] = {128, 64, 128, 128}, kXBN[kXTiles] = {96, 96, 192, 128};
+
+template <class TW, int EW, class TX, int EX>
+hipError_t launch2(const G2Args& w, const G2Args& x, int w_splits, hipStream_t s) {
+  const int wt = (w.M / TW::BM) * (w.N / TW::BN), xt = (x.M / TX::BM) * (x.N / TX::BN);
+  hipLaunchKernelGGL((gemm_dual_kernel<TW, EW, TX, EX>), dim3(wt * w_splits + xt), dim3(256), 0, s, w, x, wt,
+                     w_splits, xt);
+  return hipGetLastError();
+}
+
+template <class TW, int EW, int EX>
+hipError_t pick_x(const G2Args& w, const G2Args& x, int w_splits, int xtile, hipStream_t s) {
+  switch (xtile) {
+    case 0: return launch2<TW, EW, Cfg<128, 96, 2>, EX>(w, x, w_splits, s);
+    case 1: return launch2<TW, EW, Cfg<64, 96, 3>, EX>(w, x, w_splits, s);
+    case 2: return launch2<TW, EW, Cfg<128, 192, 2>, EX>(w, x, w_splits, s);
+    case 3: return launch2<TW, EW, Cfg<128, 128, 2>, EX>(w, x, w_splits, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int EW, int EX>
+hipError_t pick_w(const G2Args& w, const G2Args& x, int w_splits, int wtile, int xtile, hipStream_t s) {
+  switch (wtile) {
+    case 0: return pick_x<Cfg<128, 96, 2>, EW, EX>(w, x, w_splits, xtile, s);
+    case 1: return pick_x<Cfg<128, 128, 2>, EW, EX>(w, x, w_splits, xtile, s);
+    case 2: return pick_x<Cfg<96, 96, 3>, EW, EX>(w, x, w_splits, xtile, s);
+    case 3: return pick_x<Cfg<64, 96, 3>, EW, EX>(w, x, w_splits, xtile, s);
+    case 4: return pick_x<Cfg<64, 64, 4>, EW, EX>(w, x, w_splits, xtile, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+extern "C" int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,
+                                long lda, long ldb, long ldc, long ldc2, long ldr, int M, int N, int K, int mode,
+                                int epi, int bias_cols, int tile, int splits, int reduce);
+
+IIT_EXPORT int iit_gemm_dual_tiles(int* w_tiles, int* x_tiles) {
+  *w_tiles = kWTiles;
+  *x_tiles = kXTiles;
+  return 0;
+}
+
+// 1 when the pair (dW problem on dual tile ``wtile`` with ``wsplits`` K-splits -- reduction split when ``reduce`` --,
+// dX problem on dual tile ``xtile``) is covered by the dual kernel
+IIT_EXPORT int iit_gemm_dual_ok(const void* wA, const void* wB, const void* wC, long wlda, long wldb, long wldc, int wM,
+                                int wN, int wK, int wepi, int wtile, int wsplits, int reduce, const void* xA,
+                                const void* xB, const void* xC, const void* xC2, long xlda, long xldb, long xldc,
+                                long xldc2, int xM, int xN, int xK, int xepi, int xtile) {
+  if (wtile < 0 || wtile >= kWTiles || xtile < 0 || xtile >= kXTiles) return 0;
+  if (!(wepi == E_F32_STORE || wepi == E_F32_ACC) || !(xepi == E_BF16 || xepi == E_DGELU)) return 0;
+  if (!iit_gemm_glds_ok(wA, wB, wC, nullptr, nullptr, wlda, wldb, wldc, 0, 0, wM, wN, wK, 3, wepi, 0,
+                        kWTileId[wtile], wsplits, reduce))
+    return 0;
+  if (!iit_gemm_glds_ok(xA, xB, xC, xepi == E_DGELU ? xC2 : nullptr, nullptr, xlda, xldb, xldc, xldc2, 0, xM, xN, xK,
+                        0, xepi, 0, kXTileId[xtile], 1, 0))
+    return 0;
+  // the dW tiles' XCD-local order needs their count to be a multiple of the 8 XCDs only for locality, not for
+  // correctness; the grid must stay within one dimension
+  const long wg = (long)(wM / kWBM[wtile]) * (wN / kWBN[wtile]) * wsplits + (long)(xM / kXBM[xtile]) * (xN / kXBN[xtile]);
+  return wg > 0 && wg < (1L << 31) ? 1 : 0;
+}
+
+IIT_EXPORT int iit_gemm_dual(const void* wA, const void* wB, void* wC, long wlda, long wldb, long wldc, int wM, int wN,
+                             int wK, int wepi, int wtile, int wsplits, float* ws, int* counters, const void* xA,
+                             const void* xB, void* xC, void* xC2, long xlda, long xldb, long xldc, long xldc2, int xM,
+                             int xN, int xK, int xepi, int xtile, float* csum, void* stream) {
+  const int reduce = ws != nullptr;
+  if (!iit_gemm_dual_ok(wA, wB, wC, wlda, wldb, wldc, wM, wN, wK, wepi, wtile, wsplits, reduce, xA, xB, xC, xC2, xlda,
+                        xldb, xldc, xldc2, xM, xN, xK, xepi, xtile))
+    return (int)hipErrorInvalidValue;
+  if (reduce && !counters) return (int)hipErrorInvalidValue;
+  G2Args w{};
+  w.A = (const __bf16*)wA; w.B = (const __bf16*)wB; w.C = wC;
+  w.lda = wlda; w.ldb = wldb; w.ldc = wldc;
+  w.M = wM; w.N = wN; w.K = wK; w.k_per_split = wK / wsplits;
+  w.ws = reduce ? ws : nullptr;
+  w.counters = reduce ? counters : nullptr;
+  G2Args x{};
+  x.A = (const __bf16*)xA; x.B = (const __bf16*)xB; x.C = xC; x.C2 = xC2;
+  x.lda = xlda; x.ldb = xldb; x.ldc = xldc; x.ldc2 = xldc2;
+  x.M = xM; x.N = xN; x.K = xK; x.k_per_split = xK;
+  x.csum = xepi == E_DGELU ? csum : nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  if (wepi == E_F32_STORE && xepi == E_BF16) return (int)pick_w<E_F32_STORE, E_BF16>(w, x, wsplits, wtile, xtile, s);
+  if (wepi == E_F32_STORE && xepi == E_DGELU) return (int)pick_w<E_F32_STORE, E_DGELU>(w, x, wsplits, wtile, xtile, s);
+  if (wepi == E_F32_ACC && xepi == E_BF16) return (int)pick_w<E_F32_ACC, E_BF16>(w, x, wsplits, wtile, xtile, s);
+  if (wepi == E_F32_ACC && xepi == E_DGELU) return (int)pick_w<E_F32_ACC, E_DGELU>(w, x, wsplits, wtile, xtile, s);
+  return (int)hipErrorInvalidValue;
+}

@@ -18,11 +18,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 CSRC = os.path.join(ROOT, "csrc")
 OUT_DIR = os.path.join(ROOT, "iit_amd", "_native")
 LIB = os.path.join(OUT_DIR, "libiit_hip.so")
-SOURCES = ["gemm.hip", "gemm_glds.hip", "kernels.hip", "attn_mfma.hip", "flash_attn.hip", "llama_ops.hip",
+SOURCES = ["gemm.hip", "gemm_glds.hip", "gemm_dual.hip", "kernels.hip", "attn_mfma.hip", "flash_attn.hip", "llama_ops.hip",
            "splice.hip", "ioi_hl.hip"]
 # per-source compiler flags: the pipelined LDS-DMA GEMM keeps its accumulators in VGPRs (MFMA VGPR form), which
 # avoids the AGPR shuffles hipcc otherwise emits around its register double buffer
-EXTRA_FLAGS = {"gemm_glds.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+EXTRA_FLAGS = {"gemm_glds.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "gemm_dual.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+HEADERS = ["common.h", "gemm_glds_body.h"]
 ARCH = os.environ.get("IIT_OFFLOAD_ARCH", "gfx950")
 
 
@@ -39,7 +40,7 @@ def sources():
 
 def source_hash() -> str:
     h = hashlib.sha256()
-    for p in sources() + [os.path.join(CSRC, "common.h")]:
+    for p in sources() + [os.path.join(CSRC, h) for h in HEADERS]:
         with open(p, "rb") as f:
             h.update(f.read())
     h.update(ARCH.encode())

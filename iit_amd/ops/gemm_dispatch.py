@@ -19,7 +19,7 @@ can say which GEMMs ran on hand-written MFMA code.
 from __future__ import annotations
 
 import os
-from typing import Dict, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -521,6 +521,108 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
 
 K_ = K  # the kernel module (``K`` is shadowed by the reduction-size keyword above)
 
+# ------------------------------------------------------------------------------ dX + dW in one launch
+DUAL = os.environ.get("IIT_GEMM_DUAL", "1") != "0"
+DUAL_DECISIONS: Dict[Tuple, Tuple[str, Dict[str, float]]] = {}
+_DUAL_X_EPIS = (K.EPI_BF16, K.EPI_DGELU)
+_DUAL_W_EPIS = (K.EPI_F32_STORE, K.EPI_F32_ACC)
+
+
+def _dual_eligible(x: dict, w: dict) -> bool:
+    return (DUAL and POLICY == "auto" and x["A"].is_cuda and x.get("mode", 0) == 0 and x.get("epi", 0) in _DUAL_X_EPIS
+            and w.get("mode") == (K.MODE_AKM | K.MODE_BKM) and w.get("epi") in _DUAL_W_EPIS
+            and all(x.get(k) is None for k in ("bias0", "resid", "C2", "splits"))
+            and all(w.get(k) is None for k in ("bias0", "resid", "C2", "splits", "aux", "colsum")))
+
+
+def _dual_specs(x: dict, w: dict, xc, wc, csum):
+    ws = dict(A=w["A"], B=w["B"], C=wc, M=w["M"], N=w["N"], K=w["K"], lda=w["lda"], ldb=w["ldb"], ldc=w["ldc"],
+              epi=w["epi"])
+    xs = dict(A=x["A"], B=x["B"], C=xc, C2=x.get("aux"), M=x["M"], N=x["N"], K=x["K"], lda=x["lda"], ldb=x["ldb"],
+              ldc=x["ldc"], ldc2=x.get("ldc2", 0), epi=x["epi"], csum=csum)
+    return ws, xs
+
+
+def _dual_candidates(x: dict, w: dict, xc, wc, csum):
+    """name -> f() for every dual configuration (dW tile, dX tile, dW K-split) that covers the pair."""
+    ws, xs = _dual_specs(x, w, xc, wc, csum)
+    det = deterministic()
+    out = {}
+    for wt in K.DUAL_W_TILES:
+        for xt in K.DUAL_X_TILES:
+            for sp, red in ((1, False), (2, True), (4, True), (2, False), (4, False)):
+                if not red and sp > 1 and (w["epi"] != K.EPI_F32_ACC or det):
+                    continue  # atomic split-K: accumulate only, never in deterministic mode
+                if sp > 1 and w["K"] // sp < 256:
+                    continue
+                if K.gemm_dual_ok(ws, xs, wt, xt, sp, red):
+                    out[f"dual{wt}.{xt}" + (f"{'r' if red else 'k'}{sp}" if sp > 1 else "")] = \
+                        lambda wt=wt, xt=xt, sp=sp, red=red: K.gemm_dual(ws, xs, wt, xt, sp, red)
+    return out
+
+
+def gemm_pair(x: dict, w: dict) -> Optional[str]:
+    """A layer's input gradient ``x`` (mode 0: ``dX = dY W^T``, bf16 or DGELU epilogue) and weight gradient ``w``
+    (mode 3: ``dW (+)= X^T dY``), given as :func:`gemm` keyword dicts.  They are independent, so besides running
+    them one after the other (each on its own best implementation) they can share ONE launch on the dual kernel
+    (``csrc/gemm_dual.hip``): the dispatcher times both options once per problem pair and keeps the faster.
+    ``IIT_GEMM_DUAL=0`` disables the dual launch.  Returns the weight-gradient choice (for ``_settle_claim``)."""
+    def serial():
+        gemm(**x)
+        return gemm(**w)
+
+    if not _dual_eligible(x, w):
+        return serial()
+    fresh = bool(w.get("fresh")) and w["epi"] == K.EPI_F32_STORE
+    key = ("dual", x["M"], x["N"], x["K"], x["epi"], x.get("colsum") is not None,
+           w["M"], w["N"], w["K"], w["epi"], fresh, deterministic())
+    choice = DUAL_DECISIONS.get(key)
+    if choice is None:
+        shipped = _table().get(repr(key))
+        if shipped is not None:
+            choice = DUAL_DECISIONS[key] = (shipped, {shipped: float("nan")})
+    if choice is None:
+        if torch.cuda.is_current_stream_capturing():
+            return serial()
+        # time on scratch outputs (accumulate epilogues and column sums must not touch the real ones)
+        xc = _scratch(x["C"], x["M"], max(x["ldc"], x["N"]))
+        wc = _scratch(w["C"], w["M"], max(w["ldc"], w["N"]))
+        cs = torch.zeros_like(x["colsum"]) if x.get("colsum") is not None else None
+        calls = _dual_candidates(x, w, xc, wc, cs)
+        calls["serial"] = lambda: (gemm(**{**x, "C": xc, "colsum": cs}), gemm(**{**w, "C": wc}))
+        times = {n: min(_time(f) for _ in range(2)) for n, f in calls.items()}
+        for n in sorted(times, key=times.get)[:3] if len(times) > 1 else ():
+            times[n] = min(_time(calls[n], reps=30) for _ in range(3))
+        best = min(times, key=times.get)
+        choice = DUAL_DECISIONS[key] = (best, times)
+    name = FORCE.get(key, choice[0])
+    cfg = _parse_dual(name)
+    ws, xs = _dual_specs(x, w, x["C"], w["C"], x.get("colsum"))
+    if cfg is None or not K.gemm_dual_ok(ws, xs, *cfg):
+        name, cfg = "serial", None
+    s_ev = e_ev = None
+    if TIMING is not None:  # in-context tuning (scripts/tune_gemm_in_situ.py): the pair's span, serial included
+        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s_ev.record()
+    if cfg is None:
+        res = serial()
+    else:
+        K.gemm_dual(ws, xs, *cfg)
+        res = name
+    if TIMING is not None:
+        e_ev.record()
+        TIMING.append((key, name, s_ev, e_ev))
+    return res
+
+
+def _parse_dual(name: str):
+    """``dual{wtile}.{xtile}[r|k]{splits}`` -> (wtile, xtile, splits, reduce)."""
+    import re
+    m = re.fullmatch(r"dual(\d+)\.(\d+)(?:([rk])(\d+))?", name)
+    if m is None:
+        return None
+    return int(m.group(1)), int(m.group(2)), int(m.group(4) or 1), m.group(3) == "r"
+
 # Shipped decision table: the measured choice per problem key from an MI355X run (``export_table``), so a fresh
 # process skips the autotuning of known shapes (the first training epoch / the bench warm-up).  Entries are only
 # used when the named implementation is among the problem's candidates; anything else is measured as before.
@@ -551,6 +653,7 @@ def export_table(path: str) -> int:
     """Write the measured decisions of this process (``DECISIONS``) as a decision table; returns the entry count."""
     import json
     dec = {repr(k): v[0] for k, v in DECISIONS.items()}
+    dec.update({repr(k): v[0] for k, v in DUAL_DECISIONS.items()})
     arch = getattr(torch.cuda.get_device_properties(0), "gcnArchName", "").split(":")[0] \
         if torch.cuda.is_available() else None
     with open(path, "w") as f:
@@ -568,4 +671,7 @@ def report() -> str:
     for (M, N, Kd, mode, epi, bias, fresh, _), (split, whole, pieces) in sorted(RAGGED.items()):
         lines.append(f"M={M:6d} N={N:6d} K={Kd:6d} mode={mode:2d} epi={epi}{'f' if fresh else ''} bias={int(bias)} "
                      f"-> {'bulk+tail' if split else 'whole'}  whole {whole}us  bulk+tail {pieces}us")
+    for key, (c, times) in sorted(DUAL_DECISIONS.items()):
+        ts = "  ".join(f"{k} {v:8.1f}us" for k, v in sorted(times.items(), key=lambda kv: kv[1])[:6])
+        lines.append(f"pair dX {key[1:6]} dW {key[6:11]} -> {c}  {ts}")
     return "\n".join(lines)

@@ -71,6 +71,9 @@ _SIGS = {
     "iit_splice": [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_splice_spec_size": [],
     "iit_gemm_glds_set_prof": [c_void_p],
+    "iit_gemm_dual_ok": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 7 + [c_void_p] * 4 + [c_long] * 4 + [c_int] * 5,
+    "iit_gemm_dual": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 6 + [c_void_p] * 2 + [c_void_p] * 4 + [c_long] * 4
+                     + [c_int] * 5 + [c_void_p] * 2,
     "iit_gemm_glds_set_group_m": [c_int],
     "iit_ioi_hl_label": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
@@ -210,7 +213,7 @@ def gemm_glds_ok(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, resid=N
 _SPLIT_WS = {}  # (device, stream) -> [fp32 partial-tile workspace, int32 tickets, retired buffers]
 
 
-def split_workspace(M: int, N: int, tile: int, splits: int, device) -> tuple:
+def split_workspace(M: int, N: int, tile, splits: int, device) -> tuple:
     """Workspace of the reduction split-K: ``splits * M * N`` fp32 partials and one ticket per output tile.
 
     One buffer pair per (device, stream), shared by every problem launched on that stream (launches on one
@@ -221,7 +224,7 @@ def split_workspace(M: int, N: int, tile: int, splits: int, device) -> tuple:
     stream = torch.cuda.current_stream(device).cuda_stream
     key = (str(device), stream)
     ent = _SPLIT_WS.get(key)
-    bm, bn = GLDS_TILES[tile]
+    bm, bn = GLDS_TILES[tile] if isinstance(tile, int) else tile  # a tile id or its (BM, BN)
     need_ws, need_cnt = splits * M * N, (M // bm) * (N // bn)
     if ent is None:
         ent = _SPLIT_WS[key] = [None, None, []]
@@ -258,6 +261,46 @@ def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None
                                   ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits, _p(csum), _p(ws),
                                   _p(cnt), int(sm), _stream()),
            "iit_gemm_glds")
+
+
+# ------------------------------------------------------------------------------ dual GEMM (csrc/gemm_dual.hip)
+# one launch runs a layer's weight gradient dW = X^T dY (mode 3; fp32 store / accumulate, optional K-split) and its
+# input gradient dX = dY W^T (mode 0; bf16 or the fused dgelu epilogue), two workgroups per CU
+DUAL_W_TILES = {0: (128, 96), 1: (128, 128), 2: (96, 96), 3: (64, 96), 4: (64, 64)}
+DUAL_X_TILES = {0: (128, 96), 1: (64, 96), 2: (128, 192), 3: (128, 128)}
+
+
+def _bf16_cuda(*ts) -> bool:
+    return all(t is not None and t.is_cuda and t.dtype == torch.bfloat16 for t in ts)
+
+
+def gemm_dual_ok(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, reduce: bool = False) -> bool:
+    """Whether :func:`gemm_dual` covers the pair.  ``w``: A (X [T][K_in]), B (dY [T][N]), C (fp32), M, N, K, lda, ldb,
+    ldc, epi (EPI_F32_STORE / EPI_F32_ACC); ``x``: A (dY), B (W [K_in][N] as [N][K]), C (bf16), C2 (the saved
+    pre-activation for EPI_DGELU), M, N, K, lda, ldb, ldc, ldc2, epi (EPI_BF16 / EPI_DGELU)."""
+    if not _bf16_cuda(w["A"], w["B"], x["A"], x["B"]):
+        return False
+    return bool(lib().iit_gemm_dual_ok(
+        _p(w["A"]), _p(w["B"]), _p(w["C"]), w["lda"], w["ldb"], w["ldc"], w["M"], w["N"], w["K"], w["epi"], wtile,
+        splits, int(reduce), _p(x["A"]), _p(x["B"]), _p(x["C"]), _p(x.get("C2")), x["lda"], x["ldb"], x["ldc"],
+        x.get("ldc2", 0), x["M"], x["N"], x["K"], x["epi"], xtile))
+
+
+def gemm_dual(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, reduce: bool = False) -> None:
+    """Both problems of :func:`gemm_dual_ok` in one launch (``x["csum"]``: the DGELU column sums, optional)."""
+    ws = cnt = None
+    if reduce:
+        ws, cnt = split_workspace(w["M"], w["N"], DUAL_W_TILES[wtile], splits, w["A"].device)
+    if CHECK_BOUNDS:
+        _gemm_bounds("iit_gemm_dual(dW)", w["A"], w["B"], w["C"], None, None, w["M"], w["N"], w["K"], w["lda"],
+                     w["ldb"], w["ldc"], 0, 0, MODE_AKM | MODE_BKM)
+        _gemm_bounds("iit_gemm_dual(dX)", x["A"], x["B"], x["C"], x.get("C2"), None, x["M"], x["N"], x["K"],
+                     x["lda"], x["ldb"], x["ldc"], x.get("ldc2", 0), 0, MODE_NN)
+        _bounds("iit_gemm_dual", ("csum", x.get("csum"), 1, x["N"], x["N"]))
+    _check(lib().iit_gemm_dual(
+        _p(w["A"]), _p(w["B"]), _p(w["C"]), w["lda"], w["ldb"], w["ldc"], w["M"], w["N"], w["K"], w["epi"], wtile,
+        splits, _p(ws), _p(cnt), _p(x["A"]), _p(x["B"]), _p(x["C"]), _p(x.get("C2")), x["lda"], x["ldb"], x["ldc"],
+        x.get("ldc2", 0), x["M"], x["N"], x["K"], x["epi"], xtile, _p(x.get("csum")), _stream()), "iit_gemm_dual")
 
 
 def sumsq_spans(g, spans, nspans, part, step_dev, do_norm: bool):

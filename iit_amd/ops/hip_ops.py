@@ -32,7 +32,7 @@ from torch.autograd import Function
 
 from ..engine import grad_hooks
 from . import hip_kernels as K
-from .gemm_dispatch import gemm
+from .gemm_dispatch import gemm, gemm_pair
 from .torch_ops import TorchOps, act_fn
 
 BF16 = torch.bfloat16
@@ -492,21 +492,23 @@ class QKVFn(Function):
         T = B * S
         g = dqkv.to(BF16).contiguous().view(T, 3 * HD)
         dx = torch.empty(T, d, dtype=BF16, device=g.device)
-        gemm(g, ctx.layer["qkv"], dx, M=T, N=d, K=3 * HD, lda=3 * HD, ldb=3 * HD, ldc=d, epi=K.EPI_BF16)
+        xspec = dict(A=g, B=ctx.layer["qkv"], C=dx, M=T, N=d, K=3 * HD, lda=3 * HD, ldb=3 * HD, ldc=d, epi=K.EPI_BF16)
         store = W_Q.stride() == (dh, 3 * HD, 1) and _packed3(W_Q, W_K, W_V, HD) and \
             _claim_store(W_Q, W_K, W_V)
         if store:
             gq, gk, gv = W_Q.grad, W_K.grad, W_V.grad
         else:
             gq, gk, gv = _grad_slot(W_Q), _grad_slot(W_K), _grad_slot(W_V)
-        if gq is not None and gk is not None and gv is not None:
-            if gq.stride() == (dh, 3 * HD, 1) and _packed3(gq, gk, gv, HD):
-                choice = gemm(x2, g, gq, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=3 * HD,
-                              mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC,
-                              fresh=store)
-                if store:
-                    _settle_claim(choice, W_Q, W_K, W_V)
-            else:
+        if gq is not None and gk is not None and gv is not None and gq.stride() == (dh, 3 * HD, 1) and \
+                _packed3(gq, gk, gv, HD):
+            choice = gemm_pair(xspec, dict(A=x2, B=g, C=gq, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=3 * HD,
+                                           mode=K.MODE_AKM | K.MODE_BKM,
+                                           epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store))
+            if store:
+                _settle_claim(choice, W_Q, W_K, W_V)
+        else:
+            gemm(**xspec)
+            if gq is not None and gk is not None and gv is not None:
                 gemm(x2, g, gq, C2=gk, C3=gv, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=0,
                      mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_ACC_QKV, qkv=(dh, H, d))
         gbs = [_grad_slot(bp) for bp in (b_Q, b_K, b_V)]
@@ -763,30 +765,34 @@ class LinearFn(Function):
         g16 = _bf16_of(gy)
         g2 = _aligned_rows(g16, T, N)
         ldg = g2.stride(0)
-        dx = None
+        dx = xspec = dxb = None
         if ctx.needs_input_grad[0]:
             amode = K.MODE_NN
             _, splits = K._tiling(T, Kd, N, True)
-            if splits == 1:
+            if splits == 1:  # run below, paired with the weight gradient when it has one
                 dxb = torch.empty(T, Kd, dtype=BF16, device=g2.device)
-                gemm(g2, ctx.w, dxb, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ldw, ldc=Kd, mode=amode, epi=K.EPI_BF16)
-                dx = dxb if x_dtype == BF16 else dxb.to(x_dtype)
+                xspec = dict(A=g2, B=ctx.w, C=dxb, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ldw, ldc=Kd, mode=amode,
+                             epi=K.EPI_BF16)
             else:  # long reduction (unembed: K = vocab) -> split-K into fp32
                 dxf = torch.zeros(T, Kd, dtype=F32, device=g2.device)
                 gemm(g2, ctx.w, dxf, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ldw, ldc=Kd, mode=amode, epi=K.EPI_F32_ACC,
                      splits=splits)
-                dx = dxf.to(x_dtype)
-            dx = dx.view(*lead, Kd)
+                dx = dxf.to(x_dtype).view(*lead, Kd)
         store = _claim_store(W)
         gW = W.grad if store else _grad_slot(W)
         if gW is not None:
             mode = K.MODE_AKM | K.MODE_BKM
             gW2 = gW.reshape(Kd, N) if gW.is_contiguous() else gW
             assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
-            choice = gemm(x2, g2, gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode,
-                          epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+            wspec = dict(A=x2, B=g2, C=gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode,
+                         epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+            choice = gemm_pair(xspec, wspec) if xspec is not None else gemm(**wspec)
             if store:
                 _settle_claim(choice, W)
+        elif xspec is not None:
+            gemm(**xspec)
+        if dxb is not None:
+            dx = (dxb if x_dtype == BF16 else dxb.to(x_dtype)).view(*lead, Kd)
         gb = _grad_slot(b)
         if gb is not None:
             _BIAS_SUMS.add(g2, ldg, gb, T, N, b)
@@ -832,14 +838,17 @@ class MLPInFn(Function):
         else:
             dpre = gpre.to(BF16).contiguous().view(T, dm)
         dx = torch.empty(T, d, dtype=BF16, device=x2.device)
-        gemm(dpre, ctx.w, dx, M=T, N=d, K=dm, lda=dm, ldb=dm, ldc=d, epi=K.EPI_BF16)
+        xspec = dict(A=dpre, B=ctx.w, C=dx, M=T, N=d, K=dm, lda=dm, ldb=dm, ldc=d, epi=K.EPI_BF16)
         store = W_in.is_contiguous() and _claim_store(W_in)
         gW = W_in.grad if store else _grad_slot(W_in)
         if gW is not None:
-            choice = gemm(x2, dpre, gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm, mode=K.MODE_AKM | K.MODE_BKM,
-                          epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+            choice = gemm_pair(xspec, dict(A=x2, B=dpre, C=gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm,
+                                           mode=K.MODE_AKM | K.MODE_BKM,
+                                           epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store))
             if store:
                 _settle_claim(choice, W_in)
+        else:
+            gemm(**xspec)
         gb = _grad_slot(b_in)
         if gb is not None and not _bias_sum_done(gpre if gpost is None else None, b_in):
             _BIAS_SUMS.add(dpre, dm, gb, T, dm, b_in)
@@ -897,24 +906,28 @@ class MLPOutGeluFn(Function):
         g16 = _bf16_of(gy)
         g2 = _aligned_rows(g16, T, N)
         ldg = g2.stride(0)
-        dpre = None
+        dpre = xspec = gbi = None
         if ctx.needs_input_grad[0]:
             dpre = torch.empty(T, Kd, dtype=BF16, device=g2.device)
             gbi = _grad_slot(b_in)
-            gemm(g2, ctx.w, dpre, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ldw, ldc=Kd, mode=K.MODE_NN,
-                 epi=K.EPI_DGELU_ERF if ctx.erf else K.EPI_DGELU, aux=pre2, ldc2=pre2.stride(0), colsum=gbi)
-            dpre = dpre.view(*lead, Kd)
-            if gbi is not None:
-                dpre._iit_bias_sum = (dpre.data_ptr(), dpre._version, id(b_in))
+            xspec = dict(A=g2, B=ctx.w, C=dpre, M=T, N=Kd, K=N, lda=ldg, ldb=ctx.ldw, ldc=Kd, mode=K.MODE_NN,
+                         epi=K.EPI_DGELU_ERF if ctx.erf else K.EPI_DGELU, aux=pre2, ldc2=pre2.stride(0), colsum=gbi)
         store = _claim_store(W)
         gW = W.grad if store else _grad_slot(W)
         if gW is not None:
             gW2 = gW.reshape(Kd, N) if gW.is_contiguous() else gW
             assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
-            choice = gemm(x2, g2, gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0),
-                          mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+            wspec = dict(A=x2, B=g2, C=gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0),
+                         mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+            choice = gemm_pair(xspec, wspec) if xspec is not None else gemm(**wspec)
             if store:
                 _settle_claim(choice, W)
+        elif xspec is not None:
+            gemm(**xspec)
+        if dpre is not None:
+            dpre = dpre.view(*lead, Kd)
+            if gbi is not None:
+                dpre._iit_bias_sum = (dpre.data_ptr(), dpre._version, id(b_in))
         gb = _grad_slot(b)
         if gb is not None:
             _BIAS_SUMS.add(g2, ldg, gb, T, N, b)

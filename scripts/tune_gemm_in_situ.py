@@ -52,7 +52,8 @@ def main():
     del pair.sample_hl_name, pair.sample_ll_node
 
     cands = {}
-    for key, (choice, times) in gd.DECISIONS.items():
+    decisions = {**gd.DECISIONS, **gd.DUAL_DECISIONS}  # single GEMMs and dX + dW pairs (dual launch or serial)
+    for key, (choice, times) in decisions.items():
         finite = {k: v for k, v in times.items() if v == v}
         if len(finite) < 2 or min(finite.values()) < a.min_us:
             continue
@@ -87,11 +88,12 @@ def main():
         if not med:
             continue
         best = min(med, key=med.get)
-        iso = gd.DECISIONS[key][1]
-        gd.DECISIONS[key] = (best, iso)
+        store = gd.DUAL_DECISIONS if key in gd.DUAL_DECISIONS else gd.DECISIONS
+        iso = store[key][1]
+        store[key] = (best, iso)
         lines.append(f"{key}: in-context " + "  ".join(f"{c} {med[c]:.1f}us(iso {iso[c]:.1f})" for c in med)
                      + f"  -> {best}")
-    for key, (choice, _) in gd.DECISIONS.items():
+    for key, (choice, _) in {**gd.DECISIONS, **gd.DUAL_DECISIONS}.items():
         table[repr(key)] = choice
     arch = torch.cuda.get_device_properties(0).gcnArchName.split(":")[0]
     with open(a.out, "w") as f:

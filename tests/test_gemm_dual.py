@@ -1,0 +1,99 @@
+"""Dual GEMM launch (csrc/gemm_dual.hip): a layer's dW = X^T dY and dX = dY W^T in one launch vs fp32 PyTorch,
+for every (dW tile, dX tile) pair, both epilogues of each side, and the dW K-splits (reduction / atomic)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+T, KIN, NOUT = 512, 384, 384
+
+
+@pytest.fixture(scope="module")
+def K():
+    from iit_amd.ops import hip_kernels
+    hip_kernels.lib()
+    return hip_kernels
+
+
+def _problem(seed):
+    torch.manual_seed(seed)
+    x = torch.randn(T, KIN, device=dev).bfloat16()
+    dy = (torch.randn(T, NOUT, device=dev) / 4).bfloat16()
+    w = (torch.randn(KIN, NOUT, device=dev) / 8).bfloat16()
+    pre = torch.randn(T, KIN, device=dev).bfloat16()
+    return x, dy, w, pre
+
+
+VARIANTS = [  # (dW epilogue, dX epilogue, splits, reduce)
+    ("store", "bf16", 1, False),
+    ("store", "dgelu", 2, True),
+    ("acc", "bf16", 4, True),
+    ("acc", "dgelu", 2, False),
+]
+
+
+@pytest.mark.parametrize("wt", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("xt", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", VARIANTS, ids=lambda v: f"{v[0]}-{v[1]}-{'r' if v[3] else 'k'}{v[2]}")
+def test_dual_matches_fp32(K, wt, xt, variant):
+    from iit_amd.ops.torch_ops import gelu_new
+    wepi_s, xepi_s, splits, reduce = variant
+    x, dy, w, pre = _problem(wt * 10 + xt)
+    wepi = K.EPI_F32_STORE if wepi_s == "store" else K.EPI_F32_ACC
+    xepi = K.EPI_BF16 if xepi_s == "bf16" else K.EPI_DGELU
+    gW0 = torch.randn(KIN, NOUT, device=dev)
+    gW = gW0.clone()
+    dX = torch.zeros(T, KIN, device=dev, dtype=torch.bfloat16)
+    csum = torch.randn(KIN, device=dev) if xepi == K.EPI_DGELU else None
+    csum0 = csum.clone() if csum is not None else None
+    ws = dict(A=x, B=dy, C=gW, M=KIN, N=NOUT, K=T, lda=KIN, ldb=NOUT, ldc=NOUT, epi=wepi)
+    xs = dict(A=dy, B=w, C=dX, C2=pre if xepi == K.EPI_DGELU else None, M=T, N=KIN, K=NOUT, lda=NOUT, ldb=NOUT,
+              ldc=KIN, ldc2=KIN, epi=xepi, csum=csum)
+    assert K.gemm_dual_ok(ws, xs, wt, xt, splits, reduce)
+    for rep in range(2):  # a second launch reuses the reduction tickets the first one re-armed
+        gW.copy_(gW0)
+        if csum is not None:
+            csum.copy_(csum0)
+        K.gemm_dual(ws, xs, wt, xt, splits, reduce)
+        torch.cuda.synchronize()
+        ref_w = x.float().t() @ dy.float() + (gW0 if wepi == K.EPI_F32_ACC else 0)
+        torch.testing.assert_close(gW, ref_w, rtol=1e-4, atol=2e-3)
+        ref_x = dy.float() @ w.float().t()
+        if xepi == K.EPI_DGELU:
+            p = pre.float().requires_grad_(True)
+            gp, = torch.autograd.grad(gelu_new(p).sum(), p)
+            ref_x = (ref_x * gp).bfloat16().float()
+            torch.testing.assert_close(csum, csum0 + dX.float().sum(0), rtol=1e-4, atol=1e-2)
+        torch.testing.assert_close(dX.float(), ref_x, rtol=2e-2, atol=2e-2)
+
+
+def test_dual_rejects_misfit(K):
+    x, dy, w, pre = _problem(0)
+    gW = torch.zeros(KIN, NOUT, device=dev)
+    dX = torch.zeros(T, KIN, device=dev, dtype=torch.bfloat16)
+    ws = dict(A=x, B=dy, C=gW, M=KIN, N=NOUT, K=T, lda=KIN, ldb=NOUT, ldc=NOUT, epi=K.EPI_F32_STORE)
+    xs = dict(A=dy, B=w, C=dX, M=T, N=KIN - 8, K=NOUT, lda=NOUT, ldb=NOUT, ldc=KIN, epi=K.EPI_BF16)
+    assert not K.gemm_dual_ok(ws, xs, 0, 0)  # N not a multiple of the dX tile
+    xs["N"] = KIN
+    assert not K.gemm_dual_ok(ws, xs, 0, 0, 2, False)  # atomic split of a store epilogue
+    assert K.gemm_dual_ok(ws, xs, 0, 0, 2, True)
+
+
+def test_gemm_pair_dispatch_matches_serial(K):
+    """The dispatcher's pair path (whatever it picks) gives the serial results, and both layer backwards agree."""
+    from iit_amd.ops import gemm_dispatch as gd
+    x, dy, w, pre = _problem(7)
+    outs = []
+    for dual in (False, True):
+        gd.DUAL = dual
+        gW = torch.empty(KIN, NOUT, device=dev)
+        dX = torch.empty(T, KIN, device=dev, dtype=torch.bfloat16)
+        xs = dict(A=dy, B=w, C=dX, M=T, N=KIN, K=NOUT, lda=NOUT, ldb=NOUT, ldc=KIN, epi=K.EPI_BF16)
+        wspec = dict(A=x, B=dy, C=gW, M=KIN, N=NOUT, K=T, lda=KIN, ldb=NOUT, ldc=NOUT, mode=K.MODE_AKM | K.MODE_BKM,
+                     epi=K.EPI_F32_STORE, fresh=True)
+        gd.gemm_pair(xs, wspec)
+        torch.cuda.synchronize()
+        outs.append((gW.clone(), dX.clone()))
+    gd.DUAL = True
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(outs[0][1].float(), outs[1][1].float(), rtol=1e-2, atol=1e-2)
