@@ -3,8 +3,9 @@
 // and each alone is about one round of tiles on the 256 CUs: run back to back, every launch pays its own ramp,
 // pipeline fill, epilogue drain and tail (profiles/gemm_timeline_r3.txt: 5-13 us of a 20-37 us GEMM), and HIP graph
 // branches on side streams do not overlap them (profiles/graph_branch_concurrency_r3.txt).  Here the workgroups of
-// both problems share one grid, two per CU (4 waves, <= 80 KiB LDS each), so one problem's prologue / epilogue runs
-// under the other's main loop and the launch has one tail instead of two.
+// both problems share one grid -- two workgroups per CU (4 waves, <= 80 KiB LDS each), so one problem's prologue /
+// epilogue runs under the other's main loop, or one big 8-wave tile per CU -- and the launch has one tail instead of
+// two.
 //
 // The per-tile code is gemm_glds_body (csrc/gemm_glds_body.h), unchanged: workgroups [0, w_tiles * w_splits) take
 // the dW tiles (split-major, so the K-splits of a tile are a launch round apart and its reduction ticket is taken
@@ -13,50 +14,70 @@
 
 namespace {
 
-template <int BM_, int BN_, int NS_>
+// a tile of the dual launch: BM x BN, NS-deep LDS ring, NW waves, OCC workgroups per CU (both problems of one launch
+// share NW and OCC)
+template <int BM_, int BN_, int NS_, int NW_ = 4, int OCC_ = 2>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, NS = NS_;
-  static constexpr int SMEM = GldsSmem<BM_, BN_, NS_, 4, 64, 2>::BYTES;
+  static constexpr int BM = BM_, BN = BN_, NS = NS_, NW = NW_, OCC = OCC_;
+  static constexpr int SMEM = GldsSmem<BM_, BN_, NS_, NW_, 64, OCC_>::BYTES;
 };
 
 template <class TW, int EW, class TX, int EX>
-__global__ __launch_bounds__(256, 2) void gemm_dual_kernel(G2Args pw, G2Args px, int w_tiles, int w_splits,
-                                                           int x_tiles) {
+__global__ __launch_bounds__(TW::NW * 64, TW::OCC) void gemm_dual_kernel(G2Args pw, G2Args px, int w_tiles,
+                                                                         int w_splits, int x_tiles) {
+  static_assert(TW::NW == TX::NW && TW::OCC == TX::OCC, "one launch geometry");
   __shared__ __attribute__((aligned(16))) char smem[TW::SMEM > TX::SMEM ? TW::SMEM : TX::SMEM];  // ONE LDS object
   const int b = blockIdx.x;
   const int nw = w_tiles * w_splits;
   if (b < nw) {
-    gemm_glds_body<TW::BM, TW::BN, TW::NS, true, true, EW, 4, 64, 2>(pw, b % w_tiles, w_tiles, b / w_tiles, w_splits,
-                                                                      smem);
+    gemm_glds_body<TW::BM, TW::BN, TW::NS, true, true, EW, TW::NW, 64, TW::OCC>(pw, b % w_tiles, w_tiles,
+                                                                                b / w_tiles, w_splits, smem);
   } else {
-    gemm_glds_body<TX::BM, TX::BN, TX::NS, false, false, EX, 4, 64, 2>(px, b - nw, x_tiles, 0, 1, smem);
+    gemm_glds_body<TX::BM, TX::BN, TX::NS, false, false, EX, TX::NW, 64, TX::OCC>(px, b - nw, x_tiles, 0, 1, smem);
   }
 }
 
-// dW tiles (index -> the single-launch tile id of the same shape, for the shape checks): 128x96, 128x128, 96x96,
-// 64x96, 64x64; dX tiles: 128x96, 64x96, 128x192, 128x128
-constexpr int kWTiles = 5, kXTiles = 4;
-const int kWTileId[kWTiles] = {23, 25, 26, 24, 3};
-const int kXTileId[kXTiles] = {23, 24, 27, 25};
-const int kWBM[kWTiles] = {128, 128, 96, 64, 64}, kWBN[kWTiles] = {96, 128, 96, 96, 64};
-const int kXBM[kXTiles] = {128, 64, 128, 128}, kXBN[kXTiles] = {96, 96, 192, 128};
+// Two families of tiles (a launch takes both of its tiles from one family):
+// * 4 waves, two workgroups per CU: dW 128x96, 128x128, 96x96, 64x96, 64x64; dX 128x96, 64x96, 128x192, 128x128 --
+//   one problem's prologue / epilogue under the other's main loop on the same CU;
+// * 8 waves (two per SIMD), one workgroup per CU: dW 256x128, 128x128, dX 256x192, 256x128, 128x128 -- the big
+//   tiles that run the
+//   paired forward at ~1 PF/s (fewer operand bytes per flop than 128x128), which alone leave most of the CUs idle on a
+//   [768][N] weight gradient; here the dX tiles fill them.  (A 256x192 dW tile spills registers: not offered.)
+// (index -> the single-launch tile id of the same shape, for the shape checks)
+constexpr int kWTiles = 7, kXTiles = 7;
+const int kWTileId[kWTiles] = {23, 25, 26, 24, 3, 7, 6};
+const int kXTileId[kXTiles] = {23, 24, 27, 25, 5, 7, 6};
+const int kWBM[kWTiles] = {128, 128, 96, 64, 64, 256, 128}, kWBN[kWTiles] = {96, 128, 96, 96, 64, 128, 128};
+const int kXBM[kXTiles] = {128, 64, 128, 128, 256, 256, 128}, kXBN[kXTiles] = {96, 96, 192, 128, 192, 128, 128};
+__host__ __device__ constexpr bool w_big(int t) { return t >= 5; }
+__host__ __device__ constexpr bool x_big(int t) { return t >= 4; }
 
 template <class TW, int EW, class TX, int EX>
 hipError_t launch2(const G2Args& w, const G2Args& x, int w_splits, hipStream_t s) {
   const int wt = (w.M / TW::BM) * (w.N / TW::BN), xt = (x.M / TX::BM) * (x.N / TX::BN);
-  hipLaunchKernelGGL((gemm_dual_kernel<TW, EW, TX, EX>), dim3(wt * w_splits + xt), dim3(256), 0, s, w, x, wt,
-                     w_splits, xt);
+  hipLaunchKernelGGL((gemm_dual_kernel<TW, EW, TX, EX>), dim3(wt * w_splits + xt), dim3(TW::NW * 64), 0, s, w, x,
+                     wt, w_splits, xt);
   return hipGetLastError();
 }
 
 template <class TW, int EW, int EX>
 hipError_t pick_x(const G2Args& w, const G2Args& x, int w_splits, int xtile, hipStream_t s) {
-  switch (xtile) {
-    case 0: return launch2<TW, EW, Cfg<128, 96, 2>, EX>(w, x, w_splits, s);
-    case 1: return launch2<TW, EW, Cfg<64, 96, 3>, EX>(w, x, w_splits, s);
-    case 2: return launch2<TW, EW, Cfg<128, 192, 2>, EX>(w, x, w_splits, s);
-    case 3: return launch2<TW, EW, Cfg<128, 128, 2>, EX>(w, x, w_splits, s);
-    default: return hipErrorInvalidValue;
+  if constexpr (TW::NW == 4) {
+    switch (xtile) {
+      case 0: return launch2<TW, EW, Cfg<128, 96, 2>, EX>(w, x, w_splits, s);
+      case 1: return launch2<TW, EW, Cfg<64, 96, 3>, EX>(w, x, w_splits, s);
+      case 2: return launch2<TW, EW, Cfg<128, 192, 2>, EX>(w, x, w_splits, s);
+      case 3: return launch2<TW, EW, Cfg<128, 128, 2>, EX>(w, x, w_splits, s);
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (xtile) {
+      case 4: return launch2<TW, EW, Cfg<256, 192, 2, 8, 1>, EX>(w, x, w_splits, s);
+      case 5: return launch2<TW, EW, Cfg<256, 128, 2, 8, 1>, EX>(w, x, w_splits, s);
+      case 6: return launch2<TW, EW, Cfg<128, 128, 4, 8, 1>, EX>(w, x, w_splits, s);
+      default: return hipErrorInvalidValue;
+    }
   }
 }
 
@@ -68,6 +89,8 @@ hipError_t pick_w(const G2Args& w, const G2Args& x, int w_splits, int wtile, int
     case 2: return pick_x<Cfg<96, 96, 3>, EW, EX>(w, x, w_splits, xtile, s);
     case 3: return pick_x<Cfg<64, 96, 3>, EW, EX>(w, x, w_splits, xtile, s);
     case 4: return pick_x<Cfg<64, 64, 4>, EW, EX>(w, x, w_splits, xtile, s);
+    case 5: return pick_x<Cfg<256, 128, 2, 8, 1>, EW, EX>(w, x, w_splits, xtile, s);
+    case 6: return pick_x<Cfg<128, 128, 4, 8, 1>, EW, EX>(w, x, w_splits, xtile, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -90,7 +113,7 @@ IIT_EXPORT int iit_gemm_dual_ok(const void* wA, const void* wB, const void* wC, 
                                 int wN, int wK, int wepi, int wtile, int wsplits, int reduce, const void* xA,
                                 const void* xB, const void* xC, const void* xC2, long xlda, long xldb, long xldc,
                                 long xldc2, int xM, int xN, int xK, int xepi, int xtile) {
-  if (wtile < 0 || wtile >= kWTiles || xtile < 0 || xtile >= kXTiles) return 0;
+  if (wtile < 0 || wtile >= kWTiles || xtile < 0 || xtile >= kXTiles || w_big(wtile) != x_big(xtile)) return 0;
   if (!(wepi == E_F32_STORE || wepi == E_F32_ACC) || !(xepi == E_BF16 || xepi == E_DGELU)) return 0;
   if (!iit_gemm_glds_ok(wA, wB, wC, nullptr, nullptr, wlda, wldb, wldc, 0, 0, wM, wN, wK, 3, wepi, 0,
                         kWTileId[wtile], wsplits, reduce))
@@ -107,7 +130,7 @@ IIT_EXPORT int iit_gemm_dual_ok(const void* wA, const void* wB, const void* wC, 
 IIT_EXPORT int iit_gemm_dual(const void* wA, const void* wB, void* wC, long wlda, long wldb, long wldc, int wM, int wN,
                              int wK, int wepi, int wtile, int wsplits, float* ws, int* counters, const void* xA,
                              const void* xB, void* xC, void* xC2, long xlda, long xldb, long xldc, long xldc2, int xM,
-                             int xN, int xK, int xepi, int xtile, float* csum, void* stream) {
+                             int xN, int xK, int xepi, int xtile, float* csum, float* bsum, void* stream) {
   const int reduce = ws != nullptr;
   if (!iit_gemm_dual_ok(wA, wB, wC, wlda, wldb, wldc, wM, wN, wK, wepi, wtile, wsplits, reduce, xA, xB, xC, xC2, xlda,
                         xldb, xldc, xldc2, xM, xN, xK, xepi, xtile))
@@ -119,6 +142,7 @@ IIT_EXPORT int iit_gemm_dual(const void* wA, const void* wB, void* wC, long wlda
   w.M = wM; w.N = wN; w.K = wK; w.k_per_split = wK / wsplits;
   w.ws = reduce ? ws : nullptr;
   w.counters = reduce ? counters : nullptr;
+  w.bsum = bsum;  // the dW problem's column sums of dY (its bias gradient), nullable
   G2Args x{};
   x.A = (const __bf16*)xA; x.B = (const __bf16*)xB; x.C = xC; x.C2 = xC2;
   x.lda = xlda; x.ldb = xldb; x.ldc = xldc; x.ldc2 = xldc2;

@@ -150,7 +150,8 @@ IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, con
 IIT_EXPORT int iit_gemm_glds_sm(const void* A, const void* B, void* C, void* C2, const float* bias0,
                                 const float* bias1, const float* bias2, const float* resid, long lda, long ldb, long ldc,
                                 long ldc2, long ldr, int M, int N, int K, int mode, int epi, int bias_cols, int tile,
-                                int splits, float* csum, float* ws, int* counters, int store_mode, void* stream);
+                                int splits, float* csum, float* ws, int* counters, int store_mode, float* bsum,
+                                void* stream);
 
 // the timeline probe of the NEXT iit_gemm_glds* launch from this host thread (scripts/gemm_timeline.py): a
 // [workgroups][64] int64 device buffer, consumed by that launch
@@ -165,20 +166,22 @@ IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, co
                              int M, int N, int K, int mode, int epi, int bias_cols, int tile, int splits,
                              float* csum, float* ws, int* counters, void* stream) {
   return iit_gemm_glds_sm(A, B, C, C2, bias0, bias1, bias2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi,
-                          bias_cols, tile, splits, csum, ws, counters, 0, stream);
+                          bias_cols, tile, splits, csum, ws, counters, 0, nullptr, stream);
 }
 
-// the same with the epilogue store flavour (G2Args::store_mode)
+// the same with the epilogue store flavour (G2Args::store_mode) and, for the weight gradients (mode 3), the fused
+// column sums of B (``bsum``, += atomically; nullable)
 IIT_EXPORT int iit_gemm_glds_sm(const void* A, const void* B, void* C, void* C2, const float* bias0,
                                 const float* bias1, const float* bias2, const float* resid, long lda, long ldb, long ldc,
                                 long ldc2, long ldr, int M, int N, int K, int mode, int epi, int bias_cols, int tile,
-                                int splits, float* csum, float* ws, int* counters, int store_mode, void* stream) {
+                                int splits, float* csum, float* ws, int* counters, int store_mode, float* bsum,
+                                void* stream) {
   const int reduce = ws != nullptr;
   if (!iit_gemm_glds_ok(A, B, C, C2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits,
                         reduce))
     return (int)hipErrorInvalidValue;
   if (reduce && !counters) return (int)hipErrorInvalidValue;
-  G2Args a;
+  G2Args a{};
   a.A = (const __bf16*)A; a.B = (const __bf16*)B; a.C = C; a.C2 = C2;
   a.bias0 = bias0; a.bias1 = bias1; a.bias2 = bias2; a.resid = resid;
   a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.ldc2 = ldc2; a.ldr = ldr;
@@ -190,6 +193,7 @@ IIT_EXPORT int iit_gemm_glds_sm(const void* A, const void* B, void* C, void* C2,
   a.prof = g_prof_buf;
   g_prof_buf = nullptr;
   a.group_m = g_group_m;
+  a.bsum = mode == 3 ? bsum : nullptr;
   hipStream_t s = (hipStream_t)stream;
 #define G2(MODE, AK, BK_, EPI) \
   if (mode == (MODE) && epi == (EPI)) return (int)launch_tile<AK, BK_, EPI>(a, tile, s);

@@ -35,6 +35,10 @@ struct G2Args {
   // landed, 61 main loop done, 62 epilogue stores drained; the 100 MHz wall clock at 63 (start) and 60 (end)
   long long* prof;
   int group_m;  // M-tiles per column group of the XCD-local tile order (0 = 8)
+  // weight gradients (mode 3, fp32 epilogues): optional column sums of the B operand over the K range (the bias
+  // gradient colsum(dY) of the layer whose dW = X^T dY this is), += atomically by the first M-tile row of tiles
+  // from the B fragments already in registers, so dY is not read a second time
+  float* bsum;
 };
 
 __device__ __forceinline__ void prof_mark(long long* prof, int slot, int e, bool on) {
@@ -324,6 +328,14 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
   }
 
   f32x4 acc[TM][TN];
+  // fused column sums of B (``bsum``): lane l's B fragment holds B[8 (l >> 4) + e][l & 15] of its 16-column block,
+  // so the waves of the first wave row of the first M-tile row add their fragments' 8 values per lane on the VALU
+  // (beside the MFMAs) into one float per block; the 4 k-groups are combined with lane shuffles at the end
+  constexpr bool CS = AKM && BKM && (EPI == E_F32_ACC || EPI == E_F32_STORE);
+  const bool do_cs = CS && p.bsum != nullptr && tm == 0 && wm == 0;  // wave-uniform
+  float cs[CS ? TN : 1];
+#pragma unroll
+  for (int j = 0; j < (CS ? TN : 1); ++j) cs[j] = 0.f;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -380,6 +392,19 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      if constexpr (CS) {
+        if (do_cs) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const i32x4 w = __builtin_bit_cast(i32x4, b[j]);
+            float t = 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              t += __builtin_bit_cast(float, (unsigned)w[q] << 16) + __builtin_bit_cast(float, (unsigned)w[q] & 0xffff0000u);
+            cs[j] += t;
+          }
+        }
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     // ---- sub-step 1: operands in na/nb; issue the next half of this tile into ca/cb, or (last half) publish tile
@@ -417,11 +442,35 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      if constexpr (CS) {
+        if (do_cs) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const i32x4 w = __builtin_bit_cast(i32x4, b[j]);
+            float t = 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              t += __builtin_bit_cast(float, (unsigned)w[q] << 16) + __builtin_bit_cast(float, (unsigned)w[q] & 0xffff0000u);
+            cs[j] += t;
+          }
+        }
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     }  // half
   }
   prof_mark(p.prof, prof_slot, 61, prof_on);
+  if constexpr (CS) {
+    if (do_cs) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float v = cs[j];
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if (lane < 16) atomicAdd(p.bsum + n0 + wn * WN + j * 16 + lane, v);
+      }
+    }
+  }
   if constexpr (EPI == E_F32_ACC || EPI == E_F32_STORE) {
     if (p.ws != nullptr) {
       // Partial tile in MFMA register order (one 16-B chunk per lane per accumulator: 1 KiB coalesced per wave),

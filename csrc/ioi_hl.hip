@@ -7,7 +7,7 @@
 // (last position only: the name mover's cumulative sum at S-1), and the IIT label is argmax_v logits (first maximal
 // index).  An interchange intervention replaces one node's value by the source run's: the input tokens
 // (all_nodes_hook), duplicate, s_inhibition or the name-mover output.  As torch ops that is ~25 launches per
-// intervention (two HL forwards of 10-12 kernels, a [B, 50257] fp32 fill and an argmax over it); here one thread
+// intervention (two HL forwards of 10-12 kernels, a [B, 50257] fp32 fill and an argmax over it); here one wave
 // per sequence computes the intervened label directly from the <= 2S touched vocabulary entries:
 //   max over touched values > 0  -> the smallest touched index holding it;
 //   otherwise the max is 0 (an untouched index exists: V > 2S) -> the smallest index whose value is 0, i.e. the
@@ -19,80 +19,85 @@ namespace {
 
 constexpr int MAXS = 64;
 
-__device__ void duplicates(const long* t, int S, int* dup) {
-  for (int i = 0; i < S; ++i) {
-    int d = -1;
-    for (int j = 0; j < i; ++j)
-      if (t[j] == t[i]) d = j;  // the latest earlier position
-    dup[i] = d;
-  }
-}
-
+// One wave per sequence, lane i owns position i (and touched entry i / i + S): the duplicate scan, the entry sums and
+// the argmax are wave-parallel over LDS (a thread-per-sequence version kept its per-position arrays in scratch memory
+// and took ~80 us for 256 sequences).
 // node: 0 = all_nodes_hook (tokens), 1 = hook_duplicate, 2 = hook_s_inhibition, 3 = hook_name_mover
-__global__ __launch_bounds__(256) void ioi_hl_label_kernel(const long* __restrict__ base, const long* __restrict__ src,
-                                                           const float* __restrict__ name_table, int table_n, int B,
-                                                           int S, int V, int node, long* __restrict__ label) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+__global__ __launch_bounds__(64) void ioi_hl_label_kernel(const long* __restrict__ base, const long* __restrict__ src,
+                                                          const float* __restrict__ name_table, int table_n, int B,
+                                                          int S, int V, int node, long* __restrict__ label) {
+  __shared__ long tok_s[MAXS], dtok_s[MAXS], key_s[2 * MAXS];
+  __shared__ float d_s[2 * MAXS];
+  const int b = blockIdx.x, lane = threadIdx.x;
   const long* tb = base + (long)b * S;
   const long* ts = src + (long)b * S;
   // the run whose tokens feed the downstream heads: the source for an input-token or name-mover interchange
-  // (the name mover's output is the source's), the base otherwise
+  // (the name mover's output is the source's), the base otherwise; the duplicate / s-inhibition values come from
+  // the source for those interchanges
   const long* tok = (node == 0 || node == 3) ? ts : tb;
-  int dup[MAXS];
-  duplicates(node == 1 ? ts : tok, S, dup);  // hook_duplicate interchange: the source's duplicate positions
-  long inh[MAXS];
-  if (node == 2) {  // hook_s_inhibition interchange: the source's s_inhibition values
-    int dsrc[MAXS];
-    duplicates(ts, S, dsrc);
-    for (int i = 0; i < S; ++i) inh[i] = dsrc[i] == -1 ? -1 : ts[i];
-  } else {
-    for (int i = 0; i < S; ++i) inh[i] = dup[i] == -1 ? -1 : tok[i];
+  const long* dtok = (node == 1 || node == 2) ? ts : tok;
+  if (lane < S) {
+    tok_s[lane] = tok[lane];
+    dtok_s[lane] = dtok[lane];
   }
-  // touched vocabulary entries and their summed values
-  long key[2 * MAXS];
-  float val[2 * MAXS];
-  int n = 0;
-  for (int i = 0; i < 2 * S; ++i) {
-    long v;
-    float d;
-    if (i < S) {
-      v = tok[i];
-      d = (v >= 0 && v < table_n && name_table[v] != 0.f) ? 10.f : 0.f;
-    } else {
-      const long s = inh[i - S];
-      v = s != -1 ? s : (long)(V - 1);
-      d = s != -1 ? -15.f : 0.f;
-    }
-    int k = 0;
-    while (k < n && key[k] != v) ++k;
-    if (k == n) {
-      key[n] = v;
-      val[n] = 0.f;
-      ++n;
-    }
-    val[k] += d;
+  __syncthreads();
+  if (lane < S) {
+    int dup = -1;  // the latest earlier position holding the same token (of the duplicate-source run)
+    for (int j = 0; j < lane; ++j)
+      if (dtok_s[j] == dtok_s[lane]) dup = j;
+    // s_inhibition value: the duplicated token; node 1 takes the source's duplicate positions with the base's
+    // tokens, node 2 the source's s_inhibition values, others their own run's
+    const long inh = dup == -1 ? -1 : (node == 1 ? tok_s[lane] : dtok_s[lane]);
+    const long v = tok_s[lane];
+    key_s[lane] = v;
+    d_s[lane] = (v >= 0 && v < table_n && name_table[v] != 0.f) ? 10.f : 0.f;
+    key_s[S + lane] = inh != -1 ? inh : (long)(V - 1);
+    d_s[S + lane] = inh != -1 ? -15.f : 0.f;
   }
-  float best = -INFINITY;
-  for (int k = 0; k < n; ++k) best = fmaxf(best, val[k]);
-  long out = -1;
-  if (best > 0.f) {
-    for (int k = 0; k < n; ++k)
-      if (val[k] == best && (out < 0 || key[k] < out)) out = key[k];
-  } else {
-    // max is 0: the smallest untouched index, unless a smaller touched index sums to exactly 0
-    long u = 0;
-    for (;;) {
-      bool hit = false;
-      for (int k = 0; k < n; ++k) hit |= key[k] == u;
-      if (!hit) break;
-      ++u;
+  __syncthreads();
+  // per entry: the summed value of its key (entries sharing a key all see the same sum)
+  const int n = 2 * S;
+  float my_val = -INFINITY, my_zero_key = INFINITY;
+  long my_key = -1;
+  for (int e = lane; e < n; e += 64) {
+    const long k = key_s[e];
+    float sum = 0.f;
+    for (int f = 0; f < n; ++f)
+      if (key_s[f] == k) sum += d_s[f];
+    if (sum > my_val || (sum == my_val && k < my_key)) {
+      my_val = sum;
+      my_key = k;
     }
-    out = u;
-    for (int k = 0; k < n; ++k)
-      if (val[k] == 0.f && key[k] < out) out = key[k];
+    if (sum == 0.f) my_zero_key = fminf(my_zero_key, (float)k);
   }
-  label[b] = out;
+  // the smallest untouched index: candidates 0 .. n (at most n keys, so one of the n + 1 is untouched)
+  float untouched = INFINITY;
+  for (int u = lane; u <= n; u += 64) {
+    bool hit = false;
+    for (int f = 0; f < n; ++f) hit |= key_s[f] == (long)u;
+    if (!hit) untouched = fminf(untouched, (float)u);
+  }
+  // wave reductions: max value (ties -> smallest key), min zero-sum key, min untouched index
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(my_val, off);
+    const long ok = __shfl_xor(my_key, off);
+    if (ov > my_val || (ov == my_val && ok >= 0 && (my_key < 0 || ok < my_key))) {
+      my_val = ov;
+      my_key = ok;
+    }
+    my_zero_key = fminf(my_zero_key, __shfl_xor(my_zero_key, off));
+    untouched = fminf(untouched, __shfl_xor(untouched, off));
+  }
+  if (lane == 0) {
+    long out;
+    if (my_val > 0.f) {
+      out = my_key;
+    } else {  // max is 0: the smallest untouched index, unless a smaller touched index sums to exactly 0
+      out = (long)untouched;
+      if (my_zero_key < untouched) out = (long)my_zero_key;
+    }
+    label[b] = out;
+  }
 }
 
 }  // namespace
@@ -100,7 +105,7 @@ __global__ __launch_bounds__(256) void ioi_hl_label_kernel(const long* __restric
 IIT_EXPORT int iit_ioi_hl_label(const void* base, const void* src, const float* name_table, int table_n, int B, int S,
                                 int V, int node, void* label, void* stream) {
   if (S < 1 || S > MAXS || node < 0 || node > 3 || V <= 2 * S) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(ioi_hl_label_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(ioi_hl_label_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream,
                      (const long*)base, (const long*)src, name_table, table_n, B, S, V, node, (long*)label);
   return hipGetLastError();
 }

@@ -609,10 +609,13 @@ IIT_EXPORT int iit_ce_fwd(const float* logits, long ld, const long* labels, floa
 }
 
 // dlogits = (softmax - onehot) * gscale[0] * inv_rows   (fp32 or bf16 out, ld_out may be padded; pad columns zeroed)
+// ``out16`` (nullable, fp32 ``out`` only): a bf16 copy with the same row stride written in the same pass -- the operand
+// the unembed backward GEMMs read, so they need no separate cast / re-pad of the [rows][vocab] gradient
 template <typename OUT>
 __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ logits, long ld, const long* __restrict__ labels,
                                                      const float* __restrict__ lse, const float* __restrict__ gscale,
-                                                     float inv_rows, OUT* __restrict__ out, long ld_out, int V) {
+                                                     float inv_rows, OUT* __restrict__ out, long ld_out, int V,
+                                                     __bf16* __restrict__ out16) {
   const int row = blockIdx.y;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= ld_out) return;
@@ -622,17 +625,19 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ l
     v = (p - (i == labels[row] ? 1.f : 0.f)) * gscale[0] * inv_rows;
   }
   out[(long)row * ld_out + i] = (OUT)v;
+  if (out16) out16[(long)row * ld_out + i] = f2bf(v);
 }
 
 IIT_EXPORT int iit_ce_bwd(const float* logits, long ld, const long* labels, const float* lse, const float* gscale,
-                          float inv_rows, void* out, long ld_out, int R, int V, int out_bf16, void* stream) {
+                          float inv_rows, void* out, long ld_out, int R, int V, int out_bf16, void* out16,
+                          void* stream) {
   dim3 grid((unsigned)((ld_out + 255) / 256), R);
   if (out_bf16)
     hipLaunchKernelGGL(ce_bwd_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, logits, ld, labels, lse, gscale,
-                       inv_rows, (__bf16*)out, ld_out, V);
+                       inv_rows, (__bf16*)out, ld_out, V, (__bf16*)nullptr);
   else
     hipLaunchKernelGGL(ce_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, logits, ld, labels, lse, gscale,
-                       inv_rows, (float*)out, ld_out, V);
+                       inv_rows, (float*)out, ld_out, V, (__bf16*)out16);
   return hipGetLastError();
 }
 

@@ -322,11 +322,11 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
                                    C2=aux if dg else C2, resid=resid, ldc2=ldc2, ldr=ldr, bias_cols=bias_cols,
                                    tile=tile, splits=sp):
                     calls[f"glds{tile}" + (f"k{sp}" if sp > 1 else "")] = \
-                        lambda c=C, c2=C2, c3=None, t=tile, sp=sp: K_.gemm_glds(  # noqa: E731
+                        lambda c=C, c2=C2, c3=None, t=tile, sp=sp, bs=None: K_.gemm_glds(  # noqa: E731
                             A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi,
                             C2=aux if dg else c2, bias0=bias0, bias1=bias1, bias2=bias2, resid=resid, ldc2=ldc2,
                             ldr=ldr, bias_cols=bias_cols, tile=t, splits=sp,
-                            csum=csum_box[0] if csum_box is not None else None)
+                            csum=csum_box[0] if csum_box is not None else None, bsum=bs)
             # the weight gradients (X^T dY, reduction over the tokens) also get the deterministic reduction split:
             # larger tiles per CU (fewer operand bytes per flop) without fp32 atomics; they only run in backward
             # passes, which are serial on one stream
@@ -336,9 +336,9 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
                                                              mode=mode, epi=epi, resid=resid, ldr=ldr, tile=tile,
                                                              splits=sp, reduce=True):
                         continue
-                    calls[f"glds{tile}r{sp}"] = lambda c=C, c2=C2, c3=None, t=tile, sp=sp: K_.gemm_glds(  # noqa
+                    calls[f"glds{tile}r{sp}"] = lambda c=C, c2=C2, c3=None, t=tile, sp=sp, bs=None: K_.gemm_glds(  # noqa
                         A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, bias0=bias0,
-                        resid=resid, ldr=ldr, tile=t, splits=sp, reduce=True)
+                        resid=resid, ldr=ldr, tile=t, splits=sp, reduce=True, bsum=bs)
     if epi in _BLAS16_EPIS:
         calls["blas16"] = lambda c=C, c2=C2, c3=None: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
                                                              bias0, resid, ldr)
@@ -402,7 +402,7 @@ def _ragged_split(A, B, C, *, M, N, K, lda, ldb, mode, epi, C2, bias0, resid, au
 
 def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=None, bias0=None, bias1=None,
          bias2=None, resid=None, ldr=0, aux=None, ldc2=0, bias_cols=0, qkv=(0, 0, 0), splits=None, blas_bias=None,
-         fresh: bool = False, colsum=None, _decide_only: bool = False, _no_split: bool = False):
+         fresh: bool = False, colsum=None, bsum=None, _decide_only: bool = False, _no_split: bool = False):
     """``C = A @ B`` (+ epilogue) on the fastest measured implementation for this problem:
 
     * ``hip``    -- the hand-written MFMA kernel with the epilogue fused;
@@ -419,6 +419,10 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     ``colsum`` (``EPI_DGELU`` only): fp32 [N] that also receives the column sums of the bf16 output (the MLP
     input-bias gradient), fused into the LDS-DMA kernel's epilogue or as a pass after the other candidates.
 
+    ``bsum`` (weight gradients, mode 3: ``B`` is dY [K][N]): fp32 [N] that also receives ``colsum(B)`` -- the bias
+    gradient of the layer -- fused into the LDS-DMA kernel's main loop (the B fragments already in registers are
+    summed on the VALU), or as a column-sum pass after any other implementation.  It does not enter the decision.
+
     Ragged problems (the vocabulary-sized unembed GEMMs: N or K = 50257) are split into a tile-aligned bulk, which
     the LDS-DMA kernel can serve, and a narrow tail (see :func:`_ragged_split`).
 
@@ -428,7 +432,7 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         select_graph_safe_blas()
         enable_tuned_library_gemms()
     policy = POLICY
-    if policy in ("auto", "glds") and A.is_cuda and qkv[0] == 0 and colsum is None and not _no_split:
+    if policy in ("auto", "glds") and A.is_cuda and qkv[0] == 0 and colsum is None and bsum is None and not _no_split:
         parts = _ragged_split(A, B, C, M=M, N=N, K=K, lda=lda, ldb=ldb, mode=mode, epi=epi, C2=C2, bias0=bias0,
                               resid=resid, aux=aux)
         if parts is not None:
@@ -463,8 +467,23 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     hip_call = calls["hip"]
     if _decide_only and (policy != "auto" or "blas" not in calls):
         return None  # nothing to measure: a forced policy or a single candidate
+    if bsum is not None:
+        assert mode == 3, "fused bias sums are the column sums of a weight gradient's dY"
+        # every path below ends in _run: the fused column sums on the LDS-DMA kernel, else a column-sum pass
+        def _run(name):
+            if name.startswith("glds"):
+                calls[name](C, C2, C3, bs=bsum)
+            else:
+                calls[name](C, C2, C3)
+                K_.colsum_accum(B, ldb, bsum, Kd, N)
+            return name
+    else:
+        def _run(name):
+            calls[name](C, C2, C3)
+            return name
     if policy == "hip" or "blas" not in calls:
-        return hip_call(C, C2, C3)
+        _run("hip")
+        return None
     if fresh:
         acc = _candidates(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, K_.EPI_F32_ACC, None, None, None, resid, ldr,
                           aux, ldc2, bias_cols, qkv, None, blas_bias, policy)
@@ -472,9 +491,11 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
             calls["z+" + name] = lambda c=C, c2=C2, c3=None, f=f: (_as(c, M, N, ldc).zero_(), f(c, c2, c3))
     if policy == "glds":
         glds = [k for k in calls if k.startswith("glds")]
-        return calls[glds[0] if glds else "hip"](C, C2, C3)
+        _run(glds[0] if glds else "hip")
+        return None
     if policy in calls:
-        return calls[policy](C, C2, C3)
+        _run(policy)
+        return None
     # the last key field marks the variant: a fresh store (EPI_F32_STORE) or fused column sums (EPI_DGELU)
     key = (M, N, Kd, mode, epi, bias0 is not None, fresh or (colsum is not None), deterministic())
     choice = DECISIONS.get(key)
@@ -484,19 +505,28 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
             choice = DECISIONS[key] = (shipped, {shipped: float("nan")})
     if choice is None:
         if torch.cuda.is_current_stream_capturing():
-            return None if _decide_only else hip_call(C, C2, C3)
+            if _decide_only:
+                return None
+            _run("hip")
+            return None
         # time on scratch outputs so accumulate epilogues (and column sums) do not corrupt C
         sc = _scratch(C, M, max(ldc, N))
         sc2 = _scratch(C2, M, max(ldc2, N))
         sc3 = _scratch(C3, M, max(ldc, N))
         if box is not None:
             box[0] = torch.zeros_like(colsum)
+        timed = calls
+        if bsum is not None:  # candidates timed with their column sums (fused or a pass), into scratch
+            sc_bs = torch.zeros_like(bsum)
+            timed = {name: (lambda c, c2, c3, f=f: f(c, c2, c3, bs=sc_bs)) if name.startswith("glds") else
+                     (lambda c, c2, c3, f=f: (f(c, c2, c3), K_.colsum_accum(B, ldb, sc_bs, Kd, N)))
+                     for name, f in calls.items()}
         try:
-            times = {name: min(_time(lambda f=f: f(sc, sc2, sc3)) for _ in range(2)) for name, f in calls.items()}
+            times = {name: min(_time(lambda f=f: f(sc, sc2, sc3)) for _ in range(2)) for name, f in timed.items()}
             # the closest contenders are re-timed with more repetitions: near-ties (a few %) between tiles are
             # otherwise decided by timing noise
             for name in sorted(times, key=times.get)[:3] if len(times) > 1 else ():
-                f = calls[name]
+                f = timed[name]
                 times[name] = min(_time(lambda f=f: f(sc, sc2, sc3), reps=30) for _ in range(3))
         finally:
             if box is not None:
@@ -511,12 +541,11 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     if TIMING is not None:
         s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s_ev.record()
-        calls[name](C, C2, C3)
+        _run(name)
         e_ev.record()
         TIMING.append((key, name, s_ev, e_ev))
         return name
-    calls[name](C, C2, C3)
-    return name
+    return _run(name)
 
 
 K_ = K  # the kernel module (``K`` is shadowed by the reduction-size keyword above)
@@ -535,22 +564,24 @@ def _dual_eligible(x: dict, w: dict) -> bool:
             and all(w.get(k) is None for k in ("bias0", "resid", "C2", "splits", "aux", "colsum")))
 
 
-def _dual_specs(x: dict, w: dict, xc, wc, csum):
+def _dual_specs(x: dict, w: dict, xc, wc, csum, bsum=None):
     ws = dict(A=w["A"], B=w["B"], C=wc, M=w["M"], N=w["N"], K=w["K"], lda=w["lda"], ldb=w["ldb"], ldc=w["ldc"],
-              epi=w["epi"])
+              epi=w["epi"], bsum=bsum)
     xs = dict(A=x["A"], B=x["B"], C=xc, C2=x.get("aux"), M=x["M"], N=x["N"], K=x["K"], lda=x["lda"], ldb=x["ldb"],
               ldc=x["ldc"], ldc2=x.get("ldc2", 0), epi=x["epi"], csum=csum)
     return ws, xs
 
 
-def _dual_candidates(x: dict, w: dict, xc, wc, csum):
+def _dual_candidates(x: dict, w: dict, xc, wc, csum, bsum=None):
     """name -> f() for every dual configuration (dW tile, dX tile, dW K-split) that covers the pair."""
-    ws, xs = _dual_specs(x, w, xc, wc, csum)
+    ws, xs = _dual_specs(x, w, xc, wc, csum, bsum)
     det = deterministic()
     out = {}
     for wt in K.DUAL_W_TILES:
         for xt in K.DUAL_X_TILES:
-            for sp, red in ((1, False), (2, True), (4, True), (2, False), (4, False)):
+            if not K.dual_family_ok(wt, xt):
+                continue
+            for sp, red in ((1, False), (2, True), (4, True), (8, True), (2, False), (4, False), (8, False)):
                 if not red and sp > 1 and (w["epi"] != K.EPI_F32_ACC or det):
                     continue  # atomic split-K: accumulate only, never in deterministic mode
                 if sp > 1 and w["K"] // sp < 256:
@@ -588,8 +619,9 @@ def gemm_pair(x: dict, w: dict) -> Optional[str]:
         xc = _scratch(x["C"], x["M"], max(x["ldc"], x["N"]))
         wc = _scratch(w["C"], w["M"], max(w["ldc"], w["N"]))
         cs = torch.zeros_like(x["colsum"]) if x.get("colsum") is not None else None
-        calls = _dual_candidates(x, w, xc, wc, cs)
-        calls["serial"] = lambda: (gemm(**{**x, "C": xc, "colsum": cs}), gemm(**{**w, "C": wc}))
+        bs = torch.zeros_like(w["bsum"]) if w.get("bsum") is not None else None
+        calls = _dual_candidates(x, w, xc, wc, cs, bs)
+        calls["serial"] = lambda: (gemm(**{**x, "C": xc, "colsum": cs}), gemm(**{**w, "C": wc, "bsum": bs}))
         times = {n: min(_time(f) for _ in range(2)) for n, f in calls.items()}
         for n in sorted(times, key=times.get)[:3] if len(times) > 1 else ():
             times[n] = min(_time(calls[n], reps=30) for _ in range(3))
@@ -597,7 +629,7 @@ def gemm_pair(x: dict, w: dict) -> Optional[str]:
         choice = DUAL_DECISIONS[key] = (best, times)
     name = FORCE.get(key, choice[0])
     cfg = _parse_dual(name)
-    ws, xs = _dual_specs(x, w, x["C"], w["C"], x.get("colsum"))
+    ws, xs = _dual_specs(x, w, x["C"], w["C"], x.get("colsum"), w.get("bsum"))
     if cfg is None or not K.gemm_dual_ok(ws, xs, *cfg):
         name, cfg = "serial", None
     s_ev = e_ev = None

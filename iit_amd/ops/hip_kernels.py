@@ -30,7 +30,7 @@ _SIGS = {
     "iit_gemm": [c_void_p] * 10 + [c_long] * 5 + [c_int] * 12 + [c_void_p],
     "iit_gemm_glds": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p] * 4,
     "iit_gemm_glds_ok": [c_void_p] * 5 + [c_long] * 5 + [c_int] * 9,
-    "iit_gemm_glds_sm": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p] * 3 + [c_int, c_void_p],
+    "iit_gemm_glds_sm": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p] * 3 + [c_int, c_void_p, c_void_p],
     "iit_embed_pos_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_embed_pos_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_ln_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
@@ -45,7 +45,7 @@ _SIGS = {
     "iit_attn_mfma_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
     "iit_ce_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "iit_ce_bwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_long, c_int, c_int, c_int,
-                   c_void_p],
+                   c_void_p, c_void_p],
     "iit_adam_flat": [c_void_p] * 6 + [c_int, c_void_p, c_int] + [c_float] * 6 + [c_void_p] * 4,
     "iit_adam_span_size": [],
     "iit_sumsq_spans": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
@@ -73,7 +73,7 @@ _SIGS = {
     "iit_gemm_glds_set_prof": [c_void_p],
     "iit_gemm_dual_ok": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 7 + [c_void_p] * 4 + [c_long] * 4 + [c_int] * 5,
     "iit_gemm_dual": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 6 + [c_void_p] * 2 + [c_void_p] * 4 + [c_long] * 4
-                     + [c_int] * 5 + [c_void_p] * 2,
+                     + [c_int] * 5 + [c_void_p] * 3,
     "iit_gemm_glds_set_group_m": [c_int],
     "iit_ioi_hl_label": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
@@ -243,13 +243,15 @@ GLDS_STORE_MODE = int(os.environ.get("IIT_GEMM_STORE", "0"))  # epilogue stores:
 
 
 def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None, bias1=None, bias2=None, resid=None,
-              ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1, csum=None, reduce=False, store_mode=None):
+              ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1, csum=None, reduce=False, store_mode=None, bsum=None):
     """C = A @ B (+ epilogue) on the LDS-DMA MFMA kernel; bf16 operands, M/N/K multiples of the tile.
     ``EPI_DGELU`` (mode 0): ``C2`` is the saved bf16 pre-activation (row stride ``ldc2``); ``csum`` (fp32 [N],
     optional) accumulates the column sums of the stored bf16 output.
     ``splits > 1``: split-K.  By default the partial tiles are added into C with fp32 atomics (accumulate
     epilogue); with ``reduce`` they go to a workspace and the last-arriving split sums them in a fixed order
-    (run-to-run deterministic, no atomics, and valid for fp32 stores too)."""
+    (run-to-run deterministic, no atomics, and valid for fp32 stores too).
+    ``bsum`` (mode 3 only, fp32 [N], optional): += the column sums of B over K (a weight gradient's bias gradient
+    ``colsum(dY)``), fused into the main loop, added with fp32 atomics."""
     ws = cnt = None
     if reduce:
         ws, cnt = split_workspace(M, N, tile, splits, A.device)
@@ -259,15 +261,23 @@ def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None
     sm = GLDS_STORE_MODE if store_mode is None else store_mode
     _check(lib().iit_gemm_glds_sm(_p(A), _p(B), _p(C), _p(C2), _p(bias0), _p(bias1), _p(bias2), _p(resid), lda, ldb,
                                   ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits, _p(csum), _p(ws),
-                                  _p(cnt), int(sm), _stream()),
+                                  _p(cnt), int(sm), _p(bsum) if mode == 3 else None, _stream()),
            "iit_gemm_glds")
 
 
 # ------------------------------------------------------------------------------ dual GEMM (csrc/gemm_dual.hip)
 # one launch runs a layer's weight gradient dW = X^T dY (mode 3; fp32 store / accumulate, optional K-split) and its
 # input gradient dX = dY W^T (mode 0; bf16 or the fused dgelu epilogue), two workgroups per CU
-DUAL_W_TILES = {0: (128, 96), 1: (128, 128), 2: (96, 96), 3: (64, 96), 4: (64, 64)}
-DUAL_X_TILES = {0: (128, 96), 1: (64, 96), 2: (128, 192), 3: (128, 128)}
+# two families (a launch takes both tiles from one): 4-wave tiles, two workgroups per CU (W 0-4, X 0-3), and 8-wave
+# tiles, one per CU (W 5-6, X 4-6)
+DUAL_W_TILES = {0: (128, 96), 1: (128, 128), 2: (96, 96), 3: (64, 96), 4: (64, 64),
+                5: (256, 128), 6: (128, 128)}
+DUAL_X_TILES = {0: (128, 96), 1: (64, 96), 2: (128, 192), 3: (128, 128),
+                4: (256, 192), 5: (256, 128), 6: (128, 128)}
+
+
+def dual_family_ok(wtile: int, xtile: int) -> bool:
+    return (wtile >= 5) == (xtile >= 4)
 
 
 def _bf16_cuda(*ts) -> bool:
@@ -287,7 +297,8 @@ def gemm_dual_ok(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, redu
 
 
 def gemm_dual(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, reduce: bool = False) -> None:
-    """Both problems of :func:`gemm_dual_ok` in one launch (``x["csum"]``: the DGELU column sums, optional)."""
+    """Both problems of :func:`gemm_dual_ok` in one launch (``x["csum"]``: the DGELU column sums, ``w["bsum"]``: the
+    column sums of dY over the tokens, i.e. the bias gradient; both optional, += atomically)."""
     ws = cnt = None
     if reduce:
         ws, cnt = split_workspace(w["M"], w["N"], DUAL_W_TILES[wtile], splits, w["A"].device)
@@ -300,7 +311,8 @@ def gemm_dual(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, reduce:
     _check(lib().iit_gemm_dual(
         _p(w["A"]), _p(w["B"]), _p(w["C"]), w["lda"], w["ldb"], w["ldc"], w["M"], w["N"], w["K"], w["epi"], wtile,
         splits, _p(ws), _p(cnt), _p(x["A"]), _p(x["B"]), _p(x["C"]), _p(x.get("C2")), x["lda"], x["ldb"], x["ldc"],
-        x.get("ldc2", 0), x["M"], x["N"], x["K"], x["epi"], xtile, _p(x.get("csum")), _stream()), "iit_gemm_dual")
+        x.get("ldc2", 0), x["M"], x["N"], x["K"], x["epi"], xtile, _p(x.get("csum")), _p(w.get("bsum")), _stream()),
+        "iit_gemm_dual")
 
 
 def sumsq_spans(g, spans, nspans, part, step_dev, do_norm: bool):
@@ -490,12 +502,12 @@ def ce_fwd(logits, ld, labels, loss, lse, amax, R, V):
     _check(lib().iit_ce_fwd(_p(logits), ld, _p(labels), _p(loss), _p(lse), _p(amax), R, V, _stream()), "ce_fwd")
 
 
-def ce_bwd(logits, ld, labels, lse, gscale, inv_rows, out, ld_out, R, V):
+def ce_bwd(logits, ld, labels, lse, gscale, inv_rows, out, ld_out, R, V, out16=None):
     """dlogits into ``out`` (fp32 or bf16, row stride ``ld_out``; pad columns zeroed)."""
     if CHECK_BOUNDS:
         _bounds("ce_bwd", ("logits", logits, R, V, ld), ("out", out, R, V, ld_out))
     _check(lib().iit_ce_bwd(_p(logits), ld, _p(labels), _p(lse), _p(gscale), inv_rows, _p(out), ld_out, R, V,
-                            int(out.dtype == torch.bfloat16), _stream()), "ce_bwd")
+                            int(out.dtype == torch.bfloat16), _p(out16), _stream()), "ce_bwd")
 
 
 def colsum_accum(x, ld, out, T, N):

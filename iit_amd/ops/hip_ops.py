@@ -75,6 +75,21 @@ def _claim_store(*ps) -> bool:
     return flat.claim(*ps)
 
 
+_FUSE_BIAS = os.environ.get("IIT_FUSED_BIAS_SUMS", "1") != "0"
+
+
+def _fused_bias(gb: Optional[torch.Tensor], N: int) -> Optional[torch.Tensor]:
+    """``gb`` (a bias-gradient slot of ``N`` floats) when the layer's weight-gradient GEMM may add the bias gradient
+    ``colsum(dY)`` into it itself (``gemm(..., bsum=gb)``: fused into the LDS-DMA kernel's main loop, so dY is not
+    read again by a column-sum pass); None outside that case (no slot, a strided slot, deterministic mode, where the
+    fp32 atomics of the fused sums would make the bias gradient run-to-run variable, or ``IIT_FUSED_BIAS_SUMS=0``)."""
+    if gb is None or not _FUSE_BIAS or not gb.is_cuda or gb.dtype != F32 or not gb.is_contiguous() or \
+            gb.numel() != N:
+        return None
+    from .gemm_dispatch import deterministic
+    return None if deterministic() else gb
+
+
 def _done(*params):
     for p in params:
         if p is not None and p.requires_grad:
@@ -499,11 +514,16 @@ class QKVFn(Function):
             gq, gk, gv = W_Q.grad, W_K.grad, W_V.grad
         else:
             gq, gk, gv = _grad_slot(W_Q), _grad_slot(W_K), _grad_slot(W_V)
+        gbs = [_grad_slot(bp) for bp in (b_Q, b_K, b_V)]
+        packed_b = all(gb is not None for gb in gbs) and all(gb.is_contiguous() for gb in gbs) and _packed3(*gbs, HD)
+        bs = None
         if gq is not None and gk is not None and gv is not None and gq.stride() == (dh, 3 * HD, 1) and \
                 _packed3(gq, gk, gv, HD):
+            if packed_b:  # b_Q | b_K | b_V gradients are one [3 HD] run: the GEMM adds colsum(dqkv) into it
+                bs = _fused_bias(torch.as_strided(gbs[0], (3 * HD,), (1,)), 3 * HD)
             choice = gemm_pair(xspec, dict(A=x2, B=g, C=gq, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=3 * HD,
                                            mode=K.MODE_AKM | K.MODE_BKM,
-                                           epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store))
+                                           epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs))
             if store:
                 _settle_claim(choice, W_Q, W_K, W_V)
         else:
@@ -511,9 +531,10 @@ class QKVFn(Function):
             if gq is not None and gk is not None and gv is not None:
                 gemm(x2, g, gq, C2=gk, C3=gv, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=0,
                      mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_ACC_QKV, qkv=(dh, H, d))
-        gbs = [_grad_slot(bp) for bp in (b_Q, b_K, b_V)]
         if all(gb is not None for gb in gbs):
-            if all(gb.is_contiguous() for gb in gbs) and _packed3(*gbs, HD):
+            if bs is not None:
+                _done(b_Q, b_K, b_V)  # summed by the weight-gradient GEMM
+            elif packed_b:
                 _BIAS_SUMS.add(g, 3 * HD, gbs[0], T, 3 * HD, b_Q, b_K, b_V)
             else:
                 K.colsum3_accum(g, 3 * HD, gbs, T, HD)
@@ -780,12 +801,14 @@ class LinearFn(Function):
                 dx = dxf.to(x_dtype).view(*lead, Kd)
         store = _claim_store(W)
         gW = W.grad if store else _grad_slot(W)
+        gb = _grad_slot(b)
+        bs = _fused_bias(gb, N) if gW is not None else None
         if gW is not None:
             mode = K.MODE_AKM | K.MODE_BKM
             gW2 = gW.reshape(Kd, N) if gW.is_contiguous() else gW
             assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
             wspec = dict(A=x2, B=g2, C=gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode,
-                         epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+                         epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs)
             choice = gemm_pair(xspec, wspec) if xspec is not None else gemm(**wspec)
             if store:
                 _settle_claim(choice, W)
@@ -793,9 +816,11 @@ class LinearFn(Function):
             gemm(**xspec)
         if dxb is not None:
             dx = (dxb if x_dtype == BF16 else dxb.to(x_dtype)).view(*lead, Kd)
-        gb = _grad_slot(b)
         if gb is not None:
-            _BIAS_SUMS.add(g2, ldg, gb, T, N, b)
+            if bs is not None:
+                _done(b)  # summed by the weight-gradient GEMM
+            else:
+                _BIAS_SUMS.add(g2, ldg, gb, T, N, b)
         _done(W)
         return dx, None, None, None, None, gres, None
 
@@ -841,16 +866,18 @@ class MLPInFn(Function):
         xspec = dict(A=dpre, B=ctx.w, C=dx, M=T, N=d, K=dm, lda=dm, ldb=dm, ldc=d, epi=K.EPI_BF16)
         store = W_in.is_contiguous() and _claim_store(W_in)
         gW = W_in.grad if store else _grad_slot(W_in)
+        summed = _bias_sum_done(gpre if gpost is None else None, b_in)  # by MLPOutGeluFn's DGELU epilogue
+        gb = None if summed else _grad_slot(b_in)
+        bs = _fused_bias(gb, dm) if gW is not None else None
         if gW is not None:
             choice = gemm_pair(xspec, dict(A=x2, B=dpre, C=gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm,
                                            mode=K.MODE_AKM | K.MODE_BKM,
-                                           epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store))
+                                           epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs))
             if store:
                 _settle_claim(choice, W_in)
         else:
             gemm(**xspec)
-        gb = _grad_slot(b_in)
-        if gb is not None and not _bias_sum_done(gpre if gpost is None else None, b_in):
+        if gb is not None and bs is None:
             _BIAS_SUMS.add(dpre, dm, gb, T, dm, b_in)
         else:
             _done(b_in)
@@ -914,11 +941,14 @@ class MLPOutGeluFn(Function):
                          epi=K.EPI_DGELU_ERF if ctx.erf else K.EPI_DGELU, aux=pre2, ldc2=pre2.stride(0), colsum=gbi)
         store = _claim_store(W)
         gW = W.grad if store else _grad_slot(W)
+        gb = _grad_slot(b)
+        bs = _fused_bias(gb, N) if gW is not None else None
         if gW is not None:
             gW2 = gW.reshape(Kd, N) if gW.is_contiguous() else gW
             assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
             wspec = dict(A=x2, B=g2, C=gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0),
-                         mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+                         mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store,
+                         bsum=bs)
             choice = gemm_pair(xspec, wspec) if xspec is not None else gemm(**wspec)
             if store:
                 _settle_claim(choice, W)
@@ -928,9 +958,11 @@ class MLPOutGeluFn(Function):
             dpre = dpre.view(*lead, Kd)
             if gbi is not None:
                 dpre._iit_bias_sum = (dpre.data_ptr(), dpre._version, id(b_in))
-        gb = _grad_slot(b)
         if gb is not None:
-            _BIAS_SUMS.add(g2, ldg, gb, T, N, b)
+            if bs is not None:
+                _done(b)  # summed by the weight-gradient GEMM
+            else:
+                _BIAS_SUMS.add(g2, ldg, gb, T, N, b)
         _done(W)
         return dpre, None, None, None, None, None, gy, None, None
 
@@ -960,12 +992,15 @@ class CrossEntropyFn(Function):
         R, V = logits.shape
         ld = logits.stride(0)
         ldo = _pad8(V)
-        # fp32: autograd casts a gradient to its input's dtype anyway (the unembed backward makes the one
-        # bf16 copy its GEMMs read)
+        # fp32 (autograd casts a gradient to its input's dtype anyway) plus, in the same pass, the bf16 twin with
+        # the same padded row stride that the unembed backward GEMMs read
         buf = torch.empty(R, ldo, dtype=F32, device=logits.device)
+        buf16 = torch.empty(R, ldo, dtype=BF16, device=logits.device)
         gs = g.reshape(1).float().contiguous()
-        K.ce_bwd(logits, ld, lab, lse, gs, 1.0 / R, buf, ldo, R, V)
-        return buf[:, :V], None
+        K.ce_bwd(logits, ld, lab, lse, gs, 1.0 / R, buf, ldo, R, V, out16=buf16)
+        res = buf[:, :V]
+        _set_bf16_twin(res, buf16[:, :V])
+        return res, None
 
 
 def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:

@@ -15,13 +15,17 @@ def K():
     return hip_kernels
 
 
-def _problem(seed):
+def _problem(seed, kin=KIN, nout=NOUT):
     torch.manual_seed(seed)
-    x = torch.randn(T, KIN, device=dev).bfloat16()
-    dy = (torch.randn(T, NOUT, device=dev) / 4).bfloat16()
-    w = (torch.randn(KIN, NOUT, device=dev) / 8).bfloat16()
-    pre = torch.randn(T, KIN, device=dev).bfloat16()
+    x = torch.randn(T, kin, device=dev).bfloat16()
+    dy = (torch.randn(T, nout, device=dev) / 4).bfloat16()
+    w = (torch.randn(kin, nout, device=dev) / 8).bfloat16()
+    pre = torch.randn(T, kin, device=dev).bfloat16()
     return x, dy, w, pre
+
+
+# (dW tile, dX tile) pairs: every pair of the 4-wave family, every pair of the 8-wave family
+PAIRS = [(wt, xt) for wt in range(5) for xt in range(4)] + [(wt, xt) for wt in (5, 6) for xt in (4, 5, 6)]
 
 
 VARIANTS = [  # (dW epilogue, dX epilogue, splits, reduce)
@@ -32,13 +36,13 @@ VARIANTS = [  # (dW epilogue, dX epilogue, splits, reduce)
 ]
 
 
-@pytest.mark.parametrize("wt", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("xt", [0, 1, 2, 3])
+@pytest.mark.parametrize("wt,xt", PAIRS)
 @pytest.mark.parametrize("variant", VARIANTS, ids=lambda v: f"{v[0]}-{v[1]}-{'r' if v[3] else 'k'}{v[2]}")
 def test_dual_matches_fp32(K, wt, xt, variant):
     from iit_amd.ops.torch_ops import gelu_new
     wepi_s, xepi_s, splits, reduce = variant
-    x, dy, w, pre = _problem(wt * 10 + xt)
+    KIN, NOUT = (768, 768) if wt >= 5 else (384, 384)  # the 8-wave tiles need 256-row / 192-column multiples
+    x, dy, w, pre = _problem(wt * 10 + xt, KIN, NOUT)
     wepi = K.EPI_F32_STORE if wepi_s == "store" else K.EPI_F32_ACC
     xepi = K.EPI_BF16 if xepi_s == "bf16" else K.EPI_DGELU
     gW0 = torch.randn(KIN, NOUT, device=dev)
@@ -46,18 +50,22 @@ def test_dual_matches_fp32(K, wt, xt, variant):
     dX = torch.zeros(T, KIN, device=dev, dtype=torch.bfloat16)
     csum = torch.randn(KIN, device=dev) if xepi == K.EPI_DGELU else None
     csum0 = csum.clone() if csum is not None else None
-    ws = dict(A=x, B=dy, C=gW, M=KIN, N=NOUT, K=T, lda=KIN, ldb=NOUT, ldc=NOUT, epi=wepi)
+    bsum0 = torch.randn(NOUT, device=dev)
+    bsum = bsum0.clone()
+    ws = dict(A=x, B=dy, C=gW, M=KIN, N=NOUT, K=T, lda=KIN, ldb=NOUT, ldc=NOUT, epi=wepi, bsum=bsum)
     xs = dict(A=dy, B=w, C=dX, C2=pre if xepi == K.EPI_DGELU else None, M=T, N=KIN, K=NOUT, lda=NOUT, ldb=NOUT,
               ldc=KIN, ldc2=KIN, epi=xepi, csum=csum)
     assert K.gemm_dual_ok(ws, xs, wt, xt, splits, reduce)
     for rep in range(2):  # a second launch reuses the reduction tickets the first one re-armed
         gW.copy_(gW0)
+        bsum.copy_(bsum0)
         if csum is not None:
             csum.copy_(csum0)
         K.gemm_dual(ws, xs, wt, xt, splits, reduce)
         torch.cuda.synchronize()
         ref_w = x.float().t() @ dy.float() + (gW0 if wepi == K.EPI_F32_ACC else 0)
         torch.testing.assert_close(gW, ref_w, rtol=1e-4, atol=2e-3)
+        torch.testing.assert_close(bsum, bsum0 + dy.float().sum(0), rtol=1e-4, atol=2e-3)  # fused bias gradient
         ref_x = dy.float() @ w.float().t()
         if xepi == K.EPI_DGELU:
             p = pre.float().requires_grad_(True)
@@ -97,3 +105,27 @@ def test_gemm_pair_dispatch_matches_serial(K):
     gd.DUAL = True
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-4, atol=2e-3)
     torch.testing.assert_close(outs[0][1].float(), outs[1][1].float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("tile", [0, 3, 5, 8, 9, 20, 23, 25, 26, 30])
+@pytest.mark.parametrize("epi,splits,reduce", [(7, 1, False), (5, 2, False), (7, 2, True), (5, 4, True)])
+def test_glds_weight_grad_bias_sums(K, tile, epi, splits, reduce):
+    """Single-launch LDS-DMA weight gradient (mode 3) with the fused column sums of dY (``bsum``)."""
+    bm, bn = K.GLDS_TILES[tile]
+    M, N, Tk = bm * 2, bn * 2, 512
+    torch.manual_seed(tile)
+    x = torch.randn(Tk, M, device=dev).bfloat16()
+    dy = torch.randn(Tk, N, device=dev).bfloat16()
+    C0 = torch.randn(M, N, device=dev)
+    C = C0.clone()
+    bs0 = torch.randn(N, device=dev)
+    bs = bs0.clone()
+    kw = dict(M=M, N=N, K=Tk, lda=M, ldb=N, ldc=N, mode=K.MODE_AKM | K.MODE_BKM, epi=epi, tile=tile, splits=splits,
+              reduce=reduce)
+    if not K.gemm_glds_ok(x, dy, C, **{k: v for k, v in kw.items()}):
+        pytest.skip("tile does not cover this case")
+    K.gemm_glds(x, dy, C, bsum=bs, **kw)
+    torch.cuda.synchronize()
+    ref = x.float().t() @ dy.float() + (C0 if epi == K.EPI_F32_ACC else 0)
+    torch.testing.assert_close(C, ref, rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(bs, bs0 + dy.float().sum(0), rtol=1e-4, atol=2e-3)
