@@ -4,6 +4,8 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r3s2e
 mkdir -p $O
+timeout -k 10 300 python3 -u -m pytest tests/test_hip_kernels.py tests/test_hip_model.py -x -q -m gpu --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; tail -2 $O/tests.log; [ $rc -eq 0 ] || { grep -E "Error|FAIL|assert" $O/tests.log | head -30; exit $rc; }
 IIT_GEMM_TABLE=0 timeout -k 10 700 python3 -u scripts/tune_gemm_in_situ.py --out $O/table_insitu.json \
   --report $O/insitu_report.txt > $O/tune.log 2>&1 || { echo tune failed; tail -30 $O/tune.log; exit 1; }
 tail -3 $O/tune.log

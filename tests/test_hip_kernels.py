@@ -335,3 +335,19 @@ def test_cross_entropy_bf16_grad_kernel(K):
     K.ce_bwd(logits, V, labels, lse, g, 1.0 / R, out, 1008, R, V)
     ref = (logits.softmax(-1) - torch.nn.functional.one_hot(labels, V)) / R
     assert rel_err(out[:, :V], ref) < 1e-2 and out[:, V:].abs().max() == 0
+
+
+def test_cross_entropy_grad_bf16_twin(K):
+    """ce_bwd with an fp32 output also writes the bf16 copy (same padded stride) the unembed GEMMs read."""
+    torch.manual_seed(12)
+    R, V = 8, 1000
+    logits = torch.randn(R, V, device=dev) * 3
+    labels = torch.randint(0, V, (R,), device=dev)
+    loss, lse = torch.empty(R, device=dev), torch.empty(R, device=dev)
+    K.ce_fwd(logits, V, labels, loss, lse, None, R, V)
+    out = torch.full((R, 1008), 7.0, device=dev)
+    out16 = torch.full((R, 1008), 7.0, dtype=torch.bfloat16, device=dev)
+    K.ce_bwd(logits, V, labels, lse, torch.ones(1, device=dev), 1.0 / R, out, 1008, R, V, out16=out16)
+    ref = (logits.softmax(-1) - torch.nn.functional.one_hot(labels, V)) / R
+    assert rel_err(out[:, :V], ref) < 1e-5 and out[:, V:].abs().max() == 0
+    assert torch.equal(out16, out.bfloat16())
