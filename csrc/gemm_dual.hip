@@ -130,7 +130,8 @@ IIT_EXPORT int iit_gemm_dual_ok(const void* wA, const void* wB, const void* wC, 
 IIT_EXPORT int iit_gemm_dual(const void* wA, const void* wB, void* wC, long wlda, long wldb, long wldc, int wM, int wN,
                              int wK, int wepi, int wtile, int wsplits, float* ws, int* counters, const void* xA,
                              const void* xB, void* xC, void* xC2, long xlda, long xldb, long xldc, long xldc2, int xM,
-                             int xN, int xK, int xepi, int xtile, float* csum, float* bsum, void* stream) {
+                             int xN, int xK, int xepi, int xtile, float* csum, float* bsum, float* gsq,
+                             void* stream) {
   const int reduce = ws != nullptr;
   if (!iit_gemm_dual_ok(wA, wB, wC, wlda, wldb, wldc, wM, wN, wK, wepi, wtile, wsplits, reduce, xA, xB, xC, xC2, xlda,
                         xldb, xldc, xldc2, xM, xN, xK, xepi, xtile))
@@ -143,6 +144,7 @@ IIT_EXPORT int iit_gemm_dual(const void* wA, const void* wB, void* wC, long wlda
   w.ws = reduce ? ws : nullptr;
   w.counters = reduce ? counters : nullptr;
   w.bsum = bsum;  // the dW problem's column sums of dY (its bias gradient), nullable
+  w.gsq = wepi == E_F32_STORE ? gsq : nullptr;  // its sum of squares (the clip's global norm), nullable
   G2Args x{};
   x.A = (const __bf16*)xA; x.B = (const __bf16*)xB; x.C = xC; x.C2 = xC2;
   x.lda = xlda; x.ldb = xldb; x.ldc = xldc; x.ldc2 = xldc2;

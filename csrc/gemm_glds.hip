@@ -151,7 +151,7 @@ IIT_EXPORT int iit_gemm_glds_sm(const void* A, const void* B, void* C, void* C2,
                                 const float* bias1, const float* bias2, const float* resid, long lda, long ldb, long ldc,
                                 long ldc2, long ldr, int M, int N, int K, int mode, int epi, int bias_cols, int tile,
                                 int splits, float* csum, float* ws, int* counters, int store_mode, float* bsum,
-                                void* stream);
+                                float* gsq, void* stream);
 
 // the timeline probe of the NEXT iit_gemm_glds* launch from this host thread (scripts/gemm_timeline.py): a
 // [workgroups][64] int64 device buffer, consumed by that launch
@@ -166,16 +166,17 @@ IIT_EXPORT int iit_gemm_glds(const void* A, const void* B, void* C, void* C2, co
                              int M, int N, int K, int mode, int epi, int bias_cols, int tile, int splits,
                              float* csum, float* ws, int* counters, void* stream) {
   return iit_gemm_glds_sm(A, B, C, C2, bias0, bias1, bias2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi,
-                          bias_cols, tile, splits, csum, ws, counters, 0, nullptr, stream);
+                          bias_cols, tile, splits, csum, ws, counters, 0, nullptr, nullptr, stream);
 }
 
 // the same with the epilogue store flavour (G2Args::store_mode) and, for the weight gradients (mode 3), the fused
-// column sums of B (``bsum``, += atomically; nullable)
+// column sums of B (``bsum``, += atomically; nullable); ``gsq`` (fp32 store epilogue, nullable): += the sum of squares
+// of the stored values, spread over 64 slots
 IIT_EXPORT int iit_gemm_glds_sm(const void* A, const void* B, void* C, void* C2, const float* bias0,
                                 const float* bias1, const float* bias2, const float* resid, long lda, long ldb, long ldc,
                                 long ldc2, long ldr, int M, int N, int K, int mode, int epi, int bias_cols, int tile,
                                 int splits, float* csum, float* ws, int* counters, int store_mode, float* bsum,
-                                void* stream) {
+                                float* gsq, void* stream) {
   const int reduce = ws != nullptr;
   if (!iit_gemm_glds_ok(A, B, C, C2, resid, lda, ldb, ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits,
                         reduce))
@@ -194,6 +195,7 @@ IIT_EXPORT int iit_gemm_glds_sm(const void* A, const void* B, void* C, void* C2,
   g_prof_buf = nullptr;
   a.group_m = g_group_m;
   a.bsum = mode == 3 ? bsum : nullptr;
+  a.gsq = epi == E_F32_STORE ? gsq : nullptr;
   hipStream_t s = (hipStream_t)stream;
 #define G2(MODE, AK, BK_, EPI) \
   if (mode == (MODE) && epi == (EPI)) return (int)launch_tile<AK, BK_, EPI>(a, tile, s);

@@ -39,6 +39,9 @@ struct G2Args {
   // gradient colsum(dY) of the layer whose dW = X^T dY this is), += atomically by the first M-tile row of tiles
   // from the B fragments already in registers, so dY is not read a second time
   float* bsum;
+  // E_F32_STORE: optional sum of squares of the stored values (this weight gradient's share of the global gradient
+  // norm the optimizer's clip needs), += atomically into one of 64 slots, so the norm pass can skip these gradients
+  float* gsq;
 };
 
 __device__ __forceinline__ void prof_mark(long long* prof, int slot, int e, bool on) {
@@ -553,6 +556,7 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
   // thread's items up front, before the LDS tile is complete: ITEMS loads in flight instead of one per round trip
   constexpr bool PF32 = EPI == E_F32_RESID || EPI == E_F32_ACC;
   constexpr bool PF16 = EPI == E_DGELU || EPI == E_DGELU_ERF;
+  float sq = 0.f;  // E_F32_STORE with ``gsq``: this thread's sum of squares of the stored values
   for (int ch = 0; ch < ECH; ++ch) {
   float4 pf[PF32 ? 2 * ITEMS : 1];
   bf16x8 pb[PF16 ? ITEMS : 1];
@@ -639,6 +643,10 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
     } else {  // E_F32_STORE
       if (p.bias0) add8(v, p.bias0 + col);
       store8_f32((float*)p.C + (long)row * p.ldc + col, v, p.store_mode);
+      if (p.gsq) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sq += v[e] * v[e];
+      }
     }
   }
   if constexpr (EPI == E_DGELU || EPI == E_DGELU_ERF) {
@@ -658,6 +666,12 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
     }
   }
   }  // chunk
+  if constexpr (EPI == E_F32_STORE) {
+    if (p.gsq) {
+      sq = wave_sum(sq);
+      if (lane == 0) atomicAdd(p.gsq + ((lin * NW + wave) & 63), sq);
+    }
+  }
   if (p.prof != nullptr) {  // drain this workgroup's stores, then stamp (diagnostic path only)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

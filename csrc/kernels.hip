@@ -657,13 +657,20 @@ struct Span {
   int pad;
 };
 
+// ``gsq`` (nullable, 64 floats): sums of squares the weight-gradient GEMMs already added for the gradients they stored
+// (their spans are left out of ``spans``); block 0 folds them into its partial and re-zeroes the slots for the next
+// step
 __global__ __launch_bounds__(256) void sumsq_span_kernel(const float* __restrict__ g, const Span* __restrict__ spans,
                                                          int nspans, float* __restrict__ part, int do_norm,
-                                                         int* __restrict__ step) {
+                                                         int* __restrict__ step, float* __restrict__ gsq) {
   __shared__ float sm[4];
   if (blockIdx.x == 0 && threadIdx.x == 0 && step) step[0] += 1;
-  if (!do_norm) return;
   float s = 0.f;
+  if (gsq && blockIdx.x == 0 && threadIdx.x < 64) {
+    s = gsq[threadIdx.x];
+    gsq[threadIdx.x] = 0.f;
+  }
+  if (!do_norm) return;
   const float4* g4 = (const float4*)g;
   for (int e = blockIdx.x; e < nspans; e += gridDim.x) {
     const Span sp = spans[e];
@@ -681,7 +688,9 @@ __global__ __launch_bounds__(256) void sumsq_span_kernel(const float* __restrict
 // Adam (torch semantics, amsgrad=False) with the clip coefficient computed on device from the partial sums,
 // the bias corrections from the device step counter, and the bf16 mirror of the updated weights written in
 // the same pass.  Streams: read g, p, m, v; write p, m, v, mirror (the clipped gradient is not written back).
-template <bool NT>
+// U float4 groups per thread per pass (j, j + 256, ...): all 4U loads are issued before the first use, so each thread
+// keeps 64U bytes in flight (IIT_ADAM_UNROLL picks U at launch)
+template <bool NT, int U>
 __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         __bf16* __restrict__ mirror, const Span* __restrict__ spans,
@@ -730,43 +739,57 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
   float4* v4 = (float4*)v;
   for (int e = blockIdx.x; e < nspans; e += gridDim.x) {
     const Span sp = spans[e];
-    for (int j = threadIdx.x; j < sp.len4; j += 256) {
-      const long i = sp.start4 + j;   // parameter / mirror
-      const long li = sp.local4 + j;  // gradient / moments
-      // NT: the gradient and both moments are touched once per step -- stream them past the caches
-      float4 gg, pp = p4[i], mm, vv;
-      if (NT) {
-        gg = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)g4 + li));
-        mm = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)m4 + li));
-        vv = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)v4 + li));
-      } else {
-        gg = g4[li];
-        mm = m4[li];
-        vv = v4[li];
-      }
-      float* gs = (float*)&gg;
-      float* ps = (float*)&pp;
-      float* ms = (float*)&mm;
-      float* vs = (float*)&vv;
+    for (int j0 = threadIdx.x; j0 < sp.len4; j0 += 256 * U) {
+      float4 gg[U], pp[U], mm[U], vv[U];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float gr = gs[k] * coef;
-        if (wd != 0.f) gr += wd * ps[k];
-        ms[k] = b1 * ms[k] + (1.f - b1) * gr;
-        vs[k] = b2 * vs[k] + (1.f - b2) * gr * gr;
-        ps[k] -= stepsz * ms[k] / (sqrtf(vs[k]) / bc2_sqrt + eps);
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u * 256;
+        if (j < sp.len4) {
+          const long i = sp.start4 + j;   // parameter / mirror
+          const long li = sp.local4 + j;  // gradient / moments
+          pp[u] = p4[i];
+          // NT: the gradient and both moments are touched once per step -- stream them past the caches
+          if (NT) {
+            gg[u] = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)g4 + li));
+            mm[u] = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)m4 + li));
+            vv[u] = __builtin_bit_cast(float4, __builtin_nontemporal_load((const f32x4*)v4 + li));
+          } else {
+            gg[u] = g4[li];
+            mm[u] = m4[li];
+            vv[u] = v4[li];
+          }
+        }
       }
-      p4[i] = pp;
-      if (NT) {
-        __builtin_nontemporal_store(__builtin_bit_cast(f32x4, mm), (f32x4*)m4 + li);
-        __builtin_nontemporal_store(__builtin_bit_cast(f32x4, vv), (f32x4*)v4 + li);
-      } else {
-        m4[li] = mm;
-        v4[li] = vv;
-      }
-      if (mirror) {
-        bf16x4 o = {f2bf(ps[0]), f2bf(ps[1]), f2bf(ps[2]), f2bf(ps[3])};
-        ((bf16x4*)mirror)[i] = o;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u * 256;
+        if (j >= sp.len4) break;
+        const long i = sp.start4 + j;
+        const long li = sp.local4 + j;
+        float* gs = (float*)&gg[u];
+        float* ps = (float*)&pp[u];
+        float* ms = (float*)&mm[u];
+        float* vs = (float*)&vv[u];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float gr = gs[k] * coef;
+          if (wd != 0.f) gr += wd * ps[k];
+          ms[k] = b1 * ms[k] + (1.f - b1) * gr;
+          vs[k] = b2 * vs[k] + (1.f - b2) * gr * gr;
+          ps[k] -= stepsz * ms[k] / (sqrtf(vs[k]) / bc2_sqrt + eps);
+        }
+        p4[i] = pp[u];
+        if (NT) {
+          __builtin_nontemporal_store(__builtin_bit_cast(f32x4, mm[u]), (f32x4*)m4 + li);
+          __builtin_nontemporal_store(__builtin_bit_cast(f32x4, vv[u]), (f32x4*)v4 + li);
+        } else {
+          m4[li] = mm[u];
+          v4[li] = vv[u];
+        }
+        if (mirror) {
+          bf16x4 o = {f2bf(ps[0]), f2bf(ps[1]), f2bf(ps[2]), f2bf(ps[3])};
+          ((bf16x4*)mirror)[i] = o;
+        }
       }
     }
   }
@@ -775,29 +798,77 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
 // ``spans`` is a device array of ``nspans`` Span records (iit_adam_span_size() bytes each).  ``skipped``
 // (nullable) enables the non-finite-gradient guard: the global norm is then always computed and a step whose
 // gradient contains inf/nan leaves weights, moments and the step counter untouched.
+// ``sq_spans`` / ``n_sq_spans`` (nullable: the Adam spans): the spans the norm pass reads -- the Adam spans minus
+// the gradients whose sums of squares the weight-gradient GEMMs added into ``gsq`` (nullable, 64 floats)
 IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, void* mirror, const void* spans, int nspans,
                              float* part, int nparts, float clip, float lr, float b1, float b2, float eps, float wd,
-                             const float* hyper, int* step, int* skipped, void* stream) {
+                             const float* hyper, int* step, int* skipped, const void* sq_spans, int n_sq_spans,
+                             float* gsq, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool norm = clip > 0.f || skipped != nullptr;
   const Span* sp = (const Span*)spans;
-  hipLaunchKernelGGL(sumsq_span_kernel, dim3(norm ? nparts : 1), dim3(256), 0, s, g, sp, nspans, part, (int)norm,
-                     step);
+  const Span* ssp = sq_spans ? (const Span*)sq_spans : sp;
+  hipLaunchKernelGGL(sumsq_span_kernel, dim3(norm ? nparts : 1), dim3(256), 0, s, g, ssp,
+                     sq_spans ? n_sq_spans : nspans, part, (int)norm, step, gsq);
   const int blocks = min(nspans, 4096);
   static const int nt = [] {
     const char* e = getenv("IIT_ADAM_NT");
     return e ? atoi(e) : 1;
   }();
-  if (nt)
-    hipLaunchKernelGGL(adam_span_kernel<true>, dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, sp, nspans,
-                       part, nparts, clip, lr, b1, b2, eps, wd, hyper, step, skipped);
-  else
-    hipLaunchKernelGGL(adam_span_kernel<false>, dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, sp,
-                       nspans, part, nparts, clip, lr, b1, b2, eps, wd, hyper, step, skipped);
+  static const int unroll = [] {
+    const char* e = getenv("IIT_ADAM_UNROLL");
+    return e ? atoi(e) : 2;  // profiles/adam_microbench_r3s2.txt: 2 and 4 are ~4-5 % faster than 1
+  }();
+#define ADAM_LAUNCH(NT_, U_)                                                                                        \
+  hipLaunchKernelGGL((adam_span_kernel<NT_, U_>), dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, sp, \
+                     nspans, part, nparts, clip, lr, b1, b2, eps, wd, hyper, step, skipped)
+  if (nt) {
+    if (unroll >= 4) ADAM_LAUNCH(true, 4);
+    else if (unroll == 2) ADAM_LAUNCH(true, 2);
+    else ADAM_LAUNCH(true, 1);
+  } else {
+    if (unroll >= 4) ADAM_LAUNCH(false, 4);
+    else if (unroll == 2) ADAM_LAUNCH(false, 2);
+    else ADAM_LAUNCH(false, 1);
+  }
+#undef ADAM_LAUNCH
   return hipGetLastError();
 }
 
 IIT_EXPORT int iit_adam_span_size() { return (int)sizeof(Span); }
+
+// gsq[slot] += sum of squares of an fp32 [M][N] matrix (row stride ldc): the fused-norm share of a weight gradient
+// that a library GEMM stored (the LDS-DMA kernels add theirs in the epilogue)
+__global__ __launch_bounds__(256) void sumsq_2d_kernel(const float* __restrict__ c, long ldc, int M, int N,
+                                                       float* __restrict__ gsq) {
+  // work item = (row, 2048-column chunk); each thread keeps 8 independent loads in flight per item
+  __shared__ float sm[4];
+  const int chunks = (N + 2047) / 2048;
+  float s = 0.f;
+  for (long it = blockIdx.x; it < (long)M * chunks; it += gridDim.x) {
+    const int r = (int)(it / chunks), c0 = (int)(it % chunks) * 2048;
+    const float* row = c + (long)r * ldc;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int j = c0 + k * 256 + threadIdx.x;
+      v[k] = j < N ? row[j] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k] * v[k];
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(gsq + (blockIdx.x & 63), (sm[0] + sm[1]) + (sm[2] + sm[3]));
+}
+
+IIT_EXPORT int iit_sumsq_2d(const float* c, long ldc, int M, int N, float* gsq, void* stream) {
+  const long items = (long)M * ((N + 2047) / 2048);
+  hipLaunchKernelGGL(sumsq_2d_kernel, dim3((unsigned)(items < 2048 ? items : 2048)), dim3(256), 0,
+                     (hipStream_t)stream, c, ldc, M, N, gsq);
+  return hipGetLastError();
+}
 
 // The two stages separately, for the sharded optimizer (ZeRO-1, iit_amd/parallel/zero.py): per-block partial sums
 // of g^2 over this rank's shard spans (+ the device step bump), then -- after the host all-reduces the partial total
@@ -805,7 +876,7 @@ IIT_EXPORT int iit_adam_span_size() { return (int)sizeof(Span); }
 IIT_EXPORT int iit_sumsq_spans(const float* g, const void* spans, int nspans, float* part, int nparts, int do_norm,
                                int* step, void* stream) {
   hipLaunchKernelGGL(sumsq_span_kernel, dim3(do_norm ? nparts : 1), dim3(256), 0, (hipStream_t)stream, g,
-                     (const Span*)spans, nspans, part, do_norm, step);
+                     (const Span*)spans, nspans, part, do_norm, step, (float*)nullptr);
   return hipGetLastError();
 }
 
@@ -813,7 +884,7 @@ IIT_EXPORT int iit_adam_spans(float* p, const float* g, float* m, float* v, void
                               int nspans, const float* total, float clip, float lr, float b1, float b2, float eps,
                               float wd, const float* hyper, int* step, int* skipped, void* stream) {
   const int blocks = max(1, min(nspans, 4096));
-  hipLaunchKernelGGL(adam_span_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
+  hipLaunchKernelGGL((adam_span_kernel<true, 1>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
                      (__bf16*)mirror, (const Span*)spans, nspans, total, 1, clip, lr, b1, b2, eps, wd, hyper, step,
                      skipped);
   return hipGetLastError();

@@ -126,6 +126,14 @@ class FlatParams:
         self.restrict_version = 0
         self._span_cache = None
         self._listeners = []
+        # fused gradient norm (see ``norm_cover``): off unless the training loop turns it on (single process, nothing
+        # rewrites gradients between the backward and the optimizer step)
+        self.norm_fuse = False
+        self.gsq: Optional[torch.Tensor] = None
+        self._norm_covered = set()   # parameter indices whose sum of squares a store GEMM added into ``gsq``
+        self._norm_capable = set()   # ... whose producer can do so when it stores (``norm_intent``)
+        self._norm_dirty = False     # a covered gradient was accumulated into afterwards: full norm pass
+        self._sq_span_cache = {}
         module._flat_params = self
         if with_bf16_shadow:
             self.ensure_shadow()
@@ -249,6 +257,9 @@ class FlatParams:
         to its ~100 live rows).  On the GPU the memset is one launch per 64 ranges with the ranges passed as kernel
         arguments: no device table, so a plan first needed inside a graph capture is still a single node.  Plans
         are cached per (claim set, restriction)."""
+        if self._norm_covered:  # a backward ran without an optimizer step consuming its fused norm sums
+            self._norm_covered, self._norm_dirty = set(), False
+            self.gsq.zero_()
         key = (frozenset(self._claimed), self.restrict_version)
         plan = self._zero_plans.get(key)
         if plan is None:
@@ -285,6 +296,76 @@ class FlatParams:
         for i in none_ids:
             self.params[i].grad = None
 
+    # ---------------------------------------------------------------- fused gradient norm
+    def norm_cover(self, *ps: torch.Tensor) -> Optional[torch.Tensor]:
+        """Called by a producer that just claimed (``claim`` -> True) the gradients of ``ps`` and stores them
+        complete with one GEMM: returns the 64 device slots that GEMM adds the sum of squares of the stored
+        gradient into (``gemm(..., gsq=...)``), and marks ``ps`` covered, so the optimizer's norm pass skips their
+        slots (``norm_spans``).  The clip's global norm then costs no separate read of these gradients.  None when
+        fusion is off (``norm_fuse``: data parallelism reduces gradients after the GEMM; a pair that rewrites
+        gradients before the step) or in deterministic mode (the slot sums are fp32 atomics)."""
+        if not self.norm_fuse or not self.grad.is_cuda:
+            return None
+        from ..ops.gemm_dispatch import deterministic
+        if deterministic():
+            return None
+        idx = [self.index.get(id(p)) for p in ps]
+        if any(i is None for i in idx):
+            return None
+        if self.gsq is None:
+            self.gsq = torch.zeros(64, dtype=torch.float32, device=self.grad.device)
+        self._norm_covered.update(idx)
+        return self.gsq
+
+    def norm_intent(self, *ps: torch.Tensor) -> None:
+        """A producer that covers ``ps`` whenever it stores their gradient (see ``norm_cover``) ran: the norm span
+        table for that cover set is built ahead, outside graph capture (a capture cannot upload a new table)."""
+        if self.norm_fuse:
+            self._norm_capable.update(i for i in (self.index.get(id(p)) for p in ps) if i is not None)
+
+    def norm_spans(self, span_bytes: int = 24, max_len4: int = 1024):
+        """(span table, count, gsq) for the optimizer's norm pass: the active spans minus the slots whose every
+        parameter a GEMM covered this step, and the slots those GEMMs added into; (None, 0, None) for the plain
+        pass over the Adam spans.  Resets the step's cover state."""
+        covered, dirty = frozenset(self._norm_covered), self._norm_dirty
+        self._norm_covered, self._norm_dirty = set(), False
+        capturing = self.grad.is_cuda and torch.cuda.is_current_stream_capturing()
+        if self._norm_capable and not capturing:  # the table the next (possibly captured) steps will need
+            self._norm_table(frozenset(self._norm_capable), span_bytes, max_len4)
+        if not covered or self.gsq is None:
+            return None, 0, None
+        key = (covered, self.restrict_version, max_len4)
+        if dirty or (capturing and key not in self._sq_span_cache):
+            # a covered gradient changed after its GEMM (its sum is stale), or a cover set first seen inside a
+            # capture: drop the slot sums and read every gradient
+            self.gsq.zero_()
+            return None, 0, None
+        tab, n = self._norm_table(covered, span_bytes, max_len4)
+        return tab, n, self.gsq
+
+    def _norm_table(self, covered, span_bytes: int, max_len4: int):
+        key = (covered, self.restrict_version, max_len4)
+        ent = self._sq_span_cache.get(key)
+        if ent is None:
+            holes = []
+            for o, n in self.slots:
+                members = [i for i, p in enumerate(self.params) if o <= self.offset_of(p) < o + max(n, 1)]
+                if members and all(i in covered for i in members):
+                    holes.append((o, o + _align(n)))  # with the slot's zero padding: float4-aligned ends
+            live = _subtract_ranges([(0, self.numel)], sorted(holes + self.inactive_ranges()))
+            spans = []
+            for a, b in live:
+                assert a % 4 == 0 and b % 4 == 0, (a, b)
+                a4, b4 = a // 4, b // 4
+                pos = a4
+                while pos < b4:
+                    ln = min(max_len4, b4 - pos)
+                    spans.append((pos, pos, ln))
+                    pos += ln
+            assert span_bytes == 24
+            ent = self._sq_span_cache[key] = (make_span_tensor(spans, self.data.device), len(spans))
+        return ent
+
     def claim(self, *ps: torch.Tensor) -> bool:
         """Called by a producer that writes the *complete* gradient of ``ps`` (one slot, e.g. the packed
         ``W_Q|W_K|W_V`` group) with a single GEMM: True -> store (the slot holds garbage, overwrite it); False
@@ -300,6 +381,8 @@ class FlatParams:
         self._claimed.update(idx)  # a store-capable producer: lazily zero these from the next zero_grad on
         fresh = all(p.grad is None for p in ps)
         if not fresh:
+            if self._norm_covered.intersection(idx):
+                self._norm_dirty = True  # accumulating into a gradient whose square sum is already in gsq
             for p in ps:
                 if p.grad is None:
                     self.bind_zero(p)

@@ -326,7 +326,19 @@ class BaseModelPair(ABC):
         else:
             opt = torch.optim.Adam(module.parameters(), lr=lr)
         self._setup_reducer(opt)
+        if fused:
+            # the clip's global norm from the weight-gradient GEMMs (FlatParams.norm_cover): only when the gradients
+            # those GEMMs store are the ones the optimizer steps on -- one process, no reducer, no gradient rewrite
+            import os
+            opt.flat.norm_fuse = (self._reducer is None and not getattr(opt, "sharded", False)
+                                  and not self.rewrites_grads_before_step()
+                                  and os.environ.get("IIT_FUSED_NORM", "1") != "0")
         return opt
+
+    def rewrites_grads_before_step(self) -> bool:
+        """Whether this pair changes parameter gradients between the backward and the optimizer step (beyond the
+        clip, which the optimizer does itself)."""
+        return False
 
     def _zero_requested(self) -> bool:
         """Optimizer-state sharding: ``training_args["zero"]`` (or ``IIT_ZERO=1``) under data parallelism."""

@@ -31,6 +31,9 @@ class FreezedModelPair(IITBehaviorModelPair):
         self.params_not_in_circuit = node_picker.get_params_not_in_circuit(corr, ll_model)
         self.wandb_method = "freeze_unwanted"
 
+    def rewrites_grads_before_step(self) -> bool:
+        return self.training_args.get("freeze_mode", "parity") == "mask"
+
     def zero_grad_for_not_in_circuit(self):
         if self.training_args.get("freeze_mode", "parity") != "mask":
             return  # reference semantics: the assignment targets a temporary view

@@ -322,11 +322,11 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
                                    C2=aux if dg else C2, resid=resid, ldc2=ldc2, ldr=ldr, bias_cols=bias_cols,
                                    tile=tile, splits=sp):
                     calls[f"glds{tile}" + (f"k{sp}" if sp > 1 else "")] = \
-                        lambda c=C, c2=C2, c3=None, t=tile, sp=sp, bs=None: K_.gemm_glds(  # noqa: E731
+                        lambda c=C, c2=C2, c3=None, t=tile, sp=sp, bs=None, sq=None: K_.gemm_glds(  # noqa: E731
                             A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi,
                             C2=aux if dg else c2, bias0=bias0, bias1=bias1, bias2=bias2, resid=resid, ldc2=ldc2,
                             ldr=ldr, bias_cols=bias_cols, tile=t, splits=sp,
-                            csum=csum_box[0] if csum_box is not None else None, bsum=bs)
+                            csum=csum_box[0] if csum_box is not None else None, bsum=bs, gsq=sq)
             # the weight gradients (X^T dY, reduction over the tokens) also get the deterministic reduction split:
             # larger tiles per CU (fewer operand bytes per flop) without fp32 atomics; they only run in backward
             # passes, which are serial on one stream
@@ -336,9 +336,10 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
                                                              mode=mode, epi=epi, resid=resid, ldr=ldr, tile=tile,
                                                              splits=sp, reduce=True):
                         continue
-                    calls[f"glds{tile}r{sp}"] = lambda c=C, c2=C2, c3=None, t=tile, sp=sp, bs=None: K_.gemm_glds(  # noqa
-                        A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, bias0=bias0,
-                        resid=resid, ldr=ldr, tile=t, splits=sp, reduce=True, bsum=bs)
+                    calls[f"glds{tile}r{sp}"] = lambda c=C, c2=C2, c3=None, t=tile, sp=sp, bs=None, sq=None: \
+                        K_.gemm_glds(A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi,  # noqa
+                                     bias0=bias0, resid=resid, ldr=ldr, tile=t, splits=sp, reduce=True, bsum=bs,
+                                     gsq=sq)
     if epi in _BLAS16_EPIS:
         calls["blas16"] = lambda c=C, c2=C2, c3=None: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
                                                              bias0, resid, ldr)
@@ -380,29 +381,31 @@ def _shift(t, off: int):
 RAGGED = {}  # ragged problem key -> (split wins, whole time, [bulk time, tail time])
 
 
-def _ragged_split(A, B, C, *, M, N, K, lda, ldb, mode, epi, C2, bias0, resid, aux):
+def _ragged_split(A, B, C, *, M, N, K, lda, ldb, mode, epi, C2, bias0, resid, aux, bsum=None, gsq=None):
     """Problem pieces ``[kwargs, ...]`` for a GEMM whose N (any column-wise epilogue) or K (fp32 accumulate) is
     large but not tile-aligned: a bulk of N // 128 * 128 columns (resp. K // 1024 * 1024 reduction steps, so
     split-K factors up to 16 divide it) plus the remainder.  None when the problem is aligned or small."""
     if epi in (K_.EPI_BF16, K_.EPI_F32_STORE, K_.EPI_F32_ACC) and N >= 4096 and N % 128:
         n0 = N // 128 * 128
         boff = n0 if mode & K_.MODE_BKM else n0 * ldb
-        return [dict(A=A, B=B, C=C, M=M, N=n0, K=K, C2=C2, bias0=bias0, resid=resid, aux=aux),
+        return [dict(A=A, B=B, C=C, M=M, N=n0, K=K, C2=C2, bias0=bias0, resid=resid, aux=aux, bsum=bsum, gsq=gsq),
                 dict(A=A, B=_shift(B, boff), C=_shift(C, n0), M=M, N=N - n0, K=K, C2=_shift(C2, n0),
-                     bias0=_shift(bias0, n0), resid=_shift(resid, n0), aux=_shift(aux, n0))]
+                     bias0=_shift(bias0, n0), resid=_shift(resid, n0), aux=_shift(aux, n0), bsum=_shift(bsum, n0),
+                     gsq=gsq)]
     if epi == K_.EPI_F32_ACC and K >= 16384 and K % 1024:
         k0 = K // 1024 * 1024
         aoff = k0 * lda if mode & K_.MODE_AKM else k0
         boff = k0 * ldb if mode & K_.MODE_BKM else k0
-        return [dict(A=A, B=B, C=C, M=M, N=N, K=k0, C2=C2, bias0=bias0, resid=resid, aux=aux),
+        return [dict(A=A, B=B, C=C, M=M, N=N, K=k0, C2=C2, bias0=bias0, resid=resid, aux=aux, bsum=bsum, gsq=gsq),
                 dict(A=_shift(A, aoff), B=_shift(B, boff), C=C, M=M, N=N, K=K - k0, C2=C2, bias0=None,
-                     resid=resid, aux=aux)]
+                     resid=resid, aux=aux, bsum=bsum, gsq=gsq)]
     return None
 
 
 def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=None, bias0=None, bias1=None,
          bias2=None, resid=None, ldr=0, aux=None, ldc2=0, bias_cols=0, qkv=(0, 0, 0), splits=None, blas_bias=None,
-         fresh: bool = False, colsum=None, bsum=None, _decide_only: bool = False, _no_split: bool = False):
+         fresh: bool = False, colsum=None, bsum=None, gsq=None, _decide_only: bool = False,
+         _no_split: bool = False):
     """``C = A @ B`` (+ epilogue) on the fastest measured implementation for this problem:
 
     * ``hip``    -- the hand-written MFMA kernel with the epilogue fused;
@@ -422,6 +425,9 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     ``bsum`` (weight gradients, mode 3: ``B`` is dY [K][N]): fp32 [N] that also receives ``colsum(B)`` -- the bias
     gradient of the layer -- fused into the LDS-DMA kernel's main loop (the B fragments already in registers are
     summed on the VALU), or as a column-sum pass after any other implementation.  It does not enter the decision.
+    ``gsq`` (``EPI_F32_STORE``: a weight gradient stored complete): fp32 [64] slots that also receive the sum of squares
+    of the stored gradient (its share of the clip's global norm, ``FlatParams.norm_cover``) -- in the LDS-DMA kernel's
+    epilogue, or as a pass over ``C`` after any other implementation; not part of the decision either.
 
     Ragged problems (the vocabulary-sized unembed GEMMs: N or K = 50257) are split into a tile-aligned bulk, which
     the LDS-DMA kernel can serve, and a narrow tail (see :func:`_ragged_split`).
@@ -432,9 +438,9 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         select_graph_safe_blas()
         enable_tuned_library_gemms()
     policy = POLICY
-    if policy in ("auto", "glds") and A.is_cuda and qkv[0] == 0 and colsum is None and bsum is None and not _no_split:
+    if policy in ("auto", "glds") and A.is_cuda and qkv[0] == 0 and colsum is None and not _no_split:
         parts = _ragged_split(A, B, C, M=M, N=N, K=K, lda=lda, ldb=ldb, mode=mode, epi=epi, C2=C2, bias0=bias0,
-                              resid=resid, aux=aux)
+                              resid=resid, aux=aux, bsum=bsum, gsq=gsq)
         if parts is not None:
             bulk, tail = parts
 
@@ -467,15 +473,19 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     hip_call = calls["hip"]
     if _decide_only and (policy != "auto" or "blas" not in calls):
         return None  # nothing to measure: a forced policy or a single candidate
-    if bsum is not None:
-        assert mode == 3, "fused bias sums are the column sums of a weight gradient's dY"
-        # every path below ends in _run: the fused column sums on the LDS-DMA kernel, else a column-sum pass
+    if bsum is not None or gsq is not None:
+        assert bsum is None or mode == 3, "fused bias sums are the column sums of a weight gradient's dY"
+        assert gsq is None or epi == K_.EPI_F32_STORE, "fused norm sums are of a stored gradient"
+        # every path below ends in _run: the sums fused in the LDS-DMA kernel, else passes after the GEMM
         def _run(name):
             if name.startswith("glds"):
-                calls[name](C, C2, C3, bs=bsum)
+                calls[name](C, C2, C3, bs=bsum, sq=gsq)
             else:
                 calls[name](C, C2, C3)
-                K_.colsum_accum(B, ldb, bsum, Kd, N)
+                if bsum is not None:
+                    K_.colsum_accum(B, ldb, bsum, Kd, N)
+                if gsq is not None:
+                    K_.sumsq_2d(C, ldc, M, N, gsq)
             return name
     else:
         def _run(name):
@@ -516,10 +526,18 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         if box is not None:
             box[0] = torch.zeros_like(colsum)
         timed = calls
-        if bsum is not None:  # candidates timed with their column sums (fused or a pass), into scratch
-            sc_bs = torch.zeros_like(bsum)
-            timed = {name: (lambda c, c2, c3, f=f: f(c, c2, c3, bs=sc_bs)) if name.startswith("glds") else
-                     (lambda c, c2, c3, f=f: (f(c, c2, c3), K_.colsum_accum(B, ldb, sc_bs, Kd, N)))
+        if bsum is not None or gsq is not None:  # candidates timed with their fused sums or passes, into scratch
+            sc_bs = torch.zeros_like(bsum) if bsum is not None else None
+            sc_sq = torch.zeros_like(gsq) if gsq is not None else None
+
+            def _passes(c):
+                if sc_bs is not None:
+                    K_.colsum_accum(B, ldb, sc_bs, Kd, N)
+                if sc_sq is not None:
+                    K_.sumsq_2d(c, ldc, M, N, sc_sq)
+
+            timed = {name: (lambda c, c2, c3, f=f: f(c, c2, c3, bs=sc_bs, sq=sc_sq)) if name.startswith("glds") else
+                     (lambda c, c2, c3, f=f: (f(c, c2, c3), _passes(c)))
                      for name, f in calls.items()}
         try:
             times = {name: min(_time(lambda f=f: f(sc, sc2, sc3)) for _ in range(2)) for name, f in timed.items()}
@@ -564,17 +582,17 @@ def _dual_eligible(x: dict, w: dict) -> bool:
             and all(w.get(k) is None for k in ("bias0", "resid", "C2", "splits", "aux", "colsum")))
 
 
-def _dual_specs(x: dict, w: dict, xc, wc, csum, bsum=None):
+def _dual_specs(x: dict, w: dict, xc, wc, csum, bsum=None, gsq=None):
     ws = dict(A=w["A"], B=w["B"], C=wc, M=w["M"], N=w["N"], K=w["K"], lda=w["lda"], ldb=w["ldb"], ldc=w["ldc"],
-              epi=w["epi"], bsum=bsum)
+              epi=w["epi"], bsum=bsum, gsq=gsq)
     xs = dict(A=x["A"], B=x["B"], C=xc, C2=x.get("aux"), M=x["M"], N=x["N"], K=x["K"], lda=x["lda"], ldb=x["ldb"],
               ldc=x["ldc"], ldc2=x.get("ldc2", 0), epi=x["epi"], csum=csum)
     return ws, xs
 
 
-def _dual_candidates(x: dict, w: dict, xc, wc, csum, bsum=None):
+def _dual_candidates(x: dict, w: dict, xc, wc, csum, bsum=None, gsq=None):
     """name -> f() for every dual configuration (dW tile, dX tile, dW K-split) that covers the pair."""
-    ws, xs = _dual_specs(x, w, xc, wc, csum, bsum)
+    ws, xs = _dual_specs(x, w, xc, wc, csum, bsum, gsq)
     det = deterministic()
     out = {}
     for wt in K.DUAL_W_TILES:
@@ -620,8 +638,10 @@ def gemm_pair(x: dict, w: dict) -> Optional[str]:
         wc = _scratch(w["C"], w["M"], max(w["ldc"], w["N"]))
         cs = torch.zeros_like(x["colsum"]) if x.get("colsum") is not None else None
         bs = torch.zeros_like(w["bsum"]) if w.get("bsum") is not None else None
-        calls = _dual_candidates(x, w, xc, wc, cs, bs)
-        calls["serial"] = lambda: (gemm(**{**x, "C": xc, "colsum": cs}), gemm(**{**w, "C": wc, "bsum": bs}))
+        sq = torch.zeros_like(w["gsq"]) if w.get("gsq") is not None else None
+        calls = _dual_candidates(x, w, xc, wc, cs, bs, sq)
+        calls["serial"] = lambda: (gemm(**{**x, "C": xc, "colsum": cs}),
+                                   gemm(**{**w, "C": wc, "bsum": bs, "gsq": sq}))
         times = {n: min(_time(f) for _ in range(2)) for n, f in calls.items()}
         for n in sorted(times, key=times.get)[:3] if len(times) > 1 else ():
             times[n] = min(_time(calls[n], reps=30) for _ in range(3))
@@ -629,7 +649,7 @@ def gemm_pair(x: dict, w: dict) -> Optional[str]:
         choice = DUAL_DECISIONS[key] = (best, times)
     name = FORCE.get(key, choice[0])
     cfg = _parse_dual(name)
-    ws, xs = _dual_specs(x, w, x["C"], w["C"], x.get("colsum"), w.get("bsum"))
+    ws, xs = _dual_specs(x, w, x["C"], w["C"], x.get("colsum"), w.get("bsum"), w.get("gsq"))
     if cfg is None or not K.gemm_dual_ok(ws, xs, *cfg):
         name, cfg = "serial", None
     s_ev = e_ev = None

@@ -30,7 +30,7 @@ _SIGS = {
     "iit_gemm": [c_void_p] * 10 + [c_long] * 5 + [c_int] * 12 + [c_void_p],
     "iit_gemm_glds": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p] * 4,
     "iit_gemm_glds_ok": [c_void_p] * 5 + [c_long] * 5 + [c_int] * 9,
-    "iit_gemm_glds_sm": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p] * 3 + [c_int, c_void_p, c_void_p],
+    "iit_gemm_glds_sm": [c_void_p] * 8 + [c_long] * 5 + [c_int] * 8 + [c_void_p] * 3 + [c_int] + [c_void_p] * 3,
     "iit_embed_pos_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_embed_pos_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_ln_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
@@ -46,7 +46,9 @@ _SIGS = {
     "iit_ce_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "iit_ce_bwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_long, c_int, c_int, c_int,
                    c_void_p, c_void_p],
-    "iit_adam_flat": [c_void_p] * 6 + [c_int, c_void_p, c_int] + [c_float] * 6 + [c_void_p] * 4,
+    "iit_adam_flat": [c_void_p] * 6 + [c_int, c_void_p, c_int] + [c_float] * 6 + [c_void_p] * 3
+                     + [c_void_p, c_int, c_void_p, c_void_p],
+    "iit_sumsq_2d": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p],
     "iit_adam_span_size": [],
     "iit_sumsq_spans": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "iit_adam_spans": [c_void_p] * 6 + [c_int, c_void_p] + [c_float] * 6 + [c_void_p] * 4,
@@ -73,7 +75,7 @@ _SIGS = {
     "iit_gemm_glds_set_prof": [c_void_p],
     "iit_gemm_dual_ok": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 7 + [c_void_p] * 4 + [c_long] * 4 + [c_int] * 5,
     "iit_gemm_dual": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 6 + [c_void_p] * 2 + [c_void_p] * 4 + [c_long] * 4
-                     + [c_int] * 5 + [c_void_p] * 3,
+                     + [c_int] * 5 + [c_void_p] * 4,
     "iit_gemm_glds_set_group_m": [c_int],
     "iit_ioi_hl_label": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
@@ -243,7 +245,8 @@ GLDS_STORE_MODE = int(os.environ.get("IIT_GEMM_STORE", "0"))  # epilogue stores:
 
 
 def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None, bias1=None, bias2=None, resid=None,
-              ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1, csum=None, reduce=False, store_mode=None, bsum=None):
+              ldc2=0, ldr=0, bias_cols=0, tile=0, splits=1, csum=None, reduce=False, store_mode=None, bsum=None,
+              gsq=None):
     """C = A @ B (+ epilogue) on the LDS-DMA MFMA kernel; bf16 operands, M/N/K multiples of the tile.
     ``EPI_DGELU`` (mode 0): ``C2`` is the saved bf16 pre-activation (row stride ``ldc2``); ``csum`` (fp32 [N],
     optional) accumulates the column sums of the stored bf16 output.
@@ -251,7 +254,9 @@ def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None
     epilogue); with ``reduce`` they go to a workspace and the last-arriving split sums them in a fixed order
     (run-to-run deterministic, no atomics, and valid for fp32 stores too).
     ``bsum`` (mode 3 only, fp32 [N], optional): += the column sums of B over K (a weight gradient's bias gradient
-    ``colsum(dY)``), fused into the main loop, added with fp32 atomics."""
+    ``colsum(dY)``), fused into the main loop, added with fp32 atomics.
+    ``gsq`` (``EPI_F32_STORE`` only, fp32 [64], optional): += the sum of squares of the stored values (spread over the
+    64 slots) -- a weight gradient's share of the clip's global norm (:meth:`FlatParams.norm_cover`)."""
     ws = cnt = None
     if reduce:
         ws, cnt = split_workspace(M, N, tile, splits, A.device)
@@ -261,7 +266,8 @@ def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None
     sm = GLDS_STORE_MODE if store_mode is None else store_mode
     _check(lib().iit_gemm_glds_sm(_p(A), _p(B), _p(C), _p(C2), _p(bias0), _p(bias1), _p(bias2), _p(resid), lda, ldb,
                                   ldc, ldc2, ldr, M, N, K, mode, epi, bias_cols, tile, splits, _p(csum), _p(ws),
-                                  _p(cnt), int(sm), _p(bsum) if mode == 3 else None, _stream()),
+                                  _p(cnt), int(sm), _p(bsum) if mode == 3 else None,
+                                  _p(gsq) if epi == EPI_F32_STORE else None, _stream()),
            "iit_gemm_glds")
 
 
@@ -311,8 +317,16 @@ def gemm_dual(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, reduce:
     _check(lib().iit_gemm_dual(
         _p(w["A"]), _p(w["B"]), _p(w["C"]), w["lda"], w["ldb"], w["ldc"], w["M"], w["N"], w["K"], w["epi"], wtile,
         splits, _p(ws), _p(cnt), _p(x["A"]), _p(x["B"]), _p(x["C"]), _p(x.get("C2")), x["lda"], x["ldb"], x["ldc"],
-        x.get("ldc2", 0), x["M"], x["N"], x["K"], x["epi"], xtile, _p(x.get("csum")), _p(w.get("bsum")), _stream()),
+        x.get("ldc2", 0), x["M"], x["N"], x["K"], x["epi"], xtile, _p(x.get("csum")), _p(w.get("bsum")),
+        _p(w.get("gsq")) if w["epi"] == EPI_F32_STORE else None, _stream()),
         "iit_gemm_dual")
+
+
+def sumsq_2d(c, ldc: int, M: int, N: int, gsq) -> None:
+    """gsq[slot] += sum of squares of the fp32 [M][N] matrix ``c`` (row stride ``ldc``)."""
+    if CHECK_BOUNDS:
+        _bounds("sumsq_2d", ("c", c, M, N, ldc))
+    _check(lib().iit_sumsq_2d(_p(c), ldc, M, N, _p(gsq), _stream()), "sumsq_2d")
 
 
 def sumsq_spans(g, spans, nspans, part, step_dev, do_norm: bool):
@@ -594,9 +608,12 @@ def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_
     if part is None or part.numel() < nparts:
         part = flat._norm_parts = torch.zeros(nparts, dtype=torch.float32, device=flat.data.device)
     spans, nspans = flat.span_table(lib().iit_adam_span_size())
+    # fused norm: the weight gradients a GEMM stored this step already added their sums of squares into gsq
+    sq_spans, n_sq, gsq = flat.norm_spans(lib().iit_adam_span_size())
     _check(lib().iit_adam_flat(_p(flat.data), _p(flat.grad), _p(exp_avg), _p(exp_avg_sq), _p(flat.shadow),
                                _p(spans), nspans, _p(part), nparts, float(clip_norm or 0.0), lr, b1, b2, eps, wd,
-                               _p(hyper), _p(step_dev), _p(skipped), _stream()), "adam_flat")
+                               _p(hyper), _p(step_dev), _p(skipped), _p(sq_spans), n_sq, _p(gsq), _stream()),
+           "adam_flat")
     flat.after_step(mirror_written=flat.shadow is not None)
 
 

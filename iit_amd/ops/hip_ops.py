@@ -90,6 +90,16 @@ def _fused_bias(gb: Optional[torch.Tensor], N: int) -> Optional[torch.Tensor]:
     return None if deterministic() else gb
 
 
+def _norm_slots(store: bool, *ps) -> Optional[torch.Tensor]:
+    """The fused-norm slots (``FlatParams.norm_cover``) for a GEMM that stores the complete gradient of ``ps``
+    (``store``); registers the producer's capability either way (``FlatParams.norm_intent``)."""
+    flat = getattr(ps[0], "_iit_flat", None)
+    if flat is None:
+        return None
+    flat.norm_intent(*ps)
+    return flat.norm_cover(*ps) if store else None
+
+
 def _done(*params):
     for p in params:
         if p is not None and p.requires_grad:
@@ -523,7 +533,8 @@ class QKVFn(Function):
                 bs = _fused_bias(torch.as_strided(gbs[0], (3 * HD,), (1,)), 3 * HD)
             choice = gemm_pair(xspec, dict(A=x2, B=g, C=gq, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=3 * HD,
                                            mode=K.MODE_AKM | K.MODE_BKM,
-                                           epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs))
+                                           epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs,
+                                           gsq=_norm_slots(store, W_Q, W_K, W_V)))
             if store:
                 _settle_claim(choice, W_Q, W_K, W_V)
         else:
@@ -808,7 +819,8 @@ class LinearFn(Function):
             gW2 = gW.reshape(Kd, N) if gW.is_contiguous() else gW
             assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
             wspec = dict(A=x2, B=g2, C=gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode,
-                         epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs)
+                         epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs,
+                         gsq=_norm_slots(store, W))
             choice = gemm_pair(xspec, wspec) if xspec is not None else gemm(**wspec)
             if store:
                 _settle_claim(choice, W)
@@ -872,7 +884,8 @@ class MLPInFn(Function):
         if gW is not None:
             choice = gemm_pair(xspec, dict(A=x2, B=dpre, C=gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm,
                                            mode=K.MODE_AKM | K.MODE_BKM,
-                                           epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs))
+                                           epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs,
+                                           gsq=_norm_slots(store, W_in)))
             if store:
                 _settle_claim(choice, W_in)
         else:
@@ -948,7 +961,7 @@ class MLPOutGeluFn(Function):
             assert gW2.stride(-1) == 1 and gW2.dim() == 2, "weight gradient must have unit column stride"
             wspec = dict(A=x2, B=g2, C=gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0),
                          mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store,
-                         bsum=bs)
+                         bsum=bs, gsq=_norm_slots(store, W))
             choice = gemm_pair(xspec, wspec) if xspec is not None else gemm(**wspec)
             if store:
                 _settle_claim(choice, W)

@@ -52,13 +52,15 @@ def test_dual_matches_fp32(K, wt, xt, variant):
     csum0 = csum.clone() if csum is not None else None
     bsum0 = torch.randn(NOUT, device=dev)
     bsum = bsum0.clone()
-    ws = dict(A=x, B=dy, C=gW, M=KIN, N=NOUT, K=T, lda=KIN, ldb=NOUT, ldc=NOUT, epi=wepi, bsum=bsum)
+    gsq = torch.zeros(64, device=dev)
+    ws = dict(A=x, B=dy, C=gW, M=KIN, N=NOUT, K=T, lda=KIN, ldb=NOUT, ldc=NOUT, epi=wepi, bsum=bsum, gsq=gsq)
     xs = dict(A=dy, B=w, C=dX, C2=pre if xepi == K.EPI_DGELU else None, M=T, N=KIN, K=NOUT, lda=NOUT, ldb=NOUT,
               ldc=KIN, ldc2=KIN, epi=xepi, csum=csum)
     assert K.gemm_dual_ok(ws, xs, wt, xt, splits, reduce)
     for rep in range(2):  # a second launch reuses the reduction tickets the first one re-armed
         gW.copy_(gW0)
         bsum.copy_(bsum0)
+        gsq.zero_()
         if csum is not None:
             csum.copy_(csum0)
         K.gemm_dual(ws, xs, wt, xt, splits, reduce)
@@ -66,6 +68,10 @@ def test_dual_matches_fp32(K, wt, xt, variant):
         ref_w = x.float().t() @ dy.float() + (gW0 if wepi == K.EPI_F32_ACC else 0)
         torch.testing.assert_close(gW, ref_w, rtol=1e-4, atol=2e-3)
         torch.testing.assert_close(bsum, bsum0 + dy.float().sum(0), rtol=1e-4, atol=2e-3)  # fused bias gradient
+        if wepi == K.EPI_F32_STORE:  # fused sum of squares of the stored gradient (the clip's norm share)
+            torch.testing.assert_close(gsq.sum(), gW.double().pow(2).sum().float(), rtol=1e-4, atol=1e-3)
+        else:
+            assert float(gsq.abs().sum()) == 0.0
         ref_x = dy.float() @ w.float().t()
         if xepi == K.EPI_DGELU:
             p = pre.float().requires_grad_(True)
@@ -124,8 +130,11 @@ def test_glds_weight_grad_bias_sums(K, tile, epi, splits, reduce):
               reduce=reduce)
     if not K.gemm_glds_ok(x, dy, C, **{k: v for k, v in kw.items()}):
         pytest.skip("tile does not cover this case")
-    K.gemm_glds(x, dy, C, bsum=bs, **kw)
+    sq = torch.zeros(64, device=dev)
+    K.gemm_glds(x, dy, C, bsum=bs, gsq=sq, **kw)
     torch.cuda.synchronize()
     ref = x.float().t() @ dy.float() + (C0 if epi == K.EPI_F32_ACC else 0)
     torch.testing.assert_close(C, ref, rtol=1e-4, atol=2e-3)
     torch.testing.assert_close(bs, bs0 + dy.float().sum(0), rtol=1e-4, atol=2e-3)
+    if epi == K.EPI_F32_STORE:
+        torch.testing.assert_close(sq.sum(), C.double().pow(2).sum().float(), rtol=1e-4, atol=1e-2)

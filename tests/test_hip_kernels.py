@@ -351,3 +351,12 @@ def test_cross_entropy_grad_bf16_twin(K):
     ref = (logits.softmax(-1) - torch.nn.functional.one_hot(labels, V)) / R
     assert rel_err(out[:, :V], ref) < 1e-5 and out[:, V:].abs().max() == 0
     assert torch.equal(out16, out.bfloat16())
+
+
+def test_sumsq_2d_kernel(K):
+    """gsq slots += sum of squares of a strided fp32 matrix (the fused-norm pass after a library GEMM)."""
+    torch.manual_seed(13)
+    c = torch.randn(300, 520, device=dev)
+    gsq = torch.zeros(64, device=dev)
+    K.sumsq_2d(c, 520, 300, 512, gsq)
+    torch.testing.assert_close(gsq.sum(), c[:, :512].double().pow(2).sum().float(), rtol=1e-5, atol=1e-2)
