@@ -45,13 +45,19 @@ __global__ __launch_bounds__(TW::NW * 64, TW::OCC) void gemm_dual_kernel(G2Args 
 //   paired forward at ~1 PF/s (fewer operand bytes per flop than 128x128), which alone leave most of the CUs idle on a
 //   [768][N] weight gradient; here the dX tiles fill them.  (A 256x192 dW tile spills registers: not offered.)
 // (index -> the single-launch tile id of the same shape, for the shape checks)
-constexpr int kWTiles = 7, kXTiles = 7;
-const int kWTileId[kWTiles] = {23, 25, 26, 24, 3, 7, 6};
-const int kXTileId[kXTiles] = {23, 24, 27, 25, 5, 7, 6};
-const int kWBM[kWTiles] = {128, 128, 96, 64, 64, 256, 128}, kWBN[kWTiles] = {96, 128, 96, 96, 64, 128, 128};
-const int kXBM[kXTiles] = {128, 64, 128, 128, 256, 256, 128}, kXBN[kXTiles] = {96, 96, 192, 128, 192, 128, 128};
-__host__ __device__ constexpr bool w_big(int t) { return t >= 5; }
-__host__ __device__ constexpr bool x_big(int t) { return t >= 4; }
+// * 4 waves, one workgroup per CU, deep rings (3-4 K-tiles, up to 128 KiB): dW 128x128, 128x96, dX 128x128,
+//   128x192 -- more operand bytes in flight for the operands that come cold from HBM inside the step (the
+//   activations saved by the forward), where the two-stage rings of the two-per-CU tiles wait on the fill.
+constexpr int kWTiles = 9, kXTiles = 9;
+const int kWTileId[kWTiles] = {23, 25, 26, 24, 3, 7, 6, 4, 13};
+const int kXTileId[kXTiles] = {23, 24, 27, 25, 5, 7, 6, 4, 22};
+const int kWBM[kWTiles] = {128, 128, 96, 64, 64, 256, 128, 128, 128};
+const int kWBN[kWTiles] = {96, 128, 96, 96, 64, 128, 128, 128, 96};
+const int kXBM[kXTiles] = {128, 64, 128, 128, 256, 256, 128, 128, 128};
+const int kXBN[kXTiles] = {96, 96, 192, 128, 192, 128, 128, 128, 192};
+// tile family: 0 = 4 waves x 2 per CU, 1 = 8 waves x 1 per CU, 2 = 4 waves x 1 per CU with deep rings
+__host__ __device__ constexpr int w_family(int t) { return t >= 7 ? 2 : (t >= 5 ? 1 : 0); }
+__host__ __device__ constexpr int x_family(int t) { return t >= 7 ? 2 : (t >= 4 ? 1 : 0); }
 
 template <class TW, int EW, class TX, int EX>
 hipError_t launch2(const G2Args& w, const G2Args& x, int w_splits, hipStream_t s) {
@@ -63,7 +69,13 @@ hipError_t launch2(const G2Args& w, const G2Args& x, int w_splits, hipStream_t s
 
 template <class TW, int EW, int EX>
 hipError_t pick_x(const G2Args& w, const G2Args& x, int w_splits, int xtile, hipStream_t s) {
-  if constexpr (TW::NW == 4) {
+  if constexpr (TW::NW == 4 && TW::OCC == 1) {
+    switch (xtile) {
+      case 7: return launch2<TW, EW, Cfg<128, 128, 4, 4, 1>, EX>(w, x, w_splits, s);
+      case 8: return launch2<TW, EW, Cfg<128, 192, 3, 4, 1>, EX>(w, x, w_splits, s);
+      default: return hipErrorInvalidValue;
+    }
+  } else if constexpr (TW::NW == 4) {
     switch (xtile) {
       case 0: return launch2<TW, EW, Cfg<128, 96, 2>, EX>(w, x, w_splits, s);
       case 1: return launch2<TW, EW, Cfg<64, 96, 3>, EX>(w, x, w_splits, s);
@@ -91,6 +103,8 @@ hipError_t pick_w(const G2Args& w, const G2Args& x, int w_splits, int wtile, int
     case 4: return pick_x<Cfg<64, 64, 4>, EW, EX>(w, x, w_splits, xtile, s);
     case 5: return pick_x<Cfg<256, 128, 2, 8, 1>, EW, EX>(w, x, w_splits, xtile, s);
     case 6: return pick_x<Cfg<128, 128, 4, 8, 1>, EW, EX>(w, x, w_splits, xtile, s);
+    case 7: return pick_x<Cfg<128, 128, 4, 4, 1>, EW, EX>(w, x, w_splits, xtile, s);
+    case 8: return pick_x<Cfg<128, 96, 4, 4, 1>, EW, EX>(w, x, w_splits, xtile, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -113,7 +127,7 @@ IIT_EXPORT int iit_gemm_dual_ok(const void* wA, const void* wB, const void* wC, 
                                 int wN, int wK, int wepi, int wtile, int wsplits, int reduce, const void* xA,
                                 const void* xB, const void* xC, const void* xC2, long xlda, long xldb, long xldc,
                                 long xldc2, int xM, int xN, int xK, int xepi, int xtile) {
-  if (wtile < 0 || wtile >= kWTiles || xtile < 0 || xtile >= kXTiles || w_big(wtile) != x_big(xtile)) return 0;
+  if (wtile < 0 || wtile >= kWTiles || xtile < 0 || xtile >= kXTiles || w_family(wtile) != x_family(xtile)) return 0;
   if (!(wepi == E_F32_STORE || wepi == E_F32_ACC) || !(xepi == E_BF16 || xepi == E_DGELU)) return 0;
   if (!iit_gemm_glds_ok(wA, wB, wC, nullptr, nullptr, wlda, wldb, wldc, 0, 0, wM, wN, wK, 3, wepi, 0,
                         kWTileId[wtile], wsplits, reduce))

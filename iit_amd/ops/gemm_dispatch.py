@@ -456,7 +456,7 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
                 whole = gemm(A, B, C, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=C2, C3=C3,
                              bias0=bias0, bias1=bias1, bias2=bias2, resid=resid, ldr=ldr, aux=aux, ldc2=ldc2,
                              bias_cols=bias_cols, qkv=qkv, splits=splits, blas_bias=blas_bias, fresh=fresh,
-                             _decide_only=True, _no_split=True)
+                             bsum=bsum, gsq=gsq, _decide_only=True, _no_split=True)
                 pieces = [run(bulk, True), run(tail, True)]
                 split = RAGGED[rkey] = (None not in pieces and whole is not None and sum(pieces) < whole,
                                         whole, pieces)

@@ -274,16 +274,20 @@ def gemm_glds(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, bias0=None
 # ------------------------------------------------------------------------------ dual GEMM (csrc/gemm_dual.hip)
 # one launch runs a layer's weight gradient dW = X^T dY (mode 3; fp32 store / accumulate, optional K-split) and its
 # input gradient dX = dY W^T (mode 0; bf16 or the fused dgelu epilogue), two workgroups per CU
-# two families (a launch takes both tiles from one): 4-wave tiles, two workgroups per CU (W 0-4, X 0-3), and 8-wave
-# tiles, one per CU (W 5-6, X 4-6)
+# three families (a launch takes both tiles from one): 4-wave tiles, two workgroups per CU (W 0-4, X 0-3); 8-wave
+# tiles, one per CU (W 5-6, X 4-6); 4-wave tiles, one per CU with 3-4 deep rings (W 7-8, X 7-8)
 DUAL_W_TILES = {0: (128, 96), 1: (128, 128), 2: (96, 96), 3: (64, 96), 4: (64, 64),
-                5: (256, 128), 6: (128, 128)}
+                5: (256, 128), 6: (128, 128), 7: (128, 128), 8: (128, 96)}
 DUAL_X_TILES = {0: (128, 96), 1: (64, 96), 2: (128, 192), 3: (128, 128),
-                4: (256, 192), 5: (256, 128), 6: (128, 128)}
+                4: (256, 192), 5: (256, 128), 6: (128, 128), 7: (128, 128), 8: (128, 192)}
+
+
+def _dual_family(t: int, first_big: int) -> int:
+    return 2 if t >= 7 else (1 if t >= first_big else 0)
 
 
 def dual_family_ok(wtile: int, xtile: int) -> bool:
-    return (wtile >= 5) == (xtile >= 4)
+    return _dual_family(wtile, 5) == _dual_family(xtile, 4)
 
 
 def _bf16_cuda(*ts) -> bool:

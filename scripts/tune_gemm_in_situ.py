@@ -57,7 +57,18 @@ def main():
         finite = {k: v for k, v in times.items() if v == v}
         if len(finite) < 2 or min(finite.values()) < a.min_us:
             continue
-        cands[key] = sorted(finite, key=finite.get)[:a.top]
+        ranked = sorted(finite, key=finite.get)
+        cands[key] = ranked[:a.top]
+        if key in gd.DUAL_DECISIONS:
+            # the 8-wave dual family (one big tile per CU, two waves per SIMD) hides cold-operand latency that the
+            # isolated (L2-hot) timing does not show: its best configuration always competes in context
+            extra = []
+            for fam in ((5, 6), (7, 8)):  # the best of the 8-wave and of the deep-ring family
+                best = [n for n in ranked if (gd._parse_dual(n) or (-1,))[0] in fam]
+                if best and best[0] not in cands[key]:
+                    extra.append(best[0])
+            if extra:
+                cands[key] = ranked[:max(1, a.top - len(extra))] + extra
     print(f"{len(cands)} problems to tune in context", flush=True)
 
     samples = collections.defaultdict(list)  # (key, cand) -> [us]

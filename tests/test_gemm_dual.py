@@ -25,7 +25,8 @@ def _problem(seed, kin=KIN, nout=NOUT):
 
 
 # (dW tile, dX tile) pairs: every pair of the 4-wave family, every pair of the 8-wave family
-PAIRS = [(wt, xt) for wt in range(5) for xt in range(4)] + [(wt, xt) for wt in (5, 6) for xt in (4, 5, 6)]
+PAIRS = ([(wt, xt) for wt in range(5) for xt in range(4)] + [(wt, xt) for wt in (5, 6) for xt in (4, 5, 6)]
+         + [(wt, xt) for wt in (7, 8) for xt in (7, 8)])
 
 
 VARIANTS = [  # (dW epilogue, dX epilogue, splits, reduce)
