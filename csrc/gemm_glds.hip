@@ -125,8 +125,9 @@ IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, con
                                 long lda, long ldb, long ldc, long ldc2, long ldr, int M, int N, int K, int mode,
                                 int epi, int bias_cols, int tile, int splits, int reduce) {
   if (tile < 0 || tile >= IIT_GLDS_TILES || tile == 19) return 0;
-  // atomic split-K: fp32 accumulate only; reduction split-K (``reduce``): fp32 accumulate or store
-  const bool split_epi = epi == E_F32_ACC || (reduce && epi == E_F32_STORE);
+  // atomic split-K: fp32 accumulate only; reduction split-K (``reduce``): fp32 accumulate, store or residual add (the
+  // last-arriving split runs the epilogue once on the summed tile)
+  const bool split_epi = epi == E_F32_ACC || (reduce && (epi == E_F32_STORE || epi == E_F32_RESID));
   const int bk = kTileBK[tile];
   if (splits < 1 || (splits > 1 && (!split_epi || K % (bk * splits)))) return 0;
   if (reduce && splits < 2) return 0;

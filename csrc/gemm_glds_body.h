@@ -474,7 +474,7 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
       }
     }
   }
-  if constexpr (EPI == E_F32_ACC || EPI == E_F32_STORE) {
+  if constexpr (EPI == E_F32_ACC || EPI == E_F32_STORE || EPI == E_F32_RESID) {
     if (p.ws != nullptr) {
       // Partial tile in MFMA register order (one 16-B chunk per lane per accumulator: 1 KiB coalesced per wave),
       // published without any L2 writeback / invalidate: write-through (sc1) stores, drained with vmcnt(0) before

@@ -330,7 +330,10 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
             # the weight gradients (X^T dY, reduction over the tokens) also get the deterministic reduction split:
             # larger tiles per CU (fewer operand bytes per flop) without fp32 atomics; they only run in backward
             # passes, which are serial on one stream
-            if mode == 3 and epi in (K_.EPI_F32_ACC, K_.EPI_F32_STORE):
+            # ... and so do the long-K fp32 residual GEMMs (W_out's forward, K = d_mlp: [T][768] outputs are too few
+            # big tiles for 256 CUs; the last-arriving split adds bias + residual once)
+            if (mode == 3 and epi in (K_.EPI_F32_ACC, K_.EPI_F32_STORE)) or \
+                    (mode == 2 and epi == K_.EPI_F32_RESID and Kd >= 2048 and bias_cols == 0):
                 for sp in (2, 4):
                     if Kd // sp < 256 or not K_.gemm_glds_ok(A, B, C, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc,
                                                              mode=mode, epi=epi, resid=resid, ldr=ldr, tile=tile,

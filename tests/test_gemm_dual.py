@@ -139,3 +139,30 @@ def test_glds_weight_grad_bias_sums(K, tile, epi, splits, reduce):
     torch.testing.assert_close(bs, bs0 + dy.float().sum(0), rtol=1e-4, atol=2e-3)
     if epi == K.EPI_F32_STORE:
         torch.testing.assert_close(sq.sum(), C.double().pow(2).sum().float(), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("tile", [5, 7, 9, 23, 25])
+@pytest.mark.parametrize("splits", [2, 4])
+def test_glds_residual_reduction_split(K, tile, splits):
+    """Forward fp32 residual GEMM (mode 2, ``resid + x W + b``) with the deterministic reduction split-K: the
+    last-arriving split adds bias and residual once; bit-identical across launches."""
+    bm, bn = K.GLDS_TILES[tile]
+    M, N, Kd = bm * 2, bn * 2, 1024
+    torch.manual_seed(tile + splits)
+    x = torch.randn(M, Kd, device=dev).bfloat16()
+    w = (torch.randn(Kd, N, device=dev) / 16).bfloat16()
+    resid = torch.randn(M, N, device=dev)
+    bias = torch.randn(N, device=dev)
+    kw = dict(M=M, N=N, K=Kd, lda=Kd, ldb=N, ldc=N, mode=K.MODE_BKM, epi=K.EPI_F32_RESID, resid=resid, ldr=N,
+              tile=tile, splits=splits, reduce=True)
+    C = torch.empty(M, N, device=dev)
+    assert K.gemm_glds_ok(x, w, C, **kw)
+    outs = []
+    for _ in range(2):
+        C.fill_(float("nan"))
+        K.gemm_glds(x, w, C, bias0=bias, **kw)
+        torch.cuda.synchronize()
+        outs.append(C.clone())
+    ref = resid + x.float() @ w.float() + bias
+    torch.testing.assert_close(outs[0], ref, rtol=1e-4, atol=2e-3)
+    assert torch.equal(outs[0], outs[1])
