@@ -69,6 +69,11 @@ def main():
                     extra.append(best[0])
             if extra:
                 cands[key] = ranked[:max(1, a.top - len(extra))] + extra
+        elif key[4] == 2:  # fp32 residual GEMMs: the best reduction split competes (its partials are L2 traffic
+            # that the isolated timing under-prices, and its extra workgroups fill CUs the whole tiles leave idle)
+            red = [n for n in ranked if "r" in n[4:]]
+            if red and red[0] not in cands[key]:
+                cands[key] = ranked[:a.top - 1] + [red[0]]
     print(f"{len(cands)} problems to tune in context", flush=True)
 
     samples = collections.defaultdict(list)  # (key, cand) -> [us]

@@ -360,3 +360,21 @@ def test_sumsq_2d_kernel(K):
     gsq = torch.zeros(64, device=dev)
     K.sumsq_2d(c, 520, 300, 512, gsq)
     torch.testing.assert_close(gsq.sum(), c[:, :512].double().pow(2).sum().float(), rtol=1e-5, atol=1e-2)
+
+
+@pytest.mark.parametrize("T,d,vocab", [(4096, 768, 40), (1000, 768, 5000), (130, 64, 3)])
+def test_embed_bwd_combined_rows(K, T, d, vocab):
+    """Embedding backward (chunked, equal tokens pre-combined in LDS) == index_add over the positions; W_pos too."""
+    torch.manual_seed(T + vocab)
+    S = 10 if T % 10 == 0 else 1
+    B = T // S
+    tok = torch.randint(0, vocab, (B, S), device=dev)
+    g = torch.randn(B, S, d, device=dev)
+    dWE = torch.randn(vocab, d, device=dev)
+    dWpos = torch.randn(S, d, device=dev)
+    ref_E = dWE.clone().index_add_(0, tok.reshape(-1), g.reshape(-1, d))
+    ref_pos = dWpos + g.sum(0)
+    K.embed_pos_bwd(tok, g, dWE, dWpos, B, S, d)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dWE, ref_E, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(dWpos, ref_pos, rtol=1e-5, atol=1e-4)
