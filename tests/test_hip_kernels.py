@@ -363,8 +363,8 @@ def test_sumsq_2d_kernel(K):
 
 
 @pytest.mark.parametrize("T,d,vocab", [(4096, 768, 40), (1000, 768, 5000), (130, 64, 3)])
-def test_embed_bwd_combined_rows(K, T, d, vocab):
-    """Embedding backward (chunked, equal tokens pre-combined in LDS) == index_add over the positions; W_pos too."""
+def test_embed_bwd_repeated_tokens(K, T, d, vocab):
+    """Embedding backward (atomic row adds, many repeated tokens) == index_add over the positions; W_pos too."""
     torch.manual_seed(T + vocab)
     S = 10 if T % 10 == 0 else 1
     B = T // S
