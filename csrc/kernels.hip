@@ -212,9 +212,7 @@ IIT_EXPORT int iit_ln_fwd(const float* x, const float* w, const float* b, void* 
 // separate gradient-sum pass over the fp32 residual.  ``dx16`` (nullable) receives a bf16 copy of dx: the
 // next backward GEMMs (W_O / W_out dX and dW) read bf16, so the cast rides along with this pass.
 // The affine gradients dw/db are NOT done here (see ln_dwdb_kernel: per-block partial sums, few atomics).
-// XH16: ``x`` is the forward's bf16 output xhat (a norm without affine parameters, LNPre): the backward reads 2 bytes
-// per element instead of the fp32 input and needs no mean
-template <int V4, bool DY_F32, bool XH16 = false>
+template <int V4, bool DY_F32>
 __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
                                                          const float* __restrict__ w, float* __restrict__ dx,
@@ -238,13 +236,8 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const void* __restrict_
         const bf16x4 t = ((const bf16x4*)dy_)[(long)row * d4 + c];
         dy = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
       }
-      if constexpr (XH16) {
-        const bf16x4 t = ((const bf16x4*)x)[(long)row * d4 + c];
-        xv = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
-      } else {
-        const float4 xx = ((const float4*)x)[(long)row * d4 + c];
-        xv = make_float4((xx.x - mu) * rs, (xx.y - mu) * rs, (xx.z - mu) * rs, (xx.w - mu) * rs);
-      }
+      const float4 xx = ((const float4*)x)[(long)row * d4 + c];
+      xv = make_float4((xx.x - mu) * rs, (xx.y - mu) * rs, (xx.z - mu) * rs, (xx.w - mu) * rs);
       if (w) {
         const float4 ww = ((const float4*)w)[c];
         dy.x *= ww.x; dy.y *= ww.y; dy.z *= ww.z; dy.w *= ww.w;
@@ -352,26 +345,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
   }
 }
 
-// ``xhat16``: ``x`` is the forward's bf16 output of a norm without weight / bias (see ln_bwd_vec_kernel's XH16)
 IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
                           const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db, int T, int d,
-                          int accumulate, int xhat16, void* stream) {
+                          int accumulate, void* stream) {
   dim3 grid((T + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
   __bf16* d16 = (__bf16*)dx16;
-  if (xhat16) {
-    if (w || dw || db || d % 4 || d > 4096 || (((uintptr_t)x) & 7) || !aligned16(dx) || (dres && !aligned16(dres)) ||
-        (dy_f32 ? !aligned16(dy) : (((uintptr_t)dy) & 7) != 0) || (((uintptr_t)dx16) & 7))
-      return (int)hipErrorInvalidValue;
-#define LNBX(V)                                                                                                   \
-  if (dy_f32) hipLaunchKernelGGL((ln_bwd_vec_kernel<V, true, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate); \
-  else hipLaunchKernelGGL((ln_bwd_vec_kernel<V, false, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate);
-    const int v4 = (d / 4 + 63) / 64;
-    if (v4 <= 1) { LNBX(1) } else if (v4 <= 2) { LNBX(2) } else if (v4 <= 3) { LNBX(3) } else if (v4 <= 4) { LNBX(4) }
-    else if (v4 <= 6) { LNBX(6) } else if (v4 <= 8) { LNBX(8) } else if (v4 <= 12) { LNBX(12) } else { LNBX(16) }
-#undef LNBX
-    return hipGetLastError();
-  }
   const bool vec = d % 4 == 0 && d <= 4096 && aligned16(x) && aligned16(dx) && (!dres || aligned16(dres)) &&
                    (!w || aligned16(w)) && (dy_f32 ? aligned16(dy) : (((uintptr_t)dy) & 7) == 0) &&
                    (((uintptr_t)dx16) & 7) == 0;

@@ -34,7 +34,7 @@ _SIGS = {
     "iit_embed_pos_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_embed_pos_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_ln_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
-    "iit_ln_bwd": [c_void_p, c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_int, c_void_p],
+    "iit_ln_bwd": [c_void_p, c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_void_p],
     "iit_attn_small_fwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float, c_int,
                                             c_void_p],
     "iit_attn_small_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
@@ -374,14 +374,12 @@ def ln_fwd(x, w, b, y, mean, rstd, T, d, eps):
 
 
 def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False, dres=None, dx16=None):
-    """dx = LN'(dy) (+ dres, the skip-connection gradient, fp32 [T, d]); ``dx16`` (optional) gets a bf16 copy.
-    ``x`` may be the forward's bf16 output of a norm without weight and bias (the normalised input itself)."""
+    """dx = LN'(dy) (+ dres, the skip-connection gradient, fp32 [T, d]); ``dx16`` (optional) gets a bf16 copy."""
     if CHECK_BOUNDS:
         _bounds("ln_bwd", ("dy", dy, T, d, d), ("x", x, T, d, d), ("dx", dx, T, d, d), ("dres", dres, T, d, d),
                 ("dx16", dx16, T, d, d), ("mean", mean, 1, T, T))
     _check(lib().iit_ln_bwd(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx),
-                            _p(dres), _p(dx16), _p(dw), _p(db), T, d, int(accumulate),
-                            int(x.dtype == torch.bfloat16), _stream()), "ln_bwd")
+                            _p(dres), _p(dx16), _p(dw), _p(db), T, d, int(accumulate), _stream()), "ln_bwd")
 
 
 def heads_to_mask(heads: Optional[Sequence[int]]) -> int:

@@ -432,14 +432,6 @@ def _bf16_of(t: torch.Tensor) -> torch.Tensor:
     return t.to(BF16)
 
 
-_LN_XHAT16 = os.environ.get("IIT_LN_XHAT16", "1") != "0"
-
-
-def _xhat16_ok(w, b, d: int) -> bool:
-    """The LN backward may read the forward's bf16 output as xhat (``IIT_LN_XHAT16=0``: the fp32 input)."""
-    return _LN_XHAT16 and w is None and b is None and d % 4 == 0 and d <= 4096
-
-
 class LayerNormForkFn(Function):
     """``(LN(x), x)``: the second output carries the residual stream past the norm, so the backward gets
     both gradients and sums them inside the LN-backward kernel (no separate autograd add over [T, d])."""
@@ -455,9 +447,7 @@ class LayerNormForkFn(Function):
         mean = torch.empty(T, dtype=F32, device=x.device)
         rstd = torch.empty(T, dtype=F32, device=x.device)
         K.ln_fwd(x2, w, b, y, mean, rstd, T, d, eps)
-        # a norm without weight / bias outputs xhat itself: the backward reads the bf16 output (2 B / element)
-        # instead of the fp32 input
-        ctx.save_for_backward(y if _xhat16_ok(w, b, d) else x2, mean, rstd)
+        ctx.save_for_backward(x2, mean, rstd)
         ctx.params = (w, b)
         ctx.in_dtype = x.dtype
         return y.view(*shape[:-1], d), x.view_as(x)
@@ -1090,7 +1080,7 @@ class LayerNormForkPairFn(LayerNormForkFn):
         mean = torch.empty(T2, dtype=F32, device=x.device)
         rstd = torch.empty(T2, dtype=F32, device=x.device)
         K.ln_fwd(x2, w, b, y, mean, rstd, T2, d, eps)
-        ctx.save_for_backward(y[:T] if _xhat16_ok(w, b, d) else x2[:T], mean[:T], rstd[:T])
+        ctx.save_for_backward(x2[:T], mean[:T], rstd[:T])
         ctx.params = (w, b)
         ctx.in_dtype = x.dtype
         yf = y.view(*x_full.shape[:-1], d)
