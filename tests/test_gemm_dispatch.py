@@ -115,3 +115,34 @@ def test_ragged_split_pieces_cover_the_problem():
     # aligned or small problems are left whole
     assert gd._ragged_split(A, B, C, M=T, N=4096, K=d, lda=d, ldb=50264, mode=K.MODE_BKM, epi=K.EPI_F32_STORE,
                             C2=None, bias0=None, resid=None, aux=None) is None
+
+
+def test_dual_name_parsing_and_families():
+    """Dual-launch candidate names round-trip to (dW tile, dX tile, splits, reduce); the tile families pair up."""
+    assert gd._parse_dual("dual1.3") == (1, 3, 1, False)
+    assert gd._parse_dual("dual0.3r2") == (0, 3, 2, True)
+    assert gd._parse_dual("dual4.3k2") == (4, 3, 2, False)
+    assert gd._parse_dual("serial") is None and gd._parse_dual("glds5") is None
+    assert K.dual_family_ok(0, 3) and K.dual_family_ok(5, 4) and K.dual_family_ok(7, 8)
+    assert not K.dual_family_ok(0, 4) and not K.dual_family_ok(5, 7) and not K.dual_family_ok(7, 0)
+
+
+def test_gemm_pair_falls_back_to_serial_off_gpu(monkeypatch):
+    """On the CPU (or for a pair the dual kernel does not cover) gemm_pair runs both GEMMs one after the other."""
+    torch.manual_seed(0)
+    xs0 = dict(A=torch.zeros(1), mode=0, epi=K.EPI_BF16)
+    ws0 = dict(mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE)
+    assert not gd._dual_eligible(xs0, ws0)  # CPU tensors
+    monkeypatch.setattr(gd, "POLICY", "blas")  # no device timing on the CPU
+    T, kin, n = 32, 16, 24
+    x = torch.randn(T, kin).bfloat16()
+    dy = torch.randn(T, n).bfloat16()
+    w = torch.randn(kin, n).bfloat16()
+    dX = torch.empty(T, kin, dtype=torch.bfloat16)
+    gW = torch.empty(kin, n)
+    xs = dict(A=dy, B=w, C=dX, M=T, N=kin, K=n, lda=n, ldb=n, ldc=kin, epi=K.EPI_BF16)
+    ws = dict(A=x, B=dy, C=gW, M=kin, N=n, K=T, lda=kin, ldb=n, ldc=n, mode=K.MODE_AKM | K.MODE_BKM,
+              epi=K.EPI_F32_STORE, fresh=True)
+    gd.gemm_pair(xs, ws)
+    torch.testing.assert_close(gW, x.float().t() @ dy.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dX.float(), (dy.float() @ w.float().t()), rtol=2e-2, atol=5e-2)
