@@ -7,7 +7,7 @@ fused clip+Adam.  The only host decisions are the node samples, taken from the
 pair's RNG *before* the phase runs.  So :class:`GraphedTrainStep`:
 
 * keeps static device buffers for the batch (each new batch is copied in: six
-  small ``copy_`` launches);
+  small tensors, copied with one multi-tensor launch per dtype);
 * runs the first ``warmup`` occurrences of every phase key eagerly (this also
   settles lazily-built state: GEMM autotune decisions, the bf16 weight mirror,
   hipBLASLt heuristics), then captures the phase once with
@@ -79,6 +79,22 @@ def _detach_out(out):
         return loss.detach(), {k: v.detach() for k, v in extras.items()}
     return out.detach()
 
+
+
+_FOREACH_COPY = os.environ.get("IIT_FOREACH_COPY", "1") != "0"
+
+
+def _copy_all(dst, src) -> None:
+    """Batch tensors into the static graph inputs: one multi-tensor launch per dtype instead of a copy per tensor
+    (``IIT_FOREACH_COPY=0``: a copy per tensor)."""
+    if _FOREACH_COPY:
+        try:
+            torch._foreach_copy_(list(dst), list(src), non_blocking=True)
+            return
+        except (RuntimeError, TypeError, AttributeError):  # pragma: no cover - older torch / unsupported layouts
+            pass
+    for d, s_ in zip(dst, src):
+        d.copy_(s_, non_blocking=True)
 
 class _CaptureGC:
     """Context for a graph capture: collect cyclic garbage first, keep the collector off during the capture.
@@ -176,8 +192,7 @@ class GraphedTrainStep:
         if sig != self._sig:  # e.g. a short last batch: eager, keep the captured buffers
             return base, abl, True
         sb, sa = self._static
-        for d, src in zip(sb + sa, tuple(base) + tuple(abl)):
-            d.copy_(src, non_blocking=True)
+        _copy_all(sb + sa, tuple(base) + tuple(abl))
         return sb, sa, False
 
     # ------------------------------------------------------------------ phases
@@ -509,8 +524,7 @@ class GraphedEvalStep:
         if sig != self._sig:
             return self._eager(base, abl)
         sb, sa = self._static
-        for d, src in zip(sb + sa, tuple(base) + tuple(abl)):
-            d.copy_(src, non_blocking=True)
+        _copy_all(sb + sa, tuple(base) + tuple(abl))
         key = (node.name, sig)
         ent = self.graphs.get(key)
         if ent is None:
