@@ -667,9 +667,18 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
   }
   }  // chunk
   if constexpr (EPI == E_F32_STORE) {
-    if (p.gsq) {
+    if (p.gsq) {  // one atomic per workgroup (the waves' sums meet in LDS): thousands of tiles share 64 slots
       sq = wave_sum(sq);
-      if (lane == 0) atomicAdd(p.gsq + ((lin * NW + wave) & 63), sq);
+      float* red = (float*)smem;
+      __syncthreads();  // every thread is done with the epilogue's LDS tile
+      if (lane == 0) red[wave] = sq;
+      __syncthreads();
+      if (tid == 0) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) t += red[w];
+        atomicAdd(p.gsq + (lin & 63), t);
+      }
     }
   }
   if (p.prof != nullptr) {  // drain this workgroup's stores, then stamp (diagnostic path only)

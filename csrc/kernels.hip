@@ -699,7 +699,7 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
                                                         int nspans, const float* __restrict__ part, int nparts,
                                                         float clip, float lr, float b1, float b2, float eps, float wd,
                                                         const float* __restrict__ hyper, int* __restrict__ step,
-                                                        int* __restrict__ skipped) {
+                                                        int* __restrict__ skipped, int book = 1) {
   // ``hyper`` (nullable): device copy of {lr, beta1, beta2, eps, weight_decay}.  A captured graph replays the
   // kernel arguments it saw at capture; reading the hyper-parameters from device memory lets the host change the
   // learning rate (an LR scheduler) between replays with one small copy.
@@ -724,7 +724,7 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
   }
   __syncthreads();
   if (bad_s) {  // non-finite gradient: skip the whole update (uniform over the grid), count it, undo the step bump
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (book && blockIdx.x == 0 && threadIdx.x == 0) {  // (one launch of a chunked update keeps the books)
       step[0] -= 1;
       skipped[0] += 1;
     }
@@ -889,6 +889,28 @@ IIT_EXPORT int iit_adam_spans(float* p, const float* g, float* m, float* v, void
   hipLaunchKernelGGL((adam_span_kernel<true, 1>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
                      (__bf16*)mirror, (const Span*)spans, nspans, total, 1, clip, lr, b1, b2, eps, wd, hyper, step,
                      skipped);
+  return hipGetLastError();
+}
+
+// Chunked update (iit_amd/ops/optim.py, overlapped Adam): the norm stage alone, then the Adam pass over a slice of the
+// span table per launch -- the next forward's layers each wait for the slice holding their weights.  ``book`` marks
+// the one launch that undoes the step bump / counts a skipped (non-finite) step.
+IIT_EXPORT int iit_adam_norm(const float* g, const void* spans, int nspans, float* part, int nparts, int do_norm,
+                             int* step, float* gsq, void* stream) {
+  hipLaunchKernelGGL(sumsq_span_kernel, dim3(do_norm ? nparts : 1), dim3(256), 0, (hipStream_t)stream, g,
+                     (const Span*)spans, nspans, part, do_norm, step, gsq);
+  return hipGetLastError();
+}
+
+IIT_EXPORT int iit_adam_chunk(float* p, const float* g, float* m, float* v, void* mirror, const void* spans,
+                              int nspans, const float* part, int nparts, float clip, float lr, float b1, float b2,
+                              float eps, float wd, const float* hyper, int* step, int* skipped, int book,
+                              void* stream) {
+  if (nspans <= 0) return hipSuccess;
+  const int blocks = min(nspans, 4096);
+  hipLaunchKernelGGL((adam_span_kernel<true, 2>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
+                     (__bf16*)mirror, (const Span*)spans, nspans, part, nparts, clip, lr, b1, b2, eps, wd, hyper, step,
+                     skipped, book);
   return hipGetLastError();
 }
 

@@ -324,7 +324,10 @@ class GraphedTrainStep:
         return _clone_out(static_out)
 
     def _run_phase(self, key, compute_loss, optimizer, step_fn):
-        full = (key, self._sig)
+        # a deferred optimizer update (FusedAdam.defer_next) crosses the phase boundary: a phase captured with one
+        # pending launches it (its own graph), and one that leaves one behind hands the record on at each replay
+        pend_in = getattr(optimizer, "_pending", None) is not None
+        full = (key, self._sig) + ((True,) if pend_in else ())
         if not self.enabled or self._current_eager:
             return self._eager(compute_loss, optimizer, step_fn)
         if self.split:
@@ -348,6 +351,7 @@ class GraphedTrainStep:
                     loss = out[0] if isinstance(out, tuple) else out
                     step_fn(loss, optimizer)
                     static_out = _detach_out(out)
+                    pend_out = getattr(optimizer, "_pending", None)
             except Exception as e:  # something in the phase is not capturable: keep it eager
                 self.failed[full] = repr(e)
                 # an aborted capture leaves its private memory pool unusable for the next capture (the caching
@@ -361,14 +365,16 @@ class GraphedTrainStep:
                 return self._eager(compute_loss, optimizer, step_fn)
             if _RECAPTURE_ALL:  # diagnostics: a new capture drops every other graph (recaptured at next use)
                 self.graphs.clear()
-            ent = self.graphs[full] = (g, static_out)
+            ent = self.graphs[full] = (g, static_out, pend_out)
             self.captures += 1
-        g, static_out = ent
+        g, static_out, pend_out = ent
         _sync_hyper(optimizer)
         if _SYNC_BEFORE_REPLAY:
             torch.cuda.current_stream().synchronize()
         with trace_range("graph:phase"):
             g.replay()
+        if pend_in or pend_out is not None:
+            optimizer._pending = pend_out
         sync_point()
         self.replays += 1
         return _clone_out(static_out)

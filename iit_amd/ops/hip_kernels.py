@@ -52,6 +52,8 @@ _SIGS = {
     "iit_adam_span_size": [],
     "iit_sumsq_spans": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "iit_adam_spans": [c_void_p] * 6 + [c_int, c_void_p] + [c_float] * 6 + [c_void_p] * 4,
+    "iit_adam_norm": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "iit_adam_chunk": [c_void_p] * 6 + [c_int, c_void_p, c_int] + [c_float] * 6 + [c_void_p] * 3 + [c_int, c_void_p],
     "iit_gelu_fwd": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_void_p],
     "iit_shadow_refresh": [c_void_p, c_int, c_void_p],
     "iit_shadow_desc_size": [],
@@ -619,6 +621,34 @@ def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_
                                _p(hyper), _p(step_dev), _p(skipped), _p(sq_spans), n_sq, _p(gsq), _stream()),
            "adam_flat")
     flat.after_step(mirror_written=flat.shadow is not None)
+
+
+def adam_norm_stage(flat, step_dev, *, clip_norm, skipped=None):
+    """First half of a chunked fused Adam (FusedAdam's overlapped update): the global-norm partials and the device
+    step bump, as ``adam_step`` launches them; returns the argument record ``adam_chunk`` launches read."""
+    nparts = 1024
+    part = getattr(flat, "_norm_parts", None)
+    if part is None or part.numel() < nparts:
+        part = flat._norm_parts = torch.zeros(nparts, dtype=torch.float32, device=flat.data.device)
+    spans, nspans = flat.span_table(lib().iit_adam_span_size())
+    sq_spans, n_sq, gsq = flat.norm_spans(lib().iit_adam_span_size())
+    norm = bool(clip_norm) or skipped is not None
+    _check(lib().iit_adam_norm(_p(flat.grad), _p(sq_spans if sq_spans is not None else spans),
+                               n_sq if sq_spans is not None else nspans, _p(part), nparts, int(norm), _p(step_dev),
+                               _p(gsq), _stream()), "adam_norm")
+    return {"spans": spans, "nspans": nspans, "part": part, "nparts": nparts, "clip": float(clip_norm or 0.0),
+            "skipped": skipped}
+
+
+def adam_chunk(flat, exp_avg, exp_avg_sq, step_dev, rec, lo: int, hi: int, *, lr, b1, b2, eps, wd, hyper,
+               book: bool):
+    """Adam over span-table entries [lo, hi) of a norm stage's record (``adam_norm_stage``) on the current
+    stream; ``book``: the one chunk that keeps the skipped-step books."""
+    sb = lib().iit_adam_span_size()
+    _check(lib().iit_adam_chunk(_p(flat.data), _p(flat.grad), _p(exp_avg), _p(exp_avg_sq), _p(flat.shadow),
+                                rec["spans"].data_ptr() + lo * sb, hi - lo, _p(rec["part"]), rec["nparts"],
+                                rec["clip"], lr, b1, b2, eps, wd, _p(hyper), _p(step_dev), _p(rec["skipped"]),
+                                int(book), _stream()), "adam_chunk")
 
 
 IOI_HL_NODES = {"all_nodes_hook": 0, "hook_duplicate": 1, "hook_s_inhibition": 2, "hook_name_mover": 3}

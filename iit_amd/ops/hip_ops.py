@@ -76,6 +76,9 @@ def _claim_store(*ps) -> bool:
 
 
 _FUSE_BIAS = os.environ.get("IIT_FUSED_BIAS_SUMS", "1") != "0"
+# width cap of the fused bias sums (default: none; capping them below the vocabulary width measured 0.4 % slower,
+# profiles/bench_r3s2p_bias_cap_ab.txt)
+_FUSE_BIAS_MAX_N = int(os.environ.get("IIT_FUSED_BIAS_MAX_N", str(1 << 30)))
 
 
 def _fused_bias(gb: Optional[torch.Tensor], N: int) -> Optional[torch.Tensor]:
@@ -84,7 +87,7 @@ def _fused_bias(gb: Optional[torch.Tensor], N: int) -> Optional[torch.Tensor]:
     read again by a column-sum pass); None outside that case (no slot, a strided slot, deterministic mode, where the
     fp32 atomics of the fused sums would make the bias gradient run-to-run variable, or ``IIT_FUSED_BIAS_SUMS=0``)."""
     if gb is None or not _FUSE_BIAS or not gb.is_cuda or gb.dtype != F32 or not gb.is_contiguous() or \
-            gb.numel() != N:
+            gb.numel() != N or N > _FUSE_BIAS_MAX_N:
         return None
     from .gemm_dispatch import deterministic
     return None if deterministic() else gb
@@ -305,6 +308,10 @@ class ModelShadow:
                     self._bind_mirror(flat)
                 self._layout_sig = layout
                 self._value_sig = None
+            if self.mode != "mirror":
+                join = getattr(m, "_param_join", None)  # the copies read every weight: no overlapped update
+                if join is not None:
+                    join()
             if self.mode == "mirror":
                 pv = sum(p._version for p in flat.params)
                 if flat.mirror_version != wv or pv != self._value_sig:
