@@ -124,10 +124,11 @@ class FusedAdam(torch.optim.Optimizer):
         # one event per chunk, created once and re-recorded (no event is destroyed while a phase is being captured)
         while len(self._events) < len(chunks):
             self._events.append(torch.cuda.Event())
+        book = next((k for k, (lo, hi) in enumerate(chunks) if hi > lo), 0)  # (an empty chunk launches nothing)
         with torch.cuda.stream(stream):
             for k, (lo, hi) in enumerate(chunks):
                 hip_kernels.adam_chunk(self.flat, self.exp_avg, self.exp_avg_sq, self._step_dev, rec, lo, hi, lr=lr,
-                                       b1=b1, b2=b2, eps=eps, wd=wd, hyper=self._hyper_dev, book=k == 0)
+                                       b1=b1, b2=b2, eps=eps, wd=wd, hyper=self._hyper_dev, book=k == book)
                 if overlap:
                     self._events[k].record(stream)
         self._inflight = self._events[:len(chunks)] if overlap else None

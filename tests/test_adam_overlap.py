@@ -49,6 +49,7 @@ def test_chunk_bounds_split_the_span_table(monkeypatch):
     opt = FusedAdam(flat, use_hip=False)
     opt._hip = object()  # (the bounds only; no launch on CPU)
     monkeypatch.setattr(torch.cuda, "Stream", lambda device=None: None)
+    monkeypatch.setenv("IIT_ADAM_OVERLAP", "1")
     assert opt.enable_overlap(m.param_stages())
     flat.span_table(24, max_len4=16)
     idx = [0] + [flat.span_index(b) for b in opt._bounds[:-1]]
