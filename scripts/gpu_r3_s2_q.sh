@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r3s2q
 mkdir -p $O
-timeout -k 10 600 python3 -u -m pytest tests/test_adam_overlap.py tests/test_graphs.py tests/test_hip_model.py tests/test_fused_norm.py -x -v -m gpu --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+IIT_TEST_ADAM_OVERLAP=1 timeout -k 10 600 python3 -u -m pytest tests/test_adam_overlap.py tests/test_graphs.py tests/test_hip_model.py tests/test_fused_norm.py -x -v -m gpu --timeout 120 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || { grep -E "Error|FAIL|assert" $O/tests.log | head -30; exit $rc; }
 for i in 1 2; do
 IIT_ADAM_OVERLAP=1 timeout -k 10 300 python3 -u bench.py --steps 100 --warmup 10 > $O/bench_on_$i.log 2>&1 || { tail -30 $O/bench_on_$i.log; exit 1; }

@@ -5,6 +5,8 @@ chunk per model stage on a side stream under the next phase's forward, each stag
 the model's stage gates and the arena ranges the chunks split at.  GPU: training with the overlapped update
 reproduces the serial one, eager and graph-captured.
 """
+import os
+
 import pytest
 import torch
 
@@ -105,6 +107,8 @@ def _train(mode, overlap, monkeypatch, n_batches=8):
 
 
 @pytest.mark.gpu
+@pytest.mark.skipif(os.environ.get("IIT_TEST_ADAM_OVERLAP") != "1",
+                    reason="opt-in path (IIT_ADAM_OVERLAP=1) not yet run on hardware: set IIT_TEST_ADAM_OVERLAP=1")
 @pytest.mark.parametrize("mode", ["eager", "graphs"])
 def test_overlapped_update_matches_serial(mode, monkeypatch):
     ls, ps, ss = _train(mode, False, monkeypatch)
