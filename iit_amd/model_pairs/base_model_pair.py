@@ -222,7 +222,8 @@ class BaseModelPair(ABC):
         with trace_range("hl_intervened_fwd"):
             hl_output = self.hl_model.run_with_hooks(
                 base_input, fwd_hooks=[(hl_node.name, self.make_hl_ablation_hook(hl_node))], **hl_kw)
-        ll_output = self.ll_intervention(base_x, ablation_x, _ll_nodes_of(self.corr, hl_node))
+        ll_nodes = _ll_nodes_of(self.corr, hl_node)
+        ll_output = self.ll_intervention(base_x, ablation_x, ll_nodes)
         if verbose:
             print(f"{hl_node=}, {ll_nodes=}\n{hl_output=}")
         return hl_output, ll_output
@@ -514,6 +515,7 @@ class BaseModelPair(ABC):
             from ..utils.checkpoint import load_resume_state
             start_epoch = load_resume_state(checkpoint_dir, self, optimizer, lr_scheduler)
         self.optimizer = optimizer
+        self._prime_train_graphs(train_loader, loss_fn, optimizer)
         epoch = start_epoch
         for epoch in progress(range(start_epoch, epochs), disable=not pdist.is_main()):
             train_metrics = self._run_train_epoch(train_loader, loss_fn, optimizer, max_steps=max_steps)
@@ -545,6 +547,32 @@ class BaseModelPair(ABC):
         if sink is not None:
             sink.log({"final epoch": epoch})
             sink.close()
+
+    def _prime_train_graphs(self, train_loader, loss_fn, optimizer) -> None:
+        """Capture every (phase, sampled node) graph before epoch 0 and put the training state back exactly
+        (:meth:`GraphedTrainStep.prime_preserving`), so no epoch pays the capture warm-up.  The priming batch is
+        the loader's first; the torch RNG its shuffle consumed is restored with the rest.  Off with
+        ``training_args["prime_graphs"] = False`` or ``IIT_PRIME_GRAPHS=0``."""
+        import os
+        if not self.training_args.get("prime_graphs", True) or os.environ.get("IIT_PRIME_GRAPHS", "1") == "0":
+            return
+        step = self.train_step_fn(optimizer, loss_fn)
+        if not hasattr(step, "prime_preserving"):
+            return
+        import time
+        t0 = time.perf_counter()
+        rng = torch.get_rng_state()
+        try:
+            base, abl = next(iter(train_loader))
+        finally:
+            torch.set_rng_state(rng)
+        with step.stream_context():
+            n = step.prime_preserving(base, abl, loss_fn, optimizer)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        from ..utils import tracing
+        if tracing.PROFILE and pdist.is_main():
+            print(f"[perf] primed {n} phase graphs in {time.perf_counter() - t0:.2f} s before epoch 0")
 
     def _log_throughput(self, epoch: int, sink) -> None:
         """The epoch's training throughput (``self.throughput``): to the metric sink when there is one, and to

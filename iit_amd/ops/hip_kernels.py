@@ -189,7 +189,9 @@ GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 1
               # two co-resident workgroups per CU (<= 80 KiB LDS each): prologue / epilogue overlap
               23: (128, 96), 24: (64, 96), 25: (128, 128), 26: (96, 96), 27: (128, 192), 28: (64, 192),
               29: (64, 96), 30: (64, 64), 31: (64, 128),  # three / four workgroups per CU
-              32: (256, 128), 33: (128, 256), 34: (256, 256)}  # 8 waves: 3-deep rings (32, 33), 256 x 256 (34)
+              32: (256, 128), 33: (128, 256), 34: (256, 256),  # 8 waves: 3-deep rings (32, 33), 256 x 256 (34)
+              # 288-wide tiles (the packed-QKV forward: 8 N-tiles of [*][2304]), 3- and 2-deep rings
+              35: (128, 288), 37: (128, 288)}
 # tiles 12-14 measured slower than their 4-deep twins on every step shape (profiles/gemm_ring_depth_r2.txt: the tiles
 # are intake-bandwidth-bound, not latency-bound), so the dispatcher does not offer them; kept for the experiment.
 # Tiles 15-18 (128-deep K-tiles) are within a few % of the 64-deep tiles and compete per shape.

@@ -244,6 +244,9 @@ class ShardedFusedAdam(FusedAdam):
         if shard is None or shard["world"] != self.plan.world or [tuple(b) for b in shard["buckets"]] != \
                 self.plan.buckets:
             raise ValueError("sharded optimizer state was saved with another data-parallel layout")
+        if int(shard.get("rank", -1)) != self.plan.rank:
+            # same shard length on every rank: a wrong file would load silently with another rank's moments
+            raise ValueError(f"sharded optimizer state of rank {shard.get('rank')} offered to rank {self.plan.rank}")
         super().load_state_dict(sd)
 
 

@@ -18,6 +18,9 @@ so the layout above stays meaning-compatible:
     resume_state.pt      epoch, model/optimizer/scheduler state (rank 0)
     resume_rank{r}.pt    every RNG of rank r: torch CPU + GPU, numpy global, python
                          ``random``, and the pair's node-sampling ``np.random.Generator``
+    resume_optim_rank{r}.pt  with a sharded optimizer (ZeRO-1, ``optimizer.sharded``):
+                         rank r's own shard of the Adam moments (rank 0's file then
+                         holds ``"optimizer": "sharded"`` instead of the state)
 
 All files are written atomically (tmp + ``os.replace``) and read back with
 ``torch.load(weights_only=True)``.
@@ -173,15 +176,26 @@ def _tuplify(x):
     return x
 
 
+def _is_sharded(optimizer) -> bool:
+    return optimizer is not None and bool(getattr(optimizer, "sharded", False))
+
+
 def save_resume_state(checkpoint_dir: str, model_pair, optimizer, lr_scheduler, epoch: int) -> None:
-    """Every rank writes its RNG file; rank 0 writes model + optimizer + scheduler + epoch."""
+    """Every rank writes its RNG file (and, for a sharded optimizer, its own moment shard); rank 0 writes model +
+    optimizer + scheduler + epoch."""
     os.makedirs(checkpoint_dir, exist_ok=True)
     r = pdist.rank()
     _atomic_torch_save(_rng_state(model_pair), os.path.join(checkpoint_dir, f"resume_rank{r}.pt"))
+    sharded = _is_sharded(optimizer)
+    if sharded:  # each rank owns different moments: one file per rank, never rank 0's shard for everyone
+        _atomic_torch_save(optimizer.state_dict(), os.path.join(checkpoint_dir, f"resume_optim_rank{r}.pt"))
     if r == 0:
         ll = model_pair._ll_module() if hasattr(model_pair, "_ll_module") else model_pair.ll_model
+        opt_state = None
+        if optimizer is not None:
+            opt_state = "sharded" if sharded else optimizer.state_dict()
         state = {"epoch": int(epoch), "world_size": pdist.world_size(), "model": dense_state_dict(ll),
-                 "optimizer": optimizer.state_dict() if optimizer is not None else None,
+                 "optimizer": opt_state,
                  "scheduler": lr_scheduler.state_dict() if lr_scheduler is not None else None}
         _atomic_torch_save(state, os.path.join(checkpoint_dir, "resume_state.pt"))
 
@@ -201,6 +215,11 @@ def load_resume_state(checkpoint_dir: str, model_pair, optimizer, lr_scheduler) 
     ll.load_state_dict({k: v.to(dev) for k, v in state["model"].items()})
     if optimizer is not None and state.get("optimizer") is not None:
         opt_sd = state["optimizer"]
+        if opt_sd == "sharded" or _is_sharded(optimizer):
+            if opt_sd != "sharded" or not _is_sharded(optimizer):
+                raise ValueError("resume state: sharded and replicated optimizer states do not mix")
+            opath = os.path.join(checkpoint_dir, f"resume_optim_rank{pdist.rank()}.pt")
+            opt_sd = torch.load(opath, map_location="cpu", weights_only=True)
         if hasattr(optimizer, "flat"):
             opt_sd = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in opt_sd.items()}
             optimizer.load_state_dict(opt_sd)

@@ -364,6 +364,45 @@ def test_zero1_sharded_optimizer_equals_single_process(tmp_path, world, staged):
             assert torch.allclose(got[i][n], p, atol=3e-5, rtol=2e-4), (i, n, float((got[i][n] - p).abs().max()))
 
 
+def _worker_zero_resume(rank, world, port, out_dir):
+    """each rank saves and reloads ITS OWN moment shard; a shard offered to the wrong rank raises."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from iit_amd.parallel import dist as pdist
+    from iit_amd.utils import checkpoint as ck
+    pdist.init_distributed("gloo")
+    torch.set_num_threads(2)
+    pair, train = _make(64)
+    pair.training_args.update(zero=True, fused_optimizer=True)
+    pdist.broadcast_module(pair.ll_model)
+    opt = pair.make_optimizer(1e-3)
+    torch.manual_seed(5)
+    for i, (base, abl) in enumerate(train.make_loader(64 // world, 0)):
+        if i >= 2:
+            break
+        pair.run_train_step(base, abl, pair.loss_fn, opt)
+    ckdir = os.path.join(out_dir, "ck")
+    ck.save_resume_state(ckdir, pair, opt, None, epoch=1)
+    pdist.barrier()
+    saved_m, saved_v = opt.exp_avg.clone(), opt.exp_avg_sq.clone()
+    opt.exp_avg.zero_()
+    opt.exp_avg_sq.zero_()
+    assert ck.load_resume_state(ckdir, pair, opt, None) == 1
+    assert torch.equal(opt.exp_avg, saved_m) and torch.equal(opt.exp_avg_sq, saved_v)
+    other = torch.load(os.path.join(ckdir, f"resume_optim_rank{1 - rank}.pt"), weights_only=True)
+    with pytest.raises(ValueError):
+        opt.load_state_dict(other)
+    torch.save({"m": saved_m}, os.path.join(out_dir, f"zr{rank}.pt"))
+    pdist.destroy()
+
+
+def test_zero1_resume_restores_each_ranks_own_shard(tmp_path):
+    mp.spawn(_worker_zero_resume, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    m0 = torch.load(tmp_path / "zr0.pt", weights_only=True)["m"]
+    m1 = torch.load(tmp_path / "zr1.pt", weights_only=True)["m"]
+    assert not torch.equal(m0, m1)  # the shards differ, so loading rank 0's everywhere would have been wrong
+
+
 def _worker_metrics(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))

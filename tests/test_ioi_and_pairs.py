@@ -138,6 +138,17 @@ def test_gradients_native_vs_reference():
         assert torch.allclose(g1, g2, atol=1e-5)
 
 
+def test_do_intervention_verbose(capsys):
+    """``verbose=True`` (reference base_model_pair.py:75-100) prints the HL and LL nodes."""
+    from iit_amd.data.iit_dataset import IITDataset
+    pair, ds = _pair()
+    base, abl = next(iter(IITDataset(ds, ds, seed=0, device="cpu").make_loader(8, 0)))
+    hl_node = list(pair.corr.keys())[0]
+    hl_out, ll_out = pair.do_intervention(base, abl, hl_node, verbose=True)
+    assert "ll_nodes=" in capsys.readouterr().out
+    assert ll_out.shape[0] == 8
+
+
 @pytest.mark.parametrize("single", [False, True])
 def test_strict_train_step_counts(single):
     from iit_amd.data.iit_dataset import IITDataset
