@@ -88,6 +88,22 @@ IIT_EXPORT int iit_embed_pos_bwd(const long* tok, const float* g, float* dWE, fl
 }
 
 // ============================================================================ layer norm
+// Row select: the interchange splice of whole positions of an LN output inside the LN kernel itself (a paired
+// source+base forward, iit_amd/models/bert.py forward_paired: MQNLI's ``hook_normalized_resid_post`` position
+// sites).  Rows [0, Tb) are the base rows, [Tb, 2 Tb) the source rows at the same (batch, position); a base row
+// whose position s has bit s of ``mask`` set normalises the SOURCE row instead (out[idx] = src[idx] for whole
+// rows), and in the backward the same base rows get no gradient (the spliced slice is a constant).  mask == 0:
+// plain LN.
+struct RowSel {
+  unsigned long long mask;
+  int S;
+  int Tb;
+};
+
+__device__ __forceinline__ bool sel_hit(const RowSel& sel, int row) {
+  return sel.mask != 0ull && row < sel.Tb && ((sel.mask >> (row % sel.S)) & 1ull);
+}
+
 // One wave per row; each lane owns V4 float4 column groups (c4 = lane + 64*i), so every load is a 16-B
 // vector and a wave instruction moves 1 KB (fp32) / 512 B (bf16).  Requires d % 4 == 0 and 16-B aligned
 // rows; the scalar kernels below cover everything else.  Stats in fp32.
@@ -95,12 +111,13 @@ template <int V4>
 __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ b, __bf16* __restrict__ y,
                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                         int T, int d, float eps) {
+                                                         int T, int d, float eps, RowSel sel) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= T) return;
   const int d4 = d >> 2;
-  const float4* xr = (const float4*)(x + (long)row * d);
+  const int xrow = sel_hit(sel, row) ? row + sel.Tb : row;
+  const float4* xr = (const float4*)(x + (long)xrow * d);
   float4 v[V4];
   float s = 0.f;
 #pragma unroll
@@ -145,11 +162,11 @@ template <int VPL>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ b, __bf16* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int T, int d, float eps) {
+                                                     int T, int d, float eps, RowSel sel) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= T) return;
-  const float* xr = x + (long)row * d;
+  const float* xr = x + (long)(sel_hit(sel, row) ? row + sel.Tb : row) * d;
   float v[VPL];
   float s = 0.f;
 #pragma unroll
@@ -186,23 +203,34 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 
 static inline bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
+IIT_EXPORT int iit_ln_fwd_sel(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd,
+                              int T, int d, float eps, unsigned long long pos_mask, int S, int Tb, void* stream);
+
 IIT_EXPORT int iit_ln_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd, int T,
                           int d, float eps, void* stream) {
+  return iit_ln_fwd_sel(x, w, b, y, mean, rstd, T, d, eps, 0ull, 1, 0, stream);
+}
+
+// ``pos_mask`` (RowSel): base rows [0, Tb) at positions with their bit set normalise the source row row + Tb
+IIT_EXPORT int iit_ln_fwd_sel(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd,
+                              int T, int d, float eps, unsigned long long pos_mask, int S, int Tb, void* stream) {
+  const RowSel sel{pos_mask, S > 0 ? S : 1, Tb};
+  if (pos_mask && (S <= 0 || S > 64 || 2 * (long)Tb > T)) return (int)hipErrorInvalidValue;
   dim3 grid((T + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
   const bool vec = d % 4 == 0 && aligned16(x) && (((uintptr_t)y) & 7) == 0 && (!w || (aligned16(w) && aligned16(b)));
   if (vec && d <= 4096) {
-#define LNF(V) hipLaunchKernelGGL((ln_fwd_vec_kernel<V>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps)
+#define LNF(V) hipLaunchKernelGGL((ln_fwd_vec_kernel<V>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps, sel)
     const int v4 = (d / 4 + 63) / 64;
     if (v4 <= 1) LNF(1); else if (v4 <= 2) LNF(2); else if (v4 <= 3) LNF(3); else if (v4 <= 4) LNF(4);
     else if (v4 <= 6) LNF(6); else if (v4 <= 8) LNF(8); else if (v4 <= 12) LNF(12); else LNF(16);
 #undef LNF
     return hipGetLastError();
   }
-  if (d <= 256) hipLaunchKernelGGL((ln_fwd_kernel<4>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps);
-  else if (d <= 1024) hipLaunchKernelGGL((ln_fwd_kernel<16>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps);
-  else if (d <= 2048) hipLaunchKernelGGL((ln_fwd_kernel<32>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps);
-  else if (d <= 4096) hipLaunchKernelGGL((ln_fwd_kernel<64>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps);
+  if (d <= 256) hipLaunchKernelGGL((ln_fwd_kernel<4>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps, sel);
+  else if (d <= 1024) hipLaunchKernelGGL((ln_fwd_kernel<16>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps, sel);
+  else if (d <= 2048) hipLaunchKernelGGL((ln_fwd_kernel<32>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps, sel);
+  else if (d <= 4096) hipLaunchKernelGGL((ln_fwd_kernel<64>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps, sel);
   else return (int)hipErrorInvalidValue;
   return hipGetLastError();
 }
@@ -217,11 +245,12 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const void* __restrict_
                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
                                                          const float* __restrict__ w, float* __restrict__ dx,
                                                          const float* __restrict__ dres, __bf16* __restrict__ dx16,
-                                                         int T, int d, int accumulate) {
+                                                         int T, int d, int accumulate, RowSel sel) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= T) return;
   const int d4 = d >> 2;
+  const bool dead = sel_hit(sel, row);  // a spliced row: its output came from the source row (no gradient here)
   const float mu = mean[row], rs = rstd[row];
   float4 g[V4], xh[V4];
   float sg = 0.f, sgx = 0.f;
@@ -229,7 +258,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const void* __restrict_
   for (int i = 0; i < V4; ++i) {
     const int c = lane + i * 64;
     float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xv = dy;
-    if (c < d4) {
+    if (c < d4 && !dead) {
       if (DY_F32) {
         dy = ((const float4*)dy_)[(long)row * d4 + c];
       } else {
@@ -279,7 +308,8 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const void* __restrict_
 template <bool DY_F32>
 __global__ __launch_bounds__(256) void ln_dwdb_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                      float* __restrict__ dw, float* __restrict__ db, int T, int d) {
+                                                      float* __restrict__ dw, float* __restrict__ db, int T, int d,
+                                                      RowSel sel) {
   __shared__ float pw[4][64], pb[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), wv = threadIdx.x >> 6;
   const int t0 = blockIdx.y * 256;
@@ -288,6 +318,7 @@ __global__ __launch_bounds__(256) void ln_dwdb_kernel(const void* __restrict__ d
     for (int i = 0; i < 64; ++i) {
       const int t = t0 + wv * 64 + i;
       if (t >= T) break;
+      if (sel_hit(sel, t)) continue;
       const float dy = DY_F32 ? ((const float*)dy_)[(long)t * d + c] : bf2f(((const __bf16*)dy_)[(long)t * d + c]);
       sw += dy * (x[(long)t * d + c] - mean[t]) * rstd[t];
       sb += dy;
@@ -308,10 +339,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ w, float* __restrict__ dx,
                                                      const float* __restrict__ dres, __bf16* __restrict__ dx16,
-                                                     int T, int d, int accumulate) {
+                                                     int T, int d, int accumulate, RowSel sel) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= T) return;
+  const bool dead = sel_hit(sel, row);
   const float mu = mean[row], rs = rstd[row];
   float g[VPL], xh[VPL];
   float sg = 0.f, sgx = 0.f;
@@ -319,7 +351,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
   for (int i = 0; i < VPL; ++i) {
     const int c = lane + i * 64;
     float dy = 0.f, xv = 0.f;
-    if (c < d) {
+    if (c < d && !dead) {
       dy = DY_F32 ? ((const float*)dy_)[(long)row * d + c] : bf2f(((const __bf16*)dy_)[(long)row * d + c]);
       xv = (x[(long)row * d + c] - mu) * rs;
       if (w) dy *= w[c];
@@ -345,9 +377,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
   }
 }
 
+IIT_EXPORT int iit_ln_bwd_sel(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
+                              const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db, int T,
+                              int d, int accumulate, unsigned long long pos_mask, int S, void* stream);
+
 IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
                           const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db, int T, int d,
                           int accumulate, void* stream) {
+  return iit_ln_bwd_sel(dy, dy_f32, x, mean, rstd, w, dx, dres, dx16, dw, db, T, d, accumulate, 0ull, 1, stream);
+}
+
+// backward of iit_ln_fwd_sel over the base rows (T = Tb): rows at masked positions get dx = dres only and add
+// nothing to dw / db
+IIT_EXPORT int iit_ln_bwd_sel(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
+                              const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db, int T,
+                              int d, int accumulate, unsigned long long pos_mask, int S, void* stream) {
+  const RowSel sel{pos_mask, S > 0 ? S : 1, T};
+  if (pos_mask && (S <= 0 || S > 64)) return (int)hipErrorInvalidValue;
   dim3 grid((T + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
   __bf16* d16 = (__bf16*)dx16;
@@ -356,16 +402,16 @@ IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const floa
                    (((uintptr_t)dx16) & 7) == 0;
   if (vec) {
 #define LNBV(V)                                                                                                   \
-  if (dy_f32) hipLaunchKernelGGL((ln_bwd_vec_kernel<V, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate); \
-  else hipLaunchKernelGGL((ln_bwd_vec_kernel<V, false>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate);
+  if (dy_f32) hipLaunchKernelGGL((ln_bwd_vec_kernel<V, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate, sel); \
+  else hipLaunchKernelGGL((ln_bwd_vec_kernel<V, false>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate, sel);
     const int v4 = (d / 4 + 63) / 64;
     if (v4 <= 1) { LNBV(1) } else if (v4 <= 2) { LNBV(2) } else if (v4 <= 3) { LNBV(3) } else if (v4 <= 4) { LNBV(4) }
     else if (v4 <= 6) { LNBV(6) } else if (v4 <= 8) { LNBV(8) } else if (v4 <= 12) { LNBV(12) } else { LNBV(16) }
 #undef LNBV
   } else {
 #define LNB(V)                                                                                                   \
-  if (dy_f32) hipLaunchKernelGGL((ln_bwd_kernel<V, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate); \
-  else hipLaunchKernelGGL((ln_bwd_kernel<V, false>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate);
+  if (dy_f32) hipLaunchKernelGGL((ln_bwd_kernel<V, true>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate, sel); \
+  else hipLaunchKernelGGL((ln_bwd_kernel<V, false>), grid, block, 0, s, dy, x, mean, rstd, w, dx, dres, d16, T, d, accumulate, sel);
     if (d <= 256) { LNB(4) }
     else if (d <= 1024) { LNB(16) }
     else if (d <= 2048) { LNB(32) }
@@ -375,8 +421,8 @@ IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const floa
   }
   if (dw) {
     dim3 g2((d + 63) / 64, (T + 255) / 256);
-    if (dy_f32) hipLaunchKernelGGL(ln_dwdb_kernel<true>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d);
-    else hipLaunchKernelGGL(ln_dwdb_kernel<false>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d);
+    if (dy_f32) hipLaunchKernelGGL(ln_dwdb_kernel<true>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d, sel);
+    else hipLaunchKernelGGL(ln_dwdb_kernel<false>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d, sel);
   }
   return hipGetLastError();
 }

@@ -78,7 +78,8 @@ __global__ __launch_bounds__(256) void rms_fwd_kernel(const void* __restrict__ x
 template <int VB>
 __global__ __launch_bounds__(256) void rms_bwd_kernel(const __bf16* __restrict__ dy, const void* __restrict__ x, int x_f32,
                                                       const float* __restrict__ rstd, const float* __restrict__ w,
-                                                      void* __restrict__ dx, int T, int d) {
+                                                      void* __restrict__ dx, const void* __restrict__ dres, int T,
+                                                      int d) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= T) return;
   const int es = x_f32 ? 4 : 2;
@@ -111,6 +112,12 @@ __global__ __launch_bounds__(256) void rms_bwd_kernel(const __bf16* __restrict__
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = r * (g[i][e] - xh[i][e] * s);
+      if (dres) {  // the residual stream's skip-connection gradient (x's dtype), summed here instead of by autograd
+        float rr[8];
+        ld8((const char*)dres + ((long)row * d + c) * es, x_f32, rr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += rr[e];
+      }
       st8(dxr + (long)c * es, x_f32, o);
     }
   }
@@ -220,14 +227,25 @@ IIT_EXPORT int iit_rms_fwd(const void* x, int x_f32, const float* w, void* y, fl
   return (int)hipGetLastError();
 }
 
+IIT_EXPORT int iit_rms_bwd_res(const void* dy, const void* x, int x_f32, const float* rstd, const float* w, void* dx,
+                               const void* dres, float* dw, int T, int d, void* stream);
+
 // dx has x's dtype; dw (nullable) accumulates in fp32
 IIT_EXPORT int iit_rms_bwd(const void* dy, const void* x, int x_f32, const float* rstd, const float* w, void* dx,
                            float* dw, int T, int d, void* stream) {
-  if (d % 8 || d > 8192 || !al16(x) || !al16(dy) || !al16(dx) || (w && !al16(w))) return (int)hipErrorInvalidValue;
+  return iit_rms_bwd_res(dy, x, x_f32, rstd, w, dx, nullptr, dw, T, d, stream);
+}
+
+// ``dres`` (nullable, x's dtype): added to dx -- the fork form (RMSNorm output + residual passthrough) of the
+// pre-norm block, one pass instead of the norm backward plus autograd's gradient sum over [T, d]
+IIT_EXPORT int iit_rms_bwd_res(const void* dy, const void* x, int x_f32, const float* rstd, const float* w, void* dx,
+                               const void* dres, float* dw, int T, int d, void* stream) {
+  if (d % 8 || d > 8192 || !al16(x) || !al16(dy) || !al16(dx) || (w && !al16(w)) || (dres && !al16(dres)))
+    return (int)hipErrorInvalidValue;
   dim3 grid((T + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
   const int vb = (d + 511) / 512;
-#define RB(V) hipLaunchKernelGGL(rms_bwd_kernel<V>, grid, block, 0, s, (const __bf16*)dy, x, x_f32, rstd, w, dx, T, d)
+#define RB(V) hipLaunchKernelGGL(rms_bwd_kernel<V>, grid, block, 0, s, (const __bf16*)dy, x, x_f32, rstd, w, dx, dres, T, d)
   if (vb <= 1) RB(1); else if (vb <= 2) RB(2); else if (vb <= 4) RB(4); else if (vb <= 8) RB(8); else RB(16);
 #undef RB
   if (dw) {

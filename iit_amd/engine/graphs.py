@@ -353,8 +353,15 @@ class GraphedTrainStep:
             if self.pool is None or os.environ.get("IIT_GRAPH_POOL") == "private":
                 self.pool = torch.cuda.graph_pool_handle()
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            parts = None
             if getattr(optimizer, "sharded", False):
-                gb = None  # the sharded optimizer step issues collectives (norm all-reduce, all-gather): eager
+                # the sharded optimizer step issues collectives (norm all-reduce, all-gather): its device parts
+                # are captured one graph each, the collectives and host books between them stay eager
+                gb = None
+                clip = self.pair.training_args.get("clip_grad_norm") or None
+                spec = optimizer.step_parts(clip_norm=clip) if hasattr(optimizer, "step_parts") else None
+                if spec is not None:
+                    parts = [(torch.cuda.CUDAGraph() if cap else None, fn) for cap, fn in spec]
             gs = []
             try:
                 with _CaptureGC(), torch.cuda.graph(ga, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
@@ -370,6 +377,14 @@ class GraphedTrainStep:
                     with _CaptureGC(), torch.cuda.graph(gb, pool=self.pool, stream=self.stream,
                                                         capture_error_mode=_CAPTURE_MODE):
                         update()
+                elif parts is not None:
+                    # capturing runs nothing: the eager pieces are NOT run here either (the replay below runs the
+                    # whole sequence), so the host books of the step are not doubled
+                    for g_, fn in parts:
+                        if g_ is not None:
+                            with _CaptureGC(), torch.cuda.graph(g_, pool=self.pool, stream=self.stream,
+                                                                capture_error_mode=_CAPTURE_MODE):
+                                fn()
             except Exception as e:
                 self.failed[full] = repr(e)
                 self.pool = None  # see _run_phase: the aborted capture's pool is not reusable
@@ -378,9 +393,9 @@ class GraphedTrainStep:
                 if stg is not None:
                     stg.release()
                 return eager_phase()
-            ent = self.graphs[full] = ((ga, gs, gb), static_out)
+            ent = self.graphs[full] = ((ga, gs, gb, parts), static_out)
             self.captures += 1
-        (ga, gs, gb), static_out = ent
+        (ga, gs, gb, parts), static_out = ent
         _sync_hyper(optimizer)
         with trace_range("graph:fwd_bwd"):
             ga.replay()
@@ -389,10 +404,18 @@ class GraphedTrainStep:
             reduce_eagerly(lambda i, k: gs[i].replay())
         sync_point()
         with trace_range("graph:clip_adam"):
-            if gb is None:
-                update()
-            else:
+            if gb is not None:
                 gb.replay()
+            elif parts is not None:
+                self.pair.clip_grad_fn(optimizer)  # (host books only: the fused optimizer clips itself)
+                optimizer.pending_clip = None
+                for g_, fn in parts:
+                    if g_ is not None:
+                        g_.replay()
+                    else:
+                        fn()
+            else:
+                update()
         sync_point()
         self.replays += 1
         return _clone_out(static_out)

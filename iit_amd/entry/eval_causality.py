@@ -30,7 +30,8 @@ def evaluate_model_on_ablations(ll_model, task: str, test_set, eval_args: dict, 
     for hook_point in progress(hook_points or get_hook_points(ll_model), desc="Hook points"):
         _, hl_model, corr = get_alignment(task, config={"hook_point": hook_point,
                                                         "input_shape": test_set.get_input_shape()})
-        pair = IITProbeSequentialPair(ll_model=ll_model, hl_model=hl_model, corr=corr)
+        pair = IITProbeSequentialPair(ll_model=ll_model, hl_model=hl_model, corr=corr,
+                                      training_args={"engine": eval_args.get("engine", "native")})
         stats = {hl_node: torch.zeros((), device=DEVICE) for hl_node in pair.corr}
         n = len(test_set)
         bs = eval_args["batch_size"]

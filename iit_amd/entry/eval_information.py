@@ -34,7 +34,7 @@ def evaluate_model_on_probes(ll_model, task: str, probe_training_args: dict, tra
         _, hl_model, corr = get_alignment(task, config={"hook_point": hook_point,
                                                         "input_shape": test_set.get_input_shape()})
         pair = IITProbeSequentialPair(ll_model=ll_model, hl_model=hl_model, corr=corr,
-                                      training_args=probe_training_args)
+                                      training_args=probe_training_args)  # ("engine": "reference" = hook path)
         out = train_probes_on_model_pair(pair, train_set.get_input_shape(), train_set, probe_training_args)
         if save_probes:
             d = os.path.join("weights", "probes", task, hook_point)

@@ -343,7 +343,10 @@ class BaseModelPair(ABC):
             # the clip's global norm from the weight-gradient GEMMs (FlatParams.norm_cover): only when the gradients
             # those GEMMs store are the ones the optimizer steps on -- one process, no reducer, no gradient rewrite
             import os
-            opt.flat.norm_fuse = (self._reducer is None and not getattr(opt, "sharded", False)
+            # (a one-rank reducer -- the IIT_DP_FORCE_REDUCER rehearsal -- averages over one rank: the identity, so
+            # the per-rank sums ARE the global ones; at N > 1 the norm pass reads the reduced gradient once more)
+            opt.flat.norm_fuse = ((self._reducer is None or pdist.world_size() == 1)
+                                  and not getattr(opt, "sharded", False)
                                   and not self.rewrites_grads_before_step()
                                   and os.environ.get("IIT_FUSED_NORM", "1") != "0")
             # overlapped update: a phase's Adam runs under the next phase's forward (FusedAdam.enable_overlap) -- one

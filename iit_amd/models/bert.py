@@ -132,6 +132,75 @@ class BertBlock(nn.Module):
         return run.site(self.hook_normalized_resid_post, self.ln2.run(resid_post, run))
 
 
+    # ------------------------------------------------------------------ paired source + base rows
+    def paired_ok(self) -> bool:
+        a = self.attn
+        return not (a.rotary or a.gqa or self.cfg.use_attn_result) and self.cfg.act_fn in ("gelu", "gelu_new")
+
+    def forward_paired(self, p, run: _Run, sites, stop_after: str, captures):
+        """The fused block over paired rows (``ops.hip_ops.Paired``: base rows with autograd, source rows without),
+        as :meth:`iit_amd.models.transformer.TransformerBlock.forward_paired` does for the decoder.  Sites:
+        ``attn.hook_z`` (whole / heads in the attention kernel, other indices by the paired patch-spec splice),
+        ``mlp.hook_post`` and ``hook_normalized_resid_post`` (the paired splice); their source values go to
+        ``captures``.  Pairing ends after ``stop_after`` (the rest of the block runs on the base rows).  Returns
+        ``(x, still_paired)``."""
+        from .transformer import _hip_ops
+        from ..engine.plan import Splice
+        ops, attn, mlp = run.ops, self.attn, self.mlp
+        S, H, dh = p.full.shape[1], self.cfg.n_heads, self.cfg.d_head
+        erf = self.cfg.act_fn == "gelu"
+        zname = attn.hook_z.name
+        zs = sites.get(zname)
+        qkv = ops.pair_qkv(p, attn.W_Q, attn.W_K, attn.W_V, attn.b_Q, attn.b_K, attn.b_V)
+        heads, rest = None, list(zs or ())
+        if ops.pair_heads_ok(S, dh) and H <= 64 and len(rest) == 1:
+            heads = Splice(rest[0], None).head_mask(H)
+            if heads is not None:
+                rest = []
+        z = ops.pair_attention(qkv, False, attn.attn_scale, heads=heads)
+        for ix in rest:
+            z = ops.pair_splice(z, ix)
+        if zs is not None:
+            captures[zname] = z.src
+        if zname == stop_after:
+            resid_mid = ops.o_proj_residual(z.base, attn.W_O, attn.b_O, p.base)
+            x = self.ln1.run(resid_mid, run)
+            resid_post = ops.mlp_gelu_residual(x, mlp.W_in, mlp.b_in, mlp.W_out, mlp.b_out, x, erf=erf)
+            return self.ln2.run(resid_post, run), False
+        resid_mid = ops.pair_o_proj_residual(z, attn.W_O, attn.b_O, p)
+        x = ops.pair_layer_norm(resid_mid, self.ln1.w, self.ln1.b, self.ln1.eps)
+        pname = mlp.hook_post.name
+        ps = sites.get(pname)
+        if ps is None:
+            resid_post = ops.pair_mlp_gelu_residual(x, mlp.W_in, mlp.b_in, mlp.W_out, mlp.b_out, x, erf=erf)
+        else:
+            _, post = ops.pair_mlp_in(x, mlp.W_in, mlp.b_in, erf=erf)
+            for ix in ps:
+                post = ops.pair_splice(post, ix)
+            captures[pname] = post.src
+            if pname == stop_after:
+                resid_post = ops.mlp_out_residual(post.base, mlp.W_out, mlp.b_out, x.base)
+                return self.ln2.run(resid_post, run), False
+            resid_post = ops.pair_mlp_out_residual(post, mlp.W_out, mlp.b_out, x)
+        nname = self.hook_normalized_resid_post.name
+        idxs = list(sites.get(nname, ()))
+        shape = tuple(p.base.shape[:2]) + (self.cfg.d_model,)
+        masks = [ops.position_mask(ix, shape) for ix in idxs]
+        mask = 0
+        if idxs and all(masks):  # whole positions: spliced inside the LN kernel (no splice pass, fwd or bwd)
+            for m in masks:
+                mask |= m
+            idxs = []
+        out = ops.pair_layer_norm(resid_post, self.ln2.w, self.ln2.b, self.ln2.eps, pos_mask=mask)
+        for ix in idxs:
+            out = ops.pair_splice(out, ix)
+        if nname in sites:
+            captures[nname] = out.src
+            if nname == stop_after:
+                return out.base, False
+        return out, True
+
+
 class HookedEncoder(HookedRootModule):
     """BERT encoder; ``n_classes`` adds the [CLS] pooler + classifier head (forward then returns ``[B, C]``)."""
 
@@ -226,6 +295,84 @@ class HookedEncoder(HookedRootModule):
             return h @ ops.w(self.unembed.W_U) + ops.w(self.unembed.b_U)
         except _StopForward:
             return None
+
+    _PAIR_SITES = ("attn.hook_z", "mlp.hook_post", "hook_normalized_resid_post")
+
+    def _token_types(self, tokens):
+        sep = getattr(self, "sep_token_id", None)
+        if sep is None:
+            return torch.zeros_like(tokens)
+        is_sep = (tokens == sep).long()
+        return ((is_sep.cumsum(-1) - is_sep) > 0).long()
+
+    def _embed_ln(self, tokens, run: _Run):
+        ops = run.ops
+        B, S = tokens.shape
+        e = ops.embed(tokens, self.embed.embed.W_E)
+        pe = ops.pos_embed(B, S, self.embed.pos_embed.W_pos)
+        t = ops.w(self.embed.token_type_embed.W_token_type)[self._token_types(tokens)]
+        return self.embed.ln.run(e + pe + t, run)
+
+    def run_paired(self, tokens: torch.Tensor, src_tokens: torch.Tensor, sites, logits: str = "full"):
+        """Interchange intervention with the source run folded into the base forward: one pass of 2B rows
+        (source rows without autograd) through every block up to the deepest site, which splices inside the
+        paired kernels (the decoder's :meth:`iit_amd.models.transformer.HookedTransformer.run_paired`; reference
+        ``do_intervention``, /root/reference/iit/model_pairs/base_model_pair.py:80-98).  Sites: ``attn.hook_z``,
+        ``mlp.hook_post`` and ``hook_normalized_resid_post`` of any block (MQNLI's position sites).  Returns
+        ``(output, {site: source activation})`` or None when not covered (then two forwards run)."""
+        import os
+        if os.environ.get("IIT_PAIRED", "1") == "0" or not sites:
+            return None
+        ops = self.ops()
+        if not getattr(ops, "supports_pairs", False) or getattr(ops, "pair_layer_norm", None) is None:
+            return None
+        if tokens.dim() != 2 or tokens.shape != src_tokens.shape or tokens.shape[1] > 64:
+            return None
+        if any(hp.is_live for hp in self.hook_dict.values()):
+            return None
+        B, S = tokens.shape
+        cfg = self.cfg
+        from .transformer import _hip_ops
+        order = []
+        for name, idxs in sites.items():
+            parts = name.split(".")
+            if parts[0] != "blocks" or len(parts) < 3 or ".".join(parts[2:]) not in self._PAIR_SITES:
+                return None
+            li = int(parts[1])
+            suffix = ".".join(parts[2:])
+            shape = ((B, S, cfg.n_heads, cfg.d_head) if suffix == "attn.hook_z" else
+                     (B, S, cfg.d_mlp) if suffix == "mlp.hook_post" else (B, S, cfg.d_model))
+            for ix in idxs:
+                if _hip_ops().pair_specs(ix, shape) is None:
+                    return None
+            order.append((li, self._PAIR_SITES.index(suffix), name))
+        deepest = max(order)
+        if not all(blk.paired_ok() for blk in self.blocks[:deepest[0] + 1]):
+            return None
+        dev = self.embed.embed.W_E.device
+        tokens, src_tokens = tokens.to(dev), src_tokens.to(dev)
+        run = _Run(RunPlan(logits=logits), ops)
+        ops.begin_forward()
+        x = self._embed_ln(tokens, run)
+        with torch.no_grad():
+            xs = self._embed_ln(src_tokens, run)
+        p = _hip_ops().Paired(x, torch.cat([x.detach(), xs]).contiguous())
+        captures = {}
+        paired = True
+        for li, blk in enumerate(self.blocks):
+            if paired:
+                p, paired = blk.forward_paired(p, run, sites, deepest[2], captures)
+            else:
+                p = blk(p, run, None)
+        x = p.base if paired else p
+        if logits == "none":
+            return None, captures
+        if self.n_classes:
+            pooled = torch.tanh(x[:, 0] @ ops.w(self.pooler.W) + ops.w(self.pooler.b))
+            return pooled @ ops.w(self.classifier.W) + ops.w(self.classifier.b), captures
+        h = F.gelu(x @ ops.w(self.mlm_head.W) + ops.w(self.mlm_head.b))
+        h = self.mlm_head.ln.run(h, run)
+        return h @ ops.w(self.unembed.W_U) + ops.w(self.unembed.b_U), captures
 
     def run_capture(self, tokens, names, truncate: bool = True, base_plan: Optional[RunPlan] = None, **kw):
         plan = RunPlan.capture_only(list(names), truncate=truncate)

@@ -329,10 +329,15 @@ class TransformerBlock(nn.Module):
 
     def _norm_fork(self, ln, x, run):
         """(normed x, residual to carry forward): fused backends return a passthrough of ``x`` whose
-        gradient the LN backward kernel adds in (one pass instead of LN-bwd + autograd's sum)."""
+        gradient the LN (or RMSNorm) backward kernel adds in (one pass instead of norm-bwd + autograd's sum)."""
+        if ln is None or run.live(ln.hook_scale) or run.live(ln.hook_normalized) or not x.requires_grad:
+            return self._norm(ln, x, run), x
+        if ln.rms:
+            fork = getattr(run.ops, "rms_norm_fork", None)
+            out = fork(x, ln.w, ln.eps) if fork is not None else None
+            return out if out is not None else (self._norm(ln, x, run), x)
         fork = getattr(run.ops, "layer_norm_fork", None)
-        if (ln is None or ln.rms or fork is None or run.live(ln.hook_scale) or run.live(ln.hook_normalized)
-                or not x.requires_grad):
+        if fork is None:
             return self._norm(ln, x, run), x
         return fork(x, ln.w, ln.b, ln.eps)
 
@@ -375,7 +380,7 @@ class TransformerBlock(nn.Module):
             attn_out = result.sum(-2) + ops.w(attn.b_O)
             attn_out = run.site(self.hook_attn_out, attn_out)
             resid_mid_pre = ops.residual(resid, attn_out)
-        elif attn_out_live or not ops.fused:
+        elif attn_out_live or not (ops.fused or getattr(ops, "fuses_residual", False)):
             attn_out = run.site(self.hook_attn_out, ops.o_proj(z, attn.W_O, attn.b_O))
             resid_mid_pre = ops.residual(resid, attn_out)
         else:
@@ -409,7 +414,7 @@ class TransformerBlock(nn.Module):
             else:
                 _, post = ops.mlp_in(x, mlp.W_in, mlp.b_in, self.cfg.act_fn, hook_pre=pre_hook)
             post = run.site(mlp.hook_post, post)
-        if run.live(self.hook_mlp_out) or not ops.fused:
+        if run.live(self.hook_mlp_out) or not (ops.fused or getattr(ops, "fuses_residual", False)):
             mlp_out = run.site(self.hook_mlp_out, ops.mlp_out(post, mlp.W_out, mlp.b_out))
             resid_post = ops.residual(resid_mid, mlp_out)
         else:

@@ -35,6 +35,8 @@ _SIGS = {
     "iit_embed_pos_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_ln_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
     "iit_ln_bwd": [c_void_p, c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_void_p],
+    "iit_ln_fwd_sel": [c_void_p] * 6 + [c_int, c_int, c_float, c_ull, c_int, c_int, c_void_p],
+    "iit_ln_bwd_sel": [c_void_p, c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_ull, c_int, c_void_p],
     "iit_attn_small_fwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float, c_int,
                                             c_void_p],
     "iit_attn_small_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
@@ -66,6 +68,8 @@ _SIGS = {
     "iit_colsum_multi": [c_void_p] * 6 + [c_int, c_void_p],
     "iit_rms_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_rms_bwd": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "iit_rms_bwd_res": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                        c_void_p],
     "iit_rotary": [c_void_p, c_long, c_long, c_long, c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p],
     "iit_swiglu_fwd": [c_void_p, c_void_p, c_void_p, c_long, c_void_p],
     "iit_swiglu_bwd": [c_void_p] * 5 + [c_long, c_void_p],
@@ -386,6 +390,23 @@ def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False, dres=None, 
                             _p(dres), _p(dx16), _p(dw), _p(db), T, d, int(accumulate), _stream()), "ln_bwd")
 
 
+def ln_fwd_sel(x, w, b, y, mean, rstd, T, d, eps, pos_mask: int, S: int, Tb: int):
+    """``ln_fwd`` over paired rows with the whole-position splice inside the kernel: base rows [0, Tb) at positions
+    whose bit is set in ``pos_mask`` normalise the source row ``row + Tb`` (csrc/kernels.hip RowSel)."""
+    if CHECK_BOUNDS:
+        _bounds("ln_fwd_sel", ("x", x, T, d, d), ("y", y, T, d, d), ("mean", mean, 1, T, T), ("rstd", rstd, 1, T, T))
+    _check(lib().iit_ln_fwd_sel(_p(x), _p(w), _p(b), _p(y), _p(mean), _p(rstd), T, d, eps, pos_mask, S, Tb, _stream()), "ln_fwd_sel")
+
+
+def ln_bwd_sel(dy, x, mean, rstd, w, dx, dw, db, T, d, pos_mask: int, S: int, dres=None, dx16=None):
+    """Backward of :func:`ln_fwd_sel` over the base rows: spliced rows pass only ``dres`` and add nothing to dw/db."""
+    if CHECK_BOUNDS:
+        _bounds("ln_bwd_sel", ("dy", dy, T, d, d), ("x", x, T, d, d), ("dx", dx, T, d, d), ("mean", mean, 1, T, T))
+    _check(lib().iit_ln_bwd_sel(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx),
+                                _p(dres), _p(dx16), _p(dw), _p(db), T, d, 0, pos_mask, S,
+                                _stream()), "ln_bwd_sel")
+
+
 def heads_to_mask(heads: Optional[Sequence[int]]) -> int:
     m = 0
     for h in heads or ():
@@ -497,9 +518,10 @@ def rms_fwd(x, w, y, rstd, T: int, d: int, eps: float):
            "rms_fwd")
 
 
-def rms_bwd(dy, x, rstd, w, dx, dw, T: int, d: int):
-    _check(lib().iit_rms_bwd(_p(dy), _p(x), int(x.dtype == torch.float32), _p(rstd), _p(w), _p(dx), _p(dw), T, d,
-                             _stream()), "rms_bwd")
+def rms_bwd(dy, x, rstd, w, dx, dw, T: int, d: int, dres=None):
+    """RMSNorm backward; ``dres`` (optional, x's dtype [T, d]): the skip-connection gradient added into dx."""
+    _check(lib().iit_rms_bwd_res(_p(dy), _p(x), int(x.dtype == torch.float32), _p(rstd), _p(w), _p(dx), _p(dres),
+                                 _p(dw), T, d, _stream()), "rms_bwd")
 
 
 def rotary(x, out, cos, sin, rd: int, offset: int, adjacent: bool, inverse: bool):

@@ -709,6 +709,42 @@ class RMSNormFn(Function):
         return dx.view(ctx.shape), None, None
 
 
+class RMSNormForkFn(Function):
+    """``(RMSNorm(x), x)``: the second output carries the residual stream past the norm; the backward sums both
+    gradients inside the RMSNorm-backward kernel (the pre-norm block's skip connection, no autograd add)."""
+
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        ctx.set_materialize_grads(False)
+        d = x.shape[-1]
+        x2 = _c16(x.reshape(-1, d))
+        T = x2.shape[0]
+        y = torch.empty(T, d, dtype=BF16, device=x.device)
+        rstd = torch.empty(T, dtype=F32, device=x.device)
+        K.rms_fwd(x2, None if w is None else w.detach(), y, rstd, T, d, eps)
+        ctx.save_for_backward(x2, rstd)
+        ctx.w = w
+        ctx.shape = x.shape
+        return y.view(*x.shape[:-1], d), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dpass):
+        if dy is None:
+            return dpass, None, None
+        x2, rstd = ctx.saved_tensors
+        w = ctx.w
+        T, d = x2.shape
+        dx = torch.empty_like(x2)
+        dres = None
+        if dpass is not None:
+            dres = _c16(dpass.to(x2.dtype).reshape(T, d))
+        dw = _grad_slot(w) if w is not None else None
+        K.rms_bwd(_c16(dy.to(BF16).reshape(T, d)), x2, rstd, None if w is None else w.detach(), dx, dw, T, d,
+                  dres=dres)
+        _done(w)
+        return dx.view(ctx.shape), None, None
+
+
 class RotaryFn(Function):
     @staticmethod
     def forward(ctx, x, cos, sin, rd, offset, adjacent):
@@ -1099,6 +1135,57 @@ class LayerNormForkPairFn(LayerNormForkFn):
         return LayerNormForkFn.backward(ctx, dy, dpass) + (None, None)
 
 
+class LayerNormPairFn(LayerNormFn):
+    """LN of both row sets (a post-LN block's residual output, BERT): bf16 ``Paired``; backward = LayerNormFn's on
+    the base rows."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps, x_full, box, pos_mask=0):
+        ctx.set_materialize_grads(False)
+        d = x.shape[-1]
+        B = x.shape[0]
+        x2 = _flat2(x_full)
+        T2 = x2.shape[0]
+        T = T2 * B // x_full.shape[0]
+        y = torch.empty(T2, d, dtype=BF16, device=x.device)
+        mean = torch.empty(T2, dtype=F32, device=x.device)
+        rstd = torch.empty(T2, dtype=F32, device=x.device)
+        S = x.shape[1] if x.dim() == 3 else 1
+        if pos_mask:  # whole-position splice of the base rows from the source rows, inside the LN kernel
+            K.ln_fwd_sel(x2, w, b, y, mean, rstd, T2, d, eps, pos_mask, S, T)
+        else:
+            K.ln_fwd(x2, w, b, y, mean, rstd, T2, d, eps)
+        ctx.save_for_backward(x2[:T], mean[:T], rstd[:T])
+        ctx.params = (w, b)
+        ctx.in_dtype = x.dtype
+        ctx.sel = (pos_mask, S)
+        yf = y.view(*x_full.shape[:-1], d)
+        box.append(yf)
+        return yf[:B]
+
+    @staticmethod
+    def backward(ctx, dy):
+        pos_mask, S = ctx.sel
+        if not pos_mask:
+            return LayerNormFn.backward(ctx, dy) + (None, None, None)
+        if dy is None:
+            return (None,) * 7
+        x2, mean, rstd = ctx.saved_tensors
+        w, b = ctx.params
+        T, d = x2.shape
+        dx = torch.empty(T, d, dtype=F32, device=x2.device)
+        dx16 = torch.empty(T, d, dtype=BF16, device=x2.device) if ctx.in_dtype == F32 else None
+        dw = _grad_slot(w) if w is not None else None
+        db = _grad_slot(b) if b is not None else None
+        K.ln_bwd_sel(_flat2(dy.contiguous()), x2, mean, rstd, w, dx, dw, db, T, d, pos_mask, S, dx16=dx16)
+        _done(w, b)
+        dx = dx.view(*dy.shape[:-1], d)
+        if dx16 is None:
+            return (dx.to(ctx.in_dtype),) + (None,) * 6
+        _set_bf16_twin(dx, dx16)
+        return (dx,) + (None,) * 6
+
+
 class QKVPairFn(QKVFn):
     @staticmethod
     def forward(ctx, x, layer, bias_bf16, W_Q, W_K, W_V, b_Q, b_K, b_V, x_full, box):
@@ -1431,6 +1518,29 @@ class HipOps(TorchOps):
         box = []
         y, x_pass = LayerNormForkPairFn.apply(p.base, w, b, eps, p.full.float().contiguous(), box)
         return Paired(y, box[0]), Paired(x_pass, p.full)
+
+    def pair_layer_norm(self, p: Paired, w, b, eps, pos_mask: int = 0) -> Paired:
+        """LN of both row sets (no residual passthrough: post-LN blocks).  ``pos_mask``: the base rows at these
+        positions take the source rows' output -- an interchange splice of whole positions of the LN output done
+        by the LN kernel itself (and masked out of its backward), no separate splice pass."""
+        box = []
+        y = LayerNormPairFn.apply(p.base, w, b, eps, p.full.float().contiguous(), box, int(pos_mask))
+        return Paired(y, box[0])
+
+    @staticmethod
+    def position_mask(index, shape) -> int:
+        """The bit mask of positions when ``index`` selects whole positions (every batch row, every feature) of a
+        ``[B, S, d]`` hook with S <= 64, else 0."""
+        if len(shape) != 3 or shape[1] > 64:
+            return 0
+        ranges = index.to_ranges(tuple(shape))
+        if ranges is None or ranges[0] != [(0, shape[0])] or ranges[2] != [(0, shape[2])]:
+            return 0
+        m = 0
+        for lo, hi in ranges[1]:
+            for s_ in range(lo, hi):
+                m |= 1 << s_
+        return m
 
     def pair_qkv(self, p: Paired, W_Q, W_K, W_V, b_Q, b_K, b_V) -> Paired:
         i = self._layer_of[id(W_Q)]

@@ -197,6 +197,32 @@ class _MirrorMat(torch.autograd.Function):
         return (dx, None, None, None, None, None, None) + (None,) * ctx.n_leaves
 
 
+class _MirrorMatResid(torch.autograd.Function):
+    """``y = resid + x @ Wm (+ bm)``: :class:`_MirrorMat` with the residual add in the GEMM's epilogue (hipBLASLt
+    ``addmm`` with beta = 1 reads ``resid`` as C) -- the pre-norm block's skip connection without a separate [T, d]
+    elementwise pass.  ``resid``'s gradient is ``gy`` itself."""
+
+    @staticmethod
+    def forward(ctx, x, resid, wm, bm, gw, gb, wparams, bparams, *leaves):
+        lead = x.shape[:-1]
+        x2 = x.reshape(-1, x.shape[-1])
+        r2 = resid.reshape(-1, resid.shape[-1]).to(wm.dtype)
+        y = torch.addmm(r2, x2, wm)
+        if bm is not None:
+            y = y + bm
+        ctx.save_for_backward(x2)
+        ctx.wm, ctx.gw, ctx.gb, ctx.lead, ctx.n_leaves = wm, gw, gb, lead, len(leaves)
+        ctx.wparams, ctx.bparams = wparams, bparams
+        ctx.rdtype = resid.dtype
+        return y.view(*lead, y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, gy):
+        dx = _MirrorMat.backward(ctx, gy)[0]
+        dres = gy.to(ctx.rdtype) if ctx.needs_input_grad[1] else None
+        return (dx, dres) + (None,) * (6 + ctx.n_leaves)
+
+
 def _bound_to_arena(flat, p: torch.Tensor) -> bool:
     """``p.grad`` is the arena view at ``p``'s offset (so writing the arena is writing ``p.grad``)."""
     g = p.grad  # None: lazily zeroed (FlatParams.zero_grad) -- the backward claims / binds the slot itself
@@ -397,6 +423,66 @@ class TorchOps:
 
     def o_result(self, z, W_O):
         return torch.einsum("bshe,hed->bshd", z, self.w(W_O))
+
+    # -- residual epilogues (bf16 arena mirror on a GPU): the skip connection inside the projection GEMM --------
+    @property
+    def fuses_residual(self) -> bool:
+        import os
+        return self.dtype == torch.bfloat16 and os.environ.get("IIT_TORCH_RESID_EPI", "1") != "0"
+
+    def _mat_resid(self, x2, resid, W, b, wm, gw_shape):
+        """``resid + x2 @ wm (+ b)`` for arena weight ``W`` viewed as the 2-D mirror ``wm``; None when the
+        arena path does not apply (the caller adds the residual itself)."""
+        m = _arena_mirror(W)
+        mb = _arena_mirror(b) if (b is not None and b.is_contiguous()) else None
+        if m is None or (b is not None and mb is None) or not x2.is_cuda:
+            return None
+        flat = m[0]
+        if not torch.is_grad_enabled() or not W.requires_grad:
+            r2 = resid.reshape(-1, resid.shape[-1]).to(torch.bfloat16)
+            y = torch.addmm(r2, x2.reshape(-1, x2.shape[-1]), wm)
+            if mb is not None:
+                y = y + mb[1]
+            return y.view(*resid.shape[:-1], y.shape[-1])
+        if not (_bound_to_arena(flat, W) and (b is None or _bound_to_arena(flat, b))):
+            return None
+        bp = () if b is None else (b,)
+        gw = flat.grad.as_strided(gw_shape, (gw_shape[1], 1), flat.offset_of(W))
+        gb = None if b is None else flat.grad.as_strided((gw_shape[1],), (1,), flat.offset_of(b))
+        return _MirrorMatResid.apply(x2, resid, wm, None if mb is None else mb[1], gw, gb, (W,), bp, W, *bp)
+
+    def o_proj_residual(self, z, W_O, b_O, resid):
+        if self.fuses_residual and z.is_cuda and W_O.is_contiguous():
+            m = _arena_mirror(W_O)
+            if m is not None:
+                H, dh, d = W_O.shape
+                out = self._mat_resid(z.to(torch.bfloat16).reshape(*z.shape[:-2], H * dh), resid, W_O, b_O,
+                                      m[1].view(H * dh, d), (H * dh, d))
+                if out is not None:
+                    return out
+        return self.residual(resid, self.o_proj(z, W_O, b_O))
+
+    def mlp_out_residual(self, post, W_out, b_out, resid):
+        if self.fuses_residual and post.is_cuda and W_out.dim() == 2 and W_out.is_contiguous():
+            m = _arena_mirror(W_out)
+            if m is not None:
+                out = self._mat_resid(post.to(torch.bfloat16), resid, W_out, b_out, m[1], tuple(W_out.shape))
+                if out is not None:
+                    return out
+        return self.residual(resid, self.mlp_out(post, W_out, b_out))
+
+    def rms_norm_fork(self, x, w, eps):
+        """``(RMSNorm(x), x_passthrough)`` -- the backward adds the skip gradient inside the norm kernel -- or None
+        when the fused kernel does not apply."""
+        if not (self.dtype == torch.bfloat16 and x.is_cuda and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192
+                and x.dtype in (torch.bfloat16, torch.float32) and (w is None or (w.dtype == torch.float32
+                                                                                   and w.is_contiguous()))):
+            return None
+        import os
+        if os.environ.get("IIT_LLAMA_FUSED", "1") == "0":
+            return None
+        from . import hip_ops
+        return hip_ops.RMSNormForkFn.apply(x, w, eps)
 
     def mlp_in(self, x, W_in, b_in, act: str, hook_pre=None):
         pre = self.lin(x, W_in, b_in)

@@ -143,6 +143,12 @@ class GradReducer:
 
     def _launch_span(self, s: int, e: int) -> None:
         """Async all-reduce of arena elements [s, e): rows-restricted parameters compactly, the rest in place."""
+        if self.world == 1:
+            # a one-rank group (IIT_DP_FORCE_REDUCER rehearsals of the DP schedule): the average over one rank is
+            # the identity, so nothing is issued -- RCCL would run a full read + scale + write pass of the range
+            # (oneRankReduce, 3.1 ms/step in profiles/dp_schedule_1gpu_breakdown_v4.txt) that no real world-N run
+            # has (there the ring reduction replaces it)
+            return
         op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
         pieces, cur = [], s
         subsets = self.__dict__.get("_subsets_sorted")

@@ -144,6 +144,59 @@ class ShardedFusedAdam(FusedAdam):
         return buf
 
     # ------------------------------------------------------------------ optimizer
+    def step_parts(self, clip_norm: Optional[float] = None):
+        """The step as ``[(capturable, fn), ...]`` for a graph-replayed phase (the whole
+        sharded optimizer ran eagerly): the device work -- sharded sum of squares, the Adam pass, the mirror
+        refresh of the pieces other ranks own -- is capturable; the collectives between them (the 4-byte norm
+        all-reduce, the all-gather of the updated pieces) stay eager, so every rank still issues the identical
+        RCCL sequence.  Runs in order exactly what :meth:`step` runs.  None on the torch (non-HIP) path."""
+        if self._hip is None:
+            return None
+        from ..ops import hip_kernels as K
+        need_norm = bool(clip_norm) or self.nan_guard
+        world = pdist.world_size()
+        g = self.param_groups[0]
+
+        def host_books():  # eager, first: the host-side counters / hyper-parameters of this step
+            self.step_count += 1
+            self.sync_hyper()
+
+        def norm_part():
+            K.sumsq_spans(self.shard_grad, self._spans, self._nspans, self._part, self._step_dev, need_norm)
+            if need_norm:
+                torch.sum(self._part, dim=0, keepdim=True, out=self._total)
+
+        def norm_reduce():
+            dist.all_reduce(self._total, op=dist.ReduceOp.SUM)
+
+        def adam_part():
+            (b1, b2) = g["betas"]
+            K.adam_spans(self.flat, self.shard_grad, self.exp_avg, self.exp_avg_sq, self._spans, self._nspans,
+                         self._total, self._step_dev, lr=g["lr"], b1=b1, b2=b2, eps=g["eps"], wd=g["weight_decay"],
+                         clip_norm=clip_norm, skipped=self._skipped_dev if self.nan_guard else None,
+                         hyper=self._hyper_dev)
+
+        parts = [(False, host_books), (True, norm_part)]
+        if need_norm and world > 1:
+            parts.append((False, norm_reduce))
+        parts.append((True, adam_part))
+        if world > 1:
+            parts.append((False, lambda: self._all_gather(mirror=False)))
+            parts.append((True, self._refresh_foreign_mirror))
+        parts.append((False, lambda: self.flat.after_step(mirror_written=self.flat.shadow is not None)))
+        return parts
+
+    def _refresh_foreign_mirror(self) -> None:
+        """bf16 mirror of the pieces other ranks updated (the owned piece's mirror was written by the Adam pass)."""
+        flat = self.flat
+        if flat.shadow is None:
+            return
+        for (s, e), (a, b) in zip(self.plan.buckets, self.plan.own):
+            foreign = [(s, a), (b, e)] if b > a else [(s, e)]
+            for lo, hi in foreign:
+                if hi > lo:
+                    flat.shadow[lo:hi].copy_(flat.data[lo:hi])
+
     @torch.no_grad()
     def step(self, closure=None, clip_norm: Optional[float] = None):
         if closure is not None:
@@ -203,8 +256,9 @@ class ShardedFusedAdam(FusedAdam):
             denom = (v.sqrt() / (bc2 ** 0.5)).add_(eps)
             p.addcdiv_(m, denom, value=-lr / bc1)
 
-    def _all_gather(self) -> None:
-        """Every rank's updated pieces back into every arena; the bf16 mirror of each bucket re-derived locally."""
+    def _all_gather(self, mirror: bool = True) -> None:
+        """Every rank's updated pieces back into every arena; with ``mirror`` the bf16 mirror of each bucket is
+        re-derived locally here (``step_parts`` refreshes only the foreign pieces, in a captured part)."""
         flat = self.flat
         world = self.plan.world
         for bi, (s, e) in enumerate(self.plan.buckets):
@@ -229,9 +283,10 @@ class ShardedFusedAdam(FusedAdam):
                     dist.all_gather(parts, piece.clone())
                 if not exact:
                     flat.data[s:e].copy_(out[:e - s])
-            if flat.shadow is not None:
+            if mirror and flat.shadow is not None:
                 flat.shadow[s:e].copy_(flat.data[s:e])
-        flat.after_step(mirror_written=flat.shadow is not None)
+        if mirror:
+            flat.after_step(mirror_written=flat.shadow is not None)
 
     # ------------------------------------------------------------------ checkpointing
     def state_dict(self):

@@ -134,18 +134,104 @@ def resample_ablate_node(model_pair, base_in, ablation_in, node: LLNode, results
                                                     atol, verbose, node, categorical_metric)
 
 
-def resample_ablate_nodes(model_pair, base_in, ablation_in, nodes, results: Dict, atol: float = 5e-2,
-                          verbose: bool = False, categorical_metric: Categorical_Metric = Categorical_Metric.KL) -> None:
-    """Native batched form of :func:`resample_ablate_node` over ``nodes``: one source capture of every node's hook
-    and one HL base output for the batch, then one spliced base forward per node."""
+def _resample_scores(model_pair, base_in, ablation_in, nodes, atol: float = 5e-2, verbose: bool = False,
+                     categorical_metric: Categorical_Metric = Categorical_Metric.KL) -> torch.Tensor:
+    """One batch of the native resample sweep: one source capture of every node's hook and one HL base output,
+    then one spliced base forward per node; the scores as one device vector (node order)."""
     with torch.no_grad():
         cache = model_pair.ll_source_cache(ablation_in[0], nodes)
         model_pair.ll_cache = cache
         base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
+        scores = []
         for node in nodes:
             ll_out = model_pair.ll_intervened_forward(base_in[0], [node])
-            results[node] = results[node] + _resample_score(model_pair, base_in, ablation_in, ll_out, base_hl_out,
-                                                            hl_reduced, atol, verbose, node, categorical_metric)
+            scores.append(_resample_score(model_pair, base_in, ablation_in, ll_out, base_hl_out, hl_reduced, atol,
+                                          verbose, node, categorical_metric).float().reshape(()))
+        return torch.stack(scores)
+
+
+def resample_ablate_nodes(model_pair, base_in, ablation_in, nodes, results: Dict, atol: float = 5e-2,
+                          verbose: bool = False, categorical_metric: Categorical_Metric = Categorical_Metric.KL) -> None:
+    """Native batched form of :func:`resample_ablate_node` over ``nodes`` (adds into ``results``)."""
+    s = _resample_scores(model_pair, base_in, ablation_in, nodes, atol, verbose, categorical_metric)
+    for i, node in enumerate(nodes):
+        results[node] = results[node] + s[i]
+
+
+class _SweepGraph:
+    """A sweep's per-batch body (``fn(*batch) -> [n] scores``) run as ONE captured HIP graph per batch shape.
+
+    The node loop of a sweep is a fixed kernel sequence for a given batch shape (one source capture, one HL
+    forward, one spliced forward + score per node), so after one eager batch (settling lazily built state: GEMM
+    decisions, weight mirrors) the body is captured with the batch in static buffers and the running sums
+    accumulated in place on device; each later batch is a copy into the buffers and one replay -- no per-node
+    Python or launch overhead (23 ms per spliced B=256 forward eagerly).  Sums are added in the
+    same order as the eager loop, so the results are the eager ones bit for bit.  Batches of another shape (an
+    epoch tail) and bodies that cannot be captured run eagerly into the same accumulator.  ``IIT_EVAL_GRAPHS=0``
+    disables capture."""
+
+    def __init__(self, fn, n: int, device):
+        self.fn = fn
+        self.acc = torch.zeros(n, dtype=torch.float32, device=device)
+        self.enabled = (device.type == "cuda" and torch.cuda.is_available()
+                        and os.environ.get("IIT_EVAL_GRAPHS", "1") != "0")
+        self.static = None
+        self.sig = None
+        self.graph = None
+        self.eager_runs = 0
+        self.replays = 0
+
+    @staticmethod
+    def _flat(batch):
+        return [t for part in batch for t in (part if isinstance(part, (tuple, list)) else (part,))
+                if isinstance(t, torch.Tensor)]
+
+    def _rebuild(self, batch, flat_static):
+        it = iter(flat_static)
+        out = []
+        for part in batch:
+            if isinstance(part, (tuple, list)):
+                out.append(type(part)(next(it) if isinstance(t, torch.Tensor) else t for t in part))
+            else:
+                out.append(next(it) if isinstance(part, torch.Tensor) else part)
+        return out
+
+    def __call__(self, *batch) -> None:
+        flat = self._flat(batch)
+        sig = tuple((tuple(t.shape), t.dtype) for t in flat)
+        if not self.enabled or (self.sig is not None and sig != self.sig):
+            self.acc.add_(self.fn(*batch))
+            return
+        if self.static is None:
+            self.static = [t.clone() for t in flat]
+            self.sig = sig
+        for d, s_ in zip(self.static, flat):
+            d.copy_(s_, non_blocking=True)
+        sbatch = self._rebuild(batch, self.static)
+        if self.graph is None and self.eager_runs < 1:
+            self.eager_runs += 1
+            self.acc.add_(self.fn(*sbatch))
+            return
+        if self.graph is None:
+            import gc
+            from ..engine.graphs import _CAPTURE_MODE
+            g = torch.cuda.CUDAGraph()
+            gc.collect()
+            try:
+                with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+                    self.acc.add_(self.fn(*sbatch))
+            except Exception as e:  # noqa: BLE001 - not capturable: eager from now on
+                print(f"[iit eval] sweep body not captured ({type(e).__name__}: {str(e)[:120]}); eager")
+                torch.cuda.synchronize()
+                self.enabled = False
+                self.acc.add_(self.fn(*batch))
+                return
+            self.graph = g
+        self.graph.replay()
+        self.replays += 1
+
+    def sums(self) -> torch.Tensor:
+        return self.acc
 
 
 def check_causal_effect(model_pair, dataset, batch_size: int = 256, node_type: str = "a", verbose: bool = False,
@@ -157,8 +243,16 @@ def check_causal_effect(model_pair, dataset, batch_size: int = 256, node_type: s
     results = {n: 0 for n in nodes}
     loader = dataset.make_loader(batch_size=batch_size, num_workers=0)
     nb = 0
+    sweep = None
+    if native and not verbose and nodes:
+        dev = next(model_pair.ll_model.parameters()).device
+        sweep = _SweepGraph(lambda b, a: _resample_scores(model_pair, b, a, nodes,
+                                                          categorical_metric=categorical_metric), len(nodes), dev)
     for base_in, ablation_in in progress(loader, desc="resample ablation"):
         nb += 1
+        if sweep is not None:
+            sweep(base_in, ablation_in)
+            continue
         if native:
             resample_ablate_nodes(model_pair, base_in, ablation_in, nodes, results, verbose=verbose,
                                   categorical_metric=categorical_metric)
@@ -166,6 +260,9 @@ def check_causal_effect(model_pair, dataset, batch_size: int = 256, node_type: s
         for node in nodes:
             resample_ablate_node(model_pair, base_in, ablation_in, node, results, hookers.get(node), verbose=verbose,
                                  categorical_metric=categorical_metric)
+    if sweep is not None:
+        sums = sweep.sums().tolist()  # one host read for the whole sweep
+        return {n: float(sums[i]) / max(nb, 1) for i, n in enumerate(nodes)}
     return {n: float(v) / max(nb, 1) for n, v in results.items()}
 
 
@@ -251,22 +348,31 @@ def ablate_node(model_pair, base_in, node: LLNode, results: Dict, hook: Optional
     results[node] = results[node] + _ablation_score(model_pair, ll_out, base_ll_out, base_hl_out, hl_reduced, atol)
 
 
-def ablate_nodes(model_pair, base_in, nodes, results: Dict, values: Dict[str, torch.Tensor], atol: float = 5e-2) -> None:
-    """Native batched form of :func:`ablate_node` over ``nodes``: one unablated base forward and one HL base output
-    per batch, then one spliced forward per node with its [1, ...] ablation value broadcast over the batch."""
+def _ablation_scores(model_pair, base_in, nodes, values: Dict[str, torch.Tensor], atol: float = 5e-2) -> torch.Tensor:
+    """One batch of the native mean / zero ablation sweep: one unablated base forward and one HL base output, then
+    one spliced forward per node with its [1, ...] ablation value broadcast over the batch; scores as a vector."""
     model = model_pair.ll_model
     base_x = base_in[0]
     with torch.no_grad():
         base_ll_out = model_pair.ll_forward(base_x)
         base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
         B = base_x.shape[0]
+        scores = []
         for node in nodes:
             v = values[node.name]
             v = v.expand(B, *v.shape[1:]) if v.shape[0] != B else v  # a view: no per-batch copy
             plan = RunPlan.with_splices([(node.name, node.index, v)], logits=model_pair.ll_logits_mode())
             ll_out = model(base_x, plan=plan)
-            results[node] = results[node] + _ablation_score(model_pair, ll_out, base_ll_out, base_hl_out,
-                                                            hl_reduced, atol)
+            scores.append(_ablation_score(model_pair, ll_out, base_ll_out, base_hl_out, hl_reduced,
+                                          atol).float().reshape(()))
+        return torch.stack(scores)
+
+
+def ablate_nodes(model_pair, base_in, nodes, results: Dict, values: Dict[str, torch.Tensor], atol: float = 5e-2) -> None:
+    """Native batched form of :func:`ablate_node` over ``nodes`` (adds into ``results``)."""
+    s = _ablation_scores(model_pair, base_in, nodes, values, atol)
+    for i, node in enumerate(nodes):
+        results[node] = results[node] + s[i]
 
 
 def check_causal_effect_on_ablation(model_pair, dataset, batch_size: int = 256, node_type: str = "a",
@@ -281,6 +387,7 @@ def check_causal_effect_on_ablation(model_pair, dataset, batch_size: int = 256, 
     loader = dataset.make_loader(batch_size=batch_size, num_workers=0)
     nb = 0
     values = None
+    sweep = None
     for base_in in progress(loader, desc="ablation"):
         nb += 1
         if native:
@@ -293,11 +400,20 @@ def check_causal_effect_on_ablation(model_pair, dataset, batch_size: int = 256, 
                         probe = model_pair.ll_model.run_capture(base_in[0][:1], names)
                     values = {nm: (mean_cache[nm] if use_mean_cache else torch.zeros_like(probe[nm]))
                               for nm in names}
-            ablate_nodes(model_pair, base_in, nodes, results, values)
+                if nodes and not verbose:
+                    dev = next(model_pair.ll_model.parameters()).device
+                    sweep = _SweepGraph(lambda b: _ablation_scores(model_pair, b, nodes, values), len(nodes), dev)
+            if sweep is not None:
+                sweep(base_in)
+            else:
+                ablate_nodes(model_pair, base_in, nodes, results, values)
             continue
         for node in nodes:
             ablate_node(model_pair, base_in, node, results, hookers.get(node), verbose=verbose, mean_cache=mean_cache,
                         use_mean_cache=use_mean_cache)
+    if sweep is not None:
+        sums = sweep.sums().tolist()
+        return {n: float(sums[i]) / max(nb, 1) for i, n in enumerate(nodes)}
     return {n: float(v) / max(nb, 1) for n, v in results.items()}
 
 

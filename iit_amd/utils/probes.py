@@ -25,12 +25,18 @@ def _nodes(v) -> List[LLNode]:
     return [v] if isinstance(v, LLNode) else list(v)
 
 
-def capture_hooks(ll_model, x: torch.Tensor, names: Iterable[str]) -> Dict[str, torch.Tensor]:
+def capture_hooks(ll_model, x: torch.Tensor, names: Iterable[str], reference: bool = False) -> Dict[str, torch.Tensor]:
+    """The named hook activations of ``ll_model`` on ``x``: a capture-only plan run (only those hooks, stopped
+    after the last one) on a plan-capable model, else -- or with ``reference`` -- ``run_with_cache``."""
     names = sorted(set(names))
-    if getattr(ll_model, "supports_run_plan", False) or hasattr(ll_model, "run_capture"):
+    if not reference and (getattr(ll_model, "supports_run_plan", False) or hasattr(ll_model, "run_capture")):
         return ll_model.run_capture(x, names)
     _, cache = ll_model.run_with_cache(x, names_filter=lambda n: n in names)
     return cache
+
+
+def _reference(model_pair) -> bool:
+    return getattr(model_pair, "training_args", {}).get("engine", "native") == "reference"
 
 
 def construct_probe(high_level_node: HLNode, ll_nodes, dummy_cache, bias: bool = False) -> nn.Linear:
@@ -92,7 +98,7 @@ def train_probes_on_model_pair(model_pair, input_shape, train_set, training_args
             opt.zero_grad()
             x = x.to(DEVICE)
             with torch.no_grad():
-                cache = capture_hooks(model_pair.ll_model, x, names)
+                cache = capture_hooks(model_pair.ll_model, x, names, _reference(model_pair))
             total = 0
             for hl_name, probe in probes.items():
                 gt = model_pair.hl_model.get_idx_to_intermediate(hl_name)(int_vars.to(DEVICE)).to(DEVICE)
@@ -120,7 +126,7 @@ def evaluate_probe(probes, model_pair, test_set, criterion):
         acc = torch.zeros((), device=DEVICE)
         with torch.no_grad():
             for x, y, int_vars in _batches(test_set, 256, True):
-                cache = capture_hooks(model_pair.ll_model, x.to(DEVICE), names)
+                cache = capture_hooks(model_pair.ll_model, x.to(DEVICE), names, _reference(model_pair))
                 gt = model_pair.hl_model.get_idx_to_intermediate(hl_name)(int_vars.to(DEVICE)).to(DEVICE)
                 for node in _nodes(model_pair.corr[hl_name]):
                     out = probe_logits(probe, cache, node)

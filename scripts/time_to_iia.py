@@ -122,6 +122,9 @@ def main():
            "steady_s_per_epoch": (round(float(np.median(np.diff([t for _, t, _ in epochs_seen]))), 3)
                                   if len(epochs_seen) > 2 else None),
            "train_pairs_per_s": round(steps * 256 / wall, 1),
+           # wall-clock of the first epochs (epoch 0 includes the graph priming before it, train() -> prime_preserving)
+           "epoch_s_first6": [round(b - a, 3) for a, b in zip([0.0] + [t for _, t, _ in epochs_seen][:5],
+                                                              [t for _, t, _ in epochs_seen][:6])],
            "final": {k: round(float(v), 3) for k, v in last.items()},
            "device": torch.cuda.get_device_name() if dev.type == "cuda" else "cpu",
            "data": "synthetic (offline IOI prompts, random-init weights)"}

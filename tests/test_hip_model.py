@@ -184,6 +184,45 @@ def test_bert_encoder_on_hip_matches_fp32_oracle():
         assert rel(pf.grad, pr.grad) < 8e-2, n
 
 
+def test_bert_paired_forward_equals_two_forwards():
+    """HookedEncoder.run_paired (source rows folded into the base forward, MQNLI's hook_normalized_resid_post
+    position sites, a head site and an MLP site) vs the truncated source capture + spliced base forward: same
+    outputs and captured activations, same gradients, and the source rows get none."""
+    from iit_amd.core.index import Ix
+    from iit_amd.engine.plan import RunPlan
+    _, fast = _bert_pair_models()
+    torch.manual_seed(1)
+    tok = torch.randint(3, 64, (16, 15), device=dev)
+    src = torch.randint(3, 64, (16, 15), device=dev)
+    for t in (tok, src):
+        t[:, 0], t[:, 7], t[:, 14] = 1, 2, 2
+    cases = [{"blocks.0.hook_normalized_resid_post": [Ix[:, [2, 3]]]},
+             {"blocks.1.hook_normalized_resid_post": [Ix[:, [0]]]},
+             {"blocks.0.attn.hook_z": [Ix[:, :, 1, :]]},
+             {"blocks.1.mlp.hook_post": [Ix[:, 4:9]]},
+             {"blocks.0.hook_normalized_resid_post": [Ix[:, [5]]], "blocks.1.attn.hook_z": [Ix[:, :, 0, :]]}]
+    for sites in cases:
+        res = fast.run_paired(tok, src, sites)
+        assert res is not None, sites
+        out_p, caps = res
+        cache = fast.run_capture(src, list(sites))
+        for n in sites:
+            assert rel(caps[n], cache[n]) < 1e-6, (sites, n)
+        spl = [(n, ix, cache[n]) for n, ixs in sites.items() for ix in ixs]
+        out_2 = fast(tok, plan=RunPlan.with_splices(spl))
+        assert rel(out_p, out_2) < 1e-2, sites
+        grads = []
+        for o in (out_p, out_2):
+            fast.zero_grad(set_to_none=True)
+            o.float().pow(2).mean().backward()
+            grads.append({n: p.grad.detach().clone() for n, p in fast.named_parameters() if p.grad is not None})
+        assert grads[0].keys() == grads[1].keys()
+        for n in grads[1]:
+            if grads[1][n].norm() < 1e-6:
+                continue
+            assert rel(grads[0][n], grads[1][n]) < 3e-2, (sites, n)
+
+
 def test_mqnli_bert_pair_trains_on_hip_arena():
     """IIT + behaviour steps of the MQNLI pair with the flat arena mirror + fused Adam on the HIP backend."""
     from iit_amd.data.iit_dataset import IITDataset

@@ -71,3 +71,52 @@ def test_swiglu_fwd_bwd():
     post.backward(g.bfloat16())
     pr.backward(g)
     assert rel(gate.grad, gr.grad) < 2e-2 and rel(up.grad, ur.grad) < 2e-2
+
+
+@pytest.mark.parametrize("x_dtype", [torch.bfloat16, torch.float32])
+def test_rmsnorm_fork_adds_skip_gradient(x_dtype):
+    """RMSNormForkFn: (RMSNorm(x), x) whose backward sums the norm gradient and the skip-connection gradient in
+    the kernel -- equal to RMSNormFn + autograd's add."""
+    from iit_amd.ops import hip_ops
+    torch.manual_seed(3)
+    d = 512
+    x = torch.randn(4, 9, d, device=dev).to(x_dtype).requires_grad_()
+    w = (1 + 0.1 * torch.randn(d, device=dev)).requires_grad_()
+    y, xp = hip_ops.RMSNormForkFn.apply(x, w, 1e-5)
+    g1, g2 = torch.randn(4, 9, d, device=dev), torch.randn(4, 9, d, device=dev)
+    (y.float() * g1).sum().add((xp.float() * g2).sum()).backward()
+    x2 = x.detach().clone().requires_grad_()
+    w2 = w.detach().clone().requires_grad_()
+    y2 = hip_ops.RMSNormFn.apply(x2, w2, 1e-5)
+    (y2.float() * g1).sum().add((x2.float() * g2).sum()).backward()
+    assert torch.equal(y, y2)
+    assert rel(x.grad, x2.grad) < 1e-2 and rel(w.grad, w2.grad) < 1e-3
+
+
+def test_llama_torch_backend_residual_epilogue_matches_unfused(monkeypatch):
+    """Llama (torch op backend, bf16 arena mirror): W_O / W_out with the residual add in the GEMM epilogue
+    (hipBLASLt beta = 1) and the RMSNorm fork give the unfused path's logits and gradients."""
+    import copy
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.models.convert import llama_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    cfg = llama_config_dict("llama-tiny", device=dev, dtype=torch.bfloat16)
+    torch.manual_seed(0)
+    a = HookedTransformer(cfg)
+    b = copy.deepcopy(a)
+    FlatParams(a, with_bf16_shadow=True)
+    FlatParams(b, with_bf16_shadow=True)
+    tok = torch.randint(0, cfg["d_vocab"], (4, 24), device=dev)
+    outs, grads = [], []
+    for model, fused in ((a, "1"), (b, "0")):
+        monkeypatch.setenv("IIT_TORCH_RESID_EPI", fused)
+        monkeypatch.setenv("IIT_LLAMA_FUSED", "1")
+        out = model(tok)
+        out.float().pow(2).mean().backward()
+        outs.append(out.detach().float())
+        grads.append({n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.grad is not None})
+    assert rel(outs[0], outs[1]) < 1e-2
+    assert grads[0].keys() == grads[1].keys()
+    for n in grads[1]:
+        if grads[1][n].norm() > 1e-6:
+            assert rel(grads[0][n], grads[1][n]) < 3e-2, n
