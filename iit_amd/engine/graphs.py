@@ -442,6 +442,7 @@ class GraphedTrainStep:
             if self.pool is None or os.environ.get("IIT_GRAPH_POOL") == "private":
                 self.pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
+            guard = optimizer.capture_guard() if hasattr(optimizer, "capture_guard") else None
             try:
                 with _CaptureGC(), torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                     out = compute_loss()
@@ -459,6 +460,8 @@ class GraphedTrainStep:
                 print(f"[iit graphs] phase {key} not captured ({type(e).__name__}: {str(e)[:160]}); "
                       f"running it eagerly\n{tb}")
                 torch.cuda.synchronize()
+                if guard is not None:  # a pending update launched inside the aborted capture never ran
+                    guard()
                 return self._eager(compute_loss, optimizer, step_fn)
             if _RECAPTURE_ALL:  # diagnostics: a new capture drops every other graph (recaptured at next use)
                 self.graphs.clear()

@@ -131,6 +131,12 @@ class FusedAdam(torch.optim.Optimizer):
                                        b1=b1, b2=b2, eps=eps, wd=wd, hyper=self._hyper_dev, book=k == book)
                 if overlap:
                     self._events[k].record(stream)
+        if overlap and not torch.cuda.is_current_stream_capturing():
+            # the side-stream chunks read the record's span table and norm partials after the host drops it: keep
+            # the caching allocator from handing those blocks to the current stream meanwhile
+            for t in (rec.get("spans"), rec.get("part")):
+                if isinstance(t, torch.Tensor):
+                    t.record_stream(stream)
         self._inflight = self._events[:len(chunks)] if overlap else None
 
     def wait_stage(self, k: int) -> None:
@@ -142,6 +148,18 @@ class FusedAdam(torch.optim.Optimizer):
             torch.cuda.current_stream().wait_event(ev[min(k, len(ev) - 1)])
             if k >= len(ev) - 1:
                 self._inflight = None
+
+    def capture_guard(self):
+        """(state, restore) around a graph capture of a phase that may launch a pending update: if the capture
+        fails, ``restore()`` puts the pending record back, forgets events recorded inside the aborted capture and
+        drains the side stream, so the eager fallback still applies the update."""
+        saved = (self._pending, self._inflight)
+
+        def restore():
+            self._pending, self._inflight = saved[0], None
+            if self._side is not None:
+                self._side.synchronize()
+        return restore
 
     def join_pending(self) -> None:
         """Complete any deferred update before gradients or weights are touched outside a gated forward."""

@@ -26,3 +26,6 @@ step ioi_ckpt 300 python3 -u train_ioi.py --model gpt2-small --dtype bf16 --epoc
 step eval_ioi_hip 600 python3 -u eval_ioi.py --model gpt2-small -w 100_100_40 --root /tmp/r4models --backend hip --num-samples 4608 --timing-repeats 2; grep -E "eval_ioi_timing" $O/eval_ioi_hip.log | cut -c1-400
 IIT_PROFILE=1 step tti_gpt2 500 python3 -u scripts/time_to_iia.py --model gpt2-small --dtype bf16 --epochs 80; grep -E "primed|^\{" $O/tti_gpt2.log | cut -c1-600
 step eval_pvr 900 python3 -u scripts/eval_pvr_r4.py; grep -E "^\[pvr\]" $O/eval_pvr.log
+step llama_tests 300 python3 -u -m pytest tests/test_llama_ops.py -x -v -m gpu --timeout 120 --timeout-method thread; tail -3 $O/llama_tests.log
+step dp_tests 400 python3 -u -m pytest tests/test_dp_rccl_gpu.py -x -v -m gpu --timeout 200 --timeout-method thread; tail -3 $O/dp_tests.log
+IIT_GEMM_TABLE=0 IIT_GEMM_REPORT=$O/gemm_report_isolated.txt step gemm_autotune 600 python3 -u bench.py --steps 5 --warmup 2; grep -E '^\{' $O/gemm_autotune.log | cut -c1-200

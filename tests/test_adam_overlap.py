@@ -61,6 +61,19 @@ def test_chunk_bounds_split_the_span_table(monkeypatch):
         assert all(s < b for s in starts[:idx[k + 1]]) and all(s >= b for s in starts[idx[k + 1]:])
 
 
+def test_capture_guard_restores_a_pending_update():
+    """a capture that launched the pending update and then failed must hand the record back, so the
+    eager fallback still applies the previous phase's Adam (its norm stage already bumped the step)."""
+    m = tiny()
+    opt = FusedAdam(FlatParams(m), use_hip=False)
+    rec = {"chunks": [(0, 1)]}
+    opt._pending, opt._inflight = rec, None
+    restore = opt.capture_guard()
+    opt._pending, opt._inflight = None, ["event recorded inside the aborted capture"]  # the gate launched it
+    restore()
+    assert opt._pending is rec and opt._inflight is None
+
+
 def test_overlap_disabled_by_env(monkeypatch):
     m = tiny()
     opt = FusedAdam(FlatParams(m), use_hip=False)
