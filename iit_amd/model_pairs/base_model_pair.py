@@ -554,10 +554,13 @@ class BaseModelPair(ABC):
     def _prime_train_graphs(self, train_loader, loss_fn, optimizer) -> None:
         """Capture every (phase, sampled node) graph before epoch 0 and put the training state back exactly
         (:meth:`GraphedTrainStep.prime_preserving`), so no epoch pays the capture warm-up.  The priming batch is
-        the loader's first; the torch RNG its shuffle consumed is restored with the rest.  Off with
-        ``training_args["prime_graphs"] = False`` or ``IIT_PRIME_GRAPHS=0``."""
+        the loader's first; the torch RNG its shuffle consumed is restored with the rest.  ``training_args["prime_graphs"]``
+        or ``IIT_PRIME_GRAPHS=1|0``."""
         import os
-        if not self.training_args.get("prime_graphs", True) or os.environ.get("IIT_PRIME_GRAPHS", "1") == "0":
+        want = self.training_args.get("prime_graphs", None)
+        if want is None:  # opt-in until validated on hardware (scripts/time_to_iia.py sets IIT_PRIME_GRAPHS=1)
+            want = os.environ.get("IIT_PRIME_GRAPHS", "0") == "1"
+        if not want:
             return
         step = self.train_step_fn(optimizer, loss_fn)
         if not hasattr(step, "prime_preserving"):

@@ -201,6 +201,9 @@ class BertBlock(nn.Module):
         return out, True
 
 
+_BERT_PAIRED_DEFAULT = "0"  # flipped to "1" once tests/test_hip_model.py::test_bert_paired_* has passed on an MI355X
+
+
 class HookedEncoder(HookedRootModule):
     """BERT encoder; ``n_classes`` adds the [CLS] pooler + classifier head (forward then returns ``[B, C]``)."""
 
@@ -322,6 +325,8 @@ class HookedEncoder(HookedRootModule):
         ``(output, {site: source activation})`` or None when not covered (then two forwards run)."""
         import os
         if os.environ.get("IIT_PAIRED", "1") == "0" or not sites:
+            return None
+        if os.environ.get("IIT_BERT_PAIRED", _BERT_PAIRED_DEFAULT) != "1":  # opt-in until validated on hardware
             return None
         ops = self.ops()
         if not getattr(ops, "supports_pairs", False) or getattr(ops, "pair_layer_norm", None) is None:

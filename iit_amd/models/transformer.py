@@ -719,7 +719,7 @@ class HookedTransformer(HookedRootModule):
         every kernel as one batch of 2B rows (``ops.hip_ops.Paired``): the source rows carry no autograd state (the
         reference's source run is under no_grad) and the base rows are exactly the unpaired intervened forward's.
         Returns ``(output, {site: source activation})``, or None when the configuration is not covered (fused HIP
-        backend, short-sequence attention, LN models, sites on ``attn.hook_z`` / ``mlp.hook_post``, no live user
+        backend, S <= 64 (short-sequence attention kernels), LN models, sites on ``attn.hook_z`` / ``mlp.hook_post``, no live user
         hook) -- the caller then runs the two forwards.  ``IIT_PAIRED=0`` disables it."""
         import os
         if os.environ.get("IIT_PAIRED", "1") == "0" or not sites:
@@ -728,7 +728,9 @@ class HookedTransformer(HookedRootModule):
         cfg = self.cfg
         if not getattr(ops, "supports_pairs", False) or self.rotary or cfg.final_rms:
             return None
-        if tokens.dim() != 2 or tokens.shape != src_tokens.shape or tokens.shape[1] > 16 or tokens.shape[1] < 1:
+        # S <= 16: the MFMA attention kernel (in-kernel head mirroring); 16 < S <= 64: the short-sequence kernel,
+        # head splices then go through the paired patch-spec splice
+        if tokens.dim() != 2 or tokens.shape != src_tokens.shape or tokens.shape[1] > 64 or tokens.shape[1] < 1:
             return None
         if any(hp.is_live for hp in self.hook_dict.values()):
             return None

@@ -139,8 +139,19 @@ class FusedAdam(torch.optim.Optimizer):
                     t.record_stream(stream)
         self._inflight = self._events[:len(chunks)] if overlap else None
 
+    @property
+    def split_mode(self) -> bool:
+        """``IIT_ADAM_OVERLAP=2``: a graph-replayed phase with a pending update is captured as one graph per forward
+        stage and the Adam chunks are launched eagerly on the side stream at replay, each stage's graph waiting for
+        its chunk's event between replays (cross-stream waits outside any graph; see GraphedTrainStep)."""
+        return self._bounds is not None and os.environ.get("IIT_ADAM_OVERLAP", "0") == "2"
+
     def wait_stage(self, k: int) -> None:
         """Forward gate: stage ``k``'s weights are about to be read (launches a deferred update on first call)."""
+        splitter = self.__dict__.get("_splitter")
+        if splitter is not None:  # split capture: the graph runner cuts a segment here (nothing launched / waited)
+            splitter(k)
+            return
         if self._pending is not None:
             self._launch_pending(overlap=True)
         ev = self._inflight

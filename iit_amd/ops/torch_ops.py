@@ -428,7 +428,8 @@ class TorchOps:
     @property
     def fuses_residual(self) -> bool:
         import os
-        return self.dtype == torch.bfloat16 and os.environ.get("IIT_TORCH_RESID_EPI", "1") != "0"
+        # opt-in until tests/test_llama_ops.py::test_llama_torch_backend_residual_epilogue_* has run on an MI355X
+        return self.dtype == torch.bfloat16 and os.environ.get("IIT_TORCH_RESID_EPI", "0") == "1"
 
     def _mat_resid(self, x2, resid, W, b, wm, gw_shape):
         """``resid + x2 @ wm (+ b)`` for arena weight ``W`` viewed as the 2-D mirror ``wm``; None when the
@@ -479,8 +480,8 @@ class TorchOps:
                                                                                    and w.is_contiguous()))):
             return None
         import os
-        if os.environ.get("IIT_LLAMA_FUSED", "1") == "0":
-            return None
+        if os.environ.get("IIT_LLAMA_FUSED", "1") == "0" or os.environ.get("IIT_RMS_FORK", "0") != "1":
+            return None  # (the fork is opt-in until validated on hardware, like the residual epilogue)
         from . import hip_ops
         return hip_ops.RMSNormForkFn.apply(x, w, eps)
 

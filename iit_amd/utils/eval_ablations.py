@@ -158,6 +158,9 @@ def resample_ablate_nodes(model_pair, base_in, ablation_in, nodes, results: Dict
         results[node] = results[node] + s[i]
 
 
+_EVAL_GRAPHS_DEFAULT = "0"  # "1" once the graphed sweeps have been validated against the eager ones on an MI355X
+
+
 class _SweepGraph:
     """A sweep's per-batch body (``fn(*batch) -> [n] scores``) run as ONE captured HIP graph per batch shape.
 
@@ -167,14 +170,14 @@ class _SweepGraph:
     accumulated in place on device; each later batch is a copy into the buffers and one replay -- no per-node
     Python or launch overhead (23 ms per spliced B=256 forward eagerly).  Sums are added in the
     same order as the eager loop, so the results are the eager ones bit for bit.  Batches of another shape (an
-    epoch tail) and bodies that cannot be captured run eagerly into the same accumulator.  ``IIT_EVAL_GRAPHS=0``
-    disables capture."""
+    epoch tail) and bodies that cannot be captured run eagerly into the same accumulator.  ``IIT_EVAL_GRAPHS=1|0``
+    turns capture on / off."""
 
     def __init__(self, fn, n: int, device):
         self.fn = fn
         self.acc = torch.zeros(n, dtype=torch.float32, device=device)
         self.enabled = (device.type == "cuda" and torch.cuda.is_available()
-                        and os.environ.get("IIT_EVAL_GRAPHS", "1") != "0")
+                        and os.environ.get("IIT_EVAL_GRAPHS", _EVAL_GRAPHS_DEFAULT) == "1")
         self.static = None
         self.sig = None
         self.graph = None

@@ -29,3 +29,7 @@ step eval_pvr 900 python3 -u scripts/eval_pvr_r4.py; grep -E "^\[pvr\]" $O/eval_
 step llama_tests 300 python3 -u -m pytest tests/test_llama_ops.py -x -v -m gpu --timeout 120 --timeout-method thread; tail -3 $O/llama_tests.log
 step dp_tests 400 python3 -u -m pytest tests/test_dp_rccl_gpu.py -x -v -m gpu --timeout 200 --timeout-method thread; tail -3 $O/dp_tests.log
 IIT_GEMM_TABLE=0 IIT_GEMM_REPORT=$O/gemm_report_isolated.txt step gemm_autotune 600 python3 -u bench.py --steps 5 --warmup 2; grep -E '^\{' $O/gemm_autotune.log | cut -c1-200
+step fam_mqnli 400 python3 -u scripts/bench_families.py --family mqnli-bert-base --steps 30 --warmup 5; grep -E '^\{' $O/fam_mqnli.log | cut -c1-250
+step fam_mqnli_prof 400 rocprofv3 --kernel-trace --output-format csv -d $O/mqprof -o mq -- python3 scripts/bench_families.py --family mqnli-bert-base --steps 12 --warmup 3
+f=$(find $O/mqprof -name "*kernel_trace.csv" | head -n 1)
+[ -n "$f" ] && python3 scripts/step_breakdown.py "$f" --steps 8 --top 30 --gaps 5 > $O/mqnli_breakdown.txt && head -40 $O/mqnli_breakdown.txt; rm -f "$f"

@@ -26,6 +26,8 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    # every (phase, node) graph captured before epoch 0 with the training state restored (BaseModelPair.train)
+    os.environ.setdefault("IIT_PRIME_GRAPHS", "1")
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="ioi-6l", choices=["ioi-6l", "gpt2-small"])
     ap.add_argument("--engine", default="native", choices=["native", "reference"])

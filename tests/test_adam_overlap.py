@@ -83,7 +83,8 @@ def test_overlap_disabled_by_env(monkeypatch):
 
 
 def _train(mode, overlap, monkeypatch, n_batches=8):
-    monkeypatch.setenv("IIT_ADAM_OVERLAP", "1" if overlap else "0")
+    # overlap: False, True (chunks inside the captured graphs) or "split" (per-stage graphs, chunks launched eagerly)
+    monkeypatch.setenv("IIT_ADAM_OVERLAP", "2" if overlap == "split" else ("1" if overlap else "0"))
     from iit_amd.data.iit_dataset import IITDataset
     from iit_amd.engine.graphs import GraphedTrainStep
     from iit_amd.model_pairs import IOI_ModelPair
@@ -100,7 +101,7 @@ def _train(mode, overlap, monkeypatch, n_batches=8):
     pair = IOI_ModelPair(hl, ll, make_ioi_corr(6), training_args={"batch_size": 64, "lr": 1e-3, "strict_weight": 0.4,
                                                                    "lr_scheduler": None})
     opt = pair.make_optimizer(1e-3)
-    assert (opt._bounds is not None) == overlap
+    assert (opt._bounds is not None) == bool(overlap)
     torch.manual_seed(1)
     batches = [b for _, b in zip(range(n_batches), train.make_loader(64, 0))]
     step, ctx, g = pair.run_train_step, contextlib.nullcontext(), None
@@ -122,10 +123,10 @@ def _train(mode, overlap, monkeypatch, n_batches=8):
 @pytest.mark.gpu
 @pytest.mark.skipif(os.environ.get("IIT_TEST_ADAM_OVERLAP") != "1",
                     reason="opt-in path (IIT_ADAM_OVERLAP=1) not yet run on hardware: set IIT_TEST_ADAM_OVERLAP=1")
-@pytest.mark.parametrize("mode", ["eager", "graphs"])
-def test_overlapped_update_matches_serial(mode, monkeypatch):
+@pytest.mark.parametrize("mode,overlap", [("eager", True), ("graphs", True), ("graphs", "split")])
+def test_overlapped_update_matches_serial(mode, overlap, monkeypatch):
     ls, ps, ss = _train(mode, False, monkeypatch)
-    lo, po, so = _train(mode, True, monkeypatch)
+    lo, po, so = _train(mode, overlap, monkeypatch)
     assert ss == so == 3 * 16  # three optimizer phases per step, every one counted once
     # same kernels, same order of every update: only fp32-atomic accumulation noise separates two runs
     # (tests/test_graphs.py); compare the early steps tightly and the weights loosely

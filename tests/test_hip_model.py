@@ -184,12 +184,13 @@ def test_bert_encoder_on_hip_matches_fp32_oracle():
         assert rel(pf.grad, pr.grad) < 8e-2, n
 
 
-def test_bert_paired_forward_equals_two_forwards():
+def test_bert_paired_forward_equals_two_forwards(monkeypatch):
     """HookedEncoder.run_paired (source rows folded into the base forward, MQNLI's hook_normalized_resid_post
     position sites, a head site and an MLP site) vs the truncated source capture + spliced base forward: same
     outputs and captured activations, same gradients, and the source rows get none."""
     from iit_amd.core.index import Ix
     from iit_amd.engine.plan import RunPlan
+    monkeypatch.setenv("IIT_BERT_PAIRED", "1")
     _, fast = _bert_pair_models()
     torch.manual_seed(1)
     tok = torch.randint(3, 64, (16, 15), device=dev)

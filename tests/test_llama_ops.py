@@ -110,6 +110,7 @@ def test_llama_torch_backend_residual_epilogue_matches_unfused(monkeypatch):
     outs, grads = [], []
     for model, fused in ((a, "1"), (b, "0")):
         monkeypatch.setenv("IIT_TORCH_RESID_EPI", fused)
+        monkeypatch.setenv("IIT_RMS_FORK", fused)
         monkeypatch.setenv("IIT_LLAMA_FUSED", "1")
         out = model(tok)
         out.float().pow(2).mean().backward()

@@ -82,6 +82,37 @@ def test_paired_matches_two_forwards(sites, logits):
         assert err < 2e-2, (k, err)
 
 
+@pytest.mark.parametrize("sites", [SITES[0], SITES[1], SITES[3], SITES[7]], ids=["whole_z", "head", "neurons", "pos"])
+def test_paired_longer_sequences(sites):
+    """16 < S <= 64: the short-sequence attention kernel (no in-kernel head mirroring; head sites go through the
+    paired patch-spec splice) -- same outputs and gradients as the two forwards."""
+    from iit_amd.models.transformer import HookedTransformer
+    S2 = 40
+    cfg = dict(n_layers=L, d_model=D, n_heads=H, d_head=DH, d_mlp=DM, n_ctx=S2, d_vocab=V, act_fn="gelu_new",
+               normalization_type="LNPre", device="cuda", dtype=torch.bfloat16, positional_embedding_type="standard")
+    torch.manual_seed(0)
+    m = HookedTransformer(cfg)
+    m.set_op_backend("hip")
+    g = torch.Generator(device="cuda").manual_seed(2)
+    base = torch.randint(0, V, (B, S2), device="cuda", generator=g)
+    src = torch.randint(0, V, (B, S2), device="cuda", generator=g)
+    w = torch.randn(B, V, device="cuda", generator=g)
+    m.zero_grad(set_to_none=True)
+    ref, _ = _unpaired(m, base, src, sites, "last")
+    (ref.float() * w).sum().backward()
+    g_ref = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad(set_to_none=True)
+    res = m.run_paired(base, src, sites, logits="last")
+    assert res is not None
+    out, _ = res
+    (out.float() * w).sum().backward()
+    assert torch.allclose(out.float(), ref.float(), rtol=2e-2, atol=2e-2)
+    for k, gr in g_ref.items():
+        gp = m.get_parameter(k).grad
+        scale = g_ref[k[:-3] + "b_Q"].norm() if k.endswith("b_K") else gr.norm()
+        assert float((gp - gr).norm() / (scale + 1e-12)) < 2e-2, k
+
+
 def test_paired_source_rows_get_no_gradient_and_no_graph():
     """The source activations returned by the paired forward are plain tensors (no autograd history)."""
     m = _model()
@@ -98,6 +129,8 @@ def test_paired_declines_what_it_does_not_cover():
     src = torch.randint(0, V, (B, S), device="cuda")
     assert m.run_paired(base, src, {"blocks.1.hook_resid_pre": [Ix[[None]]]}) is None
     assert m.run_paired(base, src[:, :8], {"blocks.1.attn.hook_z": [Ix[[None]]]}) is None
+    long = torch.randint(0, V, (B, 65), device="cuda")
+    assert m.run_paired(long, long, {"blocks.1.attn.hook_z": [Ix[[None]]]}) is None  # S > 64
     h = m.blocks[0].attn.hook_z.add_hook(lambda x, hook: x)
     try:
         assert m.run_paired(base, src, {"blocks.1.attn.hook_z": [Ix[[None]]]}) is None
