@@ -103,12 +103,9 @@ hipError_t launch_tile(const G2Args& a, int tile, hipStream_t s) {
     case 32: return launch<256, 128, 3, AKM, BKM, EPI, 8>(a, s);
     case 33: return launch<128, 256, 3, AKM, BKM, EPI, 8>(a, s);
     case 34: return launch<256, 256, 2, AKM, BKM, EPI, 8>(a, s);
-    // 288-wide tiles for the packed-QKV forward ([T][768] x [768][2304]): 8 N-tiles, so M = 8192 at 128 x 288 is
-    // exactly two 256-CU rounds (512 tiles) and M = 4096 exactly one, where 256 x 192 leaves a half-empty round
-    // (384 tiles); 2 x 2 waves of 64 x 144 (4 x 9 MFMA blocks), B staged as nine 32-column k-major panels
-    case 35: return launch<128, 288, 3, AKM, BKM, EPI>(a, s);
-    // (tile 36, 256 x 288 on 4 waves, spills 146 registers and crashes hipcc's AGPR rewrite: not offered)
-    case 37: return launch<128, 288, 2, AKM, BKM, EPI>(a, s);
+    // (tiles 35-37, 128 / 256 x 288 for the packed-QKV forward -- 8 N-tiles of [*][2304], whole 256-CU rounds --
+    // measured 52.9-53.9 us at M = 8192 vs 39.6 us for tile 27 and 39.0 us hipBLASLt, and the 2-deep 128 x 288
+    // returned NaNs (profiles/qkv_fwd_tiles_r4.txt): removed; not offered)
     default: return launch<128, 128, 4, AKM, BKM, EPI>(a, s);
   }
 }
@@ -130,7 +127,7 @@ static const int kTileBK[IIT_GLDS_TILES] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,
                                 long lda, long ldb, long ldc, long ldc2, long ldr, int M, int N, int K, int mode,
                                 int epi, int bias_cols, int tile, int splits, int reduce) {
-  if (tile < 0 || tile >= IIT_GLDS_TILES || tile == 19 || tile == 36) return 0;
+  if (tile < 0 || tile >= IIT_GLDS_TILES || tile == 19 || tile >= 35) return 0;
   // atomic split-K: fp32 accumulate only; reduction split-K (``reduce``): fp32 accumulate, store or residual add (the
   // last-arriving split runs the epilogue once on the summed tile)
   const bool split_epi = epi == E_F32_ACC || (reduce && (epi == E_F32_STORE || epi == E_F32_RESID));

@@ -207,6 +207,16 @@ __device__ __forceinline__ bf16x8 frag_use(const RawFrag<KMAJ>& f) {
   }
 }
 
+// One 16x16x32 product into an output block's accumulator.  TR = false: C = A B, lane l holds rows 4 (l >> 4) + r
+// of column l & 15 (the MFMA's native layout).  TR = true: the operands enter swapped, the MFMA computes the block
+// of C^T, so lane l holds row l & 15, COLUMNS 4 (l >> 4) + r -- four consecutive outputs of one row, which the
+// epilogue moves into its row-major LDS tile with ONE 16-byte write per accumulator instead of four 4-byte ones.
+template <bool TR>
+__device__ __forceinline__ f32x4 mfma_tile(const bf16x8 a, const bf16x8 b, const f32x4 c) {
+  if constexpr (TR) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid % 8;
   const int q = nwg / 8, r = nwg % 8;
@@ -311,6 +321,9 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
   static_assert(SM::BYTES <= SM::LDS_BUDGET, "LDS budget");
   static_assert(STAGE == SM::STAGE, "stage size");
 
+  // transposed accumulators (mfma_tile) for every epilogue that goes through the LDS tile; the atomic split-K
+  // partials of E_F32_ACC keep the native layout (16 consecutive columns per lane group, 64-B atomic segments)
+  constexpr bool TR = EPI != E_F32_ACC;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;  // wave (wm, wn) of the WMR x 2 grid
   const int tiles_n = p.N / BN;
@@ -394,7 +407,7 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_tile<TR>(a[i], b[j], acc[i][j]);
       if constexpr (CS) {
         if (do_cs) {
 #pragma unroll
@@ -444,7 +457,7 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_tile<TR>(a[i], b[j], acc[i][j]);
       if constexpr (CS) {
         if (do_cs) {
 #pragma unroll
@@ -584,10 +597,16 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int col = wn * WN + j * 16 + (lane & 15);
-        const int row = (wm % (WMR / ECH)) * WM + i * 16 + 4 * (lane >> 4);
+        if constexpr (TR) {  // lane: row l & 15, columns 4 (l >> 4) .. + 3 -> one 16-B LDS write
+          const int col = wn * WN + j * 16 + 4 * (lane >> 4);
+          const int row = (wm % (WMR / ECH)) * WM + i * 16 + (lane & 15);
+          *(f32x4*)(E + row * EPS + col) = acc[i][j];
+        } else {
+          const int col = wn * WN + j * 16 + (lane & 15);
+          const int row = (wm % (WMR / ECH)) * WM + i * 16 + 4 * (lane >> 4);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) E[(row + r) * EPS + col] = acc[i][j][r];
+          for (int r = 0; r < 4; ++r) E[(row + r) * EPS + col] = acc[i][j][r];
+        }
       }
   }
   __syncthreads();

@@ -240,7 +240,9 @@ IIT_EXPORT int iit_ln_fwd_sel(const float* x, const float* w, const float* b, vo
 // separate gradient-sum pass over the fp32 residual.  ``dx16`` (nullable) receives a bf16 copy of dx: the
 // next backward GEMMs (W_O / W_out dX and dW) read bf16, so the cast rides along with this pass.
 // The affine gradients dw/db are NOT done here (see ln_dwdb_kernel: per-block partial sums, few atomics).
-template <int V4, bool DY_F32>
+// XH16: ``x`` is the forward's bf16 output xhat of a norm without affine parameters (LNPre): 2 bytes per element
+// instead of the fp32 input, and no mean
+template <int V4, bool DY_F32, bool XH16 = false>
 __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
                                                          const float* __restrict__ w, float* __restrict__ dx,
@@ -265,8 +267,13 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const void* __restrict_
         const bf16x4 t = ((const bf16x4*)dy_)[(long)row * d4 + c];
         dy = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
       }
-      const float4 xx = ((const float4*)x)[(long)row * d4 + c];
-      xv = make_float4((xx.x - mu) * rs, (xx.y - mu) * rs, (xx.z - mu) * rs, (xx.w - mu) * rs);
+      if constexpr (XH16) {
+        const bf16x4 t = ((const bf16x4*)x)[(long)row * d4 + c];
+        xv = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
+      } else {
+        const float4 xx = ((const float4*)x)[(long)row * d4 + c];
+        xv = make_float4((xx.x - mu) * rs, (xx.y - mu) * rs, (xx.z - mu) * rs, (xx.w - mu) * rs);
+      }
       if (w) {
         const float4 ww = ((const float4*)w)[c];
         dy.x *= ww.x; dy.y *= ww.y; dy.z *= ww.z; dy.w *= ww.w;
@@ -385,6 +392,27 @@ IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const floa
                           const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db, int T, int d,
                           int accumulate, void* stream) {
   return iit_ln_bwd_sel(dy, dy_f32, x, mean, rstd, w, dx, dres, dx16, dw, db, T, d, accumulate, 0ull, 1, stream);
+}
+
+// LNPre backward from the forward's bf16 output (``xh`` = xhat, [T, d]); no affine parameters, no row select
+IIT_EXPORT int iit_ln_bwd_xh16(const void* dy, int dy_f32, const void* xh, const float* rstd, float* dx,
+                               const float* dres, void* dx16, int T, int d, int accumulate, void* stream) {
+  if (d % 4 || d > 4096 || (((uintptr_t)xh) & 7) || !aligned16(dx) || (dres && !aligned16(dres)) ||
+      (dy_f32 ? !aligned16(dy) : (((uintptr_t)dy) & 7) != 0) || (((uintptr_t)dx16) & 7))
+    return (int)hipErrorInvalidValue;
+  const RowSel sel{0ull, 1, T};
+  dim3 grid((T + 3) / 4), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  __bf16* d16 = (__bf16*)dx16;
+  const float* x = (const float*)xh;
+#define LNBX(V)                                                                                                   \
+  if (dy_f32) hipLaunchKernelGGL((ln_bwd_vec_kernel<V, true, true>), grid, block, 0, s, dy, x, rstd, rstd, nullptr, dx, dres, d16, T, d, accumulate, sel); \
+  else hipLaunchKernelGGL((ln_bwd_vec_kernel<V, false, true>), grid, block, 0, s, dy, x, rstd, rstd, nullptr, dx, dres, d16, T, d, accumulate, sel);
+  const int v4 = (d / 4 + 63) / 64;
+  if (v4 <= 1) { LNBX(1) } else if (v4 <= 2) { LNBX(2) } else if (v4 <= 3) { LNBX(3) } else if (v4 <= 4) { LNBX(4) }
+  else if (v4 <= 6) { LNBX(6) } else if (v4 <= 8) { LNBX(8) } else if (v4 <= 12) { LNBX(12) } else { LNBX(16) }
+#undef LNBX
+  return hipGetLastError();
 }
 
 // backward of iit_ln_fwd_sel over the base rows (T = Tb): rows at masked positions get dx = dres only and add
@@ -745,7 +773,7 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
                                                         int nspans, const float* __restrict__ part, int nparts,
                                                         float clip, float lr, float b1, float b2, float eps, float wd,
                                                         const float* __restrict__ hyper, int* __restrict__ step,
-                                                        int* __restrict__ skipped, int book = 1) {
+                                                        int* __restrict__ skipped) {
   // ``hyper`` (nullable): device copy of {lr, beta1, beta2, eps, weight_decay}.  A captured graph replays the
   // kernel arguments it saw at capture; reading the hyper-parameters from device memory lets the host change the
   // learning rate (an LR scheduler) between replays with one small copy.
@@ -770,7 +798,7 @@ __global__ __launch_bounds__(256) void adam_span_kernel(float* __restrict__ p, c
   }
   __syncthreads();
   if (bad_s) {  // non-finite gradient: skip the whole update (uniform over the grid), count it, undo the step bump
-    if (book && blockIdx.x == 0 && threadIdx.x == 0) {  // (one launch of a chunked update keeps the books)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
       step[0] -= 1;
       skipped[0] += 1;
     }
@@ -935,28 +963,6 @@ IIT_EXPORT int iit_adam_spans(float* p, const float* g, float* m, float* v, void
   hipLaunchKernelGGL((adam_span_kernel<true, 1>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
                      (__bf16*)mirror, (const Span*)spans, nspans, total, 1, clip, lr, b1, b2, eps, wd, hyper, step,
                      skipped);
-  return hipGetLastError();
-}
-
-// Chunked update (iit_amd/ops/optim.py, overlapped Adam): the norm stage alone, then the Adam pass over a slice of the
-// span table per launch -- the next forward's layers each wait for the slice holding their weights.  ``book`` marks
-// the one launch that undoes the step bump / counts a skipped (non-finite) step.
-IIT_EXPORT int iit_adam_norm(const float* g, const void* spans, int nspans, float* part, int nparts, int do_norm,
-                             int* step, float* gsq, void* stream) {
-  hipLaunchKernelGGL(sumsq_span_kernel, dim3(do_norm ? nparts : 1), dim3(256), 0, (hipStream_t)stream, g,
-                     (const Span*)spans, nspans, part, do_norm, step, gsq);
-  return hipGetLastError();
-}
-
-IIT_EXPORT int iit_adam_chunk(float* p, const float* g, float* m, float* v, void* mirror, const void* spans,
-                              int nspans, const float* part, int nparts, float clip, float lr, float b1, float b2,
-                              float eps, float wd, const float* hyper, int* step, int* skipped, int book,
-                              void* stream) {
-  if (nspans <= 0) return hipSuccess;
-  const int blocks = min(nspans, 4096);
-  hipLaunchKernelGGL((adam_span_kernel<true, 2>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
-                     (__bf16*)mirror, (const Span*)spans, nspans, part, nparts, clip, lr, b1, b2, eps, wd, hyper, step,
-                     skipped, book);
   return hipGetLastError();
 }
 

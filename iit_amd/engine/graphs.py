@@ -152,8 +152,6 @@ class _TrainState:
         self.opt = optimizer
         self.scalars = {}
         if optimizer is not None and hasattr(optimizer, "exp_avg"):  # FusedAdam / ShardedFusedAdam
-            if hasattr(optimizer, "join_pending"):
-                optimizer.join_pending()
             for t in (optimizer.exp_avg, optimizer.exp_avg_sq, optimizer._step_dev, optimizer._skipped_dev):
                 if t is not None:
                     self.pairs.append((t, t.clone()))
@@ -174,8 +172,6 @@ class _TrainState:
     @torch.no_grad()
     def restore(self) -> None:
         opt = self.opt
-        if opt is not None and hasattr(opt, "join_pending"):
-            opt.join_pending()
         for live, saved in self.pairs:
             live.copy_(saved)
         for k, v in self.scalars.items():
@@ -421,18 +417,13 @@ class GraphedTrainStep:
         return _clone_out(static_out)
 
     def _run_phase(self, key, compute_loss, optimizer, step_fn):
-        # a deferred optimizer update (FusedAdam.defer_next) crosses the phase boundary: a phase captured with one
-        # pending launches it (its own graph), and one that leaves one behind hands the record on at each replay
-        pend_in = getattr(optimizer, "_pending", None) is not None
-        full = (key, self._sig) + ((True,) if pend_in else ())
+        full = (key, self._sig)
         if not self.enabled or self._current_eager:
             return self._eager(compute_loss, optimizer, step_fn)
         if self.split:
             if not self._splittable(step_fn):
                 return self._eager(compute_loss, optimizer, step_fn)
             return self._run_split_phase(full, key, compute_loss, optimizer)
-        if pend_in and getattr(optimizer, "split_mode", False):
-            return self._run_staged_update_phase(full, key, compute_loss, optimizer, step_fn)
         ent = self.graphs.get(full)
         if ent is None:
             n = self.seen.get(full, 0)
@@ -444,14 +435,12 @@ class GraphedTrainStep:
             if self.pool is None or os.environ.get("IIT_GRAPH_POOL") == "private":
                 self.pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
-            guard = optimizer.capture_guard() if hasattr(optimizer, "capture_guard") else None
             try:
                 with _CaptureGC(), torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                     out = compute_loss()
                     loss = out[0] if isinstance(out, tuple) else out
                     step_fn(loss, optimizer)
                     static_out = _detach_out(out)
-                    pend_out = getattr(optimizer, "_pending", None)
             except Exception as e:  # something in the phase is not capturable: keep it eager
                 self.failed[full] = repr(e)
                 # an aborted capture leaves its private memory pool unusable for the next capture (the caching
@@ -462,107 +451,17 @@ class GraphedTrainStep:
                 print(f"[iit graphs] phase {key} not captured ({type(e).__name__}: {str(e)[:160]}); "
                       f"running it eagerly\n{tb}")
                 torch.cuda.synchronize()
-                if guard is not None:  # a pending update launched inside the aborted capture never ran
-                    guard()
                 return self._eager(compute_loss, optimizer, step_fn)
             if _RECAPTURE_ALL:  # diagnostics: a new capture drops every other graph (recaptured at next use)
                 self.graphs.clear()
-            ent = self.graphs[full] = (g, static_out, pend_out)
+            ent = self.graphs[full] = (g, static_out)
             self.captures += 1
-        g, static_out, pend_out = ent
+        g, static_out = ent
         _sync_hyper(optimizer)
         if _SYNC_BEFORE_REPLAY:
             torch.cuda.current_stream().synchronize()
         with trace_range("graph:phase"):
             g.replay()
-        if pend_in or pend_out is not None:
-            optimizer._pending = pend_out
-        sync_point()
-        self.replays += 1
-        return _clone_out(static_out)
-
-    def _run_staged_update_phase(self, full, key, compute_loss, optimizer, step_fn):
-        """A phase that starts with the previous phase's Adam still pending, under ``IIT_ADAM_OVERLAP=2``: captured
-        as one graph per forward stage (cut at the model's stage gates), replayed as ``launch the Adam chunks
-        eagerly on the side stream; for each stage: wait for its chunk's event, replay its graph``.  The waits are
-        between graph launches, so the chunks of later stages run beside the earlier stages' kernels on a second
-        hardware queue -- the overlap graph branches did not give (profiles/graph_branch_concurrency_r3.txt)."""
-        ent = self.graphs.get(full)
-        if ent is None:
-            n = self.seen.get(full, 0)
-            if n < self.warmup or full in self.failed:
-                self.seen[full] = n + 1
-                return self._eager(compute_loss, optimizer, step_fn)
-            if self.pool is None or os.environ.get("IIT_GRAPH_POOL") == "private":
-                self.pool = torch.cuda.graph_pool_handle()
-            segs = []  # (gate k or None, graph)
-            state = {"g": torch.cuda.CUDAGraph(), "gate": None, "done": False}
-            cap_stream = self.stream if self.stream is not None else torch.cuda.Stream()
-            n_chunks = len(optimizer._bounds)
-
-            def splitter(k):
-                if state["done"]:
-                    return  # gates after the last chunk's (a second forward of the phase): already waited
-                state["g"].capture_end()
-                segs.append((state["gate"], state["g"]))
-                state["g"] = torch.cuda.CUDAGraph()
-                state["g"].capture_begin(self.pool, capture_error_mode=_CAPTURE_MODE)
-                state["gate"] = k
-                if k >= n_chunks - 1:
-                    state["done"] = True
-
-            pending = optimizer._pending
-            optimizer._pending = None  # launched eagerly at every replay, never captured
-            import gc
-            gc.collect()
-            torch.cuda.synchronize()
-            gc_was = gc.isenabled()
-            gc.disable()
-            try:
-                with torch.cuda.stream(cap_stream):
-                    optimizer.__dict__["_splitter"] = splitter
-                    state["g"].capture_begin(self.pool, capture_error_mode=_CAPTURE_MODE)
-                    try:
-                        out = compute_loss()
-                        optimizer.__dict__.pop("_splitter", None)
-                        loss = out[0] if isinstance(out, tuple) else out
-                        step_fn(loss, optimizer)
-                        static_out = _detach_out(out)
-                        pend_out = getattr(optimizer, "_pending", None)
-                    finally:
-                        optimizer.__dict__.pop("_splitter", None)
-                        state["g"].capture_end()
-                    segs.append((state["gate"], state["g"]))
-            except Exception as e:  # noqa: BLE001 - keep this phase eager
-                self.failed[full] = repr(e)
-                self.pool = None
-                print(f"[iit graphs] staged-update phase {key} not captured ({type(e).__name__}: {str(e)[:160]}); "
-                      f"eager")
-                torch.cuda.synchronize()
-                optimizer._pending = pending
-                return self._eager(compute_loss, optimizer, step_fn)
-            finally:
-                if gc_was:
-                    gc.enable()
-            if self.stream is None:
-                torch.cuda.current_stream().wait_stream(cap_stream)
-            optimizer._pending = pending
-            ent = self.graphs[full] = (segs, static_out, pend_out)
-            self.captures += 1
-        segs, static_out, pend_out = ent
-        _sync_hyper(optimizer)
-        cur = torch.cuda.current_stream()
-        with trace_range("graph:staged_update_phase"):
-            optimizer._launch_pending(overlap=True)  # the previous phase's Adam chunks, on the side stream
-            ev = optimizer._inflight or []
-            for gate, g in segs:
-                if gate is not None and ev:
-                    cur.wait_event(ev[min(gate, len(ev) - 1)])
-                g.replay()
-            if ev:
-                cur.wait_event(ev[-1])  # every chunk joined before anything after the phase
-            optimizer._inflight = None
-        optimizer._pending = pend_out
         sync_point()
         self.replays += 1
         return _clone_out(static_out)

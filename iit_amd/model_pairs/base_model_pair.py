@@ -275,7 +275,7 @@ class BaseModelPair(ABC):
 
         return ll_ablation_hook
 
-    def run_phase(self, key, compute_loss: Callable[[], Tensor], optimizer, step_fn, defer_update: bool = False):
+    def run_phase(self, key, compute_loss: Callable[[], Tensor], optimizer, step_fn):
         """One optimizer phase of a train step: ``loss = compute_loss(); step_fn(loss, optimizer)``.
 
         ``compute_loss`` may return ``(loss, extras)``; the phase then returns
@@ -285,17 +285,8 @@ class BaseModelPair(ABC):
         :class:`iit_amd.engine.graphs.GraphedTrainStep` can capture each distinct
         phase once as a HIP graph and replay it; without a runner it runs eagerly.
 
-        ``defer_update``: another phase of the same step follows, so a fused optimizer may leave this phase's Adam
-        to run under that phase's forward (FusedAdam.defer_next)."""
-        if hasattr(optimizer, "defer_next"):
-            optimizer.defer_next = defer_update
-        try:
-            return self._run_phase_now(key, compute_loss, optimizer, step_fn)
-        finally:
-            if hasattr(optimizer, "defer_next"):
-                optimizer.defer_next = False
-
-    def _run_phase_now(self, key, compute_loss, optimizer, step_fn):
+        (A phase's Adam overlapped with the next phase's forward was measured and removed: the forward GEMMs leave
+        no room for a co-resident memory-bound pass, profiles/adam_overlap_r4.txt.)"""
         runner = getattr(self, "_phase_runner", None)
         if runner is not None:
             with trace_range(f"phase:{key[0]}"):
@@ -349,14 +340,6 @@ class BaseModelPair(ABC):
                                   and not getattr(opt, "sharded", False)
                                   and not self.rewrites_grads_before_step()
                                   and os.environ.get("IIT_FUSED_NORM", "1") != "0")
-            # overlapped update: a phase's Adam runs under the next phase's forward (FusedAdam.enable_overlap) -- one
-            # process, a model that gates its stages (the bf16 weight mirror is checked at each deferral)
-            stages = getattr(module, "param_stages", None)
-            if (self._reducer is None and not getattr(opt, "sharded", False) and hasattr(opt, "enable_overlap")
-                    and stages is not None and opt.enable_overlap(stages())):
-                module.__dict__["_param_gate"] = opt.wait_stage
-                module.__dict__["_param_join"] = opt.join_pending
-                self._overlap_opt = opt
         return opt
 
     def rewrites_grads_before_step(self) -> bool:
@@ -423,9 +406,6 @@ class BaseModelPair(ABC):
 
     def backward(self, loss: Tensor) -> None:
         """``loss.backward()`` + data-parallel gradient averaging + reference grad semantics."""
-        ov = self.__dict__.get("_overlap_opt")
-        if ov is not None:  # a deferred update reads the gradients this backward rewrites
-            ov.join_pending()
         reducer = getattr(self, "_reducer", None)
         if reducer is not None:
             reducer.start()

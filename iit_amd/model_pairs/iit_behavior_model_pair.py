@@ -87,7 +87,7 @@ class IITBehaviorModelPair(IITModelPair):
 
             _, parts = self.run_phase(("single", hl_node.name), total, optimizer, self.step_on_loss)
             return {"train/iit_loss": parts["iit"], "train/behavior_loss": parts["behavior"]}
-        iit_loss = self.run_phase(("iit", hl_node.name), iit, optimizer, self.step_on_loss, defer_update=True)
+        iit_loss = self.run_phase(("iit", hl_node.name), iit, optimizer, self.step_on_loss)
         behavior_loss = self.run_phase(("behavior",), behavior, optimizer, self.step_on_loss)
         return {"train/iit_loss": iit_loss, "train/behavior_loss": behavior_loss}
 

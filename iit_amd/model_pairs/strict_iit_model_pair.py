@@ -71,13 +71,13 @@ class StrictIITModelPair(IITBehaviorModelPair):
                                       self.step_on_loss)
             return {"train/iit_loss": parts["iit"], "train/behavior_loss": parts["behavior"],
                     "train/strict_loss": parts["strict"]}
-        iit_loss = self.run_phase(("iit", hl_node.name), iit, optimizer, self.step_on_loss, defer_update=True)
+        iit_loss = self.run_phase(("iit", hl_node.name), iit, optimizer, self.step_on_loss)
         # the strict node is drawn after the IIT phase, as in the reference (same RNG stream)
         ll_node = self.sample_ll_node()
         strict_loss = self.run_phase(
             ("strict", ll_node.name, repr(ll_node.index)),
             lambda: self.get_strict_loss_over_batch(base_input, ablation_input, ll_node, loss_fn) * args["strict_weight"],
-            optimizer, self.step_on_loss, defer_update=True)
+            optimizer, self.step_on_loss)
         behavior_loss = self.run_phase(
             ("behavior",), lambda: self.get_behaviour_loss_over_batch(base_input, loss_fn) * args["behavior_weight"],
             optimizer, self.step_on_loss)

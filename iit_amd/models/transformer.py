@@ -612,13 +612,6 @@ class HookedTransformer(HookedRootModule):
             groups.append((d * Vp, [(self.unembed.W_U, lambda buf: buf.view(d, Vp)[:, :V])]))
         return groups
 
-    def param_stages(self):
-        """Parameters in forward order, one list per stage (embeddings, each block, final norm + unembed): the
-        chunks of an overlapped optimizer update (FusedAdam.enable_overlap); ``_param_gate(k)`` runs before stage k."""
-        first = [p for m in (self.embed, getattr(self, "pos_embed", None)) if m is not None for p in m.parameters()]
-        last = [p for m in (self.ln_final, self.unembed) if m is not None for p in m.parameters()]
-        return [first] + [list(b.parameters()) for b in self.blocks] + [last]
-
     # ------------------------------------------------------------------ backend
     def set_op_backend(self, backend: Optional[str]) -> "HookedTransformer":
         self.op_backend = backend
@@ -649,9 +642,6 @@ class HookedTransformer(HookedRootModule):
         if tokens.device != self.embed.W_E.device:
             tokens = tokens.to(self.embed.W_E.device)
         run = _Run(plan, self.ops())
-        gate = self.__dict__.get("_param_gate")  # overlapped optimizer update (FusedAdam.wait_stage)
-        if gate is not None:
-            gate(0)
         begin = getattr(run.ops, "begin_forward", None)
         if begin is not None:
             begin()
@@ -670,8 +660,6 @@ class HookedTransformer(HookedRootModule):
                     leaf = resid.detach().requires_grad_(True)
                     self._cut_log.append((li, resid, leaf))
                     resid = leaf
-                if gate is not None:
-                    gate(li + 1)
                 resid = block(resid, run, last_only=last_only and li == len(self.blocks) - 1)
             if stop_at_layer is not None:
                 return resid
@@ -679,8 +667,6 @@ class HookedTransformer(HookedRootModule):
                 return None
             if return_type is None:
                 return None
-            if gate is not None:
-                gate(len(self.blocks) + 1)
             if want == "last":
                 resid = resid[:, -1]  # [B, d]: only the position every IOI loss reads
             x = resid if self.ln_final is None else self.ln_final.run(resid, run)
@@ -755,9 +741,6 @@ class HookedTransformer(HookedRootModule):
         tokens = tokens.to(self.embed.W_E.device)
         src_tokens = src_tokens.to(self.embed.W_E.device)
         run = _Run(RunPlan(logits=logits), ops)
-        gate = self.__dict__.get("_param_gate")
-        if gate is not None:
-            gate(0)
         ops.begin_forward()
         n = len(self.blocks)
         final_mlp_site = not cfg.attn_only and self.blocks[-1].mlp.hook_post.name in sites
@@ -769,8 +752,6 @@ class HookedTransformer(HookedRootModule):
         cuts = self.__dict__.get("_grad_cuts") if torch.is_grad_enabled() else None
         for li, block in enumerate(self.blocks):
             lo = last_only and li == n - 1
-            if gate is not None:
-                gate(li + 1)
             base = resid.base if paired else resid
             if cuts and li in cuts and base.requires_grad:
                 # staged backward (engine.staged): the backward stops here and resumes as its own segment; the
@@ -786,8 +767,6 @@ class HookedTransformer(HookedRootModule):
             resid = resid.base
         if logits == "none":
             return None, captures
-        if gate is not None:
-            gate(n + 1)
         if logits == "last":
             resid = resid[:, -1]
         x = resid if self.ln_final is None else self.ln_final.run(resid, run)

@@ -19,6 +19,7 @@ can say which GEMMs ran on hand-written MFMA code.
 from __future__ import annotations
 
 import os
+import re
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -280,6 +281,15 @@ def _blas16(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, resid, ldr):
 _BLAS16_EPIS = (K.EPI_F32_RESID, K.EPI_F32_ACC)
 
 
+# diagnostics: ``IIT_GEMM_EXCLUDE`` = comma-separated regular expressions of candidate names the dispatcher must not
+# offer (shipped decisions naming one are re-measured among the rest); "hip" always stays
+_EXCLUDE = [re.compile(x) for x in os.environ.get("IIT_GEMM_EXCLUDE", "").split(",") if x]
+
+
+def _excluded(name: str) -> bool:
+    return name != "hip" and any(r.fullmatch(name) for r in _EXCLUDE)
+
+
 def _candidates(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, bias2, resid, ldr, aux, ldc2,
                 bias_cols, qkv, splits, blas_bias, policy, csum_box=None):
     """name -> f(c, c2, c3) for every implementation that covers the problem.
@@ -288,6 +298,8 @@ def _candidates(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, b
     ``csum_box[0]`` -- fused in the LDS-DMA kernel's DGELU epilogue, a column-sum pass after the others."""
     calls = _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, bias2, resid, ldr, aux,
                               ldc2, bias_cols, qkv, splits, blas_bias, policy, csum_box)
+    if _EXCLUDE:
+        calls = {n: f for n, f in calls.items() if not _excluded(n)}
     if csum_box is not None:
         for name in list(calls):
             if not name.startswith("glds"):
@@ -607,7 +619,8 @@ def _dual_candidates(x: dict, w: dict, xc, wc, csum, bsum=None, gsq=None):
                     continue  # atomic split-K: accumulate only, never in deterministic mode
                 if sp > 1 and w["K"] // sp < 256:
                     continue
-                if K.gemm_dual_ok(ws, xs, wt, xt, sp, red):
+                if K.gemm_dual_ok(ws, xs, wt, xt, sp, red) and not _excluded(
+                        f"dual{wt}.{xt}" + (f"{'r' if red else 'k'}{sp}" if sp > 1 else "")):
                     out[f"dual{wt}.{xt}" + (f"{'r' if red else 'k'}{sp}" if sp > 1 else "")] = \
                         lambda wt=wt, xt=xt, sp=sp, red=red: K.gemm_dual(ws, xs, wt, xt, sp, red)
     return out
@@ -631,7 +644,7 @@ def gemm_pair(x: dict, w: dict) -> Optional[str]:
     choice = DUAL_DECISIONS.get(key)
     if choice is None:
         shipped = _table().get(repr(key))
-        if shipped is not None:
+        if shipped is not None and not _excluded(shipped):
             choice = DUAL_DECISIONS[key] = (shipped, {shipped: float("nan")})
     if choice is None:
         if torch.cuda.is_current_stream_capturing():

@@ -36,6 +36,7 @@ _SIGS = {
     "iit_ln_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
     "iit_ln_bwd": [c_void_p, c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_void_p],
     "iit_ln_fwd_sel": [c_void_p] * 6 + [c_int, c_int, c_float, c_ull, c_int, c_int, c_void_p],
+    "iit_ln_bwd_xh16": [c_void_p, c_int] + [c_void_p] * 5 + [c_int, c_int, c_int, c_void_p],
     "iit_ln_bwd_sel": [c_void_p, c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_ull, c_int, c_void_p],
     "iit_attn_small_fwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float, c_int,
                                             c_void_p],
@@ -54,8 +55,6 @@ _SIGS = {
     "iit_adam_span_size": [],
     "iit_sumsq_spans": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "iit_adam_spans": [c_void_p] * 6 + [c_int, c_void_p] + [c_float] * 6 + [c_void_p] * 4,
-    "iit_adam_norm": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
-    "iit_adam_chunk": [c_void_p] * 6 + [c_int, c_void_p, c_int] + [c_float] * 6 + [c_void_p] * 3 + [c_int, c_void_p],
     "iit_gelu_fwd": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_void_p],
     "iit_shadow_refresh": [c_void_p, c_int, c_void_p],
     "iit_shadow_desc_size": [],
@@ -193,9 +192,7 @@ GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 1
               # two co-resident workgroups per CU (<= 80 KiB LDS each): prologue / epilogue overlap
               23: (128, 96), 24: (64, 96), 25: (128, 128), 26: (96, 96), 27: (128, 192), 28: (64, 192),
               29: (64, 96), 30: (64, 64), 31: (64, 128),  # three / four workgroups per CU
-              32: (256, 128), 33: (128, 256), 34: (256, 256),  # 8 waves: 3-deep rings (32, 33), 256 x 256 (34)
-              # 288-wide tiles (the packed-QKV forward: 8 N-tiles of [*][2304]), 3- and 2-deep rings
-              35: (128, 288), 37: (128, 288)}
+              32: (256, 128), 33: (128, 256), 34: (256, 256)}  # 8 waves: 3-deep rings (32, 33), 256 x 256 (34)
 # tiles 12-14 measured slower than their 4-deep twins on every step shape (profiles/gemm_ring_depth_r2.txt: the tiles
 # are intake-bandwidth-bound, not latency-bound), so the dispatcher does not offer them; kept for the experiment.
 # Tiles 15-18 (128-deep K-tiles) are within a few % of the 64-deep tiles and compete per shape.
@@ -388,6 +385,16 @@ def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False, dres=None, 
                 ("dx16", dx16, T, d, d), ("mean", mean, 1, T, T))
     _check(lib().iit_ln_bwd(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx),
                             _p(dres), _p(dx16), _p(dw), _p(db), T, d, int(accumulate), _stream()), "ln_bwd")
+
+
+def ln_bwd_xh16(dy, xh, rstd, dx, T, d, dres=None, dx16=None):
+    """LNPre backward from the forward's bf16 output ``xh`` (= xhat; 2 B per element instead of the fp32 input)."""
+    if CHECK_BOUNDS:
+        _bounds("ln_bwd_xh16", ("dy", dy, T, d, d), ("xh", xh, T, d, d), ("dx", dx, T, d, d), ("dres", dres, T, d, d),
+                ("dx16", dx16, T, d, d), ("rstd", rstd, 1, T, T))
+    assert xh.dtype == torch.bfloat16
+    _check(lib().iit_ln_bwd_xh16(_p(dy), int(dy.dtype == torch.float32), _p(xh), _p(rstd), _p(dx), _p(dres),
+                                 _p(dx16), T, d, 0, _stream()), "ln_bwd_xh16")
 
 
 def ln_fwd_sel(x, w, b, y, mean, rstd, T, d, eps, pos_mask: int, S: int, Tb: int):
@@ -645,34 +652,6 @@ def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_
                                _p(hyper), _p(step_dev), _p(skipped), _p(sq_spans), n_sq, _p(gsq), _stream()),
            "adam_flat")
     flat.after_step(mirror_written=flat.shadow is not None)
-
-
-def adam_norm_stage(flat, step_dev, *, clip_norm, skipped=None):
-    """First half of a chunked fused Adam (FusedAdam's overlapped update): the global-norm partials and the device
-    step bump, as ``adam_step`` launches them; returns the argument record ``adam_chunk`` launches read."""
-    nparts = 1024
-    part = getattr(flat, "_norm_parts", None)
-    if part is None or part.numel() < nparts:
-        part = flat._norm_parts = torch.zeros(nparts, dtype=torch.float32, device=flat.data.device)
-    spans, nspans = flat.span_table(lib().iit_adam_span_size())
-    sq_spans, n_sq, gsq = flat.norm_spans(lib().iit_adam_span_size())
-    norm = bool(clip_norm) or skipped is not None
-    _check(lib().iit_adam_norm(_p(flat.grad), _p(sq_spans if sq_spans is not None else spans),
-                               n_sq if sq_spans is not None else nspans, _p(part), nparts, int(norm), _p(step_dev),
-                               _p(gsq), _stream()), "adam_norm")
-    return {"spans": spans, "nspans": nspans, "part": part, "nparts": nparts, "clip": float(clip_norm or 0.0),
-            "skipped": skipped}
-
-
-def adam_chunk(flat, exp_avg, exp_avg_sq, step_dev, rec, lo: int, hi: int, *, lr, b1, b2, eps, wd, hyper,
-               book: bool):
-    """Adam over span-table entries [lo, hi) of a norm stage's record (``adam_norm_stage``) on the current
-    stream; ``book``: the one chunk that keeps the skipped-step books."""
-    sb = lib().iit_adam_span_size()
-    _check(lib().iit_adam_chunk(_p(flat.data), _p(flat.grad), _p(exp_avg), _p(exp_avg_sq), _p(flat.shadow),
-                                rec["spans"].data_ptr() + lo * sb, hi - lo, _p(rec["part"]), rec["nparts"],
-                                rec["clip"], lr, b1, b2, eps, wd, _p(hyper), _p(step_dev), _p(rec["skipped"]),
-                                int(book), _stream()), "adam_chunk")
 
 
 IOI_HL_NODES = {"all_nodes_hook": 0, "hook_duplicate": 1, "hook_s_inhibition": 2, "hook_name_mover": 3}

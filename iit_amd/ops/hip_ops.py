@@ -439,6 +439,35 @@ def _bf16_of(t: torch.Tensor) -> torch.Tensor:
     return t.to(BF16)
 
 
+def _xhat16(w, b, d: int) -> bool:
+    """The LN backward reads the forward's bf16 output as xhat (norms without weight and bias) -- opt-in
+    (``IIT_LN_XHAT16=1``) until it has run on hardware against the staged-backward test."""
+    return w is None and b is None and d % 4 == 0 and d <= 4096 and os.environ.get("IIT_LN_XHAT16", "0") == "1"
+
+
+def _ln_fork_bwd(ctx, dy, dpass):
+    xs, mean, rstd = ctx.saved_tensors
+    w, b = ctx.params
+    T, d = xs.shape
+    dres = None
+    if dpass is not None:
+        dres = _flat2(dpass.float().contiguous())
+    dx = torch.empty(T, d, dtype=F32, device=xs.device)
+    dx16 = torch.empty(T, d, dtype=BF16, device=xs.device) if ctx.in_dtype == F32 else None
+    if xs.dtype == BF16:
+        K.ln_bwd_xh16(_flat2(dy.contiguous()), xs, rstd, dx, T, d, dres=dres, dx16=dx16)
+    else:
+        dw = _grad_slot(w) if w is not None else None
+        db = _grad_slot(b) if b is not None else None
+        K.ln_bwd(_flat2(dy.contiguous()), xs, mean, rstd, w, dx, dw, db, T, d, dres=dres, dx16=dx16)
+        _done(w, b)
+    dx = dx.view(*dy.shape[:-1], d)
+    if dx16 is None:
+        return dx.to(ctx.in_dtype), None, None, None
+    _set_bf16_twin(dx, dx16)
+    return dx, None, None, None
+
+
 class LayerNormForkFn(Function):
     """``(LN(x), x)``: the second output carries the residual stream past the norm, so the backward gets
     both gradients and sums them inside the LN-backward kernel (no separate autograd add over [T, d])."""
@@ -454,7 +483,7 @@ class LayerNormForkFn(Function):
         mean = torch.empty(T, dtype=F32, device=x.device)
         rstd = torch.empty(T, dtype=F32, device=x.device)
         K.ln_fwd(x2, w, b, y, mean, rstd, T, d, eps)
-        ctx.save_for_backward(x2, mean, rstd)
+        ctx.save_for_backward(y if _xhat16(w, b, d) else x2, mean, rstd)
         ctx.params = (w, b)
         ctx.in_dtype = x.dtype
         return y.view(*shape[:-1], d), x.view_as(x)
@@ -463,23 +492,7 @@ class LayerNormForkFn(Function):
     def backward(ctx, dy, dpass):
         if dy is None:
             return dpass, None, None, None
-        x2, mean, rstd = ctx.saved_tensors
-        w, b = ctx.params
-        T, d = x2.shape
-        dres = None
-        if dpass is not None:
-            dres = _flat2(dpass.float().contiguous())
-        dx = torch.empty(T, d, dtype=F32, device=x2.device)
-        dx16 = torch.empty(T, d, dtype=BF16, device=x2.device) if ctx.in_dtype == F32 else None
-        dw = _grad_slot(w) if w is not None else None
-        db = _grad_slot(b) if b is not None else None
-        K.ln_bwd(_flat2(dy.contiguous()), x2, mean, rstd, w, dx, dw, db, T, d, dres=dres, dx16=dx16)
-        _done(w, b)
-        dx = dx.view(*dy.shape[:-1], d)
-        if dx16 is None:
-            return dx.to(ctx.in_dtype), None, None, None
-        _set_bf16_twin(dx, dx16)
-        return dx, None, None, None
+        return _ln_fork_bwd(ctx, dy, dpass)
 
 
 def _packed3(a: Optional[torch.Tensor], b: Optional[torch.Tensor], c: Optional[torch.Tensor], n: int) -> bool:
@@ -1123,7 +1136,7 @@ class LayerNormForkPairFn(LayerNormForkFn):
         mean = torch.empty(T2, dtype=F32, device=x.device)
         rstd = torch.empty(T2, dtype=F32, device=x.device)
         K.ln_fwd(x2, w, b, y, mean, rstd, T2, d, eps)
-        ctx.save_for_backward(x2[:T], mean[:T], rstd[:T])
+        ctx.save_for_backward(y[:T] if _xhat16(w, b, d) else x2[:T], mean[:T], rstd[:T])
         ctx.params = (w, b)
         ctx.in_dtype = x.dtype
         yf = y.view(*x_full.shape[:-1], d)

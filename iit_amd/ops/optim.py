@@ -14,7 +14,6 @@ Elsewhere a vectorised torch implementation of the same math is used.
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional
 
 import torch
@@ -53,14 +52,6 @@ class FusedAdam(torch.optim.Optimizer):
         self._hyper_host = None
         if use_hip is None:
             use_hip = flat.data.is_cuda
-        # overlapped update (enable_overlap): a phase followed by another one in the same train step launches only the
-        # norm stage; the Adam chunks run on a side stream under the next forward, each layer waiting for its chunk
-        self.defer_next = False
-        self._pending = None   # argument record of a deferred update not launched yet
-        self._inflight = None  # per-chunk events of a launched, not yet joined, deferred update
-        self._bounds = None
-        self._side = None
-        self._events = []
         self._hip = None
         if use_hip:
             from . import hip_kernels
@@ -88,97 +79,7 @@ class FusedAdam(torch.optim.Optimizer):
         return int(self._skipped_dev.item())
 
     def zero_grad(self, set_to_none: bool = False):  # noqa: D401 - arena memset
-        self.join_pending()
         self.flat.zero_grad()
-
-    # ---------------------------------------------------------------- overlapped update
-    def enable_overlap(self, stages) -> bool:
-        """Let a deferred update (``defer_next``) overlap the next forward.  ``stages``: the model's parameters in
-        forward order, one list per stage (embeddings, each block, final norm + unembed); their arena ranges must
-        not interleave.  The model calls :meth:`wait_stage` (k) before stage k reads its weights."""
-        if self._hip is None or os.environ.get("IIT_ADAM_OVERLAP", "0") == "0":
-            return False
-        flat, bounds, hi = self.flat, [], 0
-        for ps in stages:
-            ps = [p for p in ps if flat.owns(p)]
-            if ps:
-                lo = min(flat.offset_of(p) for p in ps)
-                if lo < hi:
-                    return False  # interleaved slots: one stage's chunk would hold another's later weights
-                hi = max(flat.offset_of(p) + 1 + sum((n - 1) * st for n, st in zip(p.shape, p.stride()))
-                         for p in ps)
-            bounds.append(hi)
-        self._bounds = bounds
-        self._side = torch.cuda.Stream(device=flat.data.device)
-        return True
-
-    def _launch_pending(self, overlap: bool) -> None:
-        from . import hip_kernels
-        rec, self._pending = self._pending, None
-        cur = torch.cuda.current_stream()
-        stream = self._side if overlap else cur
-        if overlap:
-            stream.wait_stream(cur)
-        lr, b1, b2, eps, wd = self._hyper_host
-        chunks = rec["chunks"]
-        # one event per chunk, created once and re-recorded (no event is destroyed while a phase is being captured)
-        while len(self._events) < len(chunks):
-            self._events.append(torch.cuda.Event())
-        book = next((k for k, (lo, hi) in enumerate(chunks) if hi > lo), 0)  # (an empty chunk launches nothing)
-        with torch.cuda.stream(stream):
-            for k, (lo, hi) in enumerate(chunks):
-                hip_kernels.adam_chunk(self.flat, self.exp_avg, self.exp_avg_sq, self._step_dev, rec, lo, hi, lr=lr,
-                                       b1=b1, b2=b2, eps=eps, wd=wd, hyper=self._hyper_dev, book=k == book)
-                if overlap:
-                    self._events[k].record(stream)
-        if overlap and not torch.cuda.is_current_stream_capturing():
-            # the side-stream chunks read the record's span table and norm partials after the host drops it: keep
-            # the caching allocator from handing those blocks to the current stream meanwhile (ADVICE r3)
-            for t in (rec.get("spans"), rec.get("part")):
-                if isinstance(t, torch.Tensor):
-                    t.record_stream(stream)
-        self._inflight = self._events[:len(chunks)] if overlap else None
-
-    @property
-    def split_mode(self) -> bool:
-        """``IIT_ADAM_OVERLAP=2``: a graph-replayed phase with a pending update is captured as one graph per forward
-        stage and the Adam chunks are launched eagerly on the side stream at replay, each stage's graph waiting for
-        its chunk's event between replays (cross-stream waits outside any graph; see GraphedTrainStep)."""
-        return self._bounds is not None and os.environ.get("IIT_ADAM_OVERLAP", "0") == "2"
-
-    def wait_stage(self, k: int) -> None:
-        """Forward gate: stage ``k``'s weights are about to be read (launches a deferred update on first call)."""
-        splitter = self.__dict__.get("_splitter")
-        if splitter is not None:  # split capture: the graph runner cuts a segment here (nothing launched / waited)
-            splitter(k)
-            return
-        if self._pending is not None:
-            self._launch_pending(overlap=True)
-        ev = self._inflight
-        if ev:
-            torch.cuda.current_stream().wait_event(ev[min(k, len(ev) - 1)])
-            if k >= len(ev) - 1:
-                self._inflight = None
-
-    def capture_guard(self):
-        """(state, restore) around a graph capture of a phase that may launch a pending update: if the capture
-        fails, ``restore()`` puts the pending record back, forgets events recorded inside the aborted capture and
-        drains the side stream, so the eager fallback still applies the update."""
-        saved = (self._pending, self._inflight)
-
-        def restore():
-            self._pending, self._inflight = saved[0], None
-            if self._side is not None:
-                self._side.synchronize()
-        return restore
-
-    def join_pending(self) -> None:
-        """Complete any deferred update before gradients or weights are touched outside a gated forward."""
-        if self._pending is not None:
-            self._launch_pending(overlap=False)
-        if self._inflight:
-            torch.cuda.current_stream().wait_event(self._inflight[-1])
-            self._inflight = None
 
     @torch.no_grad()
     def step(self, closure=None, clip_norm: Optional[float] = None):
@@ -191,10 +92,6 @@ class FusedAdam(torch.optim.Optimizer):
         g = self.flat.grad
         if self._hip is not None:
             from . import hip_kernels
-            # (only with the bf16 mirror: the chunks write it; a refresh pass right here would read stale weights)
-            defer = self.defer_next and self._bounds is not None and self.flat.shadow is not None
-            self.defer_next = False
-            self.join_pending()
             self.step_count += 1
             self._validate_restriction(wd)
             self.sync_hyper()
@@ -202,14 +99,6 @@ class FusedAdam(torch.optim.Optimizer):
             if capturing and self._hyper_host != self._hyper():
                 raise RuntimeError("FusedAdam: hyper-parameters changed since the last eager step; run one eager "
                                    "step (or sync_hyper()) before capturing")
-            if defer:
-                rec = hip_kernels.adam_norm_stage(self.flat, self._step_dev, clip_norm=clip_norm,
-                                                  skipped=self._skipped_dev if self.nan_guard else None)
-                idx = [0] + [self.flat.span_index(b) for b in self._bounds[:-1]] + [rec["nspans"]]
-                rec["chunks"] = [(a, max(a, b)) for a, b in zip(idx[:-1], idx[1:])]
-                self.flat.after_step(mirror_written=self.flat.shadow is not None)
-                self._pending = rec
-                return
             hip_kernels.adam_step(self.flat, self.exp_avg, self.exp_avg_sq, self._step_dev, lr=lr, b1=b1, b2=b2,
                                   eps=eps, wd=wd, clip_norm=clip_norm,
                                   skipped=self._skipped_dev if self.nan_guard else None, hyper=self._hyper_dev)
@@ -250,7 +139,6 @@ class FusedAdam(torch.optim.Optimizer):
 
     # ---------------------------------------------------------------- checkpointing
     def state_dict(self):
-        self.join_pending()
         self.step_count = int(self._step_dev.item())  # device counter is authoritative (guarded skips)
         return {"step": self.step_count, "skipped": self.skipped_steps, "exp_avg": self.exp_avg,
                 "exp_avg_sq": self.exp_avg_sq,

@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None, help="pairs per GPU per step")
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="pvr-resnet18 only: fp32 (the reference precision) or channels-last bf16 autocast")
     ap.add_argument("--graphs", type=int, default=None,
                     help="HIP-graph phases (default: on for BERT; off for Llama, whose strict phase has one graph per "
                          "non-circuit node -- ~1000 at 32 layers x 32 heads -- and whose GEMMs are not launch-bound)")
@@ -67,6 +69,8 @@ def setup(args, dev):
         n = 20000
         tr_set, te_set = get_dataset("mnist_pvr", {"train_size": n, "test_size": 2048, "device": dev})
         ll, hl, corr = get_alignment("mnist_pvr", {"input_shape": te_set.base_data.get_input_shape(), "device": dev})
+        if args.dtype == "bf16":  # NHWC activations for MIOpen's bf16 implicit-GEMM convolutions
+            ll.to(memory_format=torch.channels_last)
         args.batch = args.batch or 256
         pair = IITBehaviorModelPair(hl, ll, corr, training_args={"batch_size": args.batch, "lr": 1e-3,
                                                                   "lr_scheduler": None, "early_stop": False,
@@ -128,6 +132,26 @@ def main():
     t_setup = time.perf_counter()
     pair, opt, it, step_fn, test_set, model_name, seq = setup(args, dev)
     t_setup = time.perf_counter() - t_setup
+    if args.dtype == "bf16" and args.family.startswith("pvr"):
+        import contextlib
+        inner = step_fn
+        # no autocast weight-cast cache: the casts must be re-done inside every captured / replayed graph
+        amp = (lambda: torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False)) if dev.type == "cuda" \
+            else contextlib.nullcontext
+
+        class _Amp:
+            enabled = getattr(inner, "enabled", False)
+
+            def prime(self, *a):
+                if hasattr(inner, "prime"):
+                    with amp():
+                        inner.prime(*a)
+
+            def __call__(self, *a):
+                with amp():
+                    return inner(*a)
+
+        step_fn = _Amp()
     for i in range(args.warmup):
         base, abl = next(it)
         if i == 0 and hasattr(step_fn, "prime"):
@@ -161,7 +185,7 @@ def main():
             "metric": f"IIT (base,source) intervened pairs/sec, {args.family}", "value": round(
                 args.batch * world * args.steps / dt, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "dtype": "fp32" if args.family.startswith("pvr") else "bf16",
+            "scaling": "weak", "dtype": args.dtype if args.family.startswith("pvr") else "bf16",
             "data": "synthetic task data, random-init weights",
             "config": {"model": model_name, "params": n_params, "global_batch": args.batch * world, "seq_len": seq,
                        "parallelism": f"dp{world}", "graphs": bool(getattr(step_fn, "enabled", False))},

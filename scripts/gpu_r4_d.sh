@@ -29,3 +29,8 @@ IIT_EVAL_GRAPHS=0 step eval_ioi_eager 600 python3 -u eval_ioi.py --model gpt2-sm
 IIT_EVAL_GRAPHS=1 step eval_ioi_graphs 600 python3 -u eval_ioi.py --model gpt2-small -w 100_100_40 --root /tmp/r4models --backend hip --num-samples 4608 --timing-repeats 2; grep -E "eval_ioi_timing" $O/eval_ioi_graphs.log | cut -c1-400
 IIT_PROFILE=1 step tti_gpt2 500 python3 -u scripts/time_to_iia.py --model gpt2-small --dtype bf16 --epochs 80; grep -E "primed|^\{" $O/tti_gpt2.log | cut -c1-700
 step eval_pvr 900 python3 -u scripts/eval_pvr_r4.py; grep -E "^\[pvr\]" $O/eval_pvr.log
+step fam_pvr_fp32 400 python3 -u scripts/bench_families.py --family pvr-resnet18 --steps 20 --warmup 3; grep -E '^\{' $O/fam_pvr_fp32.log | cut -c1-200
+step fam_pvr_bf16 400 python3 -u scripts/bench_families.py --family pvr-resnet18 --dtype bf16 --steps 20 --warmup 3; grep -E '^\{' $O/fam_pvr_bf16.log | cut -c1-200
+step fam_pvr_bf16_prof 400 rocprofv3 --kernel-trace --output-format csv -d $O/pvrprof -o pvr -- python3 scripts/bench_families.py --family pvr-resnet18 --dtype bf16 --steps 10 --warmup 3
+f=$(find $O/pvrprof -name "*kernel_trace.csv" | head -n 1)
+[ -n "$f" ] && python3 scripts/step_breakdown.py "$f" --steps 6 --top 25 --gaps 3 > $O/pvr_bf16_breakdown.txt && head -30 $O/pvr_bf16_breakdown.txt; rm -f "$f"

@@ -133,6 +133,12 @@ def test_headline_step_matches_fp32_oracle():
     for (n, p_f), (_, p_r) in zip(pf.ll_model.named_parameters(), pr.ll_model.named_parameters()):
         df = p_f.detach().float() - w0[n]
         dr = p_r.detach().float() - w0[n]
+        if n.endswith("b_K"):
+            # zero gradient in exact arithmetic (softmax is shift-invariant along the key axis): the fp32 oracle's
+            # gradient is ~1e-12 noise, below Adam's eps, so its update is ~0, while bf16 noise (> eps) moves it by ~lr;
+            # only the size of the bf16 update is bounded
+            assert float(df.abs().max()) <= 1.5 * ARGS["lr"] * 12, n
+            continue
         if float(dr.norm()) == 0.0:
             assert float(df.norm()) == 0.0, n
             continue

@@ -127,6 +127,11 @@ def test_layernorm(K, d, affine, bf16_dy):
     assert torch.equal(dx16, dx.to(torch.bfloat16))
     if affine:
         assert rel_err(dw, wr.grad) < 1e-4 and rel_err(db, br.grad) < 1e-4
+    elif d % 4 == 0:  # LNPre backward from the bf16 output (xhat) instead of the fp32 input
+        dxh = torch.empty(T, d, device=dev)
+        K.ln_bwd_xh16(g, y, rstd, dxh, T, d, dres=dres, dx16=dx16)
+        assert rel_err(dxh, xr.grad + dres) < 1e-2
+        assert torch.equal(dx16, dxh.to(torch.bfloat16))
 
 
 def test_gelu_fwd_and_pos_bwd(K):

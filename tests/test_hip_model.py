@@ -208,7 +208,9 @@ def test_bert_paired_forward_equals_two_forwards(monkeypatch):
         out_p, caps = res
         cache = fast.run_capture(src, list(sites))
         for n in sites:
-            assert rel(caps[n], cache[n]) < 1e-6, (sites, n)
+            # the paired run's GEMMs are M = 2T problems (other tiles / splits than the T-row capture run): equal up
+            # to bf16 rounding of the last bit
+            assert rel(caps[n], cache[n]) < 5e-3, (sites, n)
         spl = [(n, ix, cache[n]) for n, ixs in sites.items() for ix in ixs]
         out_2 = fast(tok, plan=RunPlan.with_splices(spl))
         assert rel(out_p, out_2) < 1e-2, sites
