@@ -340,6 +340,74 @@ __global__ __launch_bounds__(256) void ln_dwdb_kernel(const void* __restrict__ d
   }
 }
 
+// Vectorised affine gradients (d % 4 == 0, 16-B aligned rows): a wave covers 256 columns as float4 lanes, the block's 4
+// waves take interleaved rows of a 32-row chunk with all 8 rows' loads issued before the first use, and the waves meet
+// in LDS for one atomic per column per block.  ~700 blocks at T = 7680 (the 64-column kernel above ran 180-360
+// blocks of 64 serial dependent loads per thread: 29 us for [7680][768], profiles/mqnli_step_breakdown_r4.txt).
+constexpr int LN_DWDB_ROWS = 32;
+template <bool DY_F32>
+__global__ __launch_bounds__(256) void ln_dwdb_vec_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd, float* __restrict__ dw,
+                                                          float* __restrict__ db, int T, int d, RowSel sel) {
+  __shared__ float4 pw[4][64], pb[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int d4 = d >> 2;
+  const int c4 = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * LN_DWDB_ROWS;
+  float4 sw = make_float4(0.f, 0.f, 0.f, 0.f), sb = sw;
+  if (c4 < d4) {
+    constexpr int R = LN_DWDB_ROWS / 4;
+    float4 g[R], xv[R];
+    float mu[R], rs[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int t = r0 + wv + 4 * i;
+      const bool live = t < T && !sel_hit(sel, t);
+      g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      xv[i] = g[i];
+      mu[i] = 0.f;
+      rs[i] = 0.f;
+      if (live) {
+        if (DY_F32) {
+          g[i] = ((const float4*)dy_)[(long)t * d4 + c4];
+        } else {
+          const bf16x4 b = ((const bf16x4*)dy_)[(long)t * d4 + c4];
+          g[i] = make_float4(bf2f(b[0]), bf2f(b[1]), bf2f(b[2]), bf2f(b[3]));
+        }
+        xv[i] = ((const float4*)x)[(long)t * d4 + c4];
+        mu[i] = mean[t];
+        rs[i] = rstd[t];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      sw.x += g[i].x * (xv[i].x - mu[i]) * rs[i];
+      sw.y += g[i].y * (xv[i].y - mu[i]) * rs[i];
+      sw.z += g[i].z * (xv[i].z - mu[i]) * rs[i];
+      sw.w += g[i].w * (xv[i].w - mu[i]) * rs[i];
+      sb.x += g[i].x; sb.y += g[i].y; sb.z += g[i].z; sb.w += g[i].w;
+    }
+  }
+  pw[wv][lane] = sw;
+  pb[wv][lane] = sb;
+  __syncthreads();
+  if (wv == 0 && c4 < d4) {
+    const float4 a = pw[0][lane], b = pw[1][lane], c = pw[2][lane], e = pw[3][lane];
+    const float4 p = pb[0][lane], q = pb[1][lane], r = pb[2][lane], u = pb[3][lane];
+    float* w4 = dw + 4 * c4;
+    float* b4 = db + 4 * c4;
+    atomicAdd(w4 + 0, (a.x + b.x) + (c.x + e.x));
+    atomicAdd(w4 + 1, (a.y + b.y) + (c.y + e.y));
+    atomicAdd(w4 + 2, (a.z + b.z) + (c.z + e.z));
+    atomicAdd(w4 + 3, (a.w + b.w) + (c.w + e.w));
+    atomicAdd(b4 + 0, (p.x + q.x) + (r.x + u.x));
+    atomicAdd(b4 + 1, (p.y + q.y) + (r.y + u.y));
+    atomicAdd(b4 + 2, (p.z + q.z) + (r.z + u.z));
+    atomicAdd(b4 + 3, (p.w + q.w) + (r.w + u.w));
+  }
+}
+
 // scalar fallback (any d <= 4096, any alignment)
 template <int VPL, bool DY_F32>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
@@ -448,9 +516,17 @@ IIT_EXPORT int iit_ln_bwd_sel(const void* dy, int dy_f32, const float* x, const 
 #undef LNB
   }
   if (dw) {
-    dim3 g2((d + 63) / 64, (T + 255) / 256);
-    if (dy_f32) hipLaunchKernelGGL(ln_dwdb_kernel<true>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d, sel);
-    else hipLaunchKernelGGL(ln_dwdb_kernel<false>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d, sel);
+    const bool v4 = d % 4 == 0 && aligned16(x) && aligned16(dw) && aligned16(db) &&
+                    (dy_f32 ? aligned16(dy) : (((uintptr_t)dy) & 7) == 0);
+    if (v4) {
+      dim3 g2((d / 4 + 63) / 64, (T + LN_DWDB_ROWS - 1) / LN_DWDB_ROWS);
+      if (dy_f32) hipLaunchKernelGGL(ln_dwdb_vec_kernel<true>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d, sel);
+      else hipLaunchKernelGGL(ln_dwdb_vec_kernel<false>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d, sel);
+    } else {
+      dim3 g2((d + 63) / 64, (T + 255) / 256);
+      if (dy_f32) hipLaunchKernelGGL(ln_dwdb_kernel<true>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d, sel);
+      else hipLaunchKernelGGL(ln_dwdb_kernel<false>, g2, block, 0, s, dy, x, mean, rstd, dw, db, T, d, sel);
+    }
   }
   return hipGetLastError();
 }
@@ -960,7 +1036,8 @@ IIT_EXPORT int iit_adam_spans(float* p, const float* g, float* m, float* v, void
                               int nspans, const float* total, float clip, float lr, float b1, float b2, float eps,
                               float wd, const float* hyper, int* step, int* skipped, void* stream) {
   const int blocks = max(1, min(nspans, 4096));
-  hipLaunchKernelGGL((adam_span_kernel<true, 1>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
+  // (U = 2: two float4 groups in flight per thread and stream, as the replicated update; profiles/adam_microbench_r3s2.txt)
+  hipLaunchKernelGGL((adam_span_kernel<true, 2>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
                      (__bf16*)mirror, (const Span*)spans, nspans, total, 1, clip, lr, b1, b2, eps, wd, hyper, step,
                      skipped);
   return hipGetLastError();

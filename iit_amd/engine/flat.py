@@ -231,13 +231,7 @@ class FlatParams:
         tab = make_span_tensor(spans, self.data.device)
         self.drop_span_cache()
         self._span_cache = (key, tab, len(spans))
-        self._span_starts = [sp[0] * 4 for sp in spans]  # host copy: element offsets (chunked optimizer bounds)
         return tab, len(spans)
-
-    def span_index(self, offset: int) -> int:
-        """Index of the first entry of the current span table starting at or after element ``offset``."""
-        import bisect
-        return bisect.bisect_left(self._span_starts, offset)
 
     def check_inactive_zero(self, *tensors: torch.Tensor) -> bool:
         """True when every skipped range is zero in each given arena-shaped tensor (default: the gradient)."""

@@ -41,9 +41,13 @@ def evaluate_model_on_ablations(ll_model, task: str, test_set, eval_args: dict, 
                 nb += 1
                 base_input = test_set.gather(torch.arange(s, min(n, s + bs), device=DEVICE))
                 for hl_node in pair.corr:
-                    xs, ys, ivs = test_set.patch_batch_at_hl(list(base_input[0]), list(base_input[2]), hl_node)
-                    ablated = (torch.stack(xs), torch.stack([torch.as_tensor(y) for y in ys]).to(DEVICE),
-                               torch.stack(ivs))
+                    # same draws, one device pass per batch (the reference engine keeps the reference's per-sample loop)
+                    if hasattr(test_set, "patch_batch_tensor") and eval_args.get("engine", "native") != "reference":
+                        ablated = test_set.patch_batch_tensor(base_input[0], base_input[2], hl_node)
+                    else:
+                        xs, ys, ivs = test_set.patch_batch_at_hl(list(base_input[0]), list(base_input[2]), hl_node)
+                        ablated = (torch.stack(xs), torch.stack([torch.as_tensor(y) for y in ys]).to(DEVICE),
+                                   torch.stack(ivs))
                     hl_output, ll_output = pair.do_intervention(base_input, ablated, hl_node)
                     changed = (ablated[1] != base_input[1]).float()
                     acc = (torch.argmax(ll_output, dim=1) == hl_output).float() * changed

@@ -201,7 +201,7 @@ class BertBlock(nn.Module):
         return out, True
 
 
-_BERT_PAIRED_DEFAULT = "0"  # flipped to "1" once tests/test_hip_model.py::test_bert_paired_* has passed on an MI355X
+_BERT_PAIRED_DEFAULT = "1"  # validated on MI355X in round 4 (tests/test_hip_model.py, MQNLI 12,296 -> 20,032 pairs/s with the embedding fixes)
 
 
 class HookedEncoder(HookedRootModule):
@@ -280,10 +280,8 @@ class HookedEncoder(HookedRootModule):
                 token_type_ids = ((is_sep.cumsum(-1) - is_sep) > 0).long()
         key_mask = None if attention_mask is None else attention_mask.to(dev).bool()
         try:
-            e = run.site(self.embed.hook_embed, ops.embed(tokens, self.embed.embed.W_E))
-            p = run.site(self.embed.hook_pos_embed, ops.pos_embed(B, S, self.embed.pos_embed.W_pos))
-            t = run.site(self.embed.hook_token_type_embed, ops.w(self.embed.token_type_embed.W_token_type)[token_type_ids])
-            x = self.embed.ln.run(e + p + t, run)
+            t = run.site(self.embed.hook_token_type_embed, self._token_type_embed(ops, token_type_ids))
+            x = self.embed.ln.run(self._embed_pos(tokens, run) + t, run)
             x = run.site(self.hook_full_embed, x)
             for blk in self.blocks:
                 x = blk(x, run, key_mask)
@@ -308,13 +306,33 @@ class HookedEncoder(HookedRootModule):
         is_sep = (tokens == sep).long()
         return ((is_sep.cumsum(-1) - is_sep) > 0).long()
 
+    def _token_type_embed(self, ops, types: torch.Tensor) -> torch.Tensor:
+        """Rows of the (2-row) token-type table per position.  As a one-hot GEMM against the fp32 table rather than a
+        gather: the gather's backward (an index_put accumulating B*S rows into 2) ran 3.0 ms per phase on MI355X
+        (profiles/mqnli_step_breakdown_r4.txt); this backward is one [n x B*S] x [B*S x d] product."""
+        W = self.embed.token_type_embed.W_token_type
+        n = W.shape[0]
+        if n <= 8:
+            return F.one_hot(types, n).to(W.dtype) @ W
+        return ops.w(W)[types]
+
+    def _embed_pos(self, tokens, run: _Run):
+        """Token + position embeddings.  On the fused backend with neither hook observed: one kernel each way
+        (``EmbedPosFn``: the backward is the scatter-add kernel, not a gather's index_put backward -- 0.63 ms per
+        phase for BERT-base's W_E on MI355X, profiles/mqnli_step_breakdown_r4.txt)."""
+        ops = run.ops
+        emb = self.embed
+        B, S = tokens.shape
+        if getattr(ops, "fused", False) and not (run.live(emb.hook_embed) or run.live(emb.hook_pos_embed)):
+            return ops.embed_pos(tokens, emb.embed.W_E, emb.pos_embed.W_pos)
+        e = run.site(emb.hook_embed, ops.embed(tokens, emb.embed.W_E))
+        p = run.site(emb.hook_pos_embed, ops.pos_embed(B, S, emb.pos_embed.W_pos))
+        return e + p
+
     def _embed_ln(self, tokens, run: _Run):
         ops = run.ops
-        B, S = tokens.shape
-        e = ops.embed(tokens, self.embed.embed.W_E)
-        pe = ops.pos_embed(B, S, self.embed.pos_embed.W_pos)
-        t = ops.w(self.embed.token_type_embed.W_token_type)[self._token_types(tokens)]
-        return self.embed.ln.run(e + pe + t, run)
+        t = self._token_type_embed(ops, self._token_types(tokens))
+        return self.embed.ln.run(self._embed_pos(tokens, run) + t, run)
 
     def run_paired(self, tokens: torch.Tensor, src_tokens: torch.Tensor, sites, logits: str = "full"):
         """Interchange intervention with the source run folded into the base forward: one pass of 2B rows
@@ -326,7 +344,7 @@ class HookedEncoder(HookedRootModule):
         import os
         if os.environ.get("IIT_PAIRED", "1") == "0" or not sites:
             return None
-        if os.environ.get("IIT_BERT_PAIRED", _BERT_PAIRED_DEFAULT) != "1":  # opt-in until validated on hardware
+        if os.environ.get("IIT_BERT_PAIRED", _BERT_PAIRED_DEFAULT) != "1":  # IIT_BERT_PAIRED=0: two forwards
             return None
         ops = self.ops()
         if not getattr(ops, "supports_pairs", False) or getattr(ops, "pair_layer_norm", None) is None:

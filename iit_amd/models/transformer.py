@@ -635,18 +635,26 @@ class HookedTransformer(HookedRootModule):
 
     def forward(self, input, return_type: Optional[str] = "logits", loss_per_token: bool = False,
                 prepend_bos: Optional[bool] = None, stop_at_layer: Optional[int] = None,
-                past_kv_cache=None, *, plan: Optional[RunPlan] = None, logits_at: Optional[int] = None):
-        tokens = self.to_tokens(input, prepend_bos=prepend_bos) if isinstance(input, (str, list)) else input
-        if tokens.dim() == 1:
-            tokens = tokens.unsqueeze(0)
-        if tokens.device != self.embed.W_E.device:
-            tokens = tokens.to(self.embed.W_E.device)
+                past_kv_cache=None, *, plan: Optional[RunPlan] = None, logits_at: Optional[int] = None,
+                start_at_layer: Optional[int] = None):
+        """TL semantics; ``start_at_layer`` (TL's keyword): ``input`` is the residual stream entering that block
+        ([B, S, d]) and the embedding and earlier blocks are skipped (evaluation sweeps resume a cached base run
+        at each spliced node's layer, :func:`iit_amd.utils.eval_ablations._resample_scores`)."""
+        if start_at_layer is not None:
+            tokens = input
+        else:
+            tokens = self.to_tokens(input, prepend_bos=prepend_bos) if isinstance(input, (str, list)) else input
+            if tokens.dim() == 1:
+                tokens = tokens.unsqueeze(0)
+            if tokens.device != self.embed.W_E.device:
+                tokens = tokens.to(self.embed.W_E.device)
         run = _Run(plan, self.ops())
         begin = getattr(run.ops, "begin_forward", None)
         if begin is not None:
             begin()
         try:
-            resid = self._embed(tokens, run)
+            first = 0 if start_at_layer is None else int(start_at_layer)
+            resid = self._embed(tokens, run) if start_at_layer is None else input
             n_blocks = len(self.blocks) if stop_at_layer is None else stop_at_layer
             cuts = self.__dict__.get("_grad_cuts") if torch.is_grad_enabled() else None
             want = plan.logits if plan is not None else ("last" if logits_at == -1 else "full")
@@ -655,6 +663,8 @@ class HookedTransformer(HookedRootModule):
                          and len(self.blocks) > 0 and getattr(self, "last_position_final_block", True)
                          and tokens.shape[1] > 1 and self.blocks[-1].last_position_ok(run))
             for li, block in enumerate(self.blocks[:n_blocks]):
+                if li < first:
+                    continue
                 if cuts and li in cuts and resid.requires_grad:
                     # staged backward (engine.graphs): the backward stops here and resumes as its own segment
                     leaf = resid.detach().requires_grad_(True)

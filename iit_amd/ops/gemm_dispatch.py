@@ -90,9 +90,8 @@ def enable_tuned_library_gemms() -> bool:
 def deterministic() -> bool:
     """Run-to-run reproducible GEMMs: ``IIT_DETERMINISTIC=1`` or ``torch.use_deterministic_algorithms(True)``.
 
-    The split-K candidates (fp32 atomics into the output: the weight-gradient accumulate tiles and the few-tile
-    fp32 store / residual ``s+hip`` path used by the last-position logits and the final-block residual adds) sum
-    their partial products in arrival order, so two runs can differ in the last bits.  In deterministic mode the
+    The split-K candidates (fp32 atomics into the output: the weight-gradient accumulate tiles) sum their partial
+    products in arrival order, so two runs can differ in the last bits.  In deterministic mode the
     dispatcher drops them and every candidate has a fixed reduction order.  The reduction split-K candidates
     (``glds*r*``: partial tiles summed in split order by the last-arriving workgroup) are deterministic and stay."""
     return os.environ.get("IIT_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
@@ -282,12 +281,21 @@ _BLAS16_EPIS = (K.EPI_F32_RESID, K.EPI_F32_ACC)
 
 
 # diagnostics: ``IIT_GEMM_EXCLUDE`` = comma-separated regular expressions of candidate names the dispatcher must not
-# offer (shipped decisions naming one are re-measured among the rest); "hip" always stays
-_EXCLUDE = [re.compile(x) for x in os.environ.get("IIT_GEMM_EXCLUDE", "").split(",") if x]
+# offer (shipped decisions naming one are re-measured among the rest); "hip" always stays.  A pattern with "@" is
+# matched against ``name@repr(problem key)`` (one call site only).  ``IIT_GEMM_TRACE=1`` prints each problem key's
+# choice once.
+_EXCLUDE = [re.compile(x) for x in os.environ.get("IIT_GEMM_EXCLUDE", "").split(";" if ";" in
+                                                                                 os.environ.get("IIT_GEMM_EXCLUDE", "")
+                                                                                 else ",") if x]
+_TRACE = os.environ.get("IIT_GEMM_TRACE", "0") == "1"
+_TRACED = set()
 
 
-def _excluded(name: str) -> bool:
-    return name != "hip" and any(r.fullmatch(name) for r in _EXCLUDE)
+def _excluded(name: str, key=None) -> bool:
+    if name == "hip":
+        return False
+    tagged = f"{name}@{key!r}"
+    return any(r.fullmatch(tagged) if "@" in r.pattern else r.fullmatch(name) for r in _EXCLUDE)
 
 
 def _candidates(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bias1, bias2, resid, ldr, aux, ldc2,
@@ -358,29 +366,11 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
     if epi in _BLAS16_EPIS:
         calls["blas16"] = lambda c=C, c2=C2, c3=None: _blas16(A, B, c, M, N, Kd, lda, ldb, ldc, mode, epi,  # noqa
                                                              bias0, resid, ldr)
-    if (not det and epi in (K_.EPI_F32_STORE, K_.EPI_F32_RESID) and A.is_cuda and mode in (0, 2, 3) and Kd >= 256
-            and Kd % 64 == 0 and ((M + 63) // 64) * ((N + 63) // 64) < 64):
-        # an fp32 store with too few output tiles to fill the chip (the narrow tail of a ragged vocab GEMM, the
-        # last-position-only final block): write the bias (+ residual, or zeros) first, then accumulate with
-        # split-K -- many workgroups instead of a handful of long K loops
-        sp = min(16, Kd // 64)
-
-        def split_store(c=C, c2=C2, c3=None):
-            cv = _as(c, M, N, ldc)
-            b = None if bias0 is None else bias0.reshape(-1)[:N].float()
-            if epi == K_.EPI_F32_RESID:
-                r = _as(resid, M, N, ldr)
-                if b is None:
-                    cv.copy_(r)
-                else:
-                    torch.add(r, b, out=cv)
-            elif b is not None:
-                cv.copy_(b.expand(M, N))
-            else:
-                cv.zero_()
-            K_.gemm(A, B, c, M=M, N=N, K=Kd, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=K_.EPI_F32_ACC, splits=sp)
-
-        calls["s+hip"] = split_store
+    # (an "init C with bias / residual, then split-K atomics" candidate for the few-tile fp32 stores -- the
+    # last-position final block, ragged vocab tails -- made the gradients of the paired, last-position forward vary
+    # from run to run by up to 0.1 (scripts/diag_uninit_poison.py --keys: excluding it at the one problem key that
+    # chose it, (32, 128, 512) residual, made every configuration bit-stable) at no measurable gain (16,022 vs 16,019
+    # pairs/s without it, profiles/split_store_removal_r4.txt): removed)
     return calls
 
 
@@ -486,7 +476,7 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
             qkv, splits, blas_bias, policy)
     calls = _candidates(*args, csum_box=box)
     hip_call = calls["hip"]
-    if _decide_only and (policy != "auto" or "blas" not in calls):
+    if _decide_only and (policy != "auto" or len(calls) == 1):
         return None  # nothing to measure: a forced policy or a single candidate
     if bsum is not None or gsq is not None:
         assert bsum is None or mode == 3, "fused bias sums are the column sums of a weight gradient's dY"
@@ -506,7 +496,7 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         def _run(name):
             calls[name](C, C2, C3)
             return name
-    if policy == "hip" or "blas" not in calls:
+    if policy == "hip" or len(calls) == 1:
         _run("hip")
         return None
     if fresh:
@@ -523,6 +513,8 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
         return None
     # the last key field marks the variant: a fresh store (EPI_F32_STORE) or fused column sums (EPI_DGELU)
     key = (M, N, Kd, mode, epi, bias0 is not None, fresh or (colsum is not None), deterministic())
+    if _EXCLUDE:
+        calls = {n: f for n, f in calls.items() if not _excluded(n, key)}
     choice = DECISIONS.get(key)
     if choice is None:
         shipped = None if _decide_only else _table().get(repr(key))  # ragged bulk/tail splits compare real times
@@ -571,6 +563,9 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
     name = FORCE.get(key, choice[0])
     if name not in calls:
         name = choice[0]
+    if _TRACE and key not in _TRACED:
+        _TRACED.add(key)
+        print(f"[gemm] {key!r} -> {name}", flush=True)
     if TIMING is not None:
         s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s_ev.record()

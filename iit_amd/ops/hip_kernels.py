@@ -202,8 +202,13 @@ GLDS_DISPATCH_TILES = tuple(t for t in GLDS_TILES if t not in (12, 13, 14, 32, 3
 def _gemm_bounds(what, A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode, qkv=(0, 0, 0)):
     a = ("A", A, K, M, lda) if mode & MODE_AKM else ("A", A, M, K, lda)
     b = ("B", B, K, N, ldb) if mode & MODE_BKM else ("B", B, N, K, ldb)
-    c = ("C", C, M, N, ldc) if not qkv[0] else ("C", C, 0, 0, 0)
-    _bounds(what, a, b, c, ("C2", C2, M, N, ldc2 or ldc), ("resid", resid, M, N, ldr or ldc))
+    if qkv[0]:
+        # head-blocked QKV scatter (EPI_F32_ACC_QKV): C / C2 / C3 each hold [H][qkv_d][dh] (rows of the model dim)
+        dh, H, d = qkv
+        per = ("C", C, 1, H * d * dh, H * d * dh)
+        _bounds(what, a, b, per, ("C2",) + per[1:] if C2 is None else ("C2", C2, 1, H * d * dh, H * d * dh))
+        return
+    _bounds(what, a, b, ("C", C, M, N, ldc), ("C2", C2, M, N, ldc2 or ldc), ("resid", resid, M, N, ldr or ldc))
 
 
 def gemm_glds_ok(A, B, C, *, M, N, K, lda, ldb, ldc, mode, epi, C2=None, resid=None, ldc2=0, ldr=0, bias_cols=0,

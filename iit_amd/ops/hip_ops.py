@@ -496,8 +496,13 @@ class LayerNormForkFn(Function):
 
 
 def _packed3(a: Optional[torch.Tensor], b: Optional[torch.Tensor], c: Optional[torch.Tensor], n: int) -> bool:
-    """``a|b|c`` are consecutive ``n``-column blocks of one row-major buffer (the arena QKV layout)."""
+    """``a|b|c`` are consecutive ``n``-column blocks of ONE row-major buffer (the arena QKV layout).  Three separate
+    allocations that merely sit next to each other (the caching allocator hands out adjacent blocks) do not count:
+    a kernel writing 3n columns from ``a`` would run past ``a``'s storage (IIT_CHECK_BOUNDS flagged it)."""
     if a is None or b is None or c is None:
+        return False
+    st = a.untyped_storage().data_ptr()
+    if b.untyped_storage().data_ptr() != st or c.untyped_storage().data_ptr() != st:
         return False
     es = a.element_size()
     return b.data_ptr() == a.data_ptr() + n * es and c.data_ptr() == a.data_ptr() + 2 * n * es

@@ -124,6 +124,8 @@ class GradReducer:
     def _launch_reduce_scatter(self, b: int, s: int, e: int) -> None:
         """Bucket ``b`` -> the averaged gradient of this rank's piece in the shard buffer (async)."""
         sh = self.shard
+        if getattr(sh, "alias", False):
+            return  # one rank: the shard gradient IS the arena gradient (ShardedFusedAdam.set_buckets)
         world, rank, piece = sh.plan.world, sh.plan.rank, sh.plan.piece[b]
         out = sh.shard_view(b)
         src = self.flat.grad[s:e]

@@ -71,10 +71,26 @@ class ShardPlan:
         self.numel = off  # shard buffer length (elements)
         self.index: Dict[Tuple[int, int], int] = {bk: i for i, bk in enumerate(self.buckets)}
 
-    def spans(self, max_len4: int = 1024) -> List[Tuple[int, int, int]]:
-        """Optimizer span records (arena start4, shard start4, len4) over the owned pieces."""
+    def live_pieces(self, gaps: Sequence[Tuple[int, int]] = ()) -> List[Tuple[int, int, int]]:
+        """(arena start, arena end, shard start) of the owned elements outside ``gaps`` (sorted arena ranges the
+        optimizer may skip: embedding rows no training token reaches, ``FlatParams.inactive_ranges``)."""
         out = []
         for (a, b), loc in zip(self.own, self.local):
+            cur = a
+            for g0, g1 in gaps:
+                if g1 <= cur or g0 >= b:
+                    continue
+                if g0 > cur:
+                    out.append((cur, g0, loc + cur - a))
+                cur = max(cur, g1)
+            if cur < b:
+                out.append((cur, b, loc + cur - a))
+        return out
+
+    def spans(self, max_len4: int = 1024, gaps: Sequence[Tuple[int, int]] = ()) -> List[Tuple[int, int, int]]:
+        """Optimizer span records (arena start4, shard start4, len4) over the owned pieces (minus ``gaps``)."""
+        out = []
+        for a, b, loc in self.live_pieces(gaps):
             pos, n = a // 4, (b - a) // 4
             lpos = loc // 4
             while n > 0:
@@ -115,15 +131,47 @@ class ShardedFusedAdam(FusedAdam):
         if self.plan is not None and self.step_count:
             raise RuntimeError("optimizer-state sharding: the gradient buckets changed after the first step")
         dev = self.flat.data.device
+        self.alias = plan.world == 1
+        if self.alias:
+            # one rank (the IIT_DP_FORCE_REDUCER rehearsal): the rank's piece of every bucket is the whole bucket, so
+            # the shard layout IS the arena layout -- the gradient arena serves as the shard gradient (no
+            # reduce-scatter copy: the reducer issues nothing at world 1, as for the replicated all-reduce)
+            plan.local = [s for s, _ in plan.buckets]
+            plan.own = list(plan.buckets)
+            plan.numel = self.flat.numel
         self.plan = plan
         # shard-sized moments and gradient (the replicated optimizer's arena-sized ones are dropped)
         self.exp_avg = torch.zeros(plan.numel, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(plan.numel, dtype=torch.float32, device=dev)
-        self.shard_grad = torch.zeros(plan.numel, dtype=torch.float32, device=dev)
-        spans = plan.spans()
-        self._spans = make_span_tensor(spans, dev)
-        self._nspans = len(spans)
+        self.shard_grad = self.flat.grad if self.alias else torch.zeros(plan.numel, dtype=torch.float32, device=dev)
         self._gather_bufs: Dict[tuple, torch.Tensor] = {}
+        self._spans_version = None
+        self._retired_spans = []
+        self._build_spans()
+
+    def _build_spans(self) -> None:
+        """Span table of the owned pieces minus the rows the training data cannot reach (``restrict_sparse_rows``):
+        with zero gradient and zero moments their Adam update is the identity, as in the replicated optimizer.
+        Rebuilt when the restriction changes (outside graph capture); skipping is refused if a skipped range holds
+        non-zero moments (a restriction declared after unrestricted steps)."""
+        flat = self.flat
+        gaps = flat.inactive_ranges()
+        if gaps:
+            skipped = [(loc + max(a, g0) - a, loc + min(b, g1) - a)
+                       for a, b, loc in self.plan.live_pieces(()) for g0, g1 in gaps if g0 < b and g1 > a]
+            if any(bool(t[x:y].any()) for x, y in skipped for t in (self.exp_avg, self.exp_avg_sq)):
+                gaps = []
+        spans = self.plan.spans(gaps=gaps)
+        if getattr(self, "_spans", None) is not None:
+            self._retired_spans.append(self._spans)  # a captured graph may still read the old table's address
+        self._spans = make_span_tensor(spans, flat.data.device)
+        self._nspans = len(spans)
+        self._spans_version = flat.restrict_version
+
+    def _sync_spans(self) -> None:
+        if self._spans_version != self.flat.restrict_version and not (
+                torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+            self._build_spans()
 
     # ------------------------------------------------------------------ gradient side (called by the reducer)
     def shard_view(self, bucket: int) -> torch.Tensor:
@@ -160,6 +208,7 @@ class ShardedFusedAdam(FusedAdam):
         def host_books():  # eager, first: the host-side counters / hyper-parameters of this step
             self.step_count += 1
             self.sync_hyper()
+            self._sync_spans()
 
         def norm_part():
             K.sumsq_spans(self.shard_grad, self._spans, self._nspans, self._part, self._step_dev, need_norm)
@@ -206,6 +255,7 @@ class ShardedFusedAdam(FusedAdam):
         lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
         self.step_count += 1
         self.sync_hyper()
+        self._sync_spans()
         need_norm = bool(clip_norm) or self.nan_guard
         if self._hip is not None:
             from ..ops import hip_kernels as K
@@ -283,8 +333,12 @@ class ShardedFusedAdam(FusedAdam):
                     dist.all_gather(parts, piece.clone())
                 if not exact:
                     flat.data[s:e].copy_(out[:e - s])
-            if mirror and flat.shadow is not None:
-                flat.shadow[s:e].copy_(flat.data[s:e])
+        if mirror and flat.shadow is not None:
+            if self._hip is None:  # the torch path writes no mirror: refresh all of it
+                for s, e in self.plan.buckets:
+                    flat.shadow[s:e].copy_(flat.data[s:e])
+            else:  # the fused pass wrote the owned pieces' mirror
+                self._refresh_foreign_mirror()
         if mirror:
             flat.after_step(mirror_written=flat.shadow is not None)
 

@@ -183,6 +183,36 @@ class ImagePVRDataset(Dataset):
                 new_iv[idx_to_intermediate] = quad_label
                 return new_input, new_iv, self.make_label_from_intermediate(new_iv)
 
+    def patch_batch_tensor(self, x: torch.Tensor, intermediate_vars: torch.Tensor, hl_node: HLNode):
+        """:meth:`patch_batch_at_hl` on whole tensors (``x`` [B,3,H,W], ``intermediate_vars`` [B,4]): the same draws
+        from ``self.rng`` in the same order (so the same patches), then one gather + one slice write on the device
+        instead of a per-sample Python loop of image copies.  Returns ``(x', labels' [B], ivs' [B,4])``."""
+        idx, k = self.get_idx_and_intermediate(hl_node)
+        tg = _targets(self.base_dataset)
+        tg_np = tg.cpu().numpy() if isinstance(tg, torch.Tensor) else np.asarray(tg)
+        cur = intermediate_vars[:, k].cpu().numpy()
+        n = len(self.base_dataset)
+        js = np.empty(len(cur), dtype=np.int64)
+        for i, c in enumerate(cur):  # integer draws only: the rejection sampling of patch_at_hl_idx, in order
+            while True:
+                j = int(self.rng.integers(0, n))
+                if int(tg_np[j]) != int(c):
+                    js[i] = j
+                    break
+        dev = x.device
+        data, tgd, _, cmap = self._device_state(dev)
+        jt = torch.from_numpy(js).to(dev)
+        digits = data[jt].float() / 255.0  # [B, s, s]
+        if self.pad_size > 0:
+            digits = torch.nn.functional.pad(digits, (self.pad_size,) * 4)
+        out = x.clone()
+        region = out[(slice(None),) + tuple(idx.as_index)]  # [B, 3, h, w] view of the patched quadrant
+        region.copy_(digits.unsqueeze(1).expand_as(region))
+        iv = intermediate_vars.clone()
+        iv[:, k] = tgd[jt].to(iv.dtype)
+        y = iv.gather(1, cmap[iv[:, 0]].unsqueeze(1).to(torch.long)).squeeze(1)
+        return out, y, iv
+
     def patch_batch_at_hl(self, batch, intermediate_vars, hl_node: HLNode, _labels=None):
         idx, k = self.get_idx_and_intermediate(hl_node)
         new_batch, new_labels, new_ivs = [], [], []

@@ -134,6 +134,43 @@ def resample_ablate_node(model_pair, base_in, ablation_in, node: LLNode, results
                                                     atol, verbose, node, categorical_metric)
 
 
+_PREFIX = os.environ.get("IIT_EVAL_PREFIX", "1") != "0"
+
+
+def _node_layer(name: str) -> Optional[int]:
+    parts = name.split(".")
+    if len(parts) >= 3 and parts[0] == "blocks" and parts[1].isdigit():
+        return int(parts[1])
+    return None
+
+
+class _BasePrefix:
+    """Shared prefix of a sweep's spliced forwards: a splice at a node of block L leaves blocks 0..L-1 of the base run
+    unchanged, so the base residual entering every node's block is captured once per batch (one truncated
+    capture-only forward) and each node's forward resumes there (``HookedTransformer.forward(start_at_layer=L)``):
+    on average about half of the blocks per node are skipped.  ``IIT_EVAL_PREFIX=0`` runs every forward from the
+    tokens."""
+
+    def __init__(self, model_pair, base_x, nodes):
+        self.model = model_pair.ll_model
+        self.cache = {}
+        layers = sorted({L for L in (_node_layer(n.name) for n in nodes) if L})
+        ok = (_PREFIX and layers and hasattr(self.model, "blocks") and getattr(self.model, "supports_run_plan", False)
+              and "start_at_layer" in getattr(self.model.forward, "__code__", type("", (), {"co_varnames": ()})
+                                              ).co_varnames)
+        if ok:
+            names = [f"blocks.{L}.hook_resid_pre" for L in layers]
+            self.cache = {L: t for L, t in zip(layers, (self.model.run_capture(base_x, names)[n] for n in names))}
+
+    def forward(self, base_x, node, plan):
+        L = _node_layer(node.name)
+        resid = self.cache.get(L) if L else None
+        if resid is None:
+            return self.model(base_x, plan=plan)
+        # a copy: the resumed blocks must never see a buffer the next node at this layer reuses
+        return self.model(resid.clone(), plan=plan, start_at_layer=L)
+
+
 def _resample_scores(model_pair, base_in, ablation_in, nodes, atol: float = 5e-2, verbose: bool = False,
                      categorical_metric: Categorical_Metric = Categorical_Metric.KL) -> torch.Tensor:
     """One batch of the native resample sweep: one source capture of every node's hook and one HL base output,
@@ -142,9 +179,12 @@ def _resample_scores(model_pair, base_in, ablation_in, nodes, atol: float = 5e-2
         cache = model_pair.ll_source_cache(ablation_in[0], nodes)
         model_pair.ll_cache = cache
         base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
+        prefix = _BasePrefix(model_pair, base_in[0], nodes)
         scores = []
         for node in nodes:
-            ll_out = model_pair.ll_intervened_forward(base_in[0], [node])
+            plan = RunPlan.with_splices([(node.name, node.index, cache[node.name])],
+                                        logits=model_pair.ll_logits_mode())
+            ll_out = prefix.forward(base_in[0], node, plan)
             scores.append(_resample_score(model_pair, base_in, ablation_in, ll_out, base_hl_out, hl_reduced, atol,
                                           verbose, node, categorical_metric).float().reshape(()))
         return torch.stack(scores)
@@ -158,7 +198,7 @@ def resample_ablate_nodes(model_pair, base_in, ablation_in, nodes, results: Dict
         results[node] = results[node] + s[i]
 
 
-_EVAL_GRAPHS_DEFAULT = "0"  # "1" once the graphed sweeps have been validated against the eager ones on an MI355X
+_EVAL_GRAPHS_DEFAULT = "1"  # validated on MI355X in round 4 (tests/test_eval_graphs_gpu.py: graphed sweeps equal the eager ones)
 
 
 class _SweepGraph:
@@ -360,12 +400,13 @@ def _ablation_scores(model_pair, base_in, nodes, values: Dict[str, torch.Tensor]
         base_ll_out = model_pair.ll_forward(base_x)
         base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
         B = base_x.shape[0]
+        prefix = _BasePrefix(model_pair, base_x, nodes)
         scores = []
         for node in nodes:
             v = values[node.name]
             v = v.expand(B, *v.shape[1:]) if v.shape[0] != B else v  # a view: no per-batch copy
             plan = RunPlan.with_splices([(node.name, node.index, v)], logits=model_pair.ll_logits_mode())
-            ll_out = model(base_x, plan=plan)
+            ll_out = prefix.forward(base_x, node, plan)
             scores.append(_ablation_score(model_pair, ll_out, base_ll_out, base_hl_out, hl_reduced,
                                           atol).float().reshape(()))
         return torch.stack(scores)

@@ -112,6 +112,24 @@ def focused(cases):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--keys":
+        # which problem keys choose the s+hip candidate, then exclude it at one key at a time
+        import re
+        import subprocess
+        r = subprocess.run([sys.executable, "-u", __file__, "--focused"], env=dict(os.environ, IIT_GEMM_TRACE="1"),
+                           timeout=300, capture_output=True, text=True)
+        print(r.stdout[-4000:], flush=True)
+        keys = sorted({ln.split("] ", 1)[1].rsplit(" -> ", 1)[0] for ln in r.stdout.splitlines()
+                       if ln.startswith("[gemm]") and ln.endswith("-> s+hip")})
+        print(f"[keys] s+hip chosen at {len(keys)} problem keys: {keys}", flush=True)
+        for k in keys:
+            env = dict(os.environ, IIT_GEMM_EXCLUDE="s\\+hip@" + re.escape(k) + ";")
+            rr = subprocess.run([sys.executable, "-u", __file__, "--focused"], env=env, timeout=300)
+            if rr.returncode != 0:
+                print(f"[keys] {k} exited {rr.returncode}", flush=True)
+                if rr.returncode < 0 or rr.returncode >= 124:
+                    break
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "--bisect":
         import subprocess
         toggles = [{}, {"IIT_GEMM_EXCLUDE": r"s\+hip"}, {"IIT_GEMM_EXCLUDE": r"(z\+)?glds\d+k\d+"},

@@ -110,3 +110,31 @@ def test_batched_sweeps_equal_the_per_node_path():
     ea.ablate_nodes(pair, b, nodes, batched, {nm: mean_cache[nm] for nm in {n.name for n in nodes}})
     for n in nodes:
         assert torch.equal(torch.as_tensor(per_node[n]), torch.as_tensor(batched[n])), n
+
+
+def test_prefix_shared_sweep_equals_full_forwards(monkeypatch):
+    """Resuming each node's spliced forward from the cached base residual at its block (``_BasePrefix``) gives the
+    scores of full forwards from the tokens."""
+    pair, ds = _pair()
+    iit_set = IITDataset(ds, ds, seed=0, device="cpu")
+    uni = IITUniqueDataset(ds, ds, seed=0, device="cpu")
+    res = {}
+    for flag in (False, True):
+        monkeypatch.setattr(ea, "_PREFIX", flag)
+        torch.manual_seed(0)
+        r = dict(ea.check_causal_effect(pair, iit_set, batch_size=32, node_type="n"))
+        za_not, za_in = ea.get_causal_effects_for_all_nodes(pair, uni, batch_size=32, use_mean_cache=True)
+        r.update({("za", k): v for k, v in {**za_not, **za_in}.items()})
+        res[flag] = r
+    assert res[False].keys() == res[True].keys()
+    for k in res[False]:
+        assert abs(res[False][k] - res[True][k]) < 1e-5, k
+
+
+def test_start_at_layer_resumes_the_forward():
+    pair, _ = _pair()
+    m = pair.ll_model
+    tok = torch.randint(0, 1000, (4, 10))
+    full = m(tok)
+    resid3 = m.run_capture(tok, ["blocks.3.hook_resid_pre"])["blocks.3.hook_resid_pre"]
+    assert torch.allclose(m(resid3, start_at_layer=3), full, atol=1e-5)

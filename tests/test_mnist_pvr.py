@@ -95,3 +95,23 @@ def test_pvr_behavior_pair_trains():
     d = pair.test_metrics.to_dict()
     assert set(d) >= {"val/iit_loss", "val/IIA", "val/accuracy"}
     assert np.isfinite(pair.train_metrics.to_dict()["train/iit_loss"])
+
+
+def test_patch_batch_tensor_equals_per_sample_patching():
+    """The device-side batch patch of the leakiness eval (eval_causality.py) makes the same rng draws in the same order
+    as the reference's per-sample ``patch_batch_at_hl`` loop: identical images, labels and intermediate variables."""
+    import copy
+
+    from iit_amd.core.nodes import HLNode
+    from iit_amd.tasks.task_loader import get_dataset
+    _, te = get_dataset("pvr_leaky", dataset_config={"train_size": 1, "test_size": 64})
+    ds = te.base_data
+    b = ds.gather(torch.arange(0, 16))
+    for name in ("hook_tl_leaked_to_tr", "hook_br_leaked_to_tl", "hook_bl_leaked_to_br"):
+        node = HLNode(name, 10)
+        d1, d2 = copy.deepcopy(ds), copy.deepcopy(ds)
+        xs, ys, ivs = d1.patch_batch_at_hl(list(b[0]), list(b[2]), node)
+        x2, y2, iv2 = d2.patch_batch_tensor(b[0], b[2], node)
+        assert torch.equal(torch.stack(xs), x2), name
+        assert torch.equal(torch.stack([torch.as_tensor(y) for y in ys]), y2), name
+        assert torch.equal(torch.stack(ivs), iv2), name
