@@ -440,9 +440,10 @@ def _bf16_of(t: torch.Tensor) -> torch.Tensor:
 
 
 def _xhat16(w, b, d: int) -> bool:
-    """The LN backward reads the forward's bf16 output as xhat (norms without weight and bias) -- opt-in
-    (``IIT_LN_XHAT16=1``) until it has run on hardware against the staged-backward test."""
-    return w is None and b is None and d % 4 == 0 and d <= 4096 and os.environ.get("IIT_LN_XHAT16", "0") == "1"
+    """The LN backward reads the forward's bf16 output as xhat (norms without weight and bias: 2 B per element instead
+    of the fp32 input).  Round 3 reverted it over a staged-backward mismatch that round 4 traced to the split-store GEMM
+    candidate (profiles/split_store_removal_r4.txt); ``IIT_LN_XHAT16=0`` reads the fp32 input."""
+    return w is None and b is None and d % 4 == 0 and d <= 4096 and os.environ.get("IIT_LN_XHAT16", "1") == "1"
 
 
 def _ln_fork_bwd(ctx, dy, dpass):
