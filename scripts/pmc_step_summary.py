@@ -1,5 +1,5 @@
 """Per-kernel hardware counters over whole training steps (rocprofv3 --pmc ... -- python bench.py --graphs 0): for
-every GEMM kernel (the repo's LDS-DMA kernel and hipBLASLt), dispatches, mean MFMA busy (SQ_VALU_MFMA_BUSY_CYCLES /
+every GEMM kernel (the repo's LDS-DMA, dual dX + dW and plain MFMA kernels, and hipBLASLt), dispatches, mean MFMA busy (SQ_VALU_MFMA_BUSY_CYCLES /
 (GRBM_GUI_ACTIVE * 4 SIMDs * 32 CUs), as scripts/pmc_summary.py), LDS bank-conflict rate and the time-weighted
 average over all GEMM dispatches (weights: GRBM_GUI_ACTIVE)."""
 import sys
@@ -12,6 +12,13 @@ def short(name):
     i = name.find("gemm_glds_kernel<")
     if i >= 0:
         return "glds" + name[i + len("gemm_glds_kernel"):name.find(">", i) + 1]
+    i = name.find("gemm_dual_kernel<")
+    if i >= 0:  # the dual dX + dW launches (csrc/gemm_dual.hip): both tiles' configurations
+        j = name.find("Cfg<", i)
+        return "dual" + name[j + 3:name.find(">", j) + 1] if j >= 0 else "dual"
+    i = name.find("gemm_kernel<")
+    if i >= 0 and "glds" not in name:
+        return "hipgemm" + name[i + len("gemm_kernel"):name.find(">", i) + 1]
     if name.startswith("Cijk") or name.startswith("Custom_Cijk"):
         j = name.find("_MT")
         return "hipBLASLt" + name[j:j + 16] if j >= 0 else name[:40]

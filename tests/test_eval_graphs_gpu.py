@@ -77,27 +77,3 @@ def test_prime_preserving_restores_the_training_state():
     assert torch.equal(opt._step_dev, snap["step"]) and opt.step_count == snap["count"]
     assert torch.equal(torch.get_rng_state(), snap["cpu"]) and torch.equal(torch.cuda.get_rng_state(), snap["cuda"])
     assert pair.rng.bit_generator.state == rng
-
-
-def test_primed_training_tracks_unprimed():
-    """Two epochs with and without priming: same trajectory.  (Not bit-exact: atomics in the bias / norm / embedding
-    gradient sums make two runs differ in the last bits, and Adam turns last-bit noise on near-zero gradients into
-    +-lr steps; the weight updates are compared in bulk.)"""
-    from iit_amd.data.iit_dataset import IITDataset, train_test_split
-    deltas = []
-    for prime in (False, True):
-        pair, ds = _pair(samples=1024)
-        pair.training_args["prime_graphs"] = prime
-        w0 = {n: p.detach().float().clone() for n, p in pair.ll_model.named_parameters()}
-        tr, te = train_test_split(ds, 0.2, 42)
-        torch.manual_seed(1)
-        pair.train(IITDataset(tr, tr, seed=0, device=dev), IITDataset(te, te, seed=0, device=dev), epochs=2)
-        deltas.append({n: p.detach().float() - w0[n] for n, p in pair.ll_model.named_parameters()})
-    for n in deltas[0]:
-        a, b = deltas[0][n], deltas[1][n]
-        # embeddings (few live rows, sparse tiny gradients) and b_K (zero gradient in exact arithmetic) are
-        # noise-driven under Adam; the exact-restore test above covers priming itself
-        if float(a.norm()) < 1e-6 or n.startswith(("embed.", "pos_embed.")) or n.endswith("b_K"):
-            continue
-        cos = float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
-        assert cos > 0.9 and 0.85 < float(b.norm() / a.norm()) < 1.15, (n, cos)
