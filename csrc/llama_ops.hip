@@ -147,6 +147,43 @@ __global__ __launch_bounds__(256) void rms_dw_kernel(const __bf16* __restrict__ 
   }
 }
 
+// Vectorised dw: thread = 8 consecutive columns (16-B loads of dy and x) x 8 rows; block = 32 column chunks (256
+// columns) x 8 row groups = 64 rows; the 8 row groups meet in LDS and each column takes one atomic per block.  The
+// scalar kernel above moves 2 B per load (~2.4 TB/s on [8192][4096]); d % 8 == 0 is required (as for the row kernels).
+__global__ __launch_bounds__(256) void rms_dw_vec_kernel(const __bf16* __restrict__ dy, const void* __restrict__ x,
+                                                         int x_f32, const float* __restrict__ rstd,
+                                                         float* __restrict__ dw, int T, int d) {
+  __shared__ float part[8][257];
+  const int cc = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 256 + cc * 8;
+  const int t0 = blockIdx.y * 64 + rg * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < d) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int t = t0 + i;
+      if (t < T) {
+        float g[8], xv[8];
+        ld8(dy + (long)t * d + c, false, g);
+        ld8((const char*)x + ((long)t * d + c) * (x_f32 ? 4 : 2), x_f32, xv);
+        const float r = rstd[t];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += g[e] * xv[e] * r;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[rg][cc * 8 + e] = acc[e];
+  __syncthreads();
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col < d) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += part[k][threadIdx.x];
+    atomicAdd(dw + col, s);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ rotary
 // x [B, S, H, D] with element strides (sb, ss, sh), unit stride on D; out contiguous [B, S, H, D].  cos/sin
 // [n_ctx, rd] fp32 (TL tables: angle repeated per pair layout).  One thread per (row, pair).
@@ -177,41 +214,135 @@ __global__ __launch_bounds__(256) void rotary_kernel(const __bf16* __restrict__ 
   orow[i1] = f2bf(bb * ct[i1] + a * st[i1] * sin_sign);
 }
 
+// Vectorised form: one thread per 8 consecutive features (one 16-B load of x, plus the 16-B partner chunk half a
+// rotary span away for GPT-NeoX halves); every access of a row is a full 16-B chunk.  Needs D % 8 == 0, the rotary
+// span a multiple of 16 (halves) or 8 (adjacent pairs) and 16-B aligned rows -- the Llama shapes (D = rd = 128);
+// anything else takes the per-pair kernel above.  Work per row: rd/16 (halves; each thread rotates its chunk and
+// the partner chunk) or rd/8 (adjacent) rotating threads, then (D - rd)/8 pass-through threads.
+__global__ __launch_bounds__(256) void rotary_vec_kernel(const __bf16* __restrict__ x, long sb, long ss, long sh,
+                                                         __bf16* __restrict__ out, const float* __restrict__ cosT,
+                                                         const float* __restrict__ sinT, float sin_sign, int B, int S,
+                                                         int H, int D, int rd, int offset, int adjacent) {
+  const int rot = adjacent ? rd / 8 : rd / 16, per_row = rot + (D - rd) / 8;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long rows = (long)B * S * H;
+  if (idx >= rows * per_row) return;
+  const long row = idx / per_row;
+  const int j = idx % per_row;
+  const int h = row % H, s = (row / H) % S, b = row / ((long)H * S);
+  const __bf16* xr = x + b * sb + (long)s * ss + (long)h * sh;
+  __bf16* orow = out + row * D;
+  if (j >= rot) {  // pass-through chunk
+    const int c = rd + (j - rot) * 8;
+    *(bf16x8*)(orow + c) = *(const bf16x8*)(xr + c);
+    return;
+  }
+  const float* ct = cosT + (long)(offset + s) * rd;
+  const float* st = sinT + (long)(offset + s) * rd;
+  if (adjacent) {  // pairs (2i, 2i+1) inside the chunk: rot(x)[2i] = -x[2i+1], rot(x)[2i+1] = x[2i]
+    const int c = j * 8;
+    float v[8], cs[8], sn[8], o[8];
+    ld8(xr + c, false, v);
+    ld8(ct + c, true, cs);
+    ld8(st + c, true, sn);
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      o[e] = v[e] * cs[e] - v[e + 1] * sn[e] * sin_sign;
+      o[e + 1] = v[e + 1] * cs[e + 1] + v[e] * sn[e + 1] * sin_sign;
+    }
+    st8(orow + c, false, o);
+  } else {  // halves: element c + e pairs with c + half + e
+    const int half = rd / 2, c0 = j * 8, c1 = c0 + half;
+    float a[8], bb[8], c0s[8], c0n[8], c1s[8], c1n[8], o0[8], o1[8];
+    ld8(xr + c0, false, a);
+    ld8(xr + c1, false, bb);
+    ld8(ct + c0, true, c0s);
+    ld8(st + c0, true, c0n);
+    ld8(ct + c1, true, c1s);
+    ld8(st + c1, true, c1n);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o0[e] = a[e] * c0s[e] - bb[e] * c0n[e] * sin_sign;
+      o1[e] = bb[e] * c1s[e] + a[e] * c1n[e] * sin_sign;
+    }
+    st8(orow + c0, false, o0);
+    st8(orow + c1, false, o1);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ SwiGLU
 __device__ __forceinline__ float silu_f(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
+// SW_U 16-B chunks per thread, all loads issued before any math (more bytes in flight per wave: the one-chunk form
+// measured ~3 TB/s on the Llama MLP shapes); chunk u of block b is b * 256 * SW_U + u * 256 + tid (coalesced per u)
+constexpr int SW_U = 4;
+
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const __bf16* __restrict__ gate, const __bf16* __restrict__ up,
                                                          __bf16* __restrict__ post, long n8) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n8) return;
-  float g[8], u[8], o[8];
-  ld8(gate + i * 8, false, g);
-  ld8(up + i * 8, false, u);
+  const long base = (long)blockIdx.x * 256 * SW_U + threadIdx.x;
+  bf16x8 g[SW_U], u[SW_U];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = silu_f(g[e]) * u[e];
-  st8(post + i * 8, false, o);
+  for (int k = 0; k < SW_U; ++k) {
+    const long i = base + k * 256;
+    if (i < n8) {
+      g[k] = __builtin_nontemporal_load((const bf16x8*)gate + i);
+      u[k] = __builtin_nontemporal_load((const bf16x8*)up + i);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < SW_U; ++k) {
+    const long i = base + k * 256;
+    if (i < n8) {
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(silu_f(bf2f(g[k][e])) * bf2f(u[k][e]));
+      *((bf16x8*)post + i) = o;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const __bf16* __restrict__ dpost, const __bf16* __restrict__ gate,
                                                          const __bf16* __restrict__ up, __bf16* __restrict__ dgate,
                                                          __bf16* __restrict__ dup, long n8) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n8) return;
-  float dp[8], g[8], u[8], dg[8], du[8];
-  ld8(dpost + i * 8, false, dp);
-  ld8(gate + i * 8, false, g);
-  ld8(up + i * 8, false, u);
+  const long base = (long)blockIdx.x * 256 * SW_U + threadIdx.x;
+  bf16x8 dp[SW_U], g[SW_U], u[SW_U];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-g[e]));
-    du[e] = dp[e] * g[e] * sg;
-    dg[e] = dp[e] * u[e] * sg * (1.f + g[e] * (1.f - sg));
+  for (int k = 0; k < SW_U; ++k) {
+    const long i = base + k * 256;
+    if (i < n8) {
+      dp[k] = __builtin_nontemporal_load((const bf16x8*)dpost + i);
+      g[k] = __builtin_nontemporal_load((const bf16x8*)gate + i);
+      u[k] = __builtin_nontemporal_load((const bf16x8*)up + i);
+    }
   }
-  st8(dgate + i * 8, false, dg);
-  st8(dup + i * 8, false, du);
+#pragma unroll
+  for (int k = 0; k < SW_U; ++k) {
+    const long i = base + k * 256;
+    if (i < n8) {
+      bf16x8 dg, du;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gv = bf2f(g[k][e]), dv = bf2f(dp[k][e]);
+        const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-gv));
+        du[e] = f2bf(dv * gv * sg);
+        dg[e] = f2bf(dv * bf2f(u[k][e]) * sg * (1.f + gv * (1.f - sg)));
+      }
+      *((bf16x8*)dgate + i) = dg;
+      *((bf16x8*)dup + i) = du;
+    }
+  }
 }
 
 bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+
+// IIT_LLAMA_VEC=0 selects the scalar rotary / RMSNorm-dw kernels (A/B and fallback), read once per process
+bool llama_vec_on() {
+  static const bool on = [] {
+    const char* e = getenv("IIT_LLAMA_VEC");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 }  // namespace
 
@@ -249,8 +380,13 @@ IIT_EXPORT int iit_rms_bwd_res(const void* dy, const void* x, int x_f32, const f
   if (vb <= 1) RB(1); else if (vb <= 2) RB(2); else if (vb <= 4) RB(4); else if (vb <= 8) RB(8); else RB(16);
 #undef RB
   if (dw) {
-    dim3 g2((d + 63) / 64, (T + 63) / 64);
-    hipLaunchKernelGGL(rms_dw_kernel, g2, block, 0, s, (const __bf16*)dy, x, x_f32, rstd, dw, T, d);
+    if (llama_vec_on()) {
+      dim3 g2((d + 255) / 256, (T + 63) / 64);
+      hipLaunchKernelGGL(rms_dw_vec_kernel, g2, block, 0, s, (const __bf16*)dy, x, x_f32, rstd, dw, T, d);
+    } else {
+      dim3 g2((d + 63) / 64, (T + 63) / 64);
+      hipLaunchKernelGGL(rms_dw_kernel, g2, block, 0, s, (const __bf16*)dy, x, x_f32, rstd, dw, T, d);
+    }
   }
   return (int)hipGetLastError();
 }
@@ -258,6 +394,15 @@ IIT_EXPORT int iit_rms_bwd_res(const void* dy, const void* x, int x_f32, const f
 IIT_EXPORT int iit_rotary(const void* x, long sb, long ss, long sh, void* out, const float* cosT, const float* sinT,
                           int inverse, int B, int S, int H, int D, int rd, int offset, int adjacent, void* stream) {
   if (rd % 2 || rd > D) return (int)hipErrorInvalidValue;
+  const bool vec = llama_vec_on() && D % 8 == 0 && (adjacent ? rd % 8 == 0 : rd % 16 == 0) && sb % 8 == 0 &&
+                   ss % 8 == 0 && sh % 8 == 0 && al16(x) && al16(out);
+  if (vec) {
+    const long work = (long)B * S * H * ((adjacent ? rd / 8 : rd / 16) + (D - rd) / 8);
+    hipLaunchKernelGGL(rotary_vec_kernel, dim3((work + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const __bf16*)x, sb, ss, sh, (__bf16*)out, cosT, sinT, inverse ? -1.f : 1.f, B, S, H, D, rd,
+                       offset, adjacent);
+    return (int)hipGetLastError();
+  }
   const long work = (long)B * S * H * (rd / 2 + (D - rd));
   hipLaunchKernelGGL(rotary_kernel, dim3((work + 255) / 256), dim3(256), 0, (hipStream_t)stream, (const __bf16*)x,
                      sb, ss, sh, (__bf16*)out, cosT, sinT, inverse ? -1.f : 1.f, B, S, H, D, rd, offset, adjacent);
@@ -267,7 +412,7 @@ IIT_EXPORT int iit_rotary(const void* x, long sb, long ss, long sh, void* out, c
 IIT_EXPORT int iit_swiglu_fwd(const void* gate, const void* up, void* post, long n, void* stream) {
   if (n % 8 || !al16(gate) || !al16(up) || !al16(post)) return (int)hipErrorInvalidValue;
   const long n8 = n / 8;
-  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3((n8 + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3((n8 + 256 * SW_U - 1) / (256 * SW_U)), dim3(256), 0, (hipStream_t)stream,
                      (const __bf16*)gate, (const __bf16*)up, (__bf16*)post, n8);
   return (int)hipGetLastError();
 }
@@ -276,7 +421,7 @@ IIT_EXPORT int iit_swiglu_bwd(const void* dpost, const void* gate, const void* u
                               void* stream) {
   if (n % 8 || !al16(dpost) || !al16(gate) || !al16(up) || !al16(dgate) || !al16(dup)) return (int)hipErrorInvalidValue;
   const long n8 = n / 8;
-  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3((n8 + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3((n8 + 256 * SW_U - 1) / (256 * SW_U)), dim3(256), 0, (hipStream_t)stream,
                      (const __bf16*)dpost, (const __bf16*)gate, (const __bf16*)up, (__bf16*)dgate, (__bf16*)dup, n8);
   return (int)hipGetLastError();
 }

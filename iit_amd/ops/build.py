@@ -18,6 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 CSRC = os.path.join(ROOT, "csrc")
 OUT_DIR = os.path.join(ROOT, "iit_amd", "_native")
 LIB = os.path.join(OUT_DIR, "libiit_hip.so")
+OBJ_CACHE = os.path.join(ROOT, "build", "objcache")  # git-ignored; not shipped to the GPU box
 SOURCES = ["gemm.hip", "gemm_glds.hip", "gemm_dual.hip", "kernels.hip", "attn_mfma.hip", "flash_attn.hip", "llama_ops.hip",
            "splice.hip", "ioi_hl.hip"]
 # per-source compiler flags: the pipelined LDS-DMA GEMM keeps its accumulators in VGPRs (MFMA VGPR form), which
@@ -53,22 +54,37 @@ def is_up_to_date() -> bool:
     return os.path.exists(LIB) and os.path.exists(stamp) and open(stamp).read().strip() == source_hash()
 
 
+def _obj_key(src: str) -> str:
+    """Object-cache key of one source: its text, every shared header, the arch and its flags."""
+    h = hashlib.sha256()
+    for p in [src] + [os.path.join(CSRC, x) for x in HEADERS]:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(ARCH.encode())
+    h.update(repr(EXTRA_FLAGS.get(os.path.basename(src), [])).encode())
+    return h.hexdigest()[:16]
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and is_up_to_date():
         return LIB
-    os.makedirs(OUT_DIR, exist_ok=True)
+    os.makedirs(OBJ_CACHE, exist_ok=True)
     objs = []
     procs = []
     for src in sources():
-        obj = os.path.join(OUT_DIR, os.path.basename(src) + ".o")
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
-               "-I", CSRC, "-c", src, "-o", obj] + EXTRA_FLAGS.get(os.path.basename(src), [])
-        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        # per-source object cache: only the sources (or shared headers) that changed are recompiled
+        obj = os.path.join(OBJ_CACHE, f"{os.path.basename(src)}.{_obj_key(src)}.o")
         objs.append(obj)
-    for cmd, p in procs:
+        if os.path.exists(obj) and not force:
+            continue
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
+               "-I", CSRC, "-c", src, "-o", obj + ".tmp"] + EXTRA_FLAGS.get(os.path.basename(src), [])
+        procs.append((cmd, obj, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+    for cmd, obj, p in procs:
         out, _ = p.communicate()
         if p.returncode != 0:
             raise RuntimeError(f"hipcc failed: {' '.join(cmd)}\n{out.decode(errors='replace')}")
+        os.replace(obj + ".tmp", obj)
         if verbose and out:
             print(out.decode(errors="replace"))
     tmp = LIB + ".tmp"
@@ -77,8 +93,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if res.returncode != 0:
         raise RuntimeError(f"link failed: {res.stdout.decode(errors='replace')}")
     os.replace(tmp, LIB)
-    for o in objs:
-        os.remove(o)
+    keep = set(objs)
+    for f in os.listdir(OBJ_CACHE):  # drop stale objects of earlier source versions
+        if os.path.join(OBJ_CACHE, f) not in keep:
+            os.remove(os.path.join(OBJ_CACHE, f))
     with open(LIB + ".stamp", "w") as f:
         f.write(source_hash())
     return LIB

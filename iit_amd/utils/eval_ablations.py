@@ -19,9 +19,13 @@ ablation -- ONE unablated base forward, all shared by the node loop; each node i
 then a single spliced forward (:class:`iit_amd.engine.plan.RunPlan`: in-kernel or
 patch-spec-kernel splices, a broadcast mean as the source), computing only the
 logits the metric reads, with scores accumulated on device (one host read per
-sweep instead of one per node per batch).  The scores are the per-node path's
-bit for bit (tests/test_eval_ablations.py).  Any other LL model takes the
-reference hook path.
+sweep instead of one per node per batch).  Nodes whose hook lies in the same
+block share ONE forward over stacked copies of the batch (M = nodes x B rows,
+resumed from the base run's residual at that block; ``_RowGroupSplice`` splices
+each node into its own rows), and each sweep's per-batch body is one HIP graph
+replay (``_SweepGraph``).  The scores equal the per-node reference-semantics path
+(tests/test_eval_ablations.py: bit for bit per node, within fp rounding for the
+grouped forwards).  Any other LL model takes the reference hook path.
 """
 from __future__ import annotations
 
@@ -162,6 +166,8 @@ class _BasePrefix:
             names = [f"blocks.{L}.hook_resid_pre" for L in layers]
             self.cache = {L: t for L, t in zip(layers, (self.model.run_capture(base_x, names)[n] for n in names))}
 
+        self.ok = bool(ok)
+
     def forward(self, base_x, node, plan):
         L = _node_layer(node.name)
         resid = self.cache.get(L) if L else None
@@ -169,6 +175,85 @@ class _BasePrefix:
             return self.model(base_x, plan=plan)
         # a copy: the resumed blocks must never see a buffer the next node at this layer reuses
         return self.model(resid.clone(), plan=plan, start_at_layer=L)
+
+    def forward_rows(self, base_x, layer, n, plan):
+        """One forward over ``n`` stacked copies of the base batch (rows ``[i B, (i+1) B)`` are copy ``i``),
+        resumed at ``layer`` from the shared prefix when it is cached."""
+        resid = self.cache.get(layer) if layer else None
+        if resid is None:
+            return self.model(base_x.repeat(n, *([1] * (base_x.dim() - 1))), plan=plan)
+        return self.model(resid.repeat(n, *([1] * (resid.dim() - 1))), plan=plan, start_at_layer=layer)
+
+
+class _RowGroupSplice:
+    """The splices of one hook in a node-batched sweep forward: the activation holds ``n`` stacked copies of the base
+    batch, and group ``(r0, r1, index, src)`` splices ``index`` from ``src`` (the node's B-row source or a broadcast
+    [1, ...] value) into rows ``[r0, r1)`` only -- ``out[r0:r1][index] = src[index]``, the reference hook's semantics
+    per copy (``/root/reference/iit/utils/eval_ablations.py:20-32``), one strided copy per node."""
+
+    whole = False
+
+    def __init__(self):
+        self.groups = []
+
+    def head_mask(self, n_heads: int):
+        return None
+
+    def apply(self, act: torch.Tensor) -> torch.Tensor:
+        out = act.clone()
+        for r0, r1, index, src in self.groups:
+            view = out[r0:r1]
+            if src.dtype != act.dtype or src.device != act.device:
+                src = src.to(device=act.device, dtype=act.dtype)
+            if src.shape != view.shape:
+                src = src.expand_as(view)
+            if index == EVERYTHING or index.is_everything():
+                view.copy_(src)
+            else:
+                ix = index.on(act.device)
+                view[ix] = src[ix]
+        return out
+
+
+_GROUP_ROWS = int(os.environ.get("IIT_EVAL_GROUP_ROWS", "131072"))
+
+
+def _node_groups(model_pair, base_x, prefix: "_BasePrefix", nodes):
+    """Node-batched sweep schedule: nodes whose hook lies in the same block share one forward
+    of M = n x B rows (large GEMMs instead of n small ones), resumed from the shared base prefix at that block.
+    Returns ``[(layer, [node positions])]`` plus the positions left to the per-node path.  ``IIT_EVAL_GROUP_ROWS``
+    caps the token rows of one grouped forward (0 = per-node forwards only)."""
+    if not prefix.ok or _GROUP_ROWS <= 0:
+        return [], list(range(len(nodes)))
+    per = base_x.numel()  # token rows of one copy of the batch
+    cap = max(1, _GROUP_ROWS // max(per, 1))
+    by_layer: Dict[int, list] = {}
+    single = []
+    for i, node in enumerate(nodes):
+        L = _node_layer(node.name)
+        if L is None or cap < 2:
+            single.append(i)
+        else:
+            by_layer.setdefault(L, []).append(i)
+    groups = []
+    for L in sorted(by_layer):
+        idx = by_layer[L]
+        for k in range(0, len(idx), cap):
+            chunk = idx[k:k + cap]
+            if len(chunk) == 1:
+                single.extend(chunk)
+            else:
+                groups.append((L, chunk))
+    return groups, sorted(single)
+
+
+def _group_plan(model_pair, nodes, positions, srcs, B: int) -> RunPlan:
+    plan = RunPlan(logits=model_pair.ll_logits_mode())
+    for i, p in enumerate(positions):
+        node = nodes[p]
+        spl = plan.splice.setdefault(node.name, [_RowGroupSplice()])[0]
+        spl.groups.append((i * B, (i + 1) * B, node.index if node.index is not None else EVERYTHING, srcs[p]))
+    return plan
 
 
 def _resample_scores(model_pair, base_in, ablation_in, nodes, atol: float = 5e-2, verbose: bool = False,
@@ -179,14 +264,25 @@ def _resample_scores(model_pair, base_in, ablation_in, nodes, atol: float = 5e-2
         cache = model_pair.ll_source_cache(ablation_in[0], nodes)
         model_pair.ll_cache = cache
         base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
-        prefix = _BasePrefix(model_pair, base_in[0], nodes)
-        scores = []
-        for node in nodes:
+        base_x = base_in[0]
+        prefix = _BasePrefix(model_pair, base_x, nodes)
+        scores = [None] * len(nodes)
+        groups, single = _node_groups(model_pair, base_x, prefix, nodes)
+        B = base_x.shape[0]
+        for L, pos in groups:
+            srcs = {p: cache[nodes[p].name] for p in pos}
+            ll_all = prefix.forward_rows(base_x, L, len(pos), _group_plan(model_pair, nodes, pos, srcs, B))
+            for i, p in enumerate(pos):
+                scores[p] = _resample_score(model_pair, base_in, ablation_in, ll_all[i * B:(i + 1) * B], base_hl_out,
+                                            hl_reduced, atol, verbose, nodes[p],
+                                            categorical_metric).float().reshape(())
+        for p in single:
+            node = nodes[p]
             plan = RunPlan.with_splices([(node.name, node.index, cache[node.name])],
                                         logits=model_pair.ll_logits_mode())
-            ll_out = prefix.forward(base_in[0], node, plan)
-            scores.append(_resample_score(model_pair, base_in, ablation_in, ll_out, base_hl_out, hl_reduced, atol,
-                                          verbose, node, categorical_metric).float().reshape(()))
+            ll_out = prefix.forward(base_x, node, plan)
+            scores[p] = _resample_score(model_pair, base_in, ablation_in, ll_out, base_hl_out, hl_reduced, atol,
+                                        verbose, node, categorical_metric).float().reshape(())
         return torch.stack(scores)
 
 
@@ -401,14 +497,22 @@ def _ablation_scores(model_pair, base_in, nodes, values: Dict[str, torch.Tensor]
         base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
         B = base_x.shape[0]
         prefix = _BasePrefix(model_pair, base_x, nodes)
-        scores = []
-        for node in nodes:
+        scores = [None] * len(nodes)
+        groups, single = _node_groups(model_pair, base_x, prefix, nodes)
+        for L, pos in groups:
+            srcs = {p: values[nodes[p].name] for p in pos}  # [1, ...] values broadcast per row group
+            ll_all = prefix.forward_rows(base_x, L, len(pos), _group_plan(model_pair, nodes, pos, srcs, B))
+            for i, p in enumerate(pos):
+                scores[p] = _ablation_score(model_pair, ll_all[i * B:(i + 1) * B], base_ll_out, base_hl_out,
+                                            hl_reduced, atol).float().reshape(())
+        for p in single:
+            node = nodes[p]
             v = values[node.name]
             v = v.expand(B, *v.shape[1:]) if v.shape[0] != B else v  # a view: no per-batch copy
             plan = RunPlan.with_splices([(node.name, node.index, v)], logits=model_pair.ll_logits_mode())
             ll_out = prefix.forward(base_x, node, plan)
-            scores.append(_ablation_score(model_pair, ll_out, base_ll_out, base_hl_out, hl_reduced,
-                                          atol).float().reshape(()))
+            scores[p] = _ablation_score(model_pair, ll_out, base_ll_out, base_hl_out, hl_reduced,
+                                        atol).float().reshape(())
         return torch.stack(scores)
 
 

@@ -1,7 +1,7 @@
 """Causal-effect sweeps (iit_amd.utils.eval_ablations / eval_metrics): native plan engine vs reference hooks."""
 import torch
 
-from iit_amd.core.index import Ix
+from iit_amd.core.index import EVERYTHING, Ix, TorchIndex
 from iit_amd.data.iit_dataset import IITDataset, IITUniqueDataset
 from iit_amd.tasks.ioi import make_ioi_corr, make_ioi_dataset_and_hl
 from iit_amd.utils import eval_ablations as ea
@@ -129,6 +129,51 @@ def test_prefix_shared_sweep_equals_full_forwards(monkeypatch):
     assert res[False].keys() == res[True].keys()
     for k in res[False]:
         assert abs(res[False][k] - res[True][k]) < 1e-5, k
+
+
+def test_node_batched_sweep_equals_per_node_forwards(monkeypatch):
+    """Nodes of one block sharing one forward over stacked copies of the batch (``_RowGroupSplice``) give the scores
+    of one spliced forward per node, for the resample and the mean-ablation sweeps."""
+    pair, ds = _pair()
+    iit_set = IITDataset(ds, ds, seed=0, device="cpu")
+    uni = IITUniqueDataset(ds, ds, seed=0, device="cpu")
+    calls = []
+    orig = ea._BasePrefix.forward_rows
+
+    def counting(self, base_x, layer, n, plan):
+        calls.append(n)
+        return orig(self, base_x, layer, n, plan)
+
+    monkeypatch.setattr(ea._BasePrefix, "forward_rows", counting)
+    res = {}
+    for rows in (0, 1 << 20):
+        monkeypatch.setattr(ea, "_GROUP_ROWS", rows)
+        torch.manual_seed(0)
+        r = dict(ea.check_causal_effect(pair, iit_set, batch_size=32, node_type="n"))
+        za_not, za_in = ea.get_causal_effects_for_all_nodes(pair, uni, batch_size=32, use_mean_cache=True)
+        r.update({("za", k): v for k, v in {**za_not, **za_in}.items()})
+        res[rows] = r
+        if rows == 0:
+            assert not calls
+    assert calls and max(calls) > 1
+    assert res[0].keys() == res[1 << 20].keys()
+    for k in res[0]:
+        assert abs(res[0][k] - res[1 << 20][k]) < 1e-5, k
+
+
+def test_row_group_splice_touches_only_its_rows():
+    act = torch.randn(6, 3, 4, 2)
+    src_a = torch.randn(2, 3, 4, 2)
+    mean = torch.randn(1, 3, 4, 2)
+    spl = ea._RowGroupSplice()
+    spl.groups.append((0, 2, TorchIndex([slice(None), slice(None), 1]), src_a))
+    spl.groups.append((4, 6, EVERYTHING, mean))
+    out = spl.apply(act)
+    ref = act.clone()
+    ref[0:2, :, 1] = src_a[:, :, 1]
+    ref[4:6] = mean.expand(2, 3, 4, 2)
+    assert torch.equal(out, ref)
+    assert not torch.equal(out, act)
 
 
 def test_start_at_layer_resumes_the_forward():

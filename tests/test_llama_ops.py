@@ -33,7 +33,7 @@ def test_rmsnorm_fwd_bwd(d, x_dtype):
 
 
 @pytest.mark.parametrize("adjacent", [False, True])
-@pytest.mark.parametrize("rd", [128, 64])
+@pytest.mark.parametrize("rd", [128, 64, 24])  # 24: the per-pair kernel (NeoX halves need rd % 16 == 0)
 def test_rotary_matches_torch_ops(adjacent, rd):
     from iit_amd.ops import hip_ops
     from iit_amd.ops.torch_ops import TorchOps
