@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
           ((float*)p.C)[(long)row * p.ldc + col] = p.resid[(long)row * p.ldr + col] + v;
         } else if (EPI == EPI_GELU || EPI == EPI_GELU_ERF) {
           if (p.bias0) v += p.bias0[col];
-          ((__bf16*)p.C2)[(long)row * p.ldc2 + col] = f2bf(v);
+          if (p.C2) ((__bf16*)p.C2)[(long)row * p.ldc2 + col] = f2bf(v);  // null: an inference forward
           ((__bf16*)p.C)[(long)row * p.ldc + col] = f2bf(EPI == EPI_GELU ? gelu_new_f(v) : gelu_erf_f(v));
         } else if (EPI == EPI_DGELU || EPI == EPI_DGELU_ERF) {
           const float pre = bf2f(((const __bf16*)p.aux)[(long)row * p.ldc2 + col]);

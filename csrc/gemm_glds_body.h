@@ -635,7 +635,8 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
       store8_f32((float*)p.C + (long)row * p.ldc + col, v, p.store_mode);
     } else if constexpr (EPI == E_GELU || EPI == E_GELU_ERF) {
       if (p.bias0) add8(v, p.bias0 + col);
-      store8_bf16((__bf16*)p.C2 + (long)row * p.ldc2 + col, v, p.store_mode);
+      // pre (C2) is only kept for the backward: inference forwards pass C2 = null and skip its store
+      if (p.C2) store8_bf16((__bf16*)p.C2 + (long)row * p.ldc2 + col, v, p.store_mode);
       float g[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {  // gelu of the stored (bf16) pre, which the backward reads

@@ -1511,3 +1511,64 @@ IIT_EXPORT int iit_zero_chunks(float* base, const long* chunks, int n_chunks, vo
   hipLaunchKernelGGL(zero_chunks_kernel, dim3(n_chunks), dim3(256), 0, (hipStream_t)stream, base, chunks);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------ sweep KL rows
+// Evaluation sweeps (iit_amd/utils/eval_metrics.py kl_rows): per row r of the LL output a [R][V] (fp32, row stride
+// lda) and the HL target pmf b [R][V] (row stride ldb), ONE pass over both computes
+//   out[r] = {sum_v a, logsumexp_v a, sum_v b a, sum_v b log a (terms with b = 0 skipped)}
+// -- everything KL(b || a) needs for either reading of a (logits: softmax; already a pmf: used as is), in place of
+// the reference's softmax / log / kl_div / sum chain (~10 passes over [R][V] per node).  One workgroup per row; the
+// logsumexp is the online (running max) form.
+__global__ __launch_bounds__(256) void kl_rows_kernel(const float* __restrict__ a, long lda, const float* __restrict__ b,
+                                                      long ldb, int V, float* __restrict__ out) {
+  const int r = blockIdx.x;
+  const float* ar = a + (long)r * lda;
+  const float* br = b + (long)r * ldb;
+  float s = 0.f, m = -INFINITY, e = 0.f, dba = 0.f, dbl = 0.f;
+  for (int v = threadIdx.x; v < V; v += 256) {
+    const float x = ar[v], p = br[v];
+    s += x;
+    if (x > m) {
+      e = e * __expf(m - x) + 1.f;
+      m = x;
+    } else {
+      e += __expf(x - m);
+    }
+    dba += p * x;
+    if (p != 0.f) dbl += p * __logf(x);
+  }
+  __shared__ float red[5][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // combine (m, e) pairs across the wave, then across waves
+  const float mw = wave_max(m);
+  e = m == -INFINITY ? 0.f : e * __expf(m - mw);
+  e = wave_sum(e);
+  s = wave_sum(s);
+  dba = wave_sum(dba);
+  dbl = wave_sum(dbl);
+  if (lane == 0) {
+    red[0][w] = s; red[1][w] = mw; red[2][w] = e; red[3][w] = dba; red[4][w] = dbl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = red[1][0];
+    for (int i = 1; i < 4; ++i) M = fmaxf(M, red[1][i]);
+    float E = 0.f, S = 0.f, DBA = 0.f, DBL = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      S += red[0][i];
+      E += red[1][i] == -INFINITY ? 0.f : red[2][i] * __expf(red[1][i] - M);
+      DBA += red[3][i];
+      DBL += red[4][i];
+    }
+    out[4 * r + 0] = S;
+    out[4 * r + 1] = M + __logf(E);
+    out[4 * r + 2] = DBA;
+    out[4 * r + 3] = DBL;
+  }
+}
+
+IIT_EXPORT int iit_kl_rows(const float* a, long lda, const float* b, long ldb, int R, int V, float* out, void* stream) {
+  if (R <= 0 || V <= 0) return 0;
+  hipLaunchKernelGGL(kl_rows_kernel, dim3(R), dim3(256), 0, (hipStream_t)stream, a, lda, b, ldb, V, out);
+  return hipGetLastError();
+}

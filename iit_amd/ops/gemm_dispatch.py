@@ -153,18 +153,26 @@ def _addmm_f32(c, base, a, b) -> None:
         torch.add(base, _mm_f32(a, b), out=c)
 
 
-def wgrad_into(c, x2, g2, store: bool) -> None:
+def wgrad_into(c, x2, g2, store: bool, params=()) -> None:
     """Weight gradient ``c (+)= x2^T @ g2`` (x2 [T, K_in], g2 [T, N] bf16; c [K_in, N] fp32, unit column stride):
     ``store`` writes it (beta = 0, a lazily-zeroed slot), else accumulates.  On the GPU the dispatcher measures the
     LDS-DMA kernel's fp32-store / -accumulate epilogues (and its deterministic reduction split) against hipBLASLt
-    per shape -- on the Llama-3-8B weight gradients the repo's kernel wins (profiles/llama3_8b_gemm_study_r3.txt)."""
+    per shape -- on the Llama-3-8B weight gradients the repo's kernel wins (profiles/llama3_8b_gemm_study_r3.txt).
+    ``params``: the arena parameters whose complete gradient a store writes -- the GEMM then also adds its sum of
+    squares into the arena's fused-norm slots (``FlatParams.norm_cover``), so the optimizer's clip does not read
+    these gradients again (the torch op backend's share of the fused norm; the HIP backend does the same)."""
     T, Kin = x2.shape
     N = g2.shape[1]
     ok = (c.is_cuda and x2.dtype == BF16 and g2.dtype == BF16 and c.dtype == F32 and x2.stride(1) == 1
           and g2.stride(1) == 1 and c.stride(-1) == 1 and c.dim() == 2 and POLICY in ("auto", "glds"))
     if ok:
+        gsq = None
+        flat = getattr(params[0], "_iit_flat", None) if params else None
+        if flat is not None:
+            flat.norm_intent(*params)
+            gsq = flat.norm_cover(*params) if store else None
         gemm(x2, g2, c, M=Kin, N=N, K=T, lda=x2.stride(0), ldb=g2.stride(0), ldc=c.stride(0),
-             mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store)
+             mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, gsq=gsq)
         return
     if store:
         _mm_f32_into(c, x2.t(), g2)
@@ -200,7 +208,8 @@ def _blas(A, B, C, M, N, Kd, lda, ldb, ldc, mode, epi, C2, C3, bias0, bias1, bia
         if bias0 is not None:
             c.add_(bias0.reshape(-1)[:N])
     elif epi in (K.EPI_GELU, K.EPI_GELU_ERF):
-        pre = _as(C2, M, N, ldc2)
+        # (C2 None: an inference forward that keeps no pre-activation -- a scratch for the library path)
+        pre = _as(C2, M, N, ldc2) if C2 is not None else torch.empty(M, N, dtype=BF16, device=A.device)
         torch.addmm(bias0.reshape(-1)[:N].to(BF16), a, b, out=pre)
         _gelu_into(pre, _as(C, M, N, ldc), erf=epi == K.EPI_GELU_ERF)
     elif epi in (K.EPI_DGELU, K.EPI_DGELU_ERF):

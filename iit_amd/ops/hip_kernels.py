@@ -52,6 +52,7 @@ _SIGS = {
     "iit_adam_flat": [c_void_p] * 6 + [c_int, c_void_p, c_int] + [c_float] * 6 + [c_void_p] * 3
                      + [c_void_p, c_int, c_void_p, c_void_p],
     "iit_sumsq_2d": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p],
+    "iit_kl_rows": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_void_p, c_void_p],
     "iit_adam_span_size": [],
     "iit_sumsq_spans": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "iit_adam_spans": [c_void_p] * 6 + [c_int, c_void_p] + [c_float] * 6 + [c_void_p] * 4,
@@ -334,6 +335,17 @@ def gemm_dual(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, reduce:
         x.get("ldc2", 0), x["M"], x["N"], x["K"], x["epi"], xtile, _p(x.get("csum")), _p(w.get("bsum")),
         _p(w.get("gsq")) if w["epi"] == EPI_F32_STORE else None, _stream()),
         "iit_gemm_dual")
+
+
+def kl_rows(a, b):
+    """Per-row statistics of an LL output ``a`` [R, V] against an HL pmf ``b`` [R, V] (fp32, unit column stride):
+    [R, 4] = (sum a, logsumexp a, sum b a, sum_{b > 0} b log a), one pass over both (csrc/kernels.hip)."""
+    R, V = a.shape
+    out = torch.empty(R, 4, dtype=torch.float32, device=a.device)
+    if CHECK_BOUNDS:
+        _bounds("kl_rows", ("a", a, R, V, a.stride(0)), ("b", b, R, V, b.stride(0)))
+    _check(lib().iit_kl_rows(_p(a), a.stride(0), _p(b), b.stride(0), R, V, _p(out), _stream()), "kl_rows")
+    return out
 
 
 def sumsq_2d(c, ldc: int, M: int, N: int, gsq) -> None:

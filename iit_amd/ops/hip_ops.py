@@ -1484,7 +1484,21 @@ class HipOps(TorchOps):
 
     def mlp_gelu_residual(self, x, W_in, b_in, W_out, b_out, resid, erf: bool = False):
         """``resid + gelu(x W_in + b_in) W_out + b_out`` (gelu_new, or the exact erf GELU) for a block whose MLP
-        sites are all dead: the backward forms dpre in the dX GEMM's epilogue (see :class:`MLPOutGeluFn`)."""
+        sites are all dead: the backward forms dpre in the dX GEMM's epilogue (see :class:`MLPOutGeluFn`).
+        Without autograd (evaluation sweeps, source captures) the W_in epilogue stores only ``post``: no
+        pre-activation is kept for a backward, half the epilogue's writes."""
+        if not torch.is_grad_enabled():
+            lead, d, dm, N = x.shape[:-1], x.shape[-1], W_in.shape[1], W_out.shape[1]
+            x2 = _flat2(x.to(BF16).contiguous())
+            T = x2.shape[0]
+            post = torch.empty(T, dm, dtype=BF16, device=x.device)
+            gemm(x2, self._L(W_in)["in"], post, C2=None, M=T, N=dm, K=d, lda=d, ldb=dm, ldc=dm, ldc2=dm,
+                 mode=K.MODE_BKM, epi=K.EPI_GELU_ERF if erf else K.EPI_GELU, bias0=b_in)
+            r2 = _flat2(resid.float().contiguous())
+            out = torch.empty(T, N, dtype=F32, device=x.device)
+            gemm(post, self._L(W_out)["out"], out, M=T, N=N, K=dm, lda=dm, ldb=W_out.shape[1], ldc=N,
+                 mode=K.MODE_BKM, epi=K.EPI_F32_RESID, bias0=b_out, resid=r2, ldr=N)
+            return out.view(*lead, N)
         pre, post = MLPInFn.apply(x, W_in, b_in, self._L(W_in)["in"], erf)
         return MLPOutGeluFn.apply(pre, post.detach(), W_out, b_out, self._L(W_out)["out"], W_out.shape[1], resid,
                                   b_in, erf)

@@ -139,8 +139,8 @@ class _MirrorLinear(torch.autograd.Function):
             dx = (g2 @ flat.shadow_view(W).t()).view(*ctx.lead, W.shape[0])
         if W.requires_grad:
             from .gemm_dispatch import wgrad_into
-            if flat.claim(W):  # lazily-zeroed slot: store (beta = 0)
-                wgrad_into(W.grad, x2, g2, store=True)
+            if flat.claim(W):  # lazily-zeroed slot: store (beta = 0), with its share of the fused clip norm
+                wgrad_into(W.grad, x2, g2, store=True, params=(W,))
             else:
                 slot = W.grad
                 if slot is None:
@@ -186,7 +186,7 @@ class _MirrorMat(torch.autograd.Function):
             from .gemm_dispatch import wgrad_into
             flat = ctx.wparams[0]._iit_flat
             # a claimed (lazily-zeroed) slot is stored (beta = 0), else accumulated
-            wgrad_into(ctx.gw, x2, g2, store=flat.claim(*ctx.wparams))
+            wgrad_into(ctx.gw, x2, g2, store=flat.claim(*ctx.wparams), params=ctx.wparams)
         if ctx.gb is not None:
             for b in ctx.bparams:
                 if b.grad is None:
@@ -221,6 +221,29 @@ class _MirrorMatResid(torch.autograd.Function):
         dx = _MirrorMat.backward(ctx, gy)[0]
         dres = gy.to(ctx.rdtype) if ctx.needs_input_grad[1] else None
         return (dx, dres) + (None,) * (6 + ctx.n_leaves)
+
+
+class _SplitQKV(torch.autograd.Function):
+    """``q, k, v`` head views of the packed projection output ``y [..., (H + 2 H_kv) dh]``.  The backward
+    concatenates their gradients into one ``[..., N]`` tensor with one launch; autograd's three slice backwards
+    would each zero-fill a y-sized tensor, copy into it and add the three (~25 ms/step of fills, strided copies and
+    adds on Llama-3-8B at S = 512, profiles/llama3_8b_s512_step_breakdown_r4.txt)."""
+
+    @staticmethod
+    def forward(ctx, y, H: int, Hkv: int, dh: int):
+        lead = y.shape[:-1]
+        ctx.lead, ctx.dims = lead, (H * dh, Hkv * dh, Hkv * dh)
+        q = y[..., :H * dh].view(*lead, H, dh)
+        k = y[..., H * dh:(H + Hkv) * dh].view(*lead, Hkv, dh)
+        v = y[..., (H + Hkv) * dh:].view(*lead, Hkv, dh)
+        ctx.dtype, ctx.device = y.dtype, y.device
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        parts = [torch.zeros(*ctx.lead, n, dtype=ctx.dtype, device=ctx.device) if g is None
+                 else g.reshape(*ctx.lead, n).to(ctx.dtype) for g, n in zip((dq, dk, dv), ctx.dims)]
+        return torch.cat(parts, -1), None, None, None
 
 
 def _bound_to_arena(flat, p: torch.Tensor) -> bool:
@@ -369,6 +392,7 @@ class TorchOps:
             gb = flat.grad.as_strided((N,), (1,), boff) if packed_b else None
             bp = bs if packed_b else ()
             y = _MirrorMat.apply(xb, wm, bm, gw, gb, ws, bp, *(ws + bp))
+            return _SplitQKV.apply(y, H, Hkv, dh)
         lead = x.shape[:-1]
         q = y[..., :H * dh].view(*lead, H, dh)
         k = y[..., H * dh:(H + Hkv) * dh].view(*lead, Hkv, dh)

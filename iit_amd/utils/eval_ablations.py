@@ -39,7 +39,7 @@ from ..core.index import EVERYTHING, TorchIndex
 from ..core.nodes import LLNode
 from ..engine.plan import RunPlan
 from ..hooks.hook_points import HookPoint
-from .eval_metrics import kl_div
+from .eval_metrics import kl_div, kl_div_from_stats, target_stats
 from .node_picker import get_all_nodes, get_nodes_in_circuit, get_nodes_not_in_circuit
 from .progress import progress
 
@@ -101,7 +101,8 @@ def do_intervention(model_pair, base_input, ablation_input, node: LLNode, hooker
 
 
 def _resample_score(model_pair, base_in, ablation_in, ll_out, base_hl_out, hl_reduced, atol: float = 5e-2,
-                    verbose: bool = False, node=None, categorical_metric: Categorical_Metric = Categorical_Metric.KL):
+                    verbose: bool = False, node=None, categorical_metric: Categorical_Metric = Categorical_Metric.KL,
+                    hl_stats=None):
     base_y, ablation_y = base_in[1], ablation_in[1]
     reduced = _reduced_logits(model_pair)
     if model_pair.hl_model.is_categorical():
@@ -110,7 +111,10 @@ def _resample_score(model_pair, base_in, ablation_in, ll_out, base_hl_out, hl_re
         ll_at = _at(ll_out, label_idx, reduced)
         hl_at = _at(base_hl_out.squeeze() if not hl_reduced else base_hl_out, label_idx, hl_reduced)
         if categorical_metric == Categorical_Metric.KL:
-            score = kl_div(ll_at, hl_at, EVERYTHING).mean()
+            if hl_stats is not None and ll_at.dim() == 2:  # batched sweep: the HL side computed once per batch
+                score = kl_div_from_stats(ll_at, hl_stats).mean()
+            else:
+                score = kl_div(ll_at, hl_at, EVERYTHING).mean()
             if verbose:
                 print(node, "kl base_hl vs ll_out:", float(score),
                       "fraction of labels changed:", float((~label_unchanged).float().mean()))
@@ -155,16 +159,29 @@ class _BasePrefix:
     on average about half of the blocks per node are skipped.  ``IIT_EVAL_PREFIX=0`` runs every forward from the
     tokens."""
 
-    def __init__(self, model_pair, base_x, nodes):
+    def __init__(self, model_pair, base_x, nodes, src_x=None):
+        """``src_x`` (optional, same shape as ``base_x``): also capture every node's hook on the source input in the
+        SAME truncated forward (one capture over the stacked [base; source] rows instead of two forwards);
+        ``self.src_cache`` then holds it ({} when not done -- the caller captures the source itself)."""
         self.model = model_pair.ll_model
         self.cache = {}
+        self.src_cache = {}
         layers = sorted({L for L in (_node_layer(n.name) for n in nodes) if L})
         ok = (_PREFIX and layers and hasattr(self.model, "blocks") and getattr(self.model, "supports_run_plan", False)
               and "start_at_layer" in getattr(self.model.forward, "__code__", type("", (), {"co_varnames": ()})
                                               ).co_varnames)
         if ok:
             names = [f"blocks.{L}.hook_resid_pre" for L in layers]
-            self.cache = {L: t for L, t in zip(layers, (self.model.run_capture(base_x, names)[n] for n in names))}
+            if (src_x is not None and isinstance(src_x, torch.Tensor) and isinstance(base_x, torch.Tensor)
+                    and src_x.shape == base_x.shape and src_x.device == base_x.device):
+                B = base_x.shape[0]
+                src_names = sorted({n.name for n in nodes})
+                cap = self.model.run_capture(torch.cat([base_x, src_x]), sorted(set(names) | set(src_names)))
+                self.cache = {L: cap[n][:B] for L, n in zip(layers, names)}
+                self.src_cache = {n: cap[n][B:] for n in src_names}
+            else:
+                cap = self.model.run_capture(base_x, names)  # ONE truncated forward for every block's residual
+                self.cache = {L: cap[n] for L, n in zip(layers, names)}
 
         self.ok = bool(ok)
 
@@ -261,28 +278,32 @@ def _resample_scores(model_pair, base_in, ablation_in, nodes, atol: float = 5e-2
     """One batch of the native resample sweep: one source capture of every node's hook and one HL base output,
     then one spliced base forward per node; the scores as one device vector (node order)."""
     with torch.no_grad():
-        cache = model_pair.ll_source_cache(ablation_in[0], nodes)
+        base_x = base_in[0]
+        prefix = _BasePrefix(model_pair, base_x, nodes, src_x=ablation_in[0])
+        cache = prefix.src_cache or model_pair.ll_source_cache(ablation_in[0], nodes)
         model_pair.ll_cache = cache
         base_hl_out, hl_reduced = _hl_out(model_pair, base_in)
-        base_x = base_in[0]
-        prefix = _BasePrefix(model_pair, base_x, nodes)
         scores = [None] * len(nodes)
         groups, single = _node_groups(model_pair, base_x, prefix, nodes)
         B = base_x.shape[0]
+        stats = None
+        if (categorical_metric == Categorical_Metric.KL and model_pair.hl_model.is_categorical()
+                and _reduced_logits(model_pair) and hl_reduced and base_hl_out.dim() == 2):
+            stats = target_stats(base_hl_out)  # the HL pmf side of every node's KL, once per batch
         for L, pos in groups:
             srcs = {p: cache[nodes[p].name] for p in pos}
             ll_all = prefix.forward_rows(base_x, L, len(pos), _group_plan(model_pair, nodes, pos, srcs, B))
             for i, p in enumerate(pos):
                 scores[p] = _resample_score(model_pair, base_in, ablation_in, ll_all[i * B:(i + 1) * B], base_hl_out,
-                                            hl_reduced, atol, verbose, nodes[p],
-                                            categorical_metric).float().reshape(())
+                                            hl_reduced, atol, verbose, nodes[p], categorical_metric,
+                                            stats).float().reshape(())
         for p in single:
             node = nodes[p]
             plan = RunPlan.with_splices([(node.name, node.index, cache[node.name])],
                                         logits=model_pair.ll_logits_mode())
             ll_out = prefix.forward(base_x, node, plan)
             scores[p] = _resample_score(model_pair, base_in, ablation_in, ll_out, base_hl_out, hl_reduced, atol,
-                                        verbose, node, categorical_metric).float().reshape(())
+                                        verbose, node, categorical_metric, stats).float().reshape(())
         return torch.stack(scores)
 
 

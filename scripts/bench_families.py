@@ -28,7 +28,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--family", required=True, choices=["mqnli-bert-base", "llama3-8b-causal", "llama-tiny-causal",
                                                          "mqnli-bert-tiny", "pvr-resnet18"])
@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--graphs", type=int, default=None,
                     help="HIP-graph phases (default: on for BERT; off for Llama, whose strict phase has one graph per "
                          "non-circuit node -- ~1000 at 32 layers x 32 heads -- and whose GEMMs are not launch-bound)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def setup(args, dev):

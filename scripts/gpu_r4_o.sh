@@ -25,3 +25,5 @@ IIT_TORCH_RESID_EPI=1 IIT_RMS_FORK=1 step ll_prof 900 rocprofv3 --kernel-trace -
 f=$(find $O/llprof -name "*kernel_trace.csv" | head -n 1)
 [ -n "$f" ] && python3 scripts/step_breakdown.py "$f" --steps 3 --top 40 --gaps 3 > $O/llama_breakdown.txt && head -50 $O/llama_breakdown.txt
 rm -rf $O/llprof
+IIT_EVAL_GRAPHS=0 step eval_profile 600 python3 -u scripts/profile_eval.py
+grep -E "^\[eval\]" $O/eval_profile.log

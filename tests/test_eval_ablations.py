@@ -1,4 +1,5 @@
 """Causal-effect sweeps (iit_amd.utils.eval_ablations / eval_metrics): native plan engine vs reference hooks."""
+import pytest
 import torch
 
 from iit_amd.core.index import EVERYTHING, Ix, TorchIndex
@@ -183,3 +184,24 @@ def test_start_at_layer_resumes_the_forward():
     full = m(tok)
     resid3 = m.run_capture(tok, ["blocks.3.hook_resid_pre"])["blocks.3.hook_resid_pre"]
     assert torch.allclose(m(resid3, start_at_layer=3), full, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_kl_rows_kernel_matches_kl_div():
+    """csrc/kernels.hip kl_rows (one pass over LL logits and the HL pmf) gives kl_div's per-row KL for logits and
+    for rows that are already pmfs, including a padded row stride (the unembed's fp32 output)."""
+    from iit_amd.utils.eval_metrics import kl_div_from_stats, target_stats
+    torch.manual_seed(0)
+    dev = "cuda"
+    V = 50257
+    hl = torch.randn(37, V, device=dev) * 4
+    ll_pad = torch.randn(37, V + 7, device=dev) * 3
+    ll = ll_pad[:, :V]  # row stride V + 7
+    stats = target_stats(hl)
+    got = kl_div_from_stats(ll, stats)
+    want = kl_div(ll, hl, EVERYTHING)
+    assert torch.allclose(got, want, rtol=1e-4, atol=1e-5)
+    pm = torch.softmax(torch.randn(37, V, device=dev), -1)
+    got = kl_div_from_stats(pm, stats)
+    want = kl_div(pm, hl, EVERYTHING)
+    assert torch.allclose(got, want, rtol=1e-4, atol=1e-5)

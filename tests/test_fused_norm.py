@@ -100,3 +100,51 @@ def test_fused_norm_sums_match_gradients(monkeypatch):
     for got, want in checked:
         assert want > 0 and abs(got - want) <= 1e-4 * want, (got, want)
     assert float(flat.gsq.abs().sum()) == 0.0  # consumed and re-zeroed by the norm pass
+
+
+@pytest.mark.gpu
+def test_fused_norm_torch_backend_llama(monkeypatch):
+    """GPU, torch op backend (Llama family): the weight-gradient GEMMs of ``_MirrorLinear`` / ``_MirrorMat``
+    (``gemm_dispatch.wgrad_into(..., params=...)``) add the sums of squares of the gradients they store; at every
+    optimizer step the slots hold exactly those, and the clip reads only the rest."""
+    from iit_amd.data.iit_dataset import IITDataset
+    from iit_amd.models.convert import llama_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.ops import hip_kernels
+    from iit_amd.tasks.causal_graph import CausalGraphModelPair, make_causal_graph_task
+
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    cfg = llama_config_dict("llama-tiny", device="cuda:0", dtype=torch.bfloat16)
+    ll = HookedTransformer(cfg)
+    ds, hl, corr = make_causal_graph_task(ll, n_samples=256, device=dev, seq_len=24)
+    pair = CausalGraphModelPair(hl, ll, corr, training_args={"batch_size": 32, "lr": 1e-4, "lr_scheduler": None,
+                                                             "early_stop": False, "clip_grad_norm": 1.0})
+    opt = pair.make_optimizer(1e-4)
+    flat = opt.flat
+    assert flat.norm_fuse
+    checked = []
+    real = hip_kernels.adam_step
+
+    def checking_step(fl, *a, **kw):
+        torch.cuda.synchronize()
+        covered = set(fl._norm_covered)
+        if covered and not fl._norm_dirty:
+            want = 0.0
+            for o, n in fl.slots:
+                members = [i for i, p in enumerate(fl.params) if o <= fl.offset_of(p) < o + max(n, 1)]
+                if members and all(i in covered for i in members):
+                    want += float(fl.grad[o:o + n].double().pow(2).sum())
+            checked.append((float(fl.gsq.double().sum()), want))
+        return real(fl, *a, **kw)
+
+    monkeypatch.setattr(hip_kernels, "adam_step", checking_step)
+    train = IITDataset(ds, ds, seed=0, device=dev)
+    it = iter(train.make_loader(32, 0))
+    for _ in range(2):
+        base, abl = next(it)
+        pair.run_train_step(base, abl, pair.loss_fn, opt)
+    torch.cuda.synchronize()
+    assert len(checked) >= 4, checked
+    for got, want in checked:
+        assert want > 0 and abs(got - want) <= 1e-4 * want, (got, want)
