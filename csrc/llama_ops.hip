@@ -8,6 +8,7 @@
 //             the backward is the same kernel with sin negated (the rotation is orthogonal)
 //   SwiGLU    post = silu(gate) * up;  dgate = dpost up silu'(gate), dup = dpost silu(gate)
 #include "common.h"
+#include "splice_spec.h"
 
 namespace {
 
@@ -333,6 +334,58 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const __bf16* __restric
   }
 }
 
+// SwiGLU with an interchange splice of its output (``mlp.hook_post``) applied in the producer: the elements the patch
+// spec selects take the source's value instead of silu(gate) * up, and their gate / up gradients are zero (the spliced
+// value is a constant) -- the reference's hook ``out[idx] = src[idx]`` (base_model_pair.py:151-163) without the
+// separate read + write pass of the standalone splice kernel and its gradient mask.  One thread per 8 consecutive
+// features (the spec's innermost dimension a multiple of 8).
+__global__ __launch_bounds__(256) void swiglu_splice_fwd_kernel(const __bf16* __restrict__ gate,
+                                                                const __bf16* __restrict__ up,
+                                                                __bf16* __restrict__ post,
+                                                                const __bf16* __restrict__ src, long n8,
+                                                                SpliceSpec sp) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  int c0, c1, c2, c3;
+  spec_coords(sp, i * 8, c0, c1, c2, c3);
+  const bool row = in_ranges(sp, 0, c0) && in_ranges(sp, 1, c1) && in_ranges(sp, 2, c2);
+  const bf16x8 g = *((const bf16x8*)gate + i), u = *((const bf16x8*)up + i);
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = f2bf(silu_f(bf2f(g[e])) * bf2f(u[e]));
+  if (row) {
+    const long sb = (long)c0 * sp.sstride[0] + (long)c1 * sp.sstride[1] + (long)c2 * sp.sstride[2];
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (in_ranges(sp, 3, c3 + e)) o[e] = src[sb + (long)(c3 + e) * sp.sstride[3]];
+  }
+  *((bf16x8*)post + i) = o;
+}
+
+__global__ __launch_bounds__(256) void swiglu_splice_bwd_kernel(const __bf16* __restrict__ dpost,
+                                                                const __bf16* __restrict__ gate,
+                                                                const __bf16* __restrict__ up,
+                                                                __bf16* __restrict__ dgate, __bf16* __restrict__ dup,
+                                                                long n8, SpliceSpec sp) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  int c0, c1, c2, c3;
+  spec_coords(sp, i * 8, c0, c1, c2, c3);
+  const bool row = in_ranges(sp, 0, c0) && in_ranges(sp, 1, c1) && in_ranges(sp, 2, c2);
+  const bf16x8 dp = *((const bf16x8*)dpost + i), g = *((const bf16x8*)gate + i), u = *((const bf16x8*)up + i);
+  bf16x8 dg, du;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float gv = bf2f(g[e]);
+    const float dv = (row && in_ranges(sp, 3, c3 + e)) ? 0.f : bf2f(dp[e]);
+    const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-gv));
+    du[e] = f2bf(dv * gv * sg);
+    dg[e] = f2bf(dv * bf2f(u[e]) * sg * (1.f + gv * (1.f - sg)));
+  }
+  *((bf16x8*)dgate + i) = dg;
+  *((bf16x8*)dup + i) = du;
+}
+
 bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
 // IIT_LLAMA_VEC=0 selects the scalar rotary / RMSNorm-dw kernels (A/B and fallback), read once per process
@@ -423,5 +476,28 @@ IIT_EXPORT int iit_swiglu_bwd(const void* dpost, const void* gate, const void* u
   const long n8 = n / 8;
   hipLaunchKernelGGL(swiglu_bwd_kernel, dim3((n8 + 256 * SW_U - 1) / (256 * SW_U)), dim3(256), 0, (hipStream_t)stream,
                      (const __bf16*)dpost, (const __bf16*)gate, (const __bf16*)up, (__bf16*)dgate, (__bf16*)dup, n8);
+  return (int)hipGetLastError();
+}
+
+// ``spec``: host pointer to one SpliceSpec over the [.., d_mlp] activation (innermost dimension a multiple of 8)
+IIT_EXPORT int iit_swiglu_splice_fwd(const void* gate, const void* up, void* post, const void* src, long n,
+                                     const void* spec, void* stream) {
+  const SpliceSpec sp = *(const SpliceSpec*)spec;
+  if (n % 8 || sp.shape[3] % 8 || !al16(gate) || !al16(up) || !al16(post)) return (int)hipErrorInvalidValue;
+  const long n8 = n / 8;
+  hipLaunchKernelGGL(swiglu_splice_fwd_kernel, dim3((n8 + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     (const __bf16*)gate, (const __bf16*)up, (__bf16*)post, (const __bf16*)src, n8, sp);
+  return (int)hipGetLastError();
+}
+
+IIT_EXPORT int iit_swiglu_splice_bwd(const void* dpost, const void* gate, const void* up, void* dgate, void* dup,
+                                     long n, const void* spec, void* stream) {
+  const SpliceSpec sp = *(const SpliceSpec*)spec;
+  if (n % 8 || sp.shape[3] % 8 || !al16(dpost) || !al16(gate) || !al16(up) || !al16(dgate) || !al16(dup))
+    return (int)hipErrorInvalidValue;
+  const long n8 = n / 8;
+  hipLaunchKernelGGL(swiglu_splice_bwd_kernel, dim3((n8 + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     (const __bf16*)dpost, (const __bf16*)gate, (const __bf16*)up, (__bf16*)dgate, (__bf16*)dup, n8,
+                     sp);
   return (int)hipGetLastError();
 }

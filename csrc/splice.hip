@@ -12,22 +12,7 @@
 // with no index tensors, no host synchronisation and a single pass over the activation (graph-capturable).
 // Each thread handles 8 consecutive elements of the innermost dimension (16-B bf16 / 32-B fp32 vector access).
 #include "common.h"
-
-struct SpliceSpec {
-  int shape[4];     // row-major shape (leading dims padded with 1)
-  int nr[4];        // ranges per dimension (>= 1)
-  int lo[4][8];
-  int hi[4][8];
-  long sstride[4];  // source strides in elements (0 = broadcast)
-};
-
-__device__ __forceinline__ bool in_ranges(const SpliceSpec& sp, int d, int c) {
-  bool ok = false;
-#pragma unroll
-  for (int r = 0; r < 8; ++r)
-    if (r < sp.nr[d]) ok |= (c >= sp.lo[d][r]) & (c < sp.hi[d][r]);
-  return ok;
-}
+#include "splice_spec.h"
 
 template <typename T>
 __device__ __forceinline__ float ld_f(const T* p) {

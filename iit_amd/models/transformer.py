@@ -407,13 +407,20 @@ class TransformerBlock(nn.Module):
         else:
             x, resid_mid = self._norm_fork(self.ln2, resid_mid, run)
             pre_hook = (lambda t: run.site(mlp.hook_pre, t)) if run.live(mlp.hook_pre) else None
+            spliced = False
             if mlp.gated:
                 lin_hook = (lambda t: run.site(mlp.hook_pre_linear, t)) if run.live(mlp.hook_pre_linear) else None
-                _, post = TorchOps.mlp_gated_in(ops, x, mlp.W_gate, mlp.W_in, mlp.b_in, self.cfg.act_fn,
-                                                hook_pre=pre_hook, hook_pre_linear=lin_hook)
+                pspl = run.plan.splice.get(mlp.hook_post.name) if run.plan is not None else None
+                if pspl and len(pspl) == 1 and not pspl[0].whole and pre_hook is None and lin_hook is None:
+                    # the hook_post splice inside the SwiGLU kernel (the producer), not a separate pass
+                    _, post, spliced = TorchOps.mlp_gated_in(ops, x, mlp.W_gate, mlp.W_in, mlp.b_in,
+                                                             self.cfg.act_fn, splice=pspl[0])
+                else:
+                    _, post = TorchOps.mlp_gated_in(ops, x, mlp.W_gate, mlp.W_in, mlp.b_in, self.cfg.act_fn,
+                                                    hook_pre=pre_hook, hook_pre_linear=lin_hook)
             else:
                 _, post = ops.mlp_in(x, mlp.W_in, mlp.b_in, self.cfg.act_fn, hook_pre=pre_hook)
-            post = run.site(mlp.hook_post, post)
+            post = run.site(mlp.hook_post, post, spliced=spliced)
         if run.live(self.hook_mlp_out) or not (ops.fused or getattr(ops, "fuses_residual", False)):
             mlp_out = run.site(self.hook_mlp_out, ops.mlp_out(post, mlp.W_out, mlp.b_out))
             resid_post = ops.residual(resid_mid, mlp_out)

@@ -24,7 +24,7 @@ SOURCES = ["gemm.hip", "gemm_glds.hip", "gemm_dual.hip", "kernels.hip", "attn_mf
 # per-source compiler flags: the pipelined LDS-DMA GEMM keeps its accumulators in VGPRs (MFMA VGPR form), which
 # avoids the AGPR shuffles hipcc otherwise emits around its register double buffer
 EXTRA_FLAGS = {"gemm_glds.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "gemm_dual.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
-HEADERS = ["common.h", "gemm_glds_body.h"]
+HEADERS = ["common.h", "gemm_glds_body.h", "splice_spec.h"]
 ARCH = os.environ.get("IIT_OFFLOAD_ARCH", "gfx950")
 
 

@@ -153,14 +153,16 @@ def _addmm_f32(c, base, a, b) -> None:
         torch.add(base, _mm_f32(a, b), out=c)
 
 
-def wgrad_into(c, x2, g2, store: bool, params=()) -> None:
+def wgrad_into(c, x2, g2, store: bool, params=(), bsum=None) -> None:
     """Weight gradient ``c (+)= x2^T @ g2`` (x2 [T, K_in], g2 [T, N] bf16; c [K_in, N] fp32, unit column stride):
     ``store`` writes it (beta = 0, a lazily-zeroed slot), else accumulates.  On the GPU the dispatcher measures the
     LDS-DMA kernel's fp32-store / -accumulate epilogues (and its deterministic reduction split) against hipBLASLt
     per shape -- on the Llama-3-8B weight gradients the repo's kernel wins (profiles/llama3_8b_gemm_study_r3.txt).
     ``params``: the arena parameters whose complete gradient a store writes -- the GEMM then also adds its sum of
     squares into the arena's fused-norm slots (``FlatParams.norm_cover``), so the optimizer's clip does not read
-    these gradients again (the torch op backend's share of the fused norm; the HIP backend does the same)."""
+    these gradients again (the torch op backend's share of the fused norm; the HIP backend does the same).
+    ``bsum`` (fp32 [N], optional): += the column sums of ``g2`` -- the bias gradient of the layer -- from the B
+    fragments the LDS-DMA kernel already holds (a column-sum pass after a library GEMM)."""
     T, Kin = x2.shape
     N = g2.shape[1]
     ok = (c.is_cuda and x2.dtype == BF16 and g2.dtype == BF16 and c.dtype == F32 and x2.stride(1) == 1
@@ -172,12 +174,15 @@ def wgrad_into(c, x2, g2, store: bool, params=()) -> None:
             flat.norm_intent(*params)
             gsq = flat.norm_cover(*params) if store else None
         gemm(x2, g2, c, M=Kin, N=N, K=T, lda=x2.stride(0), ldb=g2.stride(0), ldc=c.stride(0),
-             mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, gsq=gsq)
+             mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, gsq=gsq,
+             bsum=bsum)
         return
     if store:
         _mm_f32_into(c, x2.t(), g2)
     else:
         _addmm_f32(c, c, x2.t(), g2)
+    if bsum is not None:
+        bsum.add_(g2.float().sum(0))
 
 
 def _gelu_into(pre, out, erf: bool = False) -> None:

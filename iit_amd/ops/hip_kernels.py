@@ -73,6 +73,8 @@ _SIGS = {
     "iit_rotary": [c_void_p, c_long, c_long, c_long, c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p],
     "iit_swiglu_fwd": [c_void_p, c_void_p, c_void_p, c_long, c_void_p],
     "iit_swiglu_bwd": [c_void_p] * 5 + [c_long, c_void_p],
+    "iit_swiglu_splice_fwd": [c_void_p] * 4 + [c_long, c_void_p, c_void_p],
+    "iit_swiglu_splice_bwd": [c_void_p] * 5 + [c_long, c_void_p, c_void_p],
     "iit_flash_fwd": [c_void_p] * 3 + [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ull] + [c_int] * 5
                      + [c_float, c_int, c_void_p],
     "iit_flash_bwd": [c_void_p] * 3 + [c_void_p] * 11 + [c_ull] + [c_int] * 5 + [c_float, c_int, c_void_p],
@@ -557,6 +559,19 @@ def rotary(x, out, cos, sin, rd: int, offset: int, adjacent: bool, inverse: bool
 
 def swiglu_fwd(gate, up, post):
     _check(lib().iit_swiglu_fwd(_p(gate), _p(up), _p(post), gate.numel(), _stream()), "swiglu_fwd")
+
+
+def swiglu_splice_fwd(gate, up, post, src, spec_ptr):
+    """``post = silu(gate) * up`` with the patch spec at host address ``spec_ptr`` spliced from ``src`` (same
+    element order as the spec; see :mod:`iit_amd.ops.splice`)."""
+    _check(lib().iit_swiglu_splice_fwd(_p(gate), _p(up), _p(post), _p(src), gate.numel(), spec_ptr, _stream()),
+           "swiglu_splice_fwd")
+
+
+def swiglu_splice_bwd(dpost, gate, up, dgate, dup, spec_ptr):
+    """SwiGLU backward with the spliced elements' gradient zeroed."""
+    _check(lib().iit_swiglu_splice_bwd(_p(dpost), _p(gate), _p(up), _p(dgate), _p(dup), gate.numel(), spec_ptr,
+                                       _stream()), "swiglu_splice_bwd")
 
 
 def swiglu_bwd(dpost, gate, up, dgate, dup):

@@ -802,6 +802,41 @@ class SwiGLUFn(Function):
         return dg, du
 
 
+class SwiGLUSpliceFn(Function):
+    """:class:`SwiGLUFn` with an interchange splice of its output applied inside the kernel (``csrc/llama_ops.hip``
+    ``swiglu_splice_*``): selected elements take ``src``'s value, their gate / up gradients are zero."""
+
+    @staticmethod
+    def forward(ctx, gate, up, src, spec):
+        gate, up = _c16(gate.to(BF16)), _c16(up.to(BF16))
+        post = torch.empty_like(gate)
+        K.swiglu_splice_fwd(gate, up, post, src, spec.ptr)
+        ctx.save_for_backward(gate, up)
+        ctx.spec = spec
+        return post
+
+    @staticmethod
+    def backward(ctx, dpost):
+        gate, up = ctx.saved_tensors
+        dg, du = torch.empty_like(gate), torch.empty_like(up)
+        K.swiglu_splice_bwd(_c16(dpost.to(BF16)), gate, up, dg, du, ctx.spec.ptr)
+        return dg, du, None, None
+
+
+def swiglu_spliced(pre, pre_linear, index, src) -> Optional[torch.Tensor]:
+    """``silu(pre) * pre_linear`` with ``out[index] = src[index]`` fused into the SwiGLU kernel, or None when the
+    patch-spec table cannot express the index / the shapes do not fit (the caller splices separately)."""
+    from .splice import patch_spec
+    if os.environ.get("IIT_SWIGLU_SPLICE", "1") == "0" or pre.shape[-1] % 8 or pre.dtype != BF16:
+        return None
+    if src.dtype != BF16 or src.device != pre.device:
+        src = src.to(device=pre.device, dtype=BF16)
+    spec = patch_spec(index, tuple(pre.shape), src)
+    if spec is None or spec.dims[3][0] % 8:
+        return None
+    return SwiGLUSpliceFn.apply(pre, pre_linear, src, spec)
+
+
 def llama_fused_ok(x: torch.Tensor) -> bool:
     """The Llama-family fused kernels apply: a bf16 activation on the GPU (``IIT_LLAMA_FUSED=0`` disables)."""
     return x.is_cuda and x.dtype == BF16 and os.environ.get("IIT_LLAMA_FUSED", "1") != "0"

@@ -64,6 +64,17 @@ def _accumulate(p: torch.Tensor, g: torch.Tensor) -> None:
     grad_hooks.notify(p)
 
 
+def _mm_bias(x2: torch.Tensor, wm: torch.Tensor, bm: Optional[torch.Tensor]) -> torch.Tensor:
+    """``x2 @ wm (+ bm)`` as ONE library GEMM with the bias in its epilogue (``addmm`` with a 1-D bias) -- a separate
+    broadcast add is a non-vectorised elementwise pass over the [T, N] output (~48 us per Llama-3-8B projection at
+    S = 512, 5 per block and phase: 23 ms/step, profiles/llama3_8b_s512_step_breakdown_r4.txt)."""
+    if bm is None:
+        return x2 @ wm
+    if bm.dim() == 1 and bm.dtype == wm.dtype and x2.dim() == 2:
+        return torch.addmm(bm, x2, wm)
+    return x2 @ wm + bm
+
+
 def _bias_grad_accumulate(slot: torch.Tensor, g2: torch.Tensor) -> None:
     """fp32 ``slot`` += column sums of the ``[T, N]`` gradient ``g2`` (HIP column-sum kernel on the GPU)."""
     if g2.is_cuda and slot.is_contiguous() and slot.dtype == torch.float32 and g2.stride(-1) == 1:
@@ -121,9 +132,7 @@ class _MirrorLinear(torch.autograd.Function):
         Wm = _flat.shadow_view(W)
         lead = x.shape[:-1]
         x2 = x.reshape(-1, x.shape[-1])
-        y = x2 @ Wm
-        if b is not None:
-            y = y + _flat.shadow_view(b)
+        y = _mm_bias(x2, Wm, _flat.shadow_view(b) if b is not None else None)
         ctx.save_for_backward(x2)
         ctx.W, ctx.b, ctx.flat, ctx.lead = W, b, _flat, lead
         return y.view(*lead, y.shape[-1])
@@ -137,20 +146,27 @@ class _MirrorLinear(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = (g2 @ flat.shadow_view(W).t()).view(*ctx.lead, W.shape[0])
+        bsum = None
+        if b is not None and b.requires_grad:
+            if b.grad is None:
+                flat.bind_zero(b)
+            bsum = b.grad if (b.grad.is_contiguous() and b.grad.dtype == torch.float32) else None
         if W.requires_grad:
             from .gemm_dispatch import wgrad_into
+            # the bias gradient (colsum of g2) comes out of the weight-gradient GEMM (``bsum``)
             if flat.claim(W):  # lazily-zeroed slot: store (beta = 0), with its share of the fused clip norm
-                wgrad_into(W.grad, x2, g2, store=True, params=(W,))
+                wgrad_into(W.grad, x2, g2, store=True, params=(W,), bsum=bsum)
             else:
                 slot = W.grad
                 if slot is None:
                     slot = W.grad = torch.zeros_like(W)
-                wgrad_into(slot, x2, g2, store=False)
+                wgrad_into(slot, x2, g2, store=False, bsum=bsum)
             grad_hooks.notify(W)
+        else:
+            bsum = None
         if b is not None and b.requires_grad:
-            if b.grad is None:
-                flat.bind_zero(b)
-            _bias_grad_accumulate(b.grad, g2)
+            if bsum is None:
+                _bias_grad_accumulate(b.grad, g2)
             grad_hooks.notify(b)
         return dx, None, None, None
 
@@ -166,9 +182,7 @@ class _MirrorMat(torch.autograd.Function):
     def forward(ctx, x, wm, bm, gw, gb, wparams, bparams, *leaves):
         lead = x.shape[:-1]
         x2 = x.reshape(-1, x.shape[-1])
-        y = x2 @ wm
-        if bm is not None:
-            y = y + bm
+        y = _mm_bias(x2, wm, bm)
         ctx.save_for_backward(x2)
         ctx.wm, ctx.gw, ctx.gb, ctx.lead, ctx.n_leaves = wm, gw, gb, lead, len(leaves)
         ctx.wparams, ctx.bparams = wparams, bparams
@@ -182,15 +196,19 @@ class _MirrorMat(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = (g2 @ ctx.wm.t()).view(*ctx.lead, ctx.wm.shape[0])
-        if ctx.gw is not None:
-            from .gemm_dispatch import wgrad_into
-            flat = ctx.wparams[0]._iit_flat
-            # a claimed (lazily-zeroed) slot is stored (beta = 0), else accumulated
-            wgrad_into(ctx.gw, x2, g2, store=flat.claim(*ctx.wparams), params=ctx.wparams)
         if ctx.gb is not None:
             for b in ctx.bparams:
                 if b.grad is None:
                     b._iit_flat.bind_zero(b)
+        fused_b = ctx.gw is not None and ctx.gb is not None and ctx.gb.is_contiguous()
+        if ctx.gw is not None:
+            from .gemm_dispatch import wgrad_into
+            flat = ctx.wparams[0]._iit_flat
+            # a claimed (lazily-zeroed) slot is stored (beta = 0), else accumulated; the bias gradient (colsum of
+            # g2) comes out of the same GEMM
+            wgrad_into(ctx.gw, x2, g2, store=flat.claim(*ctx.wparams), params=ctx.wparams,
+                       bsum=ctx.gb if fused_b else None)
+        if ctx.gb is not None and not fused_b:
             _bias_grad_accumulate(ctx.gb, g2)
         for p in ctx.wparams + ctx.bparams:
             grad_hooks.notify(p)
@@ -383,10 +401,7 @@ class TorchOps:
         bm = sh.as_strided((N,), (1,), boff) if packed_b else None
         xb = x.to(torch.bfloat16)
         if not grad:
-            y = xb.reshape(-1, d) @ wm
-            if bm is not None:
-                y = y + bm
-            y = y.view(*x.shape[:-1], N)
+            y = _mm_bias(xb.reshape(-1, d), wm, bm).view(*x.shape[:-1], N)
         else:
             gw = flat.grad.as_strided((d, N), (N, 1), off)
             gb = flat.grad.as_strided((N,), (1,), boff) if packed_b else None
@@ -436,8 +451,8 @@ class TorchOps:
                 grad = torch.is_grad_enabled() and W_O.requires_grad
                 z2 = z.to(torch.bfloat16).reshape(*z.shape[:-2], H * dh)
                 if not grad:
-                    y = z2 @ wm
-                    return y if mb is None else y + mb[1]
+                    return _mm_bias(z2.reshape(-1, H * dh), wm, None if mb is None else mb[1]).view(
+                        *z2.shape[:-1], d)
                 if _bound_to_arena(flat, W_O) and (b_O is None or _bound_to_arena(flat, b_O)):
                     bp = () if b_O is None else (b_O,)
                     gw = flat.grad.as_strided((H * dh, d), (d, 1), flat.offset_of(W_O))
@@ -515,20 +530,31 @@ class TorchOps:
             pre = hook_pre(pre)
         return pre, act_fn(act)(pre)
 
-    def mlp_gated_in(self, x, W_gate, W_in, b_in, act: str, hook_pre=None, hook_pre_linear=None):
-        """TL ``GatedMLP``: ``pre = x W_gate`` (hook_pre), ``pre_linear = x W_in + b_in``, ``post = act(pre) * pre_linear``."""
+    def mlp_gated_in(self, x, W_gate, W_in, b_in, act: str, hook_pre=None, hook_pre_linear=None, splice=None):
+        """TL ``GatedMLP``: ``pre = x W_gate`` (hook_pre), ``pre_linear = x W_in + b_in``, ``post = act(pre) * pre_linear``.
+
+        ``splice`` (a plan ``Splice`` of ``hook_post``, optional): returns ``(pre, post, spliced)``, where
+        ``spliced`` says the splice was applied inside the SwiGLU kernel (the producer's epilogue); otherwise the
+        caller applies it at the hook site."""
         pre = self.lin(x, W_gate)
         if act == "silu" and hook_pre is None and hook_pre_linear is None and pre.is_cuda \
                 and pre.dtype == torch.bfloat16 and pre.shape[-1] % 8 == 0:
             from . import hip_ops
             if hip_ops.llama_fused_ok(pre):
                 pre_linear = self.lin(x, W_in, b_in)
+                if splice is not None:
+                    post = hip_ops.swiglu_spliced(pre, pre_linear, splice.index, splice.src)
+                    if post is not None:
+                        return pre, post, True
+                    return pre, hip_ops.SwiGLUFn.apply(pre, pre_linear), False
                 return pre, hip_ops.SwiGLUFn.apply(pre, pre_linear)
         if hook_pre is not None:
             pre = hook_pre(pre)
         pre_linear = self.lin(x, W_in, b_in)
         if hook_pre_linear is not None:
             pre_linear = hook_pre_linear(pre_linear)
+        if splice is not None:
+            return pre, act_fn(act)(pre) * pre_linear, False
         return pre, act_fn(act)(pre) * pre_linear
 
     def mlp_out(self, post, W_out, b_out):

@@ -19,3 +19,11 @@ for r in a b; do
   echo "shipped $r: $(j bench_shipped_$r)"
 done
 grep -c "blas" $O/decisions_new_a.txt || true
+# MQNLI <-> BERT-base step trace: the position splices run inside the LN kernel (no splice_kernel rows expected)
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/mq -o mq -- python3 scripts/bench_families.py --family mqnli-bert-base --steps 12 --warmup 3 > $O/mq_run.log 2>&1
+rc=$?; echo "mq prof rc=$rc"; grep -E '^\{' $O/mq_run.log | cut -c1-200
+[ $rc -eq 0 ] || exit $rc
+f=$(find $O/mq -name "*kernel_stats.csv" | head -n 1)
+echo "splice rows in the MQNLI kernel stats: $(grep -ci splice "$f" || true)"
+cp "$f" $O/mqnli_kernel_stats.csv
+rm -rf $O/mq

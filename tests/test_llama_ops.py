@@ -150,3 +150,38 @@ def test_llama_torch_backend_matches_fp32_oracle():
     for n in gr:
         if gr[n].norm() > 1e-6:
             assert rel(ga[n], gr[n]) < 5e-2, n
+
+
+@pytest.mark.parametrize("index_kind", ["last_half", "positions"])
+def test_swiglu_splice_in_kernel_matches_separate_pass(monkeypatch, index_kind):
+    """A ``mlp.hook_post`` splice applied inside the SwiGLU kernel (the producer) gives the separate patch-spec pass's
+    output and gradients exactly (forward: selected elements = source; backward: their gate / up gradients zero)."""
+    import copy
+    from iit_amd.core.index import Ix
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.engine.plan import RunPlan
+    from iit_amd.models.convert import llama_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    cfg = llama_config_dict("llama-tiny", device=dev, dtype=torch.bfloat16)
+    torch.manual_seed(1)
+    a = HookedTransformer(cfg)
+    b = copy.deepcopy(a)
+    FlatParams(a, with_bf16_shadow=True)
+    FlatParams(b, with_bf16_shadow=True)
+    tok = torch.randint(0, cfg["d_vocab"], (4, 24), device=dev)
+    src_tok = torch.randint(0, cfg["d_vocab"], (4, 24), device=dev)
+    name = "blocks.1.mlp.hook_post"
+    dm = cfg["d_mlp"]
+    idx = Ix[:, -1, :dm // 2] if index_kind == "last_half" else Ix[:, [2, 5, 6]]
+    outs, grads = [], []
+    for model, fused in ((a, "1"), (b, "0")):
+        monkeypatch.setenv("IIT_SWIGLU_SPLICE", fused)
+        with torch.no_grad():
+            src = model.run_capture(src_tok, [name])[name]
+        out = model(tok, plan=RunPlan.with_splices([(name, idx, src)]))
+        out.float().pow(2).mean().backward()
+        outs.append(out.detach().float())
+        grads.append({n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.grad is not None})
+    assert torch.equal(outs[0], outs[1])
+    for n in grads[1]:
+        assert torch.allclose(grads[0][n], grads[1][n], rtol=1e-3, atol=1e-6), n
