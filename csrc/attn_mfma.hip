@@ -15,6 +15,7 @@
 // Heads selected by ``head_mask`` are interchange-spliced: z := zsrc and their
 // q/k/v gradients are zero (the spliced value is a constant).
 #include "common.h"
+#include "splice_spec.h"
 
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4_t;
 
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(256) void attn_mfma_fwd_kernel(const __bf16* __rest
                                                             unsigned long long head_mask, int BH, int S, int H,
                                                             long ld_qkv, long ld_z, long ld_src, float scale,
                                                             int causal, __bf16* __restrict__ z2, int pair_seqs,
-                                                            unsigned long long pair_mask) {
+                                                            unsigned long long pair_mask, SpliceSpec sp, int use_sp) {
   constexpr int LDSR = DH + 8;
   __shared__ __attribute__((aligned(16))) __bf16 smem[4][16 * LDSR];
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
@@ -140,7 +141,39 @@ __global__ __launch_bounds__(256) void attn_mfma_fwd_kernel(const __bf16* __rest
     const int r = i / (DH / 8), ch = i % (DH / 8);
     if (r < S) {
       const bf16x8 v = *(const bf16x8*)(Vs + r * LDSR + ch * 8);
-      *(bf16x8*)(z + (row0 + r) * ld_z + h * DH + ch * 8) = v;
+      __bf16* zo = z + (row0 + r) * ld_z + h * DH + ch * 8;
+      if (use_sp && pair_seqs > 0) {
+        // general patch spec over the base rows' z [pair_seqs][S][H][DH]: the source wave of (b, h) also stores the
+        // selected elements of its row into the base row; the base wave stores only the unselected ones (disjoint
+        // writes, no ordering between the two waves needed).  A partly selected 16-B chunk goes out element-wise.
+        const bool base = b < pair_seqs;
+        const int bb = base ? b : b - pair_seqs;
+        const bool rowsel = in_ranges(sp, 0, bb) && in_ranges(sp, 1, r) && in_ranges(sp, 2, h);
+        unsigned m = 0;
+        if (rowsel) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m |= (unsigned)in_ranges(sp, 3, ch * 8 + e) << e;
+        }
+        if (base) {
+          if (m == 0) *(bf16x8*)zo = v;
+          else if (m != 0xffu) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (!((m >> e) & 1u)) zo[e] = v[e];
+          }
+        } else {
+          *(bf16x8*)zo = v;
+          __bf16* zb = z + (row0 - (long)pair_seqs * S + r) * ld_z + h * DH + ch * 8;
+          if (m == 0xffu) *(bf16x8*)zb = v;
+          else if (m) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if ((m >> e) & 1u) zb[e] = v[e];
+          }
+        }
+        continue;
+      }
+      *(bf16x8*)zo = v;
       if (z2) *(bf16x8*)(z2 + (row0 + r) * ld_z + h * DH + ch * 8) = v;
       if (mirror_src) *(bf16x8*)(z + (row0 - (long)pair_seqs * S + r) * ld_z + h * DH + ch * 8) = v;
     }
@@ -151,7 +184,8 @@ template <int DH>
 __global__ __launch_bounds__(256) void attn_mfma_bwd_kernel(const __bf16* __restrict__ qkv, const __bf16* __restrict__ dz,
                                                             const float* __restrict__ lse, __bf16* __restrict__ dqkv,
                                                             unsigned long long head_mask, int BH, int S, int H,
-                                                            long ld_qkv, long ld_dz, float scale, int causal) {
+                                                            long ld_qkv, long ld_dz, float scale, int causal,
+                                                            SpliceSpec sp, int use_sp) {
   constexpr int LDSR = DH + 8;
   __shared__ __attribute__((aligned(16))) __bf16 smem[4][3][16 * LDSR];
   __shared__ float Dsh[4][16];
@@ -176,6 +210,12 @@ __global__ __launch_bounds__(256) void attn_mfma_bwd_kernel(const __bf16* __rest
     kf[s] = load8(qkv + off + HD, ok);
     vf[s] = load8(qkv + off + 2 * HD, ok);
     gf[s] = load8(dz + (row0 + c) * ld_dz + h * DH + 32 * s + 8 * g, ok);
+    if (use_sp && ok && in_ranges(sp, 0, b) && in_ranges(sp, 1, c) && in_ranges(sp, 2, h)) {
+      // spliced elements of z are the source's (a constant): their gradient is zero
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (in_ranges(sp, 3, 32 * s + 8 * g + e)) gf[s][e] = f2bf(0.f);
+    }
     if (work) {
       *(bf16x8*)(Qs + c * LDSR + 32 * s + 8 * g) = qf[s];
       *(bf16x8*)(Ks + c * LDSR + 32 * s + 8 * g) = kf[s];
@@ -286,10 +326,34 @@ IIT_EXPORT int iit_attn_mfma_fwd(const void* qkv, void* z, float* lse, const voi
 
 // the same with the paired-row options of attn_mfma_fwd_kernel (``z2`` copy, ``pair_mask`` heads of the first
 // ``pair_seqs`` sequences taken from the sequences ``pair_seqs`` later)
+static int attn_fwd_launch(const void* qkv, void* z, float* lse, const void* zsrc, unsigned long long head_mask,
+                           int B, int S, int H, int dh, long ld_qkv, long ld_z, long ld_src, float scale, int causal,
+                           void* z2, int pair_seqs, unsigned long long pair_mask, const SpliceSpec& sp, int use_sp,
+                           void* stream);
+
 IIT_EXPORT int iit_attn_mfma_fwd_pair(const void* qkv, void* z, float* lse, const void* zsrc,
                                       unsigned long long head_mask, int B, int S, int H, int dh, long ld_qkv, long ld_z,
                                       long ld_src, float scale, int causal, void* z2, int pair_seqs,
                                       unsigned long long pair_mask, void* stream) {
+  const SpliceSpec none{};
+  return attn_fwd_launch(qkv, z, lse, zsrc, head_mask, B, S, H, dh, ld_qkv, ld_z, ld_src, scale, causal, z2,
+                         pair_seqs, pair_mask, none, 0, stream);
+}
+
+// Paired rows with a general interchange splice of ``hook_z`` (host SpliceSpec over the base rows' [B][S][H][dh]
+// z, e.g. one position of some heads): applied in the kernel's store (see attn_mfma_fwd_kernel); no head mirroring
+IIT_EXPORT int iit_attn_mfma_fwd_spec(const void* qkv, void* z, float* lse, int B, int S, int H, int dh, long ld_qkv,
+                                      long ld_z, float scale, int causal, int pair_seqs, const void* spec,
+                                      void* stream) {
+  if (pair_seqs <= 0) return (int)hipErrorInvalidValue;
+  return attn_fwd_launch(qkv, z, lse, nullptr, 0ull, B, S, H, dh, ld_qkv, ld_z, 0, scale, causal, nullptr, pair_seqs,
+                         0ull, *(const SpliceSpec*)spec, 1, stream);
+}
+
+static int attn_fwd_launch(const void* qkv, void* z, float* lse, const void* zsrc, unsigned long long head_mask,
+                           int B, int S, int H, int dh, long ld_qkv, long ld_z, long ld_src, float scale, int causal,
+                           void* z2, int pair_seqs, unsigned long long pair_mask, const SpliceSpec& sp, int use_sp,
+                           void* stream) {
   if (S > 16) return (int)hipErrorInvalidValue;
   if (pair_seqs < 0 || (pair_seqs > 0 && 2 * pair_seqs != B)) return (int)hipErrorInvalidValue;
   const int BH = B * H;
@@ -298,7 +362,7 @@ IIT_EXPORT int iit_attn_mfma_fwd_pair(const void* qkv, void* z, float* lse, cons
 #define AF(D)                                                                                                       \
   hipLaunchKernelGGL(attn_mfma_fwd_kernel<D>, grid, block, 0, s, (const __bf16*)qkv, (__bf16*)z, lse,               \
                      (const __bf16*)zsrc, head_mask, BH, S, H, ld_qkv, ld_z, ld_src, scale, causal, (__bf16*)z2,    \
-                     pair_seqs, pair_mask)
+                     pair_seqs, pair_mask, sp, use_sp)
   if (dh == 32) AF(32);
   else if (dh == 64) AF(64);
   else if (dh == 96) AF(96);
@@ -308,16 +372,35 @@ IIT_EXPORT int iit_attn_mfma_fwd_pair(const void* qkv, void* z, float* lse, cons
   return hipGetLastError();
 }
 
+static int attn_bwd_launch(const void* qkv, const void* dz, const float* lse, void* dqkv, unsigned long long head_mask,
+                           int B, int S, int H, int dh, long ld_qkv, long ld_dz, float scale, int causal,
+                           const SpliceSpec& sp, int use_sp, void* stream);
+
 IIT_EXPORT int iit_attn_mfma_bwd(const void* qkv, const void* dz, const float* lse, void* dqkv,
                                  unsigned long long head_mask, int B, int S, int H, int dh, long ld_qkv, long ld_dz,
                                  float scale, int causal, void* stream) {
+  const SpliceSpec none{};
+  return attn_bwd_launch(qkv, dz, lse, dqkv, head_mask, B, S, H, dh, ld_qkv, ld_dz, scale, causal, none, 0, stream);
+}
+
+// the backward of iit_attn_mfma_fwd_spec's base rows: the spliced elements of dz are zeroed as they are loaded
+IIT_EXPORT int iit_attn_mfma_bwd_spec(const void* qkv, const void* dz, const float* lse, void* dqkv, int B, int S,
+                                      int H, int dh, long ld_qkv, long ld_dz, float scale, int causal,
+                                      const void* spec, void* stream) {
+  return attn_bwd_launch(qkv, dz, lse, dqkv, 0ull, B, S, H, dh, ld_qkv, ld_dz, scale, causal,
+                         *(const SpliceSpec*)spec, 1, stream);
+}
+
+static int attn_bwd_launch(const void* qkv, const void* dz, const float* lse, void* dqkv, unsigned long long head_mask,
+                           int B, int S, int H, int dh, long ld_qkv, long ld_dz, float scale, int causal,
+                           const SpliceSpec& sp, int use_sp, void* stream) {
   if (S > 16) return (int)hipErrorInvalidValue;
   const int BH = B * H;
   dim3 grid((BH + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
 #define AB(D)                                                                                                       \
   hipLaunchKernelGGL(attn_mfma_bwd_kernel<D>, grid, block, 0, s, (const __bf16*)qkv, (const __bf16*)dz, lse,        \
-                     (__bf16*)dqkv, head_mask, BH, S, H, ld_qkv, ld_dz, scale, causal)
+                     (__bf16*)dqkv, head_mask, BH, S, H, ld_qkv, ld_dz, scale, causal, sp, use_sp)
   if (dh == 32) AB(32);
   else if (dh == 64) AB(64);
   else if (dh == 96) AB(96);

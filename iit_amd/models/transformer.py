@@ -471,11 +471,17 @@ class TransformerBlock(nn.Module):
             x, resid = ops.pair_layer_norm_fork(p, self.ln1.w, self.ln1.b, self.ln1.eps)
             qkv = ops.pair_qkv(x, attn.W_Q, attn.W_K, attn.W_V, attn.b_Q, attn.b_K, attn.b_V)
             heads, rest = None, list(zs or ())
+            z = None
             if mirror and len(rest) == 1:
                 heads = Splice(rest[0], None).head_mask(H)
                 if heads is not None:
                     rest = []  # head splice inside the attention kernel
-            z = ops.pair_attention(qkv, causal, attn.attn_scale, heads=heads)
+                else:  # any other patch-spec index (positions, features, ...) in the kernel's z store
+                    z = ops.pair_attention_spliced(qkv, causal, attn.attn_scale, rest[0])
+                    if z is not None:
+                        rest = []
+            if z is None:
+                z = ops.pair_attention(qkv, causal, attn.attn_scale, heads=heads)
             for ix in rest:
                 z = ops.pair_splice(z, ix)
         if zs is not None:

@@ -46,6 +46,9 @@ _SIGS = {
     "iit_attn_mfma_fwd_pair": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float,
                                                 c_int, c_void_p, c_int, c_ull, c_void_p],
     "iit_attn_mfma_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
+    "iit_attn_mfma_fwd_spec": [c_void_p] * 3 + [c_int] * 4 + [c_long, c_long, c_float, c_int, c_int, c_void_p,
+                                                               c_void_p],
+    "iit_attn_mfma_bwd_spec": [c_void_p] * 4 + [c_int] * 4 + [c_long, c_long, c_float, c_int, c_void_p, c_void_p],
     "iit_ce_fwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "iit_ce_bwd": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_long, c_int, c_int, c_int,
                    c_void_p, c_void_p],
@@ -473,6 +476,28 @@ def attn_pair_fwd(qkv, z, lse, B, S, H, dh, ld_qkv, ld_z, scale, causal, z2=None
                 ("z2", z2, B * S, H * dh, ld_z), ("lse", lse, 1, B * H * S, B * H * S))
     _check(lib().iit_attn_mfma_fwd_pair(_p(qkv), _p(z), _p(lse), None, 0, B, S, H, dh, ld_qkv, ld_z, 0, scale,
                                         int(causal), _p(z2), pair_seqs, pair_mask, _stream()), "attn_mfma_fwd_pair")
+
+
+def attn_pair_fwd_spec(qkv, z, lse, B, S, H, dh, ld_qkv, ld_z, scale, causal, pair_seqs, spec_ptr):
+    """Paired-row MFMA attention with a general ``hook_z`` splice (patch spec over the base rows' [B/2, S, H, dh] z at
+    host address ``spec_ptr``) applied in the kernel's store: the source rows' selected elements go to the base rows
+    (csrc/attn_mfma.hip)."""
+    if not _mfma_attn(S, dh):
+        raise RuntimeError("attn_pair_fwd_spec needs the MFMA short-sequence kernel (S <= 16, dh in 32/64/96/128)")
+    if CHECK_BOUNDS:
+        _bounds("attn_pair_fwd_spec", ("qkv", qkv, B * S, 3 * H * dh, ld_qkv), ("z", z, B * S, H * dh, ld_z),
+                ("lse", lse, 1, B * H * S, B * H * S))
+    _check(lib().iit_attn_mfma_fwd_spec(_p(qkv), _p(z), _p(lse), B, S, H, dh, ld_qkv, ld_z, scale, int(causal),
+                                        pair_seqs, spec_ptr, _stream()), "attn_mfma_fwd_spec")
+
+
+def attn_bwd_spec(qkv, dz, lse, dqkv, B, S, H, dh, ld_qkv, ld_dz, scale, causal, spec_ptr):
+    """The base rows' attention backward with the spliced elements of ``dz`` zeroed in the kernel."""
+    if CHECK_BOUNDS:
+        _bounds("attn_bwd_spec", ("qkv", qkv, B * S, 3 * H * dh, ld_qkv), ("dz", dz, B * S, H * dh, ld_dz),
+                ("dqkv", dqkv, B * S, 3 * H * dh, ld_qkv))
+    _check(lib().iit_attn_mfma_bwd_spec(_p(qkv), _p(dz), _p(lse), _p(dqkv), B, S, H, dh, ld_qkv, ld_dz, scale,
+                                        int(causal), spec_ptr, _stream()), "attn_mfma_bwd_spec")
 
 
 def attn_small_bwd(qkv, dz, lse, dqkv, head_mask, B, S, H, dh, ld_qkv, ld_dz, scale, causal):

@@ -1292,6 +1292,39 @@ class AttnPairFn(AttnFn):
         return (g[0], None, None, None, None, None)
 
 
+class AttnPairSpecFn(Function):
+    """Paired attention with a general interchange splice of ``hook_z`` (any patch-spec index over the base rows'
+    ``[B, S, H, dh]`` z: positions, head lists, feature ranges) applied in the attention kernel's store -- the source
+    rows' selected elements are written into the base rows -- and the gradient mask in its backward (SURVEY K04 /
+    K10: the z-epilogue patch point with per-head and per-position masks)."""
+
+    @staticmethod
+    def forward(ctx, qkv, causal, scale, spec, qkv_full, box):
+        ctx.set_materialize_grads(False)
+        B = qkv.shape[0]
+        B2, S, _, H, dh = qkv_full.shape
+        z = torch.empty(B2, S, H, dh, dtype=BF16, device=qkv.device)
+        lse = torch.empty(B2 * H * S, dtype=F32, device=qkv.device)
+        K.attn_pair_fwd_spec(qkv_full, z, lse, B2, S, H, dh, 3 * H * dh, H * dh, scale, causal, B, spec.ptr)
+        ctx.save_for_backward(qkv_full[:B], lse[:B * H * S])
+        ctx.cfg = (spec, causal, scale)
+        box.append(z)
+        return z[:B]
+
+    @staticmethod
+    def backward(ctx, dz):
+        if dz is None:
+            return None, None, None, None, None, None
+        qkv, lse = ctx.saved_tensors
+        spec, causal, scale = ctx.cfg
+        B, S, _, H, dh = qkv.shape
+        qkv = qkv.contiguous()
+        dz = dz.to(BF16).contiguous()
+        dqkv = torch.empty_like(qkv)
+        K.attn_bwd_spec(qkv, dz, lse, dqkv, B, S, H, dh, 3 * H * dh, H * dh, scale, causal, spec.ptr)
+        return dqkv, None, None, None, None, None
+
+
 class LinearPairFn(LinearFn):
     """bf16 out or fp32 ``resid + xW + b`` out (``resid_full`` paired with the input rows)."""
 
@@ -1621,6 +1654,21 @@ class HipOps(TorchOps):
         """Attention over paired rows; ``heads``: the base rows of these heads take the source rows' z."""
         out, full = _one(AttnPairFn, p.base, causal, 1.0 / attn_scale, K.heads_to_mask(heads) if heads else 0,
                          p.full)
+        return Paired(out, full)
+
+    def pair_attention_spliced(self, p: Paired, causal: bool, attn_scale: float, index) -> Optional[Paired]:
+        """Attention over paired rows with ``hook_z[index]`` of the base rows taken from the source rows inside the
+        kernel (``AttnPairSpecFn``); None when the patch-spec table cannot express ``index``
+        (``IIT_ATTN_SPLICE=0`` disables: the caller splices with a separate pass)."""
+        from .splice import patch_spec
+        if os.environ.get("IIT_ATTN_SPLICE", "1") == "0":
+            return None
+        B2, S, _, H, dh = p.full.shape
+        B = p.base.shape[0]
+        spec = patch_spec(index, (B, S, H, dh))
+        if spec is None or [d[0] for d in spec.dims] != [B, S, H, dh]:
+            return None
+        out, full = _one(AttnPairSpecFn, p.base, causal, 1.0 / attn_scale, spec, p.full)
         return Paired(out, full)
 
     def attention_dual(self, q, causal: bool, attn_scale: float) -> torch.Tensor:

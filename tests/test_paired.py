@@ -34,6 +34,8 @@ SITES = [
     {"blocks.1.attn.hook_z": [Ix[:, -1, :2, :]]},                             # causal graph: last position, heads
     {"blocks.2.mlp.hook_post": [Ix[2:5]]},                                    # batch subset: (base | source) axis
     {"blocks.2.attn.hook_z": [Ix[:, :, [0, 3]]]},                             # two heads (mirrored in-kernel)
+    {"blocks.1.attn.hook_z": [Ix[:, :, :, :20]]},                             # feature range (partial 16-B chunks)
+    {"blocks.2.attn.hook_z": [Ix[3:9, 5]]},                                   # batch subset x one position
 ]
 
 
@@ -206,3 +208,24 @@ def test_paired_with_staged_backward_cuts():
     assert set(got) == set(ref)
     for k in ref:
         assert torch.allclose(got[k], ref[k], rtol=1e-3, atol=1e-5), k
+
+
+@pytest.mark.parametrize("index", [Ix[:, [3, 7]], Ix[:, -1, :2, :], Ix[:, :, :, :20], Ix[3:9, 5]],
+                         ids=["positions", "last_pos_heads", "features", "batch_pos"])
+def test_paired_hook_z_spec_splice_runs_in_the_attention_kernel(monkeypatch, index):
+    """Non-head ``hook_z`` splices of the paired forward are applied in the attention kernel's store (K04 / K10:
+    per-position and per-feature patch points), not by the separate patch-spec pass."""
+    from iit_amd.ops import hip_ops
+
+    def no_pass(self, p, ix):
+        raise AssertionError("separate splice pass used for a hook_z site")
+
+    monkeypatch.setattr(hip_ops.HipOps, "pair_splice", no_pass)
+    m = _model()
+    base = torch.randint(0, V, (B, S), device="cuda")
+    src = torch.randint(0, V, (B, S), device="cuda")
+    res = m.run_paired(base, src, {"blocks.1.attn.hook_z": [index]}, logits="last")
+    assert res is not None
+    out, cache = res
+    ref, _ = _unpaired(m, base, src, {"blocks.1.attn.hook_z": [index]}, "last")
+    assert torch.allclose(out.float(), ref.float(), rtol=2e-2, atol=2e-2)

@@ -129,8 +129,9 @@ def _splice_ops_during(fn):
 @pytest.mark.gpu
 def test_causal_graph_step_has_no_index_put_splice():
     """The causal-graph correspondence splices token positions of hook_embed, last-position head halves of hook_z
-    and MLP neurons (tasks/causal_graph make_causal_graph_corr): on the GPU every site runs the patch-spec kernel,
-    so a whole Strict-IIT step dispatches no splice index_put, while the fused kernel does launch."""
+    and MLP neurons (tasks/causal_graph make_causal_graph_corr): on the GPU every site runs the patch-spec kernel or
+    (hook_z of the paired forward) the attention kernel's in-store splice, so a whole Strict-IIT step dispatches no
+    splice index_put, while a fused kernel does launch."""
     from iit_amd.data.iit_dataset import IITDataset
     from iit_amd.models.transformer import HookedTransformer
     from iit_amd.ops import hip_kernels as K
@@ -147,8 +148,10 @@ def test_causal_graph_step_has_no_index_put_splice():
     opt = pair.make_optimizer(1e-3)
     base, abl = next(iter(train.make_loader(64, 0)))
     launches = []
-    orig = K.splice
+    orig, orig_attn = K.splice, K.attn_pair_fwd_spec
     K.splice = lambda *a, **k: (launches.append(1), orig(*a, **k))[1]
+    # hook_z sites of the paired forward splice inside the attention kernel's store (also a fused launch)
+    K.attn_pair_fwd_spec = lambda *a, **k: (launches.append(2), orig_attn(*a, **k))[1]
     try:
         for node in list(pair.corr.keys()):
             pair.sample_hl_name = lambda node=node: node
@@ -156,6 +159,6 @@ def test_causal_graph_step_has_no_index_put_splice():
             launches.clear()
             bad = _splice_ops_during(lambda: pair.run_train_step(base, abl, pair.loss_fn, opt))
             assert not bad, (node, bad)
-            assert launches, node  # the LL splice ran on the fused kernel
+            assert launches, node  # the LL splice ran on a fused kernel
     finally:
-        K.splice = orig
+        K.splice, K.attn_pair_fwd_spec = orig, orig_attn
