@@ -141,6 +141,11 @@ IIT_EXPORT int iit_gemm_dual_ok(const void* wA, const void* wB, const void* wC, 
   return wg > 0 && wg < (1L << 31) ? 1 : 0;
 }
 
+// M-tiles per group of the XCD-local tile order for both problems of every later dual launch (0 = the body's default
+// of 8; IIT_GEMM_DUAL_GROUP_M, the tile-order experiment of the dual kernels)
+static int g_dual_group_m = 0;
+IIT_EXPORT void iit_gemm_dual_set_group_m(int gm) { g_dual_group_m = gm; }
+
 IIT_EXPORT int iit_gemm_dual(const void* wA, const void* wB, void* wC, long wlda, long wldb, long wldc, int wM, int wN,
                              int wK, int wepi, int wtile, int wsplits, float* ws, int* counters, const void* xA,
                              const void* xB, void* xC, void* xC2, long xlda, long xldb, long xldc, long xldc2, int xM,
@@ -164,6 +169,7 @@ IIT_EXPORT int iit_gemm_dual(const void* wA, const void* wB, void* wC, long wlda
   x.lda = xlda; x.ldb = xldb; x.ldc = xldc; x.ldc2 = xldc2;
   x.M = xM; x.N = xN; x.K = xK; x.k_per_split = xK;
   x.csum = xepi == E_DGELU ? csum : nullptr;
+  w.group_m = x.group_m = g_dual_group_m;
   hipStream_t s = (hipStream_t)stream;
   if (wepi == E_F32_STORE && xepi == E_BF16) return (int)pick_w<E_F32_STORE, E_BF16>(w, x, wsplits, wtile, xtile, s);
   if (wepi == E_F32_STORE && xepi == E_DGELU) return (int)pick_w<E_F32_STORE, E_DGELU>(w, x, wsplits, wtile, xtile, s);

@@ -102,3 +102,60 @@ IIT_EXPORT int iit_splice(const void* act, const void* src, void* out, long n, c
 #undef SPL
   return hipGetLastError();
 }
+
+// Sparse paired splice (the paired forward's ``mlp.hook_post`` sites, iit_amd/ops/hip_ops.py MLPInPairFn): the
+// activation holds T base rows followed by T source rows ([2T][ld], rows = the spec's flattened leading three
+// dimensions); one thread per SELECTED element -- the work is the size of the index, not of the activation:
+//   MODE 0  act[row][col] = act[row + T][col]   (forward: the source value into the base row, in place, right after
+//                                                the producing GEMM wrote both halves)
+//   MODE 1  act[row][col] = 0                   (backward: the spliced elements' gradient, in the producer's dpre)
+// ``cnt[d]`` = number of selected coordinates of dimension d; thread i is decoded mixed-radix over them.
+__device__ __forceinline__ int range_coord(const SpliceSpec& sp, int d, int k) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    if (r >= sp.nr[d]) break;
+    const int len = sp.hi[d][r] - sp.lo[d][r];
+    if (k < len) return sp.lo[d][r] + k;
+    k -= len;
+  }
+  return sp.lo[d][0];
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void sparse_pair_kernel(__bf16* __restrict__ act, long T, long ld, SpliceSpec sp,
+                                                          long total, int n1, int n2, int n3) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  long q = i;
+  const int k3 = (int)(q % n3); q /= n3;
+  const int k2 = (int)(q % n2); q /= n2;
+  const int k1 = (int)(q % n1);
+  const int k0 = (int)(q / n1);
+  const int c0 = range_coord(sp, 0, k0), c1 = range_coord(sp, 1, k1), c2 = range_coord(sp, 2, k2);
+  const int c3 = range_coord(sp, 3, k3);
+  const long row = ((long)c0 * sp.shape[1] + c1) * sp.shape[2] + c2;
+  if (MODE == 0) act[row * ld + c3] = act[(row + T) * ld + c3];
+  else act[row * ld + c3] = f2bf(0.f);
+}
+
+IIT_EXPORT int iit_sparse_pair(void* act, long T, long ld, const void* spec, int mode, void* stream) {
+  const SpliceSpec sp = *(const SpliceSpec*)spec;
+  long cnt[4];
+  long total = 1;
+  for (int d = 0; d < 4; ++d) {
+    cnt[d] = 0;
+    for (int r = 0; r < sp.nr[d]; ++r) cnt[d] += sp.hi[d][r] - sp.lo[d][r];
+    total *= cnt[d];
+  }
+  if ((long)sp.shape[0] * sp.shape[1] * sp.shape[2] != T) return (int)hipErrorInvalidValue;
+  if (total == 0) return 0;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == 0)
+    hipLaunchKernelGGL(sparse_pair_kernel<0>, grid, dim3(256), 0, s, (__bf16*)act, T, ld, sp, total, (int)cnt[1],
+                       (int)cnt[2], (int)cnt[3]);
+  else
+    hipLaunchKernelGGL(sparse_pair_kernel<1>, grid, dim3(256), 0, s, (__bf16*)act, T, ld, sp, total, (int)cnt[1],
+                       (int)cnt[2], (int)cnt[3]);
+  return hipGetLastError();
+}

@@ -507,9 +507,13 @@ class TransformerBlock(nn.Module):
             resid2 = resid_mid
         else:
             x, resid2 = ops.pair_layer_norm_fork(resid_mid, self.ln2.w, self.ln2.b, self.ln2.eps)
-            _, post = ops.pair_mlp_in(x, mlp.W_in, mlp.b_in, erf=erf)
-            for ix in ps:
-                post = ops.pair_splice(post, ix)
+            done = ops.pair_mlp_in(x, mlp.W_in, mlp.b_in, erf=erf, index=ps[0]) if len(ps) == 1 else None
+            if done is not None:  # the splice inside the producing op (sparse copy + masked dpre)
+                _, post = done
+            else:
+                _, post = ops.pair_mlp_in(x, mlp.W_in, mlp.b_in, erf=erf)
+                for ix in ps:
+                    post = ops.pair_splice(post, ix)
         captures[pname] = post.src
         if pname == stop_after:
             return ops.mlp_out_residual(post.base, mlp.W_out, mlp.b_out, resid2.base), False

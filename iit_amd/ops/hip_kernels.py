@@ -77,6 +77,8 @@ _SIGS = {
     "iit_swiglu_fwd": [c_void_p, c_void_p, c_void_p, c_long, c_void_p],
     "iit_swiglu_bwd": [c_void_p] * 5 + [c_long, c_void_p],
     "iit_swiglu_splice_fwd": [c_void_p] * 4 + [c_long, c_void_p, c_void_p],
+    "iit_sparse_pair": [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p],
+    "iit_gemm_dual_set_group_m": [c_int],
     "iit_swiglu_splice_bwd": [c_void_p] * 5 + [c_long, c_void_p, c_void_p],
     "iit_flash_fwd": [c_void_p] * 3 + [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ull] + [c_int] * 5
                      + [c_float, c_int, c_void_p],
@@ -104,9 +106,17 @@ def lib():
             fn.argtypes = argtypes
             fn.restype = c_int
         _LIB = L
-        gm = os.environ.get("IIT_GEMM_GROUP_M")  # XCD-local tile-order group height of the LDS-DMA GEMM (experiment)
+        # XCD-local tile-order group height of the single-problem LDS-DMA launches: 4 M-tiles per column group
+        # measured 0.2-0.3 % faster than 8 on the headline step over two alternating rounds on one box (16 slower;
+        # profiles/launch_knobs_r4s2.txt); IIT_GEMM_GROUP_M overrides
+        gm = os.environ.get("IIT_GEMM_GROUP_M", "4")
         if gm:
             L.iit_gemm_glds_set_group_m(int(gm))
+        # the same for the dual dX + dW launches: 2 measured 0.2-0.4 % faster than the body's 8 over two alternating
+        # rounds (4 in between, 16 slower; profiles/launch_knobs_r4s2.txt); IIT_GEMM_DUAL_GROUP_M overrides
+        dgm = os.environ.get("IIT_GEMM_DUAL_GROUP_M", "2")
+        if dgm:
+            L.iit_gemm_dual_set_group_m(int(dgm))
     return _LIB
 
 
@@ -584,6 +594,14 @@ def rotary(x, out, cos, sin, rd: int, offset: int, adjacent: bool, inverse: bool
 
 def swiglu_fwd(gate, up, post):
     _check(lib().iit_swiglu_fwd(_p(gate), _p(up), _p(post), gate.numel(), _stream()), "swiglu_fwd")
+
+
+def sparse_pair(act, T: int, ld: int, spec_ptr, mode: int) -> None:
+    """Sparse paired splice over a [2T][ld] bf16 activation (csrc/splice.hip): mode 0 copies the selected elements of
+    the source half into the base half in place, mode 1 zeroes them (one thread per selected element)."""
+    if CHECK_BOUNDS:
+        _bounds("sparse_pair", ("act", act, 2 * T if mode == 0 else T, ld, ld))
+    _check(lib().iit_sparse_pair(_p(act), T, ld, spec_ptr, int(mode), _stream()), "sparse_pair")
 
 
 def swiglu_splice_fwd(gate, up, post, src, spec_ptr):

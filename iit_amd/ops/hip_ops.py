@@ -967,6 +967,9 @@ class MLPInFn(Function):
         if gpost is not None:
             dpre = torch.empty(T, dm, dtype=BF16, device=x2.device)
             K.dgelu(gpost.to(BF16).contiguous().view(T, dm), pre, dpre, erf=ctx.erf)
+            zs = getattr(ctx, "zero_spec", None)
+            if zs is not None:  # MLPInPairFn's in-op splice: the spliced post elements carry no gradient
+                K.sparse_pair(dpre, T, dm, zs.ptr, 1)
             if gpre is not None:
                 dpre = (dpre.float() + gpre.float().reshape(T, dm)).to(BF16)
         else:
@@ -1361,10 +1364,17 @@ class LinearPairFn(LinearFn):
 
 
 class MLPInPairFn(MLPInFn):
+    """Paired W_in GEMM (+ gelu epilogue) over base and source rows.  ``spec`` (a PatchSpec over the base rows'
+    ``mlp.hook_post`` [B, S, d_mlp], optional): the interchange splice of that site inside this op -- right after the
+    GEMM the selected elements of the source half are copied into the base half in place (one thread per selected
+    element, not a pass over the activation), and the backward zeroes the same elements of its dpre (the spliced
+    values are constants).  ``pre`` keeps the base rows' own values, which the masked dgelu never reads."""
+
     @staticmethod
-    def forward(ctx, x, W_in, b_in, w, erf, x_full, box):
+    def forward(ctx, x, W_in, b_in, w, erf, x_full, spec, box):
         ctx.set_materialize_grads(False)
         ctx.erf = erf
+        ctx.zero_spec = spec
         B = x.shape[0]
         lead = x.shape[:-1]
         d = x.shape[-1]
@@ -1376,6 +1386,8 @@ class MLPInPairFn(MLPInFn):
         pre = torch.empty(T2, dm, dtype=BF16, device=x.device)
         gemm(x2, w, post, C2=pre, M=T2, N=dm, K=d, lda=d, ldb=dm, ldc=dm, ldc2=dm, mode=K.MODE_BKM,
              epi=K.EPI_GELU_ERF if erf else K.EPI_GELU, bias0=b_in)
+        if spec is not None:
+            K.sparse_pair(post, T, dm, spec.ptr, 0)
         ctx.save_for_backward(x2[:T], pre[:T])
         ctx.params = (W_in, b_in)
         ctx.w = w
@@ -1386,7 +1398,7 @@ class MLPInPairFn(MLPInFn):
 
     @staticmethod
     def backward(ctx, gpre, gpost):
-        return MLPInFn.backward(ctx, gpre, gpost) + (None, None)
+        return MLPInFn.backward(ctx, gpre, gpost) + (None, None, None)
 
 
 class MLPOutGeluPairFn(MLPOutGeluFn):
@@ -1690,8 +1702,18 @@ class HipOps(TorchOps):
                          resid.base, "resid", z.full.reshape(B2, S, H * dh), resid.full.float().contiguous())
         return Paired(out, full)
 
-    def pair_mlp_in(self, x: Paired, W_in, b_in, erf: bool = False):
-        (pre, post), (pf, qf) = _one(MLPInPairFn, x.base, W_in, b_in, self._L(W_in)["in"], erf, x.full)
+    def pair_mlp_in(self, x: Paired, W_in, b_in, erf: bool = False, index=None):
+        """Paired W_in + gelu.  ``index`` (optional): an ``mlp.hook_post`` splice applied inside the op
+        (``MLPInPairFn``); returns None when the patch-spec table cannot express it (``IIT_MLP_SPLICE=0``
+        disables) -- the caller then splices with a separate pass."""
+        spec = None
+        if index is not None:
+            from .splice import patch_spec
+            B, S = x.base.shape[0], x.base.shape[1]
+            spec = patch_spec(index, (B, S, W_in.shape[1])) if os.environ.get("IIT_MLP_SPLICE", "1") != "0" else None
+            if spec is None:
+                return None
+        (pre, post), (pf, qf) = _one(MLPInPairFn, x.base, W_in, b_in, self._L(W_in)["in"], erf, x.full, spec)
         return Paired(pre, pf), Paired(post, qf)
 
     def pair_mlp_out_residual(self, post: Paired, W_out, b_out, resid: Paired) -> Paired:

@@ -229,3 +229,37 @@ def test_paired_hook_z_spec_splice_runs_in_the_attention_kernel(monkeypatch, ind
     out, cache = res
     ref, _ = _unpaired(m, base, src, {"blocks.1.attn.hook_z": [index]}, "last")
     assert torch.allclose(out.float(), ref.float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("index", [Ix[:, :, :64], Ix[:, -1, :128], Ix[2:5], Ix[:, [3, 7], 100:130]],
+                         ids=["neurons", "last_pos_neurons", "batch", "pos_neurons"])
+def test_paired_mlp_post_splice_runs_inside_the_mlp_op(monkeypatch, index):
+    """``mlp.hook_post`` splices of the paired forward run inside the W_in op (sparse copy of the selected source
+    elements into the base rows, masked dpre in its backward), not by the separate patch-spec pass; outputs and
+    gradients equal the two-forward path."""
+    from iit_amd.ops import hip_ops
+
+    def no_pass(self, p, ix):
+        raise AssertionError("separate splice pass used for an mlp.hook_post site")
+
+    m = _model()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    base = torch.randint(0, V, (B, S), device="cuda", generator=g)
+    src = torch.randint(0, V, (B, S), device="cuda", generator=g)
+    w = torch.randn(B, V, device="cuda", generator=g)
+    sites = {"blocks.2.mlp.hook_post": [index]}
+    m.zero_grad(set_to_none=True)
+    ref, _ = _unpaired(m, base, src, sites, "last")
+    (ref.float() * w).sum().backward()
+    g_ref = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+    monkeypatch.setattr(hip_ops.HipOps, "pair_splice", no_pass)
+    m.zero_grad(set_to_none=True)
+    res = m.run_paired(base, src, sites, logits="last")
+    assert res is not None
+    out, _ = res
+    (out.float() * w).sum().backward()
+    assert torch.allclose(out.float(), ref.float(), rtol=2e-2, atol=2e-2)
+    for k, gr in g_ref.items():
+        gp = m.get_parameter(k).grad
+        scale = g_ref[k[:-3] + "b_Q"].norm() if k.endswith("b_K") else gr.norm()
+        assert float((gp - gr).norm() / (scale + 1e-12)) < 2e-2, k

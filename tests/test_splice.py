@@ -148,10 +148,12 @@ def test_causal_graph_step_has_no_index_put_splice():
     opt = pair.make_optimizer(1e-3)
     base, abl = next(iter(train.make_loader(64, 0)))
     launches = []
-    orig, orig_attn = K.splice, K.attn_pair_fwd_spec
+    orig, orig_attn, orig_sparse = K.splice, K.attn_pair_fwd_spec, K.sparse_pair
     K.splice = lambda *a, **k: (launches.append(1), orig(*a, **k))[1]
-    # hook_z sites of the paired forward splice inside the attention kernel's store (also a fused launch)
+    # hook_z sites of the paired forward splice inside the attention kernel's store, mlp.hook_post sites inside the
+    # W_in op (sparse copy): fused launches too
     K.attn_pair_fwd_spec = lambda *a, **k: (launches.append(2), orig_attn(*a, **k))[1]
+    K.sparse_pair = lambda *a, **k: (launches.append(3), orig_sparse(*a, **k))[1]
     try:
         for node in list(pair.corr.keys()):
             pair.sample_hl_name = lambda node=node: node
@@ -161,4 +163,4 @@ def test_causal_graph_step_has_no_index_put_splice():
             assert not bad, (node, bad)
             assert launches, node  # the LL splice ran on a fused kernel
     finally:
-        K.splice, K.attn_pair_fwd_spec = orig, orig_attn
+        K.splice, K.attn_pair_fwd_spec, K.sparse_pair = orig, orig_attn, orig_sparse
