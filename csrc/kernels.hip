@@ -962,7 +962,16 @@ IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, void* mirro
   const Span* ssp = sq_spans ? (const Span*)sq_spans : sp;
   hipLaunchKernelGGL(sumsq_span_kernel, dim3(norm ? nparts : 1), dim3(256), 0, s, g, ssp,
                      sq_spans ? n_sq_spans : nspans, part, (int)norm, step, gsq);
-  const int blocks = min(nspans, 4096);
+  // grid: up to 65536 workgroups -- one per span (<= 1024 float4 groups each, ~30 k for GPT-2-small), so the
+  // hardware dispatcher balances the ragged spans; a fixed 4096-workgroup grid striding over ~7 spans each measured
+  // 0.12 ms per headline step slower (15.851 vs 15.734 ms, two rounds, profiles/launch_knobs_r4s2.txt).  The cap
+  // bounds the per-workgroup prologue (the clip coefficient from the norm partials) on 8 B-parameter arenas.
+  // IIT_ADAM_MAX_BLOCKS overrides.
+  static const int max_blocks = [] {
+    const char* e = getenv("IIT_ADAM_MAX_BLOCKS");
+    return e ? atoi(e) : 65536;
+  }();
+  const int blocks = min(nspans, max_blocks);
   static const int nt = [] {
     const char* e = getenv("IIT_ADAM_NT");
     return e ? atoi(e) : 1;
@@ -1035,7 +1044,8 @@ IIT_EXPORT int iit_sumsq_spans(const float* g, const void* spans, int nspans, fl
 IIT_EXPORT int iit_adam_spans(float* p, const float* g, float* m, float* v, void* mirror, const void* spans,
                               int nspans, const float* total, float clip, float lr, float b1, float b2, float eps,
                               float wd, const float* hyper, int* step, int* skipped, void* stream) {
-  const int blocks = max(1, min(nspans, 4096));
+  // one workgroup per span up to 65536, as the replicated update (iit_adam_flat)
+  const int blocks = max(1, min(nspans, 65536));
   // (U = 2: two float4 groups in flight per thread and stream, as the replicated update; profiles/adam_microbench_r3s2.txt)
   hipLaunchKernelGGL((adam_span_kernel<true, 2>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
                      (__bf16*)mirror, (const Span*)spans, nspans, total, 1, clip, lr, b1, b2, eps, wd, hyper, step,

@@ -363,6 +363,11 @@ def kl_rows(a, b):
     return out
 
 
+# Adam span length (float4 groups per span record): the kernel runs one workgroup per span (IIT_ADAM_MAX_BLOCKS
+# default, csrc/kernels.hip), so this is also its per-workgroup work unit; IIT_ADAM_SPAN4 overrides
+_ADAM_SPAN4 = int(os.environ.get("IIT_ADAM_SPAN4", "1024"))
+
+
 def sumsq_2d(c, ldc: int, M: int, N: int, gsq) -> None:
     """gsq[slot] += sum of squares of the fp32 [M][N] matrix ``c`` (row stride ``ldc``)."""
     if CHECK_BOUNDS:
@@ -719,7 +724,7 @@ def adam_step(flat, exp_avg, exp_avg_sq, step_dev, *, lr, b1, b2, eps, wd, clip_
     part = getattr(flat, "_norm_parts", None)
     if part is None or part.numel() < nparts:
         part = flat._norm_parts = torch.zeros(nparts, dtype=torch.float32, device=flat.data.device)
-    spans, nspans = flat.span_table(lib().iit_adam_span_size())
+    spans, nspans = flat.span_table(lib().iit_adam_span_size(), max_len4=_ADAM_SPAN4)
     # fused norm: the weight gradients a GEMM stored this step already added their sums of squares into gsq
     sq_spans, n_sq, gsq = flat.norm_spans(lib().iit_adam_span_size())
     _check(lib().iit_adam_flat(_p(flat.data), _p(flat.grad), _p(exp_avg), _p(exp_avg_sq), _p(flat.shadow),

@@ -30,3 +30,9 @@ rc=$?; echo "pmc rc=$rc"
 f=$(find $O/pmc -name "*counter_collection.csv" | head -n 1)
 python3 scripts/pmc_step_summary.py "$f" 4 > $O/pmc_step_summary.txt; tail -3 $O/pmc_step_summary.txt
 rm -rf $O/pmc
+export IIT_REHEARSE_ONE_GPU=1 IIT_DIST_BACKEND=gloo
+IIT_ZERO=1 step dp2_zero 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 4 --warmup 3
+grep -E '^\{' $O/dp2_zero.log | cut -c1-200
+unset IIT_REHEARSE_ONE_GPU IIT_DIST_BACKEND
+IIT_ZERO=1 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29535 IIT_DP_FORCE_REDUCER=1 step dp1_zero 300 python3 -u bench.py --steps 30 --warmup 5
+grep -E '^\{' $O/dp1_zero.log | cut -c1-200
