@@ -50,7 +50,7 @@ __device__ __forceinline__ i16x4 tr_block(const __bf16* img, int g, int lane_in_
 // rows.  Heads in ``pair_mask`` are spliced from source into base: the base wave of such a head computes nothing (its
 // z is the source's, its gradient zero) and the source wave stores its z into both rows.  ``z2`` (nullable) receives
 // a second copy of every stored z row (a whole-layer splice whose base z is the source z).
-template <int DH>
+template <int DH, bool SP>
 __global__ __launch_bounds__(256) void attn_mfma_fwd_kernel(const __bf16* __restrict__ qkv, __bf16* __restrict__ z,
                                                             float* __restrict__ lse, const __bf16* __restrict__ zsrc,
                                                             unsigned long long head_mask, int BH, int S, int H,
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void attn_mfma_fwd_kernel(const __bf16* __rest
     if (r < S) {
       const bf16x8 v = *(const bf16x8*)(Vs + r * LDSR + ch * 8);
       __bf16* zo = z + (row0 + r) * ld_z + h * DH + ch * 8;
-      if (use_sp && pair_seqs > 0) {
+      if (SP && use_sp && pair_seqs > 0) {
         // general patch spec over the base rows' z [pair_seqs][S][H][DH]: the source wave of (b, h) also stores the
         // selected elements of its row into the base row; the base wave stores only the unselected ones (disjoint
         // writes, no ordering between the two waves needed).  A partly selected 16-B chunk goes out element-wise.
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void attn_mfma_fwd_kernel(const __bf16* __rest
   }
 }
 
-template <int DH>
+template <int DH, bool SP>
 __global__ __launch_bounds__(256) void attn_mfma_bwd_kernel(const __bf16* __restrict__ qkv, const __bf16* __restrict__ dz,
                                                             const float* __restrict__ lse, __bf16* __restrict__ dqkv,
                                                             unsigned long long head_mask, int BH, int S, int H,
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void attn_mfma_bwd_kernel(const __bf16* __rest
     kf[s] = load8(qkv + off + HD, ok);
     vf[s] = load8(qkv + off + 2 * HD, ok);
     gf[s] = load8(dz + (row0 + c) * ld_dz + h * DH + 32 * s + 8 * g, ok);
-    if (use_sp && ok && in_ranges(sp, 0, b) && in_ranges(sp, 1, c) && in_ranges(sp, 2, h)) {
+    if (SP && use_sp && ok && in_ranges(sp, 0, b) && in_ranges(sp, 1, c) && in_ranges(sp, 2, h)) {
       // spliced elements of z are the source's (a constant): their gradient is zero
 #pragma unroll
       for (int e = 0; e < 8; ++e)
@@ -360,7 +360,8 @@ static int attn_fwd_launch(const void* qkv, void* z, float* lse, const void* zsr
   dim3 grid((BH + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
 #define AF(D)                                                                                                       \
-  hipLaunchKernelGGL(attn_mfma_fwd_kernel<D>, grid, block, 0, s, (const __bf16*)qkv, (__bf16*)z, lse,               \
+  hipLaunchKernelGGL((use_sp ? attn_mfma_fwd_kernel<D, true> : attn_mfma_fwd_kernel<D, false>), grid, block, 0, s,    \
+                     (const __bf16*)qkv, (__bf16*)z, lse,                                                           \
                      (const __bf16*)zsrc, head_mask, BH, S, H, ld_qkv, ld_z, ld_src, scale, causal, (__bf16*)z2,    \
                      pair_seqs, pair_mask, sp, use_sp)
   if (dh == 32) AF(32);
@@ -399,7 +400,8 @@ static int attn_bwd_launch(const void* qkv, const void* dz, const float* lse, vo
   dim3 grid((BH + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
 #define AB(D)                                                                                                       \
-  hipLaunchKernelGGL(attn_mfma_bwd_kernel<D>, grid, block, 0, s, (const __bf16*)qkv, (const __bf16*)dz, lse,        \
+  hipLaunchKernelGGL((use_sp ? attn_mfma_bwd_kernel<D, true> : attn_mfma_bwd_kernel<D, false>), grid, block, 0, s,    \
+                     (const __bf16*)qkv, (const __bf16*)dz, lse,                                                    \
                      (__bf16*)dqkv, head_mask, BH, S, H, ld_qkv, ld_dz, scale, causal, sp, use_sp)
   if (dh == 32) AB(32);
   else if (dh == 64) AB(64);

@@ -44,6 +44,32 @@ __global__ void embed_bwd_kernel(const long* __restrict__ tok, const float* __re
   for (int i = threadIdx.x; i < d; i += blockDim.x) atomicAdd(dWE + v * (long)d + i, g[(long)t * d + i]);
 }
 
+// Position-major form: block = (position s, 256-column slab, chunk of EB sequences); each thread walks its column
+// down the chunk's sequences at position s and adds runs of EQUAL tokens in a register, one atomic per run.  IIT
+// batches repeat template tokens at a position across the batch (IOI: every word but the names), so the atomics on
+// a contended row drop from B to B / EB per column; distinct tokens cost what the token-major kernel costs.
+constexpr int EB = 32;
+__global__ __launch_bounds__(256) void embed_bwd_pos_kernel(const long* __restrict__ tok, const float* __restrict__ g,
+                                                            float* __restrict__ dWE, int B, int S, int d) {
+  const int s = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x, b0 = blockIdx.z * EB;
+  if (c >= d) return;
+  long cur = -1;
+  float acc = 0.f;
+  for (int b = b0; b < min(B, b0 + EB); ++b) {
+    const long t = (long)b * S + s;
+    const long v = tok[t];
+    const float x = g[t * d + c];
+    if (v != cur) {
+      if (cur >= 0) atomicAdd(dWE + cur * (long)d + c, acc);
+      cur = v;
+      acc = x;
+    } else {
+      acc += x;
+    }
+  }
+  if (cur >= 0) atomicAdd(dWE + cur * (long)d + c, acc);
+}
+
 // dW_pos[s] += sum_b g[b, s].  Block = (position s, 256-column slab); 4 waves split the batch, LDS combine.
 __global__ __launch_bounds__(256) void pos_bwd_kernel(const float* __restrict__ g, float* __restrict__ dWpos, int B,
                                                       int S, int d) {
@@ -77,7 +103,15 @@ IIT_EXPORT int iit_embed_pos_bwd(const long* tok, const float* g, float* dWE, fl
   hipStream_t st = (hipStream_t)stream;
   // (an LDS-combining variant -- 64-position chunks adding equal tokens' rows before one global atomic per distinct
   // token -- measured 54 us against this kernel's 30 us on the IOI batch: fewer, longer blocks; not kept)
-  if (dWE) hipLaunchKernelGGL(embed_bwd_kernel, dim3(B * S), dim3(256), 0, st, tok, g, dWE, B * S, d);
+  static const bool pos_major = [] {
+    const char* e = getenv("IIT_EMBED_BWD_POS");
+    return !(e && e[0] == '0');
+  }();
+  if (dWE && pos_major)
+    hipLaunchKernelGGL(embed_bwd_pos_kernel, dim3(S, (d + 255) / 256, (B + EB - 1) / EB), dim3(256), 0, st, tok, g,
+                       dWE, B, S, d);
+  else if (dWE)
+    hipLaunchKernelGGL(embed_bwd_kernel, dim3(B * S), dim3(256), 0, st, tok, g, dWE, B * S, d);
   if (dWpos) {
     if (d % 4 == 0 && (((uintptr_t)g) & 15) == 0)
       hipLaunchKernelGGL(pos_bwd_kernel, dim3(S, (d + 255) / 256), dim3(256), 0, st, g, dWpos, B, S, d);
@@ -978,7 +1012,9 @@ IIT_EXPORT int iit_adam_flat(float* p, float* g, float* m, float* v, void* mirro
   }();
   static const int unroll = [] {
     const char* e = getenv("IIT_ADAM_UNROLL");
-    return e ? atoi(e) : 2;  // profiles/adam_microbench_r3s2.txt: 2 and 4 are ~4-5 % faster than 1
+    // 4: with one workgroup per 1024-group span each thread then streams its span share in ONE pass (0.4 % on the
+    // headline step over 2, profiles/launch_knobs_r4s2.txt; profiles/adam_microbench_r3s2.txt: 2 and 4 beat 1)
+    return e ? atoi(e) : 4;
   }();
 #define ADAM_LAUNCH(NT_, U_)                                                                                        \
   hipLaunchKernelGGL((adam_span_kernel<NT_, U_>), dim3(blocks), dim3(256), 0, s, p, g, m, v, (__bf16*)mirror, sp, \

@@ -383,3 +383,20 @@ def test_embed_bwd_repeated_tokens(K, T, d, vocab):
     torch.cuda.synchronize()
     torch.testing.assert_close(dWE, ref_E, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(dWpos, ref_pos, rtol=1e-5, atol=1e-4)
+
+
+def test_embed_bwd_template_batches(K):
+    """IOI-like batches (the same token at most positions across the batch, a few varied positions): the
+    position-major embedding backward (runs of equal tokens summed in registers) == index_add."""
+    torch.manual_seed(7)
+    B, S, d, vocab = 256, 16, 768, 50257
+    template = torch.randint(0, vocab, (S,), device=dev)
+    tok = template.repeat(B, 1)
+    for s in (2, 4, 9):
+        tok[:, s] = torch.randint(0, 40, (B,), device=dev)
+    g = torch.randn(B, S, d, device=dev)
+    dWE = torch.zeros(vocab, d, device=dev)
+    ref = torch.zeros(vocab, d, device=dev).index_add_(0, tok.reshape(-1), g.reshape(-1, d))
+    K.embed_pos_bwd(tok, g, dWE, None, B, S, d)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dWE, ref, rtol=1e-5, atol=1e-4)
