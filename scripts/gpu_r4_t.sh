@@ -30,7 +30,7 @@ rc=$?; echo "pmc rc=$rc"
 f=$(find $O/pmc -name "*counter_collection.csv" | head -n 1)
 python3 scripts/pmc_step_summary.py "$f" 4 > $O/pmc_step_summary.txt; tail -3 $O/pmc_step_summary.txt
 rm -rf $O/pmc
-export IIT_REHEARSE_ONE_GPU=1 IIT_DIST_BACKEND=gloo
+export IIT_REHEARSE_ONE_GPU=1 IIT_DIST_BACKEND=gloo  # (ZeRO-1 rehearsals)
 IIT_ZERO=1 step dp2_zero 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 4 --warmup 3
 grep -E '^\{' $O/dp2_zero.log | cut -c1-200
 unset IIT_REHEARSE_ONE_GPU IIT_DIST_BACKEND
