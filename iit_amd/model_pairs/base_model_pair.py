@@ -538,8 +538,8 @@ class BaseModelPair(ABC):
         or ``IIT_PRIME_GRAPHS=1|0``."""
         import os
         want = self.training_args.get("prime_graphs", None)
-        if want is None:  # opt-in until validated on hardware (scripts/time_to_iia.py sets IIT_PRIME_GRAPHS=1)
-            want = os.environ.get("IIT_PRIME_GRAPHS", "0") == "1"
+        if want is None:  # on by default (validated on MI355X: tests/test_eval_graphs_gpu.py, profiles/time_to_iia_r4.txt)
+            want = os.environ.get("IIT_PRIME_GRAPHS", "1") == "1"
         if not want:
             return
         step = self.train_step_fn(optimizer, loss_fn)
