@@ -1512,7 +1512,7 @@ __global__ __launch_bounds__(256) void zero_chunks_kernel(float* __restrict__ ba
 // copied at launch, and at graph capture): unlike a device range table no host->device copy is needed, so a zero
 // plan first built inside a HIP-graph capture is one node instead of a fill per range.  Block b zeroes chunk
 // b - cum[r] (ZR_CHUNK floats) of the range r with cum[r] <= b < cum[r + 1].
-#define ZR_MAX 64
+#define ZR_MAX 128  // 2.6 KB of kernel arguments (limit 4 KB): the GPT-2 arena's ~150-190 ranges in two launches, not three
 #define ZR_CHUNK 16384
 struct ZeroRanges {
   long start[ZR_MAX];

@@ -254,7 +254,7 @@ class FlatParams:
 
         Rows excluded by :meth:`restrict_rows` (embedding rows of tokens the data never contains) are never written
         by a backward over that data, so they stay zero without a memset (GPT-2's 50k x 768 ``W_E`` slot shrinks
-        to its ~100 live rows).  On the GPU the memset is one launch per 64 ranges with the ranges passed as kernel
+        to its ~100 live rows).  On the GPU the memset is one launch per 128 ranges with the ranges passed as kernel
         arguments: no device table, so a plan first needed inside a graph capture is still a single node.  Plans
         are cached per (claim set, restriction)."""
         if self._norm_covered:  # a backward ran without an optimizer step consuming its fused norm sums

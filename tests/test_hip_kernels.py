@@ -400,3 +400,23 @@ def test_embed_bwd_template_batches(K):
     K.embed_pos_bwd(tok, g, dWE, None, B, S, d)
     torch.cuda.synchronize()
     torch.testing.assert_close(dWE, ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("n_ranges", [1, 64, 128, 129, 300])
+def test_zero_ranges_many_ranges(K, n_ranges):
+    """zero_ranges (the gradient arena's memset, up to 128 ranges per launch as kernel arguments) zeroes exactly
+    the given disjoint ranges -- across launch boundaries and for ranges longer than one 16 K chunk -- and nothing
+    else."""
+    import numpy as np
+    g = torch.Generator().manual_seed(n_ranges)
+    lens = torch.randint(1, 40000, (n_ranges,), generator=g).numpy().astype(np.int64)
+    gaps = torch.randint(0, 3000, (n_ranges,), generator=g).numpy().astype(np.int64)
+    starts = np.cumsum(gaps + np.concatenate([[0], lens[:-1]])).astype(np.int64)
+    total = int(starts[-1] + lens[-1] + 100)
+    base = torch.randn(total, device=dev)
+    ref = base.clone()
+    for s, n in zip(starts.tolist(), lens.tolist()):
+        ref[s:s + n] = 0
+    K.zero_ranges(base, starts, lens)
+    torch.cuda.synchronize()
+    assert torch.equal(base, ref)
