@@ -1574,14 +1574,17 @@ __global__ __launch_bounds__(256) void kl_rows_kernel(const float* __restrict__ 
   for (int v = threadIdx.x; v < V; v += 256) {
     const float x = ar[v], p = br[v];
     s += x;
+    // a -inf logit (masked) adds nothing to the logsumexp: skipped, so it never meets m = -inf (exp(NaN))
     if (x > m) {
       e = e * __expf(m - x) + 1.f;
       m = x;
-    } else {
+    } else if (x != -INFINITY) {
       e += __expf(x - m);
     }
-    dba += p * x;
-    if (p != 0.f) dbl += p * __logf(x);
+    if (p != 0.f) {  // terms with b = 0 contribute 0 (also when a = -inf: no 0 * -inf)
+      dba += p * x;
+      dbl += p * __logf(x);
+    }
   }
   __shared__ float red[5][4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

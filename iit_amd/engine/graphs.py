@@ -149,6 +149,9 @@ class _TrainState:
                 self.pairs.append((flat.shadow, flat.shadow.clone()))
         else:
             self.pairs += [(p.data, p.data.clone()) for p in ll.parameters()]
+        # module buffers the priming steps mutate in training mode: BatchNorm running statistics and
+        # ``num_batches_tracked`` of the PVR ResNet (constant buffers -- causal masks -- are copied back unchanged)
+        self.pairs += [(b, b.clone()) for b in ll.buffers() if b is not None]
         self.opt = optimizer
         self.scalars = {}
         if optimizer is not None and hasattr(optimizer, "exp_avg"):  # FusedAdam / ShardedFusedAdam
@@ -416,8 +419,19 @@ class GraphedTrainStep:
         self.replays += 1
         return _clone_out(static_out)
 
+    def _graph_key(self, key, optimizer=None):
+        """Graph identity of a phase: the pair's phase key, the batch signature, the LL module's train / eval mode
+        (a graph captured in eval mode replays eval-mode BatchNorm / dropout) and the optimizer's row-restriction
+        version (a sharded step captures its span table)."""
+        module = self.pair._ll_module() if hasattr(self.pair, "_ll_module") else getattr(self.pair, "ll_model", None)
+        training = bool(getattr(module, "training", True))
+        opt = optimizer if optimizer is not None else self.optimizer
+        flat = getattr(opt, "flat", None)
+        rv = getattr(flat, "restrict_version", 0) if flat is not None else 0
+        return (key, self._sig, training, rv)
+
     def _run_phase(self, key, compute_loss, optimizer, step_fn):
-        full = (key, self._sig)
+        full = self._graph_key(key, optimizer)
         if not self.enabled or self._current_eager:
             return self._eager(compute_loss, optimizer, step_fn)
         if self.split:

@@ -552,8 +552,16 @@ class BaseModelPair(ABC):
             base, abl = next(iter(train_loader))
         finally:
             torch.set_rng_state(rng)
-        with step.stream_context():
-            n = step.prime_preserving(base, abl, loss_fn, optimizer)
+        # the phase graphs are captured in training mode (BatchNorm batch statistics, dropout), whatever mode an
+        # earlier evaluation left the module in; the previous mode is put back afterwards
+        module = self._ll_module()
+        was_training = module.training
+        module.train()
+        try:
+            with step.stream_context():
+                n = step.prime_preserving(base, abl, loss_fn, optimizer)
+        finally:
+            module.train(was_training)
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         from ..utils import tracing

@@ -159,7 +159,11 @@ class ShardedFusedAdam(FusedAdam):
         if gaps:
             skipped = [(loc + max(a, g0) - a, loc + min(b, g1) - a)
                        for a, b, loc in self.plan.live_pieces(()) for g0, g1 in gaps if g0 < b and g1 > a]
-            if any(bool(t[x:y].any()) for x, y in skipped for t in (self.exp_avg, self.exp_avg_sq)):
+            # the same guard as the replicated optimizer (FusedAdam._validate_restriction): the skipped rows' update
+            # is the identity only without weight decay and with zero gradient and zero moments there
+            wd = self.param_groups[0].get("weight_decay", 0.0) if getattr(self, "param_groups", None) else 0.0
+            if wd != 0 or any(bool(t[x:y].any()) for x, y in skipped
+                              for t in (self.exp_avg, self.exp_avg_sq, self.shard_grad)):
                 gaps = []
         spans = self.plan.spans(gaps=gaps)
         if getattr(self, "_spans", None) is not None:

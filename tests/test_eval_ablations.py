@@ -205,3 +205,27 @@ def test_kl_rows_kernel_matches_kl_div():
     got = kl_div_from_stats(pm, stats)
     want = kl_div(pm, hl, EVERYTHING)
     assert torch.allclose(got, want, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_kl_rows_kernel_masked_logits():
+    """A -inf (masked) logit -- including as a thread's first element, where the running max is still -inf --
+    adds nothing to the logsumexp (exp(-inf - -inf) made the whole row NaN).  With the target pmf zero
+    on the masked entries the KL equals the KL over the unmasked columns."""
+    from iit_amd.utils.eval_metrics import kl_div_from_stats, target_stats
+    torch.manual_seed(1)
+    dev = "cuda"
+    V = 4099
+    a = torch.randn(9, V, device=dev) * 3
+    hl = torch.randn(9, V, device=dev) * 4
+    masked = torch.zeros(V, dtype=torch.bool, device=dev)
+    masked[:300] = True  # every thread's first element of row 0's stream (threads 0..255) and more
+    masked[1000:1013] = True
+    a[:, masked] = -float("inf")
+    hl[:, masked] = -float("inf")  # target pmf exactly 0 there
+    stats = target_stats(hl)
+    got = kl_div_from_stats(a, stats)
+    keep = ~masked
+    want = kl_div(a[:, keep], hl[:, keep], EVERYTHING)
+    assert torch.isfinite(got).all()
+    assert torch.allclose(got, want, rtol=1e-4, atol=1e-5)

@@ -53,3 +53,46 @@ def test_train_state_snapshot_restores_in_place(fused):
         assert np.isclose(float(out[k]), float(ref[k]), rtol=1e-6, atol=1e-7), k
     for a, b in zip(pair.ll_model.parameters(), ref_pair.ll_model.parameters()):
         assert torch.allclose(a, b, atol=1e-7, rtol=1e-6)
+
+
+def test_train_state_restores_batchnorm_buffers():
+    """the PVR ResNet LL is graphed and primed; the priming steps run in training mode and move every
+    BatchNorm's running statistics and ``num_batches_tracked``.  The snapshot covers module buffers, so the
+    restore puts them back exactly (eval metrics of a primed run equal an unprimed one's)."""
+    from iit_amd.model_pairs import IITBehaviorModelPair
+    from iit_amd.tasks.task_loader import get_alignment, get_dataset
+    torch.manual_seed(0)
+    tr, te = get_dataset("mnist_pvr", {"train_size": 32, "test_size": 16, "device": "cpu"})
+    ll, hl, corr = get_alignment("mnist_pvr", {"input_shape": te.base_data.get_input_shape(), "device": "cpu"})
+    pair = IITBehaviorModelPair(ll_model=ll, hl_model=hl, corr=corr,
+                                training_args={"lr": 1e-3, "batch_size": 16, "early_stop": False,
+                                               "lr_scheduler": None})
+    opt = pair.make_optimizer(1e-3)
+    module = pair._ll_module()
+    bufs = [b for b in module.buffers()]
+    assert any(b.dtype == torch.long for b in bufs)  # num_batches_tracked
+    before = [b.clone() for b in bufs]
+    snap = _TrainState(pair, opt)
+    module.train()
+    for b in list(tr.make_loader(16, 0))[:2]:
+        pair.run_train_step(*b, pair.loss_fn, opt)
+    assert any(not torch.equal(a, b) for a, b in zip(bufs, before))
+    snap.restore()
+    assert all(torch.equal(a, b) for a, b in zip(module.buffers(), before))
+
+
+def test_graph_key_includes_module_mode():
+    """a phase graph captured in eval mode must not be replayed in training mode -- the graph key carries
+    the LL module's mode (and the optimizer's row-restriction version)."""
+    from iit_amd.engine.graphs import GraphedTrainStep
+    pair, _ = _pair(True)
+    opt = pair.make_optimizer(1e-3)
+    step = GraphedTrainStep(pair, opt, pair.loss_fn, enabled=False)
+    step._sig = ("sig",)
+    pair.ll_model.train()
+    k_train = step._graph_key("iit", opt)
+    pair.ll_model.eval()
+    k_eval = step._graph_key("iit", opt)
+    assert k_train != k_eval
+    pair.ll_model.train()
+    assert step._graph_key("iit", opt) == k_train
