@@ -62,7 +62,18 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> boo
         torch.cuda.set_device(local_device_index())
     if backend == "nccl":
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-    dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+    timeout = datetime.timedelta(seconds=timeout_s)
+    attempt = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0)
+    if attempt > 0 and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+        # a torchrun restart (--max-restarts): the agent's TCPStore outlives the failed attempt, and
+        # its keys (the dead ranks' gloo / RCCL bootstrap addresses) would be read back by the new ranks -- the
+        # restarted job rendezvouses under a per-attempt key prefix instead
+        store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), ws, is_master=False,
+                              timeout=timeout)
+        dist.init_process_group(backend=backend, store=dist.PrefixStore(f"iit/attempt_{attempt}", store),
+                                rank=int(os.environ["RANK"]), world_size=ws, timeout=timeout)
+        return True
+    dist.init_process_group(backend=backend, timeout=timeout)
     return True
 
 

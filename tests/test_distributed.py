@@ -435,3 +435,26 @@ def test_metric_reduction_weights_by_batch_counts(tmp_path):
         assert float(m["val/IIA"]) == pytest.approx(50.0)  # (1 + 1 + 0 + 0) / 4 x 100
         assert float(m["val/loss"]) == pytest.approx(5.5)  # (2 + 4 + 6 + 10) / 4
         assert torch.allclose(m["val/per_token_accuracy"].double(), torch.tensor([0.5, 0.5], dtype=torch.float64))
+
+
+def _torchrun(tmp, fault, extra=()):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--max-restarts", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dp_restart_worker.py"), str(tmp), str(fault), *extra]
+    tmp.mkdir(parents=True, exist_ok=True)
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=str(tmp))
+    assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-4000:])
+    return torch.load(tmp / "final.pt", weights_only=True)
+
+
+@pytest.mark.parametrize("extra", [(), ("zero",)])
+def test_dp2_rank_failure_restart_resumes(tmp_path, extra):
+    """SURVEY §5.3 / VERDICT r4 missing #4: rank 1 dies hard (os._exit) after the epoch-0 checkpoint; torchrun
+    (--max-restarts 1) restarts both ranks, which resume from their per-rank checkpoints (weights, optimizer state --
+    each rank's own ZeRO-1 shard --, every RNG) and finish with exactly the weights of an uninterrupted run."""
+    ref = _torchrun(tmp_path / "ref", 0, extra)
+    got = _torchrun(tmp_path / "fault", 1, extra)
+    assert ref["attempt"] == 0 and got["attempt"] == 1  # the fault run really restarted
+    for n, p in ref["params"].items():
+        assert torch.equal(got["params"][n], p), n
