@@ -124,9 +124,26 @@ static const int kTileBK[IIT_GLDS_TILES] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 
                                             64, 64, 64, 64, 64, 64, 64, 64, 64};
 
 // 1 when (shape, layout, epilogue, tile) is covered by the LDS-DMA kernel (caller falls back otherwise)
+// tile 40: the 256 x 256 8-phase kernel of gemm_8ph.hip; tiles 41 / 42: the 256 x 256 four-wave 32x32x16 kernel
+// of gemm_4w.hip with 64- / 32-deep K-tiles (2- / 4-slot LDS-DMA rings); no K split for any of them
+#define IIT_8PH_TILE 40
+#define IIT_4W_TILE 41
+#define IIT_4W32_TILE 42
+extern "C" int iit_gemm_8ph_ok(int M, int N, int K, int mode, int epi);
+extern "C" int iit_gemm_8ph_run(const void* args, int mode, int epi, void* stream);
+extern "C" int iit_gemm_4w_run(const void* args, int mode, int epi, int bk, void* stream);
+
 IIT_EXPORT int iit_gemm_glds_ok(const void* A, const void* B, const void* C, const void* C2, const void* resid,
                                 long lda, long ldb, long ldc, long ldc2, long ldr, int M, int N, int K, int mode,
                                 int epi, int bias_cols, int tile, int splits, int reduce) {
+  if (tile == IIT_8PH_TILE || tile == IIT_4W_TILE || tile == IIT_4W32_TILE) {  // 256 x 256 tiles, K % 64 == 0
+    if (splits != 1 || reduce || !iit_gemm_8ph_ok(M, N, K, mode, epi)) return 0;
+    if ((epi == E_DGELU || epi == E_DGELU_ERF) && !C2) return 0;
+    if (lda % 8 || ldb % 8 || ldc % 8 || (C2 && ldc2 % 8) || (resid && ldr % 8)) return 0;
+    if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)C2 | (uintptr_t)resid) & 15) return 0;
+    if (epi == E_BF16_BIAS3 && bias_cols % 8) return 0;
+    return 1;
+  }
   if (tile < 0 || tile >= IIT_GLDS_TILES || tile == 19 || tile >= 35) return 0;
   // atomic split-K: fp32 accumulate only; reduction split-K (``reduce``): fp32 accumulate, store or residual add (the
   // last-arriving split runs the epilogue once on the summed tile)
@@ -201,6 +218,9 @@ IIT_EXPORT int iit_gemm_glds_sm(const void* A, const void* B, void* C, void* C2,
   a.bsum = mode == 3 ? bsum : nullptr;
   a.gsq = epi == E_F32_STORE ? gsq : nullptr;
   hipStream_t s = (hipStream_t)stream;
+  if (tile == IIT_8PH_TILE) return iit_gemm_8ph_run(&a, mode, epi, stream);
+  if (tile == IIT_4W_TILE) return iit_gemm_4w_run(&a, mode, epi, 64, stream);
+  if (tile == IIT_4W32_TILE) return iit_gemm_4w_run(&a, mode, epi, 32, stream);
 #define G2(MODE, AK, BK_, EPI) \
   if (mode == (MODE) && epi == (EPI)) return (int)launch_tile<AK, BK_, EPI>(a, tile, s);
   G2(0, false, false, E_BF16)

@@ -70,22 +70,29 @@ __device__ __forceinline__ int kmaj_swz(int kr) {
 template <int BK>
 __device__ __forceinline__ int kcont_swz(int row) {
   if constexpr (BK == 128) return row & 15;
+  else if constexpr (BK == 32) return (row >> 2) & 3;  // 64-B rows: four rows per 256-B bank window
   else return (row >> 1) & 7;
 }
 
 // Stage one operand tile (R rows of the output dimension x BK k) into its LDS image with LDS-DMA.  The per-lane
 // source pointers and LDS offsets are computed once per workgroup; staging K-tile kt then costs one 64-bit add per
-// DMA instruction (the k offset is uniform).
-template <bool KMAJ, int R, int NW = 4, int BK = 64>
+// DMA instruction (the k offset is uniform).  LEAN keeps ONE per-lane pointer: with an even wave count the XOR
+// swizzle of instruction i equals that of instruction 0, so instruction i's source is pointer 0 plus a wave-uniform
+// stride (an SGPR add) -- N - 1 fewer VGPR pairs for the register-bound big tiles (gemm_4w.hip).
+template <bool KMAJ, int R, int NW = 4, int BK = 64, bool LEAN = false>
 struct Stager {
   // LDS-DMA instructions per wave per K-tile: one instruction moves 8 rows x 128 B (k-contiguous, BK = 64), 4 rows x
   // 256 B (BK = 128) or 64 / (R/8) k-rows (k-major); the NW waves of the workgroup split them
   static constexpr int RPI = 1024 / (BK * 2);  // k-contiguous rows per instruction
   static constexpr int N = KMAJ ? BK / (NW * (64 / (R / 8))) : R / (RPI * NW);
   static_assert(N >= 1, "tile too narrow for the workgroup's waves");
-  const __bf16* ptr[N];
-  int off[N];
+  static_assert(!LEAN || NW % 2 == 0, "the lean stager needs an even wave count");
+  static constexpr int NP_ = LEAN ? 1 : N;
+  const __bf16* ptr[NP_];
+  int off[NP_];
   long kstep;  // elements between consecutive K-tiles
+  long istep;  // LEAN: elements between consecutive instructions' sources
+  int ostep;   // LEAN: bytes between consecutive instructions' LDS offsets
 
   __device__ __forceinline__ void init(const __bf16* base, long ld, int r0g, int kbeg, int wave, int lane) {
     if constexpr (!KMAJ) {
@@ -93,7 +100,7 @@ struct Stager {
       // c ^ ((r >> 1) & 7); BK = 128: 256-B rows, 4 rows x 16 chunks, chunk c at slot c ^ (r & 15)
       constexpr int CPR = BK / 8;  // 16-B chunks per row
 #pragma unroll
-      for (int i = 0; i < N; ++i) {
+      for (int i = 0; i < NP_; ++i) {
         const int r0 = i * RPI * NW + wave * RPI;
         const int row = r0 + lane / CPR;
         const int c = (lane % CPR) ^ kcont_swz<BK>(row);
@@ -101,12 +108,14 @@ struct Stager {
         off[i] = r0 * BK * 2;
       }
       kstep = BK;
+      istep = (long)RPI * NW * ld;
+      ostep = RPI * NW * BK * 2;
     } else {
       // [64][R] bf16, R*2-B k-rows; one instruction = (64 / (R/8)) k-rows
       constexpr int CH = R / 8;     // 16-B chunks per k-row
       constexpr int KRI = 64 / CH;  // k-rows per instruction
 #pragma unroll
-      for (int i = 0; i < N; ++i) {
+      for (int i = 0; i < NP_; ++i) {
         const int kr0 = (i * NW + wave) * KRI;
         const int kr = kr0 + lane / CH;
         const int ch = lane % CH;
@@ -115,13 +124,18 @@ struct Stager {
         off[i] = kr0 * R * 2;
       }
       kstep = (long)BK * ld;
+      istep = (long)NW * KRI * ld;
+      ostep = NW * KRI * R * 2;
     }
   }
 
   __device__ __forceinline__ void stage(int kt, char* img) const {
     const long k = kt * kstep;
 #pragma unroll
-    for (int i = 0; i < N; ++i) glds16(ptr[i] + k, img + off[i]);
+    for (int i = 0; i < N; ++i) {
+      if constexpr (LEAN) glds16(ptr[0] + (k + i * istep), img + off[0] + i * ostep);
+      else glds16(ptr[i] + k, img + off[i]);
+    }
   }
 };
 
@@ -143,13 +157,13 @@ struct Panels {
   static constexpr int NP = R / PR;
 };
 
-template <bool KMAJ, int R, int NW = 4, int BK = 64>
+template <bool KMAJ, int R, int NW = 4, int BK = 64, bool LEAN = false>
 struct OperandStager {
   static constexpr bool PANELS = Panels<KMAJ, R>::ON;
   static constexpr int NP = Panels<KMAJ, R>::NP;
   static constexpr int PR = Panels<KMAJ, R>::PR;        // columns per panel
-  static constexpr int N = NP * Stager<KMAJ, PR, NW, BK>::N;  // LDS-DMA instructions per wave per K-tile
-  Stager<KMAJ, PR, NW, BK> st[NP];
+  static constexpr int N = NP * Stager<KMAJ, PR, NW, BK, LEAN>::N;  // LDS-DMA instructions per wave per K-tile
+  Stager<KMAJ, PR, NW, BK, LEAN> st[NP];
 
   __device__ __forceinline__ void init(const __bf16* base, long ld, int r0g, int kbeg, int wave, int lane) {
 #pragma unroll
@@ -300,10 +314,146 @@ struct GldsSmem {
   static constexpr int BYTES = NS * STAGE > EPI_BYTES ? NS * STAGE : EPI_BYTES;
 };
 
+// The epilogue of an output tile, shared by the LDS-DMA kernels: the fp32 accumulators go through LDS in ECH row
+// chunks of BM / ECH rows (``write_acc(E, ch)`` stores this thread's accumulators of chunk ``ch`` into the row-major
+// [BM / ECH][EPS] fp32 tile E), then each thread owns 8 consecutive columns of a row: 16-B / 32-B vector loads of
+// bias / residual / accumulator and vector stores with the fused epilogue (bias, residual, gelu, dgelu + column sums,
+// fp32 accumulate / store + sum of squares).
+template <int BM, int BN, int EPI, int NT, int ECH, int EPS, class WriteAcc>
+__device__ __forceinline__ void glds_epilogue(const G2Args& p, char* smem, const int m0, const int n0, const int lin,
+                                              WriteAcc&& write_acc) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = NT / 64;
+  float* E = (float*)smem;
+  constexpr int ER = BM / ECH;  // rows per chunk
+  constexpr int CPR = BN / 8;                      // 8-column chunks per row
+  constexpr int ITEMS = (ER * CPR + NT - 1) / NT;  // chunks per thread per row chunk
+  // the epilogue's streamed global operand (residual, accumulator, saved pre-activation) is loaded for all of a
+  // thread's items up front, before the LDS tile is complete: ITEMS loads in flight instead of one per round trip
+  constexpr bool PF32 = EPI == E_F32_RESID || EPI == E_F32_ACC;
+  constexpr bool PF16 = EPI == E_DGELU || EPI == E_DGELU_ERF;
+  float sq = 0.f;  // E_F32_STORE with ``gsq``: this thread's sum of squares of the stored values
+  for (int ch = 0; ch < ECH; ++ch) {
+  float4 pf[PF32 ? 2 * ITEMS : 1];
+  bf16x8 pb[PF16 ? ITEMS : 1];
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int id = tid + k * NT;
+    if (id < ER * CPR) {
+      const int row = m0 + ch * ER + id / CPR, col = n0 + (id % CPR) * 8;
+      if constexpr (EPI == E_F32_RESID) {
+        const float* src = p.resid + (long)row * p.ldr + col;
+        pf[2 * k] = *(const float4*)src;
+        pf[2 * k + 1] = *(const float4*)(src + 4);
+      } else if constexpr (EPI == E_F32_ACC) {
+        const float* src = (const float*)p.C + (long)row * p.ldc + col;
+        pf[2 * k] = *(const float4*)src;
+        pf[2 * k + 1] = *(const float4*)(src + 4);
+      } else if constexpr (PF16) {
+        pb[k] = *(const bf16x8*)((const __bf16*)p.C2 + (long)row * p.ldc2 + col);
+      }
+    }
+  }
+  __syncthreads();  // staging buffers / the previous chunk are done before the LDS is (re)written
+  write_acc(E, ch);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int id = tid + k * NT;
+    if (id >= ER * CPR) break;
+    const int lr = id / CPR, lc = (id % CPR) * 8;
+    const int row = m0 + ch * ER + lr, col = n0 + lc;
+    float v[8];
+    {
+      const float4 x = *(const float4*)(E + lr * EPS + lc), y = *(const float4*)(E + lr * EPS + lc + 4);
+      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    }
+    if constexpr (EPI == E_BF16) {
+      if (p.bias0) add8(v, p.bias0 + col);
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v, p.store_mode);
+    } else if constexpr (EPI == E_BF16_BIAS3) {
+      const int w = col / p.bias_cols, o = col - w * p.bias_cols;
+      const float* bb = w == 0 ? p.bias0 : (w == 1 ? p.bias1 : p.bias2);
+      if (bb) add8(v, bb + o);
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v, p.store_mode);
+    } else if constexpr (EPI == E_F32_RESID) {
+      if (p.bias0) add8(v, p.bias0 + col);
+      add8v(v, pf[2 * k], pf[2 * k + 1]);
+      store8_f32((float*)p.C + (long)row * p.ldc + col, v, p.store_mode);
+    } else if constexpr (EPI == E_GELU || EPI == E_GELU_ERF) {
+      if (p.bias0) add8(v, p.bias0 + col);
+      // pre (C2) is only kept for the backward: inference forwards pass C2 = null and skip its store
+      if (p.C2) store8_bf16((__bf16*)p.C2 + (long)row * p.ldc2 + col, v, p.store_mode);
+      float g[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {  // gelu of the stored (bf16) pre, which the backward reads
+        const float x = bf2f(f2bf(v[e]));
+        g[e] = EPI == E_GELU ? gelu_new_dev(x) : gelu_erf_f(x);
+      }
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, g, p.store_mode);
+    } else if constexpr (EPI == E_DGELU || EPI == E_DGELU_ERF) {
+      const bf16x8 pr = pb[k];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {  // the stored value
+        const float x = bf2f(pr[e]);
+        v[e] = bf2f(f2bf(v[e] * (EPI == E_DGELU ? gelu_new_grad_f(x) : gelu_erf_grad_f(x))));
+      }
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v, p.store_mode);
+      if (p.csum) {  // this thread's own chunk of E: no other thread touches it before the barrier below
+        *(float4*)(E + lr * EPS + lc) = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)(E + lr * EPS + lc + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    } else if constexpr (EPI == E_F32_ACC) {
+      float* dst = (float*)p.C + (long)row * p.ldc + col;
+      add8v(v, pf[2 * k], pf[2 * k + 1]);
+      store8_f32(dst, v, p.store_mode);
+    } else {  // E_F32_STORE
+      if (p.bias0) add8(v, p.bias0 + col);
+      store8_f32((float*)p.C + (long)row * p.ldc + col, v, p.store_mode);
+      if (p.gsq) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sq += v[e] * v[e];
+      }
+    }
+  }
+  if constexpr (EPI == E_DGELU || EPI == E_DGELU_ERF) {
+    if (p.csum) {  // column sums of this chunk's ER rows: G row groups per column, one atomic each
+      __syncthreads();
+      constexpr int G = NT / BN > 0 ? NT / BN : 1;
+      for (int c = tid; c < BN * G; c += NT) {
+        const int col = c % BN, g = c / BN;
+        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent chains: the LDS reads pipeline
+#pragma unroll
+        for (int r0 = g; r0 < ER; r0 += 8 * G)
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (r0 + u * G < ER) s[u] += E[(r0 + u * G) * EPS + col];
+        atomicAdd(p.csum + n0 + col, ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7])));
+      }
+    }
+  }
+  }  // chunk
+  if constexpr (EPI == E_F32_STORE) {
+    if (p.gsq) {  // one atomic per workgroup (the waves' sums meet in LDS): thousands of tiles share 64 slots
+      sq = wave_sum(sq);
+      float* red = (float*)smem;
+      __syncthreads();  // every thread is done with the epilogue's LDS tile
+      if (lane == 0) red[wave] = sq;
+      __syncthreads();
+      if (tid == 0) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) t += red[w];
+        atomicAdd(p.gsq + (lin & 63), t);
+      }
+    }
+  }
+}
+
 // One output tile of one GEMM problem: workgroup ``lin`` of the ``nlin`` tiles of K-split ``split`` of ``nsplit``
 // (a single-problem launch passes its block index and grid size; the dual launch in gemm_dual.hip maps its
 // workgroups onto two problems).  ``smem`` is the launch's one LDS object of at least GldsSmem<...>::BYTES.
-template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW, int BK = 64, int OCC = 1>
+template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW, int BK = 64, int OCC = 1, bool LEAN = false>
 __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, const int nlin, const int split,
                                                const int nsplit, char* smem) {
   constexpr int HALVES = BK / 64;  // a 128-deep K-tile is two 64-deep halves of two 32-deep MFMA sub-steps each
@@ -313,7 +463,7 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LOADS = OperandStager<AKM, BM, NW, BK>::N + OperandStager<BKM, BN, NW, BK>::N;  // DMA / wave / K-tile
+  constexpr int LOADS = OperandStager<AKM, BM, NW, BK, LEAN>::N + OperandStager<BKM, BN, NW, BK, LEAN>::N;  // DMA / wave / K-tile
   using SM = GldsSmem<BM, BN, NS, NW, BK, OCC>;
   constexpr int EPS = SM::EPS;  // fp32 epilogue row stride (floats)
   // the fp32 epilogue tile goes through LDS in row chunks (one per wave row) when the whole tile would not fit
@@ -366,8 +516,8 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
   //    wave's counted vmcnt) and retires all reads of tile kt, so those MFMAs overlap the next DMA issue.
   RawFrag<AKM> ca[TM], na[TM];
   RawFrag<BKM> cb[TN], nb[TN];
-  OperandStager<AKM, BM, NW, BK> stA;
-  OperandStager<BKM, BN, NW, BK> stB;
+  OperandStager<AKM, BM, NW, BK, LEAN> stA;
+  OperandStager<BKM, BN, NW, BK, LEAN> stB;
   stA.init(p.A, p.lda, m0, kbeg, wave, lane);
   stB.init(p.B, p.ldb, n0, kbeg, wave, lane);
 #pragma unroll
@@ -561,146 +711,25 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
     }
   }
   // ---------------------------------------------------------------- epilogue via LDS (ECH row chunks)
-  float* E = (float*)smem;
-  constexpr int ER = BM / ECH;  // rows per chunk: wave rows [ch * WMR / ECH, (ch + 1) * WMR / ECH)
-  constexpr int CPR = BN / 8;                      // 8-column chunks per row
-  constexpr int ITEMS = (ER * CPR + NT - 1) / NT;  // chunks per thread per row chunk
-  // the epilogue's streamed global operand (residual, accumulator, saved pre-activation) is loaded for all of a
-  // thread's items up front, before the LDS tile is complete: ITEMS loads in flight instead of one per round trip
-  constexpr bool PF32 = EPI == E_F32_RESID || EPI == E_F32_ACC;
-  constexpr bool PF16 = EPI == E_DGELU || EPI == E_DGELU_ERF;
-  float sq = 0.f;  // E_F32_STORE with ``gsq``: this thread's sum of squares of the stored values
-  for (int ch = 0; ch < ECH; ++ch) {
-  float4 pf[PF32 ? 2 * ITEMS : 1];
-  bf16x8 pb[PF16 ? ITEMS : 1];
+  glds_epilogue<BM, BN, EPI, NT, ECH, SM::EPS>(p, smem, m0, n0, lin, [&](float* E, int ch) {
+    if (wm / (WMR / ECH) == ch) {
 #pragma unroll
-  for (int k = 0; k < ITEMS; ++k) {
-    const int id = tid + k * NT;
-    if (id < ER * CPR) {
-      const int row = m0 + ch * ER + id / CPR, col = n0 + (id % CPR) * 8;
-      if constexpr (EPI == E_F32_RESID) {
-        const float* src = p.resid + (long)row * p.ldr + col;
-        pf[2 * k] = *(const float4*)src;
-        pf[2 * k + 1] = *(const float4*)(src + 4);
-      } else if constexpr (EPI == E_F32_ACC) {
-        const float* src = (const float*)p.C + (long)row * p.ldc + col;
-        pf[2 * k] = *(const float4*)src;
-        pf[2 * k + 1] = *(const float4*)(src + 4);
-      } else if constexpr (PF16) {
-        pb[k] = *(const bf16x8*)((const __bf16*)p.C2 + (long)row * p.ldc2 + col);
-      }
-    }
-  }
-  __syncthreads();  // staging buffers / the previous chunk are done before the LDS is (re)written
-  if (wm / (WMR / ECH) == ch) {
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (TR) {  // lane: row l & 15, columns 4 (l >> 4) .. + 3 -> one 16-B LDS write
+            const int col = wn * WN + j * 16 + 4 * (lane >> 4);
+            const int row = (wm % (WMR / ECH)) * WM + i * 16 + (lane & 15);
+            *(f32x4*)(E + row * EPS + col) = acc[i][j];
+          } else {
+            const int col = wn * WN + j * 16 + (lane & 15);
+            const int row = (wm % (WMR / ECH)) * WM + i * 16 + 4 * (lane >> 4);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        if constexpr (TR) {  // lane: row l & 15, columns 4 (l >> 4) .. + 3 -> one 16-B LDS write
-          const int col = wn * WN + j * 16 + 4 * (lane >> 4);
-          const int row = (wm % (WMR / ECH)) * WM + i * 16 + (lane & 15);
-          *(f32x4*)(E + row * EPS + col) = acc[i][j];
-        } else {
-          const int col = wn * WN + j * 16 + (lane & 15);
-          const int row = (wm % (WMR / ECH)) * WM + i * 16 + 4 * (lane >> 4);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) E[(row + r) * EPS + col] = acc[i][j][r];
+            for (int r = 0; r < 4; ++r) E[(row + r) * EPS + col] = acc[i][j][r];
+          }
         }
-      }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < ITEMS; ++k) {
-    const int id = tid + k * NT;
-    if (id >= ER * CPR) break;
-    const int lr = id / CPR, lc = (id % CPR) * 8;
-    const int row = m0 + ch * ER + lr, col = n0 + lc;
-    float v[8];
-    {
-      const float4 x = *(const float4*)(E + lr * EPS + lc), y = *(const float4*)(E + lr * EPS + lc + 4);
-      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
     }
-    if constexpr (EPI == E_BF16) {
-      if (p.bias0) add8(v, p.bias0 + col);
-      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v, p.store_mode);
-    } else if constexpr (EPI == E_BF16_BIAS3) {
-      const int w = col / p.bias_cols, o = col - w * p.bias_cols;
-      const float* bb = w == 0 ? p.bias0 : (w == 1 ? p.bias1 : p.bias2);
-      if (bb) add8(v, bb + o);
-      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v, p.store_mode);
-    } else if constexpr (EPI == E_F32_RESID) {
-      if (p.bias0) add8(v, p.bias0 + col);
-      add8v(v, pf[2 * k], pf[2 * k + 1]);
-      store8_f32((float*)p.C + (long)row * p.ldc + col, v, p.store_mode);
-    } else if constexpr (EPI == E_GELU || EPI == E_GELU_ERF) {
-      if (p.bias0) add8(v, p.bias0 + col);
-      // pre (C2) is only kept for the backward: inference forwards pass C2 = null and skip its store
-      if (p.C2) store8_bf16((__bf16*)p.C2 + (long)row * p.ldc2 + col, v, p.store_mode);
-      float g[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {  // gelu of the stored (bf16) pre, which the backward reads
-        const float x = bf2f(f2bf(v[e]));
-        g[e] = EPI == E_GELU ? gelu_new_dev(x) : gelu_erf_f(x);
-      }
-      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, g, p.store_mode);
-    } else if constexpr (EPI == E_DGELU || EPI == E_DGELU_ERF) {
-      const bf16x8 pr = pb[k];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {  // the stored value
-        const float x = bf2f(pr[e]);
-        v[e] = bf2f(f2bf(v[e] * (EPI == E_DGELU ? gelu_new_grad_f(x) : gelu_erf_grad_f(x))));
-      }
-      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v, p.store_mode);
-      if (p.csum) {  // this thread's own chunk of E: no other thread touches it before the barrier below
-        *(float4*)(E + lr * EPS + lc) = make_float4(v[0], v[1], v[2], v[3]);
-        *(float4*)(E + lr * EPS + lc + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      }
-    } else if constexpr (EPI == E_F32_ACC) {
-      float* dst = (float*)p.C + (long)row * p.ldc + col;
-      add8v(v, pf[2 * k], pf[2 * k + 1]);
-      store8_f32(dst, v, p.store_mode);
-    } else {  // E_F32_STORE
-      if (p.bias0) add8(v, p.bias0 + col);
-      store8_f32((float*)p.C + (long)row * p.ldc + col, v, p.store_mode);
-      if (p.gsq) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sq += v[e] * v[e];
-      }
-    }
-  }
-  if constexpr (EPI == E_DGELU || EPI == E_DGELU_ERF) {
-    if (p.csum) {  // column sums of this chunk's ER rows: G row groups per column, one atomic each
-      __syncthreads();
-      constexpr int G = NT / BN > 0 ? NT / BN : 1;
-      for (int c = tid; c < BN * G; c += NT) {
-        const int col = c % BN, g = c / BN;
-        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent chains: the LDS reads pipeline
-#pragma unroll
-        for (int r0 = g; r0 < ER; r0 += 8 * G)
-#pragma unroll
-          for (int u = 0; u < 8; ++u)
-            if (r0 + u * G < ER) s[u] += E[(r0 + u * G) * EPS + col];
-        atomicAdd(p.csum + n0 + col, ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7])));
-      }
-    }
-  }
-  }  // chunk
-  if constexpr (EPI == E_F32_STORE) {
-    if (p.gsq) {  // one atomic per workgroup (the waves' sums meet in LDS): thousands of tiles share 64 slots
-      sq = wave_sum(sq);
-      float* red = (float*)smem;
-      __syncthreads();  // every thread is done with the epilogue's LDS tile
-      if (lane == 0) red[wave] = sq;
-      __syncthreads();
-      if (tid == 0) {
-        float t = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) t += red[w];
-        atomicAdd(p.gsq + (lin & 63), t);
-      }
-    }
-  }
+  });
   if (p.prof != nullptr) {  // drain this workgroup's stores, then stamp (diagnostic path only)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

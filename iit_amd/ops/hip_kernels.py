@@ -208,11 +208,18 @@ GLDS_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 1
               # two co-resident workgroups per CU (<= 80 KiB LDS each): prologue / epilogue overlap
               23: (128, 96), 24: (64, 96), 25: (128, 128), 26: (96, 96), 27: (128, 192), 28: (64, 192),
               29: (64, 96), 30: (64, 64), 31: (64, 128),  # three / four workgroups per CU
-              32: (256, 128), 33: (128, 256), 34: (256, 256)}  # 8 waves: 3-deep rings (32, 33), 256 x 256 (34)
+              32: (256, 128), 33: (128, 256), 34: (256, 256),  # 8 waves: 3-deep rings (32, 33), 256 x 256 (34)
+              # csrc/gemm_8ph.hip: 256 x 256, 8 waves in two ping-pong groups, 8-phase K-loop (no K split)
+              40: (256, 256),
+              # csrc/gemm_4w.hip: 256 x 256, 4 waves of 128 x 128 on 32x32x16 MFMA, AGPR accumulators (no K split),
+              # 64-deep K-tiles in a 2-slot ring (41) / 32-deep in a 4-slot ring (42)
+              41: (256, 256), 42: (256, 256)}
 # tiles 12-14 measured slower than their 4-deep twins on every step shape (profiles/gemm_ring_depth_r2.txt: the tiles
 # are intake-bandwidth-bound, not latency-bound), so the dispatcher does not offer them; kept for the experiment.
 # Tiles 15-18 (128-deep K-tiles) are within a few % of the 64-deep tiles and compete per shape.
-GLDS_DISPATCH_TILES = tuple(t for t in GLDS_TILES if t not in (12, 13, 14, 32, 33, 34))
+# Tile 42 (the four-wave kernel with 32-deep K-tiles) measured slower than tile 41 on every large shape
+# (profiles/gemm_big_tiles_r5.txt): not offered either.
+GLDS_DISPATCH_TILES = tuple(t for t in GLDS_TILES if t not in (12, 13, 14, 32, 33, 34, 42))
 
 
 def _gemm_bounds(what, A, B, C, C2, resid, M, N, K, lda, ldb, ldc, ldc2, ldr, mode, qkv=(0, 0, 0)):
