@@ -202,6 +202,7 @@ class ModelShadow:
         self._value_sig = None
         self._descs = None
         self._n = 0
+        self._frozen = []
 
     # ------------------------------------------------------------------ mirror mode
     def _mirror_layout_ok(self, flat) -> bool:
@@ -220,7 +221,15 @@ class ModelShadow:
         W_U = self._W_U()
         if W_U is not None and W_U.stride() != (self.Vp, 1):
             return False
-        return all(flat.owns(p) for p in self._matrices())
+        return all(flat.owns(p) or self._frozen_plain(p) for p in self._matrices())
+
+    def _frozen_plain(self, p) -> bool:
+        """A frozen (``requires_grad=False``) contiguous fp32 ``W_O`` / ``W_in`` / ``W_out``: outside the arena, so
+        the mirror binds a bf16 copy of it instead (refreshed when the parameter's version changes)."""
+        if p.requires_grad or p.dtype != F32 or not p.is_contiguous():
+            return False
+        return any(p is b.attn.W_O or (not self.model.cfg.attn_only and (p is b.mlp.W_in or p is b.mlp.W_out))
+                   for b in self.model.blocks)
 
     def _W_U(self):
         """The unembedding matrix, or None for models with another head (BERT classifier)."""
@@ -232,14 +241,21 @@ class ModelShadow:
         m = self.model
         d, HD = self.d, self.HD
         self.layers, self.biases = [], []
+        self._frozen = []  # (fp32 parameter, its bf16 copy) for frozen matrices outside the arena
+
+        def view(p, rows, cols):
+            if flat.owns(p):
+                return sh.as_strided((rows, cols), (cols, 1), flat.offset_of(p))
+            c = torch.empty(rows, cols, dtype=BF16, device=self.dev)
+            self._frozen.append((p, c))
+            return c
         for blk in m.blocks:
             a = blk.attn
-            L = {"qkv": sh.as_strided((d, 3 * HD), (3 * HD, 1), flat.offset_of(a.W_Q)),
-                 "o": sh.as_strided((HD, d), (d, 1), flat.offset_of(a.W_O))}
+            L = {"qkv": sh.as_strided((d, 3 * HD), (3 * HD, 1), flat.offset_of(a.W_Q)), "o": view(a.W_O, HD, d)}
             if not m.cfg.attn_only:
                 dm = m.cfg.d_mlp
-                L["in"] = sh.as_strided((d, dm), (dm, 1), flat.offset_of(blk.mlp.W_in))
-                L["out"] = sh.as_strided((dm, d), (d, 1), flat.offset_of(blk.mlp.W_out))
+                L["in"] = view(blk.mlp.W_in, d, dm)
+                L["out"] = view(blk.mlp.W_out, dm, d)
             self.layers.append(L)
             packed_b = (a.b_Q.requires_grad and flat.owns(a.b_Q) and a.b_Q.is_contiguous()
                         and a.b_K.data_ptr() == a.b_Q.data_ptr() + HD * 4
@@ -317,6 +333,12 @@ class ModelShadow:
                 if flat.mirror_version != wv or pv != self._value_sig:
                     flat.refresh_shadow()
                     self._value_sig = pv
+                if self._frozen:
+                    fv = (wv, tuple(p._version for p, _ in self._frozen))
+                    if fv != getattr(self, "_frozen_sig", None):
+                        for p, c in self._frozen:
+                            c.copy_(p.detach().view(c.shape))
+                        self._frozen_sig = fv
                 return
             value = (wv, flat.version)
         else:

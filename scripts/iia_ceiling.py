@@ -13,6 +13,13 @@ Training is ``train_ioi.py``'s configuration (BaseModelPair.train: 12k samples, 
 iit/behaviour/strict 1/1/0.4, clip 1.0) on the headline GPT-2-small model.  Prints one JSON line at the end.
 
     python scripts/iia_ceiling.py --epochs 70 --every 5
+
+3. **Control: ``--control zero-wo``.**  ``W_O`` of every block that hosts ``hook_duplicate``'s
+   LL sites is zeroed and frozen, so the duplicate splice provably cannot reach the output: the intervened LL output
+   IS the base output.  The HL label of a duplicate intervention is the base's IO name for every pair, so a correct
+   pipeline (dataset, HL model, site mapping, splice plan, IIA metric) must report ``IIA(hook_duplicate)`` equal to
+   the behaviour accuracy on the same pairs -- exactly, element for element.  The script asserts it at every
+   evaluation and prints both.
 """
 from __future__ import annotations
 
@@ -69,6 +76,24 @@ def per_node_iia(pair, test_set, batch: int = 512):
     return res, losses
 
 
+def behaviour_accuracy(pair, test_set, node, batch: int = 512):
+    """Accuracy of the un-intervened LL on the base inputs against the HL's base label, through the same code path
+    as :func:`per_node_iia` (an intervention whose source is the base itself is the identity), plus the per-pair
+    agreement with the duplicate-intervened run."""
+    hits = n = same = 0
+    pair._ll_module().eval()
+    for base, abl in test_set.make_loader(batch, 0, shuffle=False):
+        with torch.no_grad():
+            hl_b, ll_b = pair.do_intervention(base, base, node)
+            hl_i, ll_i = pair.do_intervention(base, abl, node)
+        last = (lambda t: t[:, -1] if t.dim() == 3 else t)
+        pred_b, pred_i = last(ll_b).argmax(-1), last(ll_i).argmax(-1)
+        hits += int((pred_b == last(hl_b).argmax(-1)).sum())
+        same += int(((pred_b == pred_i) & (last(hl_b).argmax(-1) == last(hl_i).argmax(-1))).sum())
+        n += pred_b.shape[0]
+    return 100.0 * hits / max(n, 1), 100.0 * same / max(n, 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="gpt2-small", choices=["gpt2-small", "ioi-6l"])
@@ -81,6 +106,8 @@ def main():
                     help="torch: the fp32 torch-op oracle backend on the same device")
     ap.add_argument("--train-nodes", default="",
                     help="comma list of HL node names the TRAINING steps sample from (default: all, as the reference)")
+    ap.add_argument("--control", default="", choices=["", "zero-wo"],
+                    help="zero-wo: zero and freeze W_O of the blocks hosting hook_duplicate (see the docstring)")
     args = ap.parse_args()
 
     from iit_amd.data.iit_dataset import IITDataset, train_test_split
@@ -100,6 +127,16 @@ def main():
     ll = HookedTransformer(cfg)
     if not fast:
         ll.set_op_backend("torch")
+    control_layers = []
+    if args.control == "zero-wo":
+        from iit_amd.tasks.ioi import make_ioi_corr_dict
+        control_layers = sorted({int(s.split(".")[1]) for s in make_ioi_corr_dict(cfg["n_layers"])["hook_duplicate"]})
+        with torch.no_grad():
+            for l in control_layers:
+                ll.blocks[l].attn.W_O.zero_()
+                ll.blocks[l].attn.W_O.requires_grad_(False)
+        ll.mark_weights_changed()
+        print(f"[control] W_O zeroed and frozen in blocks {control_layers}", flush=True)
     ds, hl = make_ioi_dataset_and_hl(args.num_samples, ll, NAMES, device=dev)
     train_ds, test_ds = train_test_split(ds, test_size=0.2, random_state=42)
     train_set = IITDataset(train_ds, train_ds, seed=0, device=dev)
@@ -154,6 +191,14 @@ def main():
             iia, ce = per_node_iia(pair, test_set)
             row["per_node_IIA"] = {k: round(v, 2) for k, v in iia.items()}
             row["per_node_IIT_loss"] = {k: round(v, 4) for k, v in ce.items()}
+            if control_layers:
+                dup = next(n for n in pair.corr.keys() if n.name == "hook_duplicate")
+                acc, agree = behaviour_accuracy(pair, test_set, dup)
+                row["control"] = {"behaviour_acc": round(acc, 2), "dup_IIA": row["per_node_IIA"]["hook_duplicate"],
+                                  "pairs_with_identical_prediction_and_label": round(agree, 2),
+                                  "W_O_absmax": max(float(ll.blocks[l].attn.W_O.abs().max()) for l in control_layers)}
+                assert row["control"]["W_O_absmax"] == 0.0, row
+                assert abs(iia["hook_duplicate"] - acc) < 1e-9 and agree == 100.0, row
             pair.rng.bit_generator.state = rng_state  # per-node evaluation draws nothing; keep the RNG anyway
             pair._ll_module().train()
             orig_log(epoch, metrics, sink)
@@ -164,10 +209,10 @@ def main():
     wall = time.perf_counter() - t0
     best = max(rows, key=lambda r: r["val/IIA"])
     print(json.dumps({"metric": "IOI val/IIA ceiling analysis", "model": args.model, "epochs": args.epochs,
-                      "train_nodes": args.train_nodes or "all", "graphs": args.graphs, "backend": args.backend, "lr": args.lr,
+                      "train_nodes": args.train_nodes or "all", "control": args.control or None, "graphs": args.graphs, "backend": args.backend, "lr": args.lr,
                       "wall_s": round(wall, 1), "tie_fraction_per_node": ties,
                       "best_epoch_val_IIA": best["val/IIA"], "best_epoch": best["epoch"],
-                      "final_per_node_IIA": rows[-1].get("per_node_IIA")}))
+                      "final_per_node_IIA": rows[-1].get("per_node_IIA"), "final_control": rows[-1].get("control")}))
 
 
 if __name__ == "__main__":

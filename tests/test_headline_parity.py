@@ -105,7 +105,8 @@ def test_headline_step_matches_fp32_oracle():
             if float(gr[n].norm()) < 1e-3 * big:  # b_K and friends: zero in exact arithmetic
                 assert float(gf[n].norm()) < 1e-2 * big, (kind, n)
                 continue
-            assert _rel(gf[n], gr[n]) < 0.12, (kind, n, _rel(gf[n], gr[n]))
+            # measured worst 0.0146 (blocks.10.attn.W_K, strict); the bf16 torch-op engine's worst is 0.024
+            assert _rel(gf[n], gr[n]) < 0.03, (kind, n, _rel(gf[n], gr[n]))
     print("grad norms (kind, bf16 HIP, fp32 oracle):", scale_print)
     for opt in (of, orf):
         opt.zero_grad()
@@ -145,7 +146,61 @@ def test_headline_step_matches_fp32_oracle():
         cos = float((df * dr).sum() / (df.norm() * dr.norm() + 1e-30))
         rn = float(df.norm() / dr.norm())
         worst.append((cos, rn, n))
-        assert cos > 0.9 and 0.85 < rn < 1.15, (n, cos, rn)
+        assert cos > 0.99 and 0.97 < rn < 1.03, (n, cos, rn)  # measured worst: cos 0.9989, ratio 0.9979-1.0017
     worst.sort()
     print("weight-delta cosine / norm ratio, worst 5:", worst[:5])
     assert np.isfinite([w[0] for w in worst]).all()
+
+
+def test_headline_gradients_kernel_error_vs_precision_error():
+    """Separates kernel error from bf16 precision error: the same phases run on three engines
+    from the same weights and batch -- the bf16 HIP engine, the bf16 torch-op engine (``TorchOps(bf16)``: the same
+    precision, library ops) and the fp32 torch-op oracle.  Per parameter, the HIP engine's gradient error against the
+    oracle must not exceed the bf16 torch-op engine's by more than a small margin (measured on MI355X: the HIP engine's
+    worst relative error is 0.0146, the torch-op engine's 0.024 -- the HIP engine keeps the residual stream in fp32,
+    TorchOps(bf16) rounds it per op).  The two bf16 engines' mutual distance is bounded by the sum of their
+    independent rounding errors (measured worst 0.0226), so the 2 % the round-4 review suggested for that pair is
+    below what two correct bf16 engines can reach; the kernel-error criterion is the first assertion."""
+    from iit_amd.model_pairs import IOI_ModelPair
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.tasks.ioi import make_ioi_corr
+
+    pf, pr, train = _setup()
+    from iit_amd.models.config import gpt2_config_dict
+    tb = HookedTransformer({**gpt2_config_dict(), "device": str(dev), "init_weights": False, "dtype": torch.bfloat16})
+    tb.load_state_dict({k: v.float() for k, v in pr.ll_model.state_dict().items()})
+    tb.set_op_backend("torch")
+    pt = IOI_ModelPair(ll_model=tb, hl_model=pf.hl_model, corr=make_ioi_corr(12),
+                       training_args={**ARGS, "fused_optimizer": False})
+    opts = [p.make_optimizer(ARGS["lr"]) for p in (pf, pt, pr)]
+    pf.restrict_sparse_rows(train)
+    base, abl = next(iter(train.make_loader(256, 0)))
+    hl_nodes = list(pf.corr.keys())
+    strict_nodes = pf.nodes_not_in_circuit
+    rows = []
+    for kind in ("iit", "strict", "behavior"):
+        gs = []
+        for pair, opt in zip((pf, pt, pr), opts):
+            if kind == "iit":
+                loss = pair.get_IIT_loss_over_batch(base, abl, hl_nodes[1], pair.loss_fn)
+            elif kind == "strict":
+                loss = pair.get_strict_loss_over_batch(base, abl, strict_nodes[3], pair.loss_fn)
+            else:
+                loss = pair.get_behaviour_loss_over_batch(base, pair.loss_fn)
+            gs.append(_grads(pair, opt, loss))
+        gf, gt, gr = gs
+        big = max(float(g.norm()) for g in gr.values())
+        for n in gr:
+            if float(gr[n].norm()) < 1e-3 * big:  # zero in exact arithmetic (b_K, ...): bf16 noise on both sides
+                continue
+            rows.append((kind, n, _rel(gf[n], gr[n]), _rel(gt[n], gr[n]), _rel(gf[n], gt[n])))
+    rows.sort(key=lambda r: -r[2])
+    print("worst HIP-vs-fp32 rows (kind, param, HIP err, torch-bf16 err, HIP vs torch-bf16):")
+    for r in rows[:12]:
+        print("  %-9s %-28s %.4f %.4f %.4f" % r)
+    print("max HIP err %.4f, max torch-bf16 err %.4f, max HIP-vs-torch-bf16 %.4f" % (
+        max(r[2] for r in rows), max(r[3] for r in rows), max(r[4] for r in rows)))
+    for kind, n, ef, et, eft in rows:
+        assert ef <= 1.25 * et + 5e-3, (kind, n, ef, et)  # no kernel error beyond bf16 precision
+        assert ef <= 0.02, (kind, n, ef)
+        assert eft <= 0.035, (kind, n, eft)
