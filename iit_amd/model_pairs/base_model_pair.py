@@ -363,10 +363,11 @@ class BaseModelPair(ABC):
                 module = self._ll_module()
                 flat = getattr(module, "_flat_params", None) or FlatParams(module)
                 module._flat_params = flat
-            wire = self.training_args.get("grad_wire_dtype")  # "bf16" halves the all-reduce bytes (opt-in)
+            # "bf16" / "fp32" overrides the reducer's default (bf16 on RCCL, fp32 on gloo: ddp.py)
+            wire = self.training_args.get("grad_wire_dtype")
             self._reducer = GradReducer(flat, bucket_mb=self.training_args.get("bucket_mb", 64.0),
                                         overlap=self.training_args.get("overlap_allreduce", True),
-                                        wire_dtype=torch.bfloat16 if wire == "bf16" else None,
+                                        wire_dtype={"bf16": torch.bfloat16, "fp32": torch.float32}.get(wire),
                                         module=self._ll_module())
             if getattr(optimizer, "sharded", False):
                 self._reducer.attach_shard(optimizer)

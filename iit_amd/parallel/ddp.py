@@ -21,11 +21,15 @@ Bucket size default 64 MiB: per xGMI ring link (~150 GB/s) that is ~0.4 ms per
 bucket, large enough to amortise RCCL launch latency, small enough that the last
 bucket's exposed tail is short.
 
-Wire precision: fp32 by default (the data-parallel step equals the single-GPU step up to summation order).
-``IIT_DP_GRAD_DTYPE=bf16`` (or ``GradReducer(..., wire_dtype=torch.bfloat16)``) halves the bytes on xGMI: each
-bucket is cast to a bf16 staging buffer, all-reduced there and cast back into the fp32 arena -- for the
-communication-bound configs (Llama-3-8B: 32 GB of fp32 gradient per optimizer step).  Opt-in: it rounds every
-rank's gradient to bf16 before the sum.
+Wire precision: bf16 on RCCL by default, fp32 on gloo.  With the bf16 wire each bucket is cast to a bf16 staging
+buffer, all-reduced there and cast back into the fp32 arena: half the bytes on xGMI (GPT-2-small: 250 instead of
+500 MB per optimizer phase, three phases per step; Llama-3-8B: 16 instead of 32 GB).  The decision is the
+8-rank summation test tests/test_wire_dtype.py: the wire's rounding moves the averaged gradient by 0.3-0.45 %
+(one bf16 rounding), never more than the single-GPU step's own bf16 compute error (1.3-2.4 % at GPT-2-small scale),
+so the DP step stays within the precision the single-GPU step already has.  ``IIT_DP_GRAD_DTYPE=fp32`` (or
+``GradReducer(..., wire_dtype=torch.float32)`` / ``training_args["grad_wire_dtype"] = "fp32"``) keeps the exact-sum
+wire: the data-parallel step then equals the single-GPU step up to summation order.  gloo (CPU tests) keeps fp32 so
+the multi-process tests compare against single-process runs at fp32 sums.
 """
 from __future__ import annotations
 
@@ -44,11 +48,16 @@ class GradReducer:
     def __init__(self, flat: FlatParams, bucket_mb: float = 64.0, overlap: bool = True,
                  wire_dtype: Optional[torch.dtype] = None, module: Optional[torch.nn.Module] = None):
         self.flat = flat
-        if wire_dtype is None and os.environ.get("IIT_DP_GRAD_DTYPE", "fp32") == "bf16":
-            wire_dtype = torch.bfloat16
-        self.wire_dtype = wire_dtype if wire_dtype not in (None, torch.float32) else None
         self.world = pdist.world_size()
         self.enabled = self.world > 1 or pdist.force_reducer()
+        if wire_dtype is None:
+            env = os.environ.get("IIT_DP_GRAD_DTYPE", "")
+            if env in ("bf16", "fp32"):
+                wire_dtype = torch.bfloat16 if env == "bf16" else torch.float32
+            else:  # default: bf16 on RCCL (tests/test_wire_dtype.py), fp32 on gloo
+                nccl = self.enabled and dist.is_initialized() and dist.get_backend() == "nccl"
+                wire_dtype = torch.bfloat16 if nccl else torch.float32
+        self.wire_dtype = wire_dtype if wire_dtype != torch.float32 else None
         self.overlap = overlap and self.enabled
         self._bucket_bytes = int(bucket_mb * (1 << 20))
         self.buckets = flat.buckets(self._bucket_bytes)
