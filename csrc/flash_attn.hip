@@ -18,7 +18,14 @@
 //   dQ        S^T = K Q^T, dP^T = V dO^T, dS^T = P^T (dP^T - D); dQ^T += K^T dS^T
 // with D = rowsum(dO o O) from a small prep kernel.  dK/dV workgroups own 64 keys of one KV head and loop over every
 // query head of its group (GQA needs no atomics); dQ workgroups own 64 queries.
+//
+// General interchange splice of ``hook_z`` (``use_sp``; any patch-spec index over z [B][S][Hq][dh], the range table
+// of csrc/splice_spec.h): the forward's output store writes the source's value into the spliced elements (no separate
+// splice pass over z), and every backward load of dO zeroes the spliced elements (the spliced z is a constant: its
+// elements carry no gradient into q / k / v) -- the prep kernel's D = rowsum(dO o O), the dK/dV kernel's dO tiles and
+// the dQ kernel's dO fragments, so no masked copy of dO is written either.
 #include "common.h"
+#include "splice_spec.h"
 #include <stdlib.h>
 
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4_t;
@@ -38,7 +45,24 @@ struct FaArgs {
   long gqb, gqs, gqh, gkb, gks, gkh, gvb, gvs, gvh;  // gradient strides
   int B, S, Hq, Hkv, causal;
   float scale;
+  int use_sp;     // general z splice: sp over [B][S][Hq][dh], source a.src with sp.sstride element strides
+  SpliceSpec sp;
 };
+
+// is (b, row, h) of z inside the splice's first three dimensions
+__device__ __forceinline__ bool sp_row(const FaArgs& a, int b, int row, int h) {
+  return a.use_sp && in_ranges(a.sp, 0, b) && in_ranges(a.sp, 1, row) && in_ranges(a.sp, 2, h);
+}
+
+// dO elements d0 .. d0 + 7 of a row inside the splice (``row_in``) read as zero
+__device__ __forceinline__ bf16x8 sp_mask8(bf16x8 v, const FaArgs& a, bool row_in, int d0) {
+  if (!row_in) return v;
+  i16x8 w = __builtin_bit_cast(i16x8, v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (in_ranges(a.sp, 3, d0 + e)) w[e] = 0;
+  return __builtin_bit_cast(bf16x8, w);
+}
 
 constexpr int T64 = 64;
 
@@ -61,12 +85,30 @@ __device__ __forceinline__ void load_tile(__bf16* img, const __bf16* base, long 
   }
 }
 
+// load_tile of dO rows with the splice mask applied (rows r0.. of batch b, query head h)
+template <int DH>
+__device__ __forceinline__ void load_tile_dz(__bf16* img, const __bf16* base, long stride, int r0, int S, int tid,
+                                             const struct FaArgs& a, int b, int h);
+
 __device__ __forceinline__ bf16x8 zero8() {
   const i16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
   return __builtin_bit_cast(bf16x8, z);
 }
 
 __device__ __forceinline__ bf16x8 gload8(const __bf16* p, bool ok) { return ok ? *(const bf16x8*)p : zero8(); }
+
+template <int DH>
+__device__ __forceinline__ void load_tile_dz(__bf16* img, const __bf16* base, long stride, int r0, int S, int tid,
+                                             const FaArgs& a, int b, int h) {
+  constexpr int CPR = DH / 8;
+#pragma unroll
+  for (int i = tid; i < T64 * CPR; i += 256) {
+    const int r = i / CPR, ch = i % CPR;
+    bf16x8 val = zero8();
+    if (r0 + r < S) val = sp_mask8(*(const bf16x8*)(base + (long)(r0 + r) * stride + ch * 8), a, sp_row(a, b, r0 + r, h), ch * 8);
+    *(bf16x8*)(img + ioff<DH>(r, ch * 8)) = val;
+  }
+}
 
 template <int DH>
 __device__ __forceinline__ bf16x8 frag_rows(const __bf16* img, int m0, int k0, int lane) {
@@ -217,8 +259,22 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FaArgs a) {
     if (qi < S) {
       const float inv = ls > 0.f ? 1.f / ls : 0.f;
       __bf16* zr = a.z + b * a.zb + (long)qi * a.zs + h * a.zh;
+      if (sp_row(a, b, qi, h)) {  // spliced row of z: the source's value in the spliced elements
+        const __bf16* sr = a.src + b * a.sp.sstride[0] + (long)qi * a.sp.sstride[1] + h * a.sp.sstride[2];
 #pragma unroll
-      for (int t = 0; t < DH / 16; ++t) store4(zr + 16 * t + 4 * g, o[j][t], inv);
+        for (int t = 0; t < DH / 16; ++t) {
+          bf16x4 ov;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int d = 16 * t + 4 * g + e;
+            ov[e] = in_ranges(a.sp, 3, d) ? sr[d * a.sp.sstride[3]] : f2bf(o[j][t][e] * inv);
+          }
+          *(bf16x4*)(zr + 16 * t + 4 * g) = ov;
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < DH / 16; ++t) store4(zr + 16 * t + 4 * g, o[j][t], inv);
+      }
       if (g == 0 && a.lse) a.lse[((long)b * a.Hq + h) * S + qi] = (m[j] + __log2f(ls)) * kLn2;
     }
   }
@@ -237,9 +293,10 @@ __global__ __launch_bounds__(256) void fa_bwd_prep_kernel(FaArgs a) {
   const __bf16* o = a.z + b * a.zb + (long)i * a.zs + h * a.zh;
   const __bf16* g = a.dz + b * a.db + (long)i * a.ds + h * a.dh_;
   float acc = 0.f;
+  const bool row_in = sp_row(a, b, i, h);
 #pragma unroll
   for (int ch = 0; ch < DH / 8; ++ch) {
-    const bf16x8 x = *(const bf16x8*)(o + ch * 8), y = *(const bf16x8*)(g + ch * 8);
+    const bf16x8 x = *(const bf16x8*)(o + ch * 8), y = sp_mask8(*(const bf16x8*)(g + ch * 8), a, row_in, ch * 8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc += bf2f(x[e]) * bf2f(y[e]);
   }
@@ -282,7 +339,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(FaArgs a) {
     for (int i0 = qbeg; i0 < S; i0 += T64) {
       __syncthreads();
       load_tile<DH>(Qs, qbase, a.qs, i0, S, tid);
-      load_tile<DH>(Gs, gbase, a.ds, i0, S, tid);
+      if (a.use_sp) load_tile_dz<DH>(Gs, gbase, a.ds, i0, S, tid, a, b, h);
+      else load_tile<DH>(Gs, gbase, a.ds, i0, S, tid);
       if (tid < T64) {
         Ls[tid] = i0 + tid < S ? lse[i0 + tid] : 0.f;
         Ds[tid] = i0 + tid < S ? D[i0 + tid] : 0.f;
@@ -387,7 +445,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(FaArgs a) {
 #pragma unroll
     for (int s = 0; s < DH / 32; ++s) {
       qf[j][s] = gload8(a.q + b * a.qb + (long)qi * a.qs + h * a.qh + 32 * s + 8 * g, qi < S);
-      gf[j][s] = gload8(a.dz + b * a.db + (long)qi * a.ds + h * a.dh_ + 32 * s + 8 * g, qi < S);
+      gf[j][s] = sp_mask8(gload8(a.dz + b * a.db + (long)qi * a.ds + h * a.dh_ + 32 * s + 8 * g, qi < S), a,
+                          qi < S && sp_row(a, b, qi, h), 32 * s + 8 * g);
     }
     lse_q[j] = qi < S ? a.lse[hrow + qi] : 0.f;
     D_q[j] = qi < S ? a.dd[hrow + qi] : 0.f;
@@ -469,7 +528,7 @@ bool args_ok(const FaArgs& a, int dh) {
 IIT_EXPORT int iit_flash_fwd(const void* q, const void* k, const void* v, const long* strides9, void* z,
                              const long* zstrides3, float* lse, const void* src, const long* sstrides3,
                              unsigned long long head_mask, int B, int S, int Hq, int Hkv, int dh, float scale,
-                             int causal, void* stream) {
+                             int causal, const void* spec, void* stream) {
   FaArgs a = {};
   a.q = (const __bf16*)q; a.k = (const __bf16*)k; a.v = (const __bf16*)v;
   a.qb = strides9[0]; a.qs = strides9[1]; a.qh = strides9[2];
@@ -478,8 +537,12 @@ IIT_EXPORT int iit_flash_fwd(const void* q, const void* k, const void* v, const 
   a.z = (__bf16*)z; a.zb = zstrides3[0]; a.zs = zstrides3[1]; a.zh = zstrides3[2];
   a.lse = lse;
   a.src = (const __bf16*)src;
-  if (src) { a.sb = sstrides3[0]; a.ss = sstrides3[1]; a.sh = sstrides3[2]; }
-  a.head_mask = src ? head_mask : 0ull;
+  if (src && sstrides3) { a.sb = sstrides3[0]; a.ss = sstrides3[1]; a.sh = sstrides3[2]; }
+  // a general splice spec (over [B][S][Hq][dh], source strides inside) replaces the head mask
+  if (spec && src) { a.sp = *(const SpliceSpec*)spec; a.use_sp = 1; }
+  a.head_mask = src && !a.use_sp ? head_mask : 0ull;
+  if (a.use_sp && (a.sp.shape[0] != B || a.sp.shape[1] != S || a.sp.shape[2] != Hq || a.sp.shape[3] != dh))
+    return (int)hipErrorInvalidValue;
   a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.scale = scale;
   if (!args_ok(a, dh) || a.zs % 8 || a.zh % 8 || ((uintptr_t)z & 15)) return (int)hipErrorInvalidValue;
   // query blocks per wave: 2 halves the LDS traffic per FLOP but halves the workgroup count -- taken when that
@@ -504,7 +567,7 @@ IIT_EXPORT int iit_flash_bwd(const void* q, const void* k, const void* v, const 
                              const long* zstrides3, const void* dz, const long* dzstrides3, const float* lse,
                              float* dd, void* dq, void* dk, void* dv, const long* gstrides9,
                              unsigned long long head_mask, int B, int S, int Hq, int Hkv, int dh, float scale,
-                             int causal, void* stream) {
+                             int causal, const void* spec, void* stream) {
   FaArgs a = {};
   a.q = (const __bf16*)q; a.k = (const __bf16*)k; a.v = (const __bf16*)v;
   a.qb = strides9[0]; a.qs = strides9[1]; a.qh = strides9[2];
@@ -512,12 +575,18 @@ IIT_EXPORT int iit_flash_bwd(const void* q, const void* k, const void* v, const 
   a.vb = strides9[6]; a.vs = strides9[7]; a.vh = strides9[8];
   a.z = (__bf16*)z; a.zb = zstrides3[0]; a.zs = zstrides3[1]; a.zh = zstrides3[2];
   a.dz = (const __bf16*)dz; a.db = dzstrides3[0]; a.ds = dzstrides3[1]; a.dh_ = dzstrides3[2];
+  if (spec) {
+    a.sp = *(const SpliceSpec*)spec;
+    a.use_sp = 1;
+    if (a.sp.shape[0] != B || a.sp.shape[1] != S || a.sp.shape[2] != Hq || a.sp.shape[3] != dh)
+      return (int)hipErrorInvalidValue;
+  }
   a.lse = (float*)lse; a.dd = dd;
   a.dq = (__bf16*)dq; a.dk = (__bf16*)dk; a.dv = (__bf16*)dv;
   a.gqb = gstrides9[0]; a.gqs = gstrides9[1]; a.gqh = gstrides9[2];
   a.gkb = gstrides9[3]; a.gks = gstrides9[4]; a.gkh = gstrides9[5];
   a.gvb = gstrides9[6]; a.gvs = gstrides9[7]; a.gvh = gstrides9[8];
-  a.head_mask = head_mask;
+  a.head_mask = a.use_sp ? 0ull : head_mask;
   a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.scale = scale;
   if (!args_ok(a, dh) || a.ds % 8 || a.dh_ % 8 || a.zs % 8 || a.zh % 8 || ((uintptr_t)dz & 15) || ((uintptr_t)z & 15))
     return (int)hipErrorInvalidValue;

@@ -24,10 +24,130 @@ from iit_amd.utils.plotter import plot_ablation_stats
 from iit_amd.utils.progress import progress
 
 
+def _resnet_site(hook_point: str):
+    """``mod.conv1.hook_point`` -> (0, 0, "stem"); ``mod.layer{L}.mod.{i}.mod.conv{c}.hook_point`` -> (L, i, "conv{c}");
+    None for any other hook."""
+    parts = hook_point.split(".")
+    if parts == ["mod", "conv1", "hook_point"]:
+        return 0, 0, "stem"
+    if len(parts) == 7 and parts[0] == "mod" and parts[1].startswith("layer") and parts[4] == "mod" \
+            and parts[5] in ("conv1", "conv2") and parts[6] == "hook_point":
+        return int(parts[1][5:]), int(parts[3]), parts[5]
+    return None
+
+
+def _block_input_name(L: int, i: int) -> str:
+    if i > 0:
+        return f"mod.layer{L}.mod.{i - 1}.hook_point"
+    return "mod.maxpool.hook_point" if L == 1 else f"mod.layer{L - 1}.hook_point"
+
+
+def _resnet_suffix(res, L: int, i: int, which: str, act: torch.Tensor, identity) -> torch.Tensor:
+    """The rest of the ResNet forward from the output of conv hook (L, i, which) -- ``act`` is that conv's output
+    (spliced), ``identity`` the block's shortcut (``downsample(block input)`` or the block input) -- to the logits."""
+    if which == "stem":
+        x = res.maxpool(res.relu(res.bn1(act)))
+        L, i = 1, 0
+    else:
+        bb = getattr(res, f"layer{L}").mod[i].mod
+        out = bb.bn2(bb.conv2(bb.relu(bb.bn1(act)))) if which == "conv1" else bb.bn2(act)
+        x = bb.relu(out + identity)
+        i += 1
+    for layer in range(L, 5):
+        blocks = getattr(res, f"layer{layer}").mod
+        for k in range(i if layer == L else 0, len(blocks)):
+            x = blocks[k](x)
+    return res.fc(torch.flatten(res.avgpool(x), 1))
+
+
+def _fast_resample_sweep(ll_model, test_set, hook_points, bs: int, node_chunk: int = 1):
+    """The leakiness sweep of :func:`evaluate_model_on_ablations` for the PVR ResNet, restructured for the device
+    (the IOI sweeps' machinery, ``iit_amd.utils.eval_ablations``):
+
+    * **node batching** (``node_chunk`` nodes per launch sequence, default 1): stacking the twelve patched source
+      batches into one [12 B] batch measured slower on MI355X -- every new convolution batch size pays MIOpen's
+      first-encounter cost (124 s vs 7.4 s for four hook points) and the warm difference is within 12 %
+      (profiles/eval_causality_r5.txt) -- so the convolutions keep the reference's batch;
+    * **truncated source runs**: the source forward stops at the hook point (``run_capture``);
+    * **shared base prefix**: the base batch runs ONCE per (hook point, batch), up to the hook point, capturing the
+      hook's activation and the enclosing block's shortcut input; each node's spliced run then starts AT the hook
+      (:func:`_resnet_suffix`) from the base activation with the node's quadrant replaced by the source's -- the
+      reference re-runs the whole base forward per node;
+    * the HL output of ``hook_{i}_leaked_to_{j}`` is the patched batch's label (the HL intervention replaces
+      quadrant i's class by the source's, which is exactly what the patch changed; asserted against the HL model
+      in tests/test_eval_causality_fast.py).
+
+    The patch draws are the reference loop's, in its order (hook point, batch, node): ``draw_patch_digits``
+    consumes ``test_set.rng`` exactly as ``patch_batch_at_hl`` does; the loop never synchronises (the draws' host
+    inputs are read once up front), so the host draws of one (hook, batch) overlap the GPU work of the previous.  Cells equal the per-node path up to fp32 batch-size effects in the convolutions."""
+    from iit_amd.tasks.mnist_pvr.pvr_check_leaky_hl import corr_for_shape
+    res = ll_model.mod
+    n = len(test_set)
+    dev = next(ll_model.parameters()).device
+    batches = [test_set.gather(torch.arange(s, min(n, s + bs), device=dev)) for s in range(0, n, bs)]
+    curs = [iv.cpu().numpy() for _, _, iv in batches]  # the draws' host inputs, read once: the loop never syncs
+    # every hook's output shape from one capture at the sweep's own batch size (no extra convolution shapes)
+    shapes = {h: t.shape for h, t in ll_model.run_capture(batches[0][0], list(hook_points)).items()}
+    out = {}
+    with torch.no_grad():
+        for hp in hook_points:
+            L, i, which = _resnet_site(hp)
+            corr = corr_for_shape(hp, shapes[hp])
+            nodes = list(corr.keys())
+            lidx = [next(iter(corr[nd])).index for nd in nodes]
+            shortcut = None if which == "stem" else _block_input_name(L, i)
+            acc = torch.zeros(len(nodes), dtype=torch.float64, device=dev)
+            for (x, y, iv), cur in zip(batches, curs):
+                B = x.shape[0]
+                srcs, ys = [], []
+                for nd in nodes:
+                    _, k = test_set.get_idx_and_intermediate(nd)
+                    js = test_set.draw_patch_digits(cur[:, k])
+                    xs, yk, _ = test_set.apply_patch_digits(x, iv, nd, js)
+                    srcs.append(xs)
+                    ys.append(yk)
+                names = [hp] if shortcut is None else [hp, shortcut]
+                base = ll_model.run_capture(x, names)
+                ident = None
+                if shortcut is not None:
+                    bb = getattr(res, f"layer{L}").mod[i].mod
+                    ident = base[shortcut] if bb.downsample is None else bb.downsample(base[shortcut])
+                preds = []
+                for c0 in range(0, len(nodes), node_chunk):  # node_chunk nodes per launch sequence
+                    cn = min(node_chunk, len(nodes) - c0)
+                    a_src = ll_model.run_capture(torch.cat(srcs[c0:c0 + cn]), [hp])[hp]
+                    a = base[hp].repeat(cn, *([1] * (base[hp].dim() - 1)))
+                    for t in range(cn):
+                        sl = (slice(t * B, (t + 1) * B),) + tuple(lidx[c0 + t].as_index)[1:]
+                        a[sl] = a_src[sl]
+                    idc = None if ident is None else ident.repeat(cn, *([1] * (ident.dim() - 1)))
+                    preds.append(_resnet_suffix(res, L, i, which, a, idc).argmax(dim=1).view(cn, B))
+                pred = torch.cat(preds)
+                hl = torch.stack(ys)
+                changed = (hl != y.unsqueeze(0)).float()
+                hit = (pred == hl).float() * changed
+                acc += (hit.sum(1) / (changed.sum(1) + 1e-10)).double()
+            vals = (acc / max(len(batches), 1)).tolist()
+            out[hp] = {nd.name: float(v) for nd, v in zip(nodes, vals)}
+            for k, v in out[hp].items():
+                assert 0 <= v <= 1, f"{k}: {v}"
+    return out
+
+
 def evaluate_model_on_ablations(ll_model, task: str, test_set, eval_args: dict, verbose: bool = False,
                                 hook_points=None):
+    hps = hook_points or get_hook_points(ll_model)
+    if (eval_args.get("engine", "native") == "native" and eval_args.get("fast", True) and task == "pvr_leaky"
+            and hasattr(test_set, "draw_patch_digits") and hasattr(getattr(ll_model, "mod", None), "layer4")
+            and not ll_model.training and all(_resnet_site(h) is not None for h in hps)):
+        stats = _fast_resample_sweep(ll_model, test_set, hps, eval_args["batch_size"],
+                                     node_chunk=int(eval_args.get("node_chunk", 1)))
+        if verbose:
+            for h, v in stats.items():
+                print(h, v)
+        return stats
     stats_per_layer = {}
-    for hook_point in progress(hook_points or get_hook_points(ll_model), desc="Hook points"):
+    for hook_point in progress(hps, desc="Hook points"):
         _, hl_model, corr = get_alignment(task, config={"hook_point": hook_point,
                                                         "input_shape": test_set.get_input_shape()})
         pair = IITProbeSequentialPair(ll_model=ll_model, hl_model=hl_model, corr=corr,

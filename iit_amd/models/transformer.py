@@ -248,7 +248,15 @@ class Attention(nn.Module):
         causal = self.cfg.attention_dir == "causal"
         if not ops.fused and q.shape[1] > 16 and _flash_ok(q) and \
                 not (run.live(self.hook_attn_scores) or run.live(self.hook_pattern)):
-            # torch op backend on the GPU (Llama family): tiled MFMA attention, GQA-native (no k/v expansion)
+            # torch op backend on the GPU (Llama family): tiled MFMA attention, GQA-native (no k/v expansion); a
+            # single interchange splice of hook_z is applied by the kernel's output store (no splice pass; the
+            # site's scale / gradient mask / hook still run after it, as after SpliceFn)
+            z_spl = run.plan.splice.get(self.hook_z.name) if run.plan is not None else None
+            if z_spl and len(z_spl) == 1 and not z_spl[0].whole:
+                z = _hip_ops().flash_attention_spliced(q, k, v, causal, self.attn_scale, z_spl[0].index,
+                                                       z_spl[0].src)
+                if z is not None:
+                    return z, True
             return _hip_ops().flash_attention(q, k, v, causal, self.attn_scale), False
         if self.gqa:
             rep = self.cfg.n_heads // self.n_kv

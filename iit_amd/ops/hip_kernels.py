@@ -81,8 +81,8 @@ _SIGS = {
     "iit_gemm_dual_set_group_m": [c_int],
     "iit_swiglu_splice_bwd": [c_void_p] * 5 + [c_long, c_void_p, c_void_p],
     "iit_flash_fwd": [c_void_p] * 3 + [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ull] + [c_int] * 5
-                     + [c_float, c_int, c_void_p],
-    "iit_flash_bwd": [c_void_p] * 3 + [c_void_p] * 11 + [c_ull] + [c_int] * 5 + [c_float, c_int, c_void_p],
+                     + [c_float, c_int, c_void_p, c_void_p],
+    "iit_flash_bwd": [c_void_p] * 3 + [c_void_p] * 11 + [c_ull] + [c_int] * 5 + [c_float, c_int, c_void_p, c_void_p],
     "iit_splice": [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_splice_spec_size": [],
     "iit_gemm_glds_set_prof": [c_void_p],
@@ -544,20 +544,23 @@ def _longs(vals):
     return (c_long * len(vals))(*vals)
 
 
-def flash_fwd(q, k, v, z, lse, src, head_mask: int, scale: float, causal: bool):
-    """Tiled attention forward (csrc/flash_attn.hip): q/z [B,S,Hq,dh], k/v [B,S,Hkv,dh], lse [B,Hq,S] fp32."""
+def flash_fwd(q, k, v, z, lse, src, head_mask: int, scale: float, causal: bool, spec=None):
+    """Tiled attention forward (csrc/flash_attn.hip): q/z [B,S,Hq,dh], k/v [B,S,Hkv,dh], lse [B,Hq,S] fp32.
+    ``spec`` (a :class:`iit_amd.ops.splice.PatchSpec` over z's [B,S,Hq,dh] with ``src``'s strides): general splice of
+    the output, applied by the output store (replaces ``head_mask``)."""
     B, S, Hq, dh = q.shape
     Hkv = k.shape[2]
     st = _longs(_bsh(q) + _bsh(k) + _bsh(v))
     zs = _longs(_bsh(z))
-    ss = _longs(_bsh(src)) if src is not None else None
+    ss = _longs(_bsh(src)) if (src is not None and spec is None) else None
     _check(lib().iit_flash_fwd(_p(q), _p(k), _p(v), ctypes.cast(st, c_void_p), _p(z), ctypes.cast(zs, c_void_p),
                                _p(lse), _p(src), None if ss is None else ctypes.cast(ss, c_void_p),
-                               head_mask if src is not None else 0, B, S, Hq, Hkv, dh, scale, int(causal), _stream()),
+                               head_mask if src is not None else 0, B, S, Hq, Hkv, dh, scale, int(causal),
+                               None if spec is None else spec.ptr, _stream()),
            "flash_fwd")
 
 
-def flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, head_mask: int, scale: float, causal: bool):
+def flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, head_mask: int, scale: float, causal: bool, spec=None):
     B, S, Hq, dh = q.shape
     Hkv = k.shape[2]
     st = _longs(_bsh(q) + _bsh(k) + _bsh(v))
@@ -565,7 +568,8 @@ def flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, head_mask: int, scale: float,
     zs, ds = _longs(_bsh(z)), _longs(_bsh(dz))
     _check(lib().iit_flash_bwd(_p(q), _p(k), _p(v), ctypes.cast(st, c_void_p), _p(z), ctypes.cast(zs, c_void_p),
                                _p(dz), ctypes.cast(ds, c_void_p), _p(lse), _p(dd), _p(dq), _p(dk), _p(dv),
-                               ctypes.cast(gs, c_void_p), head_mask, B, S, Hq, Hkv, dh, scale, int(causal), _stream()),
+                               ctypes.cast(gs, c_void_p), head_mask, B, S, Hq, Hkv, dh, scale, int(causal),
+                               None if spec is None else spec.ptr, _stream()),
            "flash_bwd")
 
 

@@ -641,7 +641,7 @@ def _flash_grads(ctx, dz, q, k, v, dq, dk, dv):
     if dz.stride(-1) != 1 or dz.stride(1) % 8 or dz.stride(2) % 8:
         dz = dz.contiguous()
     dd = torch.empty(B, Hq, S, dtype=F32, device=q.device)
-    K.flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, mask, scale, causal)
+    K.flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, mask, scale, causal, spec=getattr(ctx, "spec", None))
 
 
 class FlashPackedFn(Function):
@@ -672,27 +672,31 @@ class FlashPackedFn(Function):
 
 
 class FlashFn(Function):
-    """Tiled MFMA attention over separate q [B,S,Hq,dh] and grouped k/v [B,S,Hkv,dh] (bf16, GQA-native)."""
+    """Tiled MFMA attention over separate q [B,S,Hq,dh] and grouped k/v [B,S,Hkv,dh] (bf16, GQA-native).  With
+    ``spec`` / ``src``: an interchange splice of ``hook_z`` at any patch-spec index, applied by the kernel's output
+    store; the backward kernels read dO with the spliced elements zeroed (no splice pass, no masked dO copy)."""
 
     @staticmethod
-    def forward(ctx, q, k, v, causal, scale):
+    def forward(ctx, q, k, v, causal, scale, src=None, spec=None):
         ctx.set_materialize_grads(False)
         B, S, Hq, dh = q.shape
         z = torch.empty(B, S, Hq, dh, dtype=BF16, device=q.device)
         lse = torch.empty(B, Hq, S, dtype=F32, device=q.device)
-        K.flash_fwd(q, k, v, z, lse, None, 0, scale, causal)
+        K.flash_fwd(q, k, v, z, lse, src, 0, scale, causal, spec=spec)
         ctx.save_for_backward(q, k, v, z, lse)
         ctx.cfg = (0, causal, scale)
+        ctx.spec = spec
+        ctx.keep = src  # the spec's source pointer must outlive the launch
         return z
 
     @staticmethod
     def backward(ctx, dz):
         if dz is None:
-            return None, None, None, None, None
+            return None, None, None, None, None, None, None
         q, k, v = ctx.saved_tensors[:3]
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         _flash_grads(ctx, dz, q, k, v, dq, dk, dv)
-        return dq, dk, dv, None, None
+        return dq, dk, dv, None, None, None, None
 
 
 def _flash_view(t: torch.Tensor) -> torch.Tensor:
@@ -710,6 +714,22 @@ def flash_supported(q: torch.Tensor) -> bool:
 def flash_attention(q, k, v, causal: bool, attn_scale: float) -> torch.Tensor:
     """softmax(q k^T / attn_scale) v for q [B,S,Hq,dh], k/v [B,S,Hkv,dh] (Hkv | Hq), never materialising [S,S]."""
     return FlashFn.apply(_flash_view(q), _flash_view(k), _flash_view(v), causal, 1.0 / attn_scale)
+
+
+def flash_attention_spliced(q, k, v, causal: bool, attn_scale: float, index, src) -> Optional[torch.Tensor]:
+    """:func:`flash_attention` whose output ``z`` [B,S,Hq,dh] takes ``src[index]`` at ``index`` inside the kernel's
+    store (an interchange splice of ``hook_z``; SpliceFn's gradient: none through the spliced elements).  None when
+    the patch-spec table cannot express the index or ``src`` does not broadcast to z (the caller splices
+    separately); ``IIT_FLASH_SPLICE=0`` disables."""
+    if os.environ.get("IIT_FLASH_SPLICE", "1") == "0":
+        return None
+    from .splice import patch_spec
+    B, S, Hq, dh = q.shape
+    src = src.to(device=q.device, dtype=BF16)
+    spec = patch_spec(index, (B, S, Hq, dh), src)
+    if spec is None or tuple(spec.dims[i][0] for i in range(4)) != (B, S, Hq, dh):
+        return None
+    return FlashFn.apply(_flash_view(q), _flash_view(k), _flash_view(v), causal, 1.0 / attn_scale, src, spec)
 
 
 # ============================================================================ Llama-family fused elementwise ops

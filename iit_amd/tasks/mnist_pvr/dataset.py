@@ -188,20 +188,34 @@ class ImagePVRDataset(Dataset):
         from ``self.rng`` in the same order (so the same patches), then one gather + one slice write on the device
         instead of a per-sample Python loop of image copies.  Returns ``(x', labels' [B], ivs' [B,4])``."""
         idx, k = self.get_idx_and_intermediate(hl_node)
+        js = self.draw_patch_digits(intermediate_vars[:, k].cpu().numpy())
+        return self.apply_patch_digits(x, intermediate_vars, hl_node, js)
+
+    def draw_patch_digits(self, cur: np.ndarray) -> np.ndarray:
+        """The base-dataset indices :meth:`patch_at_hl_idx` draws for a batch whose patched quadrant currently holds
+        classes ``cur``: integer draws only, the same rejection sampling from ``self.rng`` in the same order."""
         tg = _targets(self.base_dataset)
-        tg_np = tg.cpu().numpy() if isinstance(tg, torch.Tensor) else np.asarray(tg)
-        cur = intermediate_vars[:, k].cpu().numpy()
+        tg_np = self.__dict__.get("_tg_np")
+        if tg_np is None:
+            tg_np = self._tg_np = tg.cpu().numpy() if isinstance(tg, torch.Tensor) else np.asarray(tg)
         n = len(self.base_dataset)
+        integers = self.rng.integers
         js = np.empty(len(cur), dtype=np.int64)
-        for i, c in enumerate(cur):  # integer draws only: the rejection sampling of patch_at_hl_idx, in order
+        for i, c in enumerate(cur.tolist()):
             while True:
-                j = int(self.rng.integers(0, n))
-                if int(tg_np[j]) != int(c):
+                j = int(integers(0, n))
+                if tg_np[j] != c:
                     js[i] = j
                     break
+        return js
+
+    def apply_patch_digits(self, x: torch.Tensor, intermediate_vars: torch.Tensor, hl_node: HLNode, js):
+        """Patch quadrant-of-``hl_node`` of every image of ``x`` with base-dataset digits ``js`` (device gather + one
+        slice write); returns ``(x', labels' [B], ivs' [B,4])``."""
+        idx, k = self.get_idx_and_intermediate(hl_node)
         dev = x.device
         data, tgd, _, cmap = self._device_state(dev)
-        jt = torch.from_numpy(js).to(dev)
+        jt = js.to(dev) if isinstance(js, torch.Tensor) else torch.from_numpy(js).to(dev)
         digits = data[jt].float() / 255.0  # [B, s, s]
         if self.pad_size > 0:
             digits = torch.nn.functional.pad(digits, (self.pad_size,) * 4)

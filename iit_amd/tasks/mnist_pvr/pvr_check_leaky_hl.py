@@ -71,7 +71,11 @@ def __getattr__(name):
 def get_corr(mode: str, hook_point: str, model: HookedRootModule, input_shape):
     if mode != "q":
         raise NotImplementedError(mode)
-    shape = hook_output_shape(model, hook_point, input_shape)
+    return corr_for_shape(hook_point, hook_output_shape(model, hook_point, input_shape))
+
+
+def corr_for_shape(hook_point: str, shape):
+    """``get_corr(mode="q")`` for a hook whose output shape is already known."""
     assert shape[2] == shape[3], "Input shape is not square"
     h = shape[2] // 2
     idx = {"tl": Ix[None, None, :h, :h], "tr": Ix[None, None, :h, h:2 * h],

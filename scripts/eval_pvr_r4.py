@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--epochs", type=int, default=10)
     ap.add_argument("--probe-train", type=int, default=10000)
     ap.add_argument("--hook-points", nargs="*", default=None)
+    ap.add_argument("--engines", nargs="*", default=["native", "reference"],
+                    help="native (restructured sweep), native_pernode (one do_intervention per node), reference")
+    ap.add_argument("--skip-info", action="store_true", help="skip eval_information")
     args = ap.parse_args()
     from iit_amd.entry import train as train_entry
     from iit_amd.entry.eval_causality import evaluate_model_on_ablations
@@ -45,21 +48,28 @@ def main():
 
     _, leaky_test = get_dataset("pvr_leaky", dataset_config={"train_size": 1, "test_size": args.test_size})
     res = {}
-    for eng in ("native", "reference"):
+    for eng in args.engines:
         torch.manual_seed(0)
+        # a fresh dataset object per engine: every engine starts from the same patch-draw RNG state
+        _, leaky_test = get_dataset("pvr_leaky", dataset_config={"train_size": 1, "test_size": args.test_size})
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        res[eng] = evaluate_model_on_ablations(ll, "pvr_leaky", leaky_test.base_data,
-                                               {"batch_size": 1024, "engine": eng}, hook_points=hps)
+        ea = {"batch_size": 1024, "engine": "native" if eng.startswith("native") else eng,
+              "fast": eng != "native_pernode"}
+        res[eng] = evaluate_model_on_ablations(ll, "pvr_leaky", leaky_test.base_data, ea, hook_points=hps)
         torch.cuda.synchronize()
         res[eng + "_s"] = time.perf_counter() - t0
         print(f"[pvr] eval_causality {eng}: {res[eng + '_s']:.2f} s", flush=True)
-    keys = [(h, k) for h in hps for k in sorted(res["native"][h])]
-    a = np.array([res["native"][h][k] for h, k in keys])
-    b = np.array([res["reference"][h][k] for h, k in keys])
-    print(f"[pvr] eval_causality: {len(keys)} (hook, HL node) cells; max |native - reference| = "
-          f"{np.abs(a - b).max():.3g}; native range [{a.min():.3f}, {a.max():.3f}]; speedup "
-          f"{res['reference_s'] / res['native_s']:.2f}x", flush=True)
+    first = args.engines[0]
+    keys = [(h, k) for h in hps for k in sorted(res[first][h])]
+    a = np.array([res[first][h][k] for h, k in keys])
+    for other in args.engines[1:]:
+        b = np.array([res[other][h][k] for h, k in keys])
+        print(f"[pvr] eval_causality: {len(keys)} (hook, HL node) cells; max |{first} - {other}| = "
+              f"{np.abs(a - b).max():.3g}; {first} range [{a.min():.3f}, {a.max():.3f}]; {first} is "
+              f"{res[other + '_s'] / res[first + '_s']:.2f}x faster than {other}", flush=True)
+    if args.skip_info:
+        return
 
     tr, te = get_dataset("mnist_pvr", dataset_config={"train_size": args.probe_train, "test_size": args.test_size})
     ltr, lte = get_dataset("pvr_leaky", dataset_config={"train_size": args.probe_train, "test_size": args.test_size})

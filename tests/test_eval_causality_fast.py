@@ -1,0 +1,50 @@
+"""The restructured PVR leakiness sweep (entry/eval_causality.py ``_fast_resample_sweep``: twelve HL nodes per
+launch sequence, truncated source runs, base prefix shared and spliced runs started at the hook) against the
+per-node path (one ``do_intervention`` per (hook point, batch, node), the reference loop) on the same patch draws."""
+import numpy as np
+import pytest
+import torch
+
+
+def _setup(test_size, seed=0):
+    from iit_amd.tasks.task_loader import get_alignment, get_dataset
+    torch.manual_seed(seed)
+    _, leaky = get_dataset("pvr_leaky", dataset_config={"train_size": 1, "test_size": test_size, "device": "cpu"})
+    ll, _, _ = get_alignment("mnist_pvr", config={"input_shape": leaky.base_data.get_input_shape(), "device": "cpu"})
+    ll.eval()
+    return ll, leaky.base_data
+
+
+@pytest.mark.parametrize("hooks", [("mod.conv1.hook_point", "mod.layer1.mod.0.mod.conv2.hook_point"),
+                                   ("mod.layer2.mod.0.mod.conv1.hook_point", "mod.layer3.mod.1.mod.conv2.hook_point",
+                                    "mod.layer4.mod.1.mod.conv1.hook_point")])
+def test_fast_sweep_equals_per_node_path(hooks):
+    from iit_amd.entry.eval_causality import evaluate_model_on_ablations
+    ll, ds_a = _setup(48)
+    _, ds_b = _setup(48)
+    fast = evaluate_model_on_ablations(ll, "pvr_leaky", ds_a, {"batch_size": 20}, hook_points=list(hooks))
+    slow = evaluate_model_on_ablations(ll, "pvr_leaky", ds_b, {"batch_size": 20, "fast": False},
+                                       hook_points=list(hooks))
+    assert ds_a.rng.bit_generator.state == ds_b.rng.bit_generator.state  # the same draws, in the same order
+    for h in hooks:
+        assert set(fast[h]) == set(slow[h]) and len(fast[h]) == 12
+        a = np.array([fast[h][k] for k in sorted(fast[h])])
+        b = np.array([slow[h][k] for k in sorted(fast[h])])
+        assert np.abs(a - b).max() <= 1e-6, (h, a, b)
+
+
+def test_hl_output_is_the_patched_label():
+    """The fast sweep takes the HL output of hook_{i}_leaked_to_{j} from the patched batch's label."""
+    from iit_amd.model_pairs import IITProbeSequentialPair
+    from iit_amd.tasks.task_loader import get_alignment
+    ll, ds = _setup(32)
+    x, y, iv = ds.gather(torch.arange(0, 32))
+    _, hl, corr = get_alignment("pvr_leaky", config={"hook_point": "mod.layer1.mod.0.mod.conv1.hook_point",
+                                                     "input_shape": ds.get_input_shape(), "device": "cpu"})
+    pair = IITProbeSequentialPair(ll_model=ll, hl_model=hl, corr=corr)
+    for nd in pair.corr:
+        _, k = ds.get_idx_and_intermediate(nd)
+        js = ds.draw_patch_digits(iv[:, k].numpy())
+        ab = ds.apply_patch_digits(x, iv, nd, js)
+        hl_out, _ = pair.do_intervention((x, y, iv), ab, nd)
+        assert torch.equal(hl_out.long(), ab[1].long()), nd.name

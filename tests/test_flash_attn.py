@@ -97,3 +97,72 @@ def test_long_context_gpt2_hip_backend_matches_torch_backend():
     lb.backward()
     ga, gb = a.blocks[0].attn.W_Q.grad, b.blocks[0].attn.W_Q.grad
     assert rel(ga, gb) < 5e-2
+
+
+@pytest.mark.parametrize("which", ["positions_heads", "dims", "batch_pos", "broadcast_src"])
+def test_flash_general_splice_in_store_equals_splice_pass(which):
+    """flash_attention_spliced (the splice applied by the kernel's output store, dO masked at every backward load)
+    equals flash_attention followed by the separate splice pass (SpliceFn) -- forward bitwise, q/k/v gradients
+    bitwise -- for patch-spec indices the head mask cannot express (VERDICT r4 next #2)."""
+    from iit_amd.core.index import Ix
+    from iit_amd.ops import hip_ops
+    from iit_amd.ops import splice as sp
+    torch.manual_seed(7)
+    B, S, Hq, Hkv, dh = 3, 130, 8, 2, 128
+    idx = {"positions_heads": Ix[None, 5:70, [1, 6], None], "dims": Ix[None, None, 3, 16:80],
+           "batch_pos": Ix[[0, 2], -1, None, None], "broadcast_src": Ix[None, 10:20, 2:4, None]}[which]
+    q = torch.randn(B, S, Hq, dh, device=dev).bfloat16().requires_grad_()
+    k = torch.randn(B, S, Hkv, dh, device=dev).bfloat16().requires_grad_()
+    v = torch.randn(B, S, Hkv, dh, device=dev).bfloat16().requires_grad_()
+    src = torch.randn(B, S, Hq, dh, device=dev).bfloat16()
+    if which == "broadcast_src":
+        src = src[:1]  # broadcast over the batch (stride 0)
+    z = hip_ops.flash_attention_spliced(q, k, v, True, math.sqrt(dh), idx, src)
+    assert z is not None
+    q2, k2, v2 = (t.detach().clone().requires_grad_() for t in (q, k, v))
+    zr = sp.splice(hip_ops.flash_attention(q2, k2, v2, True, math.sqrt(dh)), idx, src)
+    assert torch.equal(z, zr)
+    g = torch.randn(B, S, Hq, dh, device=dev).bfloat16()
+    z.backward(g)
+    zr.backward(g)
+    for a, b in ((q.grad, q2.grad), (k.grad, k2.grad), (v.grad, v2.grad)):
+        assert torch.equal(a, b)
+
+
+def test_llama_hook_z_splice_runs_in_the_flash_store():
+    """A rotary / GQA / RMS model on the torch op backend (the Llama path) with a hook_z splice at S > 16: no
+    splice_kernel launch, same output and gradients as IIT_FLASH_SPLICE=0 (the separate splice pass)."""
+    import os
+    from iit_amd.core.index import Ix
+    from iit_amd.engine.plan import RunPlan
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.ops import hip_kernels as K
+    torch.manual_seed(0)
+    cfg = dict(n_layers=2, d_model=256, n_heads=4, n_key_value_heads=2, d_head=64, d_mlp=512, d_vocab=300, n_ctx=64,
+               act_fn="silu", gated_mlp=True, normalization_type="RMS", positional_embedding_type="rotary",
+               rotary_dim=64, final_rms=True, attention_dir="causal", device=dev, dtype=torch.bfloat16, seed=0)
+    m = HookedTransformer(cfg).set_op_backend("torch")
+    x = torch.randint(0, 300, (2, 48), device=dev)
+    name = "blocks.1.attn.hook_z"
+    src = m.run_capture(torch.randint(0, 300, (2, 48), device=dev), [name])[name]
+    outs = []
+    for env in ("1", "0"):
+        os.environ["IIT_FLASH_SPLICE"] = env
+        try:
+            m.zero_grad(set_to_none=True)
+            calls = []
+            orig = K.splice
+            K.splice = lambda *a, **kw: (calls.append(1), orig(*a, **kw))[1]
+            try:
+                plan = RunPlan.with_splices([(name, Ix[None, 10:40, 1, None], src)])
+                y = m(x, plan=plan).float()
+                y.logsumexp(-1).mean().backward()
+            finally:
+                K.splice = orig
+            outs.append((y.detach(), m.blocks[0].attn.W_Q.grad.clone(), len(calls)))
+        finally:
+            os.environ.pop("IIT_FLASH_SPLICE", None)
+    (y1, g1, c1), (y0, g0, c0) = outs
+    assert c1 == 0 and c0 >= 2  # forward splice + backward gradient mask as separate passes only with the switch off
+    assert torch.equal(y1, y0)
+    assert torch.equal(g1, g0)
