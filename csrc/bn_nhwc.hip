@@ -1,0 +1,307 @@
+// Fused BatchNorm (+ residual add) (+ ReLU) for NHWC (channels-last) bf16 activations -- the PVR ResNet-18's
+// normalisation, forward and backward, in place of MIOpenBatchNormFwdTrainSpatial / MIOpenBatchNormBwdSpatial plus
+// the separate ReLU, residual-add and running-statistics kernels (profiles/bench_family_pvr_resnet18_r4.txt: 5.0 ms
+// of norm and ~3 ms of elementwise per bf16 step).
+//
+// Layout: x [M][C] (M = N * H * W rows, C channels contiguous, C % 8 == 0); one thread owns 8 consecutive channels
+// of a row (one 16-B load / store), a wave covers 64 / (C / 8) rows at once.
+//
+// Forward (training): stats pass -- per-channel sum and sum of squares in fp32, reduced in LDS per workgroup and
+// added with one fp32 atomic per channel per workgroup into a per-module accumulator; the LAST workgroup to finish
+// (a ticket) reads the totals back with atomics, writes mean / rstd for the apply pass and the backward, updates the
+// running mean / unbiased variance with the momentum, increments num_batches_tracked (torch.nn.BatchNorm2d's buffer
+// semantics) and re-zeroes the accumulator and the ticket for the next call (no memset launch) -- then the apply pass
+// writes y = relu(x * scale + shift (+ res)) in bf16.  Eval mode: the apply pass alone, from the running statistics.
+//
+// Backward: dz = dy * (y > 0) (the ReLU mask from the saved bf16 output), a stats pass for sum(dz) and
+// sum(dz * xhat) whose last workgroup also ADDS the weight / bias gradients sum(dz xhat) / sum(dz) into the
+// parameters' gradient buffers (no autograd accumulation launch), then dx = w rstd (dz - sum(dz) / M - xhat
+// sum(dz xhat) / M) (training; eval: w rstd dz) and the residual's gradient dz.
+//
+// Ticket protocol (MI355X_MICROARCH.md hand-off table, producer and consumer in different workgroups of one kernel):
+// the fp32 adds are memory-side atomics; every thread waits vmcnt(0) for its adds before the workgroup barrier, one
+// thread then takes the ticket with a relaxed agent-scope atomic, and the last workgroup reads the totals with atomic
+// read-modify-writes (atomicExch to 0), which also execute at the memory side -- no L2 line of the accumulator is
+// ever read with a plain load, so no acquire-side invalidate is needed either.
+#include "common.h"
+
+namespace {
+
+constexpr int TPB = 256;
+
+struct Row8 {
+  float v[8];
+};
+
+__device__ __forceinline__ Row8 load8(const __bf16* p) {
+  const bf16x8 t = *(const bf16x8*)p;
+  Row8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r.v[e] = bf2f(t[e]);
+  return r;
+}
+
+__device__ __forceinline__ void store8(__bf16* p, const Row8& r) {
+  bf16x8 t;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = f2bf(r.v[e]);
+  *(bf16x8*)p = t;
+}
+
+// block reduction of per-thread [8] pairs (a, b) over the threads sharing a channel group; adds the block totals
+// into acc[c] / acc[C + c] with one atomic per channel
+__device__ __forceinline__ void block_channel_add(const float* a, const float* b, int C, int G, int rpi, int tid,
+                                                  float* acc, float* red) {
+  const int g = tid % G, r = tid / G;
+  if (r < rpi) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(r * G + g) * 16 + e] = a[e];
+      red[(r * G + g) * 16 + 8 + e] = b[e];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < G * 16; i += TPB) {
+    const int gg = i / 16, e = i % 16;
+    float s = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) s += red[(rr * G + gg) * 16 + e];
+    const int c = gg * 8 + (e & 7);
+    atomicAdd(acc + (e < 8 ? c : C + c), s);
+  }
+}
+
+// the last workgroup of a ticketed reduction: every thread waits for its memory-side atomic adds to complete
+// (s_waitcnt vmcnt(0): no L2 writeback is needed, nothing here went through a cache), the workgroup barrier
+// collects them, then one relaxed agent-scope ticket per workgroup -- a full __threadfence() per thread (an L2
+// write-back each) made the stats pass 2.7x slower
+__device__ __forceinline__ bool last_block(unsigned* ticket, int tid, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = t == gridDim.x - 1;
+  }
+  __syncthreads();
+  return *flag;
+}
+
+// acc[0, C) += sum_rows x, acc[C, 2C) += sum_rows x^2; the last workgroup turns the totals into save = (mean, rstd),
+// updates the running statistics and num_batches_tracked, and re-arms acc / ticket
+__global__ __launch_bounds__(TPB) void bn_stats_kernel(const __bf16* __restrict__ x, long M, int C, float* acc,
+                                                       unsigned* ticket, float* __restrict__ save, float* rmean,
+                                                       float* rvar, float eps, float momentum, long long* nbt) {
+  __shared__ float red[TPB * 16];
+  __shared__ int flag;
+  const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
+  const int g = tid % G, r = tid / G;
+  float s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
+  if (r < rpi) {
+    for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
+      const Row8 v = load8(x + row * C + g * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s[e] += v.v[e];
+        q[e] = __builtin_fmaf(v.v[e], v.v[e], q[e]);
+      }
+    }
+  }
+  block_channel_add(s, q, C, G, rpi, tid, acc, red);
+  if (!last_block(ticket, tid, &flag)) return;
+  for (int c = tid; c < C; c += TPB) {
+    const float sum = atomicExch(acc + c, 0.f), sq = atomicExch(acc + C + c, 0.f);
+    const float mean = sum / (float)M;
+    const float var = fmaxf(sq / (float)M - mean * mean, 0.f);
+    save[c] = mean;
+    save[C + c] = rsqrtf(var + eps);
+    if (rmean) {
+      const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+    }
+  }
+  if (tid == 0) {
+    if (nbt) nbt[0] += 1;
+    atomicExch(ticket, 0u);
+  }
+}
+
+// y = relu?(x * scale + shift (+ res)); training: mean / rstd from ``save`` (the stats kernel); eval: from the running
+// statistics, and workgroup 0 writes them to ``save`` for the backward
+__global__ __launch_bounds__(TPB) void bn_apply_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ res,
+                                                       __bf16* __restrict__ y, float* __restrict__ save,
+                                                       const float* __restrict__ rmean, const float* __restrict__ rvar,
+                                                       const float* __restrict__ w, const float* __restrict__ b, long M,
+                                                       int C, float eps, int relu, int batch) {
+  const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
+  const int g = tid % G, r = tid / G;
+  if (!batch && blockIdx.x == 0) {
+    for (int c = tid; c < C; c += TPB) {
+      save[c] = rmean[c];
+      save[C + c] = rsqrtf(rvar[c] + eps);
+    }
+  }
+  if (r >= rpi) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = g * 8 + e;
+    const float mean = batch ? save[c] : rmean[c];
+    const float rstd = batch ? save[C + c] : rsqrtf(rvar[c] + eps);
+    sc[e] = w[c] * rstd;
+    sh[e] = b[c] - mean * sc[e];
+  }
+  for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
+    Row8 v = load8(x + row * C + g * 8);
+    if (res) {
+      const Row8 rv = load8(res + row * C + g * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v.v[e] = __builtin_fmaf(v.v[e], sc[e], sh[e]) + rv.v[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v.v[e] = __builtin_fmaf(v.v[e], sc[e], sh[e]);
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v.v[e] = fmaxf(v.v[e], 0.f);
+    }
+    store8(y + row * C + g * 8, v);
+  }
+}
+
+// acc[0, C) += sum dz, acc[C, 2C) += sum dz * xhat   (dz = dy masked by y > 0 when y is given)
+__global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ y,
+                                                           const __bf16* __restrict__ x, const float* __restrict__ save,
+                                                           long M, int C, float* acc, unsigned* ticket,
+                                                           float* __restrict__ coef, float* dw, float* db) {
+  __shared__ float red[TPB * 16];
+  __shared__ int flag;
+  const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
+  const int g = tid % G, r = tid / G;
+  float s[8], q[8], mean[8], rstd[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s[e] = q[e] = 0.f;
+    mean[e] = save[g * 8 + e];
+    rstd[e] = save[C + g * 8 + e];
+  }
+  if (r < rpi) {
+    for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
+      const long o = row * C + g * 8;
+      Row8 d = load8(dy + o);
+      const Row8 xv = load8(x + o);
+      if (y) {
+        const bf16x8 yv = *(const bf16x8*)(y + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d.v[e] = bf2f(yv[e]) > 0.f ? d.v[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s[e] += d.v[e];
+        q[e] = __builtin_fmaf(d.v[e], (xv.v[e] - mean[e]) * rstd[e], q[e]);
+      }
+    }
+  }
+  block_channel_add(s, q, C, G, rpi, tid, acc, red);
+  if (!last_block(ticket, tid, &flag)) return;
+  for (int c = tid; c < C; c += TPB) {  // coef = (sum dz, sum dz xhat); parameter gradients accumulated
+    const float sdz = atomicExch(acc + c, 0.f), sdzx = atomicExch(acc + C + c, 0.f);
+    coef[c] = sdz;
+    coef[C + c] = sdzx;
+    if (dw) dw[c] += sdzx;
+    if (db) db[c] += sdz;
+  }
+  if (tid == 0) atomicExch(ticket, 0u);
+}
+
+__global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ y,
+                                                           const __bf16* __restrict__ x, const float* __restrict__ save,
+                                                           const float* __restrict__ w, const float* __restrict__ acc,
+                                                           long M, int C, int batch, __bf16* __restrict__ dx,
+                                                           __bf16* __restrict__ dres) {
+  const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
+  const int g = tid % G, r = tid / G;
+  if (r >= rpi) return;
+  float k1[8], k2[8], k3[8], mean[8], rstd[8];
+  const float inv_m = 1.f / (float)M;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = g * 8 + e;
+    mean[e] = save[c];
+    rstd[e] = save[C + c];
+    k1[e] = w[c] * rstd[e];                          // dx = k1 (dz - k2 - xhat k3)
+    k2[e] = batch ? acc[c] * inv_m : 0.f;
+    k3[e] = batch ? acc[C + c] * inv_m : 0.f;
+  }
+  for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
+    const long o = row * C + g * 8;
+    Row8 d = load8(dy + o);
+    if (y) {
+      const bf16x8 yv = *(const bf16x8*)(y + o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d.v[e] = bf2f(yv[e]) > 0.f ? d.v[e] : 0.f;
+    }
+    if (dres) store8(dres + o, d);
+    Row8 out;
+    if (batch) {
+      const Row8 xv = load8(x + o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out.v[e] = k1[e] * (d.v[e] - k2[e] - (xv.v[e] - mean[e]) * rstd[e] * k3[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out.v[e] = k1[e] * d.v[e];
+    }
+    store8(dx + o, out);
+  }
+}
+
+int grid_for(long M, int C) {
+  const int rpi = TPB / (C / 8);
+  const long want = (M + rpi - 1) / rpi;
+  // ~8 rows per thread group: enough work per workgroup to amortise the per-channel atomics, >= 4 workgroups per CU
+  long g = (want + 7) / 8;
+  if (g < 1) g = 1;
+  if (g > 2048) g = 2048;
+  return (int)g;
+}
+
+bool shape_ok(long M, int C, const void* p) {
+  return M > 0 && C >= 8 && C % 8 == 0 && C / 8 <= TPB && (TPB % (C / 8)) == 0 && ((uintptr_t)p & 15) == 0;
+}
+
+}  // namespace
+
+// forward: ws = per-module accumulator (fp32 [2C] + a u32 ticket after it, zero at the first call, re-armed by
+// every call); y = relu?(bn(x) (+ res)); save [2C] = mean, rstd (the batch's in training, the running ones in eval)
+IIT_EXPORT int iit_bn_fwd(const void* x, const void* res, void* y, float* ws, float* rmean, float* rvar,
+                          const float* w, const float* b, long M, int C, float eps, int relu, int training,
+                          float* save, float momentum, long long* nbt, void* stream) {
+  if (!shape_ok(M, C, x) || ((uintptr_t)y & 15) || (res && ((uintptr_t)res & 15))) return (int)hipErrorInvalidValue;
+  if (!rmean || !rvar) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for(M, C);
+  if (training)
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, M, C, ws,
+                       (unsigned*)(ws + 2 * C), save, rmean, rvar, eps, momentum, nbt);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, (const __bf16*)res, (__bf16*)y,
+                     save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training);
+  return (int)hipGetLastError();
+}
+
+// backward: ws as in the forward; coef [2C] scratch; dx (and dres = the residual's gradient when non-null);
+// dw / db (nullable) ACCUMULATED into
+IIT_EXPORT int iit_bn_bwd(const void* dy, const void* y, const void* x, const float* save, const float* w,
+                          float* ws, float* coef, long M, int C, int training, void* dx, void* dres, float* dw,
+                          float* db, void* stream) {
+  if (!shape_ok(M, C, dy) || ((uintptr_t)x & 15) || ((uintptr_t)dx & 15) || (y && ((uintptr_t)y & 15)) ||
+      (dres && ((uintptr_t)dres & 15)))
+    return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for(M, C);
+  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
+                     (const __bf16*)x, save, M, C, ws, (unsigned*)(ws + 2 * C), coef, dw, db);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
+                     (const __bf16*)x, save, w, (const float*)coef, M, C, training, (__bf16*)dx, (__bf16*)dres);
+  return (int)hipGetLastError();
+}

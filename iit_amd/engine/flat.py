@@ -98,7 +98,14 @@ class FlatParams:
             else:
                 n = p.numel()
                 self.slots.append((off, n))
-                self._view_fns.append(lambda buf, o=off, n=n, shape=p.shape: buf[o:o + n].view(shape))
+                if p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last) and not p.is_contiguous():
+                    # a channels-last conv weight keeps its NHWC order in the arena (an NCHW view would make every
+                    # NHWC convolution transpose it on each call)
+                    N_, C_, H_, W_ = p.shape
+                    self._view_fns.append(lambda buf, o=off, n=n, sh=(N_, H_, W_, C_):
+                                          buf[o:o + n].view(sh).permute(0, 3, 1, 2))
+                else:
+                    self._view_fns.append(lambda buf, o=off, n=n, shape=p.shape: buf[o:o + n].view(shape))
                 off += _align(n)
         self.numel = off
         dev = self.params[0].device if self.params else torch.device("cpu")

@@ -27,12 +27,17 @@ def parse(argv=None):
     ap.add_argument("--hook-point", default="mod.layer3.mod.1.mod.conv2.hook_point")
     ap.add_argument("--wandb", action="store_true")
     ap.add_argument("--save", default=None, help="write the LL state_dict here (reference: weights/ll_model/{task}.pt)")
+    ap.add_argument("--conv-benchmark", type=int, default=1,
+                    help="1: MIOpen find mode (torch.backends.cudnn.benchmark) -- the fastest measured convolution "
+                         "solution per shape; the PVR bf16 step 12.5 -> 9.0 ms (profiles/pvr_step_r5.txt)")
     return ap.parse_args(argv)
 
 
 def main(argv=None):
     args = parse(argv)
     pdist.init_distributed()
+    if torch.cuda.is_available():
+        torch.backends.cudnn.benchmark = bool(args.conv_benchmark)
     training_args = {"lr": args.lr, "early_stop": True, "batch_size": args.batch_size}
     dataset_config = {"train_size": args.train_size, "test_size": args.test_size, "batch_size": args.batch_size,
                       "num_workers": 0}

@@ -8,9 +8,11 @@ parameter/buffer names (``conv1``, ``bn1``, ``layer{1..4}.{0,1}.conv{1,2}``,
 ``...downsample.{0,1}``, ``fc``) -- state_dicts are interchangeable -- and hook
 names like ``mod.layer3.mod.1.mod.conv2.hook_point`` after wrapping.
 
-Convolutions and batch norm run through PyTorch-ROCm (MIOpen); pass
-``memory_format=torch.channels_last`` to :func:`resnet18` for the NHWC layout
-MIOpen's MFMA convolution kernels prefer on gfx950.
+Convolutions run through PyTorch-ROCm (MIOpen); pass ``memory_format=torch.channels_last`` to :func:`resnet18`
+for the NHWC layout MIOpen's MFMA convolution kernels prefer on gfx950.  On channels-last bf16 activations (the
+bf16 PVR step: channels-last autocast) every ``BatchNorm -> ReLU`` and ``BatchNorm -> + identity -> ReLU`` chain
+runs as one fused HIP op (:mod:`iit_amd.ops.bn`, ``csrc/bn_nhwc.hip``) unless a hook on one of its sites is live;
+other inputs take the module path.
 """
 from __future__ import annotations
 
@@ -24,6 +26,24 @@ def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
 
 def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, kernel_size=1, stride=stride, bias=False)
+
+
+def _hooked(m: nn.Module) -> bool:
+    """A live hook on a (possibly HookedModuleWrapper-wrapped) module's output or input."""
+    hp, pre = getattr(m, "hook_point", None), getattr(m, "hook_pre", None)
+    return (hp is not None and hp.is_live) or (pre is not None and pre.is_live)
+
+
+def fused_bn_act(bn_m: nn.Module, relu_m, x: torch.Tensor, res: torch.Tensor = None):
+    """``relu(bn(x) (+ res))`` as one fused op when covered (:mod:`iit_amd.ops.bn`), else None; ``relu_m`` None =
+    no activation.  ``bn_m`` / ``relu_m`` may be HookedModuleWrapper-wrapped: a live hook on either refuses."""
+    if not x.is_cuda or x.dtype != torch.bfloat16 or _hooked(bn_m) or (relu_m is not None and _hooked(relu_m)):
+        return None
+    from ..ops import bn as fbn
+    bn = getattr(bn_m, "mod", bn_m)
+    if not isinstance(bn, nn.BatchNorm2d) or not fbn.enabled() or not fbn.covered(x, bn, res):
+        return None
+    return fbn.bn_act(x, bn, res, relu=relu_m is not None)
 
 
 class BasicBlock(nn.Module):
@@ -41,12 +61,22 @@ class BasicBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
+        h = self.conv1(x)
+        out = fused_bn_act(self.bn1, self.relu, h)
+        if out is None:
+            out = self.relu(self.bn1(h))
+        h = self.conv2(out)
         if self.downsample is not None:
-            identity = self.downsample(x)
-        out = out + identity
-        return self.relu(out)
+            identity = None
+            ds = getattr(self.downsample, "mod", self.downsample)  # Sequential(conv1x1, BatchNorm2d), maybe wrapped
+            if not _hooked(self.downsample) and isinstance(ds, nn.Sequential) and len(ds) == 2:
+                identity = fused_bn_act(ds[1], None, ds[0](x))
+            if identity is None:
+                identity = self.downsample(x)
+        out = fused_bn_act(self.bn2, self.relu, h, identity)
+        if out is None:
+            out = self.relu(self.bn2(h) + identity)
+        return out
 
 
 class ResNet(nn.Module):
@@ -80,7 +110,15 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        # a channels-last model gets channels-last activations from the first convolution on (an NCHW batch into
+        # NHWC weights made every MIOpen convolution transpose its operands and kept the fused BN path off)
+        conv = getattr(self.conv1, "mod", self.conv1)
+        if x.dim() == 4 and conv.weight.is_contiguous(memory_format=torch.channels_last) and \
+                not conv.weight.is_contiguous() and not x.is_contiguous(memory_format=torch.channels_last):
+            x = x.contiguous(memory_format=torch.channels_last)
+        h = self.conv1(x)
+        y = fused_bn_act(self.bn1, self.relu, h)
+        x = self.maxpool(y if y is not None else self.relu(self.bn1(h)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -1,0 +1,94 @@
+"""Fused BatchNorm (+ residual add) (+ ReLU) on channels-last bf16 activations (``csrc/bn_nhwc.hip``).
+
+The PVR ResNet-18's ``BatchNorm2d -> ReLU`` and ``BatchNorm2d -> + identity -> ReLU`` chains
+(``/root/reference/iit/tasks/mnist_pvr/get_alignment.py:9-15``: torchvision's BasicBlock) as one autograd op: two
+kernel launches forward (per-channel statistics, then normalise + add + ReLU + running-statistics update) and two
+backward (per-channel sums of dz and dz * xhat, then dx, the residual's gradient and the parameter gradients) in
+place of MIOpen's BatchNorm kernels, the ReLU, the residual add and ``num_batches_tracked += 1``.  Semantics are
+``torch.nn.BatchNorm2d``'s (batch statistics with the biased variance in training, running statistics updated with
+the unbiased variance and ``momentum``; running statistics in eval); the running buffers and ``num_batches_tracked``
+are updated on the device by the forward kernel, so a graph-captured step replays them.
+
+Used by :class:`iit_amd.models.resnet.BasicBlock` / :class:`ResNet` when the activation is a CUDA bf16
+channels-last tensor, the BatchNorm has ``momentum`` set and affine parameters, no hook on the fused sites is live,
+and ``IIT_FUSED_BN`` is not ``0``; everything else takes the module path unchanged.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+from torch.autograd import Function
+
+from . import hip_kernels as K
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def enabled() -> bool:
+    return os.environ.get("IIT_FUSED_BN", "1") != "0" and torch.cuda.is_available() and K.available()
+
+
+def covered(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res: Optional[torch.Tensor] = None) -> bool:
+    if not (x.is_cuda and x.dtype == BF16 and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    C = x.shape[1]
+    if C % 8 or C < 8 or 256 % (C // 8) or not bn.affine or bn.momentum is None:
+        return False
+    if bn.weight.dtype != F32 or bn.bias.dtype != F32 or not bn.track_running_stats or bn.running_mean is None:
+        return False
+    if res is not None and not (res.shape == x.shape and res.dtype == BF16
+                                and res.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    return True
+
+
+def _ws(bn: torch.nn.BatchNorm2d, C: int, device) -> torch.Tensor:
+    """The module's self-re-arming reduction accumulator: 2C floats + a ticket, zero at creation; every kernel call
+    leaves it zero again (csrc/bn_nhwc.hip).  Shared by the forward and backward of every call on the stream."""
+    ws = bn.__dict__.get("_iit_bn_ws")
+    if ws is None or ws.numel() < 2 * C + 1 or ws.device != device:
+        ws = bn.__dict__["_iit_bn_ws"] = torch.zeros(2 * C + 1, dtype=F32, device=device)
+    return ws
+
+
+class BNActFn(Function):
+    @staticmethod
+    def forward(ctx, x, w, b, res, bn, relu):
+        C = x.shape[1]
+        M = x.numel() // C
+        training = bn.training
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        save = torch.empty(2 * C, dtype=F32, device=x.device)
+        K.bn_fwd(x, res, y, _ws(bn, C, x.device), bn.running_mean, bn.running_var, w, b, M, C, float(bn.eps), relu,
+                 training, save, float(bn.momentum), bn.num_batches_tracked)
+        ctx.save_for_backward(x, y if relu else None, save, w)
+        ctx.cfg = (M, C, training, res is not None)
+        ctx.bn = bn
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if dy is None:
+            return None, None, None, None, None, None
+        from .hip_ops import _done, _grad_slot
+        x, y, save, w = ctx.saved_tensors
+        M, C, training, has_res = ctx.cfg
+        bn = ctx.bn
+        dy = dy.to(BF16).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if has_res else None
+        coef = torch.empty(2 * C, dtype=F32, device=x.device)
+        # the weight / bias gradients are added into their gradient buffers by the kernel (no autograd accumulation)
+        dw, db = _grad_slot(bn.weight), _grad_slot(bn.bias)
+        K.bn_bwd(dy, y, x, save, w, _ws(bn, C, x.device), coef, M, C, training, dx, dres, dw, db)
+        _done(bn.weight, bn.bias)
+        return dx, None, None, dres, None, None
+
+
+def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res: Optional[torch.Tensor] = None,
+           relu: bool = True) -> torch.Tensor:
+    """``relu?(bn(x) (+ res))`` fused (the caller checked :func:`covered`)."""
+    return BNActFn.apply(x, bn.weight, bn.bias, res, bn, relu)

@@ -65,6 +65,9 @@ def setup(args, dev):
         seq = 15
     elif args.family == "pvr-resnet18":
         from iit_amd.model_pairs import IITBehaviorModelPair
+        # MIOpen find mode: the fastest measured convolution solution per shape (bf16 step 12.5 -> 9.0 ms,
+        # profiles/pvr_step_r5.txt); IIT_CONV_BENCHMARK=0 keeps MIOpen's immediate-mode heuristic
+        torch.backends.cudnn.benchmark = os.environ.get("IIT_CONV_BENCHMARK", "1") == "1"
         from iit_amd.tasks.task_loader import get_alignment, get_dataset
         n = 20000
         tr_set, te_set = get_dataset("mnist_pvr", {"train_size": n, "test_size": 2048, "device": dev})

@@ -16,7 +16,7 @@ def group_of(k: str) -> str:
         return "gemm"
     if "attn" in k or "flash" in k or "fa_" in k:
         return "attention"
-    if "ln_" in k or "rms_" in k or "batchnorm" in k:
+    if "ln_" in k or "rms_" in k or "batchnorm" in k or "bn_stats" in k or "bn_apply" in k or "bn_bwd" in k:
         return "norm"
     if "adam" in k or "sumsq" in k:
         return "optimizer"
