@@ -24,10 +24,27 @@
 // read-modify-writes (atomicExch to 0), which also execute at the memory side -- no L2 line of the accumulator is
 // ever read with a plain load, so no acquire-side invalidate is needed either.
 #include "common.h"
+#include "splice_spec.h"
 
 namespace {
 
 constexpr int TPB = 256;
+
+// Interchange splice of the BN input (the preceding conv's hook, ``hook_point`` of mode-"q" PVR sites): the
+// activation the kernels read is x' = where(spec, src, x), spec over the logical [N][C][H][W] with src's element
+// strides; the backward zeroes the spliced elements' input gradient (SpliceFn's semantics).  ``hw`` = H * W, ``W``.
+struct XSplice {
+  const __bf16* src;
+  int hw, W;
+  SpliceSpec sp;
+};
+
+// row (n, h, w) of a spliced x: whether the row is inside the spec's batch / spatial ranges, and the source row base
+__device__ __forceinline__ bool xs_row(const XSplice& xs, long row, long& sbase) {
+  const int n = (int)(row / xs.hw), r = (int)(row - (long)n * xs.hw), h = r / xs.W, w = r - h * xs.W;
+  sbase = n * xs.sp.sstride[0] + h * xs.sp.sstride[2] + w * xs.sp.sstride[3];
+  return in_ranges(xs.sp, 0, n) && in_ranges(xs.sp, 2, h) && in_ranges(xs.sp, 3, w);
+}
 
 struct Row8 {
   float v[8];
@@ -39,6 +56,26 @@ __device__ __forceinline__ Row8 load8(const __bf16* p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) r.v[e] = bf2f(t[e]);
   return r;
+}
+
+// x' row segment [c0, c0 + 8) of row ``row`` (the spliced input when xs.src is set); ``hit`` = which of the 8
+// elements came from the source (their input gradient is zero)
+template <bool SP>
+__device__ __forceinline__ Row8 load_x(const __bf16* x, long row, int C, int c0, const XSplice& xs, unsigned& hit) {
+  Row8 v = load8(x + row * C + c0);
+  hit = 0u;
+  if (SP) {
+    long sb;
+    if (xs_row(xs, row, sb)) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (in_ranges(xs.sp, 1, c0 + e)) {
+          v.v[e] = bf2f(xs.src[sb + (long)(c0 + e) * xs.sp.sstride[1]]);
+          hit |= 1u << e;
+        }
+    }
+  }
+  return v;
 }
 
 __device__ __forceinline__ void store8(__bf16* p, const Row8& r) {
@@ -87,9 +124,11 @@ __device__ __forceinline__ bool last_block(unsigned* ticket, int tid, int* flag)
 
 // acc[0, C) += sum_rows x, acc[C, 2C) += sum_rows x^2; the last workgroup turns the totals into save = (mean, rstd),
 // updates the running statistics and num_batches_tracked, and re-arms acc / ticket
+template <bool SP>
 __global__ __launch_bounds__(TPB) void bn_stats_kernel(const __bf16* __restrict__ x, long M, int C, float* acc,
                                                        unsigned* ticket, float* __restrict__ save, float* rmean,
-                                                       float* rvar, float eps, float momentum, long long* nbt) {
+                                                       float* rvar, float eps, float momentum, long long* nbt,
+                                                       XSplice xs) {
   __shared__ float red[TPB * 16];
   __shared__ int flag;
   const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
@@ -99,7 +138,8 @@ __global__ __launch_bounds__(TPB) void bn_stats_kernel(const __bf16* __restrict_
   for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
   if (r < rpi) {
     for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
-      const Row8 v = load8(x + row * C + g * 8);
+      unsigned hit;
+      const Row8 v = load_x<SP>(x, row, C, g * 8, xs, hit);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         s[e] += v.v[e];
@@ -129,11 +169,12 @@ __global__ __launch_bounds__(TPB) void bn_stats_kernel(const __bf16* __restrict_
 
 // y = relu?(x * scale + shift (+ res)); training: mean / rstd from ``save`` (the stats kernel); eval: from the running
 // statistics, and workgroup 0 writes them to ``save`` for the backward
+template <bool SP>
 __global__ __launch_bounds__(TPB) void bn_apply_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ res,
                                                        __bf16* __restrict__ y, float* __restrict__ save,
                                                        const float* __restrict__ rmean, const float* __restrict__ rvar,
                                                        const float* __restrict__ w, const float* __restrict__ b, long M,
-                                                       int C, float eps, int relu, int batch) {
+                                                       int C, float eps, int relu, int batch, XSplice xs) {
   const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
   const int g = tid % G, r = tid / G;
   if (!batch && blockIdx.x == 0) {
@@ -153,7 +194,8 @@ __global__ __launch_bounds__(TPB) void bn_apply_kernel(const __bf16* __restrict_
     sh[e] = b[c] - mean * sc[e];
   }
   for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
-    Row8 v = load8(x + row * C + g * 8);
+    unsigned hit;
+    Row8 v = load_x<SP>(x, row, C, g * 8, xs, hit);
     if (res) {
       const Row8 rv = load8(res + row * C + g * 8);
 #pragma unroll
@@ -171,10 +213,11 @@ __global__ __launch_bounds__(TPB) void bn_apply_kernel(const __bf16* __restrict_
 }
 
 // acc[0, C) += sum dz, acc[C, 2C) += sum dz * xhat   (dz = dy masked by y > 0 when y is given)
+template <bool SP>
 __global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ y,
                                                            const __bf16* __restrict__ x, const float* __restrict__ save,
                                                            long M, int C, float* acc, unsigned* ticket,
-                                                           float* __restrict__ coef, float* dw, float* db) {
+                                                           float* __restrict__ coef, float* dw, float* db, XSplice xs) {
   __shared__ float red[TPB * 16];
   __shared__ int flag;
   const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
@@ -190,7 +233,8 @@ __global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const __bf16* __restr
     for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
       const long o = row * C + g * 8;
       Row8 d = load8(dy + o);
-      const Row8 xv = load8(x + o);
+      unsigned hit;
+      const Row8 xv = load_x<SP>(x, row, C, g * 8, xs, hit);
       if (y) {
         const bf16x8 yv = *(const bf16x8*)(y + o);
 #pragma unroll
@@ -215,11 +259,12 @@ __global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const __bf16* __restr
   if (tid == 0) atomicExch(ticket, 0u);
 }
 
+template <bool SP>
 __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ y,
                                                            const __bf16* __restrict__ x, const float* __restrict__ save,
                                                            const float* __restrict__ w, const float* __restrict__ acc,
                                                            long M, int C, int batch, __bf16* __restrict__ dx,
-                                                           __bf16* __restrict__ dres) {
+                                                           __bf16* __restrict__ dres, XSplice xs) {
   const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
   const int g = tid % G, r = tid / G;
   if (r >= rpi) return;
@@ -244,13 +289,26 @@ __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(const __bf16* __restr
     }
     if (dres) store8(dres + o, d);
     Row8 out;
+    unsigned hit = 0u;
     if (batch) {
-      const Row8 xv = load8(x + o);
+      const Row8 xv = load_x<SP>(x, row, C, g * 8, xs, hit);
 #pragma unroll
       for (int e = 0; e < 8; ++e) out.v[e] = k1[e] * (d.v[e] - k2[e] - (xv.v[e] - mean[e]) * rstd[e] * k3[e]);
     } else {
+      if (SP) {
+        long sb;
+        if (xs_row(xs, row, sb)) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hit |= (in_ranges(xs.sp, 1, g * 8 + e) ? 1u : 0u) << e;
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) out.v[e] = k1[e] * d.v[e];
+    }
+    if (SP && hit) {  // spliced input elements: a constant, no gradient
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if ((hit >> e) & 1u) out.v[e] = 0.f;
     }
     store8(dx + o, out);
   }
@@ -274,18 +332,41 @@ bool shape_ok(long M, int C, const void* p) {
 
 // forward: ws = per-module accumulator (fp32 [2C] + a u32 ticket after it, zero at the first call, re-armed by
 // every call); y = relu?(bn(x) (+ res)); save [2C] = mean, rstd (the batch's in training, the running ones in eval)
+static bool make_xsplice(XSplice& xs, const void* src, const void* spec, long M, int C, int H, int W) {
+  xs = XSplice{};
+  if (!src || !spec) return true;
+  xs.src = (const __bf16*)src;
+  xs.sp = *(const SpliceSpec*)spec;
+  xs.hw = H * W;
+  xs.W = W;
+  return H > 0 && W > 0 && (long)xs.sp.shape[0] * H * W == M && xs.sp.shape[1] == C && xs.sp.shape[2] == H &&
+         xs.sp.shape[3] == W;
+}
+
 IIT_EXPORT int iit_bn_fwd(const void* x, const void* res, void* y, float* ws, float* rmean, float* rvar,
                           const float* w, const float* b, long M, int C, float eps, int relu, int training,
-                          float* save, float momentum, long long* nbt, void* stream) {
+                          float* save, float momentum, long long* nbt, const void* src, const void* spec, int H,
+                          int W, void* stream) {
   if (!shape_ok(M, C, x) || ((uintptr_t)y & 15) || (res && ((uintptr_t)res & 15))) return (int)hipErrorInvalidValue;
   if (!rmean || !rvar) return (int)hipErrorInvalidValue;
+  XSplice xs;
+  if (!make_xsplice(xs, src, spec, M, C, H, W)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for(M, C);
-  if (training)
-    hipLaunchKernelGGL(bn_stats_kernel, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, M, C, ws,
-                       (unsigned*)(ws + 2 * C), save, rmean, rvar, eps, momentum, nbt);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, (const __bf16*)res, (__bf16*)y,
-                     save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training);
+  // the splice-reading instantiations only where a splice is given (the others keep the lean inner loop)
+  if (xs.src) {
+    if (training)
+      hipLaunchKernelGGL(bn_stats_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, M, C, ws,
+                         (unsigned*)(ws + 2 * C), save, rmean, rvar, eps, momentum, nbt, xs);
+    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, (const __bf16*)res,
+                       (__bf16*)y, save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training, xs);
+  } else {
+    if (training)
+      hipLaunchKernelGGL(bn_stats_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, M, C, ws,
+                         (unsigned*)(ws + 2 * C), save, rmean, rvar, eps, momentum, nbt, xs);
+    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, (const __bf16*)res,
+                       (__bf16*)y, save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training, xs);
+  }
   return (int)hipGetLastError();
 }
 
@@ -293,15 +374,24 @@ IIT_EXPORT int iit_bn_fwd(const void* x, const void* res, void* y, float* ws, fl
 // dw / db (nullable) ACCUMULATED into
 IIT_EXPORT int iit_bn_bwd(const void* dy, const void* y, const void* x, const float* save, const float* w,
                           float* ws, float* coef, long M, int C, int training, void* dx, void* dres, float* dw,
-                          float* db, void* stream) {
+                          float* db, const void* src, const void* spec, int H, int W, void* stream) {
   if (!shape_ok(M, C, dy) || ((uintptr_t)x & 15) || ((uintptr_t)dx & 15) || (y && ((uintptr_t)y & 15)) ||
       (dres && ((uintptr_t)dres & 15)))
     return (int)hipErrorInvalidValue;
+  XSplice xs;
+  if (!make_xsplice(xs, src, spec, M, C, H, W)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int grid = grid_for(M, C);
-  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
-                     (const __bf16*)x, save, M, C, ws, (unsigned*)(ws + 2 * C), coef, dw, db);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
-                     (const __bf16*)x, save, w, (const float*)coef, M, C, training, (__bf16*)dx, (__bf16*)dres);
+  if (xs.src) {
+    hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
+                       (const __bf16*)x, save, M, C, ws, (unsigned*)(ws + 2 * C), coef, dw, db, xs);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
+                       (const __bf16*)x, save, w, (const float*)coef, M, C, training, (__bf16*)dx, (__bf16*)dres, xs);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_stats_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
+                       (const __bf16*)x, save, M, C, ws, (unsigned*)(ws + 2 * C), coef, dw, db, xs);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
+                       (const __bf16*)x, save, w, (const float*)coef, M, C, training, (__bf16*)dx, (__bf16*)dres, xs);
+  }
   return (int)hipGetLastError();
 }

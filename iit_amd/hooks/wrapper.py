@@ -27,6 +27,16 @@ class _StopForward(Exception):
     pass
 
 
+# the RunPlan of the plan-driven forward in progress (None outside one): lets a module that fuses a hooked site's
+# consumer into one kernel (iit_amd.models.resnet: a conv hook's splice read by the fused BatchNorm) take the site
+# over instead of running the hook
+_ACTIVE_PLAN = []
+
+
+def active_plan():
+    return _ACTIVE_PLAN[-1] if _ACTIVE_PLAN else None
+
+
 class HookedModuleWrapper(HookedRootModule):
     def __init__(self, mod: nn.Module, name: str = "model", recursive: bool = False, hook_self: bool = True,
                  top_level: bool = True, hook_pre: bool = False):
@@ -94,11 +104,13 @@ class HookedModuleWrapper(HookedRootModule):
             return fn
 
         entries = [(self.hook_dict[n], self.hook_dict[n].add_hook(site(n))) for n in names]
+        _ACTIVE_PLAN.append(plan)
         try:
             out = self.forward(*args, **kwargs)
         except _StopForward:
             return None
         finally:
+            _ACTIVE_PLAN.pop()
             for hp, e in entries:
                 e.alive = False
                 if e in hp.fwd_hooks:

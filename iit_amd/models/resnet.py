@@ -16,6 +16,8 @@ other inputs take the module path.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -34,16 +36,54 @@ def _hooked(m: nn.Module) -> bool:
     return (hp is not None and hp.is_live) or (pre is not None and pre.is_live)
 
 
-def fused_bn_act(bn_m: nn.Module, relu_m, x: torch.Tensor, res: torch.Tensor = None):
+def fused_bn_act(bn_m: nn.Module, relu_m, x: torch.Tensor, res: torch.Tensor = None, splice=None):
     """``relu(bn(x) (+ res))`` as one fused op when covered (:mod:`iit_amd.ops.bn`), else None; ``relu_m`` None =
-    no activation.  ``bn_m`` / ``relu_m`` may be HookedModuleWrapper-wrapped: a live hook on either refuses."""
+    no activation; ``splice`` = (index, src) of the producing conv's hook, applied as the kernels read x.
+    ``bn_m`` / ``relu_m`` may be HookedModuleWrapper-wrapped: a live hook on either refuses."""
     if not x.is_cuda or x.dtype != torch.bfloat16 or _hooked(bn_m) or (relu_m is not None and _hooked(relu_m)):
         return None
     from ..ops import bn as fbn
     bn = getattr(bn_m, "mod", bn_m)
     if not isinstance(bn, nn.BatchNorm2d) or not fbn.enabled() or not fbn.covered(x, bn, res):
         return None
-    return fbn.bn_act(x, bn, res, relu=relu_m is not None)
+    return fbn.bn_act(x, bn, res, relu=relu_m is not None, splice=splice)
+
+
+def _conv_with_splice(conv_m: nn.Module, bn_m: nn.Module, x: torch.Tensor):
+    """(conv output, splice) where ``splice`` = (index, src) when the active plan's only business at the conv's hook
+    is one interchange splice and the fused BatchNorm can take it over: the conv then runs without its hook and the
+    splice is applied by the BatchNorm kernels' reads (no splice pass, csrc/bn_nhwc.hip); else (conv(x), None)."""
+    hp = getattr(conv_m, "hook_point", None)
+    if hp is None or not x.is_cuda or os.environ.get("IIT_BN_SPLICE", "1") == "0" or _hooked(bn_m):
+        return conv_m(x), None
+    from ..hooks.wrapper import active_plan
+    plan = active_plan()
+    name = hp.name
+    spl = plan.splice.get(name) if plan is not None else None
+    if not spl or len(spl) != 1 or spl[0].whole or name in plan.capture or name in plan.scale or \
+            name in plan.zero_grad or len(hp.fwd_hooks) != 1 or hp.bwd_hooks or hp._forward_hooks or \
+            hp._forward_pre_hooks or getattr(conv_m, "hook_pre", None) is not None:
+        return conv_m(x), None
+    h = conv_m.mod(x)  # the conv without its hook: the splice moves into the BatchNorm's reads
+    if h.dtype != torch.bfloat16:
+        return conv_m.hook_point(h), None
+    return h, (spl[0].index, spl[0].src)
+
+
+def _bn_after_conv(conv_m, bn_m, relu_m, x, res=None):
+    """relu?(bn(conv(x)) (+ res)) with the fused BatchNorm (and a conv-hook splice inside it) when covered, else the
+    module path."""
+    h, splice = _conv_with_splice(conv_m, bn_m, x)
+    out = fused_bn_act(bn_m, relu_m, h, res, splice=splice)
+    if out is None:
+        if splice is not None:  # the fused op could not take the splice: run the conv's hook after all
+            h = conv_m.hook_point(h)
+        out = bn_m(h)
+        if res is not None:
+            out = out + res
+        if relu_m is not None:
+            out = relu_m(out)
+    return out
 
 
 class BasicBlock(nn.Module):
@@ -61,11 +101,7 @@ class BasicBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = x
-        h = self.conv1(x)
-        out = fused_bn_act(self.bn1, self.relu, h)
-        if out is None:
-            out = self.relu(self.bn1(h))
-        h = self.conv2(out)
+        out = _bn_after_conv(self.conv1, self.bn1, self.relu, x)
         if self.downsample is not None:
             identity = None
             ds = getattr(self.downsample, "mod", self.downsample)  # Sequential(conv1x1, BatchNorm2d), maybe wrapped
@@ -73,10 +109,7 @@ class BasicBlock(nn.Module):
                 identity = fused_bn_act(ds[1], None, ds[0](x))
             if identity is None:
                 identity = self.downsample(x)
-        out = fused_bn_act(self.bn2, self.relu, h, identity)
-        if out is None:
-            out = self.relu(self.bn2(h) + identity)
-        return out
+        return _bn_after_conv(self.conv2, self.bn2, self.relu, out, identity)
 
 
 class ResNet(nn.Module):
@@ -116,9 +149,7 @@ class ResNet(nn.Module):
         if x.dim() == 4 and conv.weight.is_contiguous(memory_format=torch.channels_last) and \
                 not conv.weight.is_contiguous() and not x.is_contiguous(memory_format=torch.channels_last):
             x = x.contiguous(memory_format=torch.channels_last)
-        h = self.conv1(x)
-        y = fused_bn_act(self.bn1, self.relu, h)
-        x = self.maxpool(y if y is not None else self.relu(self.bn1(h)))
+        x = self.maxpool(_bn_after_conv(self.conv1, self.bn1, self.relu, x))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

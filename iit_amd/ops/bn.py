@@ -56,26 +56,29 @@ def _ws(bn: torch.nn.BatchNorm2d, C: int, device) -> torch.Tensor:
 
 class BNActFn(Function):
     @staticmethod
-    def forward(ctx, x, w, b, res, bn, relu):
+    def forward(ctx, x, w, b, res, bn, relu, src=None, spec=None):
         C = x.shape[1]
         M = x.numel() // C
+        H, W = x.shape[2], x.shape[3]
         training = bn.training
         y = torch.empty_like(x, memory_format=torch.channels_last)
         save = torch.empty(2 * C, dtype=F32, device=x.device)
         K.bn_fwd(x, res, y, _ws(bn, C, x.device), bn.running_mean, bn.running_var, w, b, M, C, float(bn.eps), relu,
-                 training, save, float(bn.momentum), bn.num_batches_tracked)
+                 training, save, float(bn.momentum), bn.num_batches_tracked, src=src, spec=spec, H=H, W=W)
         ctx.save_for_backward(x, y if relu else None, save, w)
-        ctx.cfg = (M, C, training, res is not None)
+        ctx.cfg = (M, C, training, res is not None, H, W)
         ctx.bn = bn
+        ctx.splice = (src, spec)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         if dy is None:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None
         from .hip_ops import _done, _grad_slot
         x, y, save, w = ctx.saved_tensors
-        M, C, training, has_res = ctx.cfg
+        M, C, training, has_res, H, W = ctx.cfg
+        src, spec = ctx.splice
         bn = ctx.bn
         dy = dy.to(BF16).contiguous(memory_format=torch.channels_last)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
@@ -83,12 +86,23 @@ class BNActFn(Function):
         coef = torch.empty(2 * C, dtype=F32, device=x.device)
         # the weight / bias gradients are added into their gradient buffers by the kernel (no autograd accumulation)
         dw, db = _grad_slot(bn.weight), _grad_slot(bn.bias)
-        K.bn_bwd(dy, y, x, save, w, _ws(bn, C, x.device), coef, M, C, training, dx, dres, dw, db)
+        K.bn_bwd(dy, y, x, save, w, _ws(bn, C, x.device), coef, M, C, training, dx, dres, dw, db, src=src, spec=spec,
+                 H=H, W=W)
         _done(bn.weight, bn.bias)
-        return dx, None, None, dres, None, None
+        return dx, None, None, dres, None, None, None, None
 
 
 def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res: Optional[torch.Tensor] = None,
-           relu: bool = True) -> torch.Tensor:
-    """``relu?(bn(x) (+ res))`` fused (the caller checked :func:`covered`)."""
-    return BNActFn.apply(x, bn.weight, bn.bias, res, bn, relu)
+           relu: bool = True, splice=None) -> Optional[torch.Tensor]:
+    """``relu?(bn(x') (+ res))`` fused (the caller checked :func:`covered`); ``splice`` = (index, src): x' = ``x``
+    with ``x'[index] = src[index]`` (an interchange splice of the producing conv's hook, read in place by the
+    kernels; the spliced elements get no gradient).  None when the splice's index is not expressible."""
+    if splice is None:
+        return BNActFn.apply(x, bn.weight, bn.bias, res, bn, relu)
+    from .splice import patch_spec
+    index, src = splice
+    src = src.to(device=x.device, dtype=BF16)
+    spec = patch_spec(index, tuple(x.shape), src)
+    if spec is None or tuple(d[0] for d in spec.dims) != tuple(x.shape):
+        return None
+    return BNActFn.apply(x, bn.weight, bn.bias, res, bn, relu, src, spec)

@@ -85,8 +85,10 @@ _SIGS = {
     "iit_flash_bwd": [c_void_p] * 3 + [c_void_p] * 11 + [c_ull] + [c_int] * 5 + [c_float, c_int, c_void_p, c_void_p],
     "iit_splice": [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_splice_spec_size": [],
-    "iit_bn_fwd": [c_void_p] * 8 + [c_long, c_int, c_float, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p],
-    "iit_bn_bwd": [c_void_p] * 7 + [c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "iit_bn_fwd": [c_void_p] * 8 + [c_long, c_int, c_float, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p,
+                                    c_void_p, c_int, c_int, c_void_p],
+    "iit_bn_bwd": [c_void_p] * 7 + [c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_int, c_int, c_void_p],
     "iit_gemm_glds_set_prof": [c_void_p],
     "iit_gemm_dual_ok": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 7 + [c_void_p] * 4 + [c_long] * 4 + [c_int] * 5,
     "iit_gemm_dual": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 6 + [c_void_p] * 2 + [c_void_p] * 4 + [c_long] * 4
@@ -576,7 +578,7 @@ def flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, head_mask: int, scale: float,
 
 
 def bn_fwd(x, res, y, ws, rmean, rvar, w, b, M: int, C: int, eps: float, relu: bool, training: bool, save,
-           momentum: float, nbt):
+           momentum: float, nbt, src=None, spec=None, H: int = 0, W: int = 0):
     """Fused BatchNorm (+ residual) (+ ReLU) forward over NHWC bf16 rows (csrc/bn_nhwc.hip); ``ws`` = the
     module's self-re-arming accumulator (2C floats + a ticket)."""
     if CHECK_BOUNDS:
@@ -584,16 +586,19 @@ def bn_fwd(x, res, y, ws, rmean, rvar, w, b, M: int, C: int, eps: float, relu: b
             assert _avail(t) >= M * C, "bn_fwd: activation smaller than M x C"
         assert ws.numel() >= 2 * C + 1 and save.numel() >= 2 * C
     _check(lib().iit_bn_fwd(_p(x), _p(res), _p(y), _p(ws), _p(rmean), _p(rvar), _p(w), _p(b), M, C, eps, int(relu),
-                            int(training), _p(save), momentum, _p(nbt), _stream()), "bn_fwd")
+                            int(training), _p(save), momentum, _p(nbt), _p(src), None if spec is None else spec.ptr,
+                            H, W, _stream()), "bn_fwd")
 
 
-def bn_bwd(dy, y, x, save, w, ws, coef, M: int, C: int, training: bool, dx, dres, dw, db):
+def bn_bwd(dy, y, x, save, w, ws, coef, M: int, C: int, training: bool, dx, dres, dw, db, src=None, spec=None,
+           H: int = 0, W: int = 0):
     """Backward of :func:`bn_fwd`; ``dw`` / ``db`` (fp32 [C], nullable) are accumulated into."""
     if CHECK_BOUNDS:
         for t in (dy, x, dx):
             assert _avail(t) >= M * C, "bn_bwd: activation smaller than M x C"
     _check(lib().iit_bn_bwd(_p(dy), _p(y), _p(x), _p(save), _p(w), _p(ws), _p(coef), M, C, int(training), _p(dx),
-                            _p(dres), _p(dw), _p(db), _stream()), "bn_bwd")
+                            _p(dres), _p(dw), _p(db), _p(src), None if spec is None else spec.ptr, H, W, _stream()),
+           "bn_bwd")
 
 
 def zero_ranges(base, starts, lens):

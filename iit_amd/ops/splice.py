@@ -65,8 +65,11 @@ class PatchSpec:
         return self.buf.ctypes.data
 
 
-def patch_spec(index, shape: Tuple[int, ...], src: Optional[torch.Tensor] = None) -> Optional[PatchSpec]:
-    """The range table of ``index`` on a hook of ``shape`` (with ``src``'s strides, broadcast allowed), or None."""
+def patch_spec(index, shape: Tuple[int, ...], src: Optional[torch.Tensor] = None,
+               perm: Optional[Tuple[int, ...]] = None) -> Optional[PatchSpec]:
+    """The range table of ``index`` on a hook of ``shape`` (with ``src``'s strides, broadcast allowed), or None.
+    ``perm``: the table for the activation's memory order instead (e.g. (0, 2, 3, 1) for a channels-last NCHW
+    tensor, whose flat elements run N, H, W, C) -- dimensions, ranges and source strides permuted alike."""
     ranges = index.to_ranges(tuple(shape))
     if ranges is None:
         return None
@@ -75,10 +78,12 @@ def patch_spec(index, shape: Tuple[int, ...], src: Optional[torch.Tensor] = None
         if src.dim() > len(shape) or any(sn not in (1, n) for sn, n in zip(src.shape[::-1], tuple(shape)[::-1])):
             return None
         strides = list(src.expand(tuple(shape)).stride())  # broadcast dimensions get stride 0
+    if perm is not None:
+        shape, ranges, strides = ([x[i] for i in perm] for x in (list(shape), list(ranges), strides))
     dims = _collapse(shape, ranges, strides)
     if dims is None:
         return None
-    key = (tuple(shape), tuple(strides))
+    key = (tuple(shape), tuple(strides), perm)
     cache = getattr(index, "_iit_specs", None)
     if cache is None:
         cache = {}
@@ -97,25 +102,45 @@ def _launch(act, src, out, spec: PatchSpec, mode: int, scale: float = 1.0):
     K.splice(act, src, out, act.numel(), spec.ptr, act.dtype == torch.float32, mode, scale)
 
 
+_CL = (0, 2, 3, 1)  # the memory order of a channels-last NCHW tensor
+
+
+def _channels_last(t: torch.Tensor) -> bool:
+    return t.dim() == 4 and not t.is_contiguous() and t.is_contiguous(memory_format=torch.channels_last)
+
+
 class SpliceFn(Function):
-    """``out = act`` with ``out[index] = src[index]``; gradient: ``g`` with the spliced elements zeroed."""
+    """``out = act`` with ``out[index] = src[index]``; gradient: ``g`` with the spliced elements zeroed.  A
+    channels-last ``act`` keeps its layout (the range table then runs in memory order, ``spec_cl``)."""
 
     @staticmethod
-    def forward(ctx, act, src, spec):
+    def forward(ctx, act, src, spec, spec_cl=None):
+        if spec_cl is not None and _channels_last(act):
+            out = torch.empty_like(act, memory_format=torch.channels_last)
+            _launch(act.permute(_CL), src, out.permute(_CL), spec_cl, MODE_SPLICE)
+            ctx.spec = spec_cl
+            ctx.cl = True
+            return out
         act_c = act.contiguous()
         out = torch.empty_like(act_c)
         _launch(act_c, src, out, spec, MODE_SPLICE)
         ctx.spec = spec
+        ctx.cl = False
         return out
 
     @staticmethod
     def backward(ctx, g):
         if g is None:
-            return None, None, None
+            return None, None, None, None
+        if ctx.cl:
+            g = g.contiguous(memory_format=torch.channels_last)
+            out = torch.empty_like(g, memory_format=torch.channels_last)
+            _launch(g.permute(_CL), None, out.permute(_CL), ctx.spec, MODE_ZERO)
+            return out, None, None, None
         g = g.contiguous()
         out = torch.empty_like(g)
         _launch(g, None, out, ctx.spec, MODE_ZERO)
-        return out, None, None
+        return out, None, None, None
 
 
 class GradMaskFn(Function):
@@ -166,7 +191,8 @@ def splice(act: torch.Tensor, index, src: torch.Tensor) -> Optional[torch.Tensor
     spec = patch_spec(index, tuple(act.shape), src)
     if spec is None:
         return None
-    return SpliceFn.apply(act, src, spec)
+    spec_cl = patch_spec(index, tuple(act.shape), src, perm=_CL) if _channels_last(act) else None
+    return SpliceFn.apply(act, src, spec, spec_cl)
 
 
 def grad_mask(x: torch.Tensor, indices) -> Optional[torch.Tensor]:

@@ -110,3 +110,90 @@ def test_fused_resnet_matches_module_path():
             assert torch.equal(bf, bm), n
         else:
             assert rel(bf, bm) < 1e-2, n
+
+
+@pytest.mark.parametrize("hook", ["mod.layer3.mod.1.mod.conv2.hook_point", "mod.layer1.mod.0.mod.conv1.hook_point",
+                                  "mod.conv1.hook_point"])
+def test_conv_hook_splice_read_by_fused_bn(hook):
+    """A plan splice at a conv hook of the wrapped PVR ResNet (the IIT intervention of train.py) is applied by the
+    fused BatchNorm's reads (no splice_kernel launch) and equals the separate splice pass bitwise: logits, input
+    gradient and every parameter gradient (IIT_BN_SPLICE=0 is the separate pass)."""
+    from iit_amd.core.index import Ix
+    from iit_amd.engine.plan import RunPlan
+    from iit_amd.ops import hip_kernels as K
+    from iit_amd.tasks.task_loader import get_alignment
+    torch.manual_seed(0)
+    ll, _, _ = get_alignment("mnist_pvr", config={"input_shape": (1, 3, 84, 84), "device": dev})
+    ll.to(memory_format=torch.channels_last)
+    xs = torch.rand(32, 3, 84, 84, device=dev)
+    xb = torch.rand(32, 3, 84, 84, device=dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        src = ll.run_capture(xs.contiguous(memory_format=torch.channels_last), [hook])[hook]
+    hw = src.shape[-1] // 2
+    outs = []
+    for env in ("1", "0"):
+        os.environ["IIT_BN_SPLICE"] = env
+        calls = []
+        orig = K.splice
+        K.splice = lambda *a, **kw: (calls.append(1), orig(*a, **kw))[1]
+        try:
+            ll.zero_grad(set_to_none=True)
+            x = xb.clone().requires_grad_()
+            plan = RunPlan.with_splices([(hook, Ix[None, None, :hw, hw:2 * hw], src)])
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = ll(x, plan=plan)
+            y.float().logsumexp(-1).sum().backward()
+        finally:
+            K.splice = orig
+            os.environ.pop("IIT_BN_SPLICE", None)
+        outs.append((y.detach().float(), x.grad.clone(), {n: p.grad.clone() for n, p in ll.named_parameters()},
+                     len(calls)))
+    (y1, gx1, g1, c1), (y0, gx0, g0, c0) = outs
+    assert c1 == 0 and c0 >= 2
+    # the separate pass keeps the activation channels-last, so the same fused BatchNorm reads the spliced copy; the
+    # per-channel statistics are fp32 atomic sums (order varies run to run, as MIOpen's), so the runs agree to bf16
+    # rounding, not bitwise -- the gradient semantics are pinned by test_bn_splice_on_read_exact
+    assert rel(y1, y0) < 2e-2
+
+
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("training", [True, False])
+def test_bn_splice_on_read_exact(res, training):
+    """bn_act with splice=(index, src) equals bn_act on the pre-spliced channels-last input bitwise (forward, running
+    statistics, residual / weight / bias gradients); its input gradient equals the pre-spliced run's with the spliced
+    elements zeroed."""
+    from iit_amd.core.index import Ix
+    from iit_amd.ops import bn as fbn
+    torch.manual_seed(3)
+    N, C, H = 16, 128, 11
+    idx = Ix[None, 32:96, 3:9, :5]
+    x0 = torch.randn(N, C, H, H, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
+    src = torch.randn(N, C, H, H, device=dev).bfloat16()  # NCHW source: strided reads in the kernel
+    r0 = torch.randn_like(x0, memory_format=torch.channels_last) if res else None
+    g0 = torch.randn(N, C, H, H, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for pre in (False, True):
+        bn = torch.nn.BatchNorm2d(C).to(dev).train(training)
+        x = x0.clone()
+        r = r0.clone() if res else None
+        if pre:
+            x = x.clone()
+            x[idx.as_index] = src[idx.as_index]
+        x.requires_grad_()
+        if r is not None:
+            r.requires_grad_()
+        y = fbn.bn_act(x, bn, r, relu=True, splice=None if pre else (idx, src))
+        y.backward(g0)
+        outs.append((y.detach(), x.grad, r.grad if r is not None else None, bn.weight.grad, bn.bias.grad,
+                     bn.running_mean.clone(), bn.running_var.clone()))
+    (y1, dx1, dr1, dw1, db1, rm1, rv1), (y0, dx0, dr0, dw0, db0, rm0, rv0) = outs
+    # equal up to the order of the fp32 atomic statistics sums (a last-bit difference can flip a bf16 rounding)
+    close = lambda a, b: rel(a, b) < 2e-3  # noqa: E731
+    assert close(y1, y0) and close(rm1, rm0) and close(rv1, rv0)
+    assert close(dw1, dw0) and close(db1, db0)
+    if res:
+        assert close(dr1, dr0)
+    assert int((dx1[idx.as_index] != 0).sum()) == 0  # the spliced elements carry no gradient
+    exp = dx0.clone()
+    exp[idx.as_index] = 0
+    assert close(dx1, exp)

@@ -164,3 +164,28 @@ def test_causal_graph_step_has_no_index_put_splice():
             assert launches, node  # the LL splice ran on a fused kernel
     finally:
         K.splice, K.attn_pair_fwd_spec, K.sparse_pair = orig, orig_attn, orig_sparse
+
+
+@pytest.mark.gpu
+def test_splice_channels_last_keeps_layout_and_matches_nchw():
+    """SpliceFn on a channels-last activation splices in memory order (range table permuted to N, H, W, C): the
+    output stays channels-last and equals the NCHW splice; the backward zeroes the same elements."""
+    from iit_amd.core.index import Ix
+    from iit_amd.ops import splice as sp
+    torch.manual_seed(0)
+    x = torch.randn(4, 64, 11, 11, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    src = torch.randn(4, 64, 11, 11, device="cuda").bfloat16()
+    idx = Ix[None, 8:40, :5, 5:10]
+    xa = x.detach().clone().requires_grad_()
+    xb = x.detach().contiguous().requires_grad_()
+    ya = sp.splice(xa, idx, src)
+    yb = sp.splice(xb, idx, src)
+    assert ya.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(ya, yb)
+    g = torch.randn_like(yb)
+    ya.backward(g)
+    yb.backward(g)
+    assert torch.equal(xa.grad, xb.grad)
+    exp = g.clone()
+    exp[idx.as_index] = 0
+    assert torch.equal(xb.grad, exp)
