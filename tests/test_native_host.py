@@ -13,8 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
 def test_host_checks_under_asan(tmp_path):
     exe = str(tmp_path / "host_checks")
-    src = [os.path.join(ROOT, "tests", "native", "host_checks.cpp"), os.path.join(ROOT, "csrc", "gemm_glds.hip"),
-           os.path.join(ROOT, "csrc", "kernels.hip"), os.path.join(ROOT, "csrc", "splice.hip")]
+    # gemm_glds.hip dispatches its 256 x 256 tiles to gemm_8ph.hip / gemm_4w.hip: link them too
+    src = [os.path.join(ROOT, "tests", "native", "host_checks.cpp")] + [
+        os.path.join(ROOT, "csrc", f) for f in ("gemm_glds.hip", "gemm_8ph.hip", "gemm_4w.hip", "kernels.hip",
+                                                "splice.hip")]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "csrc"),
            "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer", "-o", exe] + src
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
