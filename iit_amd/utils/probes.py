@@ -117,7 +117,52 @@ def train_probes_on_model_pair(model_pair, input_shape, train_set, training_args
     return {"probes": probes, "loss": losses, "accuracy": accs}
 
 
+def _evaluate_probes_cached(probes, model_pair, test_set, criterion, bs: int = 256):
+    """:func:`evaluate_probe` with ONE capture pass over the test set for all probes: the probed activations of every
+    sample are captured once (natural order, the evaluation's batch size) and each probe then walks its own shuffled
+    batches over them -- the same ``randperm`` draw per probe as the per-probe loop, so the same batches -- instead of
+    a truncated forward per (probe, batch): 4-12x fewer forwards per hook point on the PVR sweeps."""
+    n = len(test_set)
+    nodes = {hl: _nodes(v) for hl, v in model_pair.corr.items()}
+    if any(len(v) != 1 for v in nodes.values()):
+        raise NotImplementedError("probing a union of LL nodes is not supported")
+    names = sorted({v[0].name for v in nodes.values()})
+    acts = {hl: [] for hl in probes}
+    ivs = []
+    with torch.no_grad():
+        for s0 in range(0, n, bs):
+            x, _, iv = test_set.gather(torch.arange(s0, min(n, s0 + bs), device=DEVICE))
+            cache = capture_hooks(model_pair.ll_model, x, names)
+            for hl in probes:
+                node = nodes[hl][0]
+                acts[hl].append(cache[node.name][node.index.as_index].reshape(x.shape[0], -1))
+            ivs.append(iv)
+        ivs = torch.cat(ivs)
+        acts = {hl: torch.cat(v) for hl, v in acts.items()}
+    stats = {"test loss": {}, "test accuracy": {}}
+    nb = max(1, _num_batches(test_set, bs))
+    for hl_name, probe in probes.items():
+        probe.eval()
+        loss = torch.zeros((), device=DEVICE)
+        acc = torch.zeros((), device=DEVICE)
+        order = torch.randperm(n).to(DEVICE)  # the per-probe loop's shuffle draw
+        to_gt = model_pair.hl_model.get_idx_to_intermediate(hl_name)
+        with torch.no_grad():
+            for s0 in range(0, n, bs):
+                idx = order[s0:s0 + bs]
+                out = probe(acts[hl_name].index_select(0, idx).to(probe.weight.dtype))
+                gt = to_gt(ivs.index_select(0, idx)).to(DEVICE)
+                loss += criterion(out, gt)
+                acc += (out.argmax(1) == gt).float().mean()
+        stats["test loss"][hl_name] = float(loss) / nb
+        stats["test accuracy"][hl_name] = float(acc) / nb
+    return stats
+
+
 def evaluate_probe(probes, model_pair, test_set, criterion):
+    if not _reference(model_pair) and getattr(test_set, "gather", None) is not None and \
+            getattr(model_pair.ll_model, "supports_run_plan", False):
+        return _evaluate_probes_cached(probes, model_pair, test_set, criterion)
     stats = {"test loss": {}, "test accuracy": {}}
     names = [n.name for v in model_pair.corr.values() for n in _nodes(v)]
     for hl_name, probe in probes.items():

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--engines", nargs="*", default=["native", "reference"],
                     help="native (restructured sweep), native_pernode (one do_intervention per node), reference")
     ap.add_argument("--skip-info", action="store_true", help="skip eval_information")
+    ap.add_argument("--skip-causality", action="store_true", help="skip eval_causality")
     args = ap.parse_args()
     from iit_amd.entry import train as train_entry
     from iit_amd.entry.eval_causality import evaluate_model_on_ablations
@@ -48,7 +49,7 @@ def main():
 
     _, leaky_test = get_dataset("pvr_leaky", dataset_config={"train_size": 1, "test_size": args.test_size})
     res = {}
-    for eng in args.engines:
+    for eng in ([] if args.skip_causality else args.engines):
         torch.manual_seed(0)
         # a fresh dataset object per engine: every engine starts from the same patch-draw RNG state
         _, leaky_test = get_dataset("pvr_leaky", dataset_config={"train_size": 1, "test_size": args.test_size})
@@ -61,9 +62,9 @@ def main():
         res[eng + "_s"] = time.perf_counter() - t0
         print(f"[pvr] eval_causality {eng}: {res[eng + '_s']:.2f} s", flush=True)
     first = args.engines[0]
-    keys = [(h, k) for h in hps for k in sorted(res[first][h])]
+    keys = [(h, k) for h in hps for k in sorted(res[first][h])] if not args.skip_causality else []
     a = np.array([res[first][h][k] for h, k in keys])
-    for other in args.engines[1:]:
+    for other in ([] if args.skip_causality else args.engines[1:]):
         b = np.array([res[other][h][k] for h, k in keys])
         print(f"[pvr] eval_causality: {len(keys)} (hook, HL node) cells; max |{first} - {other}| = "
               f"{np.abs(a - b).max():.3g}; {first} range [{a.min():.3f}, {a.max():.3f}]; {first} is "

@@ -48,3 +48,25 @@ def test_hl_output_is_the_patched_label():
         ab = ds.apply_patch_digits(x, iv, nd, js)
         hl_out, _ = pair.do_intervention((x, y, iv), ab, nd)
         assert torch.equal(hl_out.long(), ab[1].long()), nd.name
+
+
+def test_cached_probe_evaluation_equals_per_probe_loop():
+    """evaluate_probe's one-capture-pass form (native engine) equals the per-probe loop (the reference engine's
+    path, one capture per probe and batch) on the same probes and the same shuffle draws."""
+    from torch import nn
+
+    from iit_amd.entry.eval_information import evaluate_model_on_probes
+    from iit_amd.tasks.task_loader import get_dataset
+    ll, _ = _setup(8)
+    tr, te = get_dataset("pvr_leaky", dataset_config={"train_size": 64, "test_size": 300, "device": "cpu"})
+    hooks = ["mod.layer3.mod.0.mod.conv1.hook_point"]
+    res = {}
+    for eng in ("native", "reference"):
+        torch.manual_seed(0)
+        res[eng] = evaluate_model_on_probes(ll, "pvr_leaky", {"batch_size": 32, "lr": 1e-3, "num_workers": 0,
+                                                              "epochs": 1, "engine": eng},
+                                            tr.base_data, te.base_data, hook_points=hooks)
+    for h in hooks:
+        a, b = res["native"][h]["test accuracy"], res["reference"][h]["test accuracy"]
+        assert set(a) == set(b) and len(a) == 12
+        assert max(abs(a[k] - b[k]) for k in a) <= 1e-6, (h, a, b)
