@@ -22,7 +22,7 @@ from iit_amd.hooks.wrapper import get_hook_points
 from iit_amd.model_pairs import IITProbeSequentialPair
 from iit_amd.tasks.task_loader import get_alignment, get_dataset
 from iit_amd.utils.plotter import plot_probe_stats
-from iit_amd.utils.probes import evaluate_probe, train_probes_on_model_pair
+from iit_amd.utils.probes import ActivationBank, evaluate_probe, train_probes_on_model_pair
 from iit_amd.utils.progress import progress
 
 
@@ -30,18 +30,27 @@ def evaluate_model_on_probes(ll_model, task: str, probe_training_args: dict, tra
                              use_wandb: bool = False, verbose: bool = False, save_probes: bool = False,
                              hook_points=None):
     stats = {}
-    for hook_point in progress(hook_points or get_hook_points(ll_model), desc="Hook points"):
+    hps = hook_points or get_hook_points(ll_model)
+    banks = (None, None)
+    if (probe_training_args.get("engine", "native") == "native" and getattr(ll_model, "supports_run_plan", False)
+            and hasattr(train_set, "gather") and hasattr(test_set, "gather")):
+        # every hook point's activations of every train / test sample, captured once (ActivationBank): the
+        # per-hook-point loop below then trains and evaluates its probes from gathers instead of forwards
+        banks = (ActivationBank(ll_model, train_set, hps, probe_training_args["batch_size"]),
+                 ActivationBank(ll_model, test_set, hps, 256))
+    for hook_point in progress(hps, desc="Hook points"):
         _, hl_model, corr = get_alignment(task, config={"hook_point": hook_point,
                                                         "input_shape": test_set.get_input_shape()})
         pair = IITProbeSequentialPair(ll_model=ll_model, hl_model=hl_model, corr=corr,
                                       training_args=probe_training_args)  # ("engine": "reference" = hook path)
-        out = train_probes_on_model_pair(pair, train_set.get_input_shape(), train_set, probe_training_args)
+        out = train_probes_on_model_pair(pair, train_set.get_input_shape(), train_set, probe_training_args,
+                                         bank=banks[0])
         if save_probes:
             d = os.path.join("weights", "probes", task, hook_point)
             os.makedirs(d, exist_ok=True)
             for k, v in out["probes"].items():
                 torch.save(v.state_dict(), os.path.join(d, f"{k}.pt"))
-        out.update(evaluate_probe(out["probes"], pair, test_set, nn.CrossEntropyLoss()))
+        out.update(evaluate_probe(out["probes"], pair, test_set, nn.CrossEntropyLoss(), bank=banks[1]))
         if verbose:
             print(hook_point, out["test accuracy"])
         stats[hook_point] = out

@@ -80,7 +80,35 @@ def probe_logits(probe: nn.Linear, cache, ll_node: LLNode) -> torch.Tensor:
     return probe(act.reshape(-1, probe.weight.shape[1]).to(probe.weight.dtype))
 
 
-def train_probes_on_model_pair(model_pair, input_shape, train_set, training_args: dict):
+class ActivationBank:
+    """Every named hook's activation for every sample of ``dataset`` (natural order, captured in batches of ``bs``
+    with one truncated forward per batch) plus the samples' intermediate variables: the probe sweeps of
+    ``eval_information`` then train and evaluate every hook point's probes from gathers of these tensors instead of
+    one forward per (hook point, batch) -- and per probe, on the evaluation side.  The batches the probes see are the
+    same draws as the per-batch path (the same ``randperm`` per epoch / per probe)."""
+
+    def __init__(self, ll_model, dataset, names, bs: int = 1024):
+        n = len(dataset)
+        names = sorted(set(names))
+        parts = {nm: [] for nm in names}
+        ivs = []
+        with torch.no_grad():
+            for s0 in range(0, n, bs):
+                x, _, iv = dataset.gather(torch.arange(s0, min(n, s0 + bs), device=DEVICE))
+                cache = capture_hooks(ll_model, x, names)
+                for nm in names:
+                    parts[nm].append(cache[nm])
+                ivs.append(iv)
+        self.n = n
+        self.acts = {nm: torch.cat(v) for nm, v in parts.items()}
+        self.iv = torch.cat(ivs)
+
+    def batch(self, idx: torch.Tensor, names):
+        return {nm: self.acts[nm].index_select(0, idx) for nm in names}, self.iv.index_select(0, idx)
+
+
+def train_probes_on_model_pair(model_pair, input_shape, train_set, training_args: dict,
+                               bank: Optional[ActivationBank] = None):
     probes = construct_probes(model_pair, input_shape=input_shape)
     params = [p for probe in probes.values() for p in probe.parameters()]
     for probe in probes.values():
@@ -94,11 +122,19 @@ def train_probes_on_model_pair(model_pair, input_shape, train_set, training_args
     for _ in range(training_args["epochs"]):
         loss_run = {k: torch.zeros((), device=DEVICE) for k in probes}
         acc_run = {k: torch.zeros((), device=DEVICE) for k in probes}
-        for x, y, int_vars in _batches(train_set, bs, True, training_args.get("num_workers", 0)):
+        if bank is not None:  # the same randperm draw as _batches, the activations gathered from the bank
+            order = torch.randperm(bank.n).to(DEVICE)
+            batches = (bank.batch(order[s0:s0 + bs], names) for s0 in range(0, bank.n, bs))
+        else:
+            batches = ((None, b[2], b[0]) for b in _batches(train_set, bs, True, training_args.get("num_workers", 0)))
+        for item in batches:
+            if bank is not None:
+                cache, int_vars = item
+            else:
+                _, int_vars, x = item
+                with torch.no_grad():
+                    cache = capture_hooks(model_pair.ll_model, x.to(DEVICE), names, _reference(model_pair))
             opt.zero_grad()
-            x = x.to(DEVICE)
-            with torch.no_grad():
-                cache = capture_hooks(model_pair.ll_model, x, names, _reference(model_pair))
             total = 0
             for hl_name, probe in probes.items():
                 gt = model_pair.hl_model.get_idx_to_intermediate(hl_name)(int_vars.to(DEVICE)).to(DEVICE)
@@ -117,7 +153,8 @@ def train_probes_on_model_pair(model_pair, input_shape, train_set, training_args
     return {"probes": probes, "loss": losses, "accuracy": accs}
 
 
-def _evaluate_probes_cached(probes, model_pair, test_set, criterion, bs: int = 256):
+def _evaluate_probes_cached(probes, model_pair, test_set, criterion, bs: int = 256,
+                            bank: Optional[ActivationBank] = None):
     """:func:`evaluate_probe` with ONE capture pass over the test set for all probes: the probed activations of every
     sample are captured once (natural order, the evaluation's batch size) and each probe then walks its own shuffled
     batches over them -- the same ``randperm`` draw per probe as the per-probe loop, so the same batches -- instead of
@@ -127,18 +164,14 @@ def _evaluate_probes_cached(probes, model_pair, test_set, criterion, bs: int = 2
     if any(len(v) != 1 for v in nodes.values()):
         raise NotImplementedError("probing a union of LL nodes is not supported")
     names = sorted({v[0].name for v in nodes.values()})
-    acts = {hl: [] for hl in probes}
-    ivs = []
+    if bank is None:
+        bank = ActivationBank(model_pair.ll_model, test_set, names, bs)
     with torch.no_grad():
-        for s0 in range(0, n, bs):
-            x, _, iv = test_set.gather(torch.arange(s0, min(n, s0 + bs), device=DEVICE))
-            cache = capture_hooks(model_pair.ll_model, x, names)
-            for hl in probes:
-                node = nodes[hl][0]
-                acts[hl].append(cache[node.name][node.index.as_index].reshape(x.shape[0], -1))
-            ivs.append(iv)
-        ivs = torch.cat(ivs)
-        acts = {hl: torch.cat(v) for hl, v in acts.items()}
+        ivs = bank.iv
+        acts = {}
+        for hl in probes:
+            node = nodes[hl][0]
+            acts[hl] = bank.acts[node.name][node.index.as_index].reshape(n, -1)
     stats = {"test loss": {}, "test accuracy": {}}
     nb = max(1, _num_batches(test_set, bs))
     for hl_name, probe in probes.items():
@@ -159,10 +192,10 @@ def _evaluate_probes_cached(probes, model_pair, test_set, criterion, bs: int = 2
     return stats
 
 
-def evaluate_probe(probes, model_pair, test_set, criterion):
+def evaluate_probe(probes, model_pair, test_set, criterion, bank: Optional[ActivationBank] = None):
     if not _reference(model_pair) and getattr(test_set, "gather", None) is not None and \
             getattr(model_pair.ll_model, "supports_run_plan", False):
-        return _evaluate_probes_cached(probes, model_pair, test_set, criterion)
+        return _evaluate_probes_cached(probes, model_pair, test_set, criterion, bank=bank)
     stats = {"test loss": {}, "test accuracy": {}}
     names = [n.name for v in model_pair.corr.values() for n in _nodes(v)]
     for hl_name, probe in probes.items():

@@ -51,15 +51,16 @@ def test_hl_output_is_the_patched_label():
 
 
 def test_cached_probe_evaluation_equals_per_probe_loop():
-    """evaluate_probe's one-capture-pass form (native engine) equals the per-probe loop (the reference engine's
-    path, one capture per probe and batch) on the same probes and the same shuffle draws."""
+    """The native engine's probe sweep (utils/probes.py ActivationBank: every hook point's train / test activations
+    captured once, probes trained and evaluated from gathers) equals the reference engine's path (one capture per
+    hook point and batch for training, one per probe and batch for evaluation) on the same shuffle draws."""
     from torch import nn
 
     from iit_amd.entry.eval_information import evaluate_model_on_probes
     from iit_amd.tasks.task_loader import get_dataset
     ll, _ = _setup(8)
     tr, te = get_dataset("pvr_leaky", dataset_config={"train_size": 64, "test_size": 300, "device": "cpu"})
-    hooks = ["mod.layer3.mod.0.mod.conv1.hook_point"]
+    hooks = ["mod.layer3.mod.0.mod.conv1.hook_point", "mod.layer1.mod.1.mod.conv2.hook_point"]
     res = {}
     for eng in ("native", "reference"):
         torch.manual_seed(0)
@@ -70,3 +71,5 @@ def test_cached_probe_evaluation_equals_per_probe_loop():
         a, b = res["native"][h]["test accuracy"], res["reference"][h]["test accuracy"]
         assert set(a) == set(b) and len(a) == 12
         assert max(abs(a[k] - b[k]) for k in a) <= 1e-6, (h, a, b)
+        la, lb = res["native"][h]["test loss"], res["reference"][h]["test loss"]
+        assert max(abs(la[k] - lb[k]) for k in la) <= 1e-4 * max(1.0, max(abs(v) for v in lb.values())), (h, la, lb)
