@@ -51,6 +51,14 @@ _SYNC_BEFORE_REPLAY = os.environ.get("IIT_GRAPH_SYNC_BEFORE_REPLAY") == "1"  # d
 _RECAPTURE_ALL = os.environ.get("IIT_GRAPH_RECAPTURE_ALL") == "1"  # diagnostics
 
 
+def _join_gathers(optimizer) -> None:
+    """Finish a ZeRO-1 optimizer's deferred all-gathers (``ShardedFusedAdam.wait_gathers``): before a graph replay
+    (a replayed forward calls no gates) and before the weights are read or written wholesale."""
+    wait = getattr(optimizer, "wait_gathers", None)
+    if wait is not None:
+        wait()
+
+
 def _sync_hyper(optimizer) -> None:
     """A captured optimizer step replays the kernel arguments of its capture; the fused Adam reads its learning
     rate (and betas / eps / weight decay) from device scalars, refreshed here when the host values changed (an LR
@@ -58,6 +66,7 @@ def _sync_hyper(optimizer) -> None:
     sync = getattr(optimizer, "sync_hyper", None)
     if sync is not None:
         sync()
+    _join_gathers(optimizer)  # a replayed forward passes no ZeRO-1 gates
 
 
 def _clone_out(out):
@@ -139,6 +148,7 @@ class _TrainState:
 
     def __init__(self, pair, optimizer):
         import copy
+        _join_gathers(optimizer)
         ll = pair._ll_module() if hasattr(pair, "_ll_module") else pair.ll_model
         flat = getattr(ll, "_flat_params", None)
         self.ll, self.flat = ll, flat
@@ -175,6 +185,7 @@ class _TrainState:
     @torch.no_grad()
     def restore(self) -> None:
         opt = self.opt
+        _join_gathers(opt)  # (a gather still in flight would land after the restore)
         for live, saved in self.pairs:
             live.copy_(saved)
         for k, v in self.scalars.items():

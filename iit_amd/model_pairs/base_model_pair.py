@@ -325,6 +325,8 @@ class BaseModelPair(ABC):
                 from ..parallel.zero import ShardedFusedAdam
                 opt = ShardedFusedAdam(flat, flat.buckets(int(self.training_args.get("bucket_mb", 64.0) * (1 << 20))),
                                        lr=lr)
+                if self.training_args.get("zero_overlap_gather", True):
+                    opt.attach_gates(module)  # the all-gather of the updated pieces overlaps the next forward
             else:
                 opt = FusedAdam(flat, lr=lr)
         else:
@@ -341,6 +343,13 @@ class BaseModelPair(ABC):
                                   and not self.rewrites_grads_before_step()
                                   and os.environ.get("IIT_FUSED_NORM", "1") != "0")
         return opt
+
+    def sync_params(self) -> None:
+        """Make every rank's parameters final: finishes the ZeRO-1 optimizer's deferred all-gathers (the next forward
+        finishes them block by block; a direct read of the parameters -- ``state_dict``, a copy -- needs this)."""
+        wait = getattr(getattr(self, "optimizer", None), "wait_gathers", None)
+        if wait is not None:
+            wait()
 
     def rewrites_grads_before_step(self) -> bool:
         """Whether this pair changes parameter gradients between the backward and the optimizer step (beyond the
@@ -526,6 +535,7 @@ class BaseModelPair(ABC):
                 fault_hook(epoch)
             if early_stop and self._check_early_stop_condition(test_metrics.metrics):
                 break
+        self.sync_params()
         # lift the row restriction: later backwards (fine-tuning on other data) may touch any embedding row
         self.restrict_sparse_rows(None)
         if sink is not None:

@@ -677,7 +677,10 @@ class HookedTransformer(HookedRootModule):
         begin = getattr(run.ops, "begin_forward", None)
         if begin is not None:
             begin()
+        gate = self.__dict__.get("_param_gate")  # ZeRO-1 deferred all-gather (parallel/zero.py attach_gates)
         try:
+            if gate is not None:
+                gate(None)
             first = 0 if start_at_layer is None else int(start_at_layer)
             resid = self._embed(tokens, run) if start_at_layer is None else input
             n_blocks = len(self.blocks) if stop_at_layer is None else stop_at_layer
@@ -695,6 +698,8 @@ class HookedTransformer(HookedRootModule):
                     leaf = resid.detach().requires_grad_(True)
                     self._cut_log.append((li, resid, leaf))
                     resid = leaf
+                if gate is not None:
+                    gate(li)
                 resid = block(resid, run, last_only=last_only and li == len(self.blocks) - 1)
             if stop_at_layer is not None:
                 return resid
@@ -721,6 +726,9 @@ class HookedTransformer(HookedRootModule):
 
     # ------------------------------------------------------------------ helpers
     supports_run_plan = True
+    # forward / run_paired call ``_param_gate(None)`` before the first weight read and ``_param_gate(li)`` before
+    # block li (ZeRO-1's all-gather overlapped with the forward, iit_amd/parallel/zero.py)
+    supports_param_gate = True
 
     def run_capture(self, tokens: torch.Tensor, names, truncate: bool = True, base_plan: Optional[RunPlan] = None):
         """Source run of an interchange intervention: no grad, capture ``names`` only, stop early."""
@@ -776,6 +784,9 @@ class HookedTransformer(HookedRootModule):
         tokens = tokens.to(self.embed.W_E.device)
         src_tokens = src_tokens.to(self.embed.W_E.device)
         run = _Run(RunPlan(logits=logits), ops)
+        gate = self.__dict__.get("_param_gate")
+        if gate is not None:
+            gate(None)
         ops.begin_forward()
         n = len(self.blocks)
         final_mlp_site = not cfg.attn_only and self.blocks[-1].mlp.hook_post.name in sites
@@ -794,6 +805,8 @@ class HookedTransformer(HookedRootModule):
                 leaf = base.detach().requires_grad_(True)
                 self._cut_log.append((li, base, leaf))
                 resid = _hip_ops().Paired(leaf, resid.full) if paired else leaf
+            if gate is not None:
+                gate(li)
             if paired:
                 resid, paired = block.forward_paired(resid, run, sites, deepest[2], captures, last_only=lo)
             else:

@@ -16,6 +16,12 @@ on every GPU (``profiles/llama3_8b_kernel_stats_v3.txt``).  With ``ShardedFusedA
      instead of 8 and the pass is ``N`` times shorter;
   4. **all-gather** of the updated fp32 pieces per bucket back into every rank's arena, then the bf16 mirror of the
      bucket is re-derived locally (a cast pass), so the next phase's forward reads identical weights on every rank.
+     On RCCL the gather is in place (each rank's piece is already at its slot of the bucket: no send copy).  With
+     a model that declares ``supports_param_gate`` (the HookedTransformer family) the eager step does not wait:
+     every bucket's gather is issued asynchronously, and the next forward calls the installed gate before the
+     embedding and before each block, which makes the compute stream wait for (and re-derives the mirror of) only
+     the buckets holding that block's weights -- the gathers of later blocks' weights run on the RCCL stream under
+     the earlier blocks' kernels (:meth:`ShardedFusedAdam.attach_gates`).
 
 Bytes on xGMI per optimizer phase equal a ring all-reduce of the gradient (reduce-scatter + all-gather of the same
 size: ``2 (N-1)/N * 4 B`` per parameter); what changes is memory (moments ``/N``) and optimizer time (``/N``).
@@ -145,6 +151,10 @@ class ShardedFusedAdam(FusedAdam):
         self.exp_avg_sq = torch.zeros(plan.numel, dtype=torch.float32, device=dev)
         self.shard_grad = self.flat.grad if self.alias else torch.zeros(plan.numel, dtype=torch.float32, device=dev)
         self._gather_bufs: Dict[tuple, torch.Tensor] = {}
+        self._pending: Dict[int, object] = {}  # bucket -> in-flight all-gather work (deferred gather)
+        self._gate_groups = None               # gate key (None = outside every block, int = block) -> buckets
+        if getattr(self, "_gated_module", None) is not None:  # re-bucketed (staged schedule): re-map the gates
+            self.attach_gates(self._gated_module)
         self._spans_version = None
         self._retired_spans = []
         self._build_spans()
@@ -210,6 +220,7 @@ class ShardedFusedAdam(FusedAdam):
         g = self.param_groups[0]
 
         def host_books():  # eager, first: the host-side counters / hyper-parameters of this step
+            self.wait_gathers()
             self.step_count += 1
             self.sync_hyper()
             self._sync_spans()
@@ -255,6 +266,7 @@ class ShardedFusedAdam(FusedAdam):
         if closure is not None:
             with torch.enable_grad():
                 closure()
+        self.wait_gathers()  # (the previous step's deferred gathers, if a forward did not consume them all)
         group = self.param_groups[0]
         lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
         self.step_count += 1
@@ -273,7 +285,7 @@ class ShardedFusedAdam(FusedAdam):
                          skipped=self._skipped_dev if self.nan_guard else None, hyper=self._hyper_dev)
         else:
             self._step_torch(clip_norm, lr, b1, b2, eps, wd, need_norm)
-        self._all_gather()
+        self._all_gather(defer=self._gate_groups is not None)
 
     def _owned_views(self):
         """(arena view, shard view) per bucket for this rank's owned elements."""
@@ -310,15 +322,19 @@ class ShardedFusedAdam(FusedAdam):
             denom = (v.sqrt() / (bc2 ** 0.5)).add_(eps)
             p.addcdiv_(m, denom, value=-lr / bc1)
 
-    def _all_gather(self, mirror: bool = True) -> None:
-        """Every rank's updated pieces back into every arena; with ``mirror`` the bf16 mirror of each bucket is
-        re-derived locally here (``step_parts`` refreshes only the foreign pieces, in a captured part)."""
+    def _all_gather(self, mirror: bool = True, defer: bool = False) -> None:
+        """Every rank's updated pieces back into every arena, one asynchronous collective per bucket; each bucket is
+        then finished (:meth:`_finish`: the compute stream waits for its gather, the padded tail is copied back, the
+        bf16 mirror of its foreign pieces is re-derived if ``mirror``) -- right away, or with ``defer`` when the
+        next forward's gate first needs it (or at :meth:`wait_gathers`).  ``step_parts`` gathers with
+        ``mirror=False``: its captured part refreshes the foreign mirror."""
         flat = self.flat
         world = self.plan.world
-        for bi, (s, e) in enumerate(self.plan.buckets):
-            p = self.plan.piece[bi]
-            a, b = self.plan.own[bi]
-            if world > 1:
+        if world > 1:
+            nccl = dist.get_backend() == "nccl"
+            for bi, (s, e) in enumerate(self.plan.buckets):
+                p = self.plan.piece[bi]
+                a, b = self.plan.own[bi]
                 full = p * world
                 exact = full == e - s
                 out = flat.data[s:e] if exact else self._gather_bufs.get(("out", bi))
@@ -330,29 +346,94 @@ class ShardedFusedAdam(FusedAdam):
                     piece.zero_()
                     if b > a:
                         piece[:b - a].copy_(flat.data[a:b])
-                parts = list(out.split(p))
-                if dist.get_backend() == "nccl":
-                    dist.all_gather_into_tensor(out, piece.clone() if exact else piece)
-                else:
-                    dist.all_gather(parts, piece.clone())
-                if not exact:
-                    flat.data[s:e].copy_(out[:e - s])
-        if mirror and flat.shadow is not None:
-            if self._hip is None:  # the torch path writes no mirror: refresh all of it
-                for s, e in self.plan.buckets:
-                    flat.shadow[s:e].copy_(flat.data[s:e])
-            else:  # the fused pass wrote the owned pieces' mirror
-                self._refresh_foreign_mirror()
+                if nccl:
+                    # in place: the input is this rank's slot of the output (RCCL's in-place all-gather)
+                    work = dist.all_gather_into_tensor(out, piece, async_op=True)
+                else:  # gloo: list form, and its input must not alias the output list
+                    work = dist.all_gather(list(out.split(p)), piece.clone(), async_op=True)
+                self._pending[bi] = (work, mirror)
+        elif mirror and flat.shadow is not None:
+            for bi in range(len(self.plan.buckets)):
+                self._pending[bi] = (None, mirror)
+        if not defer:
+            self.wait_gathers()
         if mirror:
             flat.after_step(mirror_written=flat.shadow is not None)
 
+    def _finish(self, bi: int) -> None:
+        item = self._pending.pop(bi, None)
+        if item is None:
+            return
+        work, mirror = item
+        flat = self.flat
+        s, e = self.plan.buckets[bi]
+        if work is not None:
+            work.wait()  # RCCL: the current stream waits for the collective (no host block)
+            if self.plan.piece[bi] * self.plan.world != e - s:
+                flat.data[s:e].copy_(self._gather_bufs[("out", bi)][:e - s])
+        if mirror and flat.shadow is not None:
+            if self._hip is None:  # the torch path writes no mirror: refresh the whole bucket
+                flat.shadow[s:e].copy_(flat.data[s:e])
+            else:  # the fused pass wrote the owned piece's mirror
+                a, b = self.plan.own[bi]
+                for lo, hi in ([(s, a), (b, e)] if b > a else [(s, e)]):
+                    if hi > lo:
+                        flat.shadow[lo:hi].copy_(flat.data[lo:hi])
+
+    def wait_gathers(self) -> None:
+        """Finish every in-flight bucket gather (checkpointing, the next step, a graph replay, a non-gated read)."""
+        for bi in sorted(self._pending):
+            self._finish(bi)
+
+    def attach_gates(self, module: torch.nn.Module) -> bool:
+        """Overlap the deferred all-gather with the next forward (see the module docstring).  ``module`` declares
+        ``supports_param_gate`` and calls ``module._param_gate(key)`` before it reads the weights of block ``key``
+        (``None``: the weights outside ``module.blocks`` -- embeddings, final norm, unembedding -- read first);
+        ``module._param_join`` finishes everything (readers that bypass the gates).  Returns whether installed."""
+        if not getattr(module, "supports_param_gate", False) or not hasattr(module, "blocks"):
+            return False
+        flat = self.flat
+
+        def buckets_of(params):
+            out = set()
+            for p in params:
+                if not flat.owns(p):
+                    continue
+                o = flat.offset_of(p)
+                n = p.numel()
+                for bi, (s, e) in enumerate(self.plan.buckets):
+                    if s < o + n and o < e:
+                        out.add(bi)
+            return out
+
+        in_blocks = set()
+        groups = {}
+        for li, blk in enumerate(module.blocks):
+            ps = list(blk.parameters())
+            in_blocks.update(id(p) for p in ps)
+            groups[li] = sorted(buckets_of(ps))
+        groups[None] = sorted(buckets_of([p for p in module.parameters() if id(p) not in in_blocks]))
+        self._gate_groups = groups
+        self._gated_module = module
+
+        def gate(key):
+            if self._pending:
+                for bi in self._gate_groups.get(key, ()):
+                    self._finish(bi)
+
+        module.__dict__["_param_gate"] = gate
+        module.__dict__["_param_join"] = self.wait_gathers
+        return True
+
     # ------------------------------------------------------------------ checkpointing
     def state_dict(self):
+        self.wait_gathers()
         sd = super().state_dict()
         sd["shard"] = {"world": self.plan.world, "rank": self.plan.rank, "buckets": self.plan.buckets}
         return sd
 
     def load_state_dict(self, sd):
+        self.wait_gathers()
         shard = sd.get("shard")
         if shard is None or shard["world"] != self.plan.world or [tuple(b) for b in shard["buckets"]] != \
                 self.plan.buckets:

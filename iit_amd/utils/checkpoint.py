@@ -180,10 +180,17 @@ def _is_sharded(optimizer) -> bool:
     return optimizer is not None and bool(getattr(optimizer, "sharded", False))
 
 
+def _join_gathers(optimizer) -> None:
+    wait = getattr(optimizer, "wait_gathers", None)  # ZeRO-1 deferred all-gathers (parallel/zero.py)
+    if wait is not None:
+        wait()
+
+
 def save_resume_state(checkpoint_dir: str, model_pair, optimizer, lr_scheduler, epoch: int) -> None:
     """Every rank writes its RNG file (and, for a sharded optimizer, its own moment shard); rank 0 writes model +
     optimizer + scheduler + epoch."""
     os.makedirs(checkpoint_dir, exist_ok=True)
+    _join_gathers(optimizer)
     r = pdist.rank()
     _atomic_torch_save(_rng_state(model_pair), os.path.join(checkpoint_dir, f"resume_rank{r}.pt"))
     sharded = _is_sharded(optimizer)
@@ -209,6 +216,7 @@ def load_resume_state(checkpoint_dir: str, model_pair, optimizer, lr_scheduler) 
     path = os.path.join(checkpoint_dir, "resume_state.pt")
     if not os.path.exists(path):
         return 0
+    _join_gathers(optimizer)  # (an in-flight ZeRO-1 gather would land on the restored weights)
     ll = model_pair._ll_module() if hasattr(model_pair, "_ll_module") else model_pair.ll_model
     dev = next(ll.parameters()).device
     state = torch.load(path, map_location="cpu", weights_only=True)

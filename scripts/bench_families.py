@@ -34,6 +34,8 @@ def parse(argv=None):
                                                          "mqnli-bert-tiny", "pvr-resnet18"])
     ap.add_argument("--seq", type=int, default=6, help="causal-graph prompt length (>= 6; Llama families)")
     ap.add_argument("--zero", type=int, default=0, help="optimizer-state sharding (ZeRO-1) under data parallelism")
+    ap.add_argument("--zero-overlap", type=int, default=1,
+                    help="ZeRO-1: defer the all-gather of the updated pieces to the next forward's per-block gates")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None, help="pairs per GPU per step")
@@ -96,6 +98,7 @@ def setup(args, dev):
         model_name = f"{size} + 8-node arithmetic causal graph"
         seq = args.seq
         pair.training_args["zero"] = bool(args.zero)
+    pair.training_args["zero_overlap_gather"] = bool(args.zero_overlap)
     from iit_amd.parallel import dist as pdist
     pdist.broadcast_module(ll)
     if args.family == "pvr-resnet18":
@@ -130,7 +133,7 @@ def main():
     distributed = pdist.init_distributed()
     rank, world = pdist.rank(), pdist.world_size()
     if torch.cuda.is_available():
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(pdist.local_device_index())  # (0 for every rank under IIT_REHEARSE_ONE_GPU=1)
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     t_setup = time.perf_counter()
     pair, opt, it, step_fn, test_set, model_name, seq = setup(args, dev)
@@ -175,6 +178,10 @@ def main():
     if distributed:
         torch.distributed.all_reduce(dt_t, op=torch.distributed.ReduceOp.MAX)
     dt = float(dt_t.item())
+    pair.optimizer = opt
+    pair.sync_params()
+    flat = getattr(pair._ll_module(), "_flat_params", None)
+    wsum = float(flat.data.double().sum()) if flat is not None else None  # (bitwise-comparable weight checksum)
     metrics = pair.make_test_metrics()
     with torch.no_grad():
         for i, (base, abl) in enumerate(test_set.make_loader(args.batch, 0)):
@@ -196,6 +203,7 @@ def main():
             "setup_s": round(t_setup, 1),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1) if dev.type == "cuda" else None,
             "last_train_losses": {k: round(float(v), 4) for k, v in out.items()} if isinstance(out, dict) else {},
+            "weight_checksum": wsum, "zero": bool(args.zero), "zero_overlap_gather": bool(args.zero_overlap),
         }))
     pdist.destroy()
 

@@ -342,6 +342,16 @@ def _worker_zero(rank, world, port, out_dir, staged=False):
         assert pair._ll_module()._flat_params.inactive_ranges(), "no rows restricted"
     assert isinstance(opt, ShardedFusedAdam) and pair._reducer.shard is opt
     assert opt.alias == (world == 1)
+    # the all-gather of the last step is deferred to the next forward's gates: a direct read finishes it first
+    assert opt._gate_groups is not None
+    if world > 1:
+        assert opt._pending  # issued, not waited for
+        with torch.no_grad():
+            pair.ll_model(base[0])  # the forward's gates finish every bucket, block by block
+        assert not opt._pending
+    pair.optimizer = opt
+    pair.sync_params()
+    assert not opt._pending
     flat = opt.flat
     assert opt.exp_avg.numel() <= flat.numel // world + 64 * len(opt.plan.buckets)  # moments are sharded
     torch.save({n: p.detach().clone() for n, p in pair.ll_model.named_parameters()},

@@ -81,3 +81,19 @@ def test_one_rank_rccl_dp_schedule_matches_single_gpu(monkeypatch, zero):
         assert flipped <= max(2, d.numel() // 200), (n, flipped, d.numel())
         err = float(d.norm() / (pa.detach().float().norm() + 1e-12))
         assert err < 1e-2 or flipped > 0, (n, err)
+
+
+def test_rccl_in_place_all_gather_into_tensor():
+    """ZeRO-1 gathers in place (parallel/zero.py ``_all_gather``: the input is this rank's slot of the output, no
+    send copy): RCCL accepts the aliased buffers through ``all_gather_into_tensor`` and leaves the slot intact."""
+    import torch.distributed as dist
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        out = torch.arange(4096, dtype=torch.float32, device="cuda:0")
+        ref = out.clone()
+        work = dist.all_gather_into_tensor(out, out[0:4096], async_op=True)
+        work.wait()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+    finally:
+        dist.destroy_process_group()
