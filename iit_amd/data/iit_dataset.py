@@ -173,7 +173,12 @@ class DeviceIITLoader:
     def __iter__(self) -> Iterator:
         n = len(self.dataset)
         perm = loader_epoch_permutation(n) if self.shuffle else torch.arange(n)
-        perm = perm.to(self.device)
+        if self.device.type == "cuda":
+            # pinned + asynchronous: a pageable copy would block the host until the GPU drained every queued step,
+            # and the first launches of the next epoch then run on an idle GPU
+            perm = perm.pin_memory().to(self.device, non_blocking=True)
+        else:
+            perm = perm.to(self.device)
         base_t, abl_t = self._device_tables()
         gb = self.global_batch
         for start in range(0, n, gb):

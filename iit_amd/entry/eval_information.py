@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import argparse
 import os
+import time
 from datetime import datetime
 
 import torch
@@ -32,28 +33,47 @@ def evaluate_model_on_probes(ll_model, task: str, probe_training_args: dict, tra
     stats = {}
     hps = hook_points or get_hook_points(ll_model)
     banks = (None, None)
+    timing = os.environ.get("IIT_PROBE_TIMING") == "1"
+    clock = {"bank": 0.0, "train": 0.0, "eval": 0.0}
+
+    def tick(key, t0):
+        if timing:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            clock[key] += time.perf_counter() - t0
+        return time.perf_counter()
+
+    t0 = time.perf_counter()
     if (probe_training_args.get("engine", "native") == "native" and getattr(ll_model, "supports_run_plan", False)
-            and hasattr(train_set, "gather") and hasattr(test_set, "gather")):
+            and hasattr(train_set, "gather") and hasattr(test_set, "gather")
+            and os.environ.get("IIT_PROBE_BANK", "1") != "0"):
         # every hook point's activations of every train / test sample, captured once (ActivationBank): the
         # per-hook-point loop below then trains and evaluates its probes from gathers instead of forwards
         banks = (ActivationBank(ll_model, train_set, hps, probe_training_args["batch_size"]),
                  ActivationBank(ll_model, test_set, hps, 256))
+    t0 = tick("bank", t0)
     for hook_point in progress(hps, desc="Hook points"):
         _, hl_model, corr = get_alignment(task, config={"hook_point": hook_point,
                                                         "input_shape": test_set.get_input_shape()})
         pair = IITProbeSequentialPair(ll_model=ll_model, hl_model=hl_model, corr=corr,
                                       training_args=probe_training_args)  # ("engine": "reference" = hook path)
+        t0 = time.perf_counter()
         out = train_probes_on_model_pair(pair, train_set.get_input_shape(), train_set, probe_training_args,
                                          bank=banks[0])
+        t0 = tick("train", t0)
         if save_probes:
             d = os.path.join("weights", "probes", task, hook_point)
             os.makedirs(d, exist_ok=True)
             for k, v in out["probes"].items():
                 torch.save(v.state_dict(), os.path.join(d, f"{k}.pt"))
         out.update(evaluate_probe(out["probes"], pair, test_set, nn.CrossEntropyLoss(), bank=banks[1]))
+        tick("eval", t0)
         if verbose:
             print(hook_point, out["test accuracy"])
         stats[hook_point] = out
+    if timing:
+        print(f"[probe timing] {task} engine={probe_training_args.get('engine', 'native')} bank={banks[0] is not None}: "
+              + ", ".join(f"{k} {v:.2f} s" for k, v in clock.items()), flush=True)
     return stats
 
 

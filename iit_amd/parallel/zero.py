@@ -332,9 +332,20 @@ class ShardedFusedAdam(FusedAdam):
         world = self.plan.world
         if world > 1:
             nccl = dist.get_backend() == "nccl"
+            import os
+            poison = os.environ.get("IIT_ZERO_POISON") == "1"
             for bi, (s, e) in enumerate(self.plan.buckets):
                 p = self.plan.piece[bi]
                 a, b = self.plan.own[bi]
+                if poison:
+                    # debugging aid: the foreign pieces (master and mirror) are NaN until this bucket is finished, and
+                    # its gather is only issued then (below) -- a reader that bypasses the gates always reads NaN and
+                    # turns the run's losses to NaN
+                    for lo, hi in ([(s, a), (b, e)] if b > a else [(s, e)]):
+                        if hi > lo:
+                            flat.data[lo:hi].fill_(float("nan"))
+                            if flat.shadow is not None:
+                                flat.shadow[lo:hi].fill_(float("nan"))
                 full = p * world
                 exact = full == e - s
                 out = flat.data[s:e] if exact else self._gather_bufs.get(("out", bi))
@@ -348,10 +359,11 @@ class ShardedFusedAdam(FusedAdam):
                         piece[:b - a].copy_(flat.data[a:b])
                 if nccl:
                     # in place: the input is this rank's slot of the output (RCCL's in-place all-gather)
-                    work = dist.all_gather_into_tensor(out, piece, async_op=True)
+                    issue = (lambda out=out, piece=piece: dist.all_gather_into_tensor(out, piece, async_op=True))
                 else:  # gloo: list form, and its input must not alias the output list
-                    work = dist.all_gather(list(out.split(p)), piece.clone(), async_op=True)
-                self._pending[bi] = (work, mirror)
+                    issue = (lambda out=out, piece=piece, p=p:
+                             dist.all_gather(list(out.split(p)), piece.clone(), async_op=True))
+                self._pending[bi] = (issue if poison else issue(), mirror)
         elif mirror and flat.shadow is not None:
             for bi in range(len(self.plan.buckets)):
                 self._pending[bi] = (None, mirror)
@@ -368,6 +380,8 @@ class ShardedFusedAdam(FusedAdam):
         flat = self.flat
         s, e = self.plan.buckets[bi]
         if work is not None:
+            if callable(work):  # (IIT_ZERO_POISON: issued at finish)
+                work = work()
             work.wait()  # RCCL: the current stream waits for the collective (no host block)
             if self.plan.piece[bi] * self.plan.world != e - s:
                 flat.data[s:e].copy_(self._gather_bufs[("out", bi)][:e - s])

@@ -204,6 +204,7 @@ def main():
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1) if dev.type == "cuda" else None,
             "last_train_losses": {k: round(float(v), 4) for k, v in out.items()} if isinstance(out, dict) else {},
             "weight_checksum": wsum, "zero": bool(args.zero), "zero_overlap_gather": bool(args.zero_overlap),
+            "optimizer_skipped_steps": int(getattr(opt, "_skipped_dev", torch.zeros(1)).sum()),
         }))
     pdist.destroy()
 

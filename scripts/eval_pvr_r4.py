@@ -30,6 +30,8 @@ def main():
                     help="native (restructured sweep), native_pernode (one do_intervention per node), reference")
     ap.add_argument("--skip-info", action="store_true", help="skip eval_information")
     ap.add_argument("--skip-causality", action="store_true", help="skip eval_causality")
+    ap.add_argument("--info-engines", nargs="*", default=["native", "reference"],
+                    help="eval_information engines: native (activation bank), native_nobank, reference")
     args = ap.parse_args()
     from iit_amd.entry import train as train_entry
     from iit_amd.entry.eval_causality import evaluate_model_on_ablations
@@ -75,8 +77,18 @@ def main():
     tr, te = get_dataset("mnist_pvr", dataset_config={"train_size": args.probe_train, "test_size": args.test_size})
     ltr, lte = get_dataset("pvr_leaky", dataset_config={"train_size": args.probe_train, "test_size": args.test_size})
     probe_res = {}
-    for eng in ("native", "reference"):
-        pargs = {"batch_size": 1024, "lr": 1e-3, "num_workers": 0, "epochs": 1, "engine": eng}
+    # untimed warm-up: one pass of every engine over the deepest hook point (every conv at every batch size the
+    # timed passes use), so MIOpen's first-call / find cost for those shapes is paid by none of the timed engines
+    for eng in args.info_engines:
+        os.environ["IIT_PROBE_BANK"] = "0" if eng == "native_nobank" else "1"
+        pargs = {"batch_size": 1024, "lr": 1e-3, "num_workers": 0, "epochs": 1,
+                 "engine": "native" if eng.startswith("native") else eng}
+        evaluate_model_on_probes(ll, "mnist_pvr", pargs, tr.base_data, te.base_data, hook_points=hps[-1:])
+    for eng in args.info_engines:
+        # native_nobank: the native engine without the activation bank (one capture per hook point and batch)
+        os.environ["IIT_PROBE_BANK"] = "0" if eng == "native_nobank" else "1"
+        pargs = {"batch_size": 1024, "lr": 1e-3, "num_workers": 0, "epochs": 1,
+                 "engine": "native" if eng.startswith("native") else eng}
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         torch.manual_seed(0)

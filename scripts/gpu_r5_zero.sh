@@ -18,3 +18,11 @@ done
 timeout -k 10 800 python -u scripts/eval_pvr_r4.py --skip-causality > gpurun_out/r5z/info.log 2>&1 \
   || { echo "info failed"; tail -30 gpurun_out/r5z/info.log; exit 1; }
 grep "\[pvr\]" gpurun_out/r5z/info.log
+# Llama-3-8B S=512 kernel breakdown at HEAD (hook_z spliced in the flash-attention store: no splice_kernel rows)
+timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r5z/llprof -o ll -- python3 scripts/bench_families.py \
+  --family llama3-8b-causal --seq 512 --steps 3 --warmup 2 > gpurun_out/r5z/llama_prof.log 2>&1 \
+  || { echo "llama trace failed"; tail -20 gpurun_out/r5z/llama_prof.log; exit 1; }
+grep -E '^\{' gpurun_out/r5z/llama_prof.log | cut -c1-200
+f=$(find gpurun_out/r5z/llprof -name "*kernel_trace.csv" | head -n 1)
+[ -n "$f" ] && python3 scripts/step_breakdown.py "$f" --steps 3 --per-step-adam 3 --top 45 > gpurun_out/r5z/llama_breakdown.txt \
+  && head -12 gpurun_out/r5z/llama_breakdown.txt; grep -c splice_kernel gpurun_out/r5z/llama_breakdown.txt || true; rm -f "$f"
