@@ -386,6 +386,54 @@ __global__ __launch_bounds__(256) void swiglu_splice_bwd_kernel(const __bf16* __
   *((bf16x8*)dup + i) = du;
 }
 
+// Token embedding gather with an interchange splice of its output (``hook_embed``) applied in the producer: out[t, :] =
+// W[tokens[t], :] (bf16 mirror rows, row stride ``ld``) except the elements the patch spec selects, which take the
+// source's value -- W_E[tokens] followed by ``out[idx] = src[idx]`` (base_model_pair.py:151-163) in one pass.  One
+// thread per 8 consecutive features (d a multiple of 8).
+__global__ __launch_bounds__(256) void embed_splice_fwd_kernel(const long* __restrict__ tokens,
+                                                               const __bf16* __restrict__ W, long ld,
+                                                               __bf16* __restrict__ out,
+                                                               const __bf16* __restrict__ src, long n8, int d,
+                                                               SpliceSpec sp) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const long t = i * 8 / d;
+  const int c = (int)(i * 8 - t * d);
+  bf16x8 o = *(const bf16x8*)(W + tokens[t] * ld + c);
+  int c0, c1, c2, c3;
+  spec_coords(sp, i * 8, c0, c1, c2, c3);
+  if (in_ranges(sp, 0, c0) && in_ranges(sp, 1, c1) && in_ranges(sp, 2, c2)) {
+    const long sb = (long)c0 * sp.sstride[0] + (long)c1 * sp.sstride[1] + (long)c2 * sp.sstride[2];
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (in_ranges(sp, 3, c3 + e)) o[e] = src[sb + (long)(c3 + e) * sp.sstride[3]];
+  }
+  *((bf16x8*)out + i) = o;
+}
+
+// The embedding gradient of the spliced gather: grad[tokens[t], :] += dout[t, :] (fp32 grad rows, memory-side fp32
+// atomics as torch's index_add), skipping the spliced elements (a constant from the source run: no gradient).
+template <typename G>
+__global__ __launch_bounds__(256) void embed_splice_bwd_kernel(const long* __restrict__ tokens,
+                                                               const G* __restrict__ dout,
+                                                               float* __restrict__ grad, long ldg, long n8, int d,
+                                                               SpliceSpec sp) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const long t = i * 8 / d;
+  const int c = (int)(i * 8 - t * d);
+  int c0, c1, c2, c3;
+  spec_coords(sp, i * 8, c0, c1, c2, c3);
+  const bool row = in_ranges(sp, 0, c0) && in_ranges(sp, 1, c1) && in_ranges(sp, 2, c2);
+  float* g = grad + tokens[t] * ldg + c;
+  const G* dp = dout + i * 8;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if (row && in_ranges(sp, 3, c3 + e)) continue;
+    atomicAdd(g + e, (float)dp[e]);
+  }
+}
+
 bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
 // IIT_LLAMA_VEC=0 selects the scalar rotary / RMSNorm-dw kernels (A/B and fallback), read once per process
@@ -499,5 +547,32 @@ IIT_EXPORT int iit_swiglu_splice_bwd(const void* dpost, const void* gate, const 
   hipLaunchKernelGGL(swiglu_splice_bwd_kernel, dim3((n8 + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      (const __bf16*)dpost, (const __bf16*)gate, (const __bf16*)up, (__bf16*)dgate, (__bf16*)dup, n8,
                      sp);
+  return (int)hipGetLastError();
+}
+
+// ``tokens`` int64 [T]; ``W`` the bf16 mirror of W_E (row stride ``ld``); ``out`` / ``src`` bf16 over the spec's shape
+// (T * d elements; the spec's innermost dimension a multiple of 8, so 8 consecutive features share its outer coordinates)
+IIT_EXPORT int iit_embed_splice_fwd(const void* tokens, const void* W, long ld, void* out, const void* src, long T,
+                                    int d, const void* spec, void* stream) {
+  const SpliceSpec sp = *(const SpliceSpec*)spec;
+  if (d % 8 || ld % 8 || sp.shape[3] % 8 || !al16(W) || !al16(out)) return (int)hipErrorInvalidValue;
+  const long n8 = T * d / 8;
+  hipLaunchKernelGGL(embed_splice_fwd_kernel, dim3((n8 + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     (const long*)tokens, (const __bf16*)W, ld, (__bf16*)out, (const __bf16*)src, n8, d, sp);
+  return (int)hipGetLastError();
+}
+
+// ``dout`` bf16 (dout_f32 = 0) or fp32 [T, d]; ``grad`` fp32 rows of stride ``ldg``
+IIT_EXPORT int iit_embed_splice_bwd(const void* tokens, const void* dout, int dout_f32, float* grad, long ldg, long T,
+                                    int d, const void* spec, void* stream) {
+  const SpliceSpec sp = *(const SpliceSpec*)spec;
+  if (d % 8 || sp.shape[3] % 8) return (int)hipErrorInvalidValue;
+  const long n8 = T * d / 8;
+  if (dout_f32)
+    hipLaunchKernelGGL(embed_splice_bwd_kernel<float>, dim3((n8 + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const long*)tokens, (const float*)dout, grad, ldg, n8, d, sp);
+  else
+    hipLaunchKernelGGL(embed_splice_bwd_kernel<__bf16>, dim3((n8 + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const long*)tokens, (const __bf16*)dout, grad, ldg, n8, d, sp);
   return (int)hipGetLastError();
 }

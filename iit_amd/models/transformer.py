@@ -650,8 +650,15 @@ class HookedTransformer(HookedRootModule):
         ops = run.ops
         B, S = tokens.shape
         if self.rotary:  # positions enter through the rotary q/k rotation
-            return run.site(self.hook_embed, ops.embed(tokens, self.embed.W_E)).to(
-                torch.float32 if ops.fused else ops.dtype)
+            spl = run.plan.splice.get(self.hook_embed.name) if run.plan is not None else None
+            e = None
+            if spl and len(spl) == 1 and not spl[0].whole and hasattr(ops, "embed_spliced"):
+                # a single interchange splice of hook_embed applied by the gather itself (no splice pass; the
+                # site's scale / gradient mask / hook still run after it)
+                e = ops.embed_spliced(tokens, self.embed.W_E, spl[0].index, spl[0].src)
+            e = run.site(self.hook_embed, e, spliced=True) if e is not None else \
+                run.site(self.hook_embed, ops.embed(tokens, self.embed.W_E))
+            return e.to(torch.float32 if ops.fused else ops.dtype)
         if ops.fused and not (run.live(self.hook_embed) or run.live(self.hook_pos_embed)):
             return ops.embed_pos(tokens, self.embed.W_E, self.pos_embed.W_pos)
         e = run.site(self.hook_embed, ops.embed(tokens, self.embed.W_E))

@@ -80,6 +80,8 @@ _SIGS = {
     "iit_sparse_pair": [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p],
     "iit_gemm_dual_set_group_m": [c_int],
     "iit_swiglu_splice_bwd": [c_void_p] * 5 + [c_long, c_void_p, c_void_p],
+    "iit_embed_splice_fwd": [c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p],
+    "iit_embed_splice_bwd": [c_void_p, c_void_p, c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_void_p],
     "iit_flash_fwd": [c_void_p] * 3 + [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ull] + [c_int] * 5
                      + [c_float, c_int, c_void_p, c_void_p],
     "iit_flash_bwd": [c_void_p] * 3 + [c_void_p] * 11 + [c_ull] + [c_int] * 5 + [c_float, c_int, c_void_p, c_void_p],
@@ -653,6 +655,23 @@ def swiglu_splice_fwd(gate, up, post, src, spec_ptr):
     element order as the spec; see :mod:`iit_amd.ops.splice`)."""
     _check(lib().iit_swiglu_splice_fwd(_p(gate), _p(up), _p(post), _p(src), gate.numel(), spec_ptr, _stream()),
            "swiglu_splice_fwd")
+
+
+def embed_splice_fwd(tokens, W16, out, src, spec_ptr):
+    """``out[t] = W16[tokens[t]]`` (bf16 rows, row stride ``W16.stride(0)``) with the patch spec at host address
+    ``spec_ptr`` spliced from ``src`` (csrc/llama_ops.hip)."""
+    T, d = tokens.numel(), out.shape[-1]
+    if CHECK_BOUNDS:
+        _bounds("embed_splice_fwd", ("out", out, T, d, d))
+    _check(lib().iit_embed_splice_fwd(_p(tokens), _p(W16), W16.stride(0), _p(out), _p(src), T, d, spec_ptr,
+                                      _stream()), "embed_splice_fwd")
+
+
+def embed_splice_bwd(tokens, dout, grad, spec_ptr):
+    """``grad[tokens[t]] += dout[t]`` (fp32 rows) except the spliced elements."""
+    T, d = tokens.numel(), dout.shape[-1]
+    _check(lib().iit_embed_splice_bwd(_p(tokens), _p(dout), int(dout.dtype == torch.float32), _p(grad),
+                                      grad.stride(0), T, d, spec_ptr, _stream()), "embed_splice_bwd")
 
 
 def swiglu_splice_bwd(dpost, gate, up, dgate, dup, spec_ptr):

@@ -879,6 +879,53 @@ def swiglu_spliced(pre, pre_linear, index, src) -> Optional[torch.Tensor]:
     return SwiGLUSpliceFn.apply(pre, pre_linear, src, spec)
 
 
+class EmbedSpliceFn(Function):
+    """``W_E[tokens]`` from the arena's bf16 mirror with an interchange splice of ``hook_embed`` applied in the gather
+    (``csrc/llama_ops.hip`` ``embed_splice_*``): selected elements take ``src``'s value; the backward adds the other
+    elements' gradient into W_E's fp32 grad slot (no dense ``[V, d]`` gradient, as ``TorchOps._MirrorEmbed``)."""
+
+    @staticmethod
+    def forward(ctx, tokens, W_E, flat, src, spec):
+        tok = tokens.reshape(-1).to(torch.int64).contiguous()
+        W16 = flat.shadow_view(W_E)
+        out = torch.empty(*tokens.shape, W_E.shape[-1], dtype=BF16, device=W_E.device)
+        K.embed_splice_fwd(tok, W16, out, src, spec.ptr)
+        ctx.save_for_backward(tok)
+        ctx.p, ctx.flat, ctx.spec = W_E, flat, spec
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (tok,) = ctx.saved_tensors
+        from ..engine import grad_hooks
+        W_E = ctx.p
+        slot = W_E.grad
+        if slot is None:
+            slot = ctx.flat.bind_zero(W_E)
+        g = g.reshape(-1, g.shape[-1])
+        if g.dtype not in (BF16, torch.float32):
+            g = g.float()
+        K.embed_splice_bwd(tok, g.contiguous(), slot, ctx.spec.ptr)
+        grad_hooks.notify(W_E)
+        return None, None, None, None, None
+
+
+def embed_spliced(tokens, W_E, flat, index, src) -> Optional[torch.Tensor]:
+    """``W_E[tokens]`` (bf16 mirror) with ``out[index] = src[index]`` fused into the gather, or None when the
+    patch-spec table cannot express the index / the shapes do not fit (the caller splices separately)."""
+    from .splice import patch_spec
+    d = W_E.shape[-1]
+    if os.environ.get("IIT_EMBED_SPLICE", "1") == "0" or d % 8 or W_E.stride(-1) != 1 or W_E.stride(0) % 8:
+        return None
+    if src.dtype != BF16 or src.device != W_E.device:
+        src = src.to(device=W_E.device, dtype=BF16)
+    shape = tuple(tokens.shape) + (d,)
+    spec = patch_spec(index, shape, src)
+    if spec is None or spec.dims[3][0] % 8:
+        return None
+    return EmbedSpliceFn.apply(tokens, W_E, flat, src, spec)
+
+
 def llama_fused_ok(x: torch.Tensor) -> bool:
     """The Llama-family fused kernels apply: a bf16 activation on the GPU (``IIT_LLAMA_FUSED=0`` disables)."""
     return x.is_cuda and x.dtype == BF16 and os.environ.get("IIT_LLAMA_FUSED", "1") != "0"

@@ -311,6 +311,19 @@ class TorchOps:
                 return m[1][tokens]
         return self.w(W_E)[tokens]
 
+    def embed_spliced(self, tokens, W_E, index, src):
+        """``embed`` with an interchange splice of ``hook_embed`` applied inside the gather (one HIP pass over the
+        bf16 mirror, ``hip_ops.EmbedSpliceFn``), or None when not covered -- the caller then splices separately."""
+        if self.dtype != torch.bfloat16 or W_E.dtype == self.dtype or not tokens.is_cuda:
+            return None
+        m = _arena_mirror(W_E)
+        if m is None:
+            return None
+        from . import hip_ops
+        if not hip_ops.llama_fused_ok(m[1]):
+            return None
+        return hip_ops.embed_spliced(tokens, W_E, m[0], index, src)
+
     def pos_embed(self, batch: int, seq: int, W_pos, offset: int = 0):
         return self.w(W_pos)[offset:offset + seq].unsqueeze(0).expand(batch, seq, W_pos.shape[-1])
 

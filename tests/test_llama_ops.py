@@ -185,3 +185,50 @@ def test_swiglu_splice_in_kernel_matches_separate_pass(monkeypatch, index_kind):
     assert torch.equal(outs[0], outs[1])
     for n in grads[1]:
         assert torch.allclose(grads[0][n], grads[1][n], rtol=1e-3, atol=1e-6), n
+
+
+@pytest.mark.parametrize("index_kind", ["position", "features"])
+def test_embed_splice_in_gather_matches_separate_pass(monkeypatch, index_kind):
+    """A ``hook_embed`` splice applied inside the embedding gather (``csrc/llama_ops.hip`` embed_splice_*) gives the
+    separate patch-spec pass's output and gradients (forward: selected elements = source, exactly; backward: no W_E
+    gradient from the selected elements), and the fused path is the one that ran."""
+    import copy
+    from iit_amd.core.index import Ix
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.engine.plan import RunPlan
+    from iit_amd.models.convert import llama_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.ops import hip_ops
+    cfg = llama_config_dict("llama-tiny", device=dev, dtype=torch.bfloat16)
+    torch.manual_seed(2)
+    a = HookedTransformer(cfg)
+    b = copy.deepcopy(a)
+    FlatParams(a, with_bf16_shadow=True)
+    FlatParams(b, with_bf16_shadow=True)
+    tok = torch.randint(0, cfg["d_vocab"], (4, 24), device=dev)
+    src_tok = torch.randint(0, cfg["d_vocab"], (4, 24), device=dev)
+    name = "hook_embed"
+    d = cfg["d_model"]
+    idx = Ix[:, 3] if index_kind == "position" else Ix[:, [1, 7], : d // 2]
+    calls = []
+    orig = hip_ops.EmbedSpliceFn.apply
+    monkeypatch.setattr(hip_ops.EmbedSpliceFn, "apply", lambda *a_: calls.append(1) or orig(*a_))
+    outs, grads = [], []
+    for model, fused in ((a, "1"), (b, "0")):
+        monkeypatch.setenv("IIT_EMBED_SPLICE", fused)
+        with torch.no_grad():
+            src = model.run_capture(src_tok, [name])[name]
+        out = model(tok, plan=RunPlan.with_splices([(name, idx, src)]))
+        out.float().pow(2).mean().backward()
+        outs.append(out.detach().float())
+        grads.append({n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.grad is not None})
+    assert len(calls) == 1  # the fused gather ran for model a only
+    assert torch.equal(outs[0], outs[1])
+    assert "embed.W_E" in grads[1]
+    for n in grads[1]:
+        assert torch.allclose(grads[0][n], grads[1][n], rtol=1e-3, atol=1e-6), n
+    # the spliced elements take no gradient: a source token's W_E row gets none from a fully spliced position
+    if index_kind == "position":
+        only = set(tok[:, 3].tolist()) - set(tok[:, [i for i in range(24) if i != 3]].flatten().tolist())
+        for t in only:
+            assert float(grads[0]["embed.W_E"][t].abs().max()) == 0.0
