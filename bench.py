@@ -135,12 +135,14 @@ def main():
         for _ in range(args.steps):
             base, abl = next(it)  # the device-side batch gather is part of the timed step
             out = step_fn(base, abl, loss_fn, opt)
+        t_host = time.perf_counter() - t0  # (host enqueue time: close to the wall time = launch-bound)
         if dev.type == "cuda":
             torch.cuda.synchronize()
         pdist.barrier()
         dt = time.perf_counter() - t0
     executed = getattr(step_fn, "calls", None) or (args.warmup + args.steps)
-    print(f"[bench] train steps executed in this process: {executed}", file=sys.stderr)
+    print(f"[bench] train steps executed in this process: {executed}; host enqueue {t_host / args.steps * 1e3:.3f} "
+          f"ms/step of {dt / args.steps * 1e3:.3f} ms/step wall", file=sys.stderr)
     dt_t = torch.tensor([dt], dtype=torch.float64, device=dev if distributed and dev.type == "cuda" else "cpu")
     if distributed:
         torch.distributed.all_reduce(dt_t, op=torch.distributed.ReduceOp.MAX)
