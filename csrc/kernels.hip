@@ -442,6 +442,154 @@ __global__ __launch_bounds__(256) void ln_dwdb_vec_kernel(const void* __restrict
   }
 }
 
+// ln_bwd_vec_kernel with the affine gradients fused: each wave takes R rows (row = block * 4R + 4 r + wave), so a
+// lane keeps the same float4 columns for all of them and sums dy * xhat and dy in registers; the block's 4 waves
+// meet in LDS and write ONE partial row pair (dw part, db part) to ``part[block][2 d]`` with plain stores -- no
+// atomics here (the separate ln_dwdb kernels re-read dy and x and did one memory-side fp32 atomic per column per
+// 32 rows: ~17 us for [3840][768], profiles/mqnli_step_breakdown_r5.txt).  ln_part_reduce_kernel sums the partials.
+constexpr int LN_FUSED_R = 2;
+template <int V4, bool DY_F32>
+__global__ __launch_bounds__(256) void ln_bwd_part_vec_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ rstd,
+                                                              const float* __restrict__ w, float* __restrict__ dx,
+                                                              const float* __restrict__ dres,
+                                                              __bf16* __restrict__ dx16, float* __restrict__ part,
+                                                              int T, int d, int accumulate, RowSel sel) {
+  __shared__ float4 red[2][4][64 * V4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int d4 = d >> 2;
+  float4 pw[V4], pb[V4];
+#pragma unroll
+  for (int i = 0; i < V4; ++i) pw[i] = pb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 ww[V4];
+#pragma unroll
+  for (int i = 0; i < V4; ++i) {
+    const int c = lane + i * 64;
+    ww[i] = (w && c < d4) ? ((const float4*)w)[c] : make_float4(1.f, 1.f, 1.f, 1.f);
+  }
+  // every row's operands are loaded before the first is used: the R rows' memory latency overlaps
+  float4 dyv[LN_FUSED_R][V4], xvv[LN_FUSED_R][V4];
+  float muv[LN_FUSED_R], rsv[LN_FUSED_R];
+#pragma unroll
+  for (int r = 0; r < LN_FUSED_R; ++r) {
+    const int row = blockIdx.x * 4 * LN_FUSED_R + 4 * r + wave;
+    const bool live = row < T && !sel_hit(sel, row);
+    muv[r] = row < T ? mean[row] : 0.f;
+    rsv[r] = row < T ? rstd[row] : 0.f;
+#pragma unroll
+    for (int i = 0; i < V4; ++i) {
+      const int c = lane + i * 64;
+      dyv[r][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      xvv[r][i] = dyv[r][i];
+      if (c < d4 && live) {
+        if (DY_F32) {
+          dyv[r][i] = ((const float4*)dy_)[(long)row * d4 + c];
+        } else {
+          const bf16x4 t = ((const bf16x4*)dy_)[(long)row * d4 + c];
+          dyv[r][i] = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
+        }
+        xvv[r][i] = ((const float4*)x)[(long)row * d4 + c];
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < LN_FUSED_R; ++r) {
+    const int row = blockIdx.x * 4 * LN_FUSED_R + 4 * r + wave;
+    if (row >= T) break;
+    const bool dead = sel_hit(sel, row);
+    const float mu = muv[r], rs = rsv[r];
+    float4 g[V4], xh[V4];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < V4; ++i) {
+      float4 dy = dyv[r][i];
+      const float4 xx = xvv[r][i];
+      const float4 xv = dead ? make_float4(0.f, 0.f, 0.f, 0.f)
+                             : make_float4((xx.x - mu) * rs, (xx.y - mu) * rs, (xx.z - mu) * rs, (xx.w - mu) * rs);
+      // affine partials from the raw dy (dw += dy * xhat, db += dy), then g = dy * w
+      pw[i].x += dy.x * xv.x; pw[i].y += dy.y * xv.y; pw[i].z += dy.z * xv.z; pw[i].w += dy.w * xv.w;
+      pb[i].x += dy.x; pb[i].y += dy.y; pb[i].z += dy.z; pb[i].w += dy.w;
+      dy.x *= ww[i].x; dy.y *= ww[i].y; dy.z *= ww[i].z; dy.w *= ww[i].w;
+      g[i] = dy;
+      xh[i] = xv;
+      sg += (dy.x + dy.y) + (dy.z + dy.w);
+      sgx += (dy.x * xv.x + dy.y * xv.y) + (dy.z * xv.z + dy.w * xv.w);
+    }
+    sg = wave_sum(sg) / d;
+    sgx = wave_sum(sgx) / d;
+#pragma unroll
+    for (int i = 0; i < V4; ++i) {
+      const int c = lane + i * 64;
+      if (c < d4) {
+        float4 o = make_float4(rs * (g[i].x - sg - xh[i].x * sgx), rs * (g[i].y - sg - xh[i].y * sgx),
+                               rs * (g[i].z - sg - xh[i].z * sgx), rs * (g[i].w - sg - xh[i].w * sgx));
+        if (dres) {
+          const float4 q = ((const float4*)dres)[(long)row * d4 + c];
+          o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+        }
+        float4* p = (float4*)dx + (long)row * d4 + c;
+        if (accumulate) {
+          const float4 q = *p;
+          o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+        }
+        *p = o;
+        if (dx16) {
+          bf16x4 ob = {f2bf(o.x), f2bf(o.y), f2bf(o.z), f2bf(o.w)};
+          ((bf16x4*)dx16)[(long)row * d4 + c] = ob;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V4; ++i) {
+    red[0][wave][lane + i * 64] = pw[i];
+    red[1][wave][lane + i * 64] = pb[i];
+  }
+  __syncthreads();
+  // 256 threads write the block's 2 x d4 float4 partials
+  float4* out = (float4*)(part + (long)blockIdx.x * 2 * d);
+  for (int k = threadIdx.x; k < 2 * d4; k += 256) {
+    const int which = k >= d4, c = which ? k - d4 : k;
+    const float4 a = red[which][0][c], b = red[which][1][c], e = red[which][2][c], f = red[which][3][c];
+    out[k] = make_float4((a.x + b.x) + (e.x + f.x), (a.y + b.y) + (e.y + f.y), (a.z + b.z) + (e.z + f.z),
+                         (a.w + b.w) + (e.w + f.w));
+  }
+}
+
+// dw[c] += sum_b part[b][c], db[c] += sum_b part[b][d + c]: thread = one float4 column of the 2 d, blockIdx.y = one of
+// G groups of partial rows; one fp32 atomic per element per group (G <= 32)
+__global__ __launch_bounds__(256) void ln_part_reduce_kernel(const float* __restrict__ part, int nblk, int d,
+                                                             float* __restrict__ dw, float* __restrict__ db) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  const int d4 = d >> 2;
+  if (k >= 2 * d4) return;
+  const int G = gridDim.y;
+  const int per = (nblk + G - 1) / G, b0 = blockIdx.y * per, b1 = min(nblk, b0 + per);
+  if (b1 <= b0) return;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  int b = b0;
+  for (; b + 4 <= b1; b += 4) {  // four independent loads in flight
+    const float4 v0 = ((const float4*)(part + (long)b * 2 * d))[k];
+    const float4 v1 = ((const float4*)(part + (long)(b + 1) * 2 * d))[k];
+    const float4 v2 = ((const float4*)(part + (long)(b + 2) * 2 * d))[k];
+    const float4 v3 = ((const float4*)(part + (long)(b + 3) * 2 * d))[k];
+    s.x += (v0.x + v1.x) + (v2.x + v3.x);
+    s.y += (v0.y + v1.y) + (v2.y + v3.y);
+    s.z += (v0.z + v1.z) + (v2.z + v3.z);
+    s.w += (v0.w + v1.w) + (v2.w + v3.w);
+  }
+  for (; b < b1; ++b) {
+    const float4 v = ((const float4*)(part + (long)b * 2 * d))[k];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  float* dst = k < d4 ? dw + 4 * k : db + 4 * (k - d4);
+  atomicAdd(dst + 0, s.x);
+  atomicAdd(dst + 1, s.y);
+  atomicAdd(dst + 2, s.z);
+  atomicAdd(dst + 3, s.w);
+}
+
 // scalar fallback (any d <= 4096, any alignment)
 template <int VPL, bool DY_F32>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
@@ -489,11 +637,47 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
 IIT_EXPORT int iit_ln_bwd_sel(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
                               const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db, int T,
                               int d, int accumulate, unsigned long long pos_mask, int S, void* stream);
+IIT_EXPORT int iit_ln_bwd_part(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
+                               const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db,
+                               float* part, int T, int d, int accumulate, unsigned long long pos_mask, int S,
+                               void* stream);
 
 IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
                           const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db, int T, int d,
                           int accumulate, void* stream) {
   return iit_ln_bwd_sel(dy, dy_f32, x, mean, rstd, w, dx, dres, dx16, dw, db, T, d, accumulate, 0ull, 1, stream);
+}
+
+// rows per block of the fused affine-gradient backward (the caller sizes ``part`` as blocks x 2 d floats)
+IIT_EXPORT int iit_ln_bwd_part_rows() { return 4 * LN_FUSED_R; }
+
+// iit_ln_bwd_sel with dw / db fused into the dx pass (ln_bwd_part_vec_kernel + ln_part_reduce_kernel); ``part``:
+// ceil(T / iit_ln_bwd_part_rows()) x 2 d floats of scratch.  Falls back to iit_ln_bwd_sel when the vector layout
+// does not apply.
+IIT_EXPORT int iit_ln_bwd_part(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
+                               const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db,
+                               float* part, int T, int d, int accumulate, unsigned long long pos_mask, int S,
+                               void* stream) {
+  const bool vec = part && dw && db && d % 4 == 0 && d <= 1024 && aligned16(x) && aligned16(dx) &&
+                   (!dres || aligned16(dres)) && (!w || aligned16(w)) && aligned16(dw) && aligned16(db) &&
+                   aligned16(part) && (dy_f32 ? aligned16(dy) : (((uintptr_t)dy) & 7) == 0) &&
+                   (((uintptr_t)dx16) & 7) == 0;
+  if (!vec || T <= 0)
+    return iit_ln_bwd_sel(dy, dy_f32, x, mean, rstd, w, dx, dres, dx16, dw, db, T, d, accumulate, pos_mask, S, stream);
+  if (pos_mask && (S <= 0 || S > 64)) return (int)hipErrorInvalidValue;
+  const RowSel sel{pos_mask, S > 0 ? S : 1, T};
+  const int nblk = (T + 4 * LN_FUSED_R - 1) / (4 * LN_FUSED_R);
+  hipStream_t s = (hipStream_t)stream;
+  __bf16* d16 = (__bf16*)dx16;
+#define LNP(V)                                                                                                   \
+  if (dy_f32) hipLaunchKernelGGL((ln_bwd_part_vec_kernel<V, true>), dim3(nblk), dim3(256), 0, s, dy, x, mean, rstd, w, dx, dres, d16, part, T, d, accumulate, sel); \
+  else hipLaunchKernelGGL((ln_bwd_part_vec_kernel<V, false>), dim3(nblk), dim3(256), 0, s, dy, x, mean, rstd, w, dx, dres, d16, part, T, d, accumulate, sel);
+  const int v4 = (d / 4 + 63) / 64;
+  if (v4 <= 1) { LNP(1) } else if (v4 <= 2) { LNP(2) } else if (v4 <= 3) { LNP(3) } else { LNP(4) }
+#undef LNP
+  const int G = max(1, min(32, nblk / 8));  // ~8 partial rows per thread
+  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((2 * (d / 4) + 255) / 256, G), dim3(256), 0, s, part, nblk, d, dw, db);
+  return hipGetLastError();
 }
 
 // LNPre backward from the forward's bf16 output (``xh`` = xhat, [T, d]); no affine parameters, no row select

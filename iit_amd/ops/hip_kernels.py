@@ -38,6 +38,8 @@ _SIGS = {
     "iit_ln_fwd_sel": [c_void_p] * 6 + [c_int, c_int, c_float, c_ull, c_int, c_int, c_void_p],
     "iit_ln_bwd_xh16": [c_void_p, c_int] + [c_void_p] * 5 + [c_int, c_int, c_int, c_void_p],
     "iit_ln_bwd_sel": [c_void_p, c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_ull, c_int, c_void_p],
+    "iit_ln_bwd_part": [c_void_p, c_int] + [c_void_p] * 10 + [c_int, c_int, c_int, c_ull, c_int, c_void_p],
+    "iit_ln_bwd_part_rows": [],
     "iit_attn_small_fwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float, c_int,
                                             c_void_p],
     "iit_attn_small_bwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_float, c_int, c_void_p],
@@ -428,11 +430,31 @@ def ln_fwd(x, w, b, y, mean, rstd, T, d, eps):
     _check(lib().iit_ln_fwd(_p(x), _p(w), _p(b), _p(y), _p(mean), _p(rstd), T, d, eps, _stream()), "ln_fwd")
 
 
+def _ln_part(dw, T: int, d: int):
+    """Scratch of the fused affine-gradient LN backward (``iit_ln_bwd_part``): one (dw, db) partial row pair per
+    block of ``iit_ln_bwd_part_rows()`` rows; None without affine gradients or with ``IIT_LN_FUSED_DWDB=0``."""
+    if dw is None or os.environ.get("IIT_LN_FUSED_DWDB", "1") == "0":
+        return None
+    rows = _LN_PART_ROWS[0] or lib().iit_ln_bwd_part_rows()
+    _LN_PART_ROWS[0] = rows
+    return torch.empty(((T + rows - 1) // rows) * 2 * d, dtype=torch.float32, device=dw.device)
+
+
+_LN_PART_ROWS = [0]
+
+
 def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False, dres=None, dx16=None):
-    """dx = LN'(dy) (+ dres, the skip-connection gradient, fp32 [T, d]); ``dx16`` (optional) gets a bf16 copy."""
+    """dx = LN'(dy) (+ dres, the skip-connection gradient, fp32 [T, d]); ``dx16`` (optional) gets a bf16 copy; with
+    ``dw`` / ``db`` the affine gradients are added in the same pass (``iit_ln_bwd_part``)."""
     if CHECK_BOUNDS:
         _bounds("ln_bwd", ("dy", dy, T, d, d), ("x", x, T, d, d), ("dx", dx, T, d, d), ("dres", dres, T, d, d),
                 ("dx16", dx16, T, d, d), ("mean", mean, 1, T, T))
+    part = _ln_part(dw, T, d)
+    if part is not None:
+        _check(lib().iit_ln_bwd_part(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w),
+                                     _p(dx), _p(dres), _p(dx16), _p(dw), _p(db), _p(part), T, d, int(accumulate), 0,
+                                     1, _stream()), "ln_bwd_part")
+        return
     _check(lib().iit_ln_bwd(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx),
                             _p(dres), _p(dx16), _p(dw), _p(db), T, d, int(accumulate), _stream()), "ln_bwd")
 
@@ -459,6 +481,12 @@ def ln_bwd_sel(dy, x, mean, rstd, w, dx, dw, db, T, d, pos_mask: int, S: int, dr
     """Backward of :func:`ln_fwd_sel` over the base rows: spliced rows pass only ``dres`` and add nothing to dw/db."""
     if CHECK_BOUNDS:
         _bounds("ln_bwd_sel", ("dy", dy, T, d, d), ("x", x, T, d, d), ("dx", dx, T, d, d), ("mean", mean, 1, T, T))
+    part = _ln_part(dw, T, d)
+    if part is not None:
+        _check(lib().iit_ln_bwd_part(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w),
+                                     _p(dx), _p(dres), _p(dx16), _p(dw), _p(db), _p(part), T, d, 0, pos_mask, S,
+                                     _stream()), "ln_bwd_sel_part")
+        return
     _check(lib().iit_ln_bwd_sel(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx),
                                 _p(dres), _p(dx16), _p(dw), _p(db), T, d, 0, pos_mask, S,
                                 _stream()), "ln_bwd_sel")
