@@ -145,7 +145,8 @@ template <int V4>
 __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ b, __bf16* __restrict__ y,
                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                         int T, int d, float eps, RowSel sel) {
+                                                         int T, int d, float eps, RowSel sel,
+                                                         float* __restrict__ y32 = nullptr) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= T) return;
@@ -183,6 +184,8 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(const float* __restrict
       }
       bf16x4 ob = {f2bf(o.x), f2bf(o.y), f2bf(o.z), f2bf(o.w)};
       yr[c] = ob;
+      if (y32)  // the fp32 twin of the rounded output (a post-norm block's residual operand: no separate cast pass)
+        ((float4*)(y32 + (long)row * d))[c] = make_float4(bf2f(ob[0]), bf2f(ob[1]), bf2f(ob[2]), bf2f(ob[3]));
     }
   }
   if (lane == 0) {
@@ -243,6 +246,23 @@ IIT_EXPORT int iit_ln_fwd_sel(const float* x, const float* w, const float* b, vo
 IIT_EXPORT int iit_ln_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd, int T,
                           int d, float eps, void* stream) {
   return iit_ln_fwd_sel(x, w, b, y, mean, rstd, T, d, eps, 0ull, 1, 0, stream);
+}
+
+// iit_ln_fwd that also writes ``y32`` = fp32(y) (vector layout only: d % 4 == 0, d <= 4096, 16-B aligned rows)
+IIT_EXPORT int iit_ln_fwd_twin(const float* x, const float* w, const float* b, void* y, float* y32, float* mean,
+                               float* rstd, int T, int d, float eps, void* stream) {
+  const bool vec = d % 4 == 0 && d <= 4096 && aligned16(x) && (((uintptr_t)y) & 7) == 0 && aligned16(y32) &&
+                   (!w || (aligned16(w) && aligned16(b)));
+  if (!vec) return (int)hipErrorInvalidValue;
+  const RowSel sel{0ull, 1, 0};
+  dim3 grid((T + 3) / 4), block(256);
+  hipStream_t s = (hipStream_t)stream;
+#define LNT(V) hipLaunchKernelGGL((ln_fwd_vec_kernel<V>), grid, block, 0, s, x, w, b, (__bf16*)y, mean, rstd, T, d, eps, sel, y32)
+  const int v4 = (d / 4 + 63) / 64;
+  if (v4 <= 1) LNT(1); else if (v4 <= 2) LNT(2); else if (v4 <= 3) LNT(3); else if (v4 <= 4) LNT(4);
+  else if (v4 <= 6) LNT(6); else if (v4 <= 8) LNT(8); else if (v4 <= 12) LNT(12); else LNT(16);
+#undef LNT
+  return hipGetLastError();
 }
 
 // ``pos_mask`` (RowSel): base rows [0, Tb) at positions with their bit set normalise the source row row + Tb
@@ -455,7 +475,8 @@ __global__ __launch_bounds__(256) void ln_bwd_part_vec_kernel(const void* __rest
                                                               const float* __restrict__ w, float* __restrict__ dx,
                                                               const float* __restrict__ dres,
                                                               __bf16* __restrict__ dx16, float* __restrict__ part,
-                                                              int T, int d, int accumulate, RowSel sel) {
+                                                              int T, int d, int accumulate, RowSel sel,
+                                                              const float* __restrict__ dy2) {
   __shared__ float4 red[2][4][64 * V4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int d4 = d >> 2;
@@ -488,6 +509,10 @@ __global__ __launch_bounds__(256) void ln_bwd_part_vec_kernel(const void* __rest
         } else {
           const bf16x4 t = ((const bf16x4*)dy_)[(long)row * d4 + c];
           dyv[r][i] = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
+        }
+        if (dy2) {  // the fp32 twin output's gradient (LayerNormTwinFn): dy = dy + dy2
+          const float4 e = ((const float4*)dy2)[(long)row * d4 + c];
+          dyv[r][i].x += e.x; dyv[r][i].y += e.y; dyv[r][i].z += e.z; dyv[r][i].w += e.w;
         }
         xvv[r][i] = ((const float4*)x)[(long)row * d4 + c];
       }
@@ -640,7 +665,7 @@ IIT_EXPORT int iit_ln_bwd_sel(const void* dy, int dy_f32, const float* x, const 
 IIT_EXPORT int iit_ln_bwd_part(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
                                const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db,
                                float* part, int T, int d, int accumulate, unsigned long long pos_mask, int S,
-                               void* stream);
+                               const float* dy2, void* stream);
 
 IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
                           const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db, int T, int d,
@@ -652,16 +677,17 @@ IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const floa
 IIT_EXPORT int iit_ln_bwd_part_rows() { return 4 * LN_FUSED_R; }
 
 // iit_ln_bwd_sel with dw / db fused into the dx pass (ln_bwd_part_vec_kernel + ln_part_reduce_kernel); ``part``:
-// ceil(T / iit_ln_bwd_part_rows()) x 2 d floats of scratch.  Falls back to iit_ln_bwd_sel when the vector layout
-// does not apply.
+// ceil(T / iit_ln_bwd_part_rows()) x 2 d floats of scratch; ``dy2`` (nullable, fp32 [T, d]) is added to dy.  Falls
+// back to iit_ln_bwd_sel when the vector layout does not apply (refused with a ``dy2``: the caller sums first).
 IIT_EXPORT int iit_ln_bwd_part(const void* dy, int dy_f32, const float* x, const float* mean, const float* rstd,
                                const float* w, float* dx, const float* dres, void* dx16, float* dw, float* db,
                                float* part, int T, int d, int accumulate, unsigned long long pos_mask, int S,
-                               void* stream) {
+                               const float* dy2, void* stream) {
   const bool vec = part && dw && db && d % 4 == 0 && d <= 1024 && aligned16(x) && aligned16(dx) &&
                    (!dres || aligned16(dres)) && (!w || aligned16(w)) && aligned16(dw) && aligned16(db) &&
                    aligned16(part) && (dy_f32 ? aligned16(dy) : (((uintptr_t)dy) & 7) == 0) &&
-                   (((uintptr_t)dx16) & 7) == 0;
+                   (((uintptr_t)dx16) & 7) == 0 && (!dy2 || aligned16(dy2));
+  if (dy2 && !vec) return (int)hipErrorInvalidValue;
   if (!vec || T <= 0)
     return iit_ln_bwd_sel(dy, dy_f32, x, mean, rstd, w, dx, dres, dx16, dw, db, T, d, accumulate, pos_mask, S, stream);
   if (pos_mask && (S <= 0 || S > 64)) return (int)hipErrorInvalidValue;
@@ -670,8 +696,8 @@ IIT_EXPORT int iit_ln_bwd_part(const void* dy, int dy_f32, const float* x, const
   hipStream_t s = (hipStream_t)stream;
   __bf16* d16 = (__bf16*)dx16;
 #define LNP(V)                                                                                                   \
-  if (dy_f32) hipLaunchKernelGGL((ln_bwd_part_vec_kernel<V, true>), dim3(nblk), dim3(256), 0, s, dy, x, mean, rstd, w, dx, dres, d16, part, T, d, accumulate, sel); \
-  else hipLaunchKernelGGL((ln_bwd_part_vec_kernel<V, false>), dim3(nblk), dim3(256), 0, s, dy, x, mean, rstd, w, dx, dres, d16, part, T, d, accumulate, sel);
+  if (dy_f32) hipLaunchKernelGGL((ln_bwd_part_vec_kernel<V, true>), dim3(nblk), dim3(256), 0, s, dy, x, mean, rstd, w, dx, dres, d16, part, T, d, accumulate, sel, dy2); \
+  else hipLaunchKernelGGL((ln_bwd_part_vec_kernel<V, false>), dim3(nblk), dim3(256), 0, s, dy, x, mean, rstd, w, dx, dres, d16, part, T, d, accumulate, sel, dy2);
   const int v4 = (d / 4 + 63) / 64;
   if (v4 <= 1) { LNP(1) } else if (v4 <= 2) { LNP(2) } else if (v4 <= 3) { LNP(3) } else { LNP(4) }
 #undef LNP

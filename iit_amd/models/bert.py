@@ -98,7 +98,8 @@ class BertBlock(nn.Module):
             z, spliced = attn.compute_z(resid, run)
             z = run.site(attn.hook_z, z, spliced=spliced)
             resid_mid = run.site(self.hook_resid_mid, ops.o_proj_residual(z, attn.W_O, attn.b_O, resid))
-            x = run.site(self.hook_mlp_in, self.ln1.run(resid_mid, run))
+            # (post-norm: both LN outputs are also residual operands -- fp32 twins, LayerNormTwinFn)
+            x = run.site(self.hook_mlp_in, self.ln1.run(resid_mid, run, twin=True))
             mlp = self.mlp
             if (getattr(ops, "mlp_gelu_residual", None) is not None and self.cfg.act_fn in ("gelu", "gelu_new")
                     and not (run.live(mlp.hook_pre) or run.live(mlp.hook_post))):
@@ -106,12 +107,12 @@ class BertBlock(nn.Module):
                 resid_post = ops.mlp_gelu_residual(x, mlp.W_in, mlp.b_in, mlp.W_out, mlp.b_out, x,
                                                    erf=self.cfg.act_fn == "gelu")
                 resid_post = run.site(self.hook_resid_post, resid_post)
-                return run.site(self.hook_normalized_resid_post, self.ln2.run(resid_post, run))
+                return run.site(self.hook_normalized_resid_post, self.ln2.run(resid_post, run, twin=True))
             pre_hook = (lambda t: run.site(self.mlp.hook_pre, t)) if run.live(self.mlp.hook_pre) else None
             _, post = ops.mlp_in(x, self.mlp.W_in, self.mlp.b_in, self.cfg.act_fn, hook_pre=pre_hook)
             post = run.site(self.mlp.hook_post, post)
             resid_post = run.site(self.hook_resid_post, ops.mlp_out_residual(post, self.mlp.W_out, self.mlp.b_out, x))
-            return run.site(self.hook_normalized_resid_post, self.ln2.run(resid_post, run))
+            return run.site(self.hook_normalized_resid_post, self.ln2.run(resid_post, run, twin=True))
         q, k, v = ops.qkv(resid, attn.W_Q, attn.W_K, attn.W_V, attn.b_Q, attn.b_K, attn.b_V)
         q, k, v = run.site(attn.hook_q, q), run.site(attn.hook_k, k), run.site(attn.hook_v, v)
         scores = torch.einsum("bqhe,bkhe->bhqk", q, k) / attn.attn_scale

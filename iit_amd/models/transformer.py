@@ -134,7 +134,9 @@ class LayerNormSite(nn.Module):
             raise NotImplementedError(f"normalization_type {kind}")
         return LayerNormSite(cfg, affine=kind in ("LN", "RMS"), rms=kind in ("RMS", "RMSPre"))
 
-    def run(self, x, run: _Run):
+    def run(self, x, run: _Run, twin: bool = False):
+        """``twin``: the output will also be a residual operand (post-norm blocks): the fused backend then returns
+        it with an fp32 twin (``HipOps.layer_norm_twin``)."""
         live = run.live(self.hook_scale) or run.live(self.hook_normalized)
         if self.rms:
             hs = (lambda t: run.site(self.hook_scale, t)) if live else None
@@ -146,6 +148,8 @@ class LayerNormSite(nn.Module):
                 hook_scale=lambda t: run.site(self.hook_scale, t),
                 hook_normalized=lambda t: run.site(self.hook_normalized, t),
             )
+        if twin and self.w is not None and hasattr(run.ops, "layer_norm_twin"):
+            return run.ops.layer_norm_twin(x, self.w, self.b, self.eps)
         return run.ops.layer_norm(x, self.w, self.b, self.eps)
 
 

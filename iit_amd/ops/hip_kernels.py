@@ -38,7 +38,8 @@ _SIGS = {
     "iit_ln_fwd_sel": [c_void_p] * 6 + [c_int, c_int, c_float, c_ull, c_int, c_int, c_void_p],
     "iit_ln_bwd_xh16": [c_void_p, c_int] + [c_void_p] * 5 + [c_int, c_int, c_int, c_void_p],
     "iit_ln_bwd_sel": [c_void_p, c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_ull, c_int, c_void_p],
-    "iit_ln_bwd_part": [c_void_p, c_int] + [c_void_p] * 10 + [c_int, c_int, c_int, c_ull, c_int, c_void_p],
+    "iit_ln_bwd_part": [c_void_p, c_int] + [c_void_p] * 10 + [c_int, c_int, c_int, c_ull, c_int, c_void_p, c_void_p],
+    "iit_ln_fwd_twin": [c_void_p] * 7 + [c_int, c_int, c_float, c_void_p],
     "iit_ln_bwd_part_rows": [],
     "iit_attn_small_fwd": [c_void_p] * 4 + [c_ull, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_float, c_int,
                                             c_void_p],
@@ -430,6 +431,14 @@ def ln_fwd(x, w, b, y, mean, rstd, T, d, eps):
     _check(lib().iit_ln_fwd(_p(x), _p(w), _p(b), _p(y), _p(mean), _p(rstd), T, d, eps, _stream()), "ln_fwd")
 
 
+def ln_fwd_twin(x, w, b, y, y32, mean, rstd, T, d, eps) -> bool:
+    """``ln_fwd`` that also writes ``y32`` = fp32(y) in the same pass; False when the vector layout does not apply
+    (nothing launched: the caller casts)."""
+    if CHECK_BOUNDS:
+        _bounds("ln_fwd_twin", ("x", x, T, d, d), ("y", y, T, d, d), ("y32", y32, T, d, d))
+    return lib().iit_ln_fwd_twin(_p(x), _p(w), _p(b), _p(y), _p(y32), _p(mean), _p(rstd), T, d, eps, _stream()) == 0
+
+
 def _ln_part(dw, T: int, d: int):
     """Scratch of the fused affine-gradient LN backward (``iit_ln_bwd_part``): one (dw, db) partial row pair per
     block of ``iit_ln_bwd_part_rows()`` rows; None without affine gradients or with ``IIT_LN_FUSED_DWDB=0``."""
@@ -443,18 +452,23 @@ def _ln_part(dw, T: int, d: int):
 _LN_PART_ROWS = [0]
 
 
-def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False, dres=None, dx16=None):
+def ln_bwd(dy, x, mean, rstd, w, dx, dw, db, T, d, accumulate=False, dres=None, dx16=None, dy2=None):
     """dx = LN'(dy) (+ dres, the skip-connection gradient, fp32 [T, d]); ``dx16`` (optional) gets a bf16 copy; with
-    ``dw`` / ``db`` the affine gradients are added in the same pass (``iit_ln_bwd_part``)."""
+    ``dw`` / ``db`` the affine gradients are added in the same pass (``iit_ln_bwd_part``); ``dy2`` (fp32 [T, d],
+    optional) is a second gradient of the output, added to ``dy`` inside the kernel where it can be."""
     if CHECK_BOUNDS:
         _bounds("ln_bwd", ("dy", dy, T, d, d), ("x", x, T, d, d), ("dx", dx, T, d, d), ("dres", dres, T, d, d),
-                ("dx16", dx16, T, d, d), ("mean", mean, 1, T, T))
+                ("dx16", dx16, T, d, d), ("mean", mean, 1, T, T), ("dy2", dy2, T, d, d))
     part = _ln_part(dw, T, d)
     if part is not None:
-        _check(lib().iit_ln_bwd_part(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w),
-                                     _p(dx), _p(dres), _p(dx16), _p(dw), _p(db), _p(part), T, d, int(accumulate), 0,
-                                     1, _stream()), "ln_bwd_part")
-        return
+        rc = lib().iit_ln_bwd_part(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w),
+                                   _p(dx), _p(dres), _p(dx16), _p(dw), _p(db), _p(part), T, d, int(accumulate), 0,
+                                   1, _p(dy2), _stream())
+        if rc == 0 or dy2 is None:
+            _check(rc, "ln_bwd_part")
+            return
+    if dy2 is not None:  # (no fused path: sum the two gradients first)
+        dy = dy.float() + dy2
     _check(lib().iit_ln_bwd(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx),
                             _p(dres), _p(dx16), _p(dw), _p(db), T, d, int(accumulate), _stream()), "ln_bwd")
 
@@ -485,7 +499,7 @@ def ln_bwd_sel(dy, x, mean, rstd, w, dx, dw, db, T, d, pos_mask: int, S: int, dr
     if part is not None:
         _check(lib().iit_ln_bwd_part(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w),
                                      _p(dx), _p(dres), _p(dx16), _p(dw), _p(db), _p(part), T, d, 0, pos_mask, S,
-                                     _stream()), "ln_bwd_sel_part")
+                                     None, _stream()), "ln_bwd_sel_part")
         return
     _check(lib().iit_ln_bwd_sel(_p(dy), int(dy.dtype == torch.float32), _p(x), _p(mean), _p(rstd), _p(w), _p(dx),
                                 _p(dres), _p(dx16), _p(dw), _p(db), T, d, 0, pos_mask, S,

@@ -445,6 +445,71 @@ class LayerNormFn(Function):
         return dx, None, None, None
 
 
+class LayerNormTwinFn(Function):
+    """``(LN(x), fp32(LN(x)))`` from one kernel pass (``iit_ln_fwd_twin``): a post-norm block (BERT) feeds the bf16
+    output to the next GEMM and the fp32 copy to the residual epilogue of the GEMM after it, which read a cast of
+    the bf16 output before -- a [T, d] cast pass forward, and backward a cast of the residual gradient plus
+    autograd's bf16 sum of the two gradients.  The backward takes both gradients and adds the fp32 one inside the
+    LN-backward kernel (``dy2``)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        ctx.set_materialize_grads(False)
+        shape = x.shape
+        d = shape[-1]
+        x2 = _flat2(x.float().contiguous())
+        T = x2.shape[0]
+        # allocated in the output shape (the outputs are not views: a multi-output Function's views may not be
+        # modified in place downstream)
+        y = torch.empty(*shape[:-1], d, dtype=BF16, device=x.device)
+        y32 = torch.empty(*shape[:-1], d, dtype=F32, device=x.device)
+        mean = torch.empty(T, dtype=F32, device=x.device)
+        rstd = torch.empty(T, dtype=F32, device=x.device)
+        yf, y32f = y.view(T, d), y32.view(T, d)
+        if not K.ln_fwd_twin(x2, w, b, yf, y32f, mean, rstd, T, d, eps):
+            K.ln_fwd(x2, w, b, yf, mean, rstd, T, d, eps)
+            y32f.copy_(yf)
+        ctx.save_for_backward(x2, mean, rstd)
+        ctx.params = (w, b)
+        ctx.in_dtype = x.dtype
+        return y, y32
+
+    @staticmethod
+    def backward(ctx, dy, dy32):
+        if dy is None and dy32 is None:
+            return None, None, None, None
+        x2, mean, rstd = ctx.saved_tensors
+        w, b = ctx.params
+        T, d = x2.shape
+        lead = (dy if dy is not None else dy32).shape[:-1]
+        dx = torch.empty(T, d, dtype=F32, device=x2.device)
+        dx16 = torch.empty(T, d, dtype=BF16, device=x2.device) if ctx.in_dtype == F32 else None
+        dw = _grad_slot(w) if w is not None else None
+        db = _grad_slot(b) if b is not None else None
+        if dy is None:
+            g, g2 = _flat2(dy32.float().contiguous()), None
+        else:
+            g = _flat2(dy.contiguous())
+            g2 = None if dy32 is None else _flat2(dy32.float().contiguous())
+        K.ln_bwd(g, x2, mean, rstd, w, dx, dw, db, T, d, dx16=dx16, dy2=g2)
+        _done(w, b)
+        dx = dx.view(*lead, d)
+        if dx16 is None:
+            return dx.to(ctx.in_dtype), None, None, None
+        _set_bf16_twin(dx, dx16)
+        return dx, None, None, None
+
+
+def _f32_of(t: torch.Tensor) -> torch.Tensor:
+    """The fp32 twin a :class:`LayerNormTwinFn` output carries (same storage and version as when it was produced),
+    else ``t`` itself: consumers that want an fp32 residual pass the twin as their autograd input, so its gradient
+    reaches the LN backward in fp32."""
+    twin = getattr(t, "_iit_f32", None)
+    if twin is not None and twin[0] == t.data_ptr() and twin[1] == t._version and twin[2].shape == t.shape:
+        return twin[2]
+    return t
+
+
 def _set_bf16_twin(t: torch.Tensor, t16: torch.Tensor) -> None:
     """Attach a bf16 copy to an fp32 gradient: its producer wrote both in one pass, so the consuming
     backward GEMMs skip a separate cast.  Tensor attributes survive autograd hand-off when the gradient
@@ -1593,6 +1658,15 @@ class HipOps(TorchOps):
     def layer_norm(self, x, w, b, eps):
         return LayerNormFn.apply(x, w, b, eps)
 
+    def layer_norm_twin(self, x, w, b, eps):
+        """``layer_norm`` whose bf16 output carries an fp32 twin for residual consumers (:class:`LayerNormTwinFn`;
+        ``IIT_LN_TWIN=0`` disables)."""
+        if os.environ.get("IIT_LN_TWIN", "1") == "0":
+            return LayerNormFn.apply(x, w, b, eps)
+        y, y32 = LayerNormTwinFn.apply(x, w, b, eps)
+        y._iit_f32 = (y.data_ptr(), y._version, y32)
+        return y
+
     def layer_norm_fork(self, x, w, b, eps):
         """``(LN(x), x_passthrough)``; use the passthrough for the skip connection."""
         return LayerNormForkFn.apply(x, w, b, eps)
@@ -1635,6 +1709,7 @@ class HipOps(TorchOps):
         return LinearFn.apply(z.reshape(B, S, H * dh), W_O, b_O, self._L(W_O)["o"], W_O.shape[-1], None, "bf16")
 
     def o_proj_residual(self, z, W_O, b_O, resid):
+        resid = _f32_of(resid)
         B, S, H, dh = z.shape
         return LinearFn.apply(z.reshape(B, S, H * dh), W_O, b_O, self._L(W_O)["o"], W_O.shape[-1], resid, "resid")
 
@@ -1656,6 +1731,7 @@ class HipOps(TorchOps):
         sites are all dead: the backward forms dpre in the dX GEMM's epilogue (see :class:`MLPOutGeluFn`).
         Without autograd (evaluation sweeps, source captures) the W_in epilogue stores only ``post``: no
         pre-activation is kept for a backward, half the epilogue's writes."""
+        resid = _f32_of(resid)
         if not torch.is_grad_enabled():
             lead, d, dm, N = x.shape[:-1], x.shape[-1], W_in.shape[1], W_out.shape[1]
             x2 = _flat2(x.to(BF16).contiguous())
@@ -1676,6 +1752,7 @@ class HipOps(TorchOps):
         return LinearFn.apply(post, W_out, b_out, self._L(W_out)["out"], W_out.shape[1], None, "bf16")
 
     def mlp_out_residual(self, post, W_out, b_out, resid):
+        resid = _f32_of(resid)
         return LinearFn.apply(post, W_out, b_out, self._L(W_out)["out"], W_out.shape[1], resid, "resid")
 
     # -- unembed -------------------------------------------------------------------------

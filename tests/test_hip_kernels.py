@@ -421,3 +421,34 @@ def test_zero_ranges_many_ranges(K, n_ranges):
     K.zero_ranges(base, starts, lens)
     torch.cuda.synchronize()
     assert torch.equal(base, ref)
+
+
+@pytest.mark.parametrize("use_bf16_out", [True, False])
+def test_layernorm_twin_matches_cast_path(K, use_bf16_out):
+    """LayerNormTwinFn (hip_ops): the fp32 twin equals fp32(bf16 output) exactly, and with both outputs consumed
+    (bf16 -> a GEMM-like use, fp32 -> a residual) x / w / b get the gradients of the cast path against fp32 torch."""
+    from iit_amd.ops.hip_ops import LayerNormTwinFn, _f32_of
+    torch.manual_seed(21)
+    T, d = 777, 768
+    x = (torch.randn(T, d, device=dev) * 2 + 0.5).requires_grad_(True)
+    w = torch.nn.Parameter(torch.randn(d, device=dev))
+    b = torch.nn.Parameter(torch.randn(d, device=dev))
+    y, y32 = LayerNormTwinFn.apply(x, w, b, 1e-5)
+    assert y.dtype == torch.bfloat16 and y32.dtype == torch.float32
+    assert torch.equal(y32, y.float())
+    g1 = torch.randn(T, d, device=dev)
+    g2 = torch.randn(T, d, device=dev)
+    loss = (y32 * g2).sum() + ((y.float() * g1).sum() if use_bf16_out else 0.0)
+    loss.backward()
+    xr = x.detach().clone().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (d,), wr, br, 1e-5)
+    ((yr * (g1 + g2 if use_bf16_out else g2)).sum()).backward()
+    assert rel_err(x.grad, xr.grad) < 1e-2
+    assert rel_err(w.grad, wr.grad) < 1e-2 and rel_err(b.grad, br.grad) < 1e-2
+    # the twin attribute is honoured only for the exact tensor (storage and version) it was attached to
+    y._iit_f32 = (y.data_ptr(), y._version, y32)
+    assert _f32_of(y) is y32
+    y.add_(0)  # an in-place change invalidates it (the outputs are not views: in-place ops are allowed)
+    assert _f32_of(y) is y
