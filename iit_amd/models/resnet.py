@@ -22,12 +22,32 @@ import torch
 from torch import nn
 
 
+class Conv2d(nn.Conv2d):
+    """``nn.Conv2d`` (same parameters, state_dict keys and init) that, under bf16 autocast on the GPU with its weight
+    in a flat parameter arena, convolves with the arena's bf16 mirror (``torch_ops._MirrorWeight``, written by the
+    fused Adam): no per-forward weight cast (autocast's weight cache is off in graph-captured steps), and the bf16
+    weight gradient is added straight into the fp32 grad slot instead of a cast + AccumulateGrad add.
+    ``IIT_CONV_MIRROR=0`` keeps the plain autocast path."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        w = self.weight
+        if (x.is_cuda and self.bias is None and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16 and w.dtype == torch.float32
+                and getattr(w, "_iit_flat", None) is not None and os.environ.get("IIT_CONV_MIRROR", "1") != "0"):
+            from ..ops.torch_ops import _MirrorWeight, _arena_mirror
+            m = _arena_mirror(w)
+            if m is not None:
+                w16 = _MirrorWeight.apply(w, m[0]) if torch.is_grad_enabled() else m[1]
+                return self._conv_forward(x.to(torch.bfloat16), w16, None)
+        return super().forward(x)
+
+
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(cin, cout, kernel_size=3, stride=stride, padding=1, bias=False)
+    return Conv2d(cin, cout, kernel_size=3, stride=stride, padding=1, bias=False)
 
 
 def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(cin, cout, kernel_size=1, stride=stride, bias=False)
+    return Conv2d(cin, cout, kernel_size=1, stride=stride, bias=False)
 
 
 def _hooked(m: nn.Module) -> bool:
@@ -116,7 +136,7 @@ class ResNet(nn.Module):
     def __init__(self, layers=(2, 2, 2, 2), num_classes: int = 1000, in_channels: int = 3):
         super().__init__()
         self.inplanes = 64
-        self.conv1 = nn.Conv2d(in_channels, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.conv1 = Conv2d(in_channels, 64, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = nn.BatchNorm2d(64)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)

@@ -197,3 +197,35 @@ def test_bn_splice_on_read_exact(res, training):
     exp = dx0.clone()
     exp[idx.as_index] = 0
     assert close(dx1, exp)
+
+
+def test_resnet_conv_mirror_matches_autocast_path(monkeypatch):
+    """resnet.Conv2d under bf16 autocast with its weight in a flat arena convolves with the arena's bf16 mirror
+    (torch_ops._MirrorWeight) and adds the bf16 weight gradient into the fp32 slot: the logits equal the autocast
+    cast path's and every gradient matches it (the mirror holds the same bf16 rounding of the fp32 master)."""
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.models.resnet import resnet18
+    from iit_amd.ops import torch_ops
+    torch.manual_seed(3)
+    ms = [resnet18(num_classes=10).to(dev).to(memory_format=torch.channels_last) for _ in range(2)]
+    ms[1].load_state_dict(ms[0].state_dict())
+    for m in ms:
+        FlatParams(m)
+    x = torch.rand(32, 3, 84, 84, device=dev).contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (32,), device=dev)
+    calls = []
+    orig = torch_ops._MirrorWeight.apply
+    monkeypatch.setattr(torch_ops._MirrorWeight, "apply", lambda *a: calls.append(1) or orig(*a))
+    outs = []
+    for m, env in ((ms[0], "1"), (ms[1], "0")):
+        monkeypatch.setenv("IIT_CONV_MIRROR", env)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(x)
+            loss = torch.nn.functional.cross_entropy(y.float(), t)
+        loss.backward()
+        outs.append(y.float().detach())
+    assert len(calls) == 20  # every convolution of ResNet-18 took the mirror (model 0 only)
+    assert rel(outs[0], outs[1]) < 1e-2  # (the fused BN statistics use fp32 atomics: not bitwise run to run)
+    for (n, pa), (_, pb) in zip(ms[0].named_parameters(), ms[1].named_parameters()):
+        assert pa.grad is not None and pb.grad is not None, n
+        assert rel(pa.grad, pb.grad) < 2e-2, (n, rel(pa.grad, pb.grad))
