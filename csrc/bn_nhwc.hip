@@ -328,7 +328,126 @@ bool shape_ok(long M, int C, const void* p) {
   return M > 0 && C >= 8 && C % 8 == 0 && C / 8 <= TPB && (TPB % (C / 8)) == 0 && ((uintptr_t)p & 15) == 0;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// 3x3 / stride 2 / padding 1 max pooling on channels-last bf16 (the PVR ResNet's stem pool), forward storing the
+// argmax tap (0..8, row-major in the window) as one byte per output element instead of torch's int64 flat index
+// (8x fewer index bytes), and a gather-form backward: each input element sums the gradients of the (up to 4)
+// windows that hold it and chose it -- no scatter, no atomics, no zero-fill of the input gradient.  Ties and NaN
+// follow torch's kernel: the first tap in scan order wins, a NaN is taken.  One thread per 8 channels.
+__global__ __launch_bounds__(256) void maxpool3s2_fwd_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y,
+                                                             unsigned char* __restrict__ idx, int N, int H, int W,
+                                                             int C, int OH, int OW) {
+  const int c8n = C / 8;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)N * OH * OW * c8n;
+  if (i >= total) return;
+  const int c8 = (int)(i % c8n);
+  long r = i / c8n;
+  const int ow = (int)(r % OW);
+  r /= OW;
+  const int oh = (int)(r % OH);
+  const int n = (int)(r / OH);
+  float best[8];
+  unsigned char arg[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    best[e] = -INFINITY;
+    arg[e] = 0;
+  }
+  bool first = true;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int ih = 2 * oh - 1 + kh;
+    if (ih < 0 || ih >= H) continue;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int iw = 2 * ow - 1 + kw;
+      if (iw < 0 || iw >= W) continue;
+      const bf16x8 v = *(const bf16x8*)(x + (((long)n * H + ih) * W + iw) * C + c8 * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = bf2f(v[e]);
+        if (first || f > best[e] || f != f) {
+          best[e] = f;
+          arg[e] = (unsigned char)(kh * 3 + kw);
+        }
+      }
+      first = false;
+    }
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
+  const long oi = (((long)n * OH + oh) * OW + ow) * C + c8 * 8;
+  *(bf16x8*)(y + oi) = o;
+  unsigned long long packed = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) packed |= (unsigned long long)arg[e] << (8 * e);
+  *(unsigned long long*)(idx + oi) = packed;
+}
+
+__global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const __bf16* __restrict__ dy,
+                                                             const unsigned char* __restrict__ idx,
+                                                             __bf16* __restrict__ dx, int N, int H, int W, int C,
+                                                             int OH, int OW) {
+  const int c8n = C / 8;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)N * H * W * c8n;
+  if (i >= total) return;
+  const int c8 = (int)(i % c8n);
+  long r = i / c8n;
+  const int iw = (int)(r % W);
+  r /= W;
+  const int ih = (int)(r % H);
+  const int n = (int)(r / H);
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int th = ih + 1 - kh;  // = 2 oh
+    if (th < 0 || (th & 1) || (th >> 1) >= OH) continue;
+    const int oh = th >> 1;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int tw = iw + 1 - kw;
+      if (tw < 0 || (tw & 1) || (tw >> 1) >= OW) continue;
+      const int ow = tw >> 1;
+      const long oi = (((long)n * OH + oh) * OW + ow) * C + c8 * 8;
+      const unsigned long long packed = *(const unsigned long long*)(idx + oi);
+      const bf16x8 g = *(const bf16x8*)(dy + oi);
+      const unsigned tap = (unsigned)(kh * 3 + kw);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (((packed >> (8 * e)) & 0xffull) == tap) acc[e] += bf2f(g[e]);
+    }
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
+  *(bf16x8*)(dx + (((long)n * H + ih) * W + iw) * C + c8 * 8) = o;
+}
+
 }  // namespace
+
+// channels-last bf16 [N][H][W][C] -> [N][OH][OW][C] (OH = (H - 1) / 2 + 1, OW likewise), idx one byte per output
+IIT_EXPORT int iit_maxpool3s2_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, void* stream) {
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  if (C % 8 || (((uintptr_t)x) & 15) || (((uintptr_t)y) & 15) || (((uintptr_t)idx) & 7)) return (int)hipErrorInvalidValue;
+  const long total = (long)N * OH * OW * (C / 8);
+  hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     (const __bf16*)x, (__bf16*)y, (unsigned char*)idx, N, H, W, C, OH, OW);
+  return (int)hipGetLastError();
+}
+
+IIT_EXPORT int iit_maxpool3s2_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C, void* stream) {
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  if (C % 8 || (((uintptr_t)dy) & 15) || (((uintptr_t)dx) & 15) || (((uintptr_t)idx) & 7)) return (int)hipErrorInvalidValue;
+  const long total = (long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     (const __bf16*)dy, (const unsigned char*)idx, (__bf16*)dx, N, H, W, C, OH, OW);
+  return (int)hipGetLastError();
+}
 
 // forward: ws = per-module accumulator (fp32 [2C] + a u32 ticket after it, zero at the first call, re-armed by
 // every call); y = relu?(bn(x) (+ res)); save [2C] = mean, rstd (the batch's in training, the running ones in eval)

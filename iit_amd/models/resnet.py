@@ -90,6 +90,13 @@ def _conv_with_splice(conv_m: nn.Module, bn_m: nn.Module, x: torch.Tensor):
     return h, (spl[0].index, spl[0].src)
 
 
+def _pool_covered(x: torch.Tensor, pool: nn.Module) -> bool:
+    if not x.is_cuda:
+        return False
+    from ..ops import bn as fbn
+    return fbn.maxpool_covered(x, pool)
+
+
 def _bn_after_conv(conv_m, bn_m, relu_m, x, res=None):
     """relu?(bn(conv(x)) (+ res)) with the fused BatchNorm (and a conv-hook splice inside it) when covered, else the
     module path."""
@@ -169,7 +176,13 @@ class ResNet(nn.Module):
         if x.dim() == 4 and conv.weight.is_contiguous(memory_format=torch.channels_last) and \
                 not conv.weight.is_contiguous() and not x.is_contiguous(memory_format=torch.channels_last):
             x = x.contiguous(memory_format=torch.channels_last)
-        x = self.maxpool(_bn_after_conv(self.conv1, self.bn1, self.relu, x))
+        x = _bn_after_conv(self.conv1, self.bn1, self.relu, x)
+        pool = getattr(self.maxpool, "mod", self.maxpool)
+        if not _hooked(self.maxpool) and _pool_covered(x, pool):
+            from ..ops.bn import MaxPool3s2Fn
+            x = MaxPool3s2Fn.apply(x)  # NHWC bf16, byte argmax, gather backward (csrc/bn_nhwc.hip)
+        else:
+            x = self.maxpool(x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -106,3 +106,42 @@ def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res: Optional[torch.Tensor
     if spec is None or tuple(d[0] for d in spec.dims) != tuple(x.shape):
         return None
     return BNActFn.apply(x, bn.weight, bn.bias, res, bn, relu, src, spec)
+
+
+class MaxPool3s2Fn(Function):
+    """``max_pool2d(x, 3, 2, 1)`` on a channels-last bf16 activation (``csrc/bn_nhwc.hip``): one byte of argmax per
+    output element and a gather-form backward (torch's NHWC pool keeps int64 indices and scatters its gradient)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty(N, C, OH, OW, dtype=BF16, device=x.device, memory_format=torch.channels_last)
+        idx = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=x.device)
+        K.maxpool3s2_fwd(x, y, idx, N, H, W, C)
+        ctx.save_for_backward(idx)
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        dy = dy.to(BF16).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty(N, C, H, W, dtype=BF16, device=dy.device, memory_format=torch.channels_last)
+        K.maxpool3s2_bwd(dy, idx, dx, N, H, W, C)
+        return dx
+
+
+def maxpool_covered(x: torch.Tensor, pool: torch.nn.Module) -> bool:
+    """``pool`` is ``MaxPool2d(3, 2, 1)`` (dilation 1, floor mode, no indices) and ``x`` a channels-last bf16 CUDA
+    activation with C % 8 == 0 (``IIT_FUSED_POOL=0`` disables)."""
+    if not (isinstance(pool, torch.nn.MaxPool2d) and enabled() and os.environ.get("IIT_FUSED_POOL", "1") != "0"):
+        return False
+    k, st, pd, dl = pool.kernel_size, pool.stride, pool.padding, pool.dilation
+    if not all(v in (n, (n, n)) for v, n in ((k, 3), (st, 2), (pd, 1), (dl, 1))):
+        return False
+    if pool.ceil_mode or pool.return_indices:
+        return False
+    return (x.is_cuda and x.dtype == BF16 and x.dim() == 4 and x.shape[1] % 8 == 0
+            and x.is_contiguous(memory_format=torch.channels_last))

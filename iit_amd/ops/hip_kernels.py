@@ -95,6 +95,8 @@ _SIGS = {
     "iit_bn_bwd": [c_void_p] * 7 + [c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_int, c_int, c_void_p],
     "iit_gemm_glds_set_prof": [c_void_p],
+    "iit_maxpool3s2_fwd": [c_void_p] * 3 + [c_int] * 4 + [c_void_p],
+    "iit_maxpool3s2_bwd": [c_void_p] * 3 + [c_int] * 4 + [c_void_p],
     "iit_gemm_dual_ok": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 7 + [c_void_p] * 4 + [c_long] * 4 + [c_int] * 5,
     "iit_gemm_dual": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 6 + [c_void_p] * 2 + [c_void_p] * 4 + [c_long] * 4
                      + [c_int] * 5 + [c_void_p] * 4,
@@ -619,6 +621,19 @@ def flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, head_mask: int, scale: float,
                                ctypes.cast(gs, c_void_p), head_mask, B, S, Hq, Hkv, dh, scale, int(causal),
                                None if spec is None else spec.ptr, _stream()),
            "flash_bwd")
+
+
+def maxpool3s2_fwd(x, y, idx, N: int, H: int, W: int, C: int):
+    """3x3 / stride 2 / padding 1 max pool of channels-last bf16 ``x`` [N, C, H, W] into ``y``; ``idx``: uint8 argmax
+    tap per output element (csrc/bn_nhwc.hip)."""
+    if CHECK_BOUNDS:
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        assert y.numel() == N * OH * OW * C and idx.numel() == y.numel() and x.numel() == N * H * W * C
+    _check(lib().iit_maxpool3s2_fwd(_p(x), _p(y), _p(idx), N, H, W, C, _stream()), "maxpool3s2_fwd")
+
+
+def maxpool3s2_bwd(dy, idx, dx, N: int, H: int, W: int, C: int):
+    _check(lib().iit_maxpool3s2_bwd(_p(dy), _p(idx), _p(dx), N, H, W, C, _stream()), "maxpool3s2_bwd")
 
 
 def bn_fwd(x, res, y, ws, rmean, rvar, w, b, M: int, C: int, eps: float, relu: bool, training: bool, save,

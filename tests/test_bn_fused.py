@@ -201,15 +201,18 @@ def test_bn_splice_on_read_exact(res, training):
 
 def test_resnet_conv_mirror_matches_autocast_path(monkeypatch):
     """resnet.Conv2d under bf16 autocast with its weight in a flat arena convolves with the arena's bf16 mirror
-    (torch_ops._MirrorWeight) and adds the bf16 weight gradient into the fp32 slot: the logits equal the autocast
-    cast path's and every gradient matches it (the mirror holds the same bf16 rounding of the fp32 master)."""
+    (torch_ops._MirrorWeight) and adds the bf16 weight gradient into the fp32 slot.  Against the fp32 model, its
+    logits and every parameter gradient are within the autocast cast path's own bf16 error (plus a small floor: the
+    mirror holds the same bf16 rounding of the master, but the fused BN statistics' fp32 atomics make no two bf16
+    runs bitwise equal), and every convolution took the mirror."""
     from iit_amd.engine.flat import FlatParams
     from iit_amd.models.resnet import resnet18
     from iit_amd.ops import torch_ops
     torch.manual_seed(3)
-    ms = [resnet18(num_classes=10).to(dev).to(memory_format=torch.channels_last) for _ in range(2)]
-    ms[1].load_state_dict(ms[0].state_dict())
-    for m in ms:
+    ms = [resnet18(num_classes=10).to(dev).to(memory_format=torch.channels_last) for _ in range(3)]
+    for m in ms[1:]:
+        m.load_state_dict(ms[0].state_dict())
+    for m in ms[:2]:
         FlatParams(m)
     x = torch.rand(32, 3, 84, 84, device=dev).contiguous(memory_format=torch.channels_last)
     t = torch.randint(0, 10, (32,), device=dev)
@@ -217,15 +220,41 @@ def test_resnet_conv_mirror_matches_autocast_path(monkeypatch):
     orig = torch_ops._MirrorWeight.apply
     monkeypatch.setattr(torch_ops._MirrorWeight, "apply", lambda *a: calls.append(1) or orig(*a))
     outs = []
-    for m, env in ((ms[0], "1"), (ms[1], "0")):
+    for m, env, amp in ((ms[0], "1", True), (ms[1], "0", True), (ms[2], "0", False)):
         monkeypatch.setenv("IIT_CONV_MIRROR", env)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             y = m(x)
             loss = torch.nn.functional.cross_entropy(y.float(), t)
         loss.backward()
         outs.append(y.float().detach())
     assert len(calls) == 20  # every convolution of ResNet-18 took the mirror (model 0 only)
-    assert rel(outs[0], outs[1]) < 1e-2  # (the fused BN statistics use fp32 atomics: not bitwise run to run)
-    for (n, pa), (_, pb) in zip(ms[0].named_parameters(), ms[1].named_parameters()):
-        assert pa.grad is not None and pb.grad is not None, n
-        assert rel(pa.grad, pb.grad) < 2e-2, (n, rel(pa.grad, pb.grad))
+    ym, yc, yr = outs
+    assert rel(ym, yr) <= 1.5 * rel(yc, yr) + 1e-2, (rel(ym, yr), rel(yc, yr))
+    for (n, pm), (_, pc), (_, pr) in zip(*(m.named_parameters() for m in ms)):
+        assert pm.grad is not None and pc.grad is not None, n
+        em, ec = rel(pm.grad, pr.grad), rel(pc.grad, pr.grad)
+        assert em <= 1.5 * ec + 2e-2, (n, em, ec)
+
+
+@pytest.mark.parametrize("shape,ties", [((4, 64, 42, 42), False), ((2, 16, 9, 7), True), ((3, 8, 10, 11), True)])
+def test_maxpool3s2_matches_torch(shape, ties):
+    """The NHWC bf16 3x3/s2/p1 max pool (byte argmax, gather backward) against torch's max_pool2d on the same bf16
+    input: outputs equal exactly, and the input gradient equals torch's (ties resolved to the first tap in scan order,
+    as torch's kernel does; integer-valued inputs make ties common)."""
+    from iit_amd.ops.bn import MaxPool3s2Fn
+    torch.manual_seed(7)
+    N, C, H, W = shape
+    x = (torch.randint(-3, 4, shape, device=dev).float() if ties else torch.randn(shape, device=dev))
+    x = x.bfloat16().contiguous(memory_format=torch.channels_last)
+    g = torch.randn(N, C, (H - 1) // 2 + 1, (W - 1) // 2 + 1, device=dev).bfloat16()
+    xa = x.clone().requires_grad_(True)
+    ya = MaxPool3s2Fn.apply(xa)
+    ya.backward(g)
+    xb = x.clone().requires_grad_(True)
+    yb = torch.nn.functional.max_pool2d(xb, 3, 2, 1)
+    yb.backward(g)
+    assert ya.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(ya, yb)
+    assert rel(xa.grad, xb.grad) < 1e-2, rel(xa.grad, xb.grad)
+    # routing: the gradient lands on the same elements
+    assert torch.equal(xa.grad != 0, xb.grad != 0)
