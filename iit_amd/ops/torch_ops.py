@@ -56,6 +56,17 @@ def _accumulate(p: torch.Tensor, g: torch.Tensor) -> None:
         flat = getattr(p, "_iit_flat", None)
         slot = flat.bind_zero(p) if flat is not None and flat.owns(p) else torch.zeros_like(p)
         p.grad = slot
+    if (g.dtype == torch.bfloat16 and slot.dtype == torch.float32 and slot.is_cuda and g.is_cuda
+            and slot.shape == g.shape and slot.stride() == g.stride()
+            and (slot.is_contiguous() or (slot.dim() == 4 and slot.is_contiguous(memory_format=torch.channels_last)))):
+        # same memory order (e.g. a channels-last conv weight and its gradient): one HIP pass over the dense span,
+        # fp32 += bf16 (the same math as cast + add, one launch instead of two)
+        from . import hip_kernels as K
+        if K.available():
+            n = slot.numel()
+            K.add_bf16(slot, n, slot, n, g, n, None, 1, n)
+            grad_hooks.notify(p)
+            return
     if g.dtype != slot.dtype and g.numel() <= (1 << 20):
         # small vectors (norm weights): cast + same-dtype add is two ~3 us launches; ROCm's mixed-dtype
         # add kernel takes ~50 us on a 4096-vector
