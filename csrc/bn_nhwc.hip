@@ -25,10 +25,15 @@
 // ever read with a plain load, so no acquire-side invalidate is needed either.
 #include "common.h"
 #include "splice_spec.h"
+#include <stdlib.h>
 
 namespace {
 
 constexpr int TPB = 256;
+// the per-channel accumulator is spread over BN_SLOTS copies (workgroup b adds into slot b % BN_SLOTS; the last
+// workgroup sums them): 1/BN_SLOTS of the memory-side atomics per address -- a few thousand workgroups adding into
+// the same 2C addresses serialised on them
+constexpr int BN_SLOTS = 8;
 
 // Interchange splice of the BN input (the preceding conv's hook, ``hook_point`` of mode-"q" PVR sites): the
 // activation the kernels read is x' = where(spec, src, x), spec over the logical [N][C][H][W] with src's element
@@ -137,6 +142,7 @@ __global__ __launch_bounds__(TPB) void bn_stats_kernel(const __bf16* __restrict_
 #pragma unroll
   for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
   if (r < rpi) {
+#pragma unroll 4  // several rows' loads in flight per thread (the loop was latency-bound)
     for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
       unsigned hit;
       const Row8 v = load_x<SP>(x, row, C, g * 8, xs, hit);
@@ -147,10 +153,14 @@ __global__ __launch_bounds__(TPB) void bn_stats_kernel(const __bf16* __restrict_
       }
     }
   }
-  block_channel_add(s, q, C, G, rpi, tid, acc, red);
+  block_channel_add(s, q, C, G, rpi, tid, acc + (blockIdx.x % BN_SLOTS) * 2 * C, red);
   if (!last_block(ticket, tid, &flag)) return;
   for (int c = tid; c < C; c += TPB) {
-    const float sum = atomicExch(acc + c, 0.f), sq = atomicExch(acc + C + c, 0.f);
+    float sum = 0.f, sq = 0.f;
+    for (int k = 0; k < BN_SLOTS; ++k) {
+      sum += atomicExch(acc + k * 2 * C + c, 0.f);
+      sq += atomicExch(acc + k * 2 * C + C + c, 0.f);
+    }
     const float mean = sum / (float)M;
     const float var = fmaxf(sq / (float)M - mean * mean, 0.f);
     save[c] = mean;
@@ -193,6 +203,7 @@ __global__ __launch_bounds__(TPB) void bn_apply_kernel(const __bf16* __restrict_
     sc[e] = w[c] * rstd;
     sh[e] = b[c] - mean * sc[e];
   }
+#pragma unroll 4
   for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
     unsigned hit;
     Row8 v = load_x<SP>(x, row, C, g * 8, xs, hit);
@@ -230,6 +241,7 @@ __global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const __bf16* __restr
     rstd[e] = save[C + g * 8 + e];
   }
   if (r < rpi) {
+#pragma unroll 4  // several rows' loads in flight per thread (the loop was latency-bound)
     for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
       const long o = row * C + g * 8;
       Row8 d = load8(dy + o);
@@ -247,10 +259,14 @@ __global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const __bf16* __restr
       }
     }
   }
-  block_channel_add(s, q, C, G, rpi, tid, acc, red);
+  block_channel_add(s, q, C, G, rpi, tid, acc + (blockIdx.x % BN_SLOTS) * 2 * C, red);
   if (!last_block(ticket, tid, &flag)) return;
   for (int c = tid; c < C; c += TPB) {  // coef = (sum dz, sum dz xhat); parameter gradients accumulated
-    const float sdz = atomicExch(acc + c, 0.f), sdzx = atomicExch(acc + C + c, 0.f);
+    float sdz = 0.f, sdzx = 0.f;
+    for (int k = 0; k < BN_SLOTS; ++k) {
+      sdz += atomicExch(acc + k * 2 * C + c, 0.f);
+      sdzx += atomicExch(acc + k * 2 * C + C + c, 0.f);
+    }
     coef[c] = sdz;
     coef[C + c] = sdzx;
     if (dw) dw[c] += sdzx;
@@ -279,6 +295,7 @@ __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(const __bf16* __restr
     k2[e] = batch ? acc[c] * inv_m : 0.f;
     k3[e] = batch ? acc[C + c] * inv_m : 0.f;
   }
+#pragma unroll 4
   for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
     const long o = row * C + g * 8;
     Row8 d = load8(dy + o);
@@ -314,11 +331,21 @@ __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(const __bf16* __restr
   }
 }
 
+int bn_rows_per_group() {  // IIT_BN_ROWS (A/B of the grid size; default 8), read once per process
+  static const int v = [] {
+    const char* e = getenv("IIT_BN_ROWS");
+    const int r = e ? atoi(e) : 8;
+    return r >= 1 && r <= 256 ? r : 8;
+  }();
+  return v;
+}
+
 int grid_for(long M, int C) {
   const int rpi = TPB / (C / 8);
   const long want = (M + rpi - 1) / rpi;
   // ~8 rows per thread group: enough work per workgroup to amortise the per-channel atomics, >= 4 workgroups per CU
-  long g = (want + 7) / 8;
+  const int rows = bn_rows_per_group();
+  long g = (want + rows - 1) / rows;
   if (g < 1) g = 1;
   if (g > 2048) g = 2048;
   return (int)g;
@@ -449,7 +476,7 @@ IIT_EXPORT int iit_maxpool3s2_bwd(const void* dy, const void* idx, void* dx, int
   return (int)hipGetLastError();
 }
 
-// forward: ws = per-module accumulator (fp32 [2C] + a u32 ticket after it, zero at the first call, re-armed by
+// forward: ws = per-module accumulator (fp32 [BN_SLOTS][2C] + a u32 ticket after it, zero at the first call, re-armed by
 // every call); y = relu?(bn(x) (+ res)); save [2C] = mean, rstd (the batch's in training, the running ones in eval)
 static bool make_xsplice(XSplice& xs, const void* src, const void* spec, long M, int C, int H, int W) {
   xs = XSplice{};
@@ -476,13 +503,13 @@ IIT_EXPORT int iit_bn_fwd(const void* x, const void* res, void* y, float* ws, fl
   if (xs.src) {
     if (training)
       hipLaunchKernelGGL(bn_stats_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, M, C, ws,
-                         (unsigned*)(ws + 2 * C), save, rmean, rvar, eps, momentum, nbt, xs);
+                         (unsigned*)(ws + BN_SLOTS * 2 * C), save, rmean, rvar, eps, momentum, nbt, xs);
     hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, (const __bf16*)res,
                        (__bf16*)y, save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training, xs);
   } else {
     if (training)
       hipLaunchKernelGGL(bn_stats_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, M, C, ws,
-                         (unsigned*)(ws + 2 * C), save, rmean, rvar, eps, momentum, nbt, xs);
+                         (unsigned*)(ws + BN_SLOTS * 2 * C), save, rmean, rvar, eps, momentum, nbt, xs);
     hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, (const __bf16*)res,
                        (__bf16*)y, save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training, xs);
   }
@@ -503,14 +530,17 @@ IIT_EXPORT int iit_bn_bwd(const void* dy, const void* y, const void* x, const fl
   const int grid = grid_for(M, C);
   if (xs.src) {
     hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
-                       (const __bf16*)x, save, M, C, ws, (unsigned*)(ws + 2 * C), coef, dw, db, xs);
+                       (const __bf16*)x, save, M, C, ws, (unsigned*)(ws + BN_SLOTS * 2 * C), coef, dw, db, xs);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
                        (const __bf16*)x, save, w, (const float*)coef, M, C, training, (__bf16*)dx, (__bf16*)dres, xs);
   } else {
     hipLaunchKernelGGL(bn_bwd_stats_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
-                       (const __bf16*)x, save, M, C, ws, (unsigned*)(ws + 2 * C), coef, dw, db, xs);
+                       (const __bf16*)x, save, M, C, ws, (unsigned*)(ws + BN_SLOTS * 2 * C), coef, dw, db, xs);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
                        (const __bf16*)x, save, w, (const float*)coef, M, C, training, (__bf16*)dx, (__bf16*)dres, xs);
   }
   return (int)hipGetLastError();
 }
+
+// floats of the per-module accumulator ``ws`` (ops/bn.py allocates it zeroed)
+IIT_EXPORT int iit_bn_ws_floats(int C) { return BN_SLOTS * 2 * C + 1; }

@@ -46,11 +46,12 @@ def covered(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res: Optional[torch.Tenso
 
 
 def _ws(bn: torch.nn.BatchNorm2d, C: int, device) -> torch.Tensor:
-    """The module's self-re-arming reduction accumulator: 2C floats + a ticket, zero at creation; every kernel call
+    """The module's self-re-arming reduction accumulator: [slots][2C] floats + a ticket, zero at creation; every kernel call
     leaves it zero again (csrc/bn_nhwc.hip).  Shared by the forward and backward of every call on the stream."""
+    n = K.bn_ws_floats(C)
     ws = bn.__dict__.get("_iit_bn_ws")
-    if ws is None or ws.numel() < 2 * C + 1 or ws.device != device:
-        ws = bn.__dict__["_iit_bn_ws"] = torch.zeros(2 * C + 1, dtype=F32, device=device)
+    if ws is None or ws.numel() < n or ws.device != device:
+        ws = bn.__dict__["_iit_bn_ws"] = torch.zeros(n, dtype=F32, device=device)
     return ws
 
 

@@ -96,6 +96,7 @@ _SIGS = {
                                     c_int, c_int, c_void_p],
     "iit_gemm_glds_set_prof": [c_void_p],
     "iit_maxpool3s2_fwd": [c_void_p] * 3 + [c_int] * 4 + [c_void_p],
+    "iit_bn_ws_floats": [c_int],
     "iit_maxpool3s2_bwd": [c_void_p] * 3 + [c_int] * 4 + [c_void_p],
     "iit_gemm_dual_ok": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 7 + [c_void_p] * 4 + [c_long] * 4 + [c_int] * 5,
     "iit_gemm_dual": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 6 + [c_void_p] * 2 + [c_void_p] * 4 + [c_long] * 4
@@ -621,6 +622,11 @@ def flash_bwd(q, k, v, z, dz, lse, dd, dq, dk, dv, head_mask: int, scale: float,
                                ctypes.cast(gs, c_void_p), head_mask, B, S, Hq, Hkv, dh, scale, int(causal),
                                None if spec is None else spec.ptr, _stream()),
            "flash_bwd")
+
+
+def bn_ws_floats(C: int) -> int:
+    """Length of the fused BatchNorm's self-re-arming accumulator for C channels (csrc/bn_nhwc.hip)."""
+    return int(lib().iit_bn_ws_floats(C))
 
 
 def maxpool3s2_fwd(x, y, idx, N: int, H: int, W: int, C: int):
