@@ -1,4 +1,4 @@
-// Fused BatchNorm (+ residual add) (+ ReLU) for NHWC (channels-last) bf16 activations -- the PVR ResNet-18's
+// Fused BatchNorm (+ residual add) (+ ReLU) for NHWC (channels-last) bf16 or fp32 activations -- the PVR ResNet-18's
 // normalisation, forward and backward, in place of MIOpenBatchNormFwdTrainSpatial / MIOpenBatchNormBwdSpatial plus
 // the separate ReLU, residual-add and running-statistics kernels (profiles/bench_family_pvr_resnet18_r4.txt: 5.0 ms
 // of norm and ~3 ms of elementwise per bf16 step).
@@ -39,7 +39,7 @@ constexpr int BN_SLOTS = 8;
 // activation the kernels read is x' = where(spec, src, x), spec over the logical [N][C][H][W] with src's element
 // strides; the backward zeroes the spliced elements' input gradient (SpliceFn's semantics).  ``hw`` = H * W, ``W``.
 struct XSplice {
-  const __bf16* src;
+  const void* src;  // the activation's dtype (bf16 or fp32)
   int hw, W;
   SpliceSpec sp;
 };
@@ -63,10 +63,18 @@ __device__ __forceinline__ Row8 load8(const __bf16* p) {
   return r;
 }
 
+__device__ __forceinline__ Row8 load8(const float* p) {  // fp32 activations (the reference-precision PVR step)
+  const float4 a = ((const float4*)p)[0], b = ((const float4*)p)[1];
+  Row8 r;
+  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  return r;
+}
+
 // x' row segment [c0, c0 + 8) of row ``row`` (the spliced input when xs.src is set); ``hit`` = which of the 8
 // elements came from the source (their input gradient is zero)
-template <bool SP>
-__device__ __forceinline__ Row8 load_x(const __bf16* x, long row, int C, int c0, const XSplice& xs, unsigned& hit) {
+template <bool SP, typename T>
+__device__ __forceinline__ Row8 load_x(const T* x, long row, int C, int c0, const XSplice& xs, unsigned& hit) {
   Row8 v = load8(x + row * C + c0);
   hit = 0u;
   if (SP) {
@@ -75,7 +83,7 @@ __device__ __forceinline__ Row8 load_x(const __bf16* x, long row, int C, int c0,
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         if (in_ranges(xs.sp, 1, c0 + e)) {
-          v.v[e] = bf2f(xs.src[sb + (long)(c0 + e) * xs.sp.sstride[1]]);
+          v.v[e] = (float)((const T*)xs.src)[sb + (long)(c0 + e) * xs.sp.sstride[1]];
           hit |= 1u << e;
         }
     }
@@ -88,6 +96,11 @@ __device__ __forceinline__ void store8(__bf16* p, const Row8& r) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) t[e] = f2bf(r.v[e]);
   *(bf16x8*)p = t;
+}
+
+__device__ __forceinline__ void store8(float* p, const Row8& r) {
+  ((float4*)p)[0] = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
+  ((float4*)p)[1] = make_float4(r.v[4], r.v[5], r.v[6], r.v[7]);
 }
 
 // block reduction of per-thread [8] pairs (a, b) over the threads sharing a channel group; adds the block totals
@@ -129,8 +142,8 @@ __device__ __forceinline__ bool last_block(unsigned* ticket, int tid, int* flag)
 
 // acc[0, C) += sum_rows x, acc[C, 2C) += sum_rows x^2; the last workgroup turns the totals into save = (mean, rstd),
 // updates the running statistics and num_batches_tracked, and re-arms acc / ticket
-template <bool SP>
-__global__ __launch_bounds__(TPB) void bn_stats_kernel(const __bf16* __restrict__ x, long M, int C, float* acc,
+template <bool SP, typename T>
+__global__ __launch_bounds__(TPB) void bn_stats_kernel(const T* __restrict__ x, long M, int C, float* acc,
                                                        unsigned* ticket, float* __restrict__ save, float* rmean,
                                                        float* rvar, float eps, float momentum, long long* nbt,
                                                        XSplice xs) {
@@ -179,9 +192,9 @@ __global__ __launch_bounds__(TPB) void bn_stats_kernel(const __bf16* __restrict_
 
 // y = relu?(x * scale + shift (+ res)); training: mean / rstd from ``save`` (the stats kernel); eval: from the running
 // statistics, and workgroup 0 writes them to ``save`` for the backward
-template <bool SP>
-__global__ __launch_bounds__(TPB) void bn_apply_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ res,
-                                                       __bf16* __restrict__ y, float* __restrict__ save,
+template <bool SP, typename T>
+__global__ __launch_bounds__(TPB) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                       T* __restrict__ y, float* __restrict__ save,
                                                        const float* __restrict__ rmean, const float* __restrict__ rvar,
                                                        const float* __restrict__ w, const float* __restrict__ b, long M,
                                                        int C, float eps, int relu, int batch, XSplice xs) {
@@ -224,9 +237,9 @@ __global__ __launch_bounds__(TPB) void bn_apply_kernel(const __bf16* __restrict_
 }
 
 // acc[0, C) += sum dz, acc[C, 2C) += sum dz * xhat   (dz = dy masked by y > 0 when y is given)
-template <bool SP>
-__global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ y,
-                                                           const __bf16* __restrict__ x, const float* __restrict__ save,
+template <bool SP, typename T>
+__global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                           const T* __restrict__ x, const float* __restrict__ save,
                                                            long M, int C, float* acc, unsigned* ticket,
                                                            float* __restrict__ coef, float* dw, float* db, XSplice xs) {
   __shared__ float red[TPB * 16];
@@ -248,9 +261,9 @@ __global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const __bf16* __restr
       unsigned hit;
       const Row8 xv = load_x<SP>(x, row, C, g * 8, xs, hit);
       if (y) {
-        const bf16x8 yv = *(const bf16x8*)(y + o);
+        const Row8 yv = load8(y + o);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) d.v[e] = bf2f(yv[e]) > 0.f ? d.v[e] : 0.f;
+        for (int e = 0; e < 8; ++e) d.v[e] = yv.v[e] > 0.f ? d.v[e] : 0.f;
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -275,12 +288,12 @@ __global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const __bf16* __restr
   if (tid == 0) atomicExch(ticket, 0u);
 }
 
-template <bool SP>
-__global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ y,
-                                                           const __bf16* __restrict__ x, const float* __restrict__ save,
+template <bool SP, typename T>
+__global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                           const T* __restrict__ x, const float* __restrict__ save,
                                                            const float* __restrict__ w, const float* __restrict__ acc,
-                                                           long M, int C, int batch, __bf16* __restrict__ dx,
-                                                           __bf16* __restrict__ dres, XSplice xs) {
+                                                           long M, int C, int batch, T* __restrict__ dx,
+                                                           T* __restrict__ dres, XSplice xs) {
   const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
   const int g = tid % G, r = tid / G;
   if (r >= rpi) return;
@@ -300,9 +313,9 @@ __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(const __bf16* __restr
     const long o = row * C + g * 8;
     Row8 d = load8(dy + o);
     if (y) {
-      const bf16x8 yv = *(const bf16x8*)(y + o);
+      const Row8 yv = load8(y + o);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d.v[e] = bf2f(yv[e]) > 0.f ? d.v[e] : 0.f;
+      for (int e = 0; e < 8; ++e) d.v[e] = yv.v[e] > 0.f ? d.v[e] : 0.f;
     }
     if (dres) store8(dres + o, d);
     Row8 out;
@@ -361,7 +374,8 @@ bool shape_ok(long M, int C, const void* p) {
 // (8x fewer index bytes), and a gather-form backward: each input element sums the gradients of the (up to 4)
 // windows that hold it and chose it -- no scatter, no atomics, no zero-fill of the input gradient.  Ties and NaN
 // follow torch's kernel: the first tap in scan order wins, a NaN is taken.  One thread per 8 channels.
-__global__ __launch_bounds__(256) void maxpool3s2_fwd_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool3s2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                              unsigned char* __restrict__ idx, int N, int H, int W,
                                                              int C, int OH, int OW) {
   const int c8n = C / 8;
@@ -390,10 +404,10 @@ __global__ __launch_bounds__(256) void maxpool3s2_fwd_kernel(const __bf16* __res
     for (int kw = 0; kw < 3; ++kw) {
       const int iw = 2 * ow - 1 + kw;
       if (iw < 0 || iw >= W) continue;
-      const bf16x8 v = *(const bf16x8*)(x + (((long)n * H + ih) * W + iw) * C + c8 * 8);
+      const Row8 v = load8(x + (((long)n * H + ih) * W + iw) * C + c8 * 8);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float f = bf2f(v[e]);
+        const float f = v.v[e];
         if (first || f > best[e] || f != f) {
           best[e] = f;
           arg[e] = (unsigned char)(kh * 3 + kw);
@@ -402,20 +416,21 @@ __global__ __launch_bounds__(256) void maxpool3s2_fwd_kernel(const __bf16* __res
       first = false;
     }
   }
-  bf16x8 o;
+  Row8 o;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
+  for (int e = 0; e < 8; ++e) o.v[e] = best[e];
   const long oi = (((long)n * OH + oh) * OW + ow) * C + c8 * 8;
-  *(bf16x8*)(y + oi) = o;
+  store8(y + oi, o);
   unsigned long long packed = 0;
 #pragma unroll
   for (int e = 0; e < 8; ++e) packed |= (unsigned long long)arg[e] << (8 * e);
   *(unsigned long long*)(idx + oi) = packed;
 }
 
-__global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const __bf16* __restrict__ dy,
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const T* __restrict__ dy,
                                                              const unsigned char* __restrict__ idx,
-                                                             __bf16* __restrict__ dx, int N, int H, int W, int C,
+                                                             T* __restrict__ dx, int N, int H, int W, int C,
                                                              int OH, int OW) {
   const int c8n = C / 8;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -442,37 +457,48 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const __bf16* __res
       const int ow = tw >> 1;
       const long oi = (((long)n * OH + oh) * OW + ow) * C + c8 * 8;
       const unsigned long long packed = *(const unsigned long long*)(idx + oi);
-      const bf16x8 g = *(const bf16x8*)(dy + oi);
+      const Row8 g = load8(dy + oi);
       const unsigned tap = (unsigned)(kh * 3 + kw);
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        if (((packed >> (8 * e)) & 0xffull) == tap) acc[e] += bf2f(g[e]);
+        if (((packed >> (8 * e)) & 0xffull) == tap) acc[e] += g.v[e];
     }
   }
-  bf16x8 o;
+  Row8 o;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
-  *(bf16x8*)(dx + (((long)n * H + ih) * W + iw) * C + c8 * 8) = o;
+  for (int e = 0; e < 8; ++e) o.v[e] = acc[e];
+  store8(dx + (((long)n * H + ih) * W + iw) * C + c8 * 8, o);
 }
 
 }  // namespace
 
 // channels-last bf16 [N][H][W][C] -> [N][OH][OW][C] (OH = (H - 1) / 2 + 1, OW likewise), idx one byte per output
-IIT_EXPORT int iit_maxpool3s2_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, void* stream) {
+// ``f32``: fp32 activations instead of bf16
+IIT_EXPORT int iit_maxpool3s2_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int f32,
+                                  void* stream) {
   const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
   if (C % 8 || (((uintptr_t)x) & 15) || (((uintptr_t)y) & 15) || (((uintptr_t)idx) & 7)) return (int)hipErrorInvalidValue;
   const long total = (long)N * OH * OW * (C / 8);
-  hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     (const __bf16*)x, (__bf16*)y, (unsigned char*)idx, N, H, W, C, OH, OW);
+  if (f32)
+    hipLaunchKernelGGL(maxpool3s2_fwd_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)x, (float*)y, (unsigned char*)idx, N, H, W, C, OH, OW);
+  else
+    hipLaunchKernelGGL(maxpool3s2_fwd_kernel<__bf16>, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const __bf16*)x, (__bf16*)y, (unsigned char*)idx, N, H, W, C, OH, OW);
   return (int)hipGetLastError();
 }
 
-IIT_EXPORT int iit_maxpool3s2_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C, void* stream) {
+IIT_EXPORT int iit_maxpool3s2_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C, int f32,
+                                  void* stream) {
   const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
   if (C % 8 || (((uintptr_t)dy) & 15) || (((uintptr_t)dx) & 15) || (((uintptr_t)idx) & 7)) return (int)hipErrorInvalidValue;
   const long total = (long)N * H * W * (C / 8);
-  hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     (const __bf16*)dy, (const unsigned char*)idx, (__bf16*)dx, N, H, W, C, OH, OW);
+  if (f32)
+    hipLaunchKernelGGL(maxpool3s2_bwd_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)dy, (const unsigned char*)idx, (float*)dx, N, H, W, C, OH, OW);
+  else
+    hipLaunchKernelGGL(maxpool3s2_bwd_kernel<__bf16>, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const __bf16*)dy, (const unsigned char*)idx, (__bf16*)dx, N, H, W, C, OH, OW);
   return (int)hipGetLastError();
 }
 
@@ -481,7 +507,7 @@ IIT_EXPORT int iit_maxpool3s2_bwd(const void* dy, const void* idx, void* dx, int
 static bool make_xsplice(XSplice& xs, const void* src, const void* spec, long M, int C, int H, int W) {
   xs = XSplice{};
   if (!src || !spec) return true;
-  xs.src = (const __bf16*)src;
+  xs.src = src;
   xs.sp = *(const SpliceSpec*)spec;
   xs.hw = H * W;
   xs.W = W;
@@ -489,57 +515,76 @@ static bool make_xsplice(XSplice& xs, const void* src, const void* spec, long M,
          xs.sp.shape[3] == W;
 }
 
+template <typename T>
+int bn_fwd_impl(const void* x, const void* res, void* y, float* ws, float* rmean, float* rvar, const float* w,
+                const float* b, long M, int C, float eps, int relu, int training, float* save, float momentum,
+                long long* nbt, const XSplice& xs, hipStream_t s) {
+  const int grid = grid_for(M, C);
+  unsigned* ticket = (unsigned*)(ws + BN_SLOTS * 2 * C);
+  // the splice-reading instantiations only where a splice is given (the others keep the lean inner loop)
+  if (xs.src) {
+    if (training)
+      hipLaunchKernelGGL((bn_stats_kernel<true, T>), dim3(grid), dim3(TPB), 0, s, (const T*)x, M, C, ws, ticket, save,
+                         rmean, rvar, eps, momentum, nbt, xs);
+    hipLaunchKernelGGL((bn_apply_kernel<true, T>), dim3(grid), dim3(TPB), 0, s, (const T*)x, (const T*)res, (T*)y,
+                       save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training, xs);
+  } else {
+    if (training)
+      hipLaunchKernelGGL((bn_stats_kernel<false, T>), dim3(grid), dim3(TPB), 0, s, (const T*)x, M, C, ws, ticket, save,
+                         rmean, rvar, eps, momentum, nbt, xs);
+    hipLaunchKernelGGL((bn_apply_kernel<false, T>), dim3(grid), dim3(TPB), 0, s, (const T*)x, (const T*)res, (T*)y,
+                       save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training, xs);
+  }
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int bn_bwd_impl(const void* dy, const void* y, const void* x, const float* save, const float* w, float* ws,
+                float* coef, long M, int C, int training, void* dx, void* dres, float* dw, float* db,
+                const XSplice& xs, hipStream_t s) {
+  const int grid = grid_for(M, C);
+  unsigned* ticket = (unsigned*)(ws + BN_SLOTS * 2 * C);
+  if (xs.src) {
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<true, T>), dim3(grid), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
+                       (const T*)x, save, M, C, ws, ticket, coef, dw, db, xs);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, T>), dim3(grid), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
+                       (const T*)x, save, w, (const float*)coef, M, C, training, (T*)dx, (T*)dres, xs);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<false, T>), dim3(grid), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
+                       (const T*)x, save, M, C, ws, ticket, coef, dw, db, xs);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, T>), dim3(grid), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
+                       (const T*)x, save, w, (const float*)coef, M, C, training, (T*)dx, (T*)dres, xs);
+  }
+  return (int)hipGetLastError();
+}
+
+// ``f32``: the activations (x, res, y, dy, dx, dres, the splice source) are fp32 instead of bf16
 IIT_EXPORT int iit_bn_fwd(const void* x, const void* res, void* y, float* ws, float* rmean, float* rvar,
                           const float* w, const float* b, long M, int C, float eps, int relu, int training,
                           float* save, float momentum, long long* nbt, const void* src, const void* spec, int H,
-                          int W, void* stream) {
+                          int W, int f32, void* stream) {
   if (!shape_ok(M, C, x) || ((uintptr_t)y & 15) || (res && ((uintptr_t)res & 15))) return (int)hipErrorInvalidValue;
   if (!rmean || !rvar) return (int)hipErrorInvalidValue;
   XSplice xs;
   if (!make_xsplice(xs, src, spec, M, C, H, W)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  const int grid = grid_for(M, C);
-  // the splice-reading instantiations only where a splice is given (the others keep the lean inner loop)
-  if (xs.src) {
-    if (training)
-      hipLaunchKernelGGL(bn_stats_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, M, C, ws,
-                         (unsigned*)(ws + BN_SLOTS * 2 * C), save, rmean, rvar, eps, momentum, nbt, xs);
-    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, (const __bf16*)res,
-                       (__bf16*)y, save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training, xs);
-  } else {
-    if (training)
-      hipLaunchKernelGGL(bn_stats_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, M, C, ws,
-                         (unsigned*)(ws + BN_SLOTS * 2 * C), save, rmean, rvar, eps, momentum, nbt, xs);
-    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)x, (const __bf16*)res,
-                       (__bf16*)y, save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training, xs);
-  }
-  return (int)hipGetLastError();
+  return f32 ? bn_fwd_impl<float>(x, res, y, ws, rmean, rvar, w, b, M, C, eps, relu, training, save, momentum, nbt, xs, s)
+             : bn_fwd_impl<__bf16>(x, res, y, ws, rmean, rvar, w, b, M, C, eps, relu, training, save, momentum, nbt, xs, s);
 }
 
 // backward: ws as in the forward; coef [2C] scratch; dx (and dres = the residual's gradient when non-null);
 // dw / db (nullable) ACCUMULATED into
 IIT_EXPORT int iit_bn_bwd(const void* dy, const void* y, const void* x, const float* save, const float* w,
                           float* ws, float* coef, long M, int C, int training, void* dx, void* dres, float* dw,
-                          float* db, const void* src, const void* spec, int H, int W, void* stream) {
+                          float* db, const void* src, const void* spec, int H, int W, int f32, void* stream) {
   if (!shape_ok(M, C, dy) || ((uintptr_t)x & 15) || ((uintptr_t)dx & 15) || (y && ((uintptr_t)y & 15)) ||
       (dres && ((uintptr_t)dres & 15)))
     return (int)hipErrorInvalidValue;
   XSplice xs;
   if (!make_xsplice(xs, src, spec, M, C, H, W)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  const int grid = grid_for(M, C);
-  if (xs.src) {
-    hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
-                       (const __bf16*)x, save, M, C, ws, (unsigned*)(ws + BN_SLOTS * 2 * C), coef, dw, db, xs);
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
-                       (const __bf16*)x, save, w, (const float*)coef, M, C, training, (__bf16*)dx, (__bf16*)dres, xs);
-  } else {
-    hipLaunchKernelGGL(bn_bwd_stats_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
-                       (const __bf16*)x, save, M, C, ws, (unsigned*)(ws + BN_SLOTS * 2 * C), coef, dw, db, xs);
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(grid), dim3(TPB), 0, s, (const __bf16*)dy, (const __bf16*)y,
-                       (const __bf16*)x, save, w, (const float*)coef, M, C, training, (__bf16*)dx, (__bf16*)dres, xs);
-  }
-  return (int)hipGetLastError();
+  return f32 ? bn_bwd_impl<float>(dy, y, x, save, w, ws, coef, M, C, training, dx, dres, dw, db, xs, s)
+             : bn_bwd_impl<__bf16>(dy, y, x, save, w, ws, coef, M, C, training, dx, dres, dw, db, xs, s);
 }
 
 // floats of the per-module accumulator ``ws`` (ops/bn.py allocates it zeroed)

@@ -30,6 +30,9 @@ def parse(argv=None):
     ap.add_argument("--conv-benchmark", type=int, default=1,
                     help="1: MIOpen find mode (torch.backends.cudnn.benchmark) -- the fastest measured convolution "
                          "solution per shape; the PVR bf16 step 12.5 -> 9.0 ms (profiles/pvr_step_r5.txt)")
+    ap.add_argument("--channels-last", type=int, default=1,
+                    help="1: NHWC ResNet on the GPU -- MIOpen's NHWC convolutions and the fused NHWC BatchNorm / pool "
+                         "kernels (fp32 PVR step 18.9 -> 14.6 ms, profiles/bn_fp32_r5.txt)")
     return ap.parse_args(argv)
 
 
@@ -44,6 +47,8 @@ def main(argv=None):
     train_set, test_set = get_dataset(args.task, dataset_config=dataset_config)
     ll_model, hl_model, corr = get_alignment(args.task, config={"input_shape": test_set.base_data.get_input_shape(),
                                                                 "mode": args.mode, "hook_point": args.hook_point})
+    if args.channels_last and torch.cuda.is_available():
+        ll_model.to(memory_format=torch.channels_last)  # (state_dict layout-independent: checkpoints interchange)
     model_pair = IITBehaviorModelPair(ll_model=ll_model, hl_model=hl_model, corr=corr, training_args=training_args)
     model_pair.train(train_set, test_set, epochs=args.epochs, use_wandb=args.wandb)
     if pdist.is_main():

@@ -60,7 +60,8 @@ def fused_bn_act(bn_m: nn.Module, relu_m, x: torch.Tensor, res: torch.Tensor = N
     """``relu(bn(x) (+ res))`` as one fused op when covered (:mod:`iit_amd.ops.bn`), else None; ``relu_m`` None =
     no activation; ``splice`` = (index, src) of the producing conv's hook, applied as the kernels read x.
     ``bn_m`` / ``relu_m`` may be HookedModuleWrapper-wrapped: a live hook on either refuses."""
-    if not x.is_cuda or x.dtype != torch.bfloat16 or _hooked(bn_m) or (relu_m is not None and _hooked(relu_m)):
+    if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float32) or _hooked(bn_m) or \
+            (relu_m is not None and _hooked(relu_m)):
         return None
     from ..ops import bn as fbn
     bn = getattr(bn_m, "mod", bn_m)
@@ -85,7 +86,7 @@ def _conv_with_splice(conv_m: nn.Module, bn_m: nn.Module, x: torch.Tensor):
             hp._forward_pre_hooks or getattr(conv_m, "hook_pre", None) is not None:
         return conv_m(x), None
     h = conv_m.mod(x)  # the conv without its hook: the splice moves into the BatchNorm's reads
-    if h.dtype != torch.bfloat16:
+    if h.dtype not in (torch.bfloat16, torch.float32):
         return conv_m.hook_point(h), None
     return h, (spl[0].index, spl[0].src)
 

@@ -1,4 +1,4 @@
-"""Fused BatchNorm (+ residual add) (+ ReLU) on channels-last bf16 activations (``csrc/bn_nhwc.hip``).
+"""Fused BatchNorm (+ residual add) (+ ReLU) on channels-last bf16 or fp32 activations (``csrc/bn_nhwc.hip``).
 
 The PVR ResNet-18's ``BatchNorm2d -> ReLU`` and ``BatchNorm2d -> + identity -> ReLU`` chains
 (``/root/reference/iit/tasks/mnist_pvr/get_alignment.py:9-15``: torchvision's BasicBlock) as one autograd op: two
@@ -32,14 +32,17 @@ def enabled() -> bool:
 
 
 def covered(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res: Optional[torch.Tensor] = None) -> bool:
-    if not (x.is_cuda and x.dtype == BF16 and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)):
+    if not (x.is_cuda and x.dtype in (BF16, F32) and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    if x.dtype == F32 and os.environ.get("IIT_FUSED_BN_F32", "1") == "0":
         return False
     C = x.shape[1]
     if C % 8 or C < 8 or 256 % (C // 8) or not bn.affine or bn.momentum is None:
         return False
     if bn.weight.dtype != F32 or bn.bias.dtype != F32 or not bn.track_running_stats or bn.running_mean is None:
         return False
-    if res is not None and not (res.shape == x.shape and res.dtype == BF16
+    if res is not None and not (res.shape == x.shape and res.dtype == x.dtype
                                 and res.is_contiguous(memory_format=torch.channels_last)):
         return False
     return True
@@ -81,7 +84,7 @@ class BNActFn(Function):
         M, C, training, has_res, H, W = ctx.cfg
         src, spec = ctx.splice
         bn = ctx.bn
-        dy = dy.to(BF16).contiguous(memory_format=torch.channels_last)
+        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         dres = torch.empty_like(x, memory_format=torch.channels_last) if has_res else None
         coef = torch.empty(2 * C, dtype=F32, device=x.device)
@@ -102,7 +105,7 @@ def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res: Optional[torch.Tensor
         return BNActFn.apply(x, bn.weight, bn.bias, res, bn, relu)
     from .splice import patch_spec
     index, src = splice
-    src = src.to(device=x.device, dtype=BF16)
+    src = src.to(device=x.device, dtype=x.dtype)
     spec = patch_spec(index, tuple(x.shape), src)
     if spec is None or tuple(d[0] for d in spec.dims) != tuple(x.shape):
         return None
@@ -110,32 +113,33 @@ def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res: Optional[torch.Tensor
 
 
 class MaxPool3s2Fn(Function):
-    """``max_pool2d(x, 3, 2, 1)`` on a channels-last bf16 activation (``csrc/bn_nhwc.hip``): one byte of argmax per
+    """``max_pool2d(x, 3, 2, 1)`` on a channels-last bf16 / fp32 activation (``csrc/bn_nhwc.hip``): one byte of argmax per
     output element and a gather-form backward (torch's NHWC pool keeps int64 indices and scatters its gradient)."""
 
     @staticmethod
     def forward(ctx, x):
         N, C, H, W = x.shape
         OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
-        y = torch.empty(N, C, OH, OW, dtype=BF16, device=x.device, memory_format=torch.channels_last)
+        y = torch.empty(N, C, OH, OW, dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
         idx = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=x.device)
         K.maxpool3s2_fwd(x, y, idx, N, H, W, C)
         ctx.save_for_backward(idx)
         ctx.shape = (N, C, H, W)
+        ctx.dtype = x.dtype
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
         N, C, H, W = ctx.shape
-        dy = dy.to(BF16).contiguous(memory_format=torch.channels_last)
-        dx = torch.empty(N, C, H, W, dtype=BF16, device=dy.device, memory_format=torch.channels_last)
+        dy = dy.to(ctx.dtype).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty(N, C, H, W, dtype=ctx.dtype, device=dy.device, memory_format=torch.channels_last)
         K.maxpool3s2_bwd(dy, idx, dx, N, H, W, C)
         return dx
 
 
 def maxpool_covered(x: torch.Tensor, pool: torch.nn.Module) -> bool:
-    """``pool`` is ``MaxPool2d(3, 2, 1)`` (dilation 1, floor mode, no indices) and ``x`` a channels-last bf16 CUDA
+    """``pool`` is ``MaxPool2d(3, 2, 1)`` (dilation 1, floor mode, no indices) and ``x`` a channels-last bf16 / fp32 CUDA
     activation with C % 8 == 0 (``IIT_FUSED_POOL=0`` disables)."""
     if not (isinstance(pool, torch.nn.MaxPool2d) and enabled() and os.environ.get("IIT_FUSED_POOL", "1") != "0"):
         return False
@@ -144,5 +148,5 @@ def maxpool_covered(x: torch.Tensor, pool: torch.nn.Module) -> bool:
         return False
     if pool.ceil_mode or pool.return_indices:
         return False
-    return (x.is_cuda and x.dtype == BF16 and x.dim() == 4 and x.shape[1] % 8 == 0
+    return (x.is_cuda and x.dtype in (BF16, F32) and x.dim() == 4 and x.shape[1] % 8 == 0
             and x.is_contiguous(memory_format=torch.channels_last))

@@ -91,13 +91,13 @@ _SIGS = {
     "iit_splice": [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_splice_spec_size": [],
     "iit_bn_fwd": [c_void_p] * 8 + [c_long, c_int, c_float, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p,
-                                    c_void_p, c_int, c_int, c_void_p],
+                                    c_void_p, c_int, c_int, c_int, c_void_p],
     "iit_bn_bwd": [c_void_p] * 7 + [c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                    c_int, c_int, c_void_p],
+                                    c_int, c_int, c_int, c_void_p],
     "iit_gemm_glds_set_prof": [c_void_p],
-    "iit_maxpool3s2_fwd": [c_void_p] * 3 + [c_int] * 4 + [c_void_p],
+    "iit_maxpool3s2_fwd": [c_void_p] * 3 + [c_int] * 5 + [c_void_p],
     "iit_bn_ws_floats": [c_int],
-    "iit_maxpool3s2_bwd": [c_void_p] * 3 + [c_int] * 4 + [c_void_p],
+    "iit_maxpool3s2_bwd": [c_void_p] * 3 + [c_int] * 5 + [c_void_p],
     "iit_gemm_dual_ok": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 7 + [c_void_p] * 4 + [c_long] * 4 + [c_int] * 5,
     "iit_gemm_dual": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 6 + [c_void_p] * 2 + [c_void_p] * 4 + [c_long] * 4
                      + [c_int] * 5 + [c_void_p] * 4,
@@ -635,24 +635,26 @@ def maxpool3s2_fwd(x, y, idx, N: int, H: int, W: int, C: int):
     if CHECK_BOUNDS:
         OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         assert y.numel() == N * OH * OW * C and idx.numel() == y.numel() and x.numel() == N * H * W * C
-    _check(lib().iit_maxpool3s2_fwd(_p(x), _p(y), _p(idx), N, H, W, C, _stream()), "maxpool3s2_fwd")
+    _check(lib().iit_maxpool3s2_fwd(_p(x), _p(y), _p(idx), N, H, W, C, int(x.dtype == torch.float32), _stream()),
+           "maxpool3s2_fwd")
 
 
 def maxpool3s2_bwd(dy, idx, dx, N: int, H: int, W: int, C: int):
-    _check(lib().iit_maxpool3s2_bwd(_p(dy), _p(idx), _p(dx), N, H, W, C, _stream()), "maxpool3s2_bwd")
+    _check(lib().iit_maxpool3s2_bwd(_p(dy), _p(idx), _p(dx), N, H, W, C, int(dy.dtype == torch.float32), _stream()),
+           "maxpool3s2_bwd")
 
 
 def bn_fwd(x, res, y, ws, rmean, rvar, w, b, M: int, C: int, eps: float, relu: bool, training: bool, save,
            momentum: float, nbt, src=None, spec=None, H: int = 0, W: int = 0):
-    """Fused BatchNorm (+ residual) (+ ReLU) forward over NHWC bf16 rows (csrc/bn_nhwc.hip); ``ws`` = the
-    module's self-re-arming accumulator (2C floats + a ticket)."""
+    """Fused BatchNorm (+ residual) (+ ReLU) forward over NHWC bf16 or fp32 rows (csrc/bn_nhwc.hip; every activation
+    of one call has ``x``'s dtype); ``ws`` = the module's self-re-arming accumulator (:func:`bn_ws_floats`)."""
     if CHECK_BOUNDS:
         for t in (x, y) + ((res,) if res is not None else ()):
-            assert _avail(t) >= M * C, "bn_fwd: activation smaller than M x C"
-        assert ws.numel() >= 2 * C + 1 and save.numel() >= 2 * C
+            assert _avail(t) >= M * C and t.dtype == x.dtype, "bn_fwd: activation smaller than M x C / dtype"
+        assert ws.numel() >= bn_ws_floats(C) and save.numel() >= 2 * C
     _check(lib().iit_bn_fwd(_p(x), _p(res), _p(y), _p(ws), _p(rmean), _p(rvar), _p(w), _p(b), M, C, eps, int(relu),
                             int(training), _p(save), momentum, _p(nbt), _p(src), None if spec is None else spec.ptr,
-                            H, W, _stream()), "bn_fwd")
+                            H, W, int(x.dtype == torch.float32), _stream()), "bn_fwd")
 
 
 def bn_bwd(dy, y, x, save, w, ws, coef, M: int, C: int, training: bool, dx, dres, dw, db, src=None, spec=None,
@@ -662,8 +664,8 @@ def bn_bwd(dy, y, x, save, w, ws, coef, M: int, C: int, training: bool, dx, dres
         for t in (dy, x, dx):
             assert _avail(t) >= M * C, "bn_bwd: activation smaller than M x C"
     _check(lib().iit_bn_bwd(_p(dy), _p(y), _p(x), _p(save), _p(w), _p(ws), _p(coef), M, C, int(training), _p(dx),
-                            _p(dres), _p(dw), _p(db), _p(src), None if spec is None else spec.ptr, H, W, _stream()),
-           "bn_bwd")
+                            _p(dres), _p(dw), _p(db), _p(src), None if spec is None else spec.ptr, H, W,
+                            int(x.dtype == torch.float32), _stream()), "bn_bwd")
 
 
 def zero_ranges(base, starts, lens):

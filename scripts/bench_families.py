@@ -41,6 +41,8 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=None, help="pairs per GPU per step")
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
                     help="pvr-resnet18 only: fp32 (the reference precision) or channels-last bf16 autocast")
+    ap.add_argument("--channels-last", type=int, default=None,
+                    help="pvr-resnet18: NHWC model and activations (default on)")
     ap.add_argument("--graphs", type=int, default=None,
                     help="HIP-graph phases (default: on for BERT; off for Llama, whose strict phase has one graph per "
                          "non-circuit node -- ~1000 at 32 layers x 32 heads -- and whose GEMMs are not launch-bound)")
@@ -74,7 +76,10 @@ def setup(args, dev):
         n = 20000
         tr_set, te_set = get_dataset("mnist_pvr", {"train_size": n, "test_size": 2048, "device": dev})
         ll, hl, corr = get_alignment("mnist_pvr", {"input_shape": te_set.base_data.get_input_shape(), "device": dev})
-        if args.dtype == "bf16":  # NHWC activations for MIOpen's bf16 implicit-GEMM convolutions
+        # NHWC for both dtypes: the fused NHWC BatchNorm / pool kernels take bf16 and fp32 (fp32 PVR step 18.9 ->
+        # 14.6 ms, profiles/bn_fp32_r5.txt)
+        cl = args.channels_last if args.channels_last is not None else 1
+        if cl:  # NHWC activations for MIOpen's implicit-GEMM convolutions (and the fused NHWC BatchNorm)
             ll.to(memory_format=torch.channels_last)
         args.batch = args.batch or 256
         pair = IITBehaviorModelPair(hl, ll, corr, training_args={"batch_size": args.batch, "lr": 1e-3,
