@@ -169,7 +169,7 @@ class BertBlock(nn.Module):
             resid_post = ops.mlp_gelu_residual(x, mlp.W_in, mlp.b_in, mlp.W_out, mlp.b_out, x, erf=erf)
             return self.ln2.run(resid_post, run), False
         resid_mid = ops.pair_o_proj_residual(z, attn.W_O, attn.b_O, p)
-        x = ops.pair_layer_norm(resid_mid, self.ln1.w, self.ln1.b, self.ln1.eps)
+        x = ops.pair_layer_norm(resid_mid, self.ln1.w, self.ln1.b, self.ln1.eps, twin=True)
         pname = mlp.hook_post.name
         ps = sites.get(pname)
         if ps is None:
@@ -192,7 +192,7 @@ class BertBlock(nn.Module):
             for m in masks:
                 mask |= m
             idxs = []
-        out = ops.pair_layer_norm(resid_post, self.ln2.w, self.ln2.b, self.ln2.eps, pos_mask=mask)
+        out = ops.pair_layer_norm(resid_post, self.ln2.w, self.ln2.b, self.ln2.eps, pos_mask=mask, twin=True)
         for ix in idxs:
             out = ops.pair_splice(out, ix)
         if nname in sites:

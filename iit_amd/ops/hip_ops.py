@@ -1288,10 +1288,18 @@ class Paired:
     """An activation of a paired forward: ``full`` [2B, ...] (rows [0, B) base, [B, 2B) source) and ``base``, the
     autograd-visible tensor holding the values of ``full[:B]`` (a view of it, or a passthrough of such a view)."""
 
-    __slots__ = ("base", "full")
+    __slots__ = ("base", "full", "f32")
 
-    def __init__(self, base: torch.Tensor, full: torch.Tensor):
-        self.base, self.full = base, full
+    def __init__(self, base: torch.Tensor, full: torch.Tensor, f32=None):
+        # f32: (base32, full32) fp32 twins of a bf16 LN output (LayerNormPairTwinFn) for residual consumers
+        self.base, self.full, self.f32 = base, full, f32
+
+    def resid_operands(self):
+        """(autograd base, fp32 full) for a residual epilogue: the fp32 twins when present (no cast pass; the base
+        twin's gradient reaches the LN backward in fp32), else the bf16 base and a cast of ``full``."""
+        if self.f32 is not None:
+            return self.f32
+        return self.base, self.full.float().contiguous()
 
     @property
     def nb(self) -> int:
@@ -1344,6 +1352,39 @@ class LayerNormForkPairFn(LayerNormForkFn):
     @staticmethod
     def backward(ctx, dy, dpass):
         return LayerNormForkFn.backward(ctx, dy, dpass) + (None, None)
+
+
+class LayerNormPairTwinFn(Function):
+    """:class:`LayerNormPairFn` (no position splice) that also writes the fp32 twin of both row sets in the same
+    pass (``iit_ln_fwd_twin``) -- :class:`LayerNormTwinFn` for the paired forward: outputs (base bf16, base fp32),
+    ``box`` gets (full bf16, full fp32); the backward adds the fp32 output's gradient inside the LN backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps, x_full, box):
+        ctx.set_materialize_grads(False)
+        d = x.shape[-1]
+        B = x.shape[0]
+        x2 = _flat2(x_full)
+        T2 = x2.shape[0]
+        T = T2 * B // x_full.shape[0]
+        y = torch.empty(T2, d, dtype=BF16, device=x.device)
+        y32 = torch.empty(T2, d, dtype=F32, device=x.device)
+        mean = torch.empty(T2, dtype=F32, device=x.device)
+        rstd = torch.empty(T2, dtype=F32, device=x.device)
+        if not K.ln_fwd_twin(x2, w, b, y, y32, mean, rstd, T2, d, eps):
+            K.ln_fwd(x2, w, b, y, mean, rstd, T2, d, eps)
+            y32.copy_(y)
+        ctx.save_for_backward(x2[:T], mean[:T], rstd[:T])
+        ctx.params = (w, b)
+        ctx.in_dtype = x.dtype
+        yf = y.view(*x_full.shape[:-1], d)
+        yf32 = y32.view(*x_full.shape[:-1], d)
+        box.append((yf, yf32))
+        return yf[:B], yf32[:B]
+
+    @staticmethod
+    def backward(ctx, dy, dy32):
+        return LayerNormTwinFn.backward(ctx, dy, dy32) + (None, None)
 
 
 class LayerNormPairFn(LayerNormFn):
@@ -1798,11 +1839,16 @@ class HipOps(TorchOps):
         y, x_pass = LayerNormForkPairFn.apply(p.base, w, b, eps, p.full.float().contiguous(), box)
         return Paired(y, box[0]), Paired(x_pass, p.full)
 
-    def pair_layer_norm(self, p: Paired, w, b, eps, pos_mask: int = 0) -> Paired:
+    def pair_layer_norm(self, p: Paired, w, b, eps, pos_mask: int = 0, twin: bool = False) -> Paired:
         """LN of both row sets (no residual passthrough: post-LN blocks).  ``pos_mask``: the base rows at these
         positions take the source rows' output -- an interchange splice of whole positions of the LN output done
         by the LN kernel itself (and masked out of its backward), no separate splice pass."""
         box = []
+        if twin and not pos_mask and w is not None and os.environ.get("IIT_LN_TWIN", "1") != "0":
+            y, y32 = LayerNormPairTwinFn.apply(p.base, w, b, eps, p.full.float().contiguous(), box)
+            yf, yf32 = box[0]
+            y._iit_f32 = (y.data_ptr(), y._version, y32)  # (the unpaired blocks after the pairing ends)
+            return Paired(y, yf, (y32, yf32))
         y = LayerNormPairFn.apply(p.base, w, b, eps, p.full.float().contiguous(), box, int(pos_mask))
         return Paired(y, box[0])
 
@@ -1864,8 +1910,9 @@ class HipOps(TorchOps):
     def pair_o_proj_residual(self, z: Paired, W_O, b_O, resid: Paired) -> Paired:
         B2, S, H, dh = z.full.shape
         B = z.base.shape[0]
+        rb, rf = resid.resid_operands()
         out, full = _one(LinearPairFn, z.base.reshape(B, S, H * dh), W_O, b_O, self._L(W_O)["o"], W_O.shape[-1],
-                         resid.base, "resid", z.full.reshape(B2, S, H * dh), resid.full.float().contiguous())
+                         rb, "resid", z.full.reshape(B2, S, H * dh), rf)
         return Paired(out, full)
 
     def pair_mlp_in(self, x: Paired, W_in, b_in, erf: bool = False, index=None):
@@ -1883,14 +1930,16 @@ class HipOps(TorchOps):
         return Paired(pre, pf), Paired(post, qf)
 
     def pair_mlp_out_residual(self, post: Paired, W_out, b_out, resid: Paired) -> Paired:
-        out, full = _one(LinearPairFn, post.base, W_out, b_out, self._L(W_out)["out"], W_out.shape[1], resid.base,
-                         "resid", post.full, resid.full.float().contiguous())
+        rb, rf = resid.resid_operands()
+        out, full = _one(LinearPairFn, post.base, W_out, b_out, self._L(W_out)["out"], W_out.shape[1], rb,
+                         "resid", post.full, rf)
         return Paired(out, full)
 
     def pair_mlp_gelu_residual(self, x: Paired, W_in, b_in, W_out, b_out, resid: Paired, erf: bool = False):
         pre, post = self.pair_mlp_in(x, W_in, b_in, erf)
+        rb, rf = resid.resid_operands()
         out, full = _one(MLPOutGeluPairFn, pre.base, post.base.detach(), W_out, b_out, self._L(W_out)["out"],
-                         W_out.shape[1], resid.base, b_in, erf, post.full, resid.full.float().contiguous())
+                         W_out.shape[1], rb, b_in, erf, post.full, rf)
         return Paired(out, full)
 
     def pair_splice(self, p: Paired, index) -> Optional[Paired]:
