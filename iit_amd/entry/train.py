@@ -27,9 +27,12 @@ def parse(argv=None):
     ap.add_argument("--hook-point", default="mod.layer3.mod.1.mod.conv2.hook_point")
     ap.add_argument("--wandb", action="store_true")
     ap.add_argument("--save", default=None, help="write the LL state_dict here (reference: weights/ll_model/{task}.pt)")
-    ap.add_argument("--conv-benchmark", type=int, default=1,
+    ap.add_argument("--conv-benchmark", type=int, default=0,
                     help="1: MIOpen find mode (torch.backends.cudnn.benchmark) -- the fastest measured convolution "
-                         "solution per shape; the PVR bf16 step 12.5 -> 9.0 ms (profiles/pvr_step_r5.txt)")
+                         "solution per shape (the bf16 PVR step 12.5 -> 9.0 ms, profiles/pvr_step_r5.txt), at a "
+                         "first-call search cost of ~50 s per process; the fp32 step gains nothing from it, and the "
+                         "reference config reaches its early stop in 21.4 s without vs 72.0 s with it "
+                         "(profiles/train_py_pvr_r5.txt), so it is off by default")
     ap.add_argument("--channels-last", type=int, default=1,
                     help="1: NHWC ResNet on the GPU -- MIOpen's NHWC convolutions and the fused NHWC BatchNorm / pool "
                          "kernels (fp32 PVR step 18.9 -> 14.6 ms, profiles/bn_fp32_r5.txt)")
