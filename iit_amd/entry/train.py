@@ -30,9 +30,9 @@ def parse(argv=None):
     ap.add_argument("--conv-benchmark", type=int, default=0,
                     help="1: MIOpen find mode (torch.backends.cudnn.benchmark) -- the fastest measured convolution "
                          "solution per shape (the bf16 PVR step 12.5 -> 9.0 ms, profiles/pvr_step_r5.txt), at a "
-                         "first-call search cost of ~50 s per process; the fp32 step gains nothing from it, and the "
-                         "reference config reaches its early stop in 21.4 s without vs 72.0 s with it "
-                         "(profiles/train_py_pvr_r5.txt), so it is off by default")
+                         "first-call search cost of ~50 s per process; the fp32 NHWC step gains 16.6 -> 14.5 ms, and "
+                         "the reference config reaches its early stop in 21.4 s without vs 72.0 s with it "
+                         "(profiles/train_py_pvr_r5.txt), so it is off by default (long runs: pass 1)")
     ap.add_argument("--channels-last", type=int, default=1,
                     help="1: NHWC ResNet on the GPU -- MIOpen's NHWC convolutions and the fused NHWC BatchNorm / pool "
                          "kernels (fp32 PVR step 18.9 -> 14.6 ms, profiles/bn_fp32_r5.txt)")
