@@ -53,18 +53,35 @@ __global__ __launch_bounds__(256) void embed_bwd_pos_kernel(const long* __restri
                                                             float* __restrict__ dWE, int B, int S, int d) {
   const int s = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x, b0 = blockIdx.z * EB;
   if (c >= d) return;
+  const int b1 = min(B, b0 + EB);
   long cur = -1;
   float acc = 0.f;
-  for (int b = b0; b < min(B, b0 + EB); ++b) {
-    const long t = (long)b * S + s;
-    const long v = tok[t];
-    const float x = g[t * d + c];
-    if (v != cur) {
-      if (cur >= 0) atomicAdd(dWE + cur * (long)d + c, acc);
-      cur = v;
-      acc = x;
-    } else {
-      acc += x;
+  // 8 rows' token ids and gradients loaded before the first is used: the loop was one dependent load round trip
+  // per row (latency-bound)
+  for (int bb = b0; bb < b1; bb += 8) {
+    long vv[8];
+    float xx[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int b = bb + k;
+      vv[k] = -1;
+      xx[k] = 0.f;
+      if (b < b1) {
+        const long t = (long)b * S + s;
+        vv[k] = tok[t];
+        xx[k] = g[t * d + c];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (vv[k] < 0) break;
+      if (vv[k] != cur) {
+        if (cur >= 0) atomicAdd(dWE + cur * (long)d + c, acc);
+        cur = vv[k];
+        acc = xx[k];
+      } else {
+        acc += xx[k];
+      }
     }
   }
   if (cur >= 0) atomicAdd(dWE + cur * (long)d + c, acc);
