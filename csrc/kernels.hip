@@ -95,6 +95,7 @@ __global__ __launch_bounds__(256) void pos_bwd_kernel(const float* __restrict__ 
   const int c = blockIdx.y * 256 + lane * 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c < d)
+#pragma unroll 8  // independent row loads in flight (the loop was one round trip per row)
     for (int b = w; b < B; b += 4) {
       const float4 v = *(const float4*)(g + ((long)b * S + s) * d + c);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
