@@ -93,7 +93,9 @@ def _gloo_rank(rank, world, port, payload, q):
     t = payload[rank].to(torch.bfloat16)
     dist.all_reduce(t)
     if rank == 0:
-        q.put(t.double() / world)
+        # by value (a numpy array): a torch tensor crosses the queue as a shared-memory fd that the parent can only
+        # rebuild while this process is still alive -- it may already have exited
+        q.put((t.double() / world).numpy())
     dist.destroy_process_group()
 
 
@@ -113,7 +115,7 @@ def test_gloo_world8_bf16_all_reduce_within_ring_bound(grads):
     procs = [ctx.Process(target=_gloo_rank, args=(r, WORLD, port, payload, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    got = torch.from_numpy(q.get(timeout=120))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
