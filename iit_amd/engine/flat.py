@@ -108,6 +108,13 @@ class FlatParams:
                     self._view_fns.append(lambda buf, o=off, n=n, shape=p.shape: buf[o:o + n].view(shape))
                 off += _align(n)
         self.numel = off
+        # per-parameter arena layout (slot offset, shape, element order): optimizer state saved as arena-shaped
+        # tensors is only meaningful for the same layout (see ``layout_tag``)
+        self._layout = [(nm, o, tuple(p.shape),
+                         "nhwc" if (p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last)
+                                    and not p.is_contiguous()) else "dense")
+                        for nm, p, (o, _n) in zip(self.names, self.params, self.slots)] \
+            if len(self.slots) == len(self.params) else [(nm, tuple(p.shape)) for nm, p in zip(self.names, self.params)]
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.data = torch.zeros(off, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
@@ -146,6 +153,14 @@ class FlatParams:
             self.ensure_shadow()
 
     # ---------------------------------------------------------------- layout queries
+    def layout_tag(self) -> str:
+        """Digest of the arena layout: every parameter's name, offset, shape and element order (NHWC conv weights
+        keep channels-last order).  Arena-shaped optimizer state (Adam moments, ZeRO shards) carries it, so state
+        from another layout -- e.g. an NCHW-era checkpoint of a model whose conv weights are now NHWC, whose
+        moments would load silently permuted -- is refused."""
+        import hashlib
+        return hashlib.sha1(repr((self.numel, self._layout)).encode()).hexdigest()[:16]
+
     def offset_of(self, p: torch.Tensor) -> int:
         """Element offset of ``p``'s first element inside the arena."""
         return (p.data_ptr() - self.data.data_ptr()) // self.data.element_size()

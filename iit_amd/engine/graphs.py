@@ -59,6 +59,12 @@ def _join_gathers(optimizer) -> None:
         wait()
 
 
+def _sync_gemm_decisions() -> None:
+    """Rank-consistent GEMM choices before a data-parallel capture (``gemm_dispatch.sync_decisions``)."""
+    from ..ops.gemm_dispatch import sync_decisions
+    sync_decisions()
+
+
 def _sync_hyper(optimizer) -> None:
     """A captured optimizer step replays the kernel arguments of its capture; the fused Adam reads its learning
     rate (and betas / eps / weight decay) from device scalars, refreshed here when the host values changed (an LR
@@ -373,6 +379,12 @@ class GraphedTrainStep:
                 if spec is not None:
                     parts = [(torch.cuda.CUDAGraph() if cap else None, fn) for cap, fn in spec]
             gs = []
+            # a ZeRO-1 warm-up step deferred its bucket gathers: finish them eagerly BEFORE the capture (a gate
+            # inside the capture records nothing that runs now)
+            _join_gathers(optimizer)
+            # every rank captures this phase at the same call (phase keys follow the identically seeded node RNG):
+            # agree on the GEMM kernels first, so the graphs hold rank 0's choices on every rank
+            _sync_gemm_decisions()
             try:
                 with _CaptureGC(), torch.cuda.graph(ga, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                     static_out = fwd_bwd()
@@ -460,6 +472,7 @@ class GraphedTrainStep:
             if self.pool is None or os.environ.get("IIT_GRAPH_POOL") == "private":
                 self.pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
+            _join_gathers(optimizer)  # (see _run_split_phase)
             try:
                 with _CaptureGC(), torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode=_CAPTURE_MODE):
                     out = compute_loss()
@@ -627,6 +640,14 @@ class GraphedEvalStep:
     def _eager(self, base, abl):
         return self.pair.run_eval_step(base, abl, self.loss_fn)
 
+    def _join(self) -> None:
+        """Finish a ZeRO-1 optimizer's deferred gathers (``module._param_join``, installed by ``attach_gates``)."""
+        pair = self.pair
+        module = pair._ll_module() if hasattr(pair, "_ll_module") else getattr(pair, "ll_model", None)
+        join = getattr(module, "_param_join", None) if module is not None else None
+        if join is not None:
+            join()
+
     def __call__(self, base, abl):
         pair = self.pair
         if not self.ok:
@@ -660,6 +681,7 @@ class GraphedEvalStep:
         sb, sa = self._static
         _copy_all(sb + sa, tuple(base) + tuple(abl))
         key = (node.name, sig)
+        self._join()  # a replayed (or captured) forward passes no ZeRO-1 gates
         ent = self.graphs.get(key)
         if ent is None:
             n = self.seen.get(key, 0)

@@ -46,7 +46,8 @@ def evaluate_model_on_probes(ll_model, task: str, probe_training_args: dict, tra
     t0 = time.perf_counter()
     if (probe_training_args.get("engine", "native") == "native" and getattr(ll_model, "supports_run_plan", False)
             and hasattr(train_set, "gather") and hasattr(test_set, "gather")
-            and os.environ.get("IIT_PROBE_BANK", "1") != "0"):
+            and os.environ.get("IIT_PROBE_BANK", "1") != "0"
+            and ActivationBank.fits(ll_model, (train_set, test_set), hps)):
         # every hook point's activations of every train / test sample, captured once (ActivationBank): the
         # per-hook-point loop below then trains and evaluates its probes from gathers instead of forwards
         banks = (ActivationBank(ll_model, train_set, hps, probe_training_args["batch_size"]),

@@ -421,6 +421,15 @@ def _candidates_plain(A, B, C, C2, M, N, Kd, lda, ldb, ldc, mode, epi, bias0, bi
 
 
 _SPLIT_STORE = os.environ.get("IIT_GEMM_SPLIT_STORE", "")  # test-only (see _candidates_plain)
+# ``IIT_GEMM_FREEZE=1``: no in-process timing at all -- every problem key must be in the shipped decision table (or
+# already decided / synchronised), else the GEMM raises: run-to-run and rank-to-rank identical kernel choice
+_FREEZE = os.environ.get("IIT_GEMM_FREEZE", "0") == "1"
+
+
+def _frozen_miss(key) -> None:
+    if _FREEZE:
+        raise RuntimeError(f"IIT_GEMM_FREEZE=1: GEMM problem {key!r} is not in the decision table "
+                           f"({os.environ.get('IIT_GEMM_TABLE', _TABLE_PATH)}); export one with IIT_GEMM_TABLE_EXPORT")
 _SPLIT_STORE_KEY = tuple(int(x) for x in os.environ.get("IIT_GEMM_SPLIT_STORE_KEY", "").split(",") if x) or None
 
 
@@ -506,6 +515,8 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
 
             rkey = (M, N, K, mode, epi, bias0 is not None, fresh, deterministic())
             split = RAGGED.get(rkey)
+            if split is None and _FREEZE:  # no timing: the tile-aligned bulk + tail (both keys must be in the table)
+                split = RAGGED[rkey] = (True, float("nan"), [])
             if split is None and not torch.cuda.is_current_stream_capturing():
                 # the split is one more candidate: bulk + tail against the whole problem, each at its best
                 whole = gemm(A, B, C, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc, mode=mode, epi=epi, C2=C2, C3=C3,
@@ -584,6 +595,7 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
                 return None
             _run("hip")
             return None
+        _frozen_miss(key)
         # time on scratch outputs so accumulate epilogues (and column sums) do not corrupt C
         sc = _scratch(C, M, max(ldc, N))
         sc2 = _scratch(C2, M, max(ldc2, N))
@@ -704,6 +716,7 @@ def gemm_pair(x: dict, w: dict) -> Optional[str]:
     if choice is None:
         if torch.cuda.is_current_stream_capturing():
             return serial()
+        _frozen_miss(key)
         # time on scratch outputs (accumulate epilogues and column sums must not touch the real ones)
         xc = _scratch(x["C"], x["M"], max(x["ldc"], x["N"]))
         wc = _scratch(w["C"], w["M"], max(w["ldc"], w["N"]))
@@ -770,6 +783,35 @@ def _table() -> Dict[str, str]:
             except (OSError, ValueError) as e:  # pragma: no cover - a corrupt table only costs autotuning
                 print(f"[iit] GEMM decision table not loaded ({e})")
     return _TABLE
+
+
+def sync_decisions(group=None) -> int:
+    """Make the GEMM decisions identical on every data-parallel rank.
+
+    Each rank measures the shapes it meets on its own (a shape missing from the shipped table), so two ranks can
+    time different winners.  At a point every rank reaches together -- before any HIP-graph capture of a
+    data-parallel phase (:mod:`iit_amd.engine.graphs`), and at the bench's end of warm-up -- all ranks exchange their
+    tables (one ``all_gather_object``) and adopt, per problem key, the choice of the LOWEST rank that measured it: a
+    captured graph then holds the same kernel on every rank, and rank 0's choice is the job's.  Collective: every
+    rank of ``group`` must call it.  Returns the number of local entries that changed."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return 0
+    ws = dist.get_world_size(group)
+    mine = {"gemm": dict(DECISIONS), "dual": dict(DUAL_DECISIONS), "ragged": dict(RAGGED)}
+    every = [None] * ws
+    dist.all_gather_object(every, mine, group=group)
+    changed = 0
+    for name, table in (("gemm", DECISIONS), ("dual", DUAL_DECISIONS), ("ragged", RAGGED)):
+        merged = {}
+        for r in reversed(range(ws)):  # lower ranks overwrite: the lowest rank that measured a key decides it
+            merged.update(every[r][name])
+        for k, v in merged.items():
+            old = table.get(k)
+            if old is None or old[0] != v[0]:
+                changed += 1
+            table[k] = v
+    return changed
 
 
 def export_table(path: str) -> int:

@@ -141,10 +141,17 @@ class FusedAdam(torch.optim.Optimizer):
     def state_dict(self):
         self.step_count = int(self._step_dev.item())  # device counter is authoritative (guarded skips)
         return {"step": self.step_count, "skipped": self.skipped_steps, "exp_avg": self.exp_avg,
-                "exp_avg_sq": self.exp_avg_sq,
+                "exp_avg_sq": self.exp_avg_sq, "arena_layout": self.flat.layout_tag(),
                 "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]}
 
     def load_state_dict(self, sd):
+        tag = sd.get("arena_layout")
+        if tag is None:
+            print("[iit] optimizer state without an arena layout tag (saved before round 6): loaded as is -- its "
+                  "moments are only valid for the same parameter layout")
+        elif tag != self.flat.layout_tag():
+            raise ValueError(f"optimizer state was saved for another arena layout ({tag} != "
+                             f"{self.flat.layout_tag()}): its Adam moments would land on the wrong parameters")
         self.step_count = int(sd["step"])
         self._step_dev.fill_(self.step_count)
         self._skipped_dev.fill_(int(sd.get("skipped", 0)))

@@ -44,19 +44,38 @@ from ..engine.flat import FlatParams
 from . import dist as pdist
 
 
+def computes_bf16(module: Optional[torch.nn.Module], flat: FlatParams) -> bool:
+    """Whether the model's forward / backward run in bf16: a bf16 weight mirror in the arena (the fused HIP backend,
+    the PVR conv mirror), a bf16 ``cfg.dtype``, or bf16 autocast active."""
+    if getattr(flat, "shadow", None) is not None:
+        return True
+    cfg = getattr(module, "cfg", None) if module is not None else None
+    dt = cfg.get("dtype") if isinstance(cfg, dict) else getattr(cfg, "dtype", None)
+    if dt == torch.bfloat16:
+        return True
+    return bool(torch.cuda.is_available() and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+
+
 class GradReducer:
     def __init__(self, flat: FlatParams, bucket_mb: float = 64.0, overlap: bool = True,
                  wire_dtype: Optional[torch.dtype] = None, module: Optional[torch.nn.Module] = None):
         self.flat = flat
         self.world = pdist.world_size()
         self.enabled = self.world > 1 or pdist.force_reducer()
+        self._module = module
+        self._wire_auto = False
         if wire_dtype is None:
             env = os.environ.get("IIT_DP_GRAD_DTYPE", "")
             if env in ("bf16", "fp32"):
                 wire_dtype = torch.bfloat16 if env == "bf16" else torch.float32
-            else:  # default: bf16 on RCCL (tests/test_wire_dtype.py), fp32 on gloo
+            else:
+                # default: bf16 on RCCL only for a model that computes in bf16 (its gradients already carry bf16
+                # rounding: tests/test_wire_dtype.py), fp32 for fp32 models and on gloo (ADVICE r5) -- decided at
+                # the first launch, when a lazily created bf16 mirror exists
                 nccl = self.enabled and dist.is_initialized() and dist.get_backend() == "nccl"
-                wire_dtype = torch.bfloat16 if nccl else torch.float32
+                self._wire_auto = nccl
+                wire_dtype = torch.float32
         self.wire_dtype = wire_dtype if wire_dtype != torch.float32 else None
         self.overlap = overlap and self.enabled
         self._bucket_bytes = int(bucket_mb * (1 << 20))
@@ -120,10 +139,21 @@ class GradReducer:
         self.shard = optimizer
         optimizer.set_buckets(self.buckets)
 
+    def _resolve_wire(self) -> None:
+        if not self._wire_auto:
+            return
+        self._wire_auto = False
+        if computes_bf16(self._module, self.flat):
+            self.wire_dtype = torch.bfloat16
+        if pdist.is_main():
+            print(f"[iit dp] gradient wire dtype: {'bf16' if self.wire_dtype is not None else 'fp32'} "
+                  f"(IIT_DP_GRAD_DTYPE / training_args['grad_wire_dtype'] override)", flush=True)
+
     def _launch(self, b: int):
         if self._launched[b]:
             return
         self._launched[b] = True
+        self._resolve_wire()
         s, e = self.buckets[b]
         if self.shard is not None:
             self._launch_reduce_scatter(b, s, e)

@@ -373,8 +373,14 @@ class ShardedFusedAdam(FusedAdam):
             flat.after_step(mirror_written=flat.shadow is not None)
 
     def _finish(self, bi: int) -> None:
-        item = self._pending.pop(bi, None)
+        item = self._pending.get(bi)
         if item is None:
+            return
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            # under stream capture the wait, the tail copy and the mirror refresh would only be RECORDED into the
+            # graph, not run, while the bucket left the pending set: a later join would find nothing to wait for and
+            # the first replay could race the in-flight gather.  Captures are preceded by a join
+            # (engine/graphs.py), so a pending bucket here is a caller bug -- it stays pending for the eager join.
             return
         work, mirror = item
         flat = self.flat
@@ -382,7 +388,11 @@ class ShardedFusedAdam(FusedAdam):
         if work is not None:
             if callable(work):  # (IIT_ZERO_POISON: issued at finish)
                 work = work()
+                self._pending[bi] = (work, mirror)
             work.wait()  # RCCL: the current stream waits for the collective (no host block)
+        # popped only once the wait succeeded: a wait that raises leaves the bucket pending (never a stale mirror)
+        self._pending.pop(bi, None)
+        if work is not None:
             if self.plan.piece[bi] * self.plan.world != e - s:
                 flat.data[s:e].copy_(self._gather_bufs[("out", bi)][:e - s])
         if mirror and flat.shadow is not None:
@@ -431,7 +441,7 @@ class ShardedFusedAdam(FusedAdam):
         self._gated_module = module
 
         def gate(key):
-            if self._pending:
+            if self._pending and not (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
                 for bi in self._gate_groups.get(key, ()):
                     self._finish(bi)
 

@@ -14,6 +14,8 @@ from __future__ import annotations
 
 from typing import Dict, Iterable, List, Optional
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -102,6 +104,40 @@ class ActivationBank:
         self.n = n
         self.acts = {nm: torch.cat(v) for nm, v in parts.items()}
         self.iv = torch.cat(ivs)
+
+    @staticmethod
+    def estimate_bytes(ll_model, dataset, names, sample: int = 2) -> int:
+        """Bytes the bank of ``names`` over ``dataset`` would hold: one capture of ``sample`` rows, scaled."""
+        n = len(dataset)
+        k = max(1, min(sample, n))
+        with torch.no_grad():
+            x, _, iv = dataset.gather(torch.arange(0, k, device=DEVICE))
+            cache = capture_hooks(ll_model, x, sorted(set(names)))
+            per = sum(cache[nm].element_size() * cache[nm].numel() for nm in set(names)) + iv.element_size() * iv.numel()
+        return per * n // k
+
+    @staticmethod
+    def budget_bytes() -> int:
+        """Device memory a bank may take: ``IIT_PROBE_BANK_GB``, else half of the currently free device memory
+        (host: 8 GB)."""
+        env = os.environ.get("IIT_PROBE_BANK_GB")
+        if env:
+            return int(float(env) * (1 << 30))
+        if torch.cuda.is_available():
+            free, _total = torch.cuda.mem_get_info()
+            return free // 2
+        return 8 << 30
+
+    @classmethod
+    def fits(cls, ll_model, datasets, names) -> bool:
+        """Whether banks over every dataset of ``datasets`` fit the budget together (a full 60k MNIST-PVR
+        sweep of every hook point needs tens of GB -- above the budget the per-batch path runs instead)."""
+        need = sum(cls.estimate_bytes(ll_model, d, names) for d in datasets)
+        ok = need <= cls.budget_bytes()
+        if not ok:
+            print(f"[iit probes] activation bank would take {need / 2**30:.1f} GB (budget "
+                  f"{cls.budget_bytes() / 2**30:.1f} GB): per-batch capture instead")
+        return ok
 
     def batch(self, idx: torch.Tensor, names):
         return {nm: self.acts[nm].index_select(0, idx) for nm in names}, self.iv.index_select(0, idx)

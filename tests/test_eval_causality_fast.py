@@ -73,3 +73,25 @@ def test_cached_probe_evaluation_equals_per_probe_loop():
         assert max(abs(a[k] - b[k]) for k in a) <= 1e-6, (h, a, b)
         la, lb = res["native"][h]["test loss"], res["reference"][h]["test loss"]
         assert max(abs(la[k] - lb[k]) for k in la) <= 1e-4 * max(1.0, max(abs(v) for v in lb.values())), (h, la, lb)
+
+
+def test_probe_bank_over_budget_falls_back(monkeypatch, capsys):
+    """an activation bank above the memory budget is not built; the per-batch path gives the same result."""
+    from iit_amd.entry.eval_information import evaluate_model_on_probes
+    from iit_amd.tasks.task_loader import get_dataset
+    from iit_amd.utils.probes import ActivationBank
+    ll, _ = _setup(8)
+    tr, te = get_dataset("pvr_leaky", dataset_config={"train_size": 32, "test_size": 64, "device": "cpu"})
+    hooks = ["mod.layer3.mod.0.mod.conv1.hook_point"]
+    need = ActivationBank.estimate_bytes(ll, tr.base_data, hooks)
+    assert need > 32 * 100  # a layer-3 activation per sample, 32 samples
+    res = {}
+    for budget in ("100", "1e-6"):
+        monkeypatch.setenv("IIT_PROBE_BANK_GB", budget)
+        torch.manual_seed(0)
+        res[budget] = evaluate_model_on_probes(ll, "pvr_leaky", {"batch_size": 16, "lr": 1e-3, "num_workers": 0,
+                                                                 "epochs": 1, "engine": "native"},
+                                               tr.base_data, te.base_data, hook_points=hooks)
+    assert "per-batch capture instead" in capsys.readouterr().out
+    a, b = res["100"][hooks[0]]["test accuracy"], res["1e-6"][hooks[0]]["test accuracy"]
+    assert max(abs(a[k] - b[k]) for k in a) <= 1e-6

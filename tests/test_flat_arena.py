@@ -237,3 +237,29 @@ def test_rebind_zeroes_missing_slots_only():
     assert float(m.blocks[0].mlp.W_in.grad.abs().sum()) == 0.0
     assert float(a.b_Q.grad.abs().sum()) == 0.0 and bool((a.b_K.grad == 3.0).all()) and bool((a.b_V.grad == 3.0).all())
     assert bool((m.blocks[0].mlp.W_out.grad == 3.0).all())
+
+
+def test_optimizer_state_refuses_other_arena_layout():
+    """Adam moments saved for an NCHW arena must not load into an NHWC one (they would be permuted)."""
+    import pytest
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.ops.optim import FusedAdam
+
+    def make(channels_last):
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 3, bias=False), torch.nn.Linear(4, 2))
+        if channels_last:
+            m = m.to(memory_format=torch.channels_last)
+        flat = FlatParams(m)
+        return flat, FusedAdam(flat, lr=1e-3, use_hip=False)
+
+    f_a, o_a = make(False)
+    f_b, o_b = make(True)
+    assert f_a.layout_tag() != f_b.layout_tag()
+    sd = o_a.state_dict()
+    assert sd["arena_layout"] == f_a.layout_tag()
+    o_a.load_state_dict(sd)  # same layout: fine
+    with pytest.raises(ValueError, match="arena layout"):
+        o_b.load_state_dict(sd)
+    legacy = {k: v for k, v in sd.items() if k != "arena_layout"}
+    o_b.load_state_dict(legacy)  # pre-tag state: loaded with a warning

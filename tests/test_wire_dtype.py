@@ -122,3 +122,29 @@ def test_gloo_world8_bf16_all_reduce_within_ring_bound(grads):
     W32 = sum(p.double() for p in payload) / WORLD
     assert _rel(got, W32) < 0.005, _rel(got, W32)
     assert _rel(got, W32) < 2 * _rel(_ring_bf16([p.double() for p in payload]), W32) + 1e-4
+
+
+def test_default_wire_follows_compute_dtype():
+    """the bf16 wire is the RCCL default only for models that compute in bf16 (fp32 models keep an
+    fp32 wire: their single-GPU gradients carry no bf16 rounding the wire's could hide behind)."""
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.models.config import gpt2_config_dict
+    from iit_amd.models.transformer import HookedTransformer
+    from iit_amd.parallel.ddp import GradReducer, computes_bf16
+    cfg = gpt2_config_dict()
+    cfg.update(n_layers=1, d_model=16, n_heads=2, d_head=8, d_mlp=32, d_vocab=64, n_ctx=8, device="cpu")
+    m32 = HookedTransformer(dict(cfg, dtype=torch.float32))
+    flat = FlatParams(m32)
+    assert not computes_bf16(m32, flat)
+    m16 = HookedTransformer(dict(cfg, dtype=torch.bfloat16))
+    assert computes_bf16(m16, FlatParams(m16))
+    flat.ensure_shadow()
+    assert computes_bf16(m32, flat)  # a bf16 mirror (fused HIP backend / conv mirror) means bf16 compute
+    # the lazy default: resolved at the first launch on RCCL only
+    r = GradReducer.__new__(GradReducer)
+    r._module, r.flat, r.wire_dtype, r._wire_auto = m32, FlatParams(m32), None, True
+    r._resolve_wire()
+    assert r.wire_dtype is None and not r._wire_auto
+    r._module, r.flat, r.wire_dtype, r._wire_auto = m16, FlatParams(m16), None, True
+    r._resolve_wire()
+    assert r.wire_dtype == torch.bfloat16
