@@ -25,7 +25,7 @@ SOURCES = ["gemm.hip", "gemm_glds.hip", "gemm_dual.hip", "gemm_8ph.hip", "gemm_4
 # avoids the AGPR shuffles hipcc otherwise emits around its register double buffer
 EXTRA_FLAGS = {"gemm_glds.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "gemm_dual.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
                "gemm_8ph.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
-HEADERS = ["common.h", "gemm_glds_body.h", "splice_spec.h"]
+HEADERS = ["common.h", "gemm_glds_body.h", "gemm_w4.h", "splice_spec.h"]
 ARCH = os.environ.get("IIT_OFFLOAD_ARCH", "gfx950")
 
 

@@ -263,3 +263,49 @@ def test_maxpool3s2_matches_torch(shape, ties, dtype):
     assert rel(xa.grad, xb.grad) < (1e-2 if dtype == torch.bfloat16 else 1e-6), rel(xa.grad, xb.grad)
     # routing: the gradient lands on the same elements
     assert torch.equal(xa.grad != 0, xb.grad != 0)
+
+
+@pytest.mark.parametrize("C,hw,N", [(64, 42, 256), (512, 3, 64)])
+def test_bn_stats_large_mean_offset(C, hw, N):
+    """the batch variance is formed from per-chunk (mean, M2) pairs around a pivot, combined with Chan's
+    update -- not E[x^2] - mean^2, which cancels when |mean| >> std.  fp32 activations with a per-channel mean of
+    ~1000 and unit std: mean / variance / running statistics / output against a float64 reference."""
+    from iit_amd.ops import bn as fbn
+    torch.manual_seed(3)
+    bn = torch.nn.BatchNorm2d(C).to(dev)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    bn.train(True)
+    off = (torch.rand(C, device=dev) * 200 + 900)[None, :, None, None]
+    x = (torch.randn(N, C, hw, hw, device=dev) * (torch.rand(C, device=dev)[None, :, None, None] + 0.5) + off)
+    x = x.contiguous(memory_format=torch.channels_last)
+    rv0 = bn.running_var.clone()
+    y = fbn.bn_act(x, bn, None, relu=False)
+    xd = x.double()
+    mean = xd.mean((0, 2, 3))
+    var = xd.var((0, 2, 3), unbiased=False)
+    n = x.numel() // C
+    ref = ((xd - mean[None, :, None, None]) * torch.rsqrt(var + bn.eps)[None, :, None, None]
+           * bn.weight.double()[None, :, None, None] + bn.bias.double()[None, :, None, None])
+    assert rel(y, ref) < 1e-4
+    rv = 0.9 * rv0.double() + 0.1 * var * n / (n - 1)
+    assert torch.allclose(bn.running_var.double(), rv, rtol=1e-4, atol=1e-6)
+
+
+def test_bn_partials_are_deterministic():
+    """No atomics in the statistics: two runs of forward + backward give bit-identical outputs and gradients."""
+    from iit_amd.ops import bn as fbn
+    torch.manual_seed(5)
+    outs = []
+    for _ in range(2):
+        bn = torch.nn.BatchNorm2d(64).to(dev)
+        x = torch.randn(256, 64, 21, 21, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        torch.manual_seed(5)
+        x = torch.randn(256, 64, 21, 21, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x.requires_grad_()
+        y = fbn.bn_act(x, bn, None, relu=True)
+        y.backward(torch.ones_like(y))
+        outs.append((y.detach().clone(), x.grad.clone(), bn.weight.grad.clone(), bn.running_var.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
