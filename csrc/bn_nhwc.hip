@@ -6,23 +6,24 @@
 // Layout: x [M][C] (M = N * H * W rows, C channels contiguous, C % 8 == 0); one thread owns 8 consecutive channels
 // of a row (one 16-B load / store), a wave covers 64 / (C / 8) rows at once.
 //
-// Forward (training): a stats pass over row chunks -- every workgroup owns a contiguous chunk of rows, sums x - p and
-// (x - p)^2 per channel in fp32 around a per-chunk pivot p (the chunk's first row: |mean - p| is O(std), so the
-// variance does not cancel the way E[x^2] - mean^2 does when |mean| >> std) and stores its chunk's (mean, M2) with plain
-// stores -- no atomics, no ticket, no serial last-workgroup tail.  The apply pass then combines the R chunk partials
-// of its channels in a fixed order with Chan's parallel update (deterministic, identical in every workgroup), writes
-// y = relu(x * scale + shift (+ res)) and, in workgroup 0, mean / rstd for the backward, the running mean / unbiased
-// variance with the momentum and num_batches_tracked (torch.nn.BatchNorm2d's buffer semantics).  Eval mode: the apply
-// pass alone, from the running statistics.
+// Forward (training): stats pass -- per-channel sums of x - p and (x - p)^2 in fp32 around a per-channel pivot p (the
+// batch's first row: no cancellation when |mean| >> std), reduced in LDS per workgroup and
+// added with one fp32 atomic per channel per workgroup into a per-module accumulator; the LAST workgroup to finish
+// (a ticket) reads the totals back with atomics, writes mean / rstd for the apply pass and the backward, updates the
+// running mean / unbiased variance with the momentum, increments num_batches_tracked (torch.nn.BatchNorm2d's buffer
+// semantics) and re-zeroes the accumulator and the ticket for the next call (no memset launch) -- then the apply pass
+// writes y = relu(x * scale + shift (+ res)) in bf16.  Eval mode: the apply pass alone, from the running statistics.
 //
-// Backward: dz = dy * (y > 0) (the ReLU mask from the saved output); a stats pass stores per-chunk partial sums of dz
-// and dz * xhat; the apply pass combines them (fixed order), writes dx = w rstd (dz - sum(dz) / M - xhat
-// sum(dz xhat) / M) (training; eval: w rstd dz) and the residual's gradient dz, and workgroup 0 ADDS the weight / bias
-// gradients sum(dz xhat) / sum(dz) into the parameters' gradient buffers (no autograd accumulation launch).
+// Backward: dz = dy * (y > 0) (the ReLU mask from the saved bf16 output), a stats pass for sum(dz) and
+// sum(dz * xhat) whose last workgroup also ADDS the weight / bias gradients sum(dz xhat) / sum(dz) into the
+// parameters' gradient buffers (no autograd accumulation launch), then dx = w rstd (dz - sum(dz) / M - xhat
+// sum(dz xhat) / M) (training; eval: w rstd dz) and the residual's gradient dz.
 //
-// The kernel boundary between the two passes is the only synchronisation: the partials are written by one launch and
-// read by the next (round 6: the round-5 fp32 memory-side atomics on 8 slots per channel + a ticketed last workgroup
-// cost 10-17 us per call on 0.5-3 us of HBM traffic, profiles/pvr_step_r5.txt).
+// Ticket protocol (MI355X_MICROARCH.md hand-off table, producer and consumer in different workgroups of one kernel):
+// the fp32 adds are memory-side atomics; every thread waits vmcnt(0) for its adds before the workgroup barrier, one
+// thread then takes the ticket with a relaxed agent-scope atomic, and the last workgroup reads the totals with atomic
+// read-modify-writes (atomicExch to 0), which also execute at the memory side -- no L2 line of the accumulator is
+// ever read with a plain load, so no acquire-side invalidate is needed either.
 #include "common.h"
 #include "splice_spec.h"
 #include <stdlib.h>
@@ -30,9 +31,10 @@
 namespace {
 
 constexpr int TPB = 256;
-// partial bytes the apply pass combines per workgroup: R chunks x 2C floats <= RC_MAX x 2 floats
-constexpr int RC_MAX = 8192;
-constexpr int C_MAX = 2048;  // C / 8 <= TPB
+// the per-channel accumulator is spread over BN_SLOTS copies (workgroup b adds into slot b % BN_SLOTS; the last
+// workgroup sums them): 1/BN_SLOTS of the memory-side atomics per address -- a few thousand workgroups adding into
+// the same 2C addresses serialised on them
+constexpr int BN_SLOTS = 8;
 
 // Interchange splice of the BN input (the preceding conv's hook, ``hook_point`` of mode-"q" PVR sites): the
 // activation the kernels read is x' = where(spec, src, x), spec over the logical [N][C][H][W] with src's element
@@ -102,10 +104,10 @@ __device__ __forceinline__ void store8(float* p, const Row8& r) {
   ((float4*)p)[1] = make_float4(r.v[4], r.v[5], r.v[6], r.v[7]);
 }
 
-// per-channel totals of this workgroup's per-thread [8] pairs (a, b) (threads sharing a channel group, rows r < rpi):
-// thread c (c < C, strided) gets (sum a, sum b) of channel c; ``red`` is TPB * 16 floats of LDS
-__device__ __forceinline__ void block_channel_sums(const float* a, const float* b, int C, int G, int rpi, int tid,
-                                                   float* red) {
+// block reduction of per-thread [8] pairs (a, b) over the threads sharing a channel group; adds the block totals
+// into acc[c] / acc[C + c] with one atomic per channel
+__device__ __forceinline__ void block_channel_add(const float* a, const float* b, int C, int G, int rpi, int tid,
+                                                  float* acc, float* red) {
   const int g = tid % G, r = tid / G;
   if (r < rpi) {
 #pragma unroll
@@ -115,176 +117,173 @@ __device__ __forceinline__ void block_channel_sums(const float* a, const float* 
     }
   }
   __syncthreads();
-}
-
-__device__ __forceinline__ void channel_total(const float* red, int c, int G, int rpi, float& sa, float& sb) {
-  const int gg = c / 8, e = c % 8;
-  float x = 0.f, y = 0.f;
-  for (int rr = 0; rr < rpi; ++rr) {
-    x += red[(rr * G + gg) * 16 + e];
-    y += red[(rr * G + gg) * 16 + 8 + e];
+  for (int i = tid; i < G * 16; i += TPB) {
+    const int gg = i / 16, e = i % 16;
+    float s = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) s += red[(rr * G + gg) * 16 + e];
+    const int c = gg * 8 + (e & 7);
+    atomicAdd(acc + (e < 8 ? c : C + c), s);
   }
-  sa = x;
-  sb = y;
 }
 
-// rows of chunk w of R chunks of ``chunk`` rows over M rows
-__device__ __forceinline__ long chunk_rows(int w, long chunk, long M) {
-  const long r0 = (long)w * chunk;
-  const long r1 = r0 + chunk < M ? r0 + chunk : M;
-  return r1 - r0;
-}
-
-// part[w][0, C) = mean, part[w][C, 2C) = M2 of chunk w = blockIdx.x (rows [w chunk, (w + 1) chunk))
-template <bool SP, typename T>
-__global__ __launch_bounds__(TPB) void bn_stats_kernel(const T* __restrict__ x, long M, int C, long chunk,
-                                                       float* __restrict__ part, XSplice xs) {
-  __shared__ float red[TPB * 16];
-  __shared__ float piv[C_MAX];
-  const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
+// block reduction as block_channel_add, but the totals are STORED (no atomics) channel-major at
+// part[c * R + block] / part[(C + c) * R + block] (R = gridDim.x), for the fixed-order second level
+__device__ __forceinline__ void block_channel_part(const float* a, const float* b, int C, int G, int rpi, int tid,
+                                                   float* part, float* red) {
   const int g = tid % G, r = tid / G;
-  const long r0 = (long)blockIdx.x * chunk;
-  const long r1 = r0 + chunk < M ? r0 + chunk : M;
-  float s[8], q[8], p[8];
-  {
-    unsigned hit;
-    const Row8 pv = load_x<SP>(x, r0, C, g * 8, xs, hit);  // the pivot: this chunk's first row (x' when spliced)
+  if (r < rpi) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      p[e] = pv.v[e];
-      s[e] = q[e] = 0.f;
-    }
-    if (r == 0) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) piv[g * 8 + e] = p[e];
+      red[(r * G + g) * 16 + e] = a[e];
+      red[(r * G + g) * 16 + 8 + e] = b[e];
     }
   }
+  __syncthreads();
+  const long R = gridDim.x;
+  for (int i = tid; i < G * 16; i += TPB) {
+    const int gg = i / 16, e = i % 16;
+    float s = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) s += red[(rr * G + gg) * 16 + e];
+    const int c = gg * 8 + (e & 7);
+    part[(long)(e < 8 ? c : C + c) * R + blockIdx.x] = s;
+  }
+}
+
+// fixed-order sum of one channel's R partials by one wave (lane-strided, then a butterfly): bit-identical every run
+__device__ __forceinline__ float wave_part_sum(const float* __restrict__ v, int R, int lane) {
+  float s = 0.f;
+  for (int w = lane; w < R; w += 64) s += v[w];
+  return wave_sum(s);
+}
+
+// the last workgroup of a ticketed reduction: every thread waits for its memory-side atomic adds to complete
+// (s_waitcnt vmcnt(0): no L2 writeback is needed, nothing here went through a cache), the workgroup barrier
+// collects them, then one relaxed agent-scope ticket per workgroup -- a full __threadfence() per thread (an L2
+// write-back each) made the stats pass 2.7x slower
+__device__ __forceinline__ bool last_block(unsigned* ticket, int tid, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = t == gridDim.x - 1;
+  }
+  __syncthreads();
+  return *flag;
+}
+
+// acc[0, C) += sum_rows x, acc[C, 2C) += sum_rows x^2; the last workgroup turns the totals into save = (mean, rstd),
+// updates the running statistics and num_batches_tracked, and re-arms acc / ticket
+template <bool SP, typename T>
+__global__ __launch_bounds__(TPB) void bn_stats_kernel(const T* __restrict__ x, long M, int C, float* acc,
+                                                       unsigned* ticket, float* __restrict__ save, float* rmean,
+                                                       float* rvar, float eps, float momentum, long long* nbt,
+                                                       XSplice xs, float* __restrict__ part) {
+  __shared__ float red[TPB * 16];
+  __shared__ int flag;
+  const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
+  const int g = tid % G, r = tid / G;
+  float s[8], q[8];
+  // sums of x - p and (x - p)^2 around a per-channel pivot p = x'[0][c] (the batch's first row, the same in every
+  // workgroup): |mean - p| is O(std), so var = E[(x-p)^2] - E[x-p]^2 does not cancel the way E[x^2] - mean^2 does
+  // when |mean| >> std
+  unsigned hit0;
+  const Row8 piv = load_x<SP>(x, 0, C, g * 8, xs, hit0);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
   if (r < rpi) {
-#pragma unroll 4  // several rows' loads in flight per thread (the loop is latency-bound)
-    for (long row = r0 + r; row < r1; row += rpi) {
+#pragma unroll 4  // several rows' loads in flight per thread (the loop was latency-bound)
+    for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
       unsigned hit;
       const Row8 v = load_x<SP>(x, row, C, g * 8, xs, hit);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float d = v.v[e] - p[e];
+        const float d = v.v[e] - piv.v[e];
         s[e] += d;
         q[e] = __builtin_fmaf(d, d, q[e]);
       }
     }
   }
-  block_channel_sums(s, q, C, G, rpi, tid, red);
-  const float n = (float)(r1 - r0);
-  float* dst = part + (long)blockIdx.x * 2 * C;
+  if (part) {  // two-level reduction: this workgroup's totals, channel-major, for bn_finalize_kernel
+    block_channel_part(s, q, C, G, rpi, tid, part, red);
+    return;
+  }
+  block_channel_add(s, q, C, G, rpi, tid, acc + (blockIdx.x % BN_SLOTS) * 2 * C, red);
+  if (!last_block(ticket, tid, &flag)) return;
   for (int c = tid; c < C; c += TPB) {
-    float S, Q;
-    channel_total(red, c, G, rpi, S, Q);
-    dst[c] = piv[c] + S / n;                  // chunk mean
-    dst[C + c] = fmaxf(Q - S * (S / n), 0.f);  // chunk M2 = sum (x - mean)^2
+    float sum = 0.f, sq = 0.f;
+    for (int k = 0; k < BN_SLOTS; ++k) {
+      sum += atomicExch(acc + k * 2 * C + c, 0.f);
+      sq += atomicExch(acc + k * 2 * C + C + c, 0.f);
+    }
+    unsigned hit;
+    const float p = load_x<SP>(x, 0, C, (c / 8) * 8, xs, hit).v[c % 8];  // the pivot of channel c
+    const float dm = sum / (float)M;  // mean - p
+    const float mean = p + dm;
+    const float var = fmaxf(sq / (float)M - dm * dm, 0.f);
+    save[c] = mean;
+    save[C + c] = rsqrtf(var + eps);
+    if (rmean) {
+      const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+    }
+  }
+  if (tid == 0) {
+    if (nbt) nbt[0] += 1;
+    atomicExch(ticket, 0u);
   }
 }
 
-// mean[c], var[c] (biased) of all M rows from the R chunk partials, combined in chunk order (Chan et al.'s pairwise
-// update); TPC threads per channel each fold a contiguous range of chunks, then their results are folded in order
-__device__ __forceinline__ void combine_stats(const float* __restrict__ part, int R, long chunk, long M, int C,
-                                              float* mean_out, float* var_out, float* lds3 /* [3][TPB] */) {
-  const int tid = threadIdx.x;
-  const int TPC = C >= TPB ? 1 : TPB / C;  // threads per channel (C divides TPB or TPB divides C)
-  const int per = (R + TPC - 1) / TPC;
-  for (int base = 0; base < C; base += TPB / TPC) {
-    const int c = base + tid / TPC, j = tid % TPC;
-    float na = 0.f, ma = 0.f, m2a = 0.f;
-    if (c < C) {
-      const int w0 = j * per, w1 = min(R, w0 + per);
-      for (int w = w0; w < w1; ++w) {
-        const float nb = (float)chunk_rows(w, chunk, M);
-        const float mb = part[(long)w * 2 * C + c], m2b = part[(long)w * 2 * C + C + c];
-        const float nn = na + nb;
-        const float d = mb - ma;
-        ma += d * (nb / nn);
-        m2a += m2b + d * d * (na * nb / nn);
-        na = nn;
-      }
-    }
-    lds3[tid] = na;
-    lds3[TPB + tid] = ma;
-    lds3[2 * TPB + tid] = m2a;
-    __syncthreads();
-    if (c < C && j == 0) {
-      for (int k = 1; k < TPC; ++k) {
-        const float nb = lds3[tid + k], mb = lds3[TPB + tid + k], m2b = lds3[2 * TPB + tid + k];
-        if (nb == 0.f) continue;
-        const float nn = na + nb;
-        const float d = mb - ma;
-        ma += d * (nb / nn);
-        m2a += m2b + d * d * (na * nb / nn);
-        na = nn;
-      }
-      mean_out[c] = ma;
-      var_out[c] = m2a / (float)M;
-    }
-    __syncthreads();
+// second level of the two-level forward reduction: one wave per channel sums the R channel-major partials in a fixed
+// order and writes save = (mean, rstd), the running statistics and (wave 0 of block 0) num_batches_tracked
+template <bool SP, typename T>
+__global__ __launch_bounds__(64) void bn_finalize_kernel(const T* __restrict__ x, const float* __restrict__ part,
+                                                         int R, long M, int C, float* __restrict__ save, float* rmean,
+                                                         float* rvar, float eps, float momentum, long long* nbt,
+                                                         XSplice xs) {
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const float sum = wave_part_sum(part + (long)c * R, R, lane);
+  const float sq = wave_part_sum(part + (long)(C + c) * R, R, lane);
+  if (lane != 0) return;
+  unsigned hit;
+  const float p = load_x<SP>(x, 0, C, (c / 8) * 8, xs, hit).v[c % 8];  // the pivot of channel c
+  const float dm = sum / (float)M;
+  const float mean = p + dm;
+  const float var = fmaxf(sq / (float)M - dm * dm, 0.f);
+  save[c] = mean;
+  save[C + c] = rsqrtf(var + eps);
+  if (rmean) {
+    const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
   }
+  if (c == 0 && nbt) nbt[0] += 1;
 }
 
-// (sum a, sum b)[c] over the R chunk partials, in chunk order (TPC threads per channel, then folded in order)
-__device__ __forceinline__ void combine_sums(const float* __restrict__ part, int R, int C, float* a_out, float* b_out,
-                                             float* lds2 /* [2][TPB] */) {
-  const int tid = threadIdx.x;
-  const int TPC = C >= TPB ? 1 : TPB / C;
-  const int per = (R + TPC - 1) / TPC;
-  for (int base = 0; base < C; base += TPB / TPC) {
-    const int c = base + tid / TPC, j = tid % TPC;
-    float sa = 0.f, sb = 0.f;
-    if (c < C) {
-      const int w0 = j * per, w1 = min(R, w0 + per);
-      for (int w = w0; w < w1; ++w) {
-        sa += part[(long)w * 2 * C + c];
-        sb += part[(long)w * 2 * C + C + c];
-      }
-    }
-    lds2[tid] = sa;
-    lds2[TPB + tid] = sb;
-    __syncthreads();
-    if (c < C && j == 0) {
-      for (int k = 1; k < TPC; ++k) {
-        sa += lds2[tid + k];
-        sb += lds2[TPB + tid + k];
-      }
-      a_out[c] = sa;
-      b_out[c] = sb;
-    }
-    __syncthreads();
-  }
+// second level of the backward reduction: coef = (sum dz, sum dz xhat), the parameter gradients accumulated
+__global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(const float* __restrict__ part, int R, int C,
+                                                             float* __restrict__ coef, float* dw, float* db) {
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const float sdz = wave_part_sum(part + (long)c * R, R, lane);
+  const float sdzx = wave_part_sum(part + (long)(C + c) * R, R, lane);
+  if (lane != 0) return;
+  coef[c] = sdz;
+  coef[C + c] = sdzx;
+  if (dw) dw[c] += sdzx;
+  if (db) db[c] += sdz;
 }
 
-// y = relu?(x * scale + shift (+ res)); training: the statistics from the R chunk partials (workgroup 0 also writes
-// save = (mean, rstd), the running statistics and num_batches_tracked); eval: from the running statistics, and
-// workgroup 0 writes them to ``save`` for the backward
+// y = relu?(x * scale + shift (+ res)); training: mean / rstd from ``save`` (the stats kernel); eval: from the running
+// statistics, and workgroup 0 writes them to ``save`` for the backward
 template <bool SP, typename T>
 __global__ __launch_bounds__(TPB) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                        T* __restrict__ y, float* __restrict__ save,
-                                                       float* __restrict__ rmean, float* __restrict__ rvar,
+                                                       const float* __restrict__ rmean, const float* __restrict__ rvar,
                                                        const float* __restrict__ w, const float* __restrict__ b, long M,
-                                                       int C, float eps, int relu, int batch, const float* part, int R,
-                                                       long chunk, float momentum, long long* nbt, XSplice xs) {
-  __shared__ float st_mean[C_MAX], st_var[C_MAX];
-  __shared__ float lds3[3 * TPB];
+                                                       int C, float eps, int relu, int batch, XSplice xs) {
   const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
   const int g = tid % G, r = tid / G;
-  if (batch) {
-    combine_stats(part, R, chunk, M, C, st_mean, st_var, lds3);
-    if (blockIdx.x == 0) {
-      for (int c = tid; c < C; c += TPB) {
-        const float mean = st_mean[c], var = st_var[c];
-        save[c] = mean;
-        save[C + c] = rsqrtf(var + eps);
-        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-        rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
-        rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
-      }
-      if (tid == 0 && nbt) nbt[0] += 1;
-    }
-  } else if (blockIdx.x == 0) {
+  if (!batch && blockIdx.x == 0) {
     for (int c = tid; c < C; c += TPB) {
       save[c] = rmean[c];
       save[C + c] = rsqrtf(rvar[c] + eps);
@@ -295,8 +294,8 @@ __global__ __launch_bounds__(TPB) void bn_apply_kernel(const T* __restrict__ x, 
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int c = g * 8 + e;
-    const float mean = batch ? st_mean[c] : rmean[c];
-    const float rstd = batch ? rsqrtf(st_var[c] + eps) : rsqrtf(rvar[c] + eps);
+    const float mean = batch ? save[c] : rmean[c];
+    const float rstd = batch ? save[C + c] : rsqrtf(rvar[c] + eps);
     sc[e] = w[c] * rstd;
     sh[e] = b[c] - mean * sc[e];
   }
@@ -320,17 +319,17 @@ __global__ __launch_bounds__(TPB) void bn_apply_kernel(const T* __restrict__ x, 
   }
 }
 
-// part[w][0, C) = sum dz, part[w][C, 2C) = sum dz * xhat over chunk w   (dz = dy masked by y > 0 when y is given)
+// acc[0, C) += sum dz, acc[C, 2C) += sum dz * xhat   (dz = dy masked by y > 0 when y is given)
 template <bool SP, typename T>
 __global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ y,
                                                            const T* __restrict__ x, const float* __restrict__ save,
-                                                           long M, int C, long chunk, float* __restrict__ part,
-                                                           XSplice xs) {
+                                                           long M, int C, float* acc, unsigned* ticket,
+                                                           float* __restrict__ coef, float* dw, float* db, XSplice xs,
+                                                           float* __restrict__ part) {
   __shared__ float red[TPB * 16];
+  __shared__ int flag;
   const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
   const int g = tid % G, r = tid / G;
-  const long r0 = (long)blockIdx.x * chunk;
-  const long r1 = r0 + chunk < M ? r0 + chunk : M;
   float s[8], q[8], mean[8], rstd[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -339,8 +338,8 @@ __global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const T* __restrict__
     rstd[e] = save[C + g * 8 + e];
   }
   if (r < rpi) {
-#pragma unroll 4
-    for (long row = r0 + r; row < r1; row += rpi) {
+#pragma unroll 4  // several rows' loads in flight per thread (the loop was latency-bound)
+    for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
       const long o = row * C + g * 8;
       Row8 d = load8(dy + o);
       unsigned hit;
@@ -357,38 +356,34 @@ __global__ __launch_bounds__(TPB) void bn_bwd_stats_kernel(const T* __restrict__
       }
     }
   }
-  block_channel_sums(s, q, C, G, rpi, tid, red);
-  float* dst = part + (long)blockIdx.x * 2 * C;
-  for (int c = tid; c < C; c += TPB) {
-    float S, Q;
-    channel_total(red, c, G, rpi, S, Q);
-    dst[c] = S;
-    dst[C + c] = Q;
+  if (part) {
+    block_channel_part(s, q, C, G, rpi, tid, part, red);
+    return;
   }
+  block_channel_add(s, q, C, G, rpi, tid, acc + (blockIdx.x % BN_SLOTS) * 2 * C, red);
+  if (!last_block(ticket, tid, &flag)) return;
+  for (int c = tid; c < C; c += TPB) {  // coef = (sum dz, sum dz xhat); parameter gradients accumulated
+    float sdz = 0.f, sdzx = 0.f;
+    for (int k = 0; k < BN_SLOTS; ++k) {
+      sdz += atomicExch(acc + k * 2 * C + c, 0.f);
+      sdzx += atomicExch(acc + k * 2 * C + C + c, 0.f);
+    }
+    coef[c] = sdz;
+    coef[C + c] = sdzx;
+    if (dw) dw[c] += sdzx;
+    if (db) db[c] += sdz;
+  }
+  if (tid == 0) atomicExch(ticket, 0u);
 }
 
 template <bool SP, typename T>
 __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ y,
                                                            const T* __restrict__ x, const float* __restrict__ save,
-                                                           const float* __restrict__ w, const float* __restrict__ part,
-                                                           int R, long M, int C, int batch, T* __restrict__ dx,
-                                                           T* __restrict__ dres, float* coef, float* dw, float* db,
-                                                           XSplice xs) {
-  __shared__ float st_a[C_MAX], st_b[C_MAX];
-  __shared__ float lds2[2 * TPB];
+                                                           const float* __restrict__ w, const float* __restrict__ acc,
+                                                           long M, int C, int batch, T* __restrict__ dx,
+                                                           T* __restrict__ dres, XSplice xs) {
   const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
   const int g = tid % G, r = tid / G;
-  if (batch || dw || db) {
-    combine_sums(part, R, C, st_a, st_b, lds2);
-    if (blockIdx.x == 0) {  // coef = (sum dz, sum dz xhat); parameter gradients accumulated
-      for (int c = tid; c < C; c += TPB) {
-        coef[c] = st_a[c];
-        coef[C + c] = st_b[c];
-        if (dw) dw[c] += st_b[c];
-        if (db) db[c] += st_a[c];
-      }
-    }
-  }
   if (r >= rpi) return;
   float k1[8], k2[8], k3[8], mean[8], rstd[8];
   const float inv_m = 1.f / (float)M;
@@ -398,8 +393,8 @@ __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(const T* __restrict__
     mean[e] = save[c];
     rstd[e] = save[C + c];
     k1[e] = w[c] * rstd[e];                          // dx = k1 (dz - k2 - xhat k3)
-    k2[e] = batch ? st_a[c] * inv_m : 0.f;
-    k3[e] = batch ? st_b[c] * inv_m : 0.f;
+    k2[e] = batch ? acc[c] * inv_m : 0.f;
+    k3[e] = batch ? acc[C + c] * inv_m : 0.f;
   }
 #pragma unroll 4
   for (long row = (long)blockIdx.x * rpi + r; row < M; row += (long)gridDim.x * rpi) {
@@ -455,29 +450,6 @@ int grid_for(long M, int C) {
   if (g < 1) g = 1;
   if (g > 2048) g = 2048;
   return (int)g;
-}
-
-// the stats passes' row chunks: R workgroups of ``chunk`` rows (R * C <= RC_MAX so the apply pass's fixed-order
-// combine reads <= 64 KiB of partials per workgroup; >= 4 row iterations per thread group); IIT_BN_RC overrides the cap
-int bn_rc_max() {
-  static const int v = [] {
-    const char* e = getenv("IIT_BN_RC");
-    const int r = e ? atoi(e) : RC_MAX;
-    return r >= 64 && r <= 65536 ? r : RC_MAX;
-  }();
-  return v;
-}
-
-void chunks_for(long M, int C, int& R, long& chunk) {
-  const int rpi = TPB / (C / 8);
-  int cap = bn_rc_max() / C;
-  if (cap < 1) cap = 1;
-  const long min_rows = 4L * rpi;
-  long want = (M + min_rows - 1) / min_rows;
-  if (want < 1) want = 1;
-  R = (int)(want < cap ? want : cap);
-  chunk = (M + R - 1) / R;
-  R = (int)((M + chunk - 1) / chunk);  // no empty chunk
 }
 
 bool shape_ok(long M, int C, const void* p) {
@@ -618,8 +590,8 @@ IIT_EXPORT int iit_maxpool3s2_bwd(const void* dy, const void* idx, void* dx, int
   return (int)hipGetLastError();
 }
 
-// forward: ws = per-module partials buffer (iit_bn_ws_floats, fully rewritten by every call that reads it);
-// y = relu?(bn(x) (+ res)); save [2C] = mean, rstd (the batch's in training, the running ones in eval)
+// forward: ws = per-module accumulator (fp32 [BN_SLOTS][2C] + a u32 ticket after it, zero at the first call, re-armed by
+// every call); y = relu?(bn(x) (+ res)); save [2C] = mean, rstd (the batch's in training, the running ones in eval)
 static bool make_xsplice(XSplice& xs, const void* src, const void* spec, long M, int C, int H, int W) {
   xs = XSplice{};
   if (!src || !spec) return true;
@@ -631,27 +603,46 @@ static bool make_xsplice(XSplice& xs, const void* src, const void* spec, long M,
          xs.sp.shape[3] == W;
 }
 
+// the two-level (partials + finalize) reduction instead of the memory-side atomics + ticketed last workgroup:
+// IIT_BN_REDUCE=atomic keeps the round-5 path (A/B: scripts/bench_bn.py)
+bool bn_two_level() {
+  static const bool v = [] {
+    const char* e = getenv("IIT_BN_REDUCE");
+    return !(e && e[0] == 'a');
+  }();
+  return v;
+}
+
+constexpr int BN_PART_MAX = 2048;  // grid_for's cap: partials per channel
+
 template <typename T>
 int bn_fwd_impl(const void* x, const void* res, void* y, float* ws, float* rmean, float* rvar, const float* w,
                 const float* b, long M, int C, float eps, int relu, int training, float* save, float momentum,
                 long long* nbt, const XSplice& xs, hipStream_t s) {
   const int grid = grid_for(M, C);
-  int R = 0;
-  long chunk = M;
-  if (training) chunks_for(M, C, R, chunk);
+  unsigned* ticket = (unsigned*)(ws + BN_SLOTS * 2 * C);
+  float* part = bn_two_level() ? ws + BN_SLOTS * 2 * C + 4 : nullptr;  // (16-B aligned after the ticket)
   // the splice-reading instantiations only where a splice is given (the others keep the lean inner loop)
   if (xs.src) {
-    if (training)
-      hipLaunchKernelGGL((bn_stats_kernel<true, T>), dim3(R), dim3(TPB), 0, s, (const T*)x, M, C, chunk, ws, xs);
+    if (training) {
+      hipLaunchKernelGGL((bn_stats_kernel<true, T>), dim3(grid), dim3(TPB), 0, s, (const T*)x, M, C, ws, ticket, save,
+                         rmean, rvar, eps, momentum, nbt, xs, part);
+      if (part)
+        hipLaunchKernelGGL((bn_finalize_kernel<true, T>), dim3(C), dim3(64), 0, s, (const T*)x, (const float*)part,
+                           grid, M, C, save, rmean, rvar, eps, momentum, nbt, xs);
+    }
     hipLaunchKernelGGL((bn_apply_kernel<true, T>), dim3(grid), dim3(TPB), 0, s, (const T*)x, (const T*)res, (T*)y,
-                       save, rmean, rvar, w, b, M, C, eps, relu, training, (const float*)ws, R, chunk, momentum, nbt,
-                       xs);
+                       save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training, xs);
   } else {
-    if (training)
-      hipLaunchKernelGGL((bn_stats_kernel<false, T>), dim3(R), dim3(TPB), 0, s, (const T*)x, M, C, chunk, ws, xs);
+    if (training) {
+      hipLaunchKernelGGL((bn_stats_kernel<false, T>), dim3(grid), dim3(TPB), 0, s, (const T*)x, M, C, ws, ticket, save,
+                         rmean, rvar, eps, momentum, nbt, xs, part);
+      if (part)
+        hipLaunchKernelGGL((bn_finalize_kernel<false, T>), dim3(C), dim3(64), 0, s, (const T*)x, (const float*)part,
+                           grid, M, C, save, rmean, rvar, eps, momentum, nbt, xs);
+    }
     hipLaunchKernelGGL((bn_apply_kernel<false, T>), dim3(grid), dim3(TPB), 0, s, (const T*)x, (const T*)res, (T*)y,
-                       save, rmean, rvar, w, b, M, C, eps, relu, training, (const float*)ws, R, chunk, momentum, nbt,
-                       xs);
+                       save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps, relu, training, xs);
   }
   return (int)hipGetLastError();
 }
@@ -661,23 +652,23 @@ int bn_bwd_impl(const void* dy, const void* y, const void* x, const float* save,
                 float* coef, long M, int C, int training, void* dx, void* dres, float* dw, float* db,
                 const XSplice& xs, hipStream_t s) {
   const int grid = grid_for(M, C);
-  int R = 0;
-  long chunk = M;
-  const bool sums = training || dw || db;  // the eval-mode backward needs the sums only for the parameter gradients
-  if (sums) chunks_for(M, C, R, chunk);
+  unsigned* ticket = (unsigned*)(ws + BN_SLOTS * 2 * C);
+  float* part = bn_two_level() ? ws + BN_SLOTS * 2 * C + 4 : nullptr;
   if (xs.src) {
-    if (sums)
-      hipLaunchKernelGGL((bn_bwd_stats_kernel<true, T>), dim3(R), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
-                         (const T*)x, save, M, C, chunk, ws, xs);
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, T>), dim3(grid), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
-                       (const T*)x, save, w, (const float*)ws, R, M, C, training, (T*)dx, (T*)dres, coef, dw, db, xs);
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<true, T>), dim3(grid), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
+                       (const T*)x, save, M, C, ws, ticket, coef, dw, db, xs, part);
   } else {
-    if (sums)
-      hipLaunchKernelGGL((bn_bwd_stats_kernel<false, T>), dim3(R), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
-                         (const T*)x, save, M, C, chunk, ws, xs);
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, T>), dim3(grid), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
-                       (const T*)x, save, w, (const float*)ws, R, M, C, training, (T*)dx, (T*)dres, coef, dw, db, xs);
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<false, T>), dim3(grid), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
+                       (const T*)x, save, M, C, ws, ticket, coef, dw, db, xs, part);
   }
+  if (part)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(64), 0, s, (const float*)part, grid, C, coef, dw, db);
+  if (xs.src)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, T>), dim3(grid), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
+                       (const T*)x, save, w, (const float*)coef, M, C, training, (T*)dx, (T*)dres, xs);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, T>), dim3(grid), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
+                       (const T*)x, save, w, (const float*)coef, M, C, training, (T*)dx, (T*)dres, xs);
   return (int)hipGetLastError();
 }
 
@@ -695,7 +686,7 @@ IIT_EXPORT int iit_bn_fwd(const void* x, const void* res, void* y, float* ws, fl
              : bn_fwd_impl<__bf16>(x, res, y, ws, rmean, rvar, w, b, M, C, eps, relu, training, save, momentum, nbt, xs, s);
 }
 
-// backward: ws as in the forward; coef [2C] = (sum dz, sum dz xhat) (written when computed); dx (and dres = the residual's gradient when non-null);
+// backward: ws as in the forward; coef [2C] scratch; dx (and dres = the residual's gradient when non-null);
 // dw / db (nullable) ACCUMULATED into
 IIT_EXPORT int iit_bn_bwd(const void* dy, const void* y, const void* x, const float* save, const float* w,
                           float* ws, float* coef, long M, int C, int training, void* dx, void* dres, float* dw,
@@ -710,8 +701,5 @@ IIT_EXPORT int iit_bn_bwd(const void* dy, const void* y, const void* x, const fl
              : bn_bwd_impl<__bf16>(dy, y, x, save, w, ws, coef, M, C, training, dx, dres, dw, db, xs, s);
 }
 
-// floats of the per-module partials buffer ``ws`` (R chunks x 2C, R * C <= the cap; ops/bn.py allocates it)
-IIT_EXPORT int iit_bn_ws_floats(int C) {
-  const int cap = bn_rc_max() / C;
-  return 2 * C * (cap < 1 ? 1 : cap);
-}
+// floats of the per-module accumulator ``ws`` (ops/bn.py allocates it zeroed)
+IIT_EXPORT int iit_bn_ws_floats(int C) { return BN_SLOTS * 2 * C + 4 + 2 * C * BN_PART_MAX; }

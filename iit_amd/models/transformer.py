@@ -25,6 +25,7 @@ Parameters are always fp32 masters; ``cfg.dtype`` selects the compute dtype
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Union
 
 import torch
@@ -531,6 +532,87 @@ class TransformerBlock(nn.Module):
             return ops.mlp_out_residual(post.base, mlp.W_out, mlp.b_out, resid2.base), False
         return ops.pair_mlp_out_residual(post, mlp.W_out, mlp.b_out, resid2), True
 
+    # ------------------------------------------------------------------ paired rows, torch op backend (Llama family)
+    def paired_torch_ok(self, ops) -> bool:
+        """Whether this block can run in a paired forward on the torch op backend (``ops.torch_pairs``): bf16 on the
+        GPU, RMSNorm, (rotary / GQA) flash attention, SiLU-gated MLP, no attention-result hook."""
+        cfg = self.cfg
+        if getattr(ops, "fused", True) or ops.dtype != torch.bfloat16 or cfg.use_attn_result:
+            return False
+        if self.ln1 is None or not self.ln1.rms or self.ln1.w is None or cfg.d_head not in (64, 128):
+            return False
+        if cfg.d_model % 8 or (not cfg.attn_only and cfg.d_mlp % 8) or not _hip_ops().flash_supported(
+                self.attn.W_Q):
+            return False
+        if not cfg.attn_only and (self.ln2 is None or not self.ln2.rms or self.ln2.w is None or not self.mlp.gated
+                                  or cfg.act_fn != "silu"):
+            return False
+        return True
+
+    def forward_paired_torch(self, p, run: _Run, sites, stop_after: str, captures):
+        """:meth:`forward_paired` for the torch op backend (RMSNorm / rotary / GQA flash attention / SwiGLU) with the
+        paired Functions of :mod:`iit_amd.ops.torch_pairs`; sites ``attn.hook_z`` / ``mlp.hook_post``.  Returns
+        ``(resid, still_paired)``, or None when an arena layout the paired ops need does not hold (the caller then
+        drops the partial paired run -- nothing was accumulated -- and falls back to two forwards)."""
+        from ..ops import torch_pairs as tp
+        ops = run.ops
+        attn = self.attn
+        zname = attn.hook_z.name
+        zs = sites.get(zname)
+        x = tp.pair_rms(p, self.ln1.w, self.ln1.eps)
+        Wk, Wv, bk, bv = attn.kv_params()
+        qkv = tp.pair_qkv(x, attn.W_Q, Wk, Wv, attn.b_Q, bk, bv)
+        if qkv is None:
+            return None
+        q, k, v = qkv
+        if attn.rotary:
+            q = tp.pair_rotary(q, attn.rotary_cos, attn.rotary_sin, attn.rotary_dim, self.cfg.rotary_adjacent_pairs)
+            k = tp.pair_rotary(k, attn.rotary_cos, attn.rotary_sin, attn.rotary_dim, self.cfg.rotary_adjacent_pairs)
+        z = tp.pair_flash(q, k, v, self.cfg.attention_dir == "causal", attn.attn_scale)
+        for ix in zs or ():
+            z = tp.pair_splice(z, ix)
+        if zs is not None:
+            captures[zname] = z.src
+        if zname == stop_after:
+            return self._finish_after_attn_torch(z.base, p.base, run), False
+        attn_out = tp.pair_o_proj(z, attn.W_O, attn.b_O)
+        if attn_out is None:
+            return None
+        resid_mid = tp.pair_add(p, attn_out)
+        if self.cfg.attn_only:
+            return resid_mid, True
+        mlp = self.mlp
+        x = tp.pair_rms(resid_mid, self.ln2.w, self.ln2.eps)
+        gate = tp.pair_linear(x, mlp.W_gate)
+        up = tp.pair_linear(x, mlp.W_in, mlp.b_in)
+        if gate is None or up is None:
+            return None
+        post = tp.pair_swiglu(gate, up)
+        pname = mlp.hook_post.name
+        ps = sites.get(pname)
+        for ix in ps or ():
+            post = tp.pair_splice(post, ix)
+        if ps is not None:
+            captures[pname] = post.src
+        if pname == stop_after:
+            return ops.residual(resid_mid.base, ops.mlp_out(post.base, mlp.W_out, mlp.b_out)), False
+        out = tp.pair_linear(post, mlp.W_out, mlp.b_out)
+        if out is None:
+            return None
+        return tp.pair_add(resid_mid, out), True
+
+    def _finish_after_attn_torch(self, z, resid, run: _Run):
+        """The rest of a (torch-backend) block on base rows, after a paired attention section."""
+        ops = run.ops
+        attn = self.attn
+        resid_mid = ops.residual(resid, ops.o_proj(z, attn.W_O, attn.b_O))
+        if self.cfg.attn_only:
+            return resid_mid
+        mlp = self.mlp
+        x = self.ln2.run(resid_mid, run)
+        _, post = TorchOps.mlp_gated_in(ops, x, mlp.W_gate, mlp.W_in, mlp.b_in, self.cfg.act_fn)
+        return ops.residual(resid_mid, ops.mlp_out(post, mlp.W_out, mlp.b_out))
+
     def _finish_after_attn(self, z, resid, run: _Run, last_only: bool):
         """The rest of the block (O projection + MLP) on base rows, after a paired attention section."""
         ops = run.ops
@@ -766,6 +848,8 @@ class HookedTransformer(HookedRootModule):
             return None
         ops = self.ops()
         cfg = self.cfg
+        if self._torch_pairs_ok(ops, tokens, src_tokens):
+            return self._run_paired_torch(tokens, src_tokens, sites, logits)
         if not getattr(ops, "supports_pairs", False) or self.rotary or cfg.final_rms:
             return None
         # S <= 16: the MFMA attention kernel (in-kernel head mirroring); 16 < S <= 64: the short-sequence kernel,
@@ -823,6 +907,91 @@ class HookedTransformer(HookedRootModule):
             else:
                 resid = block(resid, run, last_only=lo)
         if paired:  # (cannot happen: the deepest site ends the pairing) -- keep the base rows
+            resid = resid.base
+        if logits == "none":
+            return None, captures
+        if logits == "last":
+            resid = resid[:, -1]
+        x = resid if self.ln_final is None else self.ln_final.run(resid, run)
+        if logits == "argmax":
+            return ops.unembed_argmax(x, self.unembed.W_U, self.unembed.b_U), captures
+        return ops.unembed(x, self.unembed.W_U, self.unembed.b_U), captures
+
+    def _torch_pairs_ok(self, ops, tokens, src_tokens) -> bool:
+        """The torch-backend paired forward applies: bf16 torch ops on the GPU, the Llama block family
+        (:meth:`TransformerBlock.paired_torch_ok`), flash-attention sequence lengths, no live user hook."""
+        if getattr(ops, "fused", True) or ops.dtype != torch.bfloat16 or not self.embed.W_E.is_cuda:
+            return False
+        if self.cfg.positional_embedding_type != "rotary" or os.environ.get("IIT_PAIRED_TORCH", "1") == "0":
+            return False
+        if tokens.dim() != 2 or tokens.shape != src_tokens.shape or tokens.shape[1] <= 16:
+            return False
+        if any(hp.is_live for hp in self.hook_dict.values()):
+            return False
+        return all(blk.paired_torch_ok(ops) for blk in self.blocks)
+
+    def _run_paired_torch(self, tokens, src_tokens, sites, logits: str):
+        """:meth:`run_paired` on the torch op backend (Llama family, ``ops.torch_pairs``): sites ``hook_embed``,
+        ``blocks.L.attn.hook_z`` and ``blocks.L.mlp.hook_post``; the pairing ends after the deepest site."""
+        from ..ops import torch_pairs as tp
+        cfg = self.cfg
+        B, S = tokens.shape
+        order = []
+        for name, idxs in sites.items():
+            parts = name.split(".")
+            if name == "hook_embed":
+                order.append((-1, 0, name))
+                shape = (B, S, cfg.d_model)
+            elif len(parts) == 4 and parts[0] == "blocks" and (parts[2], parts[3]) in (("attn", "hook_z"),
+                                                                                          ("mlp", "hook_post")):
+                if parts[2] == "mlp" and cfg.attn_only:
+                    return None
+                order.append((int(parts[1]), 0 if parts[2] == "attn" else 1, name))
+                shape = (B, S, cfg.n_heads, cfg.d_head) if parts[2] == "attn" else (B, S, cfg.d_mlp)
+            else:
+                return None
+            for ix in idxs:
+                if not ix.is_everything() and _hip_ops().pair_specs(ix, shape) is None:
+                    return None
+        deepest = max(order)
+        tokens = tokens.to(self.embed.W_E.device)
+        src_tokens = src_tokens.to(self.embed.W_E.device)
+        ops = self.ops()
+        run = _Run(RunPlan(logits=logits), ops)
+        gate = self.__dict__.get("_param_gate")
+        if gate is not None:
+            gate(None)
+        ops.begin_forward()
+        captures = {}
+        resid = tp.pair_embed(tokens, src_tokens, self.embed.W_E)
+        if resid is None:
+            return None
+        for ix in sites.get("hook_embed", ()):
+            resid = tp.pair_splice(resid, ix)
+            if resid is None:
+                return None
+        if "hook_embed" in sites:
+            captures["hook_embed"] = resid.src
+        paired = deepest[2] != "hook_embed"
+        if not paired:
+            resid = resid.base
+        cuts = self.__dict__.get("_grad_cuts") if torch.is_grad_enabled() else None
+        for li, block in enumerate(self.blocks):
+            base = resid.base if paired else resid
+            if cuts and li in cuts and base.requires_grad:
+                leaf = base.detach().requires_grad_(True)
+                self._cut_log.append((li, base, leaf))
+                resid = _hip_ops().Paired(leaf, resid.full) if paired else leaf
+            if gate is not None:
+                gate(li)
+            if paired:
+                res = block.forward_paired_torch(resid, run, sites, deepest[2], captures)
+                if res is None:
+                    return None
+                resid, paired = res
+            else:
+                resid = block(resid, run)
+        if paired:
             resid = resid.base
         if logits == "none":
             return None, captures

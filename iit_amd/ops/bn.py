@@ -49,8 +49,8 @@ def covered(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res: Optional[torch.Tenso
 
 
 def _ws(bn: torch.nn.BatchNorm2d, C: int, device) -> torch.Tensor:
-    """The module's per-chunk partials buffer (csrc/bn_nhwc.hip: R row chunks x 2C floats, written by a stats pass and
-    read by the apply pass right after it on the same stream).  Shared by the forward and backward of every call."""
+    """The module's self-re-arming reduction accumulator: [slots][2C] floats + a ticket, zero at creation; every kernel call
+    leaves it zero again (csrc/bn_nhwc.hip).  Shared by the forward and backward of every call on the stream."""
     n = K.bn_ws_floats(C)
     ws = bn.__dict__.get("_iit_bn_ws")
     if ws is None or ws.numel() < n or ws.device != device:

@@ -106,6 +106,7 @@ def main():
                     help="torch: the fp32 torch-op oracle backend on the same device")
     ap.add_argument("--train-nodes", default="",
                     help="comma list of HL node names the TRAINING steps sample from (default: all, as the reference)")
+    ap.add_argument("--seed", type=int, default=0, help="model-initialisation seed (torch / numpy)")
     ap.add_argument("--control", default="", choices=["", "zero-wo"],
                     help="zero-wo: zero and freeze W_O of the blocks hosting hook_duplicate (see the docstring)")
     args = ap.parse_args()
@@ -117,8 +118,8 @@ def main():
     from iit_amd.tasks.ioi import NAMES, ioi_cfg, make_ioi_corr, make_ioi_dataset_and_hl
 
     dev = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
-    torch.manual_seed(0)
-    np.random.seed(0)
+    torch.manual_seed(args.seed)
+    np.random.seed(args.seed)
     cfg = gpt2_config_dict()
     if args.model == "ioi-6l":
         cfg.update(ioi_cfg)
@@ -180,6 +181,8 @@ def main():
     rows = []
     orig_log = pair._print_and_log_metrics
     t0 = time.perf_counter()
+    t_eval = [0.0]   # wall spent in this script's whole-split per-node evaluations (not the reference's epoch loop)
+    first95 = {}     # first evaluated epoch where EVERY node's whole-split IIA >= 95 %: epoch, training wall
 
     def log(epoch, metrics, sink=None):
         vals = {m.get_name(): m.get_value() for m in metrics if m.get_name() != "val/per_token_accuracy"}
@@ -188,7 +191,11 @@ def main():
         row = {"epoch": epoch, "val/IIA": round(float(vals["val/IIA"]), 2), "eval_node_draws": dict(mix)}
         if epoch % args.every == 0 or epoch == args.epochs - 1:
             rng_state = pair.rng.bit_generator.state
+            te = time.perf_counter()
             iia, ce = per_node_iia(pair, test_set)
+            t_eval[0] += time.perf_counter() - te
+            if not first95 and min(iia.values()) >= 95.0:
+                first95.update(epoch=epoch, train_wall_s=round(te - t0 - (t_eval[0] - (time.perf_counter() - te)), 1))
             row["per_node_IIA"] = {k: round(v, 2) for k, v in iia.items()}
             row["per_node_IIT_loss"] = {k: round(v, 4) for k, v in ce.items()}
             if control_layers:
@@ -210,7 +217,8 @@ def main():
     best = max(rows, key=lambda r: r["val/IIA"])
     print(json.dumps({"metric": "IOI val/IIA ceiling analysis", "model": args.model, "epochs": args.epochs,
                       "train_nodes": args.train_nodes or "all", "control": args.control or None, "graphs": args.graphs, "backend": args.backend, "lr": args.lr,
-                      "wall_s": round(wall, 1), "tie_fraction_per_node": ties,
+                      "wall_s": round(wall, 1), "seed": args.seed,
+                      "first_eval_all_nodes_IIA_ge_95": first95 or None, "tie_fraction_per_node": ties,
                       "best_epoch_val_IIA": best["val/IIA"], "best_epoch": best["epoch"],
                       "final_per_node_IIA": rows[-1].get("per_node_IIA"), "final_control": rows[-1].get("control")}))
 
