@@ -2,6 +2,8 @@
 // fragment reads, tile order and the per-tile body ``gemm_glds_body``, used by the single-problem launches of
 // gemm_glds.hip and the two-problem launches of gemm_dual.hip.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -42,6 +44,11 @@ struct G2Args {
   // E_F32_STORE: optional sum of squares of the stored values (this weight gradient's share of the global gradient
   // norm the optimizer's clip needs), += atomically into one of 64 slots, so the norm pass can skip these gradients
   float* gsq;
+  // implicit-GEMM convolution (csrc/conv_nhwc.hip): the A operand is gathered from an NHWC activation [n][h][w][c]
+  // (conv_h x conv_w pixels, conv_c channels) through 3 x 3 / stride-1 / pad-1 taps; rows outside the image read
+  // the 16-B-aligned zero page ``zero``; conv_flip negates the tap offsets (the input-gradient convolution)
+  const __bf16* zero;
+  int conv_h, conv_w, conv_c, conv_flip;
 };
 
 __device__ __forceinline__ void prof_mark(long long* prof, int slot, int e, bool on) {
@@ -453,9 +460,13 @@ __device__ __forceinline__ void glds_epilogue(const G2Args& p, char* smem, const
 // One output tile of one GEMM problem: workgroup ``lin`` of the ``nlin`` tiles of K-split ``split`` of ``nsplit``
 // (a single-problem launch passes its block index and grid size; the dual launch in gemm_dual.hip maps its
 // workgroups onto two problems).  ``smem`` is the launch's one LDS object of at least GldsSmem<...>::BYTES.
-template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW, int BK = 64, int OCC = 1, bool LEAN = false>
+template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW, int BK = 64, int OCC = 1, bool LEAN = false,
+          class ASTG = void>
 __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, const int nlin, const int split,
                                                const int nsplit, char* smem) {
+  // ASTG: an A-operand stager other than the strided-matrix one (the convolution's implicit im2col rows); it takes
+  // its geometry from ``p`` and must fill the same LDS image as OperandStager<AKM, BM, NW, BK>
+  using SA = std::conditional_t<std::is_void_v<ASTG>, OperandStager<AKM, BM, NW, BK, LEAN>, ASTG>;
   constexpr int HALVES = BK / 64;  // a 128-deep K-tile is two 64-deep halves of two 32-deep MFMA sub-steps each
   constexpr int NT = NW * 64;                    // threads
   constexpr int WMR = NW / 2;                    // wave rows (waves form a WMR x 2 grid)
@@ -463,7 +474,7 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LOADS = OperandStager<AKM, BM, NW, BK, LEAN>::N + OperandStager<BKM, BN, NW, BK, LEAN>::N;  // DMA / wave / K-tile
+  constexpr int LOADS = SA::N + OperandStager<BKM, BN, NW, BK, LEAN>::N;  // DMA / wave / K-tile
   using SM = GldsSmem<BM, BN, NS, NW, BK, OCC>;
   constexpr int EPS = SM::EPS;  // fp32 epilogue row stride (floats)
   // the fp32 epilogue tile goes through LDS in row chunks (one per wave row) when the whole tile would not fit
@@ -516,9 +527,10 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
   //    wave's counted vmcnt) and retires all reads of tile kt, so those MFMAs overlap the next DMA issue.
   RawFrag<AKM> ca[TM], na[TM];
   RawFrag<BKM> cb[TN], nb[TN];
-  OperandStager<AKM, BM, NW, BK, LEAN> stA;
+  SA stA;
   OperandStager<BKM, BN, NW, BK, LEAN> stB;
-  stA.init(p.A, p.lda, m0, kbeg, wave, lane);
+  if constexpr (std::is_void_v<ASTG>) stA.init(p.A, p.lda, m0, kbeg, wave, lane);
+  else stA.init(p, m0, kbeg, wave, lane);
   stB.init(p.B, p.ldb, n0, kbeg, wave, lane);
 #pragma unroll
   for (int s = 0; s < NS; ++s)

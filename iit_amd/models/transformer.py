@@ -961,7 +961,9 @@ class HookedTransformer(HookedRootModule):
         gate = self.__dict__.get("_param_gate")
         if gate is not None:
             gate(None)
-        ops.begin_forward()
+        begin = getattr(ops, "begin_forward", None)
+        if begin is not None:
+            begin()
         captures = {}
         resid = tp.pair_embed(tokens, src_tokens, self.embed.W_E)
         if resid is None:

@@ -19,11 +19,11 @@ CSRC = os.path.join(ROOT, "csrc")
 OUT_DIR = os.path.join(ROOT, "iit_amd", "_native")
 LIB = os.path.join(OUT_DIR, "libiit_hip.so")
 OBJ_CACHE = os.path.join(ROOT, "build", "objcache")  # git-ignored; not shipped to the GPU box
-SOURCES = ["gemm.hip", "gemm_glds.hip", "gemm_dual.hip", "gemm_8ph.hip", "gemm_4w.hip", "kernels.hip", "attn_mfma.hip", "flash_attn.hip", "llama_ops.hip",
+SOURCES = ["gemm.hip", "gemm_glds.hip", "gemm_dual.hip", "gemm_8ph.hip", "gemm_4w.hip", "conv_nhwc.hip", "kernels.hip", "attn_mfma.hip", "flash_attn.hip", "llama_ops.hip",
            "splice.hip", "ioi_hl.hip", "bn_nhwc.hip"]
 # per-source compiler flags: the pipelined LDS-DMA GEMM keeps its accumulators in VGPRs (MFMA VGPR form), which
 # avoids the AGPR shuffles hipcc otherwise emits around its register double buffer
-EXTRA_FLAGS = {"gemm_glds.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "gemm_dual.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+EXTRA_FLAGS = {"gemm_glds.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "conv_nhwc.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "gemm_dual.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
                "gemm_8ph.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 HEADERS = ["common.h", "gemm_glds_body.h", "gemm_w4.h", "splice_spec.h"]
 ARCH = os.environ.get("IIT_OFFLOAD_ARCH", "gfx950")

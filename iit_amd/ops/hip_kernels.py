@@ -103,6 +103,9 @@ _SIGS = {
                      + [c_int] * 5 + [c_void_p] * 4,
     "iit_gemm_glds_set_group_m": [c_int],
     "iit_ioi_hl_label": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "iit_conv3x3_tiles": [],
+    "iit_conv3x3_ok": [c_long, c_int, c_int, c_int, c_int, c_int],
+    "iit_conv3x3": [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
 }
 
 
@@ -637,6 +640,37 @@ def maxpool3s2_fwd(x, y, idx, N: int, H: int, W: int, C: int):
         assert y.numel() == N * OH * OW * C and idx.numel() == y.numel() and x.numel() == N * H * W * C
     _check(lib().iit_maxpool3s2_fwd(_p(x), _p(y), _p(idx), N, H, W, C, int(x.dtype == torch.float32), _stream()),
            "maxpool3s2_fwd")
+
+
+# ------------------------------------------------------------------------------ implicit-GEMM conv (csrc/conv_nhwc.hip)
+_ZERO_PAGE = {}
+
+
+def zero_page(device) -> torch.Tensor:
+    """>= 128 zero bytes on ``device`` (16-B aligned): the LDS-DMA source of the convolution's padding rows."""
+    key = str(device)
+    z = _ZERO_PAGE.get(key)
+    if z is None:
+        z = _ZERO_PAGE[key] = torch.zeros(256, dtype=torch.bfloat16, device=device)
+    return z
+
+
+def conv3x3_tiles() -> int:
+    return int(lib().iit_conv3x3_tiles())
+
+
+def conv3x3_ok(N: int, H: int, W: int, Cin: int, Cout: int, tile: int) -> bool:
+    return bool(lib().iit_conv3x3_ok(N, H, W, Cin, Cout, tile))
+
+
+def conv3x3(x, w, y, N: int, H: int, W: int, Cin: int, Cout: int, flip: bool = False, tile: int = 0):
+    """``y`` [N,H,W,Cout] = 3x3 / stride-1 / pad-1 convolution of the NHWC bf16 ``x`` [N,H,W,Cin] with ``w``
+    [Cout,3,3,Cin] (``flip``: negated tap offsets -- the input gradient, with ``w`` re-laid [Cin,3,3,Cout])."""
+    if CHECK_BOUNDS:
+        assert x.numel() >= N * H * W * Cin and y.numel() >= N * H * W * Cout and w.numel() >= 9 * Cin * Cout
+        assert x.dtype == w.dtype == y.dtype == torch.bfloat16
+    _check(lib().iit_conv3x3(_p(x), _p(w), _p(y), _p(zero_page(x.device)), N, H, W, Cin, Cout, int(flip), tile,
+                             _stream()), "conv3x3")
 
 
 def maxpool3s2_bwd(dy, idx, dx, N: int, H: int, W: int, C: int):
