@@ -461,12 +461,13 @@ __device__ __forceinline__ void glds_epilogue(const G2Args& p, char* smem, const
 // (a single-problem launch passes its block index and grid size; the dual launch in gemm_dual.hip maps its
 // workgroups onto two problems).  ``smem`` is the launch's one LDS object of at least GldsSmem<...>::BYTES.
 template <int BM, int BN, int NS, bool AKM, bool BKM, int EPI, int NW, int BK = 64, int OCC = 1, bool LEAN = false,
-          class ASTG = void>
+          class ASTG = void, class BSTG = void>
 __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, const int nlin, const int split,
                                                const int nsplit, char* smem) {
-  // ASTG: an A-operand stager other than the strided-matrix one (the convolution's implicit im2col rows); it takes
-  // its geometry from ``p`` and must fill the same LDS image as OperandStager<AKM, BM, NW, BK>
+  // ASTG / BSTG: operand stagers other than the strided-matrix one (the convolution's implicit im2col rows /
+  // columns); they take their geometry from ``p`` and must fill the same LDS image as OperandStager<...>
   using SA = std::conditional_t<std::is_void_v<ASTG>, OperandStager<AKM, BM, NW, BK, LEAN>, ASTG>;
+  using SB = std::conditional_t<std::is_void_v<BSTG>, OperandStager<BKM, BN, NW, BK, LEAN>, BSTG>;
   constexpr int HALVES = BK / 64;  // a 128-deep K-tile is two 64-deep halves of two 32-deep MFMA sub-steps each
   constexpr int NT = NW * 64;                    // threads
   constexpr int WMR = NW / 2;                    // wave rows (waves form a WMR x 2 grid)
@@ -474,7 +475,7 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LOADS = SA::N + OperandStager<BKM, BN, NW, BK, LEAN>::N;  // DMA / wave / K-tile
+  constexpr int LOADS = SA::N + SB::N;  // DMA / wave / K-tile
   using SM = GldsSmem<BM, BN, NS, NW, BK, OCC>;
   constexpr int EPS = SM::EPS;  // fp32 epilogue row stride (floats)
   // the fp32 epilogue tile goes through LDS in row chunks (one per wave row) when the whole tile would not fit
@@ -528,10 +529,11 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
   RawFrag<AKM> ca[TM], na[TM];
   RawFrag<BKM> cb[TN], nb[TN];
   SA stA;
-  OperandStager<BKM, BN, NW, BK, LEAN> stB;
+  SB stB;
   if constexpr (std::is_void_v<ASTG>) stA.init(p.A, p.lda, m0, kbeg, wave, lane);
   else stA.init(p, m0, kbeg, wave, lane);
-  stB.init(p.B, p.ldb, n0, kbeg, wave, lane);
+  if constexpr (std::is_void_v<BSTG>) stB.init(p.B, p.ldb, n0, kbeg, wave, lane);
+  else stB.init(p, n0, kbeg, wave, lane);
 #pragma unroll
   for (int s = 0; s < NS; ++s)
     if (s < nt) {

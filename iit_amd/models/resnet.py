@@ -37,10 +37,10 @@ class Conv2d(nn.Conv2d):
             from ..ops.torch_ops import _MirrorWeight, _arena_mirror
             m = _arena_mirror(w)
             if m is not None:
-                w16 = _MirrorWeight.apply(w, m[0]) if torch.is_grad_enabled() else m[1]
                 from ..ops import conv as hconv
-                if hconv.covered(x, self):  # 3x3 / stride 1: the repo's implicit-GEMM kernel where it wins
-                    return hconv.conv3x3(x, w16)
+                if hconv.covered(x, self):  # 3x3 / stride 1: the repo's implicit-GEMM kernels where they win
+                    return hconv.conv3x3(x, w, m[0])
+                w16 = _MirrorWeight.apply(w, m[0]) if torch.is_grad_enabled() else m[1]
                 return self._conv_forward(x.to(torch.bfloat16), w16, None)
         return super().forward(x)
 

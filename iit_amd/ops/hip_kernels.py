@@ -106,6 +106,10 @@ _SIGS = {
     "iit_conv3x3_tiles": [],
     "iit_conv3x3_ok": [c_long, c_int, c_int, c_int, c_int, c_int],
     "iit_conv3x3": [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "iit_conv3x3_wgrad_tiles": [],
+    "iit_conv3x3_wgrad_ok": [c_long, c_int, c_int, c_int, c_int, c_int, c_int],
+    "iit_conv3x3_wgrad": [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                           c_void_p],
 }
 
 
@@ -671,6 +675,38 @@ def conv3x3(x, w, y, N: int, H: int, W: int, Cin: int, Cout: int, flip: bool = F
         assert x.dtype == w.dtype == y.dtype == torch.bfloat16
     _check(lib().iit_conv3x3(_p(x), _p(w), _p(y), _p(zero_page(x.device)), N, H, W, Cin, Cout, int(flip), tile,
                              _stream()), "conv3x3")
+
+
+CONV_WG_TILES = {0: (64, 64), 1: (128, 64), 2: (128, 128), 3: (64, 128)}
+
+
+def conv3x3_wgrad_splits(pixels: int) -> list:
+    """K-split candidates of a weight gradient over ``pixels`` (a multiple of 64): for each target 1, 2, 4, ..., 64
+    the largest divisor of the K-tile count not above it (the reduction split needs equal K ranges)."""
+    nkt = pixels // 64
+    out = []
+    for target in (1, 2, 4, 8, 16, 32, 64):
+        d = max(x for x in range(1, target + 1) if nkt % x == 0)
+        if d not in out:
+            out.append(d)
+    return out
+
+
+def conv3x3_wgrad_ok(N: int, H: int, W: int, Cin: int, Cout: int, tile: int, splits: int) -> bool:
+    return bool(lib().iit_conv3x3_wgrad_ok(N, H, W, Cin, Cout, tile, splits))
+
+
+def conv3x3_wgrad(dy, x, dw, N: int, H: int, W: int, Cin: int, Cout: int, acc: bool, tile: int, splits: int = 1):
+    """``dw`` [Cout,3,3,Cin] fp32 (+)= the weight gradient of the 3x3 / stride-1 / pad-1 convolution (NHWC bf16 ``dy``
+    [N,H,W,Cout], ``x`` [N,H,W,Cin]); ``splits`` > 1: deterministic reduction split over the pixels."""
+    ws = cnt = None
+    if splits > 1:
+        ws, cnt = split_workspace(Cout, 9 * Cin, CONV_WG_TILES[tile], splits, dy.device)
+    if CHECK_BOUNDS:
+        assert dw.dtype == torch.float32 and dw.numel() >= 9 * Cin * Cout
+        assert dy.numel() >= N * H * W * Cout and x.numel() >= N * H * W * Cin
+    _check(lib().iit_conv3x3_wgrad(_p(dy), _p(x), _p(dw), _p(zero_page(x.device)), N, H, W, Cin, Cout, int(acc), tile,
+                                   splits, _p(ws), _p(cnt), _stream()), "conv3x3_wgrad")
 
 
 def maxpool3s2_bwd(dy, idx, dx, N: int, H: int, W: int, C: int):

@@ -71,7 +71,8 @@ class MirrorMatPairFn(_MirrorMat):
     """:class:`_MirrorMat` (packed QKV / ``W_O``) over both row sets: one GEMM of 2T rows."""
 
     @staticmethod
-    def forward(ctx, x, wm, bm, gw, gb, wparams, bparams, x_full, box, *leaves):
+    def forward(ctx, x, wm, bm, gw, gb, wparams, bparams, x_full, *rest):
+        leaves, box = rest[:-1], rest[-1]  # (``_one`` appends the box last)
         lead = x.shape[:-1]
         x2f = x_full.reshape(-1, x_full.shape[-1])
         T = _rows(x_full, x.shape[0], x_full.shape[0])
@@ -86,7 +87,7 @@ class MirrorMatPairFn(_MirrorMat):
     @staticmethod
     def backward(ctx, gy):
         r = _MirrorMat.backward(ctx, gy)
-        return r[:7] + (None, None) + r[7:]
+        return r[:7] + (None,) + r[7:] + (None,)
 
 
 class MirrorLinearPairFn(_MirrorLinear):

@@ -1,5 +1,5 @@
 """The fused NHWC BatchNorm passes (csrc/bn_nhwc.hip) per PVR ResNet-18 layer shape at B = 256 (84 x 84 inputs),
-graph-timed in isolation: forward (stats + apply) and backward (stats + apply), bf16 activations, with the HBM
+in isolation: forward (stats + apply, graph-timed) and forward + backward (eager, event-timed), bf16 activations, with the HBM
 floor of each (bytes / 6 TB/s) -- where the norm group's time goes.
 
     python scripts/bench_bn.py [--dtype bf16|fp32]
@@ -14,6 +14,18 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SHAPES = [("stem", 64, 42), ("layer1", 64, 21), ("layer2", 128, 11), ("layer3", 256, 6), ("layer4", 512, 3)]
+
+
+def _eager_time(fn, reps: int = 20) -> float:
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
 
 
 def main():
@@ -42,10 +54,7 @@ def main():
             out.backward(g)
 
         t_f = min(gd._time(fwd, reps=20) for _ in range(3))
-        try:
-            t_fb = min(gd._time(fwd_bwd, reps=20) for _ in range(3))
-        except Exception:  # autograd inside a capture: time eagerly
-            t_fb = float("nan")
+        t_fb = min(_eager_time(fwd_bwd) for _ in range(3))  # (autograd is not captured: eager, events)
         nbytes = x.numel() * es
         floor_f = 3 * nbytes / 6e12 * 1e6       # stats read x; apply read x + write y
         floor_b = 7 * nbytes / 6e12 * 1e6       # + bwd stats read dy, y, x; bwd apply read dy, y, x + write dx

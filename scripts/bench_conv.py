@@ -1,6 +1,6 @@
 """The PVR ResNet-18's 3x3 / stride-1 convolutions (B = 256, 84 x 84 inputs) on the repo's implicit-GEMM kernel
 (csrc/conv_nhwc.hip, every tile) against the library convolution (MIOpen / CK through F.conv2d), forward and input
-gradient, graph-timed in isolation on random bf16 NHWC operands.
+gradient and weight gradient, graph-timed in isolation on random bf16 NHWC operands.
 
     python scripts/bench_conv.py
 """
@@ -39,9 +39,17 @@ def main():
                 fwd[f"hip{t}"] = lambda t=t: K.conv3x3(x, w, y, N, hw, hw, Cin, Cout, False, t)
             if K.conv3x3_ok(N, hw, hw, Cout, Cin, t):
                 bwd[f"hip{t}"] = lambda t=t: K.conv3x3(dy, wf, dx, N, hw, hw, Cout, Cin, True, t)
-        for tag, cands in (("fwd", fwd), ("dgrad", bwd)):
+        dwt = torch.empty(Cout, Cin, 3, 3, device="cuda", dtype=torch.float32).contiguous(memory_format=CL)
+        wgr = {"lib": lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0),
+                                                                   1, (False, True, False))}
+        for t in K.CONV_WG_TILES:
+            for sp in K.conv3x3_wgrad_splits(N * hw * hw):
+                if K.conv3x3_wgrad_ok(N, hw, hw, Cin, Cout, t, sp):
+                    wgr[f"hip{t}k{sp}"] = lambda t=t, sp=sp: K.conv3x3_wgrad(dy, x, dwt, N, hw, hw, Cin, Cout, False,
+                                                                             t, sp)
+        for tag, cands in (("fwd", fwd), ("dgrad", bwd), ("wgrad", wgr)):
             times = {k: min(gd._time(f, reps=20) for _ in range(3)) for k, f in cands.items()}
-            row[tag] = {k: round(v, 1) for k, v in sorted(times.items(), key=lambda kv: kv[1])}
+            row[tag] = {k: round(v, 1) for k, v in sorted(times.items(), key=lambda kv: kv[1])[:5]}
         print(json.dumps(row), flush=True)
 
 

@@ -10,3 +10,8 @@ for seed in 0 1; do
     echo "seed $seed $be: $(grep -E '"metric"' $O/6l_s${seed}_$be.log | cut -c1-300)"
   done
 done
+# the vs_baseline denominator at HEAD (it was a 5-step round-1 run): the reference-semantics eager
+# engine (hook closures, full-vocab fp32 logits, torch Adam), 20 timed steps
+timeout -k 10 300 python3 bench.py --engine reference --dtype fp32 --graphs 0 --steps 20 --warmup 3 > $O/ref_eager.log 2>&1 \
+  || { tail -20 $O/ref_eager.log; exit 2; }
+grep -E '^\{' $O/ref_eager.log | cut -c1-300

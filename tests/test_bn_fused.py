@@ -220,9 +220,13 @@ def test_resnet_conv_mirror_matches_autocast_path(monkeypatch):
         FlatParams(m)
     x = torch.rand(32, 3, 84, 84, device=dev).contiguous(memory_format=torch.channels_last)
     t = torch.randint(0, 10, (32,), device=dev)
+    from iit_amd.ops import conv as hconv
     calls = []
     orig = torch_ops._MirrorWeight.apply
     monkeypatch.setattr(torch_ops._MirrorWeight, "apply", lambda *a: calls.append(1) or orig(*a))
+    # the 3x3 / stride-1 convolutions read the mirror through the implicit-GEMM op instead (ops/conv.py)
+    orig_c = hconv.Conv3x3Fn.apply
+    monkeypatch.setattr(hconv.Conv3x3Fn, "apply", lambda *a: calls.append(1) or orig_c(*a))
     outs = []
     for m, env, amp in ((ms[0], "1", True), (ms[1], "0", True), (ms[2], "0", False)):
         monkeypatch.setenv("IIT_CONV_MIRROR", env)
