@@ -603,25 +603,21 @@ static bool make_xsplice(XSplice& xs, const void* src, const void* spec, long M,
          xs.sp.shape[3] == W;
 }
 
-// the two-level (partials + finalize) reduction instead of the memory-side atomics + ticketed last workgroup:
-// IIT_BN_REDUCE=atomic keeps the round-5 path (A/B: scripts/bench_bn.py)
-bool bn_two_level() {
-  static const bool v = [] {
-    const char* e = getenv("IIT_BN_REDUCE");
-    return !(e && e[0] == 'a');
-  }();
-  return v;
-}
+// the two-level reduction (per-workgroup partials stored channel-major + one wave per channel summing them in a fixed
+// order): bit-identical run to run, unlike the memory-side fp32 atomics + ticketed last workgroup of the default path,
+// which measured faster (forward 16-21 vs 25-31 us on layers 1-4, PVR bf16 step 8.25 vs 8.91 ms,
+// profiles/bn_reduction_r6.txt) -- so it serves deterministic mode (ops/bn.py passes ``two_level``) and
+// IIT_BN_REDUCE=two
 
 constexpr int BN_PART_MAX = 2048;  // grid_for's cap: partials per channel
 
 template <typename T>
 int bn_fwd_impl(const void* x, const void* res, void* y, float* ws, float* rmean, float* rvar, const float* w,
                 const float* b, long M, int C, float eps, int relu, int training, float* save, float momentum,
-                long long* nbt, const XSplice& xs, hipStream_t s) {
+                long long* nbt, const XSplice& xs, int two_level, hipStream_t s) {
   const int grid = grid_for(M, C);
   unsigned* ticket = (unsigned*)(ws + BN_SLOTS * 2 * C);
-  float* part = bn_two_level() ? ws + BN_SLOTS * 2 * C + 4 : nullptr;  // (16-B aligned after the ticket)
+  float* part = two_level ? ws + BN_SLOTS * 2 * C + 4 : nullptr;  // (16-B aligned after the ticket)
   // the splice-reading instantiations only where a splice is given (the others keep the lean inner loop)
   if (xs.src) {
     if (training) {
@@ -650,10 +646,10 @@ int bn_fwd_impl(const void* x, const void* res, void* y, float* ws, float* rmean
 template <typename T>
 int bn_bwd_impl(const void* dy, const void* y, const void* x, const float* save, const float* w, float* ws,
                 float* coef, long M, int C, int training, void* dx, void* dres, float* dw, float* db,
-                const XSplice& xs, hipStream_t s) {
+                const XSplice& xs, int two_level, hipStream_t s) {
   const int grid = grid_for(M, C);
   unsigned* ticket = (unsigned*)(ws + BN_SLOTS * 2 * C);
-  float* part = bn_two_level() ? ws + BN_SLOTS * 2 * C + 4 : nullptr;
+  float* part = two_level ? ws + BN_SLOTS * 2 * C + 4 : nullptr;
   if (xs.src) {
     hipLaunchKernelGGL((bn_bwd_stats_kernel<true, T>), dim3(grid), dim3(TPB), 0, s, (const T*)dy, (const T*)y,
                        (const T*)x, save, M, C, ws, ticket, coef, dw, db, xs, part);
@@ -676,29 +672,32 @@ int bn_bwd_impl(const void* dy, const void* y, const void* x, const float* save,
 IIT_EXPORT int iit_bn_fwd(const void* x, const void* res, void* y, float* ws, float* rmean, float* rvar,
                           const float* w, const float* b, long M, int C, float eps, int relu, int training,
                           float* save, float momentum, long long* nbt, const void* src, const void* spec, int H,
-                          int W, int f32, void* stream) {
+                          int W, int f32, int two_level, void* stream) {
   if (!shape_ok(M, C, x) || ((uintptr_t)y & 15) || (res && ((uintptr_t)res & 15))) return (int)hipErrorInvalidValue;
   if (!rmean || !rvar) return (int)hipErrorInvalidValue;
   XSplice xs;
   if (!make_xsplice(xs, src, spec, M, C, H, W)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  return f32 ? bn_fwd_impl<float>(x, res, y, ws, rmean, rvar, w, b, M, C, eps, relu, training, save, momentum, nbt, xs, s)
-             : bn_fwd_impl<__bf16>(x, res, y, ws, rmean, rvar, w, b, M, C, eps, relu, training, save, momentum, nbt, xs, s);
+  return f32 ? bn_fwd_impl<float>(x, res, y, ws, rmean, rvar, w, b, M, C, eps, relu, training, save, momentum, nbt, xs,
+                                   two_level, s)
+             : bn_fwd_impl<__bf16>(x, res, y, ws, rmean, rvar, w, b, M, C, eps, relu, training, save, momentum, nbt, xs,
+                                   two_level, s);
 }
 
 // backward: ws as in the forward; coef [2C] scratch; dx (and dres = the residual's gradient when non-null);
 // dw / db (nullable) ACCUMULATED into
 IIT_EXPORT int iit_bn_bwd(const void* dy, const void* y, const void* x, const float* save, const float* w,
                           float* ws, float* coef, long M, int C, int training, void* dx, void* dres, float* dw,
-                          float* db, const void* src, const void* spec, int H, int W, int f32, void* stream) {
+                          float* db, const void* src, const void* spec, int H, int W, int f32, int two_level,
+                          void* stream) {
   if (!shape_ok(M, C, dy) || ((uintptr_t)x & 15) || ((uintptr_t)dx & 15) || (y && ((uintptr_t)y & 15)) ||
       (dres && ((uintptr_t)dres & 15)))
     return (int)hipErrorInvalidValue;
   XSplice xs;
   if (!make_xsplice(xs, src, spec, M, C, H, W)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  return f32 ? bn_bwd_impl<float>(dy, y, x, save, w, ws, coef, M, C, training, dx, dres, dw, db, xs, s)
-             : bn_bwd_impl<__bf16>(dy, y, x, save, w, ws, coef, M, C, training, dx, dres, dw, db, xs, s);
+  return f32 ? bn_bwd_impl<float>(dy, y, x, save, w, ws, coef, M, C, training, dx, dres, dw, db, xs, two_level, s)
+             : bn_bwd_impl<__bf16>(dy, y, x, save, w, ws, coef, M, C, training, dx, dres, dw, db, xs, two_level, s);
 }
 
 // floats of the per-module accumulator ``ws`` (ops/bn.py allocates it zeroed)

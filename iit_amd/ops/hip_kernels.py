@@ -91,9 +91,9 @@ _SIGS = {
     "iit_splice": [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_int, c_int, c_float, c_void_p],
     "iit_splice_spec_size": [],
     "iit_bn_fwd": [c_void_p] * 8 + [c_long, c_int, c_float, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p,
-                                    c_void_p, c_int, c_int, c_int, c_void_p],
+                                    c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "iit_bn_bwd": [c_void_p] * 7 + [c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                    c_int, c_int, c_int, c_void_p],
+                                    c_int, c_int, c_int, c_int, c_void_p],
     "iit_gemm_glds_set_prof": [c_void_p],
     "iit_maxpool3s2_fwd": [c_void_p] * 3 + [c_int] * 5 + [c_void_p],
     "iit_bn_ws_floats": [c_int],
@@ -714,6 +714,15 @@ def maxpool3s2_bwd(dy, idx, dx, N: int, H: int, W: int, C: int):
            "maxpool3s2_bwd")
 
 
+def bn_two_level() -> bool:
+    """The BatchNorm statistics' fixed-order two-level reduction (bit-identical run to run) instead of the faster
+    fp32-atomic one: in deterministic mode (``IIT_DETERMINISTIC=1`` / ``torch.use_deterministic_algorithms``) or with
+    ``IIT_BN_REDUCE=two``."""
+    if os.environ.get("IIT_BN_REDUCE", "") == "two":
+        return True
+    return os.environ.get("IIT_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
+
+
 def bn_fwd(x, res, y, ws, rmean, rvar, w, b, M: int, C: int, eps: float, relu: bool, training: bool, save,
            momentum: float, nbt, src=None, spec=None, H: int = 0, W: int = 0):
     """Fused BatchNorm (+ residual) (+ ReLU) forward over NHWC bf16 or fp32 rows (csrc/bn_nhwc.hip; every activation
@@ -724,7 +733,7 @@ def bn_fwd(x, res, y, ws, rmean, rvar, w, b, M: int, C: int, eps: float, relu: b
         assert ws.numel() >= bn_ws_floats(C) and save.numel() >= 2 * C
     _check(lib().iit_bn_fwd(_p(x), _p(res), _p(y), _p(ws), _p(rmean), _p(rvar), _p(w), _p(b), M, C, eps, int(relu),
                             int(training), _p(save), momentum, _p(nbt), _p(src), None if spec is None else spec.ptr,
-                            H, W, int(x.dtype == torch.float32), _stream()), "bn_fwd")
+                            H, W, int(x.dtype == torch.float32), int(bn_two_level()), _stream()), "bn_fwd")
 
 
 def bn_bwd(dy, y, x, save, w, ws, coef, M: int, C: int, training: bool, dx, dres, dw, db, src=None, spec=None,
@@ -735,7 +744,7 @@ def bn_bwd(dy, y, x, save, w, ws, coef, M: int, C: int, training: bool, dx, dres
             assert _avail(t) >= M * C, "bn_bwd: activation smaller than M x C"
     _check(lib().iit_bn_bwd(_p(dy), _p(y), _p(x), _p(save), _p(w), _p(ws), _p(coef), M, C, int(training), _p(dx),
                             _p(dres), _p(dw), _p(db), _p(src), None if spec is None else spec.ptr, H, W,
-                            int(x.dtype == torch.float32), _stream()), "bn_bwd")
+                            int(x.dtype == torch.float32), int(bn_two_level()), _stream()), "bn_bwd")
 
 
 def zero_ranges(base, starts, lens):

@@ -296,3 +296,24 @@ def test_bn_stats_large_mean_offset(C, hw, N):
     rv = 0.9 * rv0.double() + 0.1 * var * n / (n - 1)
     assert torch.allclose(bn.running_var.double(), rv, rtol=1e-4, atol=1e-6)
 
+
+
+def test_bn_two_level_reduction_is_deterministic(monkeypatch):
+    """Deterministic mode (IIT_DETERMINISTIC=1): the BatchNorm statistics take the fixed-order two-level reduction --
+    forward + backward twice give bit-identical outputs, gradients and running statistics, equal to the atomic path
+    within fp32 summation-order noise."""
+    from iit_amd.ops import bn as fbn
+    outs = []
+    for mode in ("1", "1", "0"):
+        monkeypatch.setenv("IIT_DETERMINISTIC", mode)
+        torch.manual_seed(5)
+        bn = torch.nn.BatchNorm2d(64).to(dev)
+        x = torch.randn(256, 64, 21, 21, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x.requires_grad_()
+        y = fbn.bn_act(x, bn, None, relu=True)
+        y.backward(torch.ones_like(y))
+        outs.append((y.detach().clone(), x.grad.clone(), bn.weight.grad.clone(), bn.running_var.clone()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    for a, b in zip(outs[0], outs[2]):
+        assert rel(a, b) < 1e-3
