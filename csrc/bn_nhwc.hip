@@ -179,6 +179,7 @@ __global__ __launch_bounds__(TPB) void bn_stats_kernel(const T* __restrict__ x, 
                                                        float* rvar, float eps, float momentum, long long* nbt,
                                                        XSplice xs, float* __restrict__ part) {
   __shared__ float red[TPB * 16];
+  __shared__ float pivs[8 * TPB];  // the pivots, for the last workgroup's finalize (no dependent global load there)
   __shared__ int flag;
   const int G = C / 8, rpi = TPB / G, tid = threadIdx.x;
   const int g = tid % G, r = tid / G;
@@ -188,6 +189,10 @@ __global__ __launch_bounds__(TPB) void bn_stats_kernel(const T* __restrict__ x, 
   // when |mean| >> std
   unsigned hit0;
   const Row8 piv = load_x<SP>(x, 0, C, g * 8, xs, hit0);
+  if (r == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pivs[g * 8 + e] = piv.v[e];
+  }
 #pragma unroll
   for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
   if (r < rpi) {
@@ -215,8 +220,7 @@ __global__ __launch_bounds__(TPB) void bn_stats_kernel(const T* __restrict__ x, 
       sum += atomicExch(acc + k * 2 * C + c, 0.f);
       sq += atomicExch(acc + k * 2 * C + C + c, 0.f);
     }
-    unsigned hit;
-    const float p = load_x<SP>(x, 0, C, (c / 8) * 8, xs, hit).v[c % 8];  // the pivot of channel c
+    const float p = pivs[c];  // the pivot of channel c (stored before block_channel_add's barrier)
     const float dm = sum / (float)M;  // mean - p
     const float mean = p + dm;
     const float var = fmaxf(sq / (float)M - dm * dm, 0.f);
@@ -432,20 +436,27 @@ __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(const T* __restrict__
   }
 }
 
-int bn_rows_per_group() {  // IIT_BN_ROWS (A/B of the grid size; default 8), read once per process
-  static const int v = [] {
-    const char* e = getenv("IIT_BN_ROWS");
-    const int r = e ? atoi(e) : 8;
-    return r >= 1 && r <= 256 ? r : 8;
-  }();
+// IIT_BN_ROWS = rows per thread group (A/B of the grid size; default 8); IIT_BN_ROWS=0 sizes the grid instead:
+// ceil(want / IIT_BN_GRID) rows (default target 1024 workgroups, 4 per CU), so the small layer-3 / layer-4 tensors
+// spread over more CUs (fewer serial row loads per thread) and the big ones keep ~8 rows.  Read once per process.
+int env_int(const char* name, int dflt, int lo, int hi) {
+  const char* e = getenv(name);
+  const int r = e ? atoi(e) : dflt;
+  return r >= lo && r <= hi ? r : dflt;
+}
+
+int bn_rows_per_group() {
+  static const int v = env_int("IIT_BN_ROWS", 8, 0, 256);
   return v;
 }
 
 int grid_for(long M, int C) {
+  static const int target = env_int("IIT_BN_GRID", 1024, 64, 2048);
   const int rpi = TPB / (C / 8);
   const long want = (M + rpi - 1) / rpi;
-  // ~8 rows per thread group: enough work per workgroup to amortise the per-channel atomics, >= 4 workgroups per CU
-  const int rows = bn_rows_per_group();
+  int rows = bn_rows_per_group();
+  if (rows == 0) rows = (int)((want + target - 1) / target);
+  if (rows < 1) rows = 1;
   long g = (want + rows - 1) / rows;
   if (g < 1) g = 1;
   if (g > 2048) g = 2048;
