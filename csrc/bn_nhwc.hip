@@ -711,5 +711,68 @@ IIT_EXPORT int iit_bn_bwd(const void* dy, const void* y, const void* x, const fl
              : bn_bwd_impl<__bf16>(dy, y, x, save, w, ws, coef, M, C, training, dx, dres, dw, db, xs, two_level, s);
 }
 
+// Training statistics from a convolution epilogue's per-tile column records (gemm_glds_body.h E_BF16_CS, written by
+// csrc/conv_nhwc.hip for the conv whose output this BatchNorm reads): T row tiles of R rows each,
+// cstat[(k C + c) T + t], k = 0 the tile's pivot p_t (its first row), 1 S1_t = sum (v - p_t), 2 S2_t = sum (v - p_t)^2.
+// One workgroup per channel combines them around the global pivot P = p_0 (the batch's first row, as bn_stats_kernel):
+// sum (v - P) = sum_t S1_t + R d_t, sum (v - P)^2 = sum_t S2_t + 2 d_t S1_t + R d_t^2 (d_t = p_t - P), in a fixed order
+// (bit-identical run to run), then mean / rstd, the running statistics and num_batches_tracked as the stats kernel's
+// last workgroup.  Replaces the statistics pass over the activation.
+__global__ __launch_bounds__(256) void bn_tile_finalize_kernel(const float* __restrict__ cstat, int T, int R, long M,
+                                                               int C, float* __restrict__ save, float* rmean,
+                                                               float* rvar, float eps, float momentum, long long* nbt) {
+  __shared__ float red[2][256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const float* pv = cstat + (long)c * T;
+  const float* s1 = cstat + (long)(C + c) * T;
+  const float* s2 = cstat + (long)(2 * C + c) * T;
+  const float P = pv[0], fr = (float)R;
+  float a = 0.f, q = 0.f;
+  for (int t = tid; t < T; t += 256) {
+    const float d = pv[t] - P, u = s1[t];
+    a += __builtin_fmaf(fr, d, u);
+    q += s2[t] + d * __builtin_fmaf(fr, d, 2.f * u);
+  }
+  red[0][tid] = a;
+  red[1][tid] = q;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st) {
+      red[0][tid] += red[0][tid + st];
+      red[1][tid] += red[1][tid + st];
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  const float dm = red[0][0] / (float)M;  // mean - P
+  const float mean = P + dm;
+  const float var = fmaxf(red[1][0] / (float)M - dm * dm, 0.f);
+  save[c] = mean;
+  save[C + c] = rsqrtf(var + eps);
+  if (rmean) {
+    const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+  }
+  if (c == 0 && nbt) nbt[0] += 1;
+}
+
+// training forward of a bf16 activation whose statistics came from its producer's epilogue (``cstat``, T tiles of R
+// rows, T R = M): the tile finalize, then the apply pass (no statistics pass over x)
+IIT_EXPORT int iit_bn_fwd_tiles(const void* x, const void* res, void* y, const float* cstat, int T, int R,
+                                float* rmean, float* rvar, const float* w, const float* b, long M, int C, float eps,
+                                int relu, float* save, float momentum, long long* nbt, void* stream) {
+  if (!shape_ok(M, C, x) || ((uintptr_t)y & 15) || (res && ((uintptr_t)res & 15))) return (int)hipErrorInvalidValue;
+  if (!rmean || !rvar || !cstat || T < 1 || R < 1 || (long)T * R != M) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_tile_finalize_kernel, dim3(C), dim3(256), 0, s, cstat, T, R, M, C, save, rmean, rvar, eps,
+                     momentum, nbt);
+  const XSplice xs{};
+  hipLaunchKernelGGL((bn_apply_kernel<false, __bf16>), dim3(grid_for(M, C)), dim3(TPB), 0, s, (const __bf16*)x,
+                     (const __bf16*)res, (__bf16*)y, save, (const float*)rmean, (const float*)rvar, w, b, M, C, eps,
+                     relu, 1, xs);
+  return (int)hipGetLastError();
+}
+
 // floats of the per-module accumulator ``ws`` (ops/bn.py allocates it zeroed)
 IIT_EXPORT int iit_bn_ws_floats(int C) { return BN_SLOTS * 2 * C + 4 + 2 * C * BN_PART_MAX; }

@@ -147,17 +147,24 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3x3_wgrad_kernel(G2Args p) {
       p, blockIdx.x, gridDim.x, blockIdx.y, gridDim.y, smem);
 }
 
-template <int BM, int BN, int NS, int NW, int OCC>
+// blockIdx.y = K-split (reduction split over the 9 Cin taps-x-channels: every split publishes its fp32 partial tile,
+// the last arriver sums them in split order and runs the bf16 epilogue -- deterministic); gridDim.y = 1: no split
+// EPI = E_BF16_CS: the epilogue also writes per-tile column statistics of the output (a.cstat) for the BatchNorm that
+// reads it (ops/bn.py: the statistics pass over the activation is skipped)
+template <int BM, int BN, int NS, int NW, int OCC, int EPI>
 __global__ __launch_bounds__(NW * 64, OCC) void conv3x3_kernel(G2Args p) {
   __shared__ __attribute__((aligned(16))) char smem[GldsSmem<BM, BN, NS, NW, 64, OCC>::BYTES];
-  gemm_glds_body<BM, BN, NS, false, false, E_BF16, NW, 64, OCC, false, ConvRowStager<BM, NW>>(p, blockIdx.x, gridDim.x,
-                                                                                              0, 1, smem);
+  gemm_glds_body<BM, BN, NS, false, false, EPI, NW, 64, OCC, false, ConvRowStager<BM, NW>>(p, blockIdx.x, gridDim.x,
+                                                                                           blockIdx.y, gridDim.y, smem);
 }
 
 template <int BM, int BN, int NS, int NW = 4, int OCC = 1>
-hipError_t launch_conv(const G2Args& a, hipStream_t s) {
+hipError_t launch_conv(const G2Args& a, int splits, hipStream_t s) {
   const int tiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((conv3x3_kernel<BM, BN, NS, NW, OCC>), dim3(tiles), dim3(NW * 64), 0, s, a);
+  if (a.cstat)
+    hipLaunchKernelGGL((conv3x3_kernel<BM, BN, NS, NW, OCC, E_BF16_CS>), dim3(tiles, splits), dim3(NW * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv3x3_kernel<BM, BN, NS, NW, OCC, E_BF16>), dim3(tiles, splits), dim3(NW * 64), 0, s, a);
   return hipGetLastError();
 }
 
@@ -166,14 +173,14 @@ constexpr int kConvTiles = 6;
 const int kConvBM[kConvTiles] = {128, 128, 64, 128, 64, 128};
 const int kConvBN[kConvTiles] = {64, 128, 64, 128, 128, 64};
 
-hipError_t launch_conv_tile(const G2Args& a, int tile, hipStream_t s) {
+hipError_t launch_conv_tile(const G2Args& a, int tile, int splits, hipStream_t s) {
   switch (tile) {
-    case 0: return launch_conv<128, 64, 4>(a, s);
-    case 1: return launch_conv<128, 128, 3>(a, s);
-    case 2: return launch_conv<64, 64, 4, 4, 2>(a, s);
-    case 3: return launch_conv<128, 128, 2, 4, 2>(a, s);
-    case 4: return launch_conv<64, 128, 2, 4, 3>(a, s);
-    case 5: return launch_conv<128, 64, 2, 4, 2>(a, s);
+    case 0: return launch_conv<128, 64, 4>(a, splits, s);
+    case 1: return launch_conv<128, 128, 3>(a, splits, s);
+    case 2: return launch_conv<64, 64, 4, 4, 2>(a, splits, s);
+    case 3: return launch_conv<128, 128, 2, 4, 2>(a, splits, s);
+    case 4: return launch_conv<64, 128, 2, 4, 3>(a, splits, s);
+    case 5: return launch_conv<128, 64, 2, 4, 2>(a, splits, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -247,21 +254,30 @@ IIT_EXPORT int iit_conv3x3_wgrad(const void* dy, const void* x, float* dw, const
 }
 
 // 1 when the implicit-GEMM kernel covers a 3x3 / stride-1 / pad-1 convolution of [N][H][W][Cin] into Cout channels on
-// ``tile``: Cin % 64 == 0 (a K-tile is one tap), Cout % BN == 0, N H W % BM == 0 (no partial row tiles)
-IIT_EXPORT int iit_conv3x3_ok(long N, int H, int W, int Cin, int Cout, int tile) {
-  if (tile < 0 || tile >= kConvTiles || N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0) return 0;
+// ``tile`` with ``splits`` K-splits: Cin % 64 == 0 (a K-tile is one tap), Cout % BN == 0, N H W % BM == 0 (no partial
+// row tiles), 9 Cin % (64 splits) == 0 (equal K ranges)
+IIT_EXPORT int iit_conv3x3_ok(long N, int H, int W, int Cin, int Cout, int tile, int splits) {
+  if (tile < 0 || tile >= kConvTiles || N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || splits < 1) return 0;
   const long M = N * H * W;
   if (Cin % 64 || Cout % kConvBN[tile] || M % kConvBM[tile] || M >= (1L << 31)) return 0;
+  if ((9 * Cin) % (64 * splits)) return 0;
   return 1;
 }
 
 // y [N][H][W][Cout] = conv3x3(x [N][H][W][Cin], w [Cout][3][3][Cin]) (bf16, NHWC, stride 1, pad 1, no bias);
 // ``flip``: the tap offsets negated (the input gradient: x = dY, w = the weight re-laid [Cin][3][3][Cout]).
-// ``zero``: >= 128 zero bytes, 16-B aligned (the padding rows' LDS-DMA source).
+// ``zero``: >= 128 zero bytes, 16-B aligned (the padding rows' LDS-DMA source).  ``splits`` > 1 needs ``ws`` (>= splits
+// N H W Cout floats) and ``counters`` (>= the tile count, zero when idle; re-armed by every launch).
+IIT_EXPORT int iit_conv3x3_rows(int tile) { return tile >= 0 && tile < kConvTiles ? kConvBM[tile] : 0; }
+
+// ``cstat`` (nullable): per-tile column statistics of y for its BatchNorm, [3][Cout][N H W / BM] floats
+// (gemm_glds_body.h E_BF16_CS; BM = iit_conv3x3_rows(tile))
 IIT_EXPORT int iit_conv3x3(const void* x, const void* w, void* y, const void* zero, long N, int H, int W, int Cin,
-                           int Cout, int flip, int tile, void* stream) {
-  if (!iit_conv3x3_ok(N, H, W, Cin, Cout, tile)) return (int)hipErrorInvalidValue;
+                           int Cout, int flip, int tile, int splits, float* ws, int* counters, float* cstat,
+                           void* stream) {
+  if (!iit_conv3x3_ok(N, H, W, Cin, Cout, tile, splits)) return (int)hipErrorInvalidValue;
   if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y | (uintptr_t)zero) & 15) return (int)hipErrorInvalidValue;
+  if (splits > 1 && (!ws || !counters)) return (int)hipErrorInvalidValue;
   G2Args a{};
   a.A = (const __bf16*)x;
   a.B = (const __bf16*)w;
@@ -272,11 +288,14 @@ IIT_EXPORT int iit_conv3x3(const void* x, const void* w, void* y, const void* ze
   a.M = (int)(N * H * W);
   a.N = Cout;
   a.K = 9 * Cin;
-  a.k_per_split = a.K;
+  a.k_per_split = a.K / splits;
+  a.ws = splits > 1 ? ws : nullptr;
+  a.counters = splits > 1 ? counters : nullptr;
   a.zero = (const __bf16*)zero;
   a.conv_h = H;
   a.conv_w = W;
   a.conv_c = Cin;
   a.conv_flip = flip;
-  return (int)launch_conv_tile(a, tile, (hipStream_t)stream);
+  a.cstat = cstat;
+  return (int)launch_conv_tile(a, tile, splits, (hipStream_t)stream);
 }

@@ -8,8 +8,10 @@
 
 namespace {
 
+// E_BF16_CS: E_BF16 + per-tile column statistics of the stored (bf16-rounded) output into ``cstat`` -- the
+// BatchNorm statistics of a convolution's output from its epilogue (csrc/conv_nhwc.hip, csrc/bn_nhwc.hip)
 enum : int { E_BF16 = 0, E_BF16_BIAS3 = 1, E_F32_RESID = 2, E_GELU = 3, E_DGELU = 4, E_F32_ACC = 5,
-             E_F32_STORE = 7, E_GELU_ERF = 8, E_DGELU_ERF = 9 };
+             E_F32_STORE = 7, E_GELU_ERF = 8, E_DGELU_ERF = 9, E_BF16_CS = 10 };
 
 struct G2Args {
   const __bf16* A;
@@ -49,6 +51,10 @@ struct G2Args {
   // the 16-B-aligned zero page ``zero``; conv_flip negates the tap offsets (the input-gradient convolution)
   const __bf16* zero;
   int conv_h, conv_w, conv_c, conv_flip;
+  // E_BF16_CS: per-tile column statistics, channel-major over the M / BM row tiles T:
+  // cstat[(k * N + col) * T + tm], k = 0 the tile's pivot (its first row's value), 1 sum(v - pivot), 2 sum((v - pivot)^2)
+  // over the tile's BM rows -- plain stores, one writer per element (the consumer is the next launch)
+  float* cstat;
 };
 
 __device__ __forceinline__ void prof_mark(long long* prof, int slot, int e, bool on) {
@@ -340,6 +346,7 @@ __device__ __forceinline__ void glds_epilogue(const G2Args& p, char* smem, const
   constexpr bool PF32 = EPI == E_F32_RESID || EPI == E_F32_ACC;
   constexpr bool PF16 = EPI == E_DGELU || EPI == E_DGELU_ERF;
   float sq = 0.f;  // E_F32_STORE with ``gsq``: this thread's sum of squares of the stored values
+  float cpiv = 0.f, cs1 = 0.f, cs2 = 0.f;  // E_BF16_CS: this thread's column group (pivot, sum d, sum d^2)
   for (int ch = 0; ch < ECH; ++ch) {
   float4 pf[PF32 ? 2 * ITEMS : 1];
   bf16x8 pb[PF16 ? ITEMS : 1];
@@ -378,6 +385,14 @@ __device__ __forceinline__ void glds_epilogue(const G2Args& p, char* smem, const
     if constexpr (EPI == E_BF16) {
       if (p.bias0) add8(v, p.bias0 + col);
       store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v, p.store_mode);
+    } else if constexpr (EPI == E_BF16_CS) {
+      if (p.bias0) add8(v, p.bias0 + col);
+      store8_bf16((__bf16*)p.C + (long)row * p.ldc + col, v, p.store_mode);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(v[e]));  // the statistics of what the consumer reads
+      // this thread's own chunk of E: no other thread touches it before the barrier below
+      *(float4*)(E + lr * EPS + lc) = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)(E + lr * EPS + lc + 4) = make_float4(v[4], v[5], v[6], v[7]);
     } else if constexpr (EPI == E_BF16_BIAS3) {
       const int w = col / p.bias_cols, o = col - w * p.bias_cols;
       const float* bb = w == 0 ? p.bias0 : (w == 1 ? p.bias1 : p.bias2);
@@ -439,7 +454,39 @@ __device__ __forceinline__ void glds_epilogue(const G2Args& p, char* smem, const
       }
     }
   }
+  if constexpr (EPI == E_BF16_CS) {  // this chunk's rows into the thread's column-group sums (one group per thread)
+    __syncthreads();
+    static_assert(NT % BN == 0, "column groups");
+    constexpr int G = NT / BN;
+    const int col = tid % BN, g = tid / BN;
+    if (ch == 0) cpiv = E[col];  // the tile's first row: the pivot (sums of v - pivot do not cancel)
+    for (int r = g; r < ER; r += G) {
+      const float d = E[r * EPS + col] - cpiv;
+      cs1 += d;
+      cs2 = __builtin_fmaf(d, d, cs2);
+    }
+  }
   }  // chunk
+  if constexpr (EPI == E_BF16_CS) {  // the G groups of each column summed in a fixed order, one record per tile
+    constexpr int G = NT / BN;
+    float* red = (float*)smem;
+    __syncthreads();  // every thread is done with the epilogue's LDS tile
+    red[tid] = cs1;
+    red[NT + tid] = cs2;
+    __syncthreads();
+    if (tid < BN) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        a += red[g * BN + tid];
+        b += red[NT + g * BN + tid];
+      }
+      const long T = p.M / BM, tm = m0 / BM, c = n0 + tid;
+      p.cstat[c * T + tm] = cpiv;
+      p.cstat[((long)p.N + c) * T + tm] = a;
+      p.cstat[(2L * p.N + c) * T + tm] = b;
+    }
+  }
   if constexpr (EPI == E_F32_STORE) {
     if (p.gsq) {  // one atomic per workgroup (the waves' sums meet in LDS): thousands of tiles share 64 slots
       sq = wave_sum(sq);
@@ -651,7 +698,7 @@ __device__ __forceinline__ void gemm_glds_body(const G2Args& p, const int lin, c
       }
     }
   }
-  if constexpr (EPI == E_F32_ACC || EPI == E_F32_STORE || EPI == E_F32_RESID) {
+  if constexpr (EPI == E_F32_ACC || EPI == E_F32_STORE || EPI == E_F32_RESID || EPI == E_BF16 || EPI == E_BF16_CS) {
     if (p.ws != nullptr) {
       // Partial tile in MFMA register order (one 16-B chunk per lane per accumulator: 1 KiB coalesced per wave),
       // published without any L2 writeback / invalidate: write-through (sc1) stores, drained with vmcnt(0) before

@@ -104,7 +104,11 @@ def _pool_covered(x: torch.Tensor, pool: nn.Module) -> bool:
 def _bn_after_conv(conv_m, bn_m, relu_m, x, res=None):
     """relu?(bn(conv(x)) (+ res)) with the fused BatchNorm (and a conv-hook splice inside it) when covered, else the
     module path."""
-    h, splice = _conv_with_splice(conv_m, bn_m, x)
+    from ..ops import conv as hconv
+    bn = getattr(bn_m, "mod", bn_m)
+    # a training BatchNorm reading the conv's output unhooked: the conv's epilogue writes its statistics
+    with hconv.stats_for_bn(isinstance(bn, nn.BatchNorm2d) and bn.training and not _hooked(bn_m)):
+        h, splice = _conv_with_splice(conv_m, bn_m, x)
     out = fused_bn_act(bn_m, relu_m, h, res, splice=splice)
     if out is None:
         if splice is not None:  # the fused op could not take the splice: run the conv's hook after all

@@ -60,15 +60,19 @@ def _ws(bn: torch.nn.BatchNorm2d, C: int, device) -> torch.Tensor:
 
 class BNActFn(Function):
     @staticmethod
-    def forward(ctx, x, w, b, res, bn, relu, src=None, spec=None):
+    def forward(ctx, x, w, b, res, bn, relu, src=None, spec=None, cstat=None):
         C = x.shape[1]
         M = x.numel() // C
         H, W = x.shape[2], x.shape[3]
         training = bn.training
         y = torch.empty_like(x, memory_format=torch.channels_last)
         save = torch.empty(2 * C, dtype=F32, device=x.device)
-        K.bn_fwd(x, res, y, _ws(bn, C, x.device), bn.running_mean, bn.running_var, w, b, M, C, float(bn.eps), relu,
-                 training, save, float(bn.momentum), bn.num_batches_tracked, src=src, spec=spec, H=H, W=W)
+        if cstat is not None:  # statistics from the producing conv's epilogue: no statistics pass over x
+            K.bn_fwd_tiles(x, res, y, cstat[0], cstat[1], cstat[2], bn.running_mean, bn.running_var, w, b, M, C,
+                           float(bn.eps), relu, save, float(bn.momentum), bn.num_batches_tracked)
+        else:
+            K.bn_fwd(x, res, y, _ws(bn, C, x.device), bn.running_mean, bn.running_var, w, b, M, C, float(bn.eps),
+                     relu, training, save, float(bn.momentum), bn.num_batches_tracked, src=src, spec=spec, H=H, W=W)
         ctx.save_for_backward(x, y if relu else None, save, w)
         ctx.cfg = (M, C, training, res is not None, H, W)
         ctx.bn = bn
@@ -78,7 +82,7 @@ class BNActFn(Function):
     @staticmethod
     def backward(ctx, dy):
         if dy is None:
-            return None, None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None, None
         from .hip_ops import _done, _grad_slot
         x, y, save, w = ctx.saved_tensors
         M, C, training, has_res, H, W = ctx.cfg
@@ -93,7 +97,7 @@ class BNActFn(Function):
         K.bn_bwd(dy, y, x, save, w, _ws(bn, C, x.device), coef, M, C, training, dx, dres, dw, db, src=src, spec=spec,
                  H=H, W=W)
         _done(bn.weight, bn.bias)
-        return dx, None, None, dres, None, None, None, None
+        return dx, None, None, dres, None, None, None, None, None
 
 
 def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res: Optional[torch.Tensor] = None,
@@ -102,7 +106,11 @@ def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res: Optional[torch.Tensor
     with ``x'[index] = src[index]`` (an interchange splice of the producing conv's hook, read in place by the
     kernels; the spliced elements get no gradient).  None when the splice's index is not expressible."""
     if splice is None:
-        return BNActFn.apply(x, bn.weight, bn.bias, res, bn, relu)
+        st = getattr(x, "_iit_cstat", None)
+        if st is not None and not (bn.training and x.dtype == BF16 and st[3] == x._version
+                                   and st[1] * st[2] * x.shape[1] == x.numel()):
+            st = None  # (eval mode, or the activation was modified in place after its conv)
+        return BNActFn.apply(x, bn.weight, bn.bias, res, bn, relu, None, None, st)
     from .splice import patch_spec
     index, src = splice
     src = src.to(device=x.device, dtype=x.dtype)

@@ -28,6 +28,25 @@ from . import hip_kernels as K
 BF16 = torch.bfloat16
 CL = torch.channels_last
 POLICY = os.environ.get("IIT_CONV_HIP", "auto")
+# the forward kernel's epilogue also writes per-tile column statistics of its output when the consumer is a training
+# BatchNorm (set around the conv by models/resnet.py), which then skips its statistics pass (ops/bn.py);
+# IIT_BN_CONV_STATS=0 keeps the BatchNorm's own pass
+CONV_STATS = os.environ.get("IIT_BN_CONV_STATS", "1") != "0"
+_WANT_STATS = [False]
+
+
+class stats_for_bn:
+    """Context: convolutions issued inside feed a training-mode BatchNorm (their outputs carry ``_iit_cstat``)."""
+
+    def __init__(self, on: bool):
+        self.on = bool(on) and CONV_STATS
+
+    def __enter__(self):
+        self.prev = _WANT_STATS[0]
+        _WANT_STATS[0] = self.on
+
+    def __exit__(self, *exc):
+        _WANT_STATS[0] = self.prev
 # (pass, N, H, W, Cin, Cout) -> (choice: (tile, splits) | None = the library, {candidate: us})
 DECISIONS: Dict[Tuple, Tuple[Optional[Tuple[int, int]], Dict[str, float]]] = {}
 
@@ -70,14 +89,26 @@ def _flip_weight(w: torch.Tensor) -> torch.Tensor:
     return w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
 
 
+def _name(tile: int, splits: int) -> str:
+    return f"hip{tile}" + (f"k{splits}" if splits > 1 else "")
+
+
+def _tile_splits(N, H, W, Cin, Cout):
+    """(tile, K-splits) candidates of the forward / input-gradient kernel: every tile, unsplit and split into 2..9
+    equal K ranges (the reduction split: more workgroups for the few-tile deep layers, e.g. layer4's 2304 x 512
+    output over K = 4608)."""
+    return [(t, sp) for t in range(K.conv3x3_tiles()) for sp in (1, 2, 3, 4, 6, 8, 9)
+            if K.conv3x3_ok(N, H, W, Cin, Cout, t, sp)]
+
+
 def _fwd_choice(x, w):
     N, Cin, H, W = x.shape
     Cout = w.shape[0]
     if ("fwd", N, H, W, Cin, Cout) in DECISIONS:
         return DECISIONS["fwd", N, H, W, Cin, Cout][0]
     y = torch.empty(N, Cout, H, W, dtype=BF16, device=x.device, memory_format=CL)
-    cands = {f"hip{t}": ((t, 1), lambda t=t: K.conv3x3(x, w, y, N, H, W, Cin, Cout, False, t))
-             for t in range(K.conv3x3_tiles()) if K.conv3x3_ok(N, H, W, Cin, Cout, t)}
+    cands = {_name(t, sp): ((t, sp), lambda t=t, sp=sp: K.conv3x3(x, w, y, N, H, W, Cin, Cout, False, t, sp))
+             for t, sp in _tile_splits(N, H, W, Cin, Cout)}
     cands["lib"] = (None, lambda: F.conv2d(x, w, None, 1, 1))
     return _decide(("fwd", N, H, W, Cin, Cout), cands)
 
@@ -88,8 +119,8 @@ def _dgrad_choice(dy, wf, x_shape):
     if ("dgrad", N, H, W, Cin, Cout) in DECISIONS:
         return DECISIONS["dgrad", N, H, W, Cin, Cout][0]
     dx = torch.empty(N, Cin, H, W, dtype=BF16, device=dy.device, memory_format=CL)
-    cands = {f"hip{t}": ((t, 1), lambda t=t: K.conv3x3(dy, wf, dx, N, H, W, Cout, Cin, True, t))
-             for t in range(K.conv3x3_tiles()) if K.conv3x3_ok(N, H, W, Cout, Cin, t)}
+    cands = {_name(t, sp): ((t, sp), lambda t=t, sp=sp: K.conv3x3(dy, wf, dx, N, H, W, Cout, Cin, True, t, sp))
+             for t, sp in _tile_splits(N, H, W, Cout, Cin)}
     w = wf.permute(1, 0, 2, 3)
     cands["lib"] = (None, lambda: torch.nn.grad.conv2d_input(x_shape, w, dy, 1, 1))
     return _decide(("dgrad", N, H, W, Cin, Cout), cands)
@@ -118,22 +149,30 @@ class Conv3x3Fn(Function):
     for the shape; the weight gradient lands in W's fp32 arena slot (stored when the slot is claimable, else added)."""
 
     @staticmethod
-    def forward(ctx, x, W, flat):
+    def forward(ctx, x, W, flat, want_stats=False):
         w = flat.shadow_view(W)
         N, Cin, H, Wd = x.shape
         Cout = w.shape[0]
         ch = _fwd_choice(x, w)
+        cstat = None
         if ch is None:
             y = F.conv2d(x, w, None, 1, 1)
         else:
             y = torch.empty(N, Cout, H, Wd, dtype=BF16, device=x.device, memory_format=CL)
-            K.conv3x3(x, w, y, N, H, Wd, Cin, Cout, False, ch[0])
+            if want_stats:  # per-tile column statistics for the consuming BatchNorm (3 x Cout x T fp32)
+                cstat = torch.empty(3 * Cout * (N * H * Wd // K.conv3x3_rows(ch[0])), dtype=torch.float32,
+                                    device=x.device)
+            K.conv3x3(x, w, y, N, H, Wd, Cin, Cout, False, ch[0], ch[1], cstat=cstat)
         ctx.save_for_backward(x)
         ctx.W, ctx.flat = W, flat
-        return y
+        ctx.stat_rows = K.conv3x3_rows(ch[0]) if cstat is not None else 0
+        if cstat is None:
+            cstat = torch.empty(0, dtype=torch.float32, device=x.device)
+        ctx.mark_non_differentiable(cstat)
+        return y, cstat
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, _dstat=None):
         from ..engine import grad_hooks
         (x,) = ctx.saved_tensors
         W, flat = ctx.W, ctx.flat
@@ -149,7 +188,7 @@ class Conv3x3Fn(Function):
                 dx = torch.nn.grad.conv2d_input(x.shape, w, dy, 1, 1)
             else:
                 dx = torch.empty(N, Cin, H, Wd, dtype=BF16, device=x.device, memory_format=CL)
-                K.conv3x3(dy, wf, dx, N, H, Wd, Cout, Cin, True, ch[0])
+                K.conv3x3(dy, wf, dx, N, H, Wd, Cout, Cin, True, ch[0], ch[1])
         if W.requires_grad:
             ch = _wgrad_choice(dy, x, w)
             if ch is None:
@@ -163,15 +202,22 @@ class Conv3x3Fn(Function):
                     flat.bind_zero(W)
                 K.conv3x3_wgrad(dy, x, W.grad, N, H, Wd, Cin, Cout, not store, ch[0], ch[1])
                 grad_hooks.notify(W)
-        return dx, None, None
+        return dx, None, None, None
 
 
 def conv3x3(x: torch.Tensor, W: torch.Tensor, flat) -> torch.Tensor:
-    """The convolution of ``x`` with the arena weight ``W`` (bf16 mirror) on the measured-faster implementation."""
+    """The convolution of ``x`` with the arena weight ``W`` (bf16 mirror) on the measured-faster implementation.
+    Inside :class:`stats_for_bn`, an output of the repo's kernel carries ``_iit_cstat`` = (records, T, rows per tile,
+    the output's version): its BatchNorm statistics, valid while the tensor is not modified in place."""
     x = x.to(BF16)
     if not W.is_contiguous(memory_format=CL):
         return F.conv2d(x, flat.shadow_view(W), None, 1, 1)
-    return Conv3x3Fn.apply(x, W, flat)
+    y, cstat = Conv3x3Fn.apply(x, W, flat, _WANT_STATS[0])
+    if cstat.numel():
+        N, C, H, Wd = y.shape
+        rows = N * H * Wd // (cstat.numel() // (3 * C))
+        y._iit_cstat = (cstat, N * H * Wd // rows, rows, y._version)
+    return y
 
 
 def report() -> str:

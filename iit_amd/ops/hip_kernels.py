@@ -104,8 +104,12 @@ _SIGS = {
     "iit_gemm_glds_set_group_m": [c_int],
     "iit_ioi_hl_label": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "iit_conv3x3_tiles": [],
-    "iit_conv3x3_ok": [c_long, c_int, c_int, c_int, c_int, c_int],
-    "iit_conv3x3": [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "iit_conv3x3_ok": [c_long, c_int, c_int, c_int, c_int, c_int, c_int],
+    "iit_conv3x3": [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                     c_void_p, c_void_p],
+    "iit_conv3x3_rows": [c_int],
+    "iit_bn_fwd_tiles": [c_void_p] * 4 + [c_int, c_int] + [c_void_p] * 4 + [c_long, c_int, c_float, c_int, c_void_p,
+                                                                           c_float, c_void_p, c_void_p],
     "iit_conv3x3_wgrad_tiles": [],
     "iit_conv3x3_wgrad_ok": [c_long, c_int, c_int, c_int, c_int, c_int, c_int],
     "iit_conv3x3_wgrad": [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
@@ -663,18 +667,34 @@ def conv3x3_tiles() -> int:
     return int(lib().iit_conv3x3_tiles())
 
 
-def conv3x3_ok(N: int, H: int, W: int, Cin: int, Cout: int, tile: int) -> bool:
-    return bool(lib().iit_conv3x3_ok(N, H, W, Cin, Cout, tile))
+def conv3x3_ok(N: int, H: int, W: int, Cin: int, Cout: int, tile: int, splits: int = 1) -> bool:
+    return bool(lib().iit_conv3x3_ok(N, H, W, Cin, Cout, tile, splits))
 
 
-def conv3x3(x, w, y, N: int, H: int, W: int, Cin: int, Cout: int, flip: bool = False, tile: int = 0):
+CONV_TILES = {0: (128, 64), 1: (128, 128), 2: (64, 64), 3: (128, 128), 4: (64, 128), 5: (128, 64)}
+
+
+def conv3x3_rows(tile: int) -> int:
+    """Output rows per tile (BM) of forward tile ``tile``: the row-tile size of the ``cstat`` records."""
+    return CONV_TILES[tile][0]
+
+
+def conv3x3(x, w, y, N: int, H: int, W: int, Cin: int, Cout: int, flip: bool = False, tile: int = 0,
+            splits: int = 1, cstat=None):
     """``y`` [N,H,W,Cout] = 3x3 / stride-1 / pad-1 convolution of the NHWC bf16 ``x`` [N,H,W,Cin] with ``w``
-    [Cout,3,3,Cin] (``flip``: negated tap offsets -- the input gradient, with ``w`` re-laid [Cin,3,3,Cout])."""
+    [Cout,3,3,Cin] (``flip``: negated tap offsets -- the input gradient, with ``w`` re-laid [Cin,3,3,Cout]);
+    ``splits`` > 1: deterministic reduction split over the 9 Cin reduction.  ``cstat`` (fp32, >= 3 Cout T floats,
+    T = N H W / :func:`conv3x3_rows`): per-tile column statistics of ``y`` for :func:`bn_fwd_tiles`."""
+    ws = cnt = None
+    if splits > 1:
+        ws, cnt = split_workspace(N * H * W, Cout, CONV_TILES[tile], splits, x.device)
     if CHECK_BOUNDS:
         assert x.numel() >= N * H * W * Cin and y.numel() >= N * H * W * Cout and w.numel() >= 9 * Cin * Cout
         assert x.dtype == w.dtype == y.dtype == torch.bfloat16
+        if cstat is not None:
+            assert cstat.dtype == torch.float32 and cstat.numel() >= 3 * Cout * (N * H * W // conv3x3_rows(tile))
     _check(lib().iit_conv3x3(_p(x), _p(w), _p(y), _p(zero_page(x.device)), N, H, W, Cin, Cout, int(flip), tile,
-                             _stream()), "conv3x3")
+                             splits, _p(ws), _p(cnt), _p(cstat), _stream()), "conv3x3")
 
 
 CONV_WG_TILES = {0: (64, 64), 1: (128, 64), 2: (128, 128), 3: (64, 128)}
@@ -734,6 +754,19 @@ def bn_fwd(x, res, y, ws, rmean, rvar, w, b, M: int, C: int, eps: float, relu: b
     _check(lib().iit_bn_fwd(_p(x), _p(res), _p(y), _p(ws), _p(rmean), _p(rvar), _p(w), _p(b), M, C, eps, int(relu),
                             int(training), _p(save), momentum, _p(nbt), _p(src), None if spec is None else spec.ptr,
                             H, W, int(x.dtype == torch.float32), int(bn_two_level()), _stream()), "bn_fwd")
+
+
+def bn_fwd_tiles(x, res, y, cstat, T: int, R: int, rmean, rvar, w, b, M: int, C: int, eps: float, relu: bool, save,
+                 momentum: float, nbt):
+    """Training forward of :func:`bn_fwd` on a bf16 ``x`` whose statistics its producing convolution's epilogue wrote
+    (``cstat``: T row tiles of R rows, :func:`conv3x3`): a per-channel combine of the tile records, then the apply
+    pass -- no statistics pass over ``x``."""
+    if CHECK_BOUNDS:
+        for t in (x, y) + ((res,) if res is not None else ()):
+            assert _avail(t) >= M * C and t.dtype == torch.bfloat16, "bn_fwd_tiles: activation smaller than M x C"
+        assert T * R == M and cstat.numel() >= 3 * C * T and save.numel() >= 2 * C
+    _check(lib().iit_bn_fwd_tiles(_p(x), _p(res), _p(y), _p(cstat), T, R, _p(rmean), _p(rvar), _p(w), _p(b), M, C,
+                                  eps, int(relu), _p(save), momentum, _p(nbt), _stream()), "bn_fwd_tiles")
 
 
 def bn_bwd(dy, y, x, save, w, ws, coef, M: int, C: int, training: bool, dx, dres, dw, db, src=None, spec=None,

@@ -19,7 +19,7 @@ SHAPES = [("layer1", 64, 64, 21), ("layer2", 128, 128, 11), ("layer3", 256, 256,
 def main():
     from iit_amd.ops import gemm_dispatch as gd
     from iit_amd.ops import hip_kernels as K
-    from iit_amd.ops.conv import _flip_weight
+    from iit_amd.ops.conv import _flip_weight, _name, _tile_splits
     CL = torch.channels_last
     N = int(os.environ.get("BATCH", "256"))
     for name, Cin, Cout, hw in SHAPES:
@@ -34,11 +34,10 @@ def main():
                "GFLOP": round(2 * N * hw * hw * Cout * 9 * Cin / 1e9, 2)}
         fwd = {"lib": lambda: F.conv2d(x, w, None, 1, 1)}
         bwd = {"lib": lambda: torch.nn.grad.conv2d_input(x.shape, w, dy, 1, 1)}
-        for t in range(K.conv3x3_tiles()):
-            if K.conv3x3_ok(N, hw, hw, Cin, Cout, t):
-                fwd[f"hip{t}"] = lambda t=t: K.conv3x3(x, w, y, N, hw, hw, Cin, Cout, False, t)
-            if K.conv3x3_ok(N, hw, hw, Cout, Cin, t):
-                bwd[f"hip{t}"] = lambda t=t: K.conv3x3(dy, wf, dx, N, hw, hw, Cout, Cin, True, t)
+        for t, sp in _tile_splits(N, hw, hw, Cin, Cout):
+            fwd[_name(t, sp)] = lambda t=t, sp=sp: K.conv3x3(x, w, y, N, hw, hw, Cin, Cout, False, t, sp)
+        for t, sp in _tile_splits(N, hw, hw, Cout, Cin):
+            bwd[_name(t, sp)] = lambda t=t, sp=sp: K.conv3x3(dy, wf, dx, N, hw, hw, Cout, Cin, True, t, sp)
         dwt = torch.empty(Cout, Cin, 3, 3, device="cuda", dtype=torch.float32).contiguous(memory_format=CL)
         wgr = {"lib": lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0),
                                                                    1, (False, True, False))}

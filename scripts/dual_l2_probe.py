@@ -58,13 +58,14 @@ def record_pairs(pair, loss_fn, opt, it, gd, K):
                     seen[key] = (dict(x), dict(w))
         return res
 
-    gd.gemm_pair = wrap
+    from iit_amd.ops import hip_ops  # the callers' binding (``from .gemm_dispatch import gemm_pair``)
+    hip_ops.gemm_pair = wrap
     try:
         base, abl = next(it)
         pair.run_train_step(base, abl, loss_fn, opt)
         torch.cuda.synchronize()
     finally:
-        gd.gemm_pair = orig
+        hip_ops.gemm_pair = orig
     return seen, order
 
 

@@ -16,13 +16,13 @@ for p in 1 2; do
 done
 cat $O/time.log | tail -12
 cat $O/sum1.txt $O/sum2.txt
-# MQNLI: the library / cast sites, then library-free vs default (twice, interleaved)
+# MQNLI: op sites, then the traced breakdown and the untraced step with the library-free shipped table
 timeout -k 10 300 python3 -u scripts/op_sites.py --family mqnli-bert-base > $O/mq_sites.txt 2>&1 || { echo sites failed; tail -20 $O/mq_sites.txt; exit 1; }
 head -45 $O/mq_sites.txt
+timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/mqprof -o mq -- python3 scripts/bench_families.py --family mqnli-bert-base --steps 12 --warmup 3 > $O/mq_prof.log 2>&1 || { tail -20 $O/mq_prof.log; exit 1; }
+f=$(find $O/mqprof -name "*kernel_trace.csv" | head -n 1)
+[ -n "$f" ] && python3 scripts/step_breakdown.py "$f" --steps 8 --top 40 --gaps 5 > $O/mqnli_breakdown.txt && head -50 $O/mqnli_breakdown.txt; rm -f "$f"
 for r in 1 2; do
-  timeout -k 10 300 env IIT_GEMM_TRACE=1 python3 -u scripts/bench_families.py --family mqnli-bert-base --steps 30 --warmup 5 > $O/mq_def$r.log 2>&1 || { echo mq failed; tail -20 $O/mq_def$r.log; exit 1; }
-  timeout -k 10 300 env IIT_GEMM_TRACE=1 IIT_GEMM_EXCLUDE='blas.*' python3 -u scripts/bench_families.py --family mqnli-bert-base --steps 30 --warmup 5 > $O/mq_nob$r.log 2>&1 || { echo mq nob failed; tail -20 $O/mq_nob$r.log; exit 1; }
-  echo "default: $(grep -E '^\{' $O/mq_def$r.log | cut -c1-200)"
-  echo "no blas: $(grep -E '^\{' $O/mq_nob$r.log | cut -c1-200)"
+  timeout -k 10 300 python3 -u scripts/bench_families.py --family mqnli-bert-base --steps 30 --warmup 5 > $O/mq$r.log 2>&1 || { echo mq failed; tail -20 $O/mq$r.log; exit 1; }
+  echo "mqnli: $(grep -E '^\{' $O/mq$r.log | cut -c1-200)"
 done
-grep -E "^\[gemm\].*blas" $O/mq_def1.log | sort | uniq -c | head -20 || true

@@ -1,54 +1,74 @@
-"""Which lines of the engine issue the library / cast / elementwise ops of a family's training step: eager steps
-(no graphs) under ``torch.profiler`` with stacks, ATen ops grouped by their innermost ``iit_amd`` frame.
+"""Which lines of the engine issue the ATen ops of a family's training step (library GEMMs, casts, copies, fills,
+adds): eager steps (no graphs) under a TorchDispatchMode that attributes every op to its innermost ``iit_amd`` frame
+(the profiler's stacks are empty on this ROCm build), with call counts and output bytes per step.
 
-    python scripts/op_sites.py --family mqnli-bert-base [--ops copy_,_to_copy,add,mm,addmm,linear]
+    python scripts/op_sites.py --family mqnli-bert-base [--ops mm,addmm,_to_copy,copy_,add,fill_]
 """
 import argparse
 import collections
 import os
 import sys
+import traceback
 
 import torch
+from torch.utils._python_dispatch import TorchDispatchMode
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 
+class Sites(TorchDispatchMode):
+    def __init__(self, wanted):
+        super().__init__()
+        self.wanted = wanted
+        self.rows = collections.defaultdict(lambda: [0, 0])
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        out = func(*args, **(kwargs or {}))
+        name = func.overloadpacket.__name__
+        if name in self.wanted:
+            site = "(no iit_amd frame)"
+            for fr in reversed(traceback.extract_stack()[:-1]):
+                if "iit_amd" in fr.filename:
+                    site = f"{os.path.relpath(fr.filename, ROOT)}:{fr.lineno} {fr.name}"
+                    break
+            nbytes = sum(t.numel() * t.element_size() for t in (out if isinstance(out, (tuple, list)) else [out])
+                         if isinstance(t, torch.Tensor))
+            r = self.rows[(name, site)]
+            r[0] += 1
+            r[1] += nbytes
+        return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--family", default="mqnli-bert-base")
-    ap.add_argument("--ops", default="copy_,_to_copy,add,add_,mm,addmm,linear,matmul,bmm,cat,index_select,fill_,zero_")
+    ap.add_argument("--ops", default="mm,addmm,bmm,matmul,linear,_to_copy,copy_,add,add_,fill_,zero_,cat,index_select,"
+                                     "clone,mul,sum")
     ap.add_argument("--steps", type=int, default=2)
     a = ap.parse_args()
     import bench_families as bf
     args = bf.parse(["--family", a.family, "--graphs", "0"])
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(0)
     pair, opt, it, step_fn, _, _, _ = bf.setup(args, dev)
     for _ in range(3):
         base, abl = next(it)
         step_fn(base, abl, pair.loss_fn, opt)
-    torch.cuda.synchronize()
-    wanted = {f"aten::{o}" for o in a.ops.split(",")}
-    from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    mode = Sites(set(a.ops.split(",")))
+    with mode:
         for _ in range(a.steps):
             base, abl = next(it)
             step_fn(base, abl, pair.loss_fn, opt)
+    if dev.type == "cuda":
         torch.cuda.synchronize()
-    sites = collections.defaultdict(lambda: [0, 0.0])
-    for ev in prof.events():
-        if ev.name not in wanted:
-            continue
-        frames = [f for f in (ev.stack or []) if "iit_amd" in f]
-        site = frames[0] if frames else "(no iit_amd frame)"
-        s = sites[(ev.name, site)]
-        s[0] += 1
-        s[1] += ev.device_time_total if hasattr(ev, "device_time_total") else ev.cuda_time_total
-    print(f"{'op':22s} {'calls/step':>10s} {'dev us/step':>11s}  site")
-    for (name, site), (n, t) in sorted(sites.items(), key=lambda kv: -kv[1][1])[:40]:
-        print(f"{name:22s} {n / a.steps:10.1f} {t / a.steps:11.1f}  {site}")
+    print(f"{'op':14s} {'calls/step':>10s} {'MB out/step':>11s}  site")
+    for (name, site), (n, b) in sorted(mode.rows.items(), key=lambda kv: -kv[1][1])[:50]:
+        print(f"{name:14s} {n / a.steps:10.1f} {b / a.steps / 1e6:11.2f}  {site}")
 
 
 if __name__ == "__main__":

@@ -1,6 +1,6 @@
 """The implicit-GEMM NHWC 3x3 convolution (csrc/conv_nhwc.hip, iit_amd/ops/conv.py) against an fp32 PyTorch
 convolution of the same bf16 inputs: forward on every kernel tile, the input gradient (negated taps on the re-laid
-weight) and the autograd op (library weight gradient)."""
+weight), with and without the reduction split-K, the weight-gradient kernel and the autograd op."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -25,19 +25,26 @@ def test_conv3x3_matches_fp32(N, Cin, Cout, hw):
     ref = F.conv2d(x.float(), w.float(), None, 1, 1)
     dy = torch.randn_like(ref).to(torch.bfloat16).contiguous(memory_format=CL)
     dx_ref = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), 1, 1)
-    ran = 0
+    ran = split = 0
     for t in range(K.conv3x3_tiles()):
-        if not K.conv3x3_ok(N, hw, hw, Cin, Cout, t):
-            continue
-        ran += 1
-        y = torch.full((N, Cout, hw, hw), float("nan"), device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
-        K.conv3x3(x, w, y, N, hw, hw, Cin, Cout, False, t)
-        assert rel(y, ref) < 8e-3, t
-        if K.conv3x3_ok(N, hw, hw, Cout, Cin, t):
-            dx = torch.full_like(x, float("nan"))
-            K.conv3x3(dy, _flip_weight(w), dx, N, hw, hw, Cout, Cin, True, t)
-            assert rel(dx, dx_ref) < 8e-3, t
-    assert ran > 0
+        for sp in (1, 2, 3, 4, 8):  # unsplit and the reduction split-K (fixed-order sum of fp32 partial tiles)
+            if not K.conv3x3_ok(N, hw, hw, Cin, Cout, t, sp):
+                continue
+            ran += 1
+            split += sp > 1
+            y = torch.full((N, Cout, hw, hw), float("nan"), device=dev, dtype=torch.bfloat16).contiguous(
+                memory_format=CL)
+            K.conv3x3(x, w, y, N, hw, hw, Cin, Cout, False, t, sp)
+            assert rel(y, ref) < 8e-3, (t, sp)
+            if sp > 1:  # twice: the tickets were re-armed by the first launch
+                y2 = torch.full_like(y, float("nan"))
+                K.conv3x3(x, w, y2, N, hw, hw, Cin, Cout, False, t, sp)
+                assert torch.equal(y, y2), (t, sp)
+            if K.conv3x3_ok(N, hw, hw, Cout, Cin, t, sp):
+                dx = torch.full_like(x, float("nan"))
+                K.conv3x3(dy, _flip_weight(w), dx, N, hw, hw, Cout, Cin, True, t, sp)
+                assert rel(dx, dx_ref) < 8e-3, (t, sp)
+    assert ran > 0 and split > 0
 
 
 @pytest.mark.parametrize("N,Cin,Cout,hw", [(64, 64, 64, 21), (64, 128, 128, 11), (64, 256, 256, 6),
@@ -87,3 +94,58 @@ def test_conv3x3_autograd_arena_weight(monkeypatch):
     yr.backward(g.float())
     assert rel(y, yr) < 8e-3
     assert rel(x.grad, xr.grad) < 1e-2 and rel(W.grad, wr.grad) < 1e-3
+
+
+@pytest.mark.parametrize("N,C,hw,tile,splits,offset", [(128, 64, 21, 0, 1, 0.0), (64, 128, 11, 3, 2, 0.0),
+                                                       (128, 256, 6, 4, 1, 40.0), (128, 512, 3, 2, 4, 0.0)])
+def test_conv_epilogue_bn_statistics(N, C, hw, tile, splits, offset):
+    """BatchNorm statistics from the conv epilogue (per-tile column records, gemm_glds_body.h E_BF16_CS, combined
+    around the batch's first row by bn_tile_finalize_kernel) against the BatchNorm's own statistics pass on the same
+    bf16 output: same normalised output, running statistics and num_batches_tracked; ``offset`` puts the channel means
+    far from zero (the pivot keeps the variance from cancelling), checked against float64."""
+    from iit_amd.ops import hip_kernels as K
+    torch.manual_seed(C + hw)
+    if not K.conv3x3_ok(N, hw, hw, C, C, tile, splits):
+        pytest.skip("tile does not cover the shape")
+    x = torch.randn(N, C, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(C, C, 3, 3, device=dev) / (3 * C ** 0.5)).to(torch.bfloat16).contiguous(memory_format=CL)
+    y = torch.empty(N, C, hw, hw, device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    T = N * hw * hw // K.conv3x3_rows(tile)
+    cstat = torch.full((3 * C * T,), float("nan"), device=dev)
+    K.conv3x3(x, w, y, N, hw, hw, C, C, False, tile, splits, cstat=cstat)
+    y0 = torch.empty_like(y)
+    K.conv3x3(x, w, y0, N, hw, hw, C, C, False, tile, splits)
+    assert torch.equal(y, y0)  # the statistics do not change the output
+    if offset:
+        y = (y.float() + offset).to(torch.bfloat16).contiguous(memory_format=CL)
+        cstat2 = torch.full_like(cstat, float("nan"))  # re-derive the records of the shifted output from its rows
+        v = y.permute(0, 2, 3, 1).reshape(T, -1, C).float()
+        piv = v[:, 0, :]
+        d = v - piv[:, None, :]
+        cstat2.view(3, C, T)[0] = piv.t()
+        cstat2.view(3, C, T)[1] = d.sum(1).t()
+        cstat2.view(3, C, T)[2] = (d * d).sum(1).t()
+        cstat = cstat2
+    M = N * hw * hw
+    gw = torch.rand(C, device=dev) + 0.5
+    gb = torch.randn(C, device=dev)
+    outs = []
+    for use_tiles in (True, False):
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        nbt = torch.zeros((), dtype=torch.long, device=dev)
+        out = torch.empty_like(y)
+        save = torch.empty(2 * C, device=dev)
+        if use_tiles:
+            K.bn_fwd_tiles(y, None, out, cstat, T, M // T, rm, rv, gw, gb, M, C, 1e-5, True, save, 0.1, nbt)
+        else:
+            ws = torch.zeros(K.bn_ws_floats(C), device=dev)
+            K.bn_fwd(y, None, out, ws, rm, rv, gw, gb, M, C, 1e-5, True, True, save, 0.1, nbt)
+        outs.append((out, rm, rv, nbt, save))
+    (o1, rm1, rv1, n1, s1), (o2, rm2, rv2, n2, s2) = outs
+    assert int(n1) == int(n2) == 1
+    assert rel(o1, o2) < 4e-3
+    yd = y.double().permute(0, 2, 3, 1).reshape(-1, C)
+    mean, var = yd.mean(0), yd.var(0, unbiased=False)
+    assert float(((s1[:C].double() - mean).abs() / (var.sqrt() + 1e-6)).max()) < 1e-3
+    assert float(((s1[C:].double() - (var + 1e-5).rsqrt()).abs() / (var + 1e-5).rsqrt()).max()) < 2e-3
+    assert rel(rm1, rm2) < 1e-3 and rel(rv1, rv2) < 1e-3
