@@ -47,23 +47,29 @@ def main():
     ap.add_argument("--ops", default="mm,addmm,bmm,matmul,linear,_to_copy,copy_,add,add_,fill_,zero_,cat,index_select,"
                                      "clone,mul,sum")
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--dtype", default="fp32", help="pvr-resnet18: bf16 = channels-last bf16 autocast (as the bench)")
     a = ap.parse_args()
+    import contextlib
     import bench_families as bf
-    args = bf.parse(["--family", a.family, "--graphs", "0"])
+    args = bf.parse(["--family", a.family, "--graphs", "0", "--dtype", a.dtype])
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(0)
     pair, opt, it, step_fn, _, _, _ = bf.setup(args, dev)
+    amp = (lambda: torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False)) \
+        if a.dtype == "bf16" and dev.type == "cuda" else contextlib.nullcontext
     for _ in range(3):
         base, abl = next(it)
-        step_fn(base, abl, pair.loss_fn, opt)
+        with amp():
+            step_fn(base, abl, pair.loss_fn, opt)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     mode = Sites(set(a.ops.split(",")))
     with mode:
         for _ in range(a.steps):
             base, abl = next(it)
-            step_fn(base, abl, pair.loss_fn, opt)
+            with amp():
+                step_fn(base, abl, pair.loss_fn, opt)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     print(f"{'op':14s} {'calls/step':>10s} {'MB out/step':>11s}  site")
