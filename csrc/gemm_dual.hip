@@ -22,12 +22,51 @@ struct Cfg {
   static constexpr int SMEM = GldsSmem<BM_, BN_, NS_, NW_, 64, OCC_>::BYTES;
 };
 
+// Cold-operand prefetch (profiles/dual_l2_hypothesis_r6.txt: inside the step a pair runs 7-19 % slower than back to
+// back because its forward-saved activation and its weight come from HBM, not the Infinity Cache): the first
+// ``pf.wgs`` workgroups of the launch read the NEXT pair's cold operands (up to two ranges) once, one 4-B load per
+// 64-B granule, so they are cache-resident when that pair starts.  They run beside the tiles, whose operand intake is
+// L2 -> LDS bound and leaves HBM bandwidth unused.  Loads only: nothing is written.
+struct Prefetch {
+  const char* p[2];
+  long bytes[2];
+  int wgs;
+};
+
+__device__ __forceinline__ void prefetch_part(const Prefetch& pf, int part) {
+  unsigned acc = 0u;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (!pf.p[r] || pf.bytes[r] <= 0) continue;
+    const long gran = (pf.bytes[r] + 63) / 64;
+    const long per = (gran + pf.wgs - 1) / pf.wgs;
+    const long g0 = (long)part * per;
+    const long g1 = g0 + per < gran ? g0 + per : gran;
+    const char* base = pf.p[r];
+    for (long g = g0 + threadIdx.x; g < g1; g += (long)blockDim.x * 8) {
+      unsigned v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const long gg = g + (long)u * blockDim.x;
+        v[u] = gg < g1 ? *(const unsigned*)(base + gg * 64) : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc ^= v[u];
+    }
+  }
+  asm volatile("" ::"v"(acc));  // keep the loads
+}
+
 template <class TW, int EW, class TX, int EX>
 __global__ __launch_bounds__(TW::NW * 64, TW::OCC) void gemm_dual_kernel(G2Args pw, G2Args px, int w_tiles,
-                                                                         int w_splits, int x_tiles) {
+                                                                         int w_splits, int x_tiles, Prefetch pf) {
   static_assert(TW::NW == TX::NW && TW::OCC == TX::OCC, "one launch geometry");
   __shared__ __attribute__((aligned(16))) char smem[TW::SMEM > TX::SMEM ? TW::SMEM : TX::SMEM];  // ONE LDS object
-  const int b = blockIdx.x;
+  if ((int)blockIdx.x < pf.wgs) {
+    prefetch_part(pf, blockIdx.x);
+    return;
+  }
+  const int b = blockIdx.x - pf.wgs;  // (pf.wgs is a multiple of 8: the tiles keep their XCD placement)
   const int nw = w_tiles * w_splits;
   if (b < nw) {
     gemm_glds_body<TW::BM, TW::BN, TW::NS, true, true, EW, TW::NW, 64, TW::OCC>(pw, b % w_tiles, w_tiles,
@@ -60,51 +99,52 @@ __host__ __device__ constexpr int w_family(int t) { return t >= 7 ? 2 : (t >= 5 
 __host__ __device__ constexpr int x_family(int t) { return t >= 7 ? 2 : (t >= 4 ? 1 : 0); }
 
 template <class TW, int EW, class TX, int EX>
-hipError_t launch2(const G2Args& w, const G2Args& x, int w_splits, hipStream_t s) {
+hipError_t launch2(const G2Args& w, const G2Args& x, int w_splits, const Prefetch& pf, hipStream_t s) {
   const int wt = (w.M / TW::BM) * (w.N / TW::BN), xt = (x.M / TX::BM) * (x.N / TX::BN);
-  hipLaunchKernelGGL((gemm_dual_kernel<TW, EW, TX, EX>), dim3(wt * w_splits + xt), dim3(TW::NW * 64), 0, s, w, x,
-                     wt, w_splits, xt);
+  hipLaunchKernelGGL((gemm_dual_kernel<TW, EW, TX, EX>), dim3(pf.wgs + wt * w_splits + xt), dim3(TW::NW * 64), 0, s,
+                     w, x, wt, w_splits, xt, pf);
   return hipGetLastError();
 }
 
 template <class TW, int EW, int EX>
-hipError_t pick_x(const G2Args& w, const G2Args& x, int w_splits, int xtile, hipStream_t s) {
+hipError_t pick_x(const G2Args& w, const G2Args& x, int w_splits, int xtile, const Prefetch& pf, hipStream_t s) {
   if constexpr (TW::NW == 4 && TW::OCC == 1) {
     switch (xtile) {
-      case 7: return launch2<TW, EW, Cfg<128, 128, 4, 4, 1>, EX>(w, x, w_splits, s);
-      case 8: return launch2<TW, EW, Cfg<128, 192, 3, 4, 1>, EX>(w, x, w_splits, s);
+      case 7: return launch2<TW, EW, Cfg<128, 128, 4, 4, 1>, EX>(w, x, w_splits, pf, s);
+      case 8: return launch2<TW, EW, Cfg<128, 192, 3, 4, 1>, EX>(w, x, w_splits, pf, s);
       default: return hipErrorInvalidValue;
     }
   } else if constexpr (TW::NW == 4) {
     switch (xtile) {
-      case 0: return launch2<TW, EW, Cfg<128, 96, 2>, EX>(w, x, w_splits, s);
-      case 1: return launch2<TW, EW, Cfg<64, 96, 3>, EX>(w, x, w_splits, s);
-      case 2: return launch2<TW, EW, Cfg<128, 192, 2>, EX>(w, x, w_splits, s);
-      case 3: return launch2<TW, EW, Cfg<128, 128, 2>, EX>(w, x, w_splits, s);
+      case 0: return launch2<TW, EW, Cfg<128, 96, 2>, EX>(w, x, w_splits, pf, s);
+      case 1: return launch2<TW, EW, Cfg<64, 96, 3>, EX>(w, x, w_splits, pf, s);
+      case 2: return launch2<TW, EW, Cfg<128, 192, 2>, EX>(w, x, w_splits, pf, s);
+      case 3: return launch2<TW, EW, Cfg<128, 128, 2>, EX>(w, x, w_splits, pf, s);
       default: return hipErrorInvalidValue;
     }
   } else {
     switch (xtile) {
-      case 4: return launch2<TW, EW, Cfg<256, 192, 2, 8, 1>, EX>(w, x, w_splits, s);
-      case 5: return launch2<TW, EW, Cfg<256, 128, 2, 8, 1>, EX>(w, x, w_splits, s);
-      case 6: return launch2<TW, EW, Cfg<128, 128, 4, 8, 1>, EX>(w, x, w_splits, s);
+      case 4: return launch2<TW, EW, Cfg<256, 192, 2, 8, 1>, EX>(w, x, w_splits, pf, s);
+      case 5: return launch2<TW, EW, Cfg<256, 128, 2, 8, 1>, EX>(w, x, w_splits, pf, s);
+      case 6: return launch2<TW, EW, Cfg<128, 128, 4, 8, 1>, EX>(w, x, w_splits, pf, s);
       default: return hipErrorInvalidValue;
     }
   }
 }
 
 template <int EW, int EX>
-hipError_t pick_w(const G2Args& w, const G2Args& x, int w_splits, int wtile, int xtile, hipStream_t s) {
+hipError_t pick_w(const G2Args& w, const G2Args& x, int w_splits, int wtile, int xtile, const Prefetch& pf,
+                  hipStream_t s) {
   switch (wtile) {
-    case 0: return pick_x<Cfg<128, 96, 2>, EW, EX>(w, x, w_splits, xtile, s);
-    case 1: return pick_x<Cfg<128, 128, 2>, EW, EX>(w, x, w_splits, xtile, s);
-    case 2: return pick_x<Cfg<96, 96, 3>, EW, EX>(w, x, w_splits, xtile, s);
-    case 3: return pick_x<Cfg<64, 96, 3>, EW, EX>(w, x, w_splits, xtile, s);
-    case 4: return pick_x<Cfg<64, 64, 4>, EW, EX>(w, x, w_splits, xtile, s);
-    case 5: return pick_x<Cfg<256, 128, 2, 8, 1>, EW, EX>(w, x, w_splits, xtile, s);
-    case 6: return pick_x<Cfg<128, 128, 4, 8, 1>, EW, EX>(w, x, w_splits, xtile, s);
-    case 7: return pick_x<Cfg<128, 128, 4, 4, 1>, EW, EX>(w, x, w_splits, xtile, s);
-    case 8: return pick_x<Cfg<128, 96, 4, 4, 1>, EW, EX>(w, x, w_splits, xtile, s);
+    case 0: return pick_x<Cfg<128, 96, 2>, EW, EX>(w, x, w_splits, xtile, pf, s);
+    case 1: return pick_x<Cfg<128, 128, 2>, EW, EX>(w, x, w_splits, xtile, pf, s);
+    case 2: return pick_x<Cfg<96, 96, 3>, EW, EX>(w, x, w_splits, xtile, pf, s);
+    case 3: return pick_x<Cfg<64, 96, 3>, EW, EX>(w, x, w_splits, xtile, pf, s);
+    case 4: return pick_x<Cfg<64, 64, 4>, EW, EX>(w, x, w_splits, xtile, pf, s);
+    case 5: return pick_x<Cfg<256, 128, 2, 8, 1>, EW, EX>(w, x, w_splits, xtile, pf, s);
+    case 6: return pick_x<Cfg<128, 128, 4, 8, 1>, EW, EX>(w, x, w_splits, xtile, pf, s);
+    case 7: return pick_x<Cfg<128, 128, 4, 4, 1>, EW, EX>(w, x, w_splits, xtile, pf, s);
+    case 8: return pick_x<Cfg<128, 96, 4, 4, 1>, EW, EX>(w, x, w_splits, xtile, pf, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -150,6 +190,7 @@ IIT_EXPORT int iit_gemm_dual(const void* wA, const void* wB, void* wC, long wlda
                              int wK, int wepi, int wtile, int wsplits, float* ws, int* counters, const void* xA,
                              const void* xB, void* xC, void* xC2, long xlda, long xldb, long xldc, long xldc2, int xM,
                              int xN, int xK, int xepi, int xtile, float* csum, float* bsum, float* gsq,
+                             const void* pf0, long pf0_bytes, const void* pf1, long pf1_bytes, int pf_wgs,
                              void* stream) {
   const int reduce = ws != nullptr;
   if (!iit_gemm_dual_ok(wA, wB, wC, wlda, wldb, wldc, wM, wN, wK, wepi, wtile, wsplits, reduce, xA, xB, xC, xC2, xlda,
@@ -170,10 +211,16 @@ IIT_EXPORT int iit_gemm_dual(const void* wA, const void* wB, void* wC, long wlda
   x.M = xM; x.N = xN; x.K = xK; x.k_per_split = xK;
   x.csum = xepi == E_DGELU ? csum : nullptr;
   w.group_m = x.group_m = g_dual_group_m;
+  // prefetch workgroups: a multiple of 8 (the tiles keep their blockIdx % 8 XCD placement), none without a range
+  Prefetch pf{{(const char*)pf0, (const char*)pf1}, {pf0 ? pf0_bytes : 0, pf1 ? pf1_bytes : 0}, 0};
+  if ((pf.bytes[0] > 0 || pf.bytes[1] > 0) && pf_wgs > 0) pf.wgs = ((pf_wgs + 7) / 8) * 8;
+  if (pf.wgs > 1024) pf.wgs = 1024;
   hipStream_t s = (hipStream_t)stream;
-  if (wepi == E_F32_STORE && xepi == E_BF16) return (int)pick_w<E_F32_STORE, E_BF16>(w, x, wsplits, wtile, xtile, s);
-  if (wepi == E_F32_STORE && xepi == E_DGELU) return (int)pick_w<E_F32_STORE, E_DGELU>(w, x, wsplits, wtile, xtile, s);
-  if (wepi == E_F32_ACC && xepi == E_BF16) return (int)pick_w<E_F32_ACC, E_BF16>(w, x, wsplits, wtile, xtile, s);
-  if (wepi == E_F32_ACC && xepi == E_DGELU) return (int)pick_w<E_F32_ACC, E_DGELU>(w, x, wsplits, wtile, xtile, s);
+  if (wepi == E_F32_STORE && xepi == E_BF16)
+    return (int)pick_w<E_F32_STORE, E_BF16>(w, x, wsplits, wtile, xtile, pf, s);
+  if (wepi == E_F32_STORE && xepi == E_DGELU)
+    return (int)pick_w<E_F32_STORE, E_DGELU>(w, x, wsplits, wtile, xtile, pf, s);
+  if (wepi == E_F32_ACC && xepi == E_BF16) return (int)pick_w<E_F32_ACC, E_BF16>(w, x, wsplits, wtile, xtile, pf, s);
+  if (wepi == E_F32_ACC && xepi == E_DGELU) return (int)pick_w<E_F32_ACC, E_DGELU>(w, x, wsplits, wtile, xtile, pf, s);
   return (int)hipErrorInvalidValue;
 }

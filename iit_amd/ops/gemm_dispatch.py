@@ -693,12 +693,13 @@ def _dual_candidates(x: dict, w: dict, xc, wc, csum, bsum=None, gsq=None):
     return out
 
 
-def gemm_pair(x: dict, w: dict) -> Optional[str]:
+def gemm_pair(x: dict, w: dict, prefetch=None) -> Optional[str]:
     """A layer's input gradient ``x`` (mode 0: ``dX = dY W^T``, bf16 or DGELU epilogue) and weight gradient ``w``
     (mode 3: ``dW (+)= X^T dY``), given as :func:`gemm` keyword dicts.  They are independent, so besides running
     them one after the other (each on its own best implementation) they can share ONE launch on the dual kernel
     (``csrc/gemm_dual.hip``): the dispatcher times both options once per problem pair and keeps the faster.
-    ``IIT_GEMM_DUAL=0`` disables the dual launch.  Returns the weight-gradient choice (for ``_settle_claim``)."""
+    ``IIT_GEMM_DUAL=0`` disables the dual launch.  ``prefetch``: tensors (the next pair's cold operands) the dual
+    launch reads into the caches from extra workgroups.  Returns the weight-gradient choice (for ``_settle_claim``)."""
     def serial():
         gemm(**x)
         return gemm(**w)
@@ -743,7 +744,7 @@ def gemm_pair(x: dict, w: dict) -> Optional[str]:
     if cfg is None:
         res = serial()
     else:
-        K.gemm_dual(ws, xs, *cfg)
+        K.gemm_dual(ws, xs, *cfg, prefetch=prefetch)
         res = name
     if TIMING is not None:
         e_ev.record()

@@ -100,7 +100,7 @@ _SIGS = {
     "iit_maxpool3s2_bwd": [c_void_p] * 3 + [c_int] * 5 + [c_void_p],
     "iit_gemm_dual_ok": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 7 + [c_void_p] * 4 + [c_long] * 4 + [c_int] * 5,
     "iit_gemm_dual": [c_void_p] * 3 + [c_long] * 3 + [c_int] * 6 + [c_void_p] * 2 + [c_void_p] * 4 + [c_long] * 4
-                     + [c_int] * 5 + [c_void_p] * 4,
+                     + [c_int] * 5 + [c_void_p] * 3 + [c_void_p, c_long, c_void_p, c_long, c_int, c_void_p],
     "iit_gemm_glds_set_group_m": [c_int],
     "iit_ioi_hl_label": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "iit_conv3x3_tiles": [],
@@ -362,9 +362,11 @@ def gemm_dual_ok(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, redu
         x.get("ldc2", 0), x["M"], x["N"], x["K"], x["epi"], xtile))
 
 
-def gemm_dual(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, reduce: bool = False) -> None:
+def gemm_dual(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, reduce: bool = False,
+              prefetch=None) -> None:
     """Both problems of :func:`gemm_dual_ok` in one launch (``x["csum"]``: the DGELU column sums, ``w["bsum"]``: the
-    column sums of dY over the tokens, i.e. the bias gradient; both optional, += atomically)."""
+    column sums of dY over the tokens, i.e. the bias gradient; both optional, += atomically).  ``prefetch``: up to two
+    tensors (the next pair's cold operands) that extra workgroups of the launch read into the caches."""
     ws = cnt = None
     if reduce:
         ws, cnt = split_workspace(w["M"], w["N"], DUAL_W_TILES[wtile], splits, w["A"].device)
@@ -378,8 +380,24 @@ def gemm_dual(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, reduce:
         _p(w["A"]), _p(w["B"]), _p(w["C"]), w["lda"], w["ldb"], w["ldc"], w["M"], w["N"], w["K"], w["epi"], wtile,
         splits, _p(ws), _p(cnt), _p(x["A"]), _p(x["B"]), _p(x["C"]), _p(x.get("C2")), x["lda"], x["ldb"], x["ldc"],
         x.get("ldc2", 0), x["M"], x["N"], x["K"], x["epi"], xtile, _p(x.get("csum")), _p(w.get("bsum")),
-        _p(w.get("gsq")) if w["epi"] == EPI_F32_STORE else None, _stream()),
+        _p(w.get("gsq")) if w["epi"] == EPI_F32_STORE else None, *_prefetch_args(prefetch), _stream()),
         "iit_gemm_dual")
+
+
+# workgroups of a dual launch that prefetch the next pair's cold operands, per MiB of them (IIT_DUAL_PREFETCH_WGS_PER_MB;
+# 0 disables the prefetch).  Headline step, same box: off 15.58-15.60, 4/MiB 15.46-15.49, 8/MiB 15.46-15.47 ms
+# (profiles/dual_l2_hypothesis_r6.txt)
+_PF_PER_MB = float(os.environ.get("IIT_DUAL_PREFETCH_WGS_PER_MB", "8"))
+
+
+def _prefetch_args(prefetch):
+    ts = [t for t in (prefetch or ()) if t is not None and t.is_cuda and t.is_contiguous()][:2]
+    if not ts or _PF_PER_MB <= 0:
+        return (None, 0, None, 0, 0)
+    ts += [None] * (2 - len(ts))
+    nb = [t.numel() * t.element_size() if t is not None else 0 for t in ts]
+    wgs = max(8, min(1024, int(sum(nb) / 2 ** 20 * _PF_PER_MB)))
+    return (_p(ts[0]), nb[0], _p(ts[1]), nb[1], wgs)
 
 
 def kl_rows(a, b):

@@ -383,6 +383,25 @@ def _aligned_rows(g: torch.Tensor, T: int, N: int) -> torch.Tensor:
     return g2
 
 
+# ---- cold-operand prefetch for the dual dX + dW launches (profiles/dual_l2_hypothesis_r6.txt): inside the step a
+# pair's forward-saved activation X and its weight come from HBM (7-19 % over back-to-back timing).  Every op whose
+# backward launches a pair registers (X, W) in forward order; the backward's pair then prefetches the operands of the
+# pair that runs right after it -- the previous registration -- from extra workgroups of its own launch
+# (csrc/gemm_dual.hip).  The list holds references, so a prefetched range is always live memory.
+_PF_SEQ: list = []
+
+
+def _pf_register(ctx, x2, w):
+    if any(ctx.needs_input_grad):
+        ctx.pf_idx = len(_PF_SEQ)
+        _PF_SEQ.append((x2, w))
+
+
+def _pf_next(ctx):
+    i = getattr(ctx, "pf_idx", 0) - 1
+    return _PF_SEQ[i] if 0 <= i < len(_PF_SEQ) else None
+
+
 class EmbedPosFn(Function):
     @staticmethod
     def forward(ctx, tokens, W_E, W_pos):
@@ -617,6 +636,7 @@ class QKVFn(Function):
         ctx.layer = layer
         ctx.params = (W_Q, W_K, W_V, b_Q, b_K, b_V)
         ctx.dims = (B, S, d, H, dh)
+        _pf_register(ctx, x2, layer["qkv"])
         return out
 
     @staticmethod
@@ -647,7 +667,7 @@ class QKVFn(Function):
             choice = gemm_pair(xspec, dict(A=x2, B=g, C=gq, M=d, N=3 * HD, K=T, lda=d, ldb=3 * HD, ldc=3 * HD,
                                            mode=K.MODE_AKM | K.MODE_BKM,
                                            epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs,
-                                           gsq=_norm_slots(store, W_Q, W_K, W_V)))
+                                           gsq=_norm_slots(store, W_Q, W_K, W_V)), prefetch=_pf_next(ctx))
             if store:
                 _settle_claim(choice, W_Q, W_K, W_V)
         else:
@@ -1030,6 +1050,7 @@ class LinearFn(Function):
         ctx.save_for_backward(x2)
         ctx.params = (W, b)
         ctx.w = w
+        _pf_register(ctx, x2, w)
         ctx.ldw = ldw
         ctx.meta = (lead, Kd, N, out_kind, x.dtype)
         return res
@@ -1072,7 +1093,7 @@ class LinearFn(Function):
             wspec = dict(A=x2, B=g2, C=gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0), mode=mode,
                          epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs,
                          gsq=_norm_slots(store, W))
-            choice = gemm_pair(xspec, wspec) if xspec is not None else gemm(**wspec)
+            choice = gemm_pair(xspec, wspec, prefetch=_pf_next(ctx)) if xspec is not None else gemm(**wspec)
             if store:
                 _settle_claim(choice, W)
         elif xspec is not None:
@@ -1107,6 +1128,7 @@ class MLPInFn(Function):
         ctx.save_for_backward(x2, pre)
         ctx.params = (W_in, b_in)
         ctx.w = w
+        _pf_register(ctx, x2, w)
         ctx.meta = (lead, d, dm)
         return pre.view(*lead, dm), post.view(*lead, dm)
 
@@ -1139,7 +1161,7 @@ class MLPInFn(Function):
             choice = gemm_pair(xspec, dict(A=x2, B=dpre, C=gW, M=d, N=dm, K=T, lda=d, ldb=dm, ldc=dm,
                                            mode=K.MODE_AKM | K.MODE_BKM,
                                            epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store, bsum=bs,
-                                           gsq=_norm_slots(store, W_in)))
+                                           gsq=_norm_slots(store, W_in)), prefetch=_pf_next(ctx))
             if store:
                 _settle_claim(choice, W_in)
         else:
@@ -1185,6 +1207,7 @@ class MLPOutGeluFn(Function):
         ctx.save_for_backward(x2, _flat2(pre))
         ctx.params = (W, b, b_in)
         ctx.w = w
+        _pf_register(ctx, x2, w)
         ctx.ldw = ldw
         ctx.meta = (lead, Kd, N)
         return out.view(*lead, N)
@@ -1216,7 +1239,7 @@ class MLPOutGeluFn(Function):
             wspec = dict(A=x2, B=g2, C=gW2, M=Kd, N=N, K=T, lda=Kd, ldb=ldg, ldc=gW2.stride(0),
                          mode=K.MODE_AKM | K.MODE_BKM, epi=K.EPI_F32_STORE if store else K.EPI_F32_ACC, fresh=store,
                          bsum=bs, gsq=_norm_slots(store, W))
-            choice = gemm_pair(xspec, wspec) if xspec is not None else gemm(**wspec)
+            choice = gemm_pair(xspec, wspec, prefetch=_pf_next(ctx)) if xspec is not None else gemm(**wspec)
             if store:
                 _settle_claim(choice, W)
         elif xspec is not None:
@@ -1455,6 +1478,7 @@ class QKVPairFn(QKVFn):
         ctx.layer = layer
         ctx.params = (W_Q, W_K, W_V, b_Q, b_K, b_V)
         ctx.dims = (B, S, d, H, dh)
+        _pf_register(ctx, x2[:B * S], layer["qkv"])
         box.append(out)
         return out[:B]
 
@@ -1547,6 +1571,7 @@ class LinearPairFn(LinearFn):
         ctx.save_for_backward(x2[:T])
         ctx.params = (W, b)
         ctx.w = w
+        _pf_register(ctx, x2[:T], w)
         ctx.ldw = ldw
         ctx.meta = (lead, Kd, N, out_kind, x.dtype)
         of = out.view(*x_full.shape[:-1], N)
@@ -1586,6 +1611,7 @@ class MLPInPairFn(MLPInFn):
         ctx.save_for_backward(x2[:T], pre[:T])
         ctx.params = (W_in, b_in)
         ctx.w = w
+        _pf_register(ctx, x2[:T], w)
         ctx.meta = (lead, d, dm)
         pf, qf = pre.view(*x_full.shape[:-1], dm), post.view(*x_full.shape[:-1], dm)
         box.append((pf, qf))
@@ -1615,6 +1641,7 @@ class MLPOutGeluPairFn(MLPOutGeluFn):
         ctx.save_for_backward(x2[:T], _flat2(pre))
         ctx.params = (W, b, b_in)
         ctx.w = w
+        _pf_register(ctx, x2[:T], w)
         ctx.ldw = ldw
         ctx.meta = (lead, Kd, N)
         of = out.view(*post_full.shape[:-1], N)
@@ -1675,6 +1702,7 @@ class HipOps(TorchOps):
 
     def begin_forward(self):
         self.shadow.ensure()
+        _PF_SEQ.clear()  # a new forward: the prefetch order restarts (the references of the last one are dropped)
 
     def _L(self, p):
         return self.shadow.layers[self._layer_of[id(p)]]

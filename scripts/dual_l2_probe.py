@@ -13,7 +13,9 @@ its shipped dual configuration is timed on scratch outputs:
   - ``dirty_19mb``: write 19 MB to an unrelated buffer (dirty L2 lines that must be written back, operands hot),
   - ``dirty_dy_wb``: rewrite dY, then stream 64 MB of unrelated reads (dY written back, still in the 256 MB MALL),
   - ``evict``: stream 512 MB of reads (clean L2 and MALL, every operand cold),
-  - ``dirty_19mb_evict``: both.
+  - ``dirty_19mb_evict``: both;
+  - ``evict_read``: evict, then read the pair's cold operands (X, W) once (a reduction over each): the lines the
+    pair needs are back in the caches -- what a perfect prefetch would achieve.
 
 ``--pmc`` runs the same conditions eagerly (``--reps`` each) after 3 eager steps, for rocprofv3 --pmc
 (``scripts/gpu_r6_dual.sh``), and writes the dispatch sequence to ``--seq``; ``--summarize <counter csv>`` then maps
@@ -30,7 +32,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-CONDS = ("hot", "dirty_dy", "dirty_19mb", "dirty_dy_wb", "evict", "dirty_19mb_evict")
+CONDS = ("hot", "dirty_dy", "dirty_19mb", "dirty_dy_wb", "evict", "dirty_19mb_evict", "evict_read")
 
 
 def label(key):
@@ -125,8 +127,12 @@ def main():
             sink.fill_(1.0)
         if cond == "dirty_dy_wb":
             torch.sum(mid, dim=0, keepdim=True, out=out1)
-        if cond in ("evict", "dirty_19mb_evict"):
+        if cond in ("evict", "dirty_19mb_evict", "evict_read"):
             torch.sum(big, dim=0, keepdim=True, out=out1)
+        if cond == "evict_read":
+            x, w = pairs[k]
+            for t in (w["A"], x["B"]):  # dW = X^T dY: A = X; dX = dY W^T: B = W
+                torch.sum(t)  # one read of every line
 
     launch = {}
     for k in keys:
