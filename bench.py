@@ -111,8 +111,9 @@ def setup(args, dev):
 
 
 # the reference publishes no throughput; its semantics (fp32, eager hook closures, full-vocab
-# logits, torch Adam) measured on one MI355X with ``--engine reference --dtype fp32 --graphs 0``
-REFERENCE_EAGER_PAIRS_PER_S = 1559.65
+# logits, torch Adam) measured on one MI355X with ``--engine reference --dtype fp32 --graphs 0 --steps 20``
+# (round 6 at HEAD, profiles/iia_6l_seeds_r6.txt: 153.9 ms/step; round 1's 5-step figure was 1,559.65)
+REFERENCE_EAGER_PAIRS_PER_S = 1663.5
 
 
 def _free_port() -> int:

@@ -46,11 +46,14 @@ struct G2Args {
   // E_F32_STORE: optional sum of squares of the stored values (this weight gradient's share of the global gradient
   // norm the optimizer's clip needs), += atomically into one of 64 slots, so the norm pass can skip these gradients
   float* gsq;
-  // implicit-GEMM convolution (csrc/conv_nhwc.hip): the A operand is gathered from an NHWC activation [n][h][w][c]
-  // (conv_h x conv_w pixels, conv_c channels) through 3 x 3 / stride-1 / pad-1 taps; rows outside the image read
-  // the 16-B-aligned zero page ``zero``; conv_flip negates the tap offsets (the input-gradient convolution)
+  // implicit-GEMM convolution (csrc/conv_nhwc.hip): GEMM rows are the output pixels (n, h, w) of a conv_h x conv_w
+  // image; an operand is gathered from the NHWC source activation [n][conv_sh][conv_sw][conv_c] through the
+  // conv_k x conv_k taps with stride conv_s and padding conv_pad -- forward: source (s h + kh - pad, s w + kw - pad);
+  // conv_flip (the input gradient, a transposed convolution): source ((h + pad - kh) / s, (w + pad - kw) / s) where
+  // divisible.  Taps outside the source image read the 16-B-aligned zero page ``zero``.
   const __bf16* zero;
   int conv_h, conv_w, conv_c, conv_flip;
+  int conv_sh, conv_sw, conv_k, conv_s, conv_pad;
   // E_BF16_CS: per-tile column statistics, channel-major over the M / BM row tiles T:
   // cstat[(k * N + col) * T + tm], k = 0 the tile's pivot (its first row's value), 1 sum(v - pivot), 2 sum((v - pivot)^2)
   // over the tile's BM rows -- plain stores, one writer per element (the consumer is the next launch)

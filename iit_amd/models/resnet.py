@@ -38,8 +38,8 @@ class Conv2d(nn.Conv2d):
             m = _arena_mirror(w)
             if m is not None:
                 from ..ops import conv as hconv
-                if hconv.covered(x, self):  # 3x3 / stride 1: the repo's implicit-GEMM kernels where they win
-                    return hconv.conv3x3(x, w, m[0])
+                if hconv.covered(x, self):  # 3x3 / 1x1, stride 1 / 2: the repo's implicit-GEMM kernels where they win
+                    return hconv.conv(x, w, m[0], hconv.geometry(self))
                 w16 = _MirrorWeight.apply(w, m[0]) if torch.is_grad_enabled() else m[1]
                 return self._conv_forward(x.to(torch.bfloat16), w16, None)
         return super().forward(x)
@@ -141,7 +141,10 @@ class BasicBlock(nn.Module):
             identity = None
             ds = getattr(self.downsample, "mod", self.downsample)  # Sequential(conv1x1, BatchNorm2d), maybe wrapped
             if not _hooked(self.downsample) and isinstance(ds, nn.Sequential) and len(ds) == 2:
-                identity = fused_bn_act(ds[1], None, ds[0](x))
+                from ..ops import conv as hconv
+                with hconv.stats_for_bn(isinstance(ds[1], nn.BatchNorm2d) and ds[1].training):
+                    h = ds[0](x)
+                identity = fused_bn_act(ds[1], None, h)
             if identity is None:
                 identity = self.downsample(x)
         return _bn_after_conv(self.conv2, self.bn2, self.relu, out, identity)

@@ -1,18 +1,22 @@
-"""3 x 3 / stride-1 / pad-1 NHWC bf16 convolution on the repo's implicit-GEMM MFMA kernels (``csrc/conv_nhwc.hip``).
+"""NHWC bf16 convolutions (kernel 3 x 3 / pad 1 or 1 x 1 / pad 0, stride 1 or 2) on the repo's implicit-GEMM MFMA
+kernels (``csrc/conv_nhwc.hip``).
 
 The PVR task's low-level ResNet-18 (``/root/reference/iit/tasks/mnist_pvr/get_alignment.py:9-15``, trained by
-``/root/reference/train.py:16-23``) spends most of its convolution time in the BasicBlock 3 x 3 convolutions.  All
-three passes run as implicit GEMMs on the LDS-DMA kernel:
+``/root/reference/train.py:16-23``) spends its convolution time in the BasicBlock convolutions: the 3 x 3 stride-1
+ones, the first 3 x 3 of layers 2-4 (stride 2) and the 1 x 1 stride-2 downsamples.  All three passes run as implicit
+GEMMs on the LDS-DMA kernel:
 
-* forward: ``Y [N H W][Cout] = im2col(x) W^T`` -- the im2col rows gathered by the DMA's per-lane addresses, the
-  padding read from a zero page;
-* input gradient: the same kernel with the tap offsets negated, on ``dY`` and the weight re-laid [Cin][3][3][Cout];
-* weight gradient: ``dW [Cout][9 Cin] = dY^T im2col(x)`` (reduction over the pixels, deterministic reduction
+* forward: ``Y [N Ho Wo][Cout] = im2col(x) W^T`` -- the im2col rows gathered by the DMA's per-lane addresses, the
+  padding read from a zero page; optionally with per-tile column statistics of Y for the consuming BatchNorm;
+* input gradient: the transposed convolution on ``dY`` and the weight re-laid [Cin][k][k][Cout] (stride 2: the taps
+  that do not divide read the zero page);
+* weight gradient: ``dW [Cout][k k Cin] = dY^T im2col(x)`` (reduction over the output pixels, deterministic reduction
   split-K), written in fp32 straight into the parameter's arena gradient slot (no bf16 ``dW``, no accumulate pass).
 
-Per problem shape and pass the kernel's tiles (and, for the weight gradient, K-splits) compete with the library's
-convolution once (graph-timed, outside capture, like :mod:`iit_amd.ops.gemm_dispatch`) and the faster runs;
-``IIT_CONV_HIP=0`` keeps the library everywhere, ``=1`` forces the repo's kernels wherever they apply.
+Per problem shape and pass the kernel's tiles and K-splits compete with the library's convolution once (graph-timed,
+outside capture, like :mod:`iit_amd.ops.gemm_dispatch`) and the faster runs; ``IIT_CONV_HIP=0`` keeps the library
+everywhere, ``=1`` forces the repo's kernels wherever they apply.  (The 7 x 7 stem with its 3 input channels is not
+covered: a K-tile is 64 channels of one tap.)
 """
 from __future__ import annotations
 
@@ -33,6 +37,8 @@ POLICY = os.environ.get("IIT_CONV_HIP", "auto")
 # IIT_BN_CONV_STATS=0 keeps the BatchNorm's own pass
 CONV_STATS = os.environ.get("IIT_BN_CONV_STATS", "1") != "0"
 _WANT_STATS = [False]
+# (pass, N, H, W, Cin, Cout, k, stride) -> (choice: (tile, splits) | None = the library, {candidate: us})
+DECISIONS: Dict[Tuple, Tuple[Optional[Tuple[int, int]], Dict[str, float]]] = {}
 
 
 class stats_for_bn:
@@ -47,21 +53,30 @@ class stats_for_bn:
 
     def __exit__(self, *exc):
         _WANT_STATS[0] = self.prev
-# (pass, N, H, W, Cin, Cout) -> (choice: (tile, splits) | None = the library, {candidate: us})
-DECISIONS: Dict[Tuple, Tuple[Optional[Tuple[int, int]], Dict[str, float]]] = {}
+
+
+def geometry(conv: torch.nn.Conv2d) -> Optional[Tuple[int, int, int]]:
+    """(kernel, stride, pad) when the kernels cover the convolution's geometry -- 3 x 3 pad 1 or 1 x 1 pad 0, stride
+    1 or 2, no dilation / groups / bias -- else None."""
+    k, s, pd = conv.kernel_size, conv.stride, conv.padding
+    if k not in ((3, 3), (1, 1)) or s not in ((1, 1), (2, 2)) or pd != (k[0] // 2, k[0] // 2):
+        return None
+    if conv.dilation != (1, 1) or conv.groups != 1 or conv.bias is not None or conv.padding_mode != "zeros":
+        return None
+    return k[0], s[0], pd[0]
 
 
 def covered(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
-    """A 3 x 3 / stride 1 / pad 1 / ungrouped, bias-free convolution of a channels-last CUDA activation whose channel
-    counts fit the kernels (Cin, Cout multiples of 64)."""
-    if POLICY == "0" or not K.available():
-        return False
-    if conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1) or conv.dilation != (1, 1):
-        return False
-    if conv.groups != 1 or conv.bias is not None or conv.padding_mode != "zeros":
+    """A covered geometry (:func:`geometry`) on a channels-last CUDA activation whose channel counts fit the kernels
+    (Cin, Cout multiples of 64)."""
+    if POLICY == "0" or not K.available() or geometry(conv) is None:
         return False
     return (x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=CL) and x.shape[1] % 64 == 0
             and conv.out_channels % 64 == 0)
+
+
+def _out_hw(H: int, W: int, k: int, s: int, pad: int) -> Tuple[int, int]:
+    return (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
 
 
 def _decide(key, cands) -> Optional[Tuple[int, int]]:
@@ -85,7 +100,7 @@ def _decide(key, cands) -> Optional[Tuple[int, int]]:
 
 
 def _flip_weight(w: torch.Tensor) -> torch.Tensor:
-    """[Cout, Cin, 3, 3] (memory [Cout][3][3][Cin]) -> [Cin, Cout, 3, 3] with memory [Cin][3][3][Cout]."""
+    """[Cout, Cin, k, k] (memory [Cout][k][k][Cin]) -> [Cin, Cout, k, k] with memory [Cin][k][k][Cout]."""
     return w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
 
 
@@ -93,79 +108,87 @@ def _name(tile: int, splits: int) -> str:
     return f"hip{tile}" + (f"k{splits}" if splits > 1 else "")
 
 
-def _tile_splits(N, H, W, Cin, Cout):
+def _tile_splits(N, SH, SW, Cs, OH, OW, Co, k=3, s=1, pad=1, transposed=False):
     """(tile, K-splits) candidates of the forward / input-gradient kernel: every tile, unsplit and split into 2..9
     equal K ranges (the reduction split: more workgroups for the few-tile deep layers, e.g. layer4's 2304 x 512
     output over K = 4608)."""
     return [(t, sp) for t in range(K.conv3x3_tiles()) for sp in (1, 2, 3, 4, 6, 8, 9)
-            if K.conv3x3_ok(N, H, W, Cin, Cout, t, sp)]
+            if K.conv2d_ok(N, SH, SW, Cs, OH, OW, Co, k, s, pad, transposed, t, sp)]
 
 
-def _fwd_choice(x, w):
+def _fwd_choice(x, w, k, s, pad):
     N, Cin, H, W = x.shape
     Cout = w.shape[0]
-    if ("fwd", N, H, W, Cin, Cout) in DECISIONS:
-        return DECISIONS["fwd", N, H, W, Cin, Cout][0]
-    y = torch.empty(N, Cout, H, W, dtype=BF16, device=x.device, memory_format=CL)
-    cands = {_name(t, sp): ((t, sp), lambda t=t, sp=sp: K.conv3x3(x, w, y, N, H, W, Cin, Cout, False, t, sp))
-             for t, sp in _tile_splits(N, H, W, Cin, Cout)}
-    cands["lib"] = (None, lambda: F.conv2d(x, w, None, 1, 1))
-    return _decide(("fwd", N, H, W, Cin, Cout), cands)
+    key = ("fwd", N, H, W, Cin, Cout, k, s)
+    if key in DECISIONS:
+        return DECISIONS[key][0]
+    OH, OW = _out_hw(H, W, k, s, pad)
+    y = torch.empty(N, Cout, OH, OW, dtype=BF16, device=x.device, memory_format=CL)
+    cands = {_name(t, sp): ((t, sp), lambda t=t, sp=sp: K.conv2d(x, w, y, N, H, W, Cin, OH, OW, Cout, k, s, pad,
+                                                                 False, t, sp))
+             for t, sp in _tile_splits(N, H, W, Cin, OH, OW, Cout, k, s, pad)}
+    cands["lib"] = (None, lambda: F.conv2d(x, w, None, s, pad))
+    return _decide(key, cands)
 
 
-def _dgrad_choice(dy, wf, x_shape):
-    N, Cout, H, W = dy.shape
-    Cin = wf.shape[0]
-    if ("dgrad", N, H, W, Cin, Cout) in DECISIONS:
-        return DECISIONS["dgrad", N, H, W, Cin, Cout][0]
+def _dgrad_choice(dy, wf, x_shape, k, s, pad):
+    N, Cout, OH, OW = dy.shape
+    Cin, H, W = x_shape[1], x_shape[2], x_shape[3]
+    key = ("dgrad", N, H, W, Cin, Cout, k, s)
+    if key in DECISIONS:
+        return DECISIONS[key][0]
     dx = torch.empty(N, Cin, H, W, dtype=BF16, device=dy.device, memory_format=CL)
-    cands = {_name(t, sp): ((t, sp), lambda t=t, sp=sp: K.conv3x3(dy, wf, dx, N, H, W, Cout, Cin, True, t, sp))
-             for t, sp in _tile_splits(N, H, W, Cout, Cin)}
+    cands = {_name(t, sp): ((t, sp), lambda t=t, sp=sp: K.conv2d(dy, wf, dx, N, OH, OW, Cout, H, W, Cin, k, s, pad,
+                                                                 True, t, sp))
+             for t, sp in _tile_splits(N, OH, OW, Cout, H, W, Cin, k, s, pad, True)}
     w = wf.permute(1, 0, 2, 3)
-    cands["lib"] = (None, lambda: torch.nn.grad.conv2d_input(x_shape, w, dy, 1, 1))
-    return _decide(("dgrad", N, H, W, Cin, Cout), cands)
+    cands["lib"] = (None, lambda: torch.nn.grad.conv2d_input(x_shape, w, dy, s, pad))
+    return _decide(key, cands)
 
 
-def _wgrad_choice(dy, x, w16):
+def _wgrad_choice(dy, x, w16, k, s, pad):
     N, Cin, H, W = x.shape
-    Cout = dy.shape[1]
-    if ("wgrad", N, H, W, Cin, Cout) in DECISIONS:
-        return DECISIONS["wgrad", N, H, W, Cin, Cout][0]
-    dw = torch.empty(Cout, Cin, 3, 3, dtype=torch.float32, device=x.device, memory_format=CL)
+    Cout, OH, OW = dy.shape[1], dy.shape[2], dy.shape[3]
+    key = ("wgrad", N, H, W, Cin, Cout, k, s)
+    if key in DECISIONS:
+        return DECISIONS[key][0]
+    dw = torch.empty(Cout, Cin, k, k, dtype=torch.float32, device=x.device, memory_format=CL)
     cands = {}
+    pixels = N * OH * OW
     for t in K.CONV_WG_TILES:
-        for sp in K.conv3x3_wgrad_splits(N * H * W) if (N * H * W) % 64 == 0 else ():
-            if K.conv3x3_wgrad_ok(N, H, W, Cin, Cout, t, sp):
-                cands[f"hip{t}k{sp}"] = ((t, sp), lambda t=t, sp=sp: K.conv3x3_wgrad(dy, x, dw, N, H, W, Cin, Cout,
-                                                                                    False, t, sp))
+        for sp in K.conv3x3_wgrad_splits(pixels) if pixels % 64 == 0 else ():
+            if K.conv2d_wgrad_ok(N, H, W, Cin, OH, OW, Cout, k, s, pad, t, sp):
+                cands[f"hip{t}k{sp}"] = ((t, sp), lambda t=t, sp=sp: K.conv2d_wgrad(
+                    dy, x, dw, N, H, W, Cin, OH, OW, Cout, k, s, pad, False, t, sp))
     cands["lib"] = (None, lambda: torch.ops.aten.convolution_backward(
-        dy, x, w16, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1, (False, True, False)))
-    return _decide(("wgrad", N, H, W, Cin, Cout), cands)
+        dy, x, w16, None, (s, s), (pad, pad), (1, 1), False, (0, 0), 1, (False, True, False)))
+    return _decide(key, cands)
 
 
-class Conv3x3Fn(Function):
-    """``conv2d(x, W, stride 1, pad 1)`` for an arena weight ``W`` (fp32 master, bf16 mirror ``flat.shadow_view``):
+class ConvFn(Function):
+    """``conv2d(x, W, stride s, pad)`` for an arena weight ``W`` (fp32 master, bf16 mirror ``flat.shadow_view``):
     forward / input gradient / weight gradient each on the repo's kernel or the library, whichever measured faster
     for the shape; the weight gradient lands in W's fp32 arena slot (stored when the slot is claimable, else added)."""
 
     @staticmethod
-    def forward(ctx, x, W, flat, want_stats=False):
+    def forward(ctx, x, W, flat, want_stats=False, geom=(3, 1, 1)):
+        k, s, pad = geom
         w = flat.shadow_view(W)
         N, Cin, H, Wd = x.shape
         Cout = w.shape[0]
-        ch = _fwd_choice(x, w)
+        OH, OW = _out_hw(H, Wd, k, s, pad)
+        ch = _fwd_choice(x, w, k, s, pad)
         cstat = None
         if ch is None:
-            y = F.conv2d(x, w, None, 1, 1)
+            y = F.conv2d(x, w, None, s, pad)
         else:
-            y = torch.empty(N, Cout, H, Wd, dtype=BF16, device=x.device, memory_format=CL)
+            y = torch.empty(N, Cout, OH, OW, dtype=BF16, device=x.device, memory_format=CL)
             if want_stats:  # per-tile column statistics for the consuming BatchNorm (3 x Cout x T fp32)
-                cstat = torch.empty(3 * Cout * (N * H * Wd // K.conv3x3_rows(ch[0])), dtype=torch.float32,
+                cstat = torch.empty(3 * Cout * (N * OH * OW // K.conv3x3_rows(ch[0])), dtype=torch.float32,
                                     device=x.device)
-            K.conv3x3(x, w, y, N, H, Wd, Cin, Cout, False, ch[0], ch[1], cstat=cstat)
+            K.conv2d(x, w, y, N, H, Wd, Cin, OH, OW, Cout, k, s, pad, False, ch[0], ch[1], cstat=cstat)
         ctx.save_for_backward(x)
-        ctx.W, ctx.flat = W, flat
-        ctx.stat_rows = K.conv3x3_rows(ch[0]) if cstat is not None else 0
+        ctx.W, ctx.flat, ctx.geom = W, flat, geom
         if cstat is None:
             cstat = torch.empty(0, dtype=torch.float32, device=x.device)
         ctx.mark_non_differentiable(cstat)
@@ -176,43 +199,50 @@ class Conv3x3Fn(Function):
         from ..engine import grad_hooks
         (x,) = ctx.saved_tensors
         W, flat = ctx.W, ctx.flat
+        k, s, pad = ctx.geom
         w = flat.shadow_view(W)
         N, Cin, H, Wd = x.shape
         Cout = w.shape[0]
         dy = dy.to(BF16).contiguous(memory_format=CL)
+        OH, OW = dy.shape[2], dy.shape[3]
         dx = None
         if ctx.needs_input_grad[0]:
             wf = _flip_weight(w)
-            ch = _dgrad_choice(dy, wf, x.shape)
+            ch = _dgrad_choice(dy, wf, x.shape, k, s, pad)
             if ch is None:
-                dx = torch.nn.grad.conv2d_input(x.shape, w, dy, 1, 1)
+                dx = torch.nn.grad.conv2d_input(x.shape, w, dy, s, pad)
             else:
                 dx = torch.empty(N, Cin, H, Wd, dtype=BF16, device=x.device, memory_format=CL)
-                K.conv3x3(dy, wf, dx, N, H, Wd, Cout, Cin, True, ch[0], ch[1])
+                K.conv2d(dy, wf, dx, N, OH, OW, Cout, H, Wd, Cin, k, s, pad, True, ch[0], ch[1])
         if W.requires_grad:
-            ch = _wgrad_choice(dy, x, w)
+            ch = _wgrad_choice(dy, x, w, k, s, pad)
             if ch is None:
                 from .torch_ops import _accumulate
-                gw = torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
+                gw = torch.ops.aten.convolution_backward(dy, x, w, None, (s, s), (pad, pad), (1, 1), False, (0, 0), 1,
                                                         (False, True, False))[1]
                 _accumulate(W, gw)
             else:
                 store = flat.claim(W)  # a lazily-zeroed slot: store (beta = 0), else accumulate
                 if W.grad is None:
                     flat.bind_zero(W)
-                K.conv3x3_wgrad(dy, x, W.grad, N, H, Wd, Cin, Cout, not store, ch[0], ch[1])
+                K.conv2d_wgrad(dy, x, W.grad, N, H, Wd, Cin, OH, OW, Cout, k, s, pad, not store, ch[0], ch[1])
                 grad_hooks.notify(W)
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
-def conv3x3(x: torch.Tensor, W: torch.Tensor, flat) -> torch.Tensor:
-    """The convolution of ``x`` with the arena weight ``W`` (bf16 mirror) on the measured-faster implementation.
-    Inside :class:`stats_for_bn`, an output of the repo's kernel carries ``_iit_cstat`` = (records, T, rows per tile,
-    the output's version): its BatchNorm statistics, valid while the tensor is not modified in place."""
+Conv3x3Fn = ConvFn  # (the stride-1 3 x 3 name of round 6's first version)
+
+
+def conv(x: torch.Tensor, W: torch.Tensor, flat, geom=(3, 1, 1)) -> torch.Tensor:
+    """The convolution (``geom`` = (kernel, stride, pad)) of ``x`` with the arena weight ``W`` (bf16 mirror) on the
+    measured-faster implementation.  Inside :class:`stats_for_bn`, an output of the repo's kernel carries
+    ``_iit_cstat`` = (records, T, rows per tile, the output's version): its BatchNorm statistics, valid while the
+    tensor is not modified in place."""
     x = x.to(BF16)
+    k, s, pad = geom
     if not W.is_contiguous(memory_format=CL):
-        return F.conv2d(x, flat.shadow_view(W), None, 1, 1)
-    y, cstat = Conv3x3Fn.apply(x, W, flat, _WANT_STATS[0])
+        return F.conv2d(x, flat.shadow_view(W), None, s, pad)
+    y, cstat = ConvFn.apply(x, W, flat, _WANT_STATS[0], tuple(geom))
     if cstat.numel():
         N, C, H, Wd = y.shape
         rows = N * H * Wd // (cstat.numel() // (3 * C))
@@ -220,9 +250,14 @@ def conv3x3(x: torch.Tensor, W: torch.Tensor, flat) -> torch.Tensor:
     return y
 
 
+def conv3x3(x: torch.Tensor, W: torch.Tensor, flat) -> torch.Tensor:
+    return conv(x, W, flat, (3, 1, 1))
+
+
 def report() -> str:
     lines = []
-    for (kind, N, H, W, Cin, Cout), (ch, times) in sorted(DECISIONS.items()):
-        ts = "  ".join(f"{k} {v:7.1f}us" for k, v in sorted(times.items(), key=lambda kv: kv[1])[:4])
-        lines.append(f"{kind:5s} N={N} H={H} W={W} Cin={Cin} Cout={Cout} -> {'lib' if ch is None else ch}  {ts}")
+    for (kind, N, H, W, Cin, Cout, k, s), (ch, times) in sorted(DECISIONS.items()):
+        ts = "  ".join(f"{n} {v:7.1f}us" for n, v in sorted(times.items(), key=lambda kv: kv[1])[:4])
+        lines.append(f"{kind:5s} N={N} H={H} W={W} Cin={Cin} Cout={Cout} k={k} s={s} -> "
+                     f"{'lib' if ch is None else ch}  {ts}")
     return "\n".join(lines)

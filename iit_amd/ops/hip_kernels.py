@@ -108,6 +108,10 @@ _SIGS = {
     "iit_conv3x3": [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                      c_void_p, c_void_p],
     "iit_conv3x3_rows": [c_int],
+    "iit_conv2d_ok": [c_long] + [c_int] * 12,
+    "iit_conv2d": [c_void_p] * 4 + [c_long] + [c_int] * 12 + [c_void_p] * 4,
+    "iit_conv2d_wgrad_ok": [c_long] + [c_int] * 11,
+    "iit_conv2d_wgrad": [c_void_p] * 4 + [c_long] + [c_int] * 12 + [c_void_p] * 3,
     "iit_bn_fwd_tiles": [c_void_p] * 4 + [c_int, c_int] + [c_void_p] * 4 + [c_long, c_int, c_float, c_int, c_void_p,
                                                                            c_float, c_void_p, c_void_p],
     "iit_conv3x3_wgrad_tiles": [],
@@ -713,6 +717,47 @@ def conv3x3(x, w, y, N: int, H: int, W: int, Cin: int, Cout: int, flip: bool = F
             assert cstat.dtype == torch.float32 and cstat.numel() >= 3 * Cout * (N * H * W // conv3x3_rows(tile))
     _check(lib().iit_conv3x3(_p(x), _p(w), _p(y), _p(zero_page(x.device)), N, H, W, Cin, Cout, int(flip), tile,
                              splits, _p(ws), _p(cnt), _p(cstat), _stream()), "conv3x3")
+
+
+def conv2d_ok(N: int, SH: int, SW: int, Cs: int, OH: int, OW: int, Co: int, k: int, s: int, pad: int,
+              transposed: bool, tile: int, splits: int = 1) -> bool:
+    return bool(lib().iit_conv2d_ok(N, SH, SW, Cs, OH, OW, Co, k, s, pad, int(transposed), tile, splits))
+
+
+def conv2d(x, w, y, N: int, SH: int, SW: int, Cs: int, OH: int, OW: int, Co: int, k: int, s: int, pad: int,
+           transposed: bool, tile: int = 0, splits: int = 1, cstat=None):
+    """Implicit-GEMM convolution (csrc/conv_nhwc.hip): forward ``y`` [N,OH,OW,Co] = conv(``x`` [N,SH,SW,Cs], ``w``
+    [Co,k,k,Cs], stride ``s``, padding ``pad``), or (``transposed``) the input gradient of a forward conv from
+    [OH,OW,Co] to [SH,SW,Cs]: ``x`` = dy, ``w`` the weight re-laid [Co = Cin][k][k][Cs = Cout], ``y`` = dx."""
+    ws = cnt = None
+    if splits > 1:
+        ws, cnt = split_workspace(N * OH * OW, Co, CONV_TILES[tile], splits, x.device)
+    if CHECK_BOUNDS:
+        assert x.numel() >= N * SH * SW * Cs and y.numel() >= N * OH * OW * Co and w.numel() >= k * k * Cs * Co
+        assert x.dtype == w.dtype == y.dtype == torch.bfloat16
+        if cstat is not None:
+            assert cstat.dtype == torch.float32 and cstat.numel() >= 3 * Co * (N * OH * OW // conv3x3_rows(tile))
+    _check(lib().iit_conv2d(_p(x), _p(w), _p(y), _p(zero_page(x.device)), N, SH, SW, Cs, OH, OW, Co, k, s, pad,
+                            int(transposed), tile, splits, _p(ws), _p(cnt), _p(cstat), _stream()), "conv2d")
+
+
+def conv2d_wgrad_ok(N: int, SH: int, SW: int, Cin: int, OH: int, OW: int, Cout: int, k: int, s: int, pad: int,
+                    tile: int, splits: int) -> bool:
+    return bool(lib().iit_conv2d_wgrad_ok(N, SH, SW, Cin, OH, OW, Cout, k, s, pad, tile, splits))
+
+
+def conv2d_wgrad(dy, x, dw, N: int, SH: int, SW: int, Cin: int, OH: int, OW: int, Cout: int, k: int, s: int,
+                 pad: int, acc: bool, tile: int, splits: int = 1):
+    """``dw`` [Cout,k,k,Cin] fp32 (+)= the weight gradient of the conv ``x`` [N,SH,SW,Cin] -> ``dy`` [N,OH,OW,Cout];
+    ``splits`` > 1: deterministic reduction split over the output pixels."""
+    ws = cnt = None
+    if splits > 1:
+        ws, cnt = split_workspace(Cout, k * k * Cin, CONV_WG_TILES[tile], splits, dy.device)
+    if CHECK_BOUNDS:
+        assert dw.dtype == torch.float32 and dw.numel() >= k * k * Cin * Cout
+        assert dy.numel() >= N * OH * OW * Cout and x.numel() >= N * SH * SW * Cin
+    _check(lib().iit_conv2d_wgrad(_p(dy), _p(x), _p(dw), _p(zero_page(x.device)), N, SH, SW, Cin, OH, OW, Cout, k, s,
+                                  pad, int(acc), tile, splits, _p(ws), _p(cnt), _stream()), "conv2d_wgrad")
 
 
 CONV_WG_TILES = {0: (64, 64), 1: (128, 64), 2: (128, 128), 3: (64, 128)}

@@ -149,3 +149,86 @@ def test_conv_epilogue_bn_statistics(N, C, hw, tile, splits, offset):
     assert float(((s1[:C].double() - mean).abs() / (var.sqrt() + 1e-6)).max()) < 1e-3
     assert float(((s1[C:].double() - (var + 1e-5).rsqrt()).abs() / (var + 1e-5).rsqrt()).max()) < 2e-3
     assert rel(rm1, rm2) < 1e-3 and rel(rv1, rv2) < 1e-3
+
+
+@pytest.mark.parametrize("N,Cin,Cout,hw,k,s", [(64, 64, 128, 21, 3, 2), (64, 128, 256, 11, 3, 2),
+                                              (64, 256, 512, 6, 3, 2), (64, 64, 128, 21, 1, 2),
+                                              (64, 256, 512, 6, 1, 2), (32, 64, 64, 9, 1, 1)])
+def test_conv2d_strided_and_pointwise_match_fp32(N, Cin, Cout, hw, k, s):
+    """The general implicit-GEMM entry points on the ResNet's other body convolutions -- the 3 x 3 stride-2 first
+    convolution of layers 2-4 and the 1 x 1 (stride-2) downsample: forward, the transposed input gradient (stride 2:
+    the taps that do not divide read the zero page) and the weight gradient, every covering tile / split, against
+    fp32 torch on the same bf16 operands."""
+    from iit_amd.ops import hip_kernels as K
+    from iit_amd.ops.conv import _flip_weight, _out_hw
+    torch.manual_seed(Cin + hw + k + s)
+    pad = k // 2
+    x = torch.randn(N, Cin, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(Cout, Cin, k, k, device=dev) / (k * Cin ** 0.5)).to(torch.bfloat16).contiguous(memory_format=CL)
+    ref = F.conv2d(x.float(), w.float(), None, s, pad)
+    OH, OW = _out_hw(hw, hw, k, s, pad)
+    assert ref.shape[2:] == (OH, OW)
+    dy = torch.randn_like(ref).to(torch.bfloat16).contiguous(memory_format=CL)
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), s, pad)
+    dw_ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), s, pad)
+    wf = _flip_weight(w)
+    fwd = dgr = wgr = 0
+    for t in range(K.conv3x3_tiles()):
+        for sp in (1, 2, 3):
+            if K.conv2d_ok(N, hw, hw, Cin, OH, OW, Cout, k, s, pad, False, t, sp):
+                fwd += 1
+                y = torch.full((N, Cout, OH, OW), float("nan"), device=dev, dtype=torch.bfloat16).contiguous(
+                    memory_format=CL)
+                K.conv2d(x, w, y, N, hw, hw, Cin, OH, OW, Cout, k, s, pad, False, t, sp)
+                assert rel(y, ref) < 8e-3, ("fwd", t, sp)
+            if K.conv2d_ok(N, OH, OW, Cout, hw, hw, Cin, k, s, pad, True, t, sp):
+                dgr += 1
+                dx = torch.full_like(x, float("nan"))
+                K.conv2d(dy, wf, dx, N, OH, OW, Cout, hw, hw, Cin, k, s, pad, True, t, sp)
+                assert rel(dx, dx_ref) < 8e-3, ("dgrad", t, sp)
+    for t in K.CONV_WG_TILES:
+        for sp in K.conv3x3_wgrad_splits(N * OH * OW)[:3]:
+            if K.conv2d_wgrad_ok(N, hw, hw, Cin, OH, OW, Cout, k, s, pad, t, sp):
+                wgr += 1
+                dw = torch.full((Cout, Cin, k, k), float("nan"), device=dev).contiguous(memory_format=CL)
+                K.conv2d_wgrad(dy, x, dw, N, hw, hw, Cin, OH, OW, Cout, k, s, pad, False, t, sp)
+                assert rel(dw, dw_ref) < 1e-4, ("wgrad", t, sp)
+    assert fwd > 0 and dgr > 0 and wgr > 0, (fwd, dgr, wgr)
+
+
+def test_resnet_block_convs_on_repo_kernels(monkeypatch):
+    """A stride-2 BasicBlock with its 1 x 1 downsample under bf16 autocast, every convolution forced onto the repo's
+    kernels (IIT_CONV_HIP=1 policy): output and every parameter gradient against the same block in fp32 within the
+    library bf16 path's own error."""
+    from iit_amd.engine.flat import FlatParams
+    from iit_amd.models.resnet import BasicBlock, conv1x1
+    from iit_amd.ops import conv as hconv
+    monkeypatch.setattr(hconv, "POLICY", "1")
+    hconv.DECISIONS.clear()
+    torch.manual_seed(1)
+    blocks = []
+    for _ in range(3):
+        ds = torch.nn.Sequential(conv1x1(64, 128, 2), torch.nn.BatchNorm2d(128))
+        blocks.append(BasicBlock(64, 128, 2, ds).to(dev).to(memory_format=CL))
+    for b in blocks[1:]:
+        b.load_state_dict(blocks[0].state_dict())
+    FlatParams(blocks[0], with_bf16_shadow=True)
+    x = torch.randn(64, 64, 21, 21, device=dev).contiguous(memory_format=CL)
+    outs = []
+    for b, env, amp in ((blocks[0], "1", True), (blocks[1], "0", True), (blocks[2], "0", False)):
+        monkeypatch.setenv("IIT_CONV_MIRROR", env)
+        xi = x.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            y = b(xi)
+        y.float().square().mean().backward()
+        outs.append((y.float().detach(), xi.grad.float()))
+    kinds = {key[0] + str(key[6]) + str(key[7]) for key in hconv.DECISIONS}
+    assert {"fwd32", "fwd12", "dgrad32", "dgrad12", "wgrad32", "wgrad12"} <= kinds, kinds
+    assert all(ch is not None for ch, _ in hconv.DECISIONS.values())
+    (ym, gm), (yc, gc), (yr, gr) = outs
+    assert rel(ym, yr) <= 1.5 * rel(yc, yr) + 1e-2
+    assert rel(gm, gr) <= 1.5 * rel(gc, gr) + 2e-2
+    for (n, pm), (_, pc), (_, pr) in zip(*(b.named_parameters() for b in blocks)):
+        assert pm.grad is not None, n
+        em, ec = rel(pm.grad, pr.grad), rel(pc.grad, pr.grad)
+        assert em <= 1.5 * ec + 2e-2, (n, em, ec)
