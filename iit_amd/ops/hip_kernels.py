@@ -389,9 +389,9 @@ def gemm_dual(w: dict, x: dict, wtile: int, xtile: int, splits: int = 1, reduce:
 
 
 # workgroups of a dual launch that prefetch the next pair's cold operands, per MiB of them (IIT_DUAL_PREFETCH_WGS_PER_MB;
-# 0 disables the prefetch).  Headline step, same box: off 15.58-15.60, 4/MiB 15.46-15.49, 8/MiB 15.46-15.47 ms
-# (profiles/dual_l2_hypothesis_r6.txt)
-_PF_PER_MB = float(os.environ.get("IIT_DUAL_PREFETCH_WGS_PER_MB", "8"))
+# 0 disables the prefetch).  Headline step, same box: off 15.58-15.65, 4/MiB 15.46-15.49, 8/MiB 15.44-15.47, 16/MiB
+# 15.43, 32/MiB 15.48-15.51 ms (profiles/dual_l2_hypothesis_r6.txt)
+_PF_PER_MB = float(os.environ.get("IIT_DUAL_PREFETCH_WGS_PER_MB", "16"))
 
 
 def _prefetch_args(prefetch):

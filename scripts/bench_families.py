@@ -211,6 +211,9 @@ def main():
             "weight_checksum": wsum, "zero": bool(args.zero), "zero_overlap_gather": bool(args.zero_overlap),
             "optimizer_skipped_steps": int(getattr(opt, "_skipped_dev", torch.zeros(1)).sum()),
         }))
+    if os.environ.get("IIT_CONV_REPORT") == "1" and rank == 0:  # the per-shape conv decisions (ops/conv.py)
+        from iit_amd.ops import conv as hconv
+        print(hconv.report(), file=sys.stderr)
     pdist.destroy()
 
 

@@ -47,8 +47,8 @@ def record_pairs(pair, loss_fn, opt, it, gd, K):
     order = []
     orig = gd.gemm_pair
 
-    def wrap(x, w):
-        res = orig(x, w)
+    def wrap(x, w, prefetch=None):
+        res = orig(x, w, prefetch=prefetch)
         if gd._dual_eligible(x, w):
             fresh = bool(w.get("fresh")) and w["epi"] == K.EPI_F32_STORE
             key = ("dual", x["M"], x["N"], x["K"], x["epi"], x.get("colsum") is not None,
