@@ -204,6 +204,7 @@ def test_resnet_block_convs_on_repo_kernels(monkeypatch):
     from iit_amd.models.resnet import BasicBlock, conv1x1
     from iit_amd.ops import conv as hconv
     monkeypatch.setattr(hconv, "POLICY", "1")
+    monkeypatch.setattr(hconv, "GEOMS", {"k3s1", "k3s2", "k1s1", "k1s2"})  # (k3s2 is opt-in by default)
     hconv.DECISIONS.clear()
     torch.manual_seed(1)
     blocks = []

@@ -247,7 +247,7 @@ def test_mqnli_bert_pair_trains_on_hip_arena():
     assert all(torch.isfinite(torch.tensor(losses)))
 
 
-def test_torch_backend_reads_arena_mirror_and_accumulates_in_place():
+def test_torch_backend_reads_arena_mirror_and_accumulates_in_place(monkeypatch):
     """Llama-family (torch op backend, bf16 on GPU): weights come from the arena's bf16 mirror and gradients land
     in the fp32 arena directly (fp32-output weight-gradient GEMMs, fp32 bias sums) -- the plain cast +
     AccumulateGrad path agrees to bf16 rounding (it rounds dW and the bias sums to bf16 first)."""
@@ -259,30 +259,29 @@ def test_torch_backend_reads_arena_mirror_and_accumulates_in_place():
     assert cfg["n_key_value_heads"] < cfg["n_heads"]  # grouped-query heads: packed [d][(H + 2 H_kv) dh] arena group
     calls = []
     orig = torch_ops._MirrorMat.apply
-    torch_ops._MirrorMat.apply = lambda *a_: calls.append(1) or orig(*a_)
-    try:
-        for S in (9, 40):  # 40 > 16 with d_head 64: the tiled MFMA attention kernel on the torch backend
-            if S > 16:
-                cfg = llama_config_dict("llama-tiny", device=dev, dtype=torch.bfloat16, d_head=64, rotary_dim=64)
-            torch.manual_seed(0)
-            a = HookedTransformer(cfg)
-            b = copy.deepcopy(a)
-            flat = FlatParams(a)
-            tok = torch.randint(0, cfg["d_vocab"], (4, S), device=dev)
-            with torch.no_grad():
-                assert rel(a(tok), b(tok)) < 1e-2
-            for m in (a, b):
-                m(tok).float().pow(2).mean().backward()
-            assert flat.shadow is not None  # the mirror was used
-            scale = max(pb.grad.float().norm().item() for pb in b.parameters())
-            for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
-                # near-cancelling gradients (the key bias: softmax is shift-invariant up to the rotary) are noise
-                # in both paths: relative to the model's gradient scale there
-                err = (pa.grad.float() - pb.grad.float()).norm().item()
-                assert err <= 1e-2 * pb.grad.float().norm().item() + 1e-4 * scale, (S, n)
-            assert flat.grad.abs().sum() > 0
-    finally:
-        torch_ops._MirrorMat.apply = orig
+    # (monkeypatch removes the class attribute afterwards; assigning ``orig`` back would leave a bound _MirrorMat.apply
+    # on the class, which its subclasses -- torch_pairs.MirrorMatPairFn -- would then inherit)
+    monkeypatch.setattr(torch_ops._MirrorMat, "apply", lambda *a_: calls.append(1) or orig(*a_))
+    for S in (9, 40):  # 40 > 16 with d_head 64: the tiled MFMA attention kernel on the torch backend
+        if S > 16:
+            cfg = llama_config_dict("llama-tiny", device=dev, dtype=torch.bfloat16, d_head=64, rotary_dim=64)
+        torch.manual_seed(0)
+        a = HookedTransformer(cfg)
+        b = copy.deepcopy(a)
+        flat = FlatParams(a)
+        tok = torch.randint(0, cfg["d_vocab"], (4, S), device=dev)
+        with torch.no_grad():
+            assert rel(a(tok), b(tok)) < 1e-2
+        for m in (a, b):
+            m(tok).float().pow(2).mean().backward()
+        assert flat.shadow is not None  # the mirror was used
+        scale = max(pb.grad.float().norm().item() for pb in b.parameters())
+        for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+            # near-cancelling gradients (the key bias: softmax is shift-invariant up to the rotary) are noise
+            # in both paths: relative to the model's gradient scale there
+            err = (pa.grad.float() - pb.grad.float()).norm().item()
+            assert err <= 1e-2 * pb.grad.float().norm().item() + 1e-4 * scale, (S, n)
+        assert flat.grad.abs().sum() > 0
     assert calls  # packed QKV / 2-D W_O projections ran
 
 
