@@ -13,8 +13,8 @@
 // outside the image (the padding) -- into exactly the swizzled LDS image the strided stager builds, so the main loop,
 // the MFMA fragments and the epilogue are the GEMM's, unchanged.  No im2col buffer, no padding copy.
 //
-// The input gradient is the same kernel in transposed mode (conv_flip) on A = dY and B = the weight re-laid
-// [Cin][k][k][Cout]:  dx[n][h][w][ci] = sum_{kh, kw, co} dy[n][(h + pad - kh) / s][(w + pad - kw) / s][co]
+// The input gradient is the same GEMM body in transposed mode (conv_flip) on A = dY and B = the forward weight read
+// k-major in place (ConvWTStager):  dx[n][h][w][ci] = sum_{kh, kw, co} dy[n][(h + pad - kh) / s][(w + pad - kw) / s][co]
 // W[co][kh][kw][ci] over the taps where the division is exact (stride 2: the other taps read the zero page).
 #include "gemm_glds_body.h"
 
@@ -155,6 +155,48 @@ struct ConvColStager {
   }
 };
 
+// The transposed convolution's (input gradient's) B operand read straight from the FORWARD weight
+// [Cout][k][k][Cin] -- no re-laid copy of the weight per backward: B [n = ci][K = tap * Cout + co] = W[co][tap][ci],
+// staged k-major ([64 K rows][R columns], the image of Stager<true, R, NW, 64>): a K-tile is 64 output channels co of
+// one tap (Cout % 64 == 0), so k-row r of the tile is the contiguous 2R-byte run W[co0 + r][tap][n0 .. n0 + R).
+template <int R, int NW>
+struct ConvWTStager {
+  static constexpr int CH = R / 8;      // 16-B chunks per k-row
+  static constexpr int KRI = 64 / CH;   // k-rows per LDS-DMA instruction
+  static constexpr int N = 64 / (NW * KRI);
+  static_assert(N >= 1 && (R == 64 || R == 128), "64- or 128-column tiles");
+  const __bf16* w;
+  long kkC;  // row stride of W: k k Cin
+  int kr[N], col[N], off[N];
+  int C, CS, n0, kbeg;
+
+  __device__ __forceinline__ void init(const G2Args& p, int r0g, int kbeg_, int wave, int lane) {
+    w = p.B;
+    C = p.N;        // GEMM columns = the conv's input channels
+    CS = p.conv_c;  // the source (dy) channels = the conv's output channels
+    kkC = (long)p.conv_k * p.conv_k * C;
+    n0 = r0g;
+    kbeg = kbeg_;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int kr0 = (i * NW + wave) * KRI;
+      const int k = kr0 + lane / CH;
+      const int ch = lane % CH;
+      kr[i] = k;
+      col[i] = (((ch >> 1) ^ kmaj_swz<R>(k)) << 4) + ((ch & 1) << 3);
+      off[i] = kr0 * R * 2;
+    }
+  }
+
+  __device__ __forceinline__ void stage(int kt, char* img) const {
+    const int k0 = kbeg + kt * 64;
+    const int tap = k0 / CS, co0 = k0 - tap * CS;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      glds16(w + (long)(co0 + kr[i]) * kkC + (long)tap * C + n0 + col[i], img + off[i]);
+  }
+};
+
 template <int BM, int BN, int NS, int NW, int OCC, int EPI>
 __global__ __launch_bounds__(NW * 64, OCC) void conv3x3_wgrad_kernel(G2Args p) {
   __shared__ __attribute__((aligned(16))) char smem[GldsSmem<BM, BN, NS, NW, 64, OCC>::BYTES];
@@ -173,10 +215,20 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3x3_kernel(G2Args p) {
                                                                                            blockIdx.y, gridDim.y, smem);
 }
 
+// the transposed convolution (input gradient): B k-major from the forward weight (ConvWTStager)
+template <int BM, int BN, int NS, int NW, int OCC>
+__global__ __launch_bounds__(NW * 64, OCC) void conv_t_kernel(G2Args p) {
+  __shared__ __attribute__((aligned(16))) char smem[GldsSmem<BM, BN, NS, NW, 64, OCC>::BYTES];
+  gemm_glds_body<BM, BN, NS, false, true, E_BF16, NW, 64, OCC, false, ConvRowStager<BM, NW>, ConvWTStager<BN, NW>>(
+      p, blockIdx.x, gridDim.x, blockIdx.y, gridDim.y, smem);
+}
+
 template <int BM, int BN, int NS, int NW = 4, int OCC = 1>
 hipError_t launch_conv(const G2Args& a, int splits, hipStream_t s) {
   const int tiles = (a.M / BM) * (a.N / BN);
-  if (a.cstat)
+  if (a.conv_flip)
+    hipLaunchKernelGGL((conv_t_kernel<BM, BN, NS, NW, OCC>), dim3(tiles, splits), dim3(NW * 64), 0, s, a);
+  else if (a.cstat)
     hipLaunchKernelGGL((conv3x3_kernel<BM, BN, NS, NW, OCC, E_BF16_CS>), dim3(tiles, splits), dim3(NW * 64), 0, s, a);
   else
     hipLaunchKernelGGL((conv3x3_kernel<BM, BN, NS, NW, OCC, E_BF16>), dim3(tiles, splits), dim3(NW * 64), 0, s, a);
@@ -251,7 +303,8 @@ IIT_EXPORT int iit_conv2d_ok(long N, int SH, int SW, int Cs, int OH, int OW, int
   return 1;
 }
 
-// y = conv(x, w) (forward: w [Co][k][k][Cs]) or the transposed convolution (w re-laid [Co = Cin][k][k][Cs = Cout]);
+// y = conv(x, w) (forward: w [Co][k][k][Cs]) or the transposed convolution (w = the FORWARD weight [Cs = Cout][k][k]
+// [Co = Cin], read k-major in place);
 // bf16 NHWC, no bias.  ``zero``: >= 128 zero bytes, 16-B aligned.  ``splits`` > 1 needs ``ws`` (>= splits N OH OW Co
 // floats) and ``counters`` (>= the tile count, zero when idle; re-armed by every launch).  ``cstat`` (nullable):
 // per-tile column statistics of y for its BatchNorm, [3][Co][N OH OW / BM] floats (gemm_glds_body.h E_BF16_CS).

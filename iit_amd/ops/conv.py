@@ -8,8 +8,8 @@ GEMMs on the LDS-DMA kernel:
 
 * forward: ``Y [N Ho Wo][Cout] = im2col(x) W^T`` -- the im2col rows gathered by the DMA's per-lane addresses, the
   padding read from a zero page; optionally with per-tile column statistics of Y for the consuming BatchNorm;
-* input gradient: the transposed convolution on ``dY`` and the weight re-laid [Cin][k][k][Cout] (stride 2: the taps
-  that do not divide read the zero page);
+* input gradient: the transposed convolution on ``dY``, the forward weight read k-major in place (stride 2: the
+  taps that do not divide read the zero page);
 * weight gradient: ``dW [Cout][k k Cin] = dY^T im2col(x)`` (reduction over the output pixels, deterministic reduction
   split-K), written in fp32 straight into the parameter's arena gradient slot (no bf16 ``dW``, no accumulate pass).
 
@@ -116,11 +116,6 @@ def _decide(key, cands) -> Optional[Tuple[int, int]]:
     return cands[best][0]
 
 
-def _flip_weight(w: torch.Tensor) -> torch.Tensor:
-    """[Cout, Cin, k, k] (memory [Cout][k][k][Cin]) -> [Cin, Cout, k, k] with memory [Cin][k][k][Cout]."""
-    return w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
-
-
 def _name(tile: int, splits: int) -> str:
     return f"hip{tile}" + (f"k{splits}" if splits > 1 else "")
 
@@ -148,17 +143,16 @@ def _fwd_choice(x, w, k, s, pad):
     return _decide(key, cands)
 
 
-def _dgrad_choice(dy, wf, x_shape, k, s, pad):
+def _dgrad_choice(dy, w, x_shape, k, s, pad):
     N, Cout, OH, OW = dy.shape
     Cin, H, W = x_shape[1], x_shape[2], x_shape[3]
     key = ("dgrad", N, H, W, Cin, Cout, k, s)
     if key in DECISIONS:
         return DECISIONS[key][0]
     dx = torch.empty(N, Cin, H, W, dtype=BF16, device=dy.device, memory_format=CL)
-    cands = {_name(t, sp): ((t, sp), lambda t=t, sp=sp: K.conv2d(dy, wf, dx, N, OH, OW, Cout, H, W, Cin, k, s, pad,
+    cands = {_name(t, sp): ((t, sp), lambda t=t, sp=sp: K.conv2d(dy, w, dx, N, OH, OW, Cout, H, W, Cin, k, s, pad,
                                                                  True, t, sp))
              for t, sp in _tile_splits(N, OH, OW, Cout, H, W, Cin, k, s, pad, True)}
-    w = wf.permute(1, 0, 2, 3)
     cands["lib"] = (None, lambda: torch.nn.grad.conv2d_input(x_shape, w, dy, s, pad))
     return _decide(key, cands)
 
@@ -224,13 +218,12 @@ class ConvFn(Function):
         OH, OW = dy.shape[2], dy.shape[3]
         dx = None
         if ctx.needs_input_grad[0]:
-            wf = _flip_weight(w)
-            ch = _dgrad_choice(dy, wf, x.shape, k, s, pad)
+            ch = _dgrad_choice(dy, w, x.shape, k, s, pad)
             if ch is None:
                 dx = torch.nn.grad.conv2d_input(x.shape, w, dy, s, pad)
-            else:
+            else:  # (the transposed kernel reads the forward weight k-major: no re-laid copy)
                 dx = torch.empty(N, Cin, H, Wd, dtype=BF16, device=x.device, memory_format=CL)
-                K.conv2d(dy, wf, dx, N, OH, OW, Cout, H, Wd, Cin, k, s, pad, True, ch[0], ch[1])
+                K.conv2d(dy, w, dx, N, OH, OW, Cout, H, Wd, Cin, k, s, pad, True, ch[0], ch[1])
         if W.requires_grad:
             ch = _wgrad_choice(dy, x, w, k, s, pad)
             if ch is None:

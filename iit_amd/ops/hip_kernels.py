@@ -704,7 +704,8 @@ def conv3x3_rows(tile: int) -> int:
 def conv3x3(x, w, y, N: int, H: int, W: int, Cin: int, Cout: int, flip: bool = False, tile: int = 0,
             splits: int = 1, cstat=None):
     """``y`` [N,H,W,Cout] = 3x3 / stride-1 / pad-1 convolution of the NHWC bf16 ``x`` [N,H,W,Cin] with ``w``
-    [Cout,3,3,Cin] (``flip``: negated tap offsets -- the input gradient, with ``w`` re-laid [Cin,3,3,Cout]);
+    [Cout,3,3,Cin] (``flip``: the input gradient -- ``x`` = dy [N,H,W,Cout'], ``w`` the forward weight [Cout',3,3,Cin'],
+    output channels ``Cout`` = Cin');
     ``splits`` > 1: deterministic reduction split over the 9 Cin reduction.  ``cstat`` (fp32, >= 3 Cout T floats,
     T = N H W / :func:`conv3x3_rows`): per-tile column statistics of ``y`` for :func:`bn_fwd_tiles`."""
     ws = cnt = None
@@ -728,7 +729,7 @@ def conv2d(x, w, y, N: int, SH: int, SW: int, Cs: int, OH: int, OW: int, Co: int
            transposed: bool, tile: int = 0, splits: int = 1, cstat=None):
     """Implicit-GEMM convolution (csrc/conv_nhwc.hip): forward ``y`` [N,OH,OW,Co] = conv(``x`` [N,SH,SW,Cs], ``w``
     [Co,k,k,Cs], stride ``s``, padding ``pad``), or (``transposed``) the input gradient of a forward conv from
-    [OH,OW,Co] to [SH,SW,Cs]: ``x`` = dy, ``w`` the weight re-laid [Co = Cin][k][k][Cs = Cout], ``y`` = dx."""
+    [OH,OW,Co] to [SH,SW,Cs]: ``x`` = dy, ``w`` the FORWARD weight [Cs = Cout][k][k][Co = Cin], ``y`` = dx."""
     ws = cnt = None
     if splits > 1:
         ws, cnt = split_workspace(N * OH * OW, Co, CONV_TILES[tile], splits, x.device)

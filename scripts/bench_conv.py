@@ -19,7 +19,7 @@ SHAPES = [("layer1", 64, 64, 21), ("layer2", 128, 128, 11), ("layer3", 256, 256,
 def main():
     from iit_amd.ops import gemm_dispatch as gd
     from iit_amd.ops import hip_kernels as K
-    from iit_amd.ops.conv import _flip_weight, _name, _tile_splits
+    from iit_amd.ops.conv import _name, _tile_splits
     CL = torch.channels_last
     N = int(os.environ.get("BATCH", "256"))
     for name, Cin, Cout, hw in SHAPES:
@@ -28,15 +28,15 @@ def main():
         w = (torch.randn(Cout, Cin, 3, 3, device="cuda") / 24).to(torch.bfloat16).contiguous(memory_format=CL)
         y = torch.empty(N, Cout, hw, hw, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=CL)
         dy = torch.randn_like(y)
-        wf = _flip_weight(w)
+        wf = w  # the transposed kernel reads the forward weight in place
         dx = torch.empty_like(x)
         row = {"layer": name, "N": N, "Cin": Cin, "Cout": Cout, "HW": hw,
                "GFLOP": round(2 * N * hw * hw * Cout * 9 * Cin / 1e9, 2)}
         fwd = {"lib": lambda: F.conv2d(x, w, None, 1, 1)}
         bwd = {"lib": lambda: torch.nn.grad.conv2d_input(x.shape, w, dy, 1, 1)}
-        for t, sp in _tile_splits(N, hw, hw, Cin, Cout):
+        for t, sp in _tile_splits(N, hw, hw, Cin, hw, hw, Cout):
             fwd[_name(t, sp)] = lambda t=t, sp=sp: K.conv3x3(x, w, y, N, hw, hw, Cin, Cout, False, t, sp)
-        for t, sp in _tile_splits(N, hw, hw, Cout, Cin):
+        for t, sp in _tile_splits(N, hw, hw, Cout, hw, hw, Cin, 3, 1, 1, True):
             bwd[_name(t, sp)] = lambda t=t, sp=sp: K.conv3x3(dy, wf, dx, N, hw, hw, Cout, Cin, True, t, sp)
         dwt = torch.empty(Cout, Cin, 3, 3, device="cuda", dtype=torch.float32).contiguous(memory_format=CL)
         wgr = {"lib": lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0),

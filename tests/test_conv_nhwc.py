@@ -18,7 +18,6 @@ def rel(a, b):
                                            (128, 512, 512, 3), (16, 64, 128, 8)])
 def test_conv3x3_matches_fp32(N, Cin, Cout, hw):
     from iit_amd.ops import hip_kernels as K
-    from iit_amd.ops.conv import _flip_weight
     torch.manual_seed(Cin + hw)
     x = torch.randn(N, Cin, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=CL)
     w = (torch.randn(Cout, Cin, 3, 3, device=dev) / (3 * Cin ** 0.5)).to(torch.bfloat16).contiguous(memory_format=CL)
@@ -42,7 +41,7 @@ def test_conv3x3_matches_fp32(N, Cin, Cout, hw):
                 assert torch.equal(y, y2), (t, sp)
             if K.conv3x3_ok(N, hw, hw, Cout, Cin, t, sp):
                 dx = torch.full_like(x, float("nan"))
-                K.conv3x3(dy, _flip_weight(w), dx, N, hw, hw, Cout, Cin, True, t, sp)
+                K.conv3x3(dy, w, dx, N, hw, hw, Cout, Cin, True, t, sp)
                 assert rel(dx, dx_ref) < 8e-3, (t, sp)
     assert ran > 0 and split > 0
 
@@ -160,7 +159,7 @@ def test_conv2d_strided_and_pointwise_match_fp32(N, Cin, Cout, hw, k, s):
     the taps that do not divide read the zero page) and the weight gradient, every covering tile / split, against
     fp32 torch on the same bf16 operands."""
     from iit_amd.ops import hip_kernels as K
-    from iit_amd.ops.conv import _flip_weight, _out_hw
+    from iit_amd.ops.conv import _out_hw
     torch.manual_seed(Cin + hw + k + s)
     pad = k // 2
     x = torch.randn(N, Cin, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=CL)
@@ -171,7 +170,7 @@ def test_conv2d_strided_and_pointwise_match_fp32(N, Cin, Cout, hw, k, s):
     dy = torch.randn_like(ref).to(torch.bfloat16).contiguous(memory_format=CL)
     dx_ref = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), s, pad)
     dw_ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), s, pad)
-    wf = _flip_weight(w)
+    wf = w  # the transposed kernel reads the forward weight in place
     fwd = dgr = wgr = 0
     for t in range(K.conv3x3_tiles()):
         for sp in (1, 2, 3):
