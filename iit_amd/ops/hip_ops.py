@@ -389,10 +389,11 @@ def _aligned_rows(g: torch.Tensor, T: int, N: int) -> torch.Tensor:
 # pair that runs right after it -- the previous registration -- from extra workgroups of its own launch
 # (csrc/gemm_dual.hip).  The list holds references, so a prefetched range is always live memory.
 _PF_SEQ: list = []
+_PF_ON = [True]  # set per forward by HipOps.begin_forward (the model's ``prefetch`` policy)
 
 
 def _pf_register(ctx, x2, w):
-    if any(ctx.needs_input_grad):
+    if _PF_ON[0] and any(ctx.needs_input_grad):
         ctx.pf_idx = len(_PF_SEQ)
         _PF_SEQ.append((x2, w))
 
@@ -1692,6 +1693,11 @@ class HipOps(TorchOps):
         super().__init__(BF16)
         self.model = model
         self.shadow = ModelShadow(model)
+        # dual-pair cold-operand prefetch (IIT_DUAL_PREFETCH=auto|0|1): auto = on for the decoder (GPT-2 headline step
+        # 15.58-15.65 -> 15.43-15.49 ms) and off for the post-LN encoder, where it measured slower (MQNLI 12.14 -> 12.31 ms,
+        # profiles/dual_l2_hypothesis_r6.txt)
+        pol = os.environ.get("IIT_DUAL_PREFETCH", "auto")
+        self.prefetch = pol == "1" or (pol == "auto" and type(model).__name__ != "HookedEncoder")
         self._layer_of = {}
         for i, blk in enumerate(model.blocks):
             self._layer_of[id(blk.attn.W_Q)] = i
@@ -1703,6 +1709,7 @@ class HipOps(TorchOps):
     def begin_forward(self):
         self.shadow.ensure()
         _PF_SEQ.clear()  # a new forward: the prefetch order restarts (the references of the last one are dropped)
+        _PF_ON[0] = self.prefetch
 
     def _L(self, p):
         return self.shadow.layers[self._layer_of[id(p)]]

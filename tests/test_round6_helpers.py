@@ -31,8 +31,9 @@ class _Ctx:
         self.needs_input_grad = (grad, False)
 
 
-def test_dual_prefetch_registry_order():
+def test_dual_prefetch_registry_order(monkeypatch):
     from iit_amd.ops import hip_ops
+    monkeypatch.setattr(hip_ops, "_PF_ON", [True])
     hip_ops._PF_SEQ.clear()
     ctxs = [_Ctx() for _ in range(4)]
     ops = [(torch.zeros(1), torch.zeros(2)) for _ in range(4)]  # (X, W) of QKV, W_O, W_in, W_out in forward order
@@ -47,6 +48,10 @@ def test_dual_prefetch_registry_order():
     assert hip_ops._pf_next(ctxs[0]) is None  # the last pair of the backward has nothing after it
     hip_ops._PF_SEQ.clear()  # (begin_forward) a stale index finds nothing
     assert hip_ops._pf_next(ctxs[3]) is None
+    hip_ops._PF_ON[0] = False  # a model whose policy is off (the encoder) registers nothing
+    c = _Ctx()
+    hip_ops._pf_register(c, torch.zeros(1), torch.zeros(1))
+    assert not hasattr(c, "pf_idx") and not hip_ops._PF_SEQ
 
 
 def test_prefetch_args_packing():
