@@ -226,7 +226,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv_t_kernel(G2Args p) {
 template <int BM, int BN, int NS, int NW = 4, int OCC = 1>
 hipError_t launch_conv(const G2Args& a, int splits, hipStream_t s) {
   const int tiles = (a.M / BM) * (a.N / BN);
-  if (a.conv_flip)
+  if (a.conv_flip == 1)  // transposed, forward weight in place; 2 = transposed on a re-laid [Cin][k][k][Cout] copy
     hipLaunchKernelGGL((conv_t_kernel<BM, BN, NS, NW, OCC>), dim3(tiles, splits), dim3(NW * 64), 0, s, a);
   else if (a.cstat)
     hipLaunchKernelGGL((conv3x3_kernel<BM, BN, NS, NW, OCC, E_BF16_CS>), dim3(tiles, splits), dim3(NW * 64), 0, s, a);
@@ -303,15 +303,17 @@ IIT_EXPORT int iit_conv2d_ok(long N, int SH, int SW, int Cs, int OH, int OW, int
   return 1;
 }
 
-// y = conv(x, w) (forward: w [Co][k][k][Cs]) or the transposed convolution (w = the FORWARD weight [Cs = Cout][k][k]
-// [Co = Cin], read k-major in place);
+// y = conv(x, w) (forward: w [Co][k][k][Cs]) or the transposed convolution: ``transposed`` 1 = w is the FORWARD
+// weight [Cs = Cout][k][k][Co = Cin], read k-major in place; 2 = w re-laid [Co = Cin][k][k][Cs = Cout] (k-contiguous:
+// faster per call, but the caller pays a copy);
 // bf16 NHWC, no bias.  ``zero``: >= 128 zero bytes, 16-B aligned.  ``splits`` > 1 needs ``ws`` (>= splits N OH OW Co
 // floats) and ``counters`` (>= the tile count, zero when idle; re-armed by every launch).  ``cstat`` (nullable):
 // per-tile column statistics of y for its BatchNorm, [3][Co][N OH OW / BM] floats (gemm_glds_body.h E_BF16_CS).
 IIT_EXPORT int iit_conv2d(const void* x, const void* w, void* y, const void* zero, long N, int SH, int SW, int Cs,
                           int OH, int OW, int Co, int k, int s, int pad, int transposed, int tile, int splits,
                           float* ws, int* counters, float* cstat, void* stream) {
-  if (!iit_conv2d_ok(N, SH, SW, Cs, OH, OW, Co, k, s, pad, transposed, tile, splits)) return (int)hipErrorInvalidValue;
+  if (transposed < 0 || transposed > 2 || !iit_conv2d_ok(N, SH, SW, Cs, OH, OW, Co, k, s, pad, transposed, tile, splits))
+    return (int)hipErrorInvalidValue;
   if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y | (uintptr_t)zero) & 15) return (int)hipErrorInvalidValue;
   if (splits > 1 && (!ws || !counters)) return (int)hipErrorInvalidValue;
   G2Args a{};

@@ -8,8 +8,9 @@ GEMMs on the LDS-DMA kernel:
 
 * forward: ``Y [N Ho Wo][Cout] = im2col(x) W^T`` -- the im2col rows gathered by the DMA's per-lane addresses, the
   padding read from a zero page; optionally with per-tile column statistics of Y for the consuming BatchNorm;
-* input gradient: the transposed convolution on ``dY``, the forward weight read k-major in place (stride 2: the
-  taps that do not divide read the zero page);
+* input gradient: the transposed convolution on ``dY`` with the forward weight read k-major in place, or with a
+  re-laid k-contiguous copy where that measures faster including the copy (stride 2: the taps that do not divide read
+  the zero page);
 * weight gradient: ``dW [Cout][k k Cin] = dY^T im2col(x)`` (reduction over the output pixels, deterministic reduction
   split-K), written in fp32 straight into the parameter's arena gradient slot (no bf16 ``dW``, no accumulate pass).
 
@@ -143,16 +144,26 @@ def _fwd_choice(x, w, k, s, pad):
     return _decide(key, cands)
 
 
+def _relaid(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, k, k] (memory [Cout][k][k][Cin]) -> memory [Cin][k][k][Cout]: the k-contiguous transposed weight."""
+    return w.permute(1, 0, 2, 3).contiguous(memory_format=CL)
+
+
 def _dgrad_choice(dy, w, x_shape, k, s, pad):
+    """(tile, splits, mode): mode 1 = the transposed kernel reads the forward weight k-major in place, 2 = it reads a
+    re-laid k-contiguous copy (faster per call; the candidate's time includes making the copy)."""
     N, Cout, OH, OW = dy.shape
     Cin, H, W = x_shape[1], x_shape[2], x_shape[3]
     key = ("dgrad", N, H, W, Cin, Cout, k, s)
     if key in DECISIONS:
         return DECISIONS[key][0]
     dx = torch.empty(N, Cin, H, W, dtype=BF16, device=dy.device, memory_format=CL)
-    cands = {_name(t, sp): ((t, sp), lambda t=t, sp=sp: K.conv2d(dy, w, dx, N, OH, OW, Cout, H, W, Cin, k, s, pad,
-                                                                 True, t, sp))
-             for t, sp in _tile_splits(N, OH, OW, Cout, H, W, Cin, k, s, pad, True)}
+    cands = {}
+    for t, sp in _tile_splits(N, OH, OW, Cout, H, W, Cin, k, s, pad, True):
+        cands[_name(t, sp)] = ((t, sp, 1), lambda t=t, sp=sp: K.conv2d(dy, w, dx, N, OH, OW, Cout, H, W, Cin, k, s,
+                                                                         pad, 1, t, sp))
+        cands[_name(t, sp) + "c"] = ((t, sp, 2), lambda t=t, sp=sp: K.conv2d(dy, _relaid(w), dx, N, OH, OW, Cout, H,
+                                                                             W, Cin, k, s, pad, 2, t, sp))
     cands["lib"] = (None, lambda: torch.nn.grad.conv2d_input(x_shape, w, dy, s, pad))
     return _decide(key, cands)
 
@@ -221,9 +232,10 @@ class ConvFn(Function):
             ch = _dgrad_choice(dy, w, x.shape, k, s, pad)
             if ch is None:
                 dx = torch.nn.grad.conv2d_input(x.shape, w, dy, s, pad)
-            else:  # (the transposed kernel reads the forward weight k-major: no re-laid copy)
+            else:
                 dx = torch.empty(N, Cin, H, Wd, dtype=BF16, device=x.device, memory_format=CL)
-                K.conv2d(dy, w, dx, N, OH, OW, Cout, H, Wd, Cin, k, s, pad, True, ch[0], ch[1])
+                K.conv2d(dy, w if ch[2] == 1 else _relaid(w), dx, N, OH, OW, Cout, H, Wd, Cin, k, s, pad, ch[2],
+                         ch[0], ch[1])
         if W.requires_grad:
             ch = _wgrad_choice(dy, x, w, k, s, pad)
             if ch is None:

@@ -729,7 +729,8 @@ def conv2d(x, w, y, N: int, SH: int, SW: int, Cs: int, OH: int, OW: int, Co: int
            transposed: bool, tile: int = 0, splits: int = 1, cstat=None):
     """Implicit-GEMM convolution (csrc/conv_nhwc.hip): forward ``y`` [N,OH,OW,Co] = conv(``x`` [N,SH,SW,Cs], ``w``
     [Co,k,k,Cs], stride ``s``, padding ``pad``), or (``transposed``) the input gradient of a forward conv from
-    [OH,OW,Co] to [SH,SW,Cs]: ``x`` = dy, ``w`` the FORWARD weight [Cs = Cout][k][k][Co = Cin], ``y`` = dx."""
+    [OH,OW,Co] to [SH,SW,Cs]: ``x`` = dy, ``w`` the FORWARD weight [Cs = Cout][k][k][Co = Cin] (``transposed`` = 1 or
+    True; read k-major in place) or its re-laid copy [Co = Cin][k][k][Cs = Cout] (``transposed`` = 2), ``y`` = dx."""
     ws = cnt = None
     if splits > 1:
         ws, cnt = split_workspace(N * OH * OW, Co, CONV_TILES[tile], splits, x.device)

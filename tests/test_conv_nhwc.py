@@ -159,7 +159,7 @@ def test_conv2d_strided_and_pointwise_match_fp32(N, Cin, Cout, hw, k, s):
     the taps that do not divide read the zero page) and the weight gradient, every covering tile / split, against
     fp32 torch on the same bf16 operands."""
     from iit_amd.ops import hip_kernels as K
-    from iit_amd.ops.conv import _out_hw
+    from iit_amd.ops.conv import _out_hw, _relaid
     torch.manual_seed(Cin + hw + k + s)
     pad = k // 2
     x = torch.randn(N, Cin, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=CL)
@@ -185,6 +185,9 @@ def test_conv2d_strided_and_pointwise_match_fp32(N, Cin, Cout, hw, k, s):
                 dx = torch.full_like(x, float("nan"))
                 K.conv2d(dy, wf, dx, N, OH, OW, Cout, hw, hw, Cin, k, s, pad, True, t, sp)
                 assert rel(dx, dx_ref) < 8e-3, ("dgrad", t, sp)
+                dx2 = torch.full_like(x, float("nan"))  # mode 2: the re-laid k-contiguous weight copy
+                K.conv2d(dy, _relaid(w), dx2, N, OH, OW, Cout, hw, hw, Cin, k, s, pad, 2, t, sp)
+                assert rel(dx2, dx_ref) < 8e-3, ("dgrad relaid", t, sp)
     for t in K.CONV_WG_TILES:
         for sp in K.conv3x3_wgrad_splits(N * OH * OW)[:3]:
             if K.conv2d_wgrad_ok(N, hw, hw, Cin, OH, OW, Cout, k, s, pad, t, sp):
