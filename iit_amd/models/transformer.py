@@ -922,7 +922,10 @@ class HookedTransformer(HookedRootModule):
         (:meth:`TransformerBlock.paired_torch_ok`), flash-attention sequence lengths, no live user hook."""
         if getattr(ops, "fused", True) or ops.dtype != torch.bfloat16 or not self.embed.W_E.is_cuda:
             return False
-        if self.cfg.positional_embedding_type != "rotary" or os.environ.get("IIT_PAIRED_TORCH", "1") == "0":
+        # opt-in (IIT_PAIRED_TORCH=1): at Llama-3-8B / S = 512 every projection is already an 8192-row GEMM and the
+        # paired forward measured 0.9-3.5 % slower than the two forwards, with ~10 GB more peak memory
+        # (profiles/llama3_8b_paired_r6.txt)
+        if self.cfg.positional_embedding_type != "rotary" or os.environ.get("IIT_PAIRED_TORCH", "0") != "1":
             return False
         if tokens.dim() != 2 or tokens.shape != src_tokens.shape or tokens.shape[1] <= 16:
             return False

@@ -271,6 +271,7 @@ def test_llama_paired_forward_matches_two_forwards(monkeypatch, sites_kind):
     calls = []
     orig = torch_pairs.RMSNormPairFn.apply
     monkeypatch.setattr(torch_pairs.RMSNormPairFn, "apply", lambda *a_: calls.append(1) or orig(*a_))
+    monkeypatch.setenv("IIT_PAIRED_TORCH", "1")  # (opt-in: measured slower at Llama-3-8B scale)
     res = a.run_paired(tok, src_tok, sites, logits="full")
     assert res is not None, "the torch-backend paired forward did not engage"
     out_p, caps = res
