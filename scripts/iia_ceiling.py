@@ -102,8 +102,9 @@ def main():
     ap.add_argument("--num-samples", type=int, default=12000)
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--graphs", type=int, default=1, help="0: eager phases (no HIP graphs)")
-    ap.add_argument("--backend", default="hip", choices=["hip", "torch"],
-                    help="torch: the fp32 torch-op oracle backend on the same device")
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch", "torch-bf16"],
+                    help="torch: the fp32 torch-op oracle backend on the same device; torch-bf16: the torch-op backend "
+                         "computing in bf16 (separates bf16 precision from the HIP kernels)")
     ap.add_argument("--train-nodes", default="",
                     help="comma list of HL node names the TRAINING steps sample from (default: all, as the reference)")
     ap.add_argument("--seed", type=int, default=0, help="model-initialisation seed (torch / numpy)")
@@ -124,7 +125,8 @@ def main():
     if args.model == "ioi-6l":
         cfg.update(ioi_cfg)
     fast = dev.type == "cuda" and args.backend == "hip"
-    cfg.update(init_weights=True, device=str(dev), dtype=torch.bfloat16 if fast else torch.float32)
+    bf16 = fast or (dev.type == "cuda" and args.backend == "torch-bf16")
+    cfg.update(init_weights=True, device=str(dev), dtype=torch.bfloat16 if bf16 else torch.float32)
     ll = HookedTransformer(cfg)
     if not fast:
         ll.set_op_backend("torch")
