@@ -108,6 +108,9 @@ def main():
     ap.add_argument("--train-nodes", default="",
                     help="comma list of HL node names the TRAINING steps sample from (default: all, as the reference)")
     ap.add_argument("--seed", type=int, default=0, help="model-initialisation seed (torch / numpy)")
+    ap.add_argument("--plain-adam", action="store_true",
+                    help="torch.optim.Adam on the module's own parameters: no flat arena, no bf16 mirror, no fused "
+                         "clip norm (separates the fused-optimizer machinery from compute precision)")
     ap.add_argument("--control", default="", choices=["", "zero-wo"],
                     help="zero-wo: zero and freeze W_O of the blocks hosting hook_duplicate (see the docstring)")
     args = ap.parse_args()
@@ -147,6 +150,8 @@ def main():
     training_args = {"batch_size": 256, "lr": args.lr, "iit_weight": 1.0, "behavior_weight": 1.0, "strict_weight": 0.4,
                      "next_token": False, "lr_scheduler": None, "clip_grad_norm": 1.0, "early_stop": False,
                      "use_single_loss": False, "graphs": bool(args.graphs)}
+    if args.plain_adam:
+        training_args["fused_optimizer"] = False
     pair = IOI_ModelPair(ll_model=ll, hl_model=hl, corr=make_ioi_corr(cfg["n_layers"]), training_args=training_args)
 
     if args.train_nodes:  # learnability probe: train on a subset of nodes, still evaluate every node
@@ -218,7 +223,8 @@ def main():
     wall = time.perf_counter() - t0
     best = max(rows, key=lambda r: r["val/IIA"])
     print(json.dumps({"metric": "IOI val/IIA ceiling analysis", "model": args.model, "epochs": args.epochs,
-                      "train_nodes": args.train_nodes or "all", "control": args.control or None, "graphs": args.graphs, "backend": args.backend, "lr": args.lr,
+                      "train_nodes": args.train_nodes or "all", "control": args.control or None, "graphs": args.graphs, "backend": args.backend, "plain_adam": args.plain_adam,
+                      "fused_norm": os.environ.get("IIT_FUSED_NORM", "1"), "lr": args.lr,
                       "wall_s": round(wall, 1), "seed": args.seed,
                       "first_eval_all_nodes_IIA_ge_95": first95 or None, "tie_fraction_per_node": ties,
                       "best_epoch_val_IIA": best["val/IIA"], "best_epoch": best["epoch"],
