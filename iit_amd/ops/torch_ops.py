@@ -285,12 +285,40 @@ class TorchOps:
     name = "torch"
     fused = False
 
+    # ops whose outputs IIT_EMULATE_BF16=act rounds to bf16 (the activations a bf16 engine stores between ops)
+    _EMU_ACT_OPS = ("embed", "pos_embed", "layer_norm", "qkv", "attention", "o_proj", "mlp_in", "mlp_out", "unembed")
+
     def __init__(self, dtype: torch.dtype = torch.float32):
         self.dtype = dtype
+        # precision study (scripts/iia_ceiling.py, profiles/iia_precision_r6.txt): an fp32 backend that rounds its
+        # weights ("w") and/or its op outputs ("act") to bf16 -- forward values and, through the casts' autograd,
+        # the activation gradients -- to find which bf16 rounding changes a training trajectory.  Off by default.
+        import os
+        emu = set(os.environ.get("IIT_EMULATE_BF16", "").split(",")) - {""} if dtype == torch.float32 else set()
+        self.emu_w = "w" in emu
+        if "act" in emu:
+            for name in self._EMU_ACT_OPS:
+                setattr(self, name, self._rounding(getattr(self, name)))
+
+    @staticmethod
+    def _rounding(fn):
+        def rnd(t):
+            if isinstance(t, torch.Tensor) and t.dtype == torch.float32:
+                return t.to(torch.bfloat16).to(torch.float32)
+            if isinstance(t, tuple):
+                return tuple(rnd(u) for u in t)
+            return t
+
+        def wrapped(*args, **kwargs):
+            return rnd(fn(*args, **kwargs))
+        return wrapped
 
     # -- helpers --------------------------------------------------------------
     def w(self, p: torch.Tensor) -> torch.Tensor:
         if p.dtype == self.dtype:
+            if getattr(self, "emu_w", False) and p.dtype == torch.float32:
+                # bf16-rounded value, gradient straight through to the fp32 parameter
+                return p + (p.detach().to(torch.bfloat16).to(torch.float32) - p.detach())
             return p
         if self.dtype == torch.bfloat16 and torch.is_grad_enabled():
             m = _arena_mirror(p)

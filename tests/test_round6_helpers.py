@@ -58,3 +58,28 @@ def test_prefetch_args_packing():
     from iit_amd.ops import hip_kernels as K
     assert K._prefetch_args(None) == (None, 0, None, 0, 0)
     assert K._prefetch_args((torch.zeros(4),)) == (None, 0, None, 0, 0)  # host tensors are never prefetched
+
+
+def test_torch_ops_bf16_emulation(monkeypatch):
+    """IIT_EMULATE_BF16 (precision study): "w" rounds weights to bf16 with a straight-through gradient, "act" rounds
+    op outputs to bf16; an fp32 backend without it is unchanged."""
+    from iit_amd.ops.torch_ops import TorchOps
+    torch.manual_seed(0)
+    x = torch.randn(4, 8)
+    W = torch.randn(8, 5, requires_grad=True)
+    ref = TorchOps(torch.float32).lin(x, W)
+    assert torch.equal(ref, x @ W)
+    monkeypatch.setenv("IIT_EMULATE_BF16", "w")
+    y = TorchOps(torch.float32).lin(x, W)
+    assert torch.equal(y, x @ W.detach().bfloat16().float())
+    y.sum().backward()
+    assert torch.allclose(W.grad, x.sum(0)[:, None].expand(8, 5))
+    monkeypatch.setenv("IIT_EMULATE_BF16", "act")
+    ops = TorchOps(torch.float32)
+    z = ops.layer_norm(torch.randn(3, 16), None, None, 1e-5)
+    assert torch.equal(z, z.bfloat16().float())
+    q, k, v = (torch.randn(2, 5, 2, 4) for _ in range(3))
+    out = ops.attention(q, k, v, True, 2.0)
+    assert torch.equal(out, out.bfloat16().float())
+    monkeypatch.setenv("IIT_EMULATE_BF16", "w,act")
+    assert TorchOps(torch.bfloat16).emu_w is False  # only an fp32 backend emulates
