@@ -485,8 +485,16 @@ __global__ __launch_bounds__(256) void ln_dwdb_vec_kernel(const void* __restrict
 // meet in LDS and write ONE partial row pair (dw part, db part) to ``part[block][2 d]`` with plain stores -- no
 // atomics here (the separate ln_dwdb kernels re-read dy and x and did one memory-side fp32 atomic per column per
 // 32 rows: ~17 us for [3840][768], profiles/mqnli_step_breakdown_r5.txt).  ln_part_reduce_kernel sums the partials.
-constexpr int LN_FUSED_R = 2;
-template <int V4, bool DY_F32>
+// R = rows per wave (the block covers 4 R rows): IIT_LN_PART_R = 1 / 2 / 4, default 2
+static int ln_part_r() {
+  static const int r = [] {
+    const char* e = getenv("IIT_LN_PART_R");
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 4) ? v : 2;
+  }();
+  return r;
+}
+template <int V4, bool DY_F32, int LN_FUSED_R>
 __global__ __launch_bounds__(256) void ln_bwd_part_vec_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ rstd,
@@ -692,7 +700,7 @@ IIT_EXPORT int iit_ln_bwd(const void* dy, int dy_f32, const float* x, const floa
 }
 
 // rows per block of the fused affine-gradient backward (the caller sizes ``part`` as blocks x 2 d floats)
-IIT_EXPORT int iit_ln_bwd_part_rows() { return 4 * LN_FUSED_R; }
+IIT_EXPORT int iit_ln_bwd_part_rows() { return 4 * ln_part_r(); }
 
 // iit_ln_bwd_sel with dw / db fused into the dx pass (ln_bwd_part_vec_kernel + ln_part_reduce_kernel); ``part``:
 // ceil(T / iit_ln_bwd_part_rows()) x 2 d floats of scratch; ``dy2`` (nullable, fp32 [T, d]) is added to dy.  Falls
@@ -710,15 +718,18 @@ IIT_EXPORT int iit_ln_bwd_part(const void* dy, int dy_f32, const float* x, const
     return iit_ln_bwd_sel(dy, dy_f32, x, mean, rstd, w, dx, dres, dx16, dw, db, T, d, accumulate, pos_mask, S, stream);
   if (pos_mask && (S <= 0 || S > 64)) return (int)hipErrorInvalidValue;
   const RowSel sel{pos_mask, S > 0 ? S : 1, T};
-  const int nblk = (T + 4 * LN_FUSED_R - 1) / (4 * LN_FUSED_R);
+  const int R = ln_part_r();
+  const int nblk = (T + 4 * R - 1) / (4 * R);
   hipStream_t s = (hipStream_t)stream;
   __bf16* d16 = (__bf16*)dx16;
-#define LNP(V)                                                                                                   \
-  if (dy_f32) hipLaunchKernelGGL((ln_bwd_part_vec_kernel<V, true>), dim3(nblk), dim3(256), 0, s, dy, x, mean, rstd, w, dx, dres, d16, part, T, d, accumulate, sel, dy2); \
-  else hipLaunchKernelGGL((ln_bwd_part_vec_kernel<V, false>), dim3(nblk), dim3(256), 0, s, dy, x, mean, rstd, w, dx, dres, d16, part, T, d, accumulate, sel, dy2);
+#define LNPR(V, RR)                                                                                              \
+  if (dy_f32) hipLaunchKernelGGL((ln_bwd_part_vec_kernel<V, true, RR>), dim3(nblk), dim3(256), 0, s, dy, x, mean, rstd, w, dx, dres, d16, part, T, d, accumulate, sel, dy2); \
+  else hipLaunchKernelGGL((ln_bwd_part_vec_kernel<V, false, RR>), dim3(nblk), dim3(256), 0, s, dy, x, mean, rstd, w, dx, dres, d16, part, T, d, accumulate, sel, dy2);
+#define LNP(V) if (R == 1) { LNPR(V, 1) } else if (R == 4) { LNPR(V, 4) } else { LNPR(V, 2) }
   const int v4 = (d / 4 + 63) / 64;
   if (v4 <= 1) { LNP(1) } else if (v4 <= 2) { LNP(2) } else if (v4 <= 3) { LNP(3) } else { LNP(4) }
 #undef LNP
+#undef LNPR
   const int G = max(1, min(32, nblk / 8));  // ~8 partial rows per thread
   hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((2 * (d / 4) + 255) / 256, G), dim3(256), 0, s, part, nblk, d, dw, db);
   return hipGetLastError();
