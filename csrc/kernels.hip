@@ -485,12 +485,14 @@ __global__ __launch_bounds__(256) void ln_dwdb_vec_kernel(const void* __restrict
 // meet in LDS and write ONE partial row pair (dw part, db part) to ``part[block][2 d]`` with plain stores -- no
 // atomics here (the separate ln_dwdb kernels re-read dy and x and did one memory-side fp32 atomic per column per
 // 32 rows: ~17 us for [3840][768], profiles/mqnli_step_breakdown_r5.txt).  ln_part_reduce_kernel sums the partials.
-// R = rows per wave (the block covers 4 R rows): IIT_LN_PART_R = 1 / 2 / 4, default 2
+// R = rows per wave (the block covers 4 R rows): IIT_LN_PART_R = 1 / 2 / 4, default 1 -- the MQNLI (BERT-base)
+// step measured 11.93-11.96 ms at R = 1, 12.03-12.04 at 2 and 12.38-12.40 at 4 (interleaved, one box;
+// profiles/mqnli_native_r6.txt): more, shorter blocks beat the smaller partial array
 static int ln_part_r() {
   static const int r = [] {
     const char* e = getenv("IIT_LN_PART_R");
-    const int v = e ? atoi(e) : 2;
-    return (v == 1 || v == 4) ? v : 2;
+    const int v = e ? atoi(e) : 1;
+    return (v == 2 || v == 4) ? v : 1;
   }();
   return r;
 }
