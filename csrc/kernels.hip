@@ -732,7 +732,12 @@ IIT_EXPORT int iit_ln_bwd_part(const void* dy, int dy_f32, const float* x, const
   if (v4 <= 1) { LNP(1) } else if (v4 <= 2) { LNP(2) } else if (v4 <= 3) { LNP(3) } else { LNP(4) }
 #undef LNP
 #undef LNPR
-  const int G = max(1, min(32, nblk / 8));  // ~8 partial rows per thread
+  static const int gcap = [] {  // IIT_LN_REDUCE_G: most groups of partial rows (default 32)
+    const char* e = getenv("IIT_LN_REDUCE_G");
+    const int v = e ? atoi(e) : 32;
+    return v >= 1 && v <= 1024 ? v : 32;
+  }();
+  const int G = max(1, min(gcap, nblk / 8));  // >= ~8 partial rows per thread
   hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((2 * (d / 4) + 255) / 256, G), dim3(256), 0, s, part, nblk, d, dw, db);
   return hipGetLastError();
 }
