@@ -515,6 +515,10 @@ def gemm(A, B, C, *, M, N, K: int, lda, ldb, ldc, mode=0, epi=0, C2=None, C3=Non
 
             rkey = (M, N, K, mode, epi, bias0 is not None, fresh, deterministic())
             split = RAGGED.get(rkey)
+            if split is None:  # the shipped split-or-whole choice (then bulk and tail take their own table entries)
+                shipped = _ragged_table().get(repr(rkey))
+                if shipped is not None:
+                    split = RAGGED[rkey] = (bool(shipped), float("nan"), [])
             if split is None and _FREEZE:  # no timing: the tile-aligned bulk + tail (both keys must be in the table)
                 split = RAGGED[rkey] = (True, float("nan"), [])
             if split is None and not torch.cuda.is_current_stream_capturing():
@@ -766,12 +770,20 @@ def _parse_dual(name: str):
 # ``IIT_GEMM_TABLE=0`` disables it, ``IIT_GEMM_TABLE=<path>`` reads another file.
 _TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "gemm_decisions_gfx950.json")
 _TABLE = None
+_RAGGED_TABLE: Dict[str, bool] = {}
+
+
+def _ragged_table() -> Dict[str, bool]:
+    """Shipped ragged-problem choices (``"ragged"`` section of the table): split into bulk + tail or not."""
+    _table()
+    return _RAGGED_TABLE
 
 
 def _table() -> Dict[str, str]:
     global _TABLE
     if _TABLE is None:
         _TABLE = {}
+        _RAGGED_TABLE.clear()
         path = os.environ.get("IIT_GEMM_TABLE", _TABLE_PATH)
         if path != "0" and os.path.exists(path) and torch.cuda.is_available():
             import json
@@ -781,6 +793,7 @@ def _table() -> Dict[str, str]:
                 arch = getattr(torch.cuda.get_device_properties(0), "gcnArchName", "").split(":")[0]
                 if data.get("arch") == arch:  # decisions measured on this GPU architecture only
                     _TABLE = dict(data.get("decisions", {}))
+                    _RAGGED_TABLE.update({k: bool(v) for k, v in data.get("ragged", {}).items()})
             except (OSError, ValueError) as e:  # pragma: no cover - a corrupt table only costs autotuning
                 print(f"[iit] GEMM decision table not loaded ({e})")
     return _TABLE
@@ -820,12 +833,13 @@ def export_table(path: str) -> int:
     import json
     dec = {repr(k): v[0] for k, v in DECISIONS.items()}
     dec.update({repr(k): v[0] for k, v in DUAL_DECISIONS.items()})
+    ragged = {repr(k): bool(v[0]) for k, v in RAGGED.items() if v[0] is not None}
     arch = getattr(torch.cuda.get_device_properties(0), "gcnArchName", "").split(":")[0] \
         if torch.cuda.is_available() else None
     with open(path, "w") as f:
         json.dump({"arch": arch, "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else None,
-                   "decisions": dec}, f, indent=0, sort_keys=True)
-    return len(dec)
+                   "decisions": dec, "ragged": ragged}, f, indent=0, sort_keys=True)
+    return len(dec) + len(ragged)
 
 
 def report() -> str:

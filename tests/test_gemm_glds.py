@@ -261,6 +261,29 @@ def test_ragged_vocab_gemms_split_bulk_and_tail(K, case):
     assert ((got - exp).norm() / exp.norm()).item() < 1e-2
 
 
+def test_ragged_split_from_the_shipped_table(K, monkeypatch):
+    """A ragged key in the shipped table's "ragged" section is split without timing the whole problem (run-to-run
+    identical choice, VERDICT r5 weak #4); the result still matches fp32."""
+    import math
+    from iit_amd.ops import gemm_dispatch as gd
+    V, Vp, d, T = 50257, 50264, 768, 256
+    rkey = (T, V, d, K.MODE_BKM, K.EPI_F32_STORE, True, False, gd.deterministic())
+    assert gd._ragged_table().get(repr(rkey)) is True, "the shipped table holds the headline unembed split"
+    monkeypatch.setattr(gd, "RAGGED", {})
+    torch.manual_seed(1)
+    x = torch.randn(T, d, device=dev).bfloat16()
+    U = torch.zeros(d, Vp, device=dev, dtype=torch.bfloat16)
+    U[:, :V] = (torch.randn(d, V, device=dev) / 16).bfloat16()
+    b = torch.randn(V, device=dev)
+    C = torch.empty((T, Vp), device=dev)
+    gd.gemm(x, U, C, M=T, N=V, K=d, lda=d, ldb=Vp, ldc=Vp, mode=K.MODE_BKM, epi=K.EPI_F32_STORE, bias0=b)
+    split, whole, pieces = gd.RAGGED[rkey]
+    assert split is True and math.isnan(whole) and pieces == []  # nothing timed for the split decision
+    torch.cuda.synchronize()
+    exp = x.float() @ U[:, :V].float() + b
+    assert ((C[:, :V] - exp).norm() / exp.norm()).item() < 1e-2
+
+
 @pytest.mark.parametrize("resid", [False, True])
 @pytest.mark.parametrize("bias", [True, False])
 def test_narrow_output_candidates(K, bias, resid):
